@@ -1,0 +1,61 @@
+"""ctypes binding of the C ABI in ``include/srf.h`` (``srf_amd/libsrf.so``).
+
+The library is the only compute path for the routing layers: there is no CPU
+or eager-PyTorch fallback, so a missing or stale build raises here instead of
+silently running something else.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libsrf.so')
+
+_c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/srf.h one to one.
+_SIGNATURES = {
+    'srf_version': (_c_int, []),
+    'srf_last_error': (ctypes.c_char_p, []),
+    'srf_route_dr_auto_chunks': (_c_int, [_c_int] * 8),
+    'srf_route_dr_saved_floats': (_c_size, [_c_int] * 5),
+    'srf_route_dr_fwd_workspace': (_c_size, [_c_int] * 10),
+    'srf_route_dr_bwd_workspace': (_c_size, [_c_int] * 10),
+    'srf_route_dr_fwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _c_size, _vp]),
+    'srf_route_dr_bwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+}
+
+
+class SrfError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the bound library; raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f'{LIB_PATH} is missing: build it with `make -C srf_amd/csrc` '
+                              '(or __graft_entry__.build()); there is no fallback path')
+        # torch must be imported first so that its HIP runtime (same SONAME as
+        # /opt/rocm's) is the one this library binds to.
+        import torch  # noqa: F401
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().srf_last_error().decode(errors='replace')
+        raise SrfError(f'{what} failed (rc={rc}): {msg}')

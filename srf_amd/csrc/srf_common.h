@@ -1,0 +1,57 @@
+// Shared helpers for the SRF HIP library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace srf {
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+}  // namespace srf
+
+#define SRF_OK 0
+#define SRF_EINVAL (-1)
+#define SRF_EHIP (-2)
+#define SRF_EUNSUPPORTED (-3)
+#define SRF_EWORKSPACE (-4)
+
+#define SRF_REQUIRE(cond, ...)                 \
+  do {                                         \
+    if (!(cond)) {                             \
+      srf::set_error(__VA_ARGS__);             \
+      return SRF_EINVAL;                       \
+    }                                          \
+  } while (0)
+
+#define SRF_HIP_TRY(call)                                                      \
+  do {                                                                         \
+    hipError_t e_ = (call);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      srf::set_error("%s failed: %s", #call, hipGetErrorString(e_));           \
+      return SRF_EHIP;                                                         \
+    }                                                                          \
+  } while (0)
+
+#define SRF_LAUNCH_CHECK(name)                                                 \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess) {                                                    \
+      srf::set_error("launch of %s failed: %s", name, hipGetErrorString(e_));  \
+      return SRF_EHIP;                                                         \
+    }                                                                          \
+  } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// v_mfma_f32_16x16x4_f32: lane l holds A[row=l&15][k=l>>4], B[k=l>>4][col=l&15];
+// C/D lane l holds col = l&15, rows 4*(l>>4) + reg.
+__device__ __forceinline__ f4 mfma16x16x4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
