@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""bench.py -- SRF training-step throughput (acoustic frames/sec) on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1] = C2): TIMIT SRF L=3, PH=CH=8, DIM=16,
+LPAD=RPAD=4, DR iter 3, fp32, class_n 63; per GPU B=17 utterances of T=320
+frames (the reference's bucket rule for 7000 frames/batch);
+synthetic N(0,1) 123-d fbank, labels uniform in [1, 61], L = T'/2.
+One step = process_train_step: crop, forward, CTC, backward, RCCL gradient
+all-reduce (N > 1), fused Adam.  value = sum(inp_len) over all ranks / step time
+(the reference's frame counter, trainer_sr.py:74), weak scaling.
+
+Prints ONE JSON line on rank 0 (roofline of the dominant kernel from HIP events
+inside the timed region; CPU baseline = torch-CPU op-for-op mirror of
+sequence_router_naive.py on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+WORKLOADS = {
+    # name: (config kwargs, class_n, per-GPU B, T)
+    'timit_c2': (dict(enc=3, iters=3, lpad=4, rpad=4, ph=8, pd=16, ch=8, cd=16, vd=16, context=False), 63, 17, 320),
+    'wsj_c4': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=False), 32, 28, 800),
+}
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def make_config(kw):
+    from srf_amd.common_helper import build_parser
+    ns = build_parser().parse_args([])
+    ns.feat_dim = 123
+    ns.model_encoder_num = kw['enc']
+    ns.model_caps_iter = kw['iters']
+    ns.model_caps_window_lpad, ns.model_caps_window_rpad = kw['lpad'], kw['rpad']
+    ns.model_caps_primary_num, ns.model_caps_primary_dim = kw['ph'], kw['pd']
+    ns.model_caps_convolution_num, ns.model_caps_convolution_dim = kw['ch'], kw['cd']
+    ns.model_caps_class_dim = kw['vd']
+    ns.model_caps_context = kw['context']
+    ns.model_caps_type = 'naive'
+    ns.model_initializer = 'fan_avg'
+    ns.train_lr_param_k, ns.train_warmup_n = 0.5, 1200      # train_srf_timit.sh:49-51
+    return ns
+
+
+def synthetic_batch(B, T, class_n, rank, dev):
+    g = torch.Generator().manual_seed(1234 + rank)
+    feats = torch.randn(B, T, 123, generator=g)
+    Tp = (T + 3) // 4
+    L = Tp // 2
+    gl = torch.Generator().manual_seed(4321 + rank)
+    labels = torch.randint(1, class_n - 1, (B, L), generator=gl)
+    inp_len = torch.full((B,), T, dtype=torch.int32)
+    tar_len = torch.full((B,), L, dtype=torch.int32)
+    return tuple(t.to(dev) for t in (feats, labels, inp_len, tar_len))
+
+
+class HipEvents:
+    """Raw hipEvent_t handles from the HIP runtime torch already loaded."""
+
+    def __init__(self):
+        self.hip = ctypes.CDLL('libamdhip64.so.7')
+        self.hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        self.hip.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+
+    def create(self, n):
+        arr = (ctypes.c_void_p * n)()
+        for i in range(n):
+            h = ctypes.c_void_p()
+            assert self.hip.hipEventCreate(ctypes.byref(h)) == 0
+            arr[i] = h.value
+        return arr
+
+    def elapsed_ms(self, a, b):
+        self.hip.hipEventSynchronize(ctypes.c_void_p(b))
+        ms = ctypes.c_float()
+        assert self.hip.hipEventElapsedTime(ctypes.byref(ms), ctypes.c_void_p(a), ctypes.c_void_p(b)) == 0
+        return ms.value
+
+
+def cpu_baseline(model_gpu, cfg, class_n, T, seconds):
+    """torch-CPU op-for-op mirror of naive (oracle/naive_mirror.py), fp32,
+    one T-frame utterance per step, timed for >= `seconds` (>= 1 step)."""
+    from oracle import naive_mirror as nm
+    from oracle import srf_oracle as so
+    kw = dict(feat_dim=123, enc_num=cfg.model_encoder_num, iters=cfg.model_caps_iter,
+              lpad=cfg.model_caps_window_lpad, rpad=cfg.model_caps_window_rpad, ph=cfg.model_caps_primary_num,
+              pd=cfg.model_caps_primary_dim, ch=cfg.model_caps_convolution_num, cd=cfg.model_caps_convolution_dim,
+              vd=cfg.model_caps_class_dim, class_n=class_n, context=bool(cfg.model_caps_context))
+    shape = so.SrfShape(**kw)
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16') or 16))
+    torch.set_num_threads(threads)
+    params = model_gpu.export_params()
+    mirror = nm.NaiveMirror(shape, params, dtype=torch.float32)
+    opt = nm.TfAdam(mirror.parameters(), k=0.5, warmup=1200)
+    feats, labels, inp_len, tar_len = synthetic_batch(1, T, class_n, 0, 'cpu')
+    frames, steps = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        nm.train_step(mirror, opt, feats, labels, inp_len, tar_len)
+        frames += int(inp_len.sum())
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 50:
+            break
+    return {'value': frames / el, 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{steps} train steps x 1 utterance x {T} frames (torch-CPU mirror of '
+                      f'sequence_router_naive.py, fp32, {el:.1f}s)'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--workload', default='timit_c2', choices=sorted(WORKLOADS))
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    from srf_amd import train_helper, trainer_sr
+    from srf_amd.sequence_router import SequenceRouter
+
+    kw, class_n, B, T = WORKLOADS[args.workload]
+    cfg = make_config(kw)
+    model = SequenceRouter(cfg, None, class_n, device=dev, seed=1234)   # same init on every rank
+    opt = train_helper.get_optimizer(cfg)
+    batch = synthetic_batch(B, T, class_n, rank, dev)
+    loss_state, frame_state, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
+
+    def step():
+        trainer_sr.process_train_step(4, batch, model, opt, loss_state, frame_state, world, class_n - 1, samples)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # HIP events around the dominant kernel (forward routing pass of the last
+    # layer) for every timed step, recorded on the launch stream.
+    ev = HipEvents()
+    Tp = (T + 3) // 4
+    last = model.enc_num - 1
+    geom = model._geom(last, B, Tp)
+    R = model.iter
+    ev_pairs = [(ev.create(R), ev.create(R)) for _ in range(args.steps)]
+    geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    geom.timing = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    in_n, J, D, Din = model.layer_shapes[last]
+    frames_prime = B * Tp
+    # algorithmic FLOPs per launch: the layer's pose contraction (once per
+    # forward, spread over its R pass launches) + one routing iteration
+    pose = 2.0 * in_n * J * D * Din
+    route = 4.0 * in_n * J * D
+    flops_launch = frames_prime * (pose / R + route)
+    achieved_tflops = flops_launch / (kern_avg_ms * 1e-3) / 1e12
+
+    frames_per_step = B * T * world
+    value = frames_per_step * args.steps / elapsed
+    line = {
+        'metric': 'acoustic frames/sec through SRF (123-d fbank, 3-iter DR) at 1/2/4/8 MI355X',
+        'value': round(value, 1), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic (N(0,1) 123-d fbank, random init)',
+        'config': {'workload': f'{args.workload}: SRF L={cfg.model_encoder_num} PH=CH={cfg.model_caps_primary_num} '
+                               f'DIM={cfg.model_caps_primary_dim} LPAD=RPAD={cfg.model_caps_window_lpad} DR iter='
+                               f'{cfg.model_caps_iter}, train step (fwd+bwd+allreduce+Adam)',
+                   'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
+                   'parallelism': f'dp{world}'},
+        'roofline': {'kernel': f'route_pass_kernel<16,16,8,FWD> (layer {last + 1} DR forward pass)', 'bound': 'mfma',
+                     'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+                     'avg_launch_us': round(kern_avg_ms * 1e3, 2),
+                     'flops_per_launch': flops_launch},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

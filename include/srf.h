@@ -44,12 +44,24 @@ size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rp
 int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, float* v_out,
                      float* saved, void* workspace, size_t workspace_bytes, void* stream);
+/* Profiling hook (opt-in, this thread only): the next srf_route_dr_fwd call
+ * records starts[r] / stops[r] (hipEvent_t) on its stream around the routing-pass
+ * kernel of iteration r < n, then forgets the arrays. */
+int srf_route_dr_set_timing_events(void* const* starts, void* const* stops, int n);
 /* Gradients are written (not accumulated): g_emb [B*T][N][din], g_W like W,
  * g_bias like bias. */
 int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
                      const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
                      size_t workspace_bytes, void* stream);
+
+/* ---- Fused Adam over one flat parameter buffer ----------------------------
+ * Replaces the Keras Adam apply of trainer_sr.py:71 / train_helper.py:60-70:
+ * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= alpha m / (sqrt(v) + eps),
+ * alpha = lr(step) sqrt(1-b2^t)/(1-b1^t) computed by the caller.  All four
+ * buffers 16-byte aligned, n floats each. */
+int srf_adam_step(float* params, const float* grads, float* m, float* v, size_t n, float alpha, float b1,
+                  float b2, float eps, void* stream);
 
 #ifdef __cplusplus
 }

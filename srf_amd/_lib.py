@@ -16,12 +16,15 @@ _c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
 _SIGNATURES = {
     'srf_version': (_c_int, []),
     'srf_last_error': (ctypes.c_char_p, []),
+    'srf_route_dr_set_timing_events': (_c_int, [_vp, _vp, _c_int]),
     'srf_route_dr_auto_chunks': (_c_int, [_c_int] * 8),
     'srf_route_dr_saved_floats': (_c_size, [_c_int] * 5),
     'srf_route_dr_fwd_workspace': (_c_size, [_c_int] * 10),
     'srf_route_dr_bwd_workspace': (_c_size, [_c_int] * 10),
     'srf_route_dr_fwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _c_size, _vp]),
     'srf_route_dr_bwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    'srf_adam_step': (_c_int, [_vp, _vp, _vp, _vp, _c_size, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                               ctypes.c_float, _vp]),
 }
 
 

@@ -25,6 +25,13 @@
 namespace {
 
 constexpr float kSquashEps = 1e-7f;  // naive:248
+
+// Opt-in profiling hook (srf_route_dr_set_timing_events): events recorded on the
+// launch stream around each forward routing-pass kernel of the next
+// srf_route_dr_fwd call made by this thread, then cleared.
+thread_local hipEvent_t* t_ev_start = nullptr;
+thread_local hipEvent_t* t_ev_stop = nullptr;
+thread_local int t_ev_n = 0;
 constexpr int MODE_FWD = 0;
 constexpr int MODE_BWD = 1;
 
@@ -39,6 +46,12 @@ struct Geom {
 // ---------------------------------------------------------------- fragments
 // MFMA operand k-permutation: k-step ks of lane group g carries input element
 // e = g*KS + ks, so each lane reads KS contiguous floats of x and of W.
+//
+// Loads are never predicated: row indices past J*Dout (only in the last, partial
+// row tile) and tile indices past NT are clamped to valid addresses.  Such rows
+// belong to output capsules j >= J, whose coupling c is exactly 0, so they never
+// reach a valid output; keeping every load unconditional lets hipcc batch them
+// instead of serialising load -> wait -> MFMA behind exec-mask branches.
 template <int KS>
 __device__ __forceinline__ void load_vec(const float* __restrict__ p, float (&v)[KS]) {
   if constexpr (KS % 4 == 0) {
@@ -54,48 +67,53 @@ __device__ __forceinline__ void load_vec(const float* __restrict__ p, float (&v)
   }
 }
 
-// Windowed input (naive:150-151): capsule i = w*N + n of frame (b,t) is
-// emb[b, t + w - lpad, n] or zero outside [0, T).
-__device__ __forceinline__ const float* window_src(const float* __restrict__ emb, int f, int F, int T,
-                                                   int N, int din, int lpad, int i) {
-  if (f >= F) return nullptr;
-  const int w = i / N, n = i - w * N;
-  const int b = f / T, t = f - b * T;
-  const int ts = t + w - lpad;
-  if (ts < 0 || ts >= T) return nullptr;
-  return emb + ((size_t)(b * T + ts) * N + n) * din;
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+// Frame coordinates of one lane, computed once per kernel.
+struct FrameLoc {
+  int b, t;
+  bool valid;
+};
+
+__device__ __forceinline__ FrameLoc frame_loc(int f, int F, int T) {
+  const int fc = min(f, F - 1);
+  FrameLoc r;
+  r.b = fc / T;
+  r.t = fc - r.b * T;
+  r.valid = f < F;
+  return r;
 }
 
+// Windowed input (naive:150-151): capsule i = w*N + n of frame (b,t) is
+// emb[b, t + w - lpad, n] or zero outside [0, T).
 template <int DIN>
-__device__ __forceinline__ void load_x(const float* __restrict__ src, int g, float (&x)[DIN / 4]) {
+__device__ __forceinline__ void load_x(const float* __restrict__ emb, const FrameLoc& fl, int T, int N, int lpad,
+                                       int i, int g, float (&x)[DIN / 4]) {
   constexpr int KS = DIN / 4;
-  if (src) {
-    load_vec<KS>(src + g * KS, x);
-  } else {
+  const int w = i / N, n = i - w * N;
+  const int ts = fl.t + w - lpad;
+  const bool ok = fl.valid && ts >= 0 && ts < T;
+  const int tsc = min(max(ts, 0), T - 1);
+  load_vec<KS>(emb + ((size_t)(fl.b * T + tsc) * N + n) * DIN + g * KS, x);
 #pragma unroll
-    for (int k = 0; k < KS; ++k) x[k] = 0.f;
-  }
+  for (int k = 0; k < KS; ++k) x[k] = ok ? x[k] : 0.f;
 }
 
 // u tile (16 rows of (j,d) x 16 frames) for capsule i and global tile tg.
 template <int DIN>
 __device__ __forceinline__ f4 pose_tile(const float* __restrict__ W, const float* __restrict__ bias, int i,
-                                        int JD, int tg, int lane, const float (&x)[DIN / 4]) {
+                                        int JD, int NT, int tg, int lane, const float (&x)[DIN / 4]) {
   constexpr int KS = DIN / 4;
-  const int arow = tg * 16 + (lane & 15);
+  const int tc = min(tg, NT - 1);
+  const int arow = min(tc * 16 + (lane & 15), JD - 1);
   const int g = lane >> 4;
   float a[KS];
-  if (arow < JD) {
-    load_vec<KS>(W + ((size_t)i * JD + arow) * DIN + g * KS, a);
-  } else {
-#pragma unroll
-    for (int k = 0; k < KS; ++k) a[k] = 0.f;
-  }
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  load_vec<KS>(W + ((size_t)i * JD + arow) * DIN + g * KS, a);
+  const int crow = min(tc * 16 + 4 * g, JD - 4);
+  f4 acc = ld4(bias + (size_t)i * JD + crow);
 #pragma unroll
   for (int k = 0; k < KS; ++k) acc = mfma16x16x4(a[k], x[k], acc);
-  const int crow = tg * 16 + 4 * g;
-  if (crow < JD) acc += *reinterpret_cast<const f4*>(bias + (size_t)i * JD + crow);
   return acc;
 }
 
@@ -130,13 +148,185 @@ __device__ __forceinline__ bool tile_primary(int tg) {
   return true;
 }
 
-__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
-__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+// Per-frame vector rows 4g..4g+3 of tile tg (zero past J*Dout or past F).
+__device__ __forceinline__ void load_rows(const float* __restrict__ v, int f, bool fvalid, int JD, int tg, int g,
+                                          float (&o)[4]) {
+  const int row = tg * 16 + 4 * g;
+  const bool ok = fvalid && row < JD;
+  const f4 a = ld4(v + (size_t)(fvalid ? f : 0) * JD + min(row, JD - 4));
+  o[0] = ok ? a.x : 0.f; o[1] = ok ? a.y : 0.f; o[2] = ok ? a.z : 0.f; o[3] = ok ? a.w : 0.f;
+}
 
 // ---------------------------------------------------------------- routing pass
-// grid: n_ftiles * n_chunks workgroups (chunk = blockIdx % n_chunks, so with
-// n_chunks == 8 every XCD streams one i-chunk of W from its own L2);
-// block: NW waves, wave w owns row tiles [w*TW, (w+1)*TW).
+// Operand fragments of one input capsule i for a wave's TW row tiles.
+template <int DIN, int TW>
+struct Frags {
+  float x[DIN / 4];
+  float w[TW][DIN / 4];
+  f4 b[TW];
+};
+
+template <int DIN, int TW>
+__device__ __forceinline__ void fetch_frags(const float* __restrict__ emb, const float* __restrict__ W,
+                                            const float* __restrict__ bias, const FrameLoc& loc, int T, int N,
+                                            int lpad, int i, int JD, int NT, int tbase, int lane,
+                                            Frags<DIN, TW>& fr) {
+  constexpr int KS = DIN / 4;
+  const int g = lane >> 4;
+  load_x<DIN>(emb, loc, T, N, lpad, i, g, fr.x);
+  // Tile bases are wave-uniform (scalar registers); one per-lane offset serves
+  // every tile.  J*Dout is a multiple of 16 for Dout >= 16, so only Dout == 8
+  // needs the per-lane row clamp of the last, partial tile.
+  const float* Wi = W + (size_t)i * JD * DIN;
+  const float* bi = bias + (size_t)i * JD;
+  int lrow = lane & 15, brow = 4 * g;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int tc = __builtin_amdgcn_readfirstlane(min(tbase + t, NT - 1));
+    if constexpr (DIN < 16) {
+      lrow = min(tc * 16 + (lane & 15), JD - 1) - tc * 16;
+      brow = min(tc * 16 + 4 * g, JD - 4) - tc * 16;
+    }
+    load_vec<KS>(Wi + (size_t)tc * 16 * DIN + lrow * DIN + g * KS, fr.w[t]);
+    fr.b[t] = ld4(bi + tc * 16 + brow);
+  }
+}
+
+template <int DIN, int TW>
+__device__ __forceinline__ void pose_tiles(const Frags<DIN, TW>& fr, float (&u)[TW][4]) {
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    f4 acc = fr.b[t];
+#pragma unroll
+    for (int k = 0; k < DIN / 4; ++k) acc = mfma16x16x4(fr.w[t][k], fr.x[k], acc);
+    u[t][0] = acc.x; u[t][1] = acc.y; u[t][2] = acc.z; u[t][3] = acc.w;
+  }
+}
+
+// Per-wave state of a routing pass over one frame tile.
+template <int TW>
+struct PassState {
+  float vcr[TW][4], gsr[TW][4], acc[TW][4];
+};
+
+// One input capsule i of a routing pass: u tile -> logits <u, Vc> -> softmax
+// over all output capsules (cross-wave through LDS) -> accumulate.
+template <int DIN, int DOUT, int TW, int MODE>
+__device__ __forceinline__ void pass_step(Frags<DIN, TW>& fr, PassState<TW>& st, float* red, int& parity, int i,
+                                          int r, int J, int Jeff, int mask_first, int tbase, int wv, int NW, int lane,
+                                          int in_n, int f, bool fvalid, float* __restrict__ stats,
+                                          const float* __restrict__ emb, const float* __restrict__ W,
+                                          const float* __restrict__ bias, const FrameLoc& loc, int T, int N,
+                                          int lpad, int inext, int JD, int NT) {
+  const int fl = lane & 15, g = lane >> 4;
+  float u[TW][4];
+  pose_tiles<DIN, TW>(fr, u);
+  // the MFMAs have consumed the fragments: refill them with capsule inext now,
+  // so the loads are in flight across the softmax and its barrier
+  fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
+  float c[TW];
+  float gL[TW];
+  if (MODE == MODE_FWD && r == 0) {
+    // iteration 0: logits are 0 (+ the mask), so c is uniform (naive:172-181)
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int j = tile_j<DOUT>(tbase + t, g);
+      const bool valid = j < J && !(mask_first && j == 0);
+      c[t] = valid ? 1.f / (float)Jeff : 0.f;
+      gL[t] = 0.f;
+    }
+  } else {
+    float p[TW], q[TW];
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s += u[t][k] * st.vcr[t][k];
+        if constexpr (MODE == MODE_BWD) s2 += u[t][k] * st.gsr[t][k];
+      }
+      p[t] = s;
+      q[t] = s2;
+    }
+    jreduce<DOUT, TW>(p);
+    if constexpr (MODE == MODE_BWD) jreduce<DOUT, TW>(q);
+    // local softmax statistics over this lane's output capsules
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int tg = tbase + t;
+      const int j = tile_j<DOUT>(tg, g);
+      if (tile_primary<DOUT>(tg) && j < J && !(mask_first && j == 0)) m = fmaxf(m, p[t]);
+    }
+    float z = 0.f, y = 0.f;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int tg = tbase + t;
+      const int j = tile_j<DOUT>(tg, g);
+      const bool ok = tile_primary<DOUT>(tg) && j < J && !(mask_first && j == 0);
+      const float e = ok ? __expf(p[t] - m) : 0.f;
+      z += e;
+      if constexpr (MODE == MODE_BWD) y += e * q[t];
+    }
+    if constexpr (DOUT == 8) {
+      // lane groups {0,1} and {2,3} hold different capsules: combine
+      const float mo = __shfl_xor(m, 32, 64), zo = __shfl_xor(z, 32, 64), yo = __shfl_xor(y, 32, 64);
+      const float M = fmaxf(m, mo);
+      const float s1 = (m == -INFINITY) ? 0.f : __expf(m - M);
+      const float s2 = (mo == -INFINITY) ? 0.f : __expf(mo - M);
+      z = z * s1 + zo * s2;
+      y = y * s1 + yo * s2;
+      m = M;
+    }
+    if (NW > 1) {
+      float* slot = red + parity * (NW * 48);
+      if (g == 0) {
+        slot[wv * 48 + fl * 3 + 0] = m;
+        slot[wv * 48 + fl * 3 + 1] = z;
+        slot[wv * 48 + fl * 3 + 2] = y;
+      }
+      __syncthreads();
+      float M = -INFINITY;
+      for (int w = 0; w < NW; ++w) M = fmaxf(M, slot[w * 48 + fl * 3]);
+      float Z = 0.f, Y = 0.f;
+      for (int w = 0; w < NW; ++w) {
+        const float mw = slot[w * 48 + fl * 3];
+        const float sc = (mw == -INFINITY) ? 0.f : __expf(mw - M);
+        Z += slot[w * 48 + fl * 3 + 1] * sc;
+        Y += slot[w * 48 + fl * 3 + 2] * sc;
+      }
+      m = M; z = Z; y = Y;
+      parity ^= 1;
+    }
+    const float invz = 1.f / z;
+    const float sigma = y * invz;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int j = tile_j<DOUT>(tbase + t, g);
+      const bool valid = j < J && !(mask_first && j == 0);
+      c[t] = valid ? __expf(p[t] - m) * invz : 0.f;
+      gL[t] = c[t] * (q[t] - sigma);
+    }
+    if constexpr (MODE == MODE_BWD) {
+      if (wv == 0 && g == 0 && fvalid) {
+        stats[((size_t)f * in_n + i) * 2 + 0] = m + __logf(z);
+        stats[((size_t)f * in_n + i) * 2 + 1] = sigma;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const float w = (MODE == MODE_FWD) ? c[t] : gL[t];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st.acc[t][k] += w * u[t][k];
+  }
+}
+
+// grid: n_ftiles * n_chunks workgroups (chunk = blockIdx % n_chunks, so when
+// n_chunks divides 8 the workgroups of one i-chunk share an XCD and its L2);
+// block: NW waves, wave w owns row tiles [w*TW, (w+1)*TW).  The fragments of
+// capsule i+1 are fetched before capsule i is processed (two register sets,
+// loop unrolled by 2), so the loads fly across the softmax barrier.
 template <int DIN, int DOUT, int TW, int MODE>
 __global__ __launch_bounds__(512) void route_pass_kernel(
     const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ bias,
@@ -150,174 +340,79 @@ __global__ __launch_bounds__(512) void route_pass_kernel(
   const int fl = lane & 15, g = lane >> 4;
   const int ft = blockIdx.x / n_chunks, chunk = blockIdx.x - ft * n_chunks;
   const int f = ft * 16 + fl;
-  const bool fvalid = f < F;
+  const FrameLoc loc = frame_loc(f, F, T);
   const int i0 = chunk * chunk_len, i1 = min(in_n, i0 + chunk_len);
-  const int tbase = wv * TW;
+  const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
   const int Jeff = J - (mask_first ? 1 : 0);
 
-  float vcr[TW][4], gsr[TW][4], acc[TW][4];
-  const bool use_vc = (r > 0);
+  PassState<TW> st;
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
-    const int row = (tbase + t) * 16 + 4 * g;
-    const bool ok = fvalid && row < JD;
-    f4 z = {0.f, 0.f, 0.f, 0.f};
-    f4 a = (ok && use_vc) ? ld4(vc + (size_t)f * JD + row) : z;
-    f4 b = z;
-    if constexpr (MODE == MODE_BWD) b = ok ? ld4(gsv + (size_t)f * JD + row) : z;
-    vcr[t][0] = a.x; vcr[t][1] = a.y; vcr[t][2] = a.z; vcr[t][3] = a.w;
-    gsr[t][0] = b.x; gsr[t][1] = b.y; gsr[t][2] = b.z; gsr[t][3] = b.w;
+    if (r > 0) {
+      load_rows(vc, f, loc.valid, JD, tbase + t, g, st.vcr[t]);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) acc[t][k] = 0.f;
+      for (int k = 0; k < 4; ++k) st.vcr[t][k] = 0.f;
+    }
+    if constexpr (MODE == MODE_BWD) {
+      load_rows(gsv, f, loc.valid, JD, tbase + t, g, st.gsr[t]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) st.gsr[t][k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st.acc[t][k] = 0.f;
   }
 
   int parity = 0;
-  for (int i = i0; i < i1; ++i) {
-    float x[DIN / 4];
-    load_x<DIN>(window_src(emb, f, F, T, N, DIN, lpad, i), g, x);
-    float u[TW][4];
-#pragma unroll
-    for (int t = 0; t < TW; ++t) {
-      const int tg = tbase + t;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (tg < NT) v = pose_tile<DIN>(W, bias, i, JD, tg, lane, x);
-      u[t][0] = v.x; u[t][1] = v.y; u[t][2] = v.z; u[t][3] = v.w;
-    }
-
-    float c[TW];
-    float gL[TW];
-    if (MODE == MODE_FWD && r == 0) {
-      // iteration 0: logits are 0 (+ the mask), so c is uniform (naive:172-181)
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        const int j = tile_j<DOUT>(tbase + t, g);
-        const bool valid = j < J && !(mask_first && j == 0);
-        c[t] = valid ? 1.f / (float)Jeff : 0.f;
-      }
-    } else {
-      float p[TW], q[TW];
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          s += u[t][k] * vcr[t][k];
-          s2 += u[t][k] * gsr[t][k];
-        }
-        p[t] = s;
-        q[t] = s2;
-      }
-      jreduce<DOUT, TW>(p);
-      if constexpr (MODE == MODE_BWD) jreduce<DOUT, TW>(q);
-      // local softmax statistics over this lane's output capsules
-      float m = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        const int tg = tbase + t;
-        const int j = tile_j<DOUT>(tg, g);
-        if (tile_primary<DOUT>(tg) && j < J && !(mask_first && j == 0)) m = fmaxf(m, p[t]);
-      }
-      float z = 0.f, y = 0.f;
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        const int tg = tbase + t;
-        const int j = tile_j<DOUT>(tg, g);
-        if (tile_primary<DOUT>(tg) && j < J && !(mask_first && j == 0)) {
-          const float e = __expf(p[t] - m);
-          z += e;
-          if constexpr (MODE == MODE_BWD) y += e * q[t];
-        }
-      }
-      if constexpr (DOUT == 8) {
-        // lane groups {0,1} and {2,3} hold different capsules: combine
-        const float mo = __shfl_xor(m, 32, 64), zo = __shfl_xor(z, 32, 64), yo = __shfl_xor(y, 32, 64);
-        const float M = fmaxf(m, mo);
-        const float s1 = (m == -INFINITY) ? 0.f : __expf(m - M);
-        const float s2 = (mo == -INFINITY) ? 0.f : __expf(mo - M);
-        z = z * s1 + zo * s2;
-        y = y * s1 + yo * s2;
-        m = M;
-      }
-      if (NW > 1) {
-        float* slot = red + parity * (NW * 48);
-        if (g == 0) {
-          slot[wv * 48 + fl * 3 + 0] = m;
-          slot[wv * 48 + fl * 3 + 1] = z;
-          slot[wv * 48 + fl * 3 + 2] = y;
-        }
-        __syncthreads();
-        float M = -INFINITY;
-        for (int w = 0; w < NW; ++w) M = fmaxf(M, slot[w * 48 + fl * 3]);
-        float Z = 0.f, Y = 0.f;
-        for (int w = 0; w < NW; ++w) {
-          const float mw = slot[w * 48 + fl * 3];
-          if (mw != -INFINITY) {
-            const float s = __expf(mw - M);
-            Z += slot[w * 48 + fl * 3 + 1] * s;
-            Y += slot[w * 48 + fl * 3 + 2] * s;
-          }
-        }
-        m = M; z = Z; y = Y;
-        parity ^= 1;
-      }
-      const float invz = 1.f / z;
-      const float sigma = y * invz;
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        const int j = tile_j<DOUT>(tbase + t, g);
-        const bool valid = j < J && !(mask_first && j == 0);
-        c[t] = valid ? __expf(p[t] - m) * invz : 0.f;
-        gL[t] = c[t] * (q[t] - sigma);
-      }
-      if constexpr (MODE == MODE_BWD) {
-        if (wv == 0 && g == 0 && fvalid) {
-          stats[((size_t)f * in_n + i) * 2 + 0] = m + __logf(z);
-          stats[((size_t)f * in_n + i) * 2 + 1] = sigma;
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < TW; ++t) {
-      const float w = (MODE == MODE_FWD) ? c[t] : gL[t];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc[t][k] += w * u[t][k];
+  if (i0 < i1) {
+    Frags<DIN, TW> fr;
+    fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, i0, JD, NT, tbase, lane, fr);
+    for (int i = i0; i < i1; ++i) {
+      pass_step<DIN, DOUT, TW, MODE>(fr, st, red, parity, i, r, J, Jeff, mask_first, tbase, wv, NW, lane, in_n, f,
+                                     loc.valid, stats, emb, W, bias, loc, T, N, lpad, min(i + 1, i1 - 1), JD, NT);
     }
   }
   if (!want_acc) return;
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
     const int row = (tbase + t) * 16 + 4 * g;
-    if (fvalid && row < JD) {
-      f4 v = {acc[t][0], acc[t][1], acc[t][2], acc[t][3]};
+    if (loc.valid && row < JD) {
+      f4 v = {st.acc[t][0], st.acc[t][1], st.acc[t][2], st.acc[t][3]};
       st4(slab + ((size_t)chunk * F + f) * JD + row, v);
     }
   }
 }
 
 // ---------------------------------------------------------------- gu pass
-// gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j with c^r = exp(L^r - logZ^r),
-// gL^r = c^r (<gs^r_j, u_ij> - sigma^r).  One wave = 16 frames x TW row tiles x
-// an i-chunk; no cross-wave traffic.
+// gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j with c^r = exp(L^r - logZ^r) and
+// gL^r = c^r (<gs^r_j, u_ij> - sigma^r): only per-(frame,i) scalars are shared
+// across output capsules, so j tiles are independent.  A workgroup = 4 waves
+// (4 x TW row tiles) of one frame tile and i-chunk.  Per i it
+//   * stores gu frame-contiguous, gu_t[i][row][f] (f padded to Fp), for the gW pass;
+//   * contracts gx^T[e][f] = sum_row W[i][row][e] gu[row][f] on the matrix cores
+//     straight from the gu registers, reduces it over the 4 waves in LDS and
+//     scatter-adds it into g_emb through the window adjoint (naive:150-151).
 template <int DIN, int DOUT, int TW, int R>
 __global__ __launch_bounds__(256) void route_gu_kernel(
-    const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ bias, int F, int T,
-    int N, int lpad, int in_n, int J, int mask_first, int n_tgroups, int n_chunks, int chunk_len,
+    const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ bias, int F, int Fp,
+    int T, int N, int lpad, int in_n, int J, int mask_first, int n_wgroups, int n_chunks, int chunk_len,
     const float* __restrict__ saved, const float* __restrict__ gs, const float* __restrict__ stats,
-    float* __restrict__ gu) {
+    float* __restrict__ gu_t, float* __restrict__ g_emb) {
+  constexpr int NCT = (DIN + 15) / 16;
+  __shared__ __attribute__((aligned(16))) float red[2][4][16 * DIN];
   const int JD = J * DOUT;
   const int NT = (JD + 15) / 16;
   const size_t FJD = (size_t)F * JD;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fl = lane & 15, g = lane >> 4;
-  const int n_ftiles = (F + 15) / 16;
-  const int task = blockIdx.x * 4 + wv;
-  if (task >= n_ftiles * n_tgroups * n_chunks) return;
-  const int chunk = task % n_chunks;
-  const int tgrp = (task / n_chunks) % n_tgroups;
-  const int ft = task / (n_chunks * n_tgroups);
+  const int chunk = blockIdx.x % n_chunks;
+  const int rest = blockIdx.x / n_chunks;
+  const int wgrp = rest % n_wgroups;
+  const int ft = rest / n_wgroups;
   const int f = ft * 16 + fl;
-  const bool fvalid = f < F;
-  const int tbase = tgrp * TW;
+  const FrameLoc loc = frame_loc(f, F, T);
+  const int tbase = (wgrp * 4 + wv) * TW;
   const int i0 = chunk * chunk_len, i1 = min(in_n, i0 + chunk_len);
 
   float vcr[R][TW][4], gsr[R][TW][4];
@@ -325,26 +420,25 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
   for (int r = 0; r < R; ++r) {
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
-      const int row = (tbase + t) * 16 + 4 * g;
-      const bool ok = fvalid && row < JD;
-      f4 z = {0.f, 0.f, 0.f, 0.f};
       // Vc^r (r >= 1) is stored after iteration r-1 at saved[(r-1)*2+1]
-      f4 a = (ok && r > 0) ? ld4(saved + (size_t)(2 * (r - 1) + 1) * FJD + (size_t)f * JD + row) : z;
-      f4 b = ok ? ld4(gs + (size_t)r * FJD + (size_t)f * JD + row) : z;
-      vcr[r][t][0] = a.x; vcr[r][t][1] = a.y; vcr[r][t][2] = a.z; vcr[r][t][3] = a.w;
-      gsr[r][t][0] = b.x; gsr[r][t][1] = b.y; gsr[r][t][2] = b.z; gsr[r][t][3] = b.w;
+      if (r > 0) {
+        load_rows(saved + (size_t)(2 * (r - 1) + 1) * FJD, f, loc.valid, JD, tbase + t, g, vcr[r][t]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vcr[r][t][k] = 0.f;
+      }
+      load_rows(gs + (size_t)r * FJD, f, loc.valid, JD, tbase + t, g, gsr[r][t]);
     }
   }
 
+  int parity = 0;
   for (int i = i0; i < i1; ++i) {
     float x[DIN / 4];
-    load_x<DIN>(window_src(emb, f, F, T, N, DIN, lpad, i), g, x);
+    load_x<DIN>(emb, loc, T, N, lpad, i, g, x);
     float u[TW][4], ga[TW][4];
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
-      const int tg = tbase + t;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (tg < NT) v = pose_tile<DIN>(W, bias, i, JD, tg, lane, x);
+      const f4 v = pose_tile<DIN>(W, bias, i, JD, NT, tbase + t, lane, x);
       u[t][0] = v.x; u[t][1] = v.y; u[t][2] = v.z; u[t][3] = v.w;
 #pragma unroll
       for (int k = 0; k < 4; ++k) ga[t][k] = 0.f;
@@ -365,11 +459,9 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
       }
       if (r > 0) jreduce<DOUT, TW>(p);
       jreduce<DOUT, TW>(q);
-      float logz = 0.f, sigma = 0.f;
-      if (fvalid) {
-        logz = stats[(((size_t)r * F + f) * in_n + i) * 2 + 0];
-        sigma = stats[(((size_t)r * F + f) * in_n + i) * 2 + 1];
-      }
+      const size_t si = (((size_t)r * F + (loc.valid ? f : 0)) * in_n + i) * 2;
+      const float logz = loc.valid ? stats[si] : 0.f;
+      const float sigma = loc.valid ? stats[si + 1] : 0.f;
 #pragma unroll
       for (int t = 0; t < TW; ++t) {
         const int j = tile_j<DOUT>(tbase + t, g);
@@ -380,25 +472,85 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
         for (int k = 0; k < 4; ++k) ga[t][k] += c * gsr[r][t][k] + gl * vcr[r][t][k];
       }
     }
+    // gu, frame-contiguous (rows past JD are skipped; frames past F carry 0)
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
-      const int row = (tbase + t) * 16 + 4 * g;
-      if (fvalid && row < JD) {
-        f4 v = {ga[t][0], ga[t][1], ga[t][2], ga[t][3]};
-        st4(gu + ((size_t)f * in_n + i) * JD + row, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int row = (tbase + t) * 16 + 4 * g + k;
+        if (row < JD) gu_t[((size_t)i * JD + row) * Fp + f] = ga[t][k];
       }
     }
+    // gx^T[e][f] over this wave's rows (rows past JD carry ga == 0)
+    f4 gx[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) gx[ct] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int row = min(min(tbase + t, NT - 1) * 16 + 4 * g + k, JD - 1);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const int e = min(ct * 16 + fl, DIN - 1);
+          gx[ct] = mfma16x16x4(W[((size_t)i * JD + row) * DIN + e], ga[t][k], gx[ct]);
+        }
+      }
+    }
+    float* buf = &red[parity][0][0];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = ct * 16 + 4 * g + k;
+        if (e < DIN) buf[wv * 16 * DIN + fl * DIN + e] = gx[ct][k];
+      }
+    }
+    __syncthreads();
+    {
+      const int w = i / N, n = i - w * N;
+      for (int idx = threadIdx.x; idx < 16 * DIN; idx += 256) {
+        const float sum = buf[idx] + buf[16 * DIN + idx] + buf[32 * DIN + idx] + buf[48 * DIN + idx];
+        const int flo = idx / DIN, e = idx - flo * DIN;
+        const int fo = ft * 16 + flo;
+        if (fo < F) {
+          const int bo = fo / T, to = fo - bo * T;
+          const int ts = to + w - lpad;
+          if (ts >= 0 && ts < T) atomicAdd(g_emb + ((size_t)(bo * T + ts) * N + n) * DIN + e, sum);
+        }
+      }
+    }
+    parity ^= 1;
   }
 }
 
+// Windowed input, transposed and frame-padded: xT[i][e][f] (f < Fp), the B
+// operand of the gW contraction.
+__global__ void window_xt_kernel(const float* __restrict__ emb, int F, int Fp, int T, int N, int din, int lpad,
+                                 int in_n, float* __restrict__ xT) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)in_n * din * Fp) return;
+  const int f = idx % Fp;
+  const int e = (idx / Fp) % din;
+  const int i = idx / ((size_t)Fp * din);
+  float v = 0.f;
+  if (f < F) {
+    const int w = i / N, n = i - w * N;
+    const int b = f / T, t = f - b * T;
+    const int ts = t + w - lpad;
+    if (ts >= 0 && ts < T) v = emb[((size_t)(b * T + ts) * N + n) * din + e];
+  }
+  xT[idx] = v;
+}
+
 // ---------------------------------------------------------------- gW, gbias
-// gW[i][row][e] = sum_f gu[f][i][row] x[f][i][e]  (MFMA, K = frames);
-// gbias[i][row] = sum_f gu[f][i][row].  One wave per (i, row tile).
+// gW[i][row][e] = sum_f gu[i][row][f] x[f][i][e]  (MFMA, K = frames, float4
+// loads of both frame-contiguous operands); gbias[i][row] = sum_f gu[i][row][f].
+// One wave per (i, row tile).
 template <int DIN>
-__global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__ gu,
-                                                       const float* __restrict__ emb, int F, int T, int N,
-                                                       int lpad, int in_n, int JD, float* __restrict__ gW,
-                                                       float* __restrict__ gbias) {
+__global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__ gu_t,
+                                                       const float* __restrict__ xT, int Fp, int in_n, int JD,
+                                                       float* __restrict__ gW, float* __restrict__ gbias) {
   constexpr int NCT = (DIN + 15) / 16;
   const int NT = (JD + 15) / 16;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -407,28 +559,30 @@ __global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__
   if (task >= in_n * NT) return;
   const int i = task / NT, tg = task - i * NT;
   const int arow = tg * 16 + l16;
-  const bool rvalid = arow < JD;
+  const float* ap = gu_t + ((size_t)i * JD + min(arow, JD - 1)) * Fp + 4 * g;
+  const float* bp[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) bp[ct] = xT + ((size_t)i * DIN + min(ct * 16 + l16, DIN - 1)) * Fp + 4 * g;
   f4 acc[NCT][2];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) acc[ct][0] = acc[ct][1] = f4{0.f, 0.f, 0.f, 0.f};
   float gb = 0.f;
-#pragma unroll 4
-  for (int f0 = 0; f0 < F; f0 += 4) {
-    const int f = f0 + g;
-    const float a = (f < F && rvalid) ? gu[((size_t)f * in_n + i) * JD + arow] : 0.f;
-    gb += a;
-    const float* src = window_src(emb, f, F, T, N, DIN, lpad, i);
-    const int h = (f0 >> 2) & 1;
+#pragma unroll 2
+  for (int s = 0; s < Fp; s += 16) {
+    const f4 a = ld4(ap + s);
+    gb += (a.x + a.y) + (a.z + a.w);
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
-      const int e = ct * 16 + l16;
-      const float bx = (src && e < DIN) ? src[e] : 0.f;
-      acc[ct][h] = mfma16x16x4(a, bx, acc[ct][h]);
+      const f4 b = ld4(bp[ct] + s);
+      acc[ct][0] = mfma16x16x4(a.x, b.x, acc[ct][0]);
+      acc[ct][1] = mfma16x16x4(a.y, b.y, acc[ct][1]);
+      acc[ct][0] = mfma16x16x4(a.z, b.z, acc[ct][0]);
+      acc[ct][1] = mfma16x16x4(a.w, b.w, acc[ct][1]);
     }
   }
   gb += __shfl_xor(gb, 16, 64);
   gb += __shfl_xor(gb, 32, 64);
-  if (g == 0 && rvalid) gbias[(size_t)i * JD + arow] = gb;
+  if (g == 0 && arow < JD) gbias[(size_t)i * JD + arow] = gb;
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {
     const f4 v = acc[ct][0] + acc[ct][1];
@@ -441,71 +595,6 @@ __global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__
       }
     }
   }
-}
-
-// ---------------------------------------------------------------- gx
-// gx[f][i][e] = sum_row gu[f][i][row] W[i][row][e]  (MFMA, K = J*Dout).
-template <int DIN>
-__global__ __launch_bounds__(256) void route_gx_kernel(const float* __restrict__ gu,
-                                                       const float* __restrict__ W, int F, int in_n, int JD,
-                                                       float* __restrict__ gx) {
-  constexpr int NCT = (DIN + 15) / 16;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int g = lane >> 4, l16 = lane & 15;
-  const int n_ftiles = (F + 15) / 16;
-  const int task = blockIdx.x * 4 + wv;
-  if (task >= n_ftiles * in_n) return;
-  const int ft = task / in_n, i = task - ft * in_n;
-  const int f = ft * 16 + l16;
-  const bool fvalid = f < F;
-  const int KQ = JD / 4;  // JD is a multiple of 8
-  const float* arow = gu + ((size_t)f * in_n + i) * JD + g * KQ;
-  const float* brow = W + ((size_t)i * JD + g * KQ) * DIN;
-  f4 acc[NCT][2];
-#pragma unroll
-  for (int ct = 0; ct < NCT; ++ct) acc[ct][0] = acc[ct][1] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int s = 0; s < KQ; ++s) {
-    const float a = fvalid ? arow[s] : 0.f;
-    const int h = s & 1;
-#pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
-      const int e = ct * 16 + l16;
-      const float b = (e < DIN) ? brow[(size_t)s * DIN + e] : 0.f;
-      acc[ct][h] = mfma16x16x4(a, b, acc[ct][h]);
-    }
-  }
-#pragma unroll
-  for (int ct = 0; ct < NCT; ++ct) {
-    const f4 v = acc[ct][0] + acc[ct][1];
-    const int e = ct * 16 + l16;
-    if (e < DIN) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int fo = ft * 16 + 4 * g + k;
-        if (fo < F) gx[((size_t)fo * in_n + i) * DIN + e] = v[k];
-      }
-    }
-  }
-}
-
-// Adjoint of the window (naive:150-151): g_emb[b,t,n] = sum_w gx[b, t-w+lpad, w*N+n].
-__global__ void unwindow_kernel(const float* __restrict__ gx, int F, int T, int N, int din, int lpad, int win,
-                                float* __restrict__ g_emb) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)F * N * din;
-  if (idx >= total) return;
-  const int e = idx % din;
-  const int n = (idx / din) % N;
-  const int f = idx / ((size_t)din * N);
-  const int b = f / T, t = f - b * T;
-  const int in_n = N * win;
-  float s = 0.f;
-  for (int w = 0; w < win; ++w) {
-    const int tc = t - w + lpad;
-    if (tc >= 0 && tc < T) s += gx[((size_t)(b * T + tc) * in_n + w * N + n) * din + e];
-  }
-  g_emb[idx] = s;
 }
 
 // ---------------------------------------------------------------- finish kernels
@@ -603,11 +692,27 @@ PassCfg pass_cfg(const Geom& g) {
   return {TW, NW};
 }
 
+// Pick the i-chunk count: minimise (scheduling rounds x capsules per workgroup)
+// given the workgroups that fit on 256 CUs, preferring chunk counts that divide
+// 8 (one i-chunk of W per XCD L2) and fewer slabs.
 int auto_chunks(const Geom& g, int NW) {
   const int n_ftiles = (g.F() + 15) / 16;
-  int c = (2560 + n_ftiles * NW - 1) / (n_ftiles * NW);
-  if (c >= 8) c = c / 8 * 8;
-  return std::max(1, std::min(c, g.in_n()));
+  const int wg_per_cu = std::max(1, 8 / NW);   // ~2 waves per SIMD at our register budget
+  const int slots = 256 * wg_per_cu;
+  int best = 1;
+  double best_cost = 1e30;
+  for (int c = 1; c <= std::min(g.in_n(), 96); ++c) {
+    const int rounds = (n_ftiles * c + slots - 1) / slots;
+    const int len = (g.in_n() + c - 1) / c;
+    double cost = (double)rounds * (len + 2);          // +2: per-workgroup prologue/epilogue
+    if (8 % c != 0 && c % 8 != 0) cost *= 1.05;          // W chunk not XCD-local
+    cost *= 1.0 + 0.002 * c;                             // slab traffic
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
 }
 
 int check_geom(const Geom& g) {
@@ -657,28 +762,31 @@ void launch_bwd_finish(const Geom& g, const float* slab, int n_chunks, const flo
                      a_init, A, s, gs);
 }
 
+constexpr int kGuTW = 4;  // row tiles per wave in the gu pass
+
+inline int gu_wgroups(const Geom& g) { return (g.NT() + 4 * kGuTW - 1) / (4 * kGuTW); }
+inline int padded_frames(const Geom& g) { return (g.F() + 15) / 16 * 16; }
+
 template <int D, int R>
 void launch_gu(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias, const float* saved,
-               const float* gs, const float* stats, float* gu, hipStream_t st) {
-  constexpr int TW = (D >= 64) ? 4 : 4;
+               const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
   const int n_ftiles = (g.F() + 15) / 16;
-  const int n_tgroups = (g.NT() + TW - 1) / TW;
+  const int n_wgroups = gu_wgroups(g);
   const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
-  const int tasks = n_ftiles * n_tgroups * n_chunks;
-  hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R>), dim3((tasks + 3) / 4), dim3(256), 0, st, emb, W, bias, g.F(),
-                     g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_tgroups, n_chunks, chunk_len, saved, gs,
-                     stats, gu);
+  hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R>), dim3(n_ftiles * n_wgroups * n_chunks), dim3(256), 0, st, emb,
+                     W, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups,
+                     n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb);
 }
 
 template <int D>
 void launch_gu_r(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias,
-                 const float* saved, const float* gs, const float* stats, float* gu, hipStream_t st) {
+                 const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
   switch (g.iters) {
-    case 1: launch_gu<D, 1>(g, n_chunks, emb, W, bias, saved, gs, stats, gu, st); break;
-    case 2: launch_gu<D, 2>(g, n_chunks, emb, W, bias, saved, gs, stats, gu, st); break;
-    case 3: launch_gu<D, 3>(g, n_chunks, emb, W, bias, saved, gs, stats, gu, st); break;
-    case 4: launch_gu<D, 4>(g, n_chunks, emb, W, bias, saved, gs, stats, gu, st); break;
-    default: launch_gu<D, 5>(g, n_chunks, emb, W, bias, saved, gs, stats, gu, st); break;
+    case 1: launch_gu<D, 1>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 2: launch_gu<D, 2>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 3: launch_gu<D, 3>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 4: launch_gu<D, 4>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    default: launch_gu<D, 5>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
   }
 }
 
@@ -687,10 +795,17 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
              float* saved, float* slab, hipStream_t st) {
   const PassCfg pc = pass_cfg(g);
   const size_t FJD = (size_t)g.F() * g.JD();
+  hipEvent_t* ev0 = t_ev_start;
+  hipEvent_t* ev1 = t_ev_stop;
+  const int nev = t_ev_n;
+  t_ev_start = t_ev_stop = nullptr;
+  t_ev_n = 0;
   for (int r = 0; r < g.iters; ++r) {
     const float* vc = r > 0 ? saved + (size_t)(2 * (r - 1) + 1) * FJD : nullptr;
+    if (r < nev) SRF_HIP_TRY(hipEventRecord(ev0[r], st));
     dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, nullptr, slab, nullptr, 1, st);
     SRF_LAUNCH_CHECK("route_pass(fwd)");
+    if (r < nev) SRF_HIP_TRY(hipEventRecord(ev1[r], st));
     launch_fwd_finish<D>(g, slab, n_chunks, vc, saved + (size_t)(2 * r) * FJD, saved + (size_t)(2 * r + 1) * FJD,
                          r == g.iters - 1 ? v_out : nullptr, st);
     SRF_LAUNCH_CHECK("fwd_finish");
@@ -699,12 +814,12 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
 }
 
 struct BwdWs {
-  float *A, *gs, *slab, *stats, *gu, *gx;
+  float *A, *gs, *slab, *stats, *gu_t, *xT;
   size_t bytes;
 };
 
 BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
-  const size_t F = g.F(), JD = g.JD(), in_n = g.in_n();
+  const size_t F = g.F(), JD = g.JD(), in_n = g.in_n(), Fp = padded_frames(g);
   size_t off = 0;
   auto take = [&](size_t nfloat) {
     size_t o = off;
@@ -712,15 +827,16 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
     return o;
   };
   const size_t oA = take(F * JD), ogs = take((size_t)g.iters * F * JD), oslab = take((size_t)n_chunks * F * JD),
-               ostats = take((size_t)g.iters * F * in_n * 2), ogu = take(F * in_n * JD), ogx = take(F * in_n * g.din);
+               ostats = take((size_t)g.iters * F * in_n * 2), ogu = take(in_n * JD * Fp),
+               oxt = take(in_n * g.din * Fp);
   char* b = static_cast<char*>(base);
   BwdWs w;
   w.A = (float*)(b + oA);
   w.gs = (float*)(b + ogs);
   w.slab = (float*)(b + oslab);
   w.stats = (float*)(b + ostats);
-  w.gu = (float*)(b + ogu);
-  w.gx = (float*)(b + ogx);
+  w.gu_t = (float*)(b + ogu);
+  w.xT = (float*)(b + oxt);
   w.bytes = off;
   return w;
 }
@@ -731,6 +847,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   const PassCfg pc = pass_cfg(g);
   const size_t FJD = (size_t)g.F() * g.JD();
   const int R = g.iters;
+  const int Fp = padded_frames(g);
   // gs^{R-1} = squash'(s^{R-1}) g_v.  A accumulates sum_{r'>r} gVc^{r'}, the
   // gradient of v^r for r < R-1 (those v reach the loss only through the logits).
   SRF_HIP_TRY(hipMemsetAsync(w.A, 0, FJD * sizeof(float), st));
@@ -749,25 +866,21 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
       SRF_LAUNCH_CHECK("bwd_finish");
     }
   }
-  launch_gu_r<D>(g, n_chunks, emb, W, bias, saved, w.gs, w.stats, w.gu, st);
+  // g_emb is accumulated by the gu pass (window adjoint folded into its scatter-add)
+  SRF_HIP_TRY(hipMemsetAsync(g_emb, 0, (size_t)g.F() * g.N * g.din * sizeof(float), st));
+  launch_gu_r<D>(g, n_chunks, emb, W, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");
   {
+    const size_t total = (size_t)g.in_n() * g.din * Fp;
+    hipLaunchKernelGGL(window_xt_kernel, dim3((total + 255) / 256), dim3(256), 0, st, emb, g.F(), Fp, g.T, g.N,
+                       g.din, g.lpad, g.in_n(), w.xT);
+    SRF_LAUNCH_CHECK("window_xt");
+  }
+  {
     const int tasks = g.in_n() * g.NT();
-    hipLaunchKernelGGL((route_gw_kernel<D>), dim3((tasks + 3) / 4), dim3(256), 0, st, w.gu, emb, g.F(), g.T, g.N,
-                       g.lpad, g.in_n(), g.JD(), g_W, g_bias);
+    hipLaunchKernelGGL((route_gw_kernel<D>), dim3((tasks + 3) / 4), dim3(256), 0, st, w.gu_t, w.xT, Fp, g.in_n(),
+                       g.JD(), g_W, g_bias);
     SRF_LAUNCH_CHECK("route_gw");
-  }
-  {
-    const int tasks = ((g.F() + 15) / 16) * g.in_n();
-    hipLaunchKernelGGL((route_gx_kernel<D>), dim3((tasks + 3) / 4), dim3(256), 0, st, w.gu, W, g.F(), g.in_n(),
-                       g.JD(), w.gx);
-    SRF_LAUNCH_CHECK("route_gx");
-  }
-  {
-    const size_t total = (size_t)g.F() * g.N * g.din;
-    hipLaunchKernelGGL(unwindow_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w.gx, g.F(), g.T, g.N, g.din,
-                       g.lpad, g.lpad + g.rpad + 1, g_emb);
-    SRF_LAUNCH_CHECK("unwindow");
   }
   return SRF_OK;
 }
@@ -775,6 +888,14 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
 }  // namespace
 
 extern "C" {
+
+int srf_route_dr_set_timing_events(void* const* starts, void* const* stops, int n) {
+  SRF_REQUIRE(n >= 0 && (n == 0 || (starts && stops)), "bad timing event arrays");
+  t_ev_start = (hipEvent_t*)starts;
+  t_ev_stop = (hipEvent_t*)stops;
+  t_ev_n = n;
+  return SRF_OK;
+}
 
 int srf_route_dr_auto_chunks(int B, int T, int N, int din, int lpad, int rpad, int J, int dout) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};

@@ -37,6 +37,7 @@ class RouteGeom:
         self.lpad, self.rpad, self.J, self.dout = lpad, rpad, J, dout
         self.iters, self.mask_first = iters, int(bool(mask_first))
         self.in_n = N * (lpad + rpad + 1)
+        self.timing = None   # optional (starts, stops) hipEvent_t arrays for the profiling hook
         L = _lib.lib()
         if n_chunks <= 0:
             n_chunks = L.srf_route_dr_auto_chunks(B, T, N, din, lpad, rpad, J, dout)
@@ -69,6 +70,11 @@ class DynamicRouting(torch.autograd.Function):
                             dtype=torch.float32)
         ws_bytes = L.srf_route_dr_fwd_workspace(*g.ws_args())
         ws = torch.empty(max(ws_bytes, 16), device=dev, dtype=torch.uint8)
+        if g.timing is not None:
+            starts, stops, n = g.timing.pop(0)
+            _lib.check(L.srf_route_dr_set_timing_events(starts, stops, n), 'set_timing_events')
+            if not g.timing:
+                g.timing = None
         rc = L.srf_route_dr_fwd(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(v), _ptr(saved), _ptr(ws),
                                 ws_bytes, _stream())
         _lib.check(rc, 'srf_route_dr_fwd')

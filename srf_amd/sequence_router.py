@@ -1,0 +1,282 @@
+"""``SequenceRouter`` -- drop-in for tfsr/model/sequence_router_naive.py:33-258.
+
+Same constructor ``SequenceRouter(config, logger, class_n)`` and call
+``model(feats, input_lengths=..., training=...)`` returning logits
+[B, ceil(T/4), class_n].  ``feats`` must already be cropped to max(inp_len)
+(trainer_sr.py:59-60), as in the reference.
+
+Compute placement: the routing layers (window + pose transform + DR) run in the
+HIP library through ``srf_amd.ops`` (no fallback); the CNN front end, primary
+capsules and the norms are assembled from torch device ops in this revision
+(DESIGN.md lists them as the next kernels).  All parameters are views into one
+flat fp32 buffer (``flat_params``) with a matching flat gradient buffer, so the
+data-parallel all-reduce and the Adam update are one launch each.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import ops
+
+SQUASH_EPS = 1e-7   # naive:248
+LENGTH_EPS = 1e-7   # naive:256
+LN_EPS = 1e-3       # Keras LayerNormalization default
+BN_EPS = 1e-3       # Keras BatchNormalization default
+BN_MOMENTUM = 0.99
+CNN_DROPOUT = 0.2   # hard-coded, sequence_router.py:62 and naive:82
+
+
+def same_pad(n, k, s):
+    out = -(-n // s)
+    total = max((out - 1) * s + k - n, 0)
+    return out, total // 2, total - total // 2
+
+
+def conv2d_same_nhwc(x, kern, bias, stride):
+    """Keras Conv2D(padding='same') on NHWC with kernel [kh, kw, Cin, Cout]."""
+    _, H, W, _ = x.shape
+    _, pt, pb = same_pad(H, kern.shape[0], stride)
+    _, pl, pr = same_pad(W, kern.shape[1], stride)
+    xn = F.pad(x.permute(0, 3, 1, 2), (pl, pr, pt, pb))
+    return F.conv2d(xn, kern.permute(3, 2, 0, 1), bias, stride=stride).permute(0, 2, 3, 1)
+
+
+def time_mask(inp_len, div, T, dtype):
+    """model_helper.py:125-140: 1 for t < ceil(len/div)."""
+    lens = (inp_len.to(torch.int64) + div - 1) // div
+    return (torch.arange(T, device=inp_len.device)[None, :] < lens[:, None]).to(dtype)
+
+
+def squash(s, dim=-1):
+    n2 = torch.sum(s * s, dim=dim, keepdim=True)
+    return n2 / (1.0 + n2) * (s / torch.sqrt(n2 + SQUASH_EPS))
+
+
+def layer_norm(x, gamma, beta):
+    return F.layer_norm(x, x.shape[-1:], gamma, beta, LN_EPS)
+
+
+class SequenceRouter(torch.nn.Module):
+    """SRF acoustic model (naive variant semantics)."""
+
+    iter = -1  # class-level like the reference (naive:40,56): shared by every instance
+
+    def __init__(self, config, logger, class_n, device=None, seed=None):
+        super().__init__()
+        dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self.stride = 2
+        self.cnn_n = config.model_conv_layer_num
+        if self.cnn_n != 2:
+            # the reference's transposed conv-list indexing only works for 2 layers
+            # (sequence_router.py:76-77)
+            raise ValueError('model-conv-layer-num must be 2 (as in the reference CapsulationLayer)')
+        self.feat_dim_in = config.feat_dim
+        self.feat_dim = math.ceil(config.feat_dim / (self.stride * self.cnn_n))   # naive:50
+        self.nfilt = config.model_conv_filter_num
+        self.class_n = class_n
+        self.enc_num = config.model_encoder_num
+        self.iter = SequenceRouter.iter = config.model_caps_iter
+        self.lpad = config.model_caps_window_lpad
+        self.rpad = config.model_caps_window_rpad
+        self.window = self.lpad + self.rpad + 1
+        self.is_context = bool(config.model_caps_context)
+        self.caps_inp_n = config.model_caps_primary_num
+        self.caps_inp_d = config.model_caps_primary_dim
+        self.caps_cov_n = config.model_caps_convolution_num
+        self.caps_cov_d = config.model_caps_convolution_dim
+        self.caps_cls_d = config.model_caps_class_dim
+        self.inp_dropout = float(config.train_inp_dropout)
+        self.inn_dropout = float(config.train_inn_dropout)
+        self.init = config.model_initializer
+        self.dropout_enabled = True     # test hook: parity runs use BN batch stats without dropout
+        self.n_chunks_override = {}     # layer -> n_chunks (tuning hook)
+
+        w = self.window
+        if self.enc_num > 1:   # (in_n, out_n, out_d, in_d), naive:88-95
+            shapes = [(self.caps_inp_n * w, self.caps_cov_n, self.caps_cov_d, self.caps_inp_d)]
+            shapes += [(self.caps_cov_n * w, self.caps_cov_n, self.caps_cov_d, self.caps_cov_d)] * (self.enc_num - 2)
+            shapes.append((self.caps_cov_n * w, class_n, self.caps_cls_d, self.caps_cov_d))
+        else:
+            shapes = [(self.caps_inp_n * w, class_n, self.caps_cls_d, self.caps_inp_d)]
+        self.layer_shapes = shapes
+
+        spec = []   # (name, shape, init)
+        cin = 1
+        for k in range(self.cnn_n):
+            for ab in 'ab':
+                spec.append((f'conv{k}{ab}_kernel', (3, 3, cin, self.nfilt), 'kernel'))
+                spec.append((f'conv{k}{ab}_bias', (self.nfilt,), 'zeros'))
+            spec.append((f'bn{k}_gamma', (self.nfilt,), 'ones'))
+            spec.append((f'bn{k}_beta', (self.nfilt,), 'zeros'))
+            cin = self.nfilt
+        spec.append(('proj_kernel', (self.feat_dim * self.nfilt, self.caps_inp_n), 'kernel'))
+        spec.append(('proj_bias', (self.caps_inp_n,), 'zeros'))
+        for e in (1, 2):
+            spec.append((f'encaps{e}_kernel', (3, 3, 1, self.caps_inp_d), 'kernel'))
+            spec.append((f'encaps{e}_bias', (self.caps_inp_d,), 'zeros'))
+        spec.append(('ln_input_gamma', (self.caps_inp_n * self.caps_inp_d,), 'ones'))
+        spec.append(('ln_input_beta', (self.caps_inp_n * self.caps_inp_d,), 'zeros'))
+        for l, (in_n, out_n, out_d, in_d) in enumerate(shapes):
+            spec.append((f'W{l}', (in_n, out_n, out_d, in_d), 'normal0.1'))
+            spec.append((f'b{l}', (in_n, out_n, out_d), 'normal0.1'))
+            spec.append((f'ln_mid{l + 1}_gamma', (out_n * out_d,), 'ones'))
+            spec.append((f'ln_mid{l + 1}_beta', (out_n * out_d,), 'zeros'))
+        spec.append(('ln_output_gamma', (class_n,), 'ones'))
+        spec.append(('ln_output_beta', (class_n,), 'zeros'))
+        self._spec = spec
+
+        offsets, off = {}, 0
+        for name, shape, _ in spec:
+            offsets[name] = off
+            off += (int(np.prod(shape)) + 63) // 64 * 64   # 256-B aligned slices (float4 kernel loads)
+        self.n_flat = off
+        self.flat_params = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.flat_grad = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.params = torch.nn.ParameterDict()
+        rng = np.random.default_rng(seed)
+        for name, shape, init in spec:
+            n = int(np.prod(shape))
+            view = self.flat_params[offsets[name]:offsets[name] + n].view(shape)
+            with torch.no_grad():
+                view.copy_(torch.from_numpy(self._init_value(rng, shape, init)))
+            p = torch.nn.Parameter(view)
+            p.grad = self.flat_grad[offsets[name]:offsets[name] + n].view(shape)
+            self.params[name] = p
+        self.offsets = offsets
+        for k in range(self.cnn_n):
+            self.register_buffer(f'bn{k}_moving_mean', torch.zeros(self.nfilt, device=dev))
+            self.register_buffer(f'bn{k}_moving_var', torch.ones(self.nfilt, device=dev))
+        self._geoms = {}
+        if logger is not None:
+            logger.info('Layer x %d, Iter x %d, Init %s, Win %d (l:%d, r:%d), ' % (
+                self.enc_num, SequenceRouter.iter, 'SDR' if self.is_context else 'DR', self.window, self.lpad,
+                self.rpad))
+
+    def _init_value(self, rng, shape, init):
+        """Keras initialisers used by the reference (model_helper.py:156-164,
+        naive:97-103); conv/dense biases, LN/BN as Keras defaults."""
+        if init == 'zeros':
+            return np.zeros(shape, np.float32)
+        if init == 'ones':
+            return np.ones(shape, np.float32)
+        if init == 'normal0.1':
+            return (0.1 * rng.standard_normal(shape)).astype(np.float32)
+        # kernel: fan_avg uniform (== glorot_uniform), or uniform(-0.05, 0.05)
+        if self.init == 'uniform':
+            return rng.uniform(-0.05, 0.05, size=shape).astype(np.float32)
+        rf = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+        fan_in, fan_out = shape[-2] * rf, shape[-1] * rf
+        lim = math.sqrt(6.0 / (fan_in + fan_out))
+        return rng.uniform(-lim, lim, size=shape).astype(np.float32)
+
+    # ------------------------------------------------------------------ utils
+    def P(self, name):
+        return self.params[name]
+
+    def zero_grad(self, set_to_none=False):
+        self.flat_grad.zero_()
+
+    def load_params(self, named):
+        """Copy parameters from a dict keyed like ``conv0a.kernel`` / ``W0``."""
+        with torch.no_grad():
+            for k, v in named.items():
+                key = k.replace('.', '_')
+                if key.endswith('moving_mean') or key.endswith('moving_var'):
+                    getattr(self, key).copy_(torch.as_tensor(v, dtype=torch.float32))
+                else:
+                    self.params[key].copy_(torch.as_tensor(v, dtype=torch.float32))
+
+    def export_params(self):
+        """Parameters + BN moving statistics as numpy, keyed like ``conv0a.kernel``."""
+        out = {}
+        for k, v in self.params.items():
+            head, _, tail = k.rpartition('_')
+            key = f'{head}.{tail}' if tail in ('kernel', 'bias', 'gamma', 'beta') else k
+            out[key] = v.detach().cpu().numpy()
+        for k in range(self.cnn_n):
+            out[f'bn{k}.moving_mean'] = getattr(self, f'bn{k}_moving_mean').cpu().numpy()
+            out[f'bn{k}.moving_var'] = getattr(self, f'bn{k}_moving_var').cpu().numpy()
+        return out
+
+    def _geom(self, l, B, T):
+        key = (l, B, T)
+        g = self._geoms.get(key)
+        if g is None:
+            in_n, out_n, out_d, in_d = self.layer_shapes[l]
+            N = in_n // self.window
+            g = ops.RouteGeom(B, T, N, in_d, self.lpad, self.rpad, out_n, out_d, self.iter,
+                              l == self.enc_num - 1, self.n_chunks_override.get(l, 0))
+            self._geoms[key] = g
+        return g
+
+    def _dropout(self, x, p, training):
+        if training and self.dropout_enabled and p > 0:
+            return F.dropout(x, p, training=True)
+        return x
+
+    # ---------------------------------------------------------------- forward
+    def cnn_fe(self, feats, inp_len, training):
+        """CapsulationLayer.call (sequence_router.py:69-82), NHWC."""
+        x = feats.unsqueeze(-1)
+        for k in range(self.cnn_n):
+            x1 = self._dropout(conv2d_same_nhwc(x, self.P(f'conv{k}a_kernel'), self.P(f'conv{k}a_bias'), 2),
+                               CNN_DROPOUT, training)
+            x2 = self._dropout(conv2d_same_nhwc(x, self.P(f'conv{k}b_kernel'), self.P(f'conv{k}b_bias'), 2),
+                               CNN_DROPOUT, training)
+            x = torch.maximum(x1, x2)
+            m = time_mask(inp_len, 2 ** (k + 1), x.shape[1], x.dtype)[:, :, None, None]
+            x = x * m
+            x = self._batch_norm(x, k, training)
+            x = x * m
+        return x
+
+    def _batch_norm(self, x, k, training):
+        gamma, beta = self.P(f'bn{k}_gamma'), self.P(f'bn{k}_beta')
+        mm, mv = getattr(self, f'bn{k}_moving_mean'), getattr(self, f'bn{k}_moving_var')
+        if training:
+            mu = x.mean(dim=(0, 1, 2))
+            var = x.var(dim=(0, 1, 2), unbiased=False)
+            with torch.no_grad():
+                n = x.numel() // x.shape[-1]
+                mm.mul_(BN_MOMENTUM).add_(mu.detach(), alpha=1 - BN_MOMENTUM)
+                mv.mul_(BN_MOMENTUM).add_(var.detach() * (n / max(n - 1, 1)), alpha=1 - BN_MOMENTUM)
+        else:
+            mu, var = mm, mv
+        return (x - mu) * torch.rsqrt(var + BN_EPS) * gamma + beta
+
+    def primary_caps(self, conv_out, inp_len, training):
+        """naive:129-142."""
+        B, T2, F2, C = conv_out.shape
+        emb = conv_out.reshape(B, T2, F2 * C) @ self.P('proj_kernel') + self.P('proj_bias')
+        emb = emb.unsqueeze(-1)
+        e1 = self._dropout(conv2d_same_nhwc(emb, self.P('encaps1_kernel'), self.P('encaps1_bias'), 1),
+                           CNN_DROPOUT, training)
+        e2 = self._dropout(conv2d_same_nhwc(emb, self.P('encaps2_kernel'), self.P('encaps2_bias'), 1),
+                           CNN_DROPOUT, training)
+        emb = torch.maximum(e1, e2) * time_mask(inp_len, 4, T2, emb.dtype)[:, :, None, None]
+        emb = squash(emb, -1)
+        flat = layer_norm(emb.reshape(B, T2, -1), self.P('ln_input_gamma'), self.P('ln_input_beta'))
+        flat = self._dropout(flat, self.inp_dropout, training)
+        return flat.reshape(B, T2, self.caps_inp_n, self.caps_inp_d)
+
+    def forward(self, feats, input_lengths=None, training=False, **kwargs):
+        inp_len = input_lengths
+        if not torch.is_tensor(inp_len):
+            inp_len = torch.as_tensor(inp_len, device=feats.device)
+        inp_len = inp_len.to(feats.device)
+        if self.is_context:
+            raise NotImplementedError('SDR (model-caps-context=True) routing kernel is not built in this revision')
+        x = self.cnn_fe(feats, inp_len, training)
+        emb = self.primary_caps(x, inp_len, training)
+        B, T2 = emb.shape[:2]
+        for l in range(self.enc_num):
+            emb = emb.contiguous()
+            v = ops.dynamic_routing(emb, self.P(f'W{l}'), self.P(f'b{l}'), self._geom(l, B, T2))
+            J, D = v.shape[2], v.shape[3]
+            flat = layer_norm(v.reshape(B, T2, J * D), self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'))
+            flat = self._dropout(flat, self.inn_dropout, training)
+            emb = flat.reshape(B, T2, J, D)
+        length = torch.sqrt(torch.sum(emb * emb, dim=-1) + LENGTH_EPS)
+        return layer_norm(length, self.P('ln_output_gamma'), self.P('ln_output_beta'))

@@ -1,0 +1,103 @@
+"""Step functions and driver of tfsr/trainer_sr.py, one process per GPU.
+
+``process_train_step`` / ``process_valid_step`` / ``process_test_step`` keep the
+reference's argument lists (trainer_sr.py:41-117).  Data parallelism replaces
+tf.distribute.MirroredStrategy (trainer_sr.py:139) with one process per GPU
+(torchrun); the implicit NCCL all-reduce inside ``apply_gradients`` becomes one
+explicit RCCL all-reduce (SUM) of the model's flat gradient buffer -- with the
+loss scaled by 1/(B_local * n_gpus) as in trainer_sr.py:58,67-68 the sum is the
+global-batch mean.
+"""
+import torch
+import torch.distributed as dist
+
+from . import ctc
+
+
+class Mean:
+    """tf.keras.metrics.Mean (trainer_sr.py:161-163)."""
+
+    def __init__(self, name=''):
+        self.name = name
+        self.reset_states()
+
+    def reset_states(self):
+        self.total = 0.0
+        self.count = 0
+
+    def update_state(self, values):
+        v = torch.as_tensor(values).detach().double().reshape(-1)
+        self.total += float(v.sum())
+        self.count += v.numel()
+
+    def result(self):
+        return self.total / self.count if self.count else 0.0
+
+
+class Sum(Mean):
+    """tf.keras.metrics.Sum (trainer_sr.py:164)."""
+
+    def result(self):
+        return self.total
+
+
+def _crop(feats, inp_len):
+    """trainer_sr.py:59-60: crop the padded batch to the longest utterance."""
+    T = int(inp_len.max())
+    return feats[:, :T, :].contiguous()
+
+
+def ceil_div(inp_len, div):
+    return (inp_len.to(torch.int64) + div - 1) // div
+
+
+def allreduce_grads(model):
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(model.flat_grad, op=dist.ReduceOp.SUM)
+
+
+def process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_state, n_gpus, blank_idx, samples):
+    """trainer_sr.py:41-75."""
+    feats, labels, inp_len, tar_len = inputs
+    batch = feats.shape[0]
+    feats = _crop(feats, inp_len)
+    model.zero_grad()
+    y_pred = model(feats, input_lengths=inp_len, training=True)
+    pe_loss = ctc.ctc_loss(labels, y_pred, tar_len, ceil_div(inp_len, in_len_div), blank_index=blank_idx)
+    loss = pe_loss.sum() / float(batch * n_gpus)
+    loss.backward()
+    allreduce_grads(model)
+    optimizer.apply_gradients(model)
+    if loss_state is not None:
+        loss_state.update_state(pe_loss)
+    if frame_state is not None:
+        frame_state.update_state(inp_len.sum())
+    if samples is not None:
+        samples.update_state(batch)
+    return pe_loss
+
+
+@torch.no_grad()
+def process_valid_step(in_len_div, inputs, model, loss_state, blank_idx):
+    """trainer_sr.py:77-94."""
+    feats, labels, inp_len, tar_len = inputs
+    feats = _crop(feats, inp_len)
+    y_pred = model(feats, input_lengths=inp_len, training=False)
+    pe_loss = ctc.ctc_loss(labels, y_pred, tar_len, ceil_div(inp_len, in_len_div), blank_index=blank_idx)
+    if loss_state is not None:
+        loss_state.update_state(pe_loss)
+    return pe_loss
+
+
+@torch.no_grad()
+def process_test_step(in_len_div, inputs, model, beam_width=None):
+    """trainer_sr.py:96-117 with best-path decoding (beam search is a next row).
+    Decode lengths use floor division, as the reference does (:110)."""
+    feats, _, inp_len, _, utt_id = inputs
+    feats = _crop(feats, inp_len)
+    y_pred = model(feats, input_lengths=inp_len, training=False)
+    hyps = ctc.greedy_decode(y_pred, inp_len.to(torch.int64) // in_len_div, y_pred.shape[-1] - 1)
+    for u, h in zip(utt_id, hyps):
+        print('UTTID:', u)
+        print(h)
+    return hyps

@@ -1,0 +1,70 @@
+"""Data-parallel path on CPU (gloo, world_size 2): the per-rank loss scaling of
+process_train_step (sum / (B_local * n_gpus), trainer_sr.py:58,67-68) followed by
+allreduce_grads (SUM over the flat gradient buffer) must give every rank the
+gradient of the global-batch mean, and identical parameters after the update."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from srf_amd import trainer_sr
+
+
+class FlatModel:
+    """Stand-in with the model's flat-buffer contract (flat_params/flat_grad)."""
+
+    def __init__(self, n):
+        g = torch.Generator().manual_seed(0)
+        self.flat_params = torch.randn(n, generator=g)
+        self.flat_grad = torch.zeros(n)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.manual_seed(100 + rank)
+    B = 3 + rank                               # ragged local batches, as bucketing yields
+    X = torch.randn(B, 5)
+    model = FlatModel(5)
+    w = model.flat_params.clone().requires_grad_()
+    per_utt = (X @ w) ** 2
+    loss = per_utt.sum() / float(B * world)    # compute_average_loss with global size B*world... per rank
+    loss.backward()
+    model.flat_grad.copy_(w.grad)
+    trainer_sr.allreduce_grads(model)
+    q.put((rank, model.flat_grad.clone(), X, B))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_allreduce_gives_global_gradient():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g0, g1 = res[0][1], res[1][1]
+    assert torch.allclose(g0, g1)
+    # reference: each rank scales by its own B (the reference's semantics), summed
+    w = FlatModel(5).flat_params.clone().requires_grad_()
+    total = sum(((X @ w) ** 2).sum() / float(B * world) for _, _, X, B in res)
+    total.backward()
+    assert torch.allclose(g0, w.grad, atol=1e-6)

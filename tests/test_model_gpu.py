@@ -1,0 +1,92 @@
+"""End-to-end GPU parity of SequenceRouter + CTC against the golden fixtures
+(numpy float64 oracle of sequence_router_naive.py; gradients from the float64
+torch mirror).  Batch-norm runs in training mode (batch statistics, as in
+process_train_step); dropout is disabled so the two sides see identical graphs.
+
+Tolerances (fp32 GPU vs fp64 oracle, stated per north_star): logits
+|err| <= 1e-4 * (1 + |ref|); CTC NLL |err| <= 1e-4 * max(1, |ref|);
+greedy label sequences bit-exact; gradients |err| <= 2e-3 * max|ref| + 1e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import config_from_shape, load_model_fixture
+
+pytestmark = pytest.mark.gpu
+
+DR_FIXTURES = ['c1_mini', 'c2_mini']
+
+
+def _build(name, dev):
+    from srf_amd.sequence_router import SequenceRouter
+    kw, sh, P, z = load_model_fixture(name)
+    cfg = config_from_shape(kw)
+    model = SequenceRouter(cfg, None, sh.class_n, device=dev)
+    model.load_params(P)
+    model.dropout_enabled = False
+    return model, sh, z
+
+
+@pytest.mark.parametrize('name', DR_FIXTURES)
+def test_forward_logits_ctc_greedy(cuda, name):
+    from srf_amd import ctc
+    model, sh, z = _build(name, cuda)
+    feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
+    inp_len = torch.tensor(z['inp_len'], device=cuda)
+    logits = model(feats, input_lengths=inp_len, training=True)
+    got = logits.detach().cpu().double().numpy()
+    ref = z['logits']
+    assert got.shape == ref.shape
+    assert np.all(np.abs(got - ref) <= 1e-4 * (1 + np.abs(ref))), np.abs(got - ref).max()
+    nll = ctc.ctc_loss(torch.tensor(z['labels'], device=cuda), logits, torch.tensor(z['tar_len'], device=cuda),
+                       (inp_len + 3) // 4, blank_index=sh.class_n - 1)
+    nll = nll.detach().cpu().double().numpy()
+    assert np.all(np.abs(nll - z['nll']) <= 1e-4 * np.maximum(1, np.abs(z['nll']))), (nll, z['nll'])
+    hyp = ctc.greedy_decode(logits, (inp_len + 3) // 4, sh.class_n - 1)
+    assert hyp == z['greedy']
+
+
+@pytest.mark.parametrize('name', DR_FIXTURES)
+def test_gradients(cuda, name):
+    from srf_amd import ctc
+    model, sh, z = _build(name, cuda)
+    feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
+    inp_len = torch.tensor(z['inp_len'], device=cuda)
+    model.zero_grad()
+    logits = model(feats, input_lengths=inp_len, training=True)
+    nll = ctc.ctc_loss(torch.tensor(z['labels'], device=cuda), logits, torch.tensor(z['tar_len'], device=cuda),
+                       (inp_len + 3) // 4, blank_index=sh.class_n - 1)
+    (nll.sum() / feats.shape[0]).backward()
+    bad = []
+    for key in z:
+        if not key.startswith('grad.'):
+            continue
+        pname = key[5:].replace('.', '_')
+        ref = z[key].astype(np.float64)
+        got = model.P(pname).grad.detach().cpu().double().numpy()
+        err = np.abs(got - ref).max()
+        if err > 2e-3 * np.abs(ref).max() + 1e-5:
+            bad.append((pname, err, np.abs(ref).max()))
+    assert not bad, bad
+
+
+def test_train_step_runs_and_updates(cuda):
+    """process_train_step: loss finite, params move after step 2 (lr(0) == 0)."""
+    from srf_amd import train_helper, trainer_sr
+    model, sh, z = _build('c2_mini', cuda)
+    model.dropout_enabled = True
+    cfg = config_from_shape({'feat_dim': 123, 'enc_num': 3, 'iters': 3, 'lpad': 4, 'rpad': 4, 'ph': 8,
+                             'pd': 16, 'ch': 8, 'cd': 16, 'vd': 16, 'context': False})
+    opt = train_helper.get_optimizer(cfg)
+    inputs = (torch.tensor(z['feats'], dtype=torch.float32, device=cuda),
+              torch.tensor(z['labels'], device=cuda), torch.tensor(z['inp_len'], device=cuda),
+              torch.tensor(z['tar_len'], device=cuda))
+    p0 = model.flat_params.clone()
+    loss_state, frames, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
+    trainer_sr.process_train_step(4, inputs, model, opt, loss_state, frames, 1, sh.class_n - 1, samples)
+    assert torch.equal(model.flat_params, p0)          # lr(0) = 0: first update is a no-op
+    trainer_sr.process_train_step(4, inputs, model, opt, loss_state, frames, 1, sh.class_n - 1, samples)
+    assert not torch.equal(model.flat_params, p0)
+    assert np.isfinite(loss_state.result())
+    assert samples.result() == 4
