@@ -55,6 +55,81 @@ int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B,
                      const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* ---- CNN front end (CapsulationLayer, tfsr/model/sequence_router.py:44-82) ---
+ * feats [B][T][feat_dim] fp32 (already cropped to max(inp_len), trainer_sr.py:59-60),
+ * inp_len [B] int32 (device).  Kernels [3][3][Cin][64] (kh, kw, cin, cout), as the
+ * reference's Conv2D variables; biases/gamma/beta [64].  The two convolutions of
+ * each stage are the reference's conv_layers[0][k] and conv_layers[1][k]
+ * (sequence_router.py:76-77).  out = mask2(BN2(.)) [B][T2][F2][64] with
+ * T2 = ceil(ceil(T/2)/2), F2 = ceil(ceil(feat_dim/2)/2) (srf_cnnfe_out_dims).
+ * training = 1: batch statistics, moving statistics updated in place (momentum
+ * 0.99), dropout drop_p on every conv output; training = 0: moving statistics,
+ * no dropout.  Dropout masks are a pure function of (seed, element), so
+ * srf_cnnfe_bwd regenerates them.  nfilt must be 64. */
+int srf_cnnfe_out_dims(int T, int feat_dim, int* T2, int* F2);
+size_t srf_cnnfe_saved_bytes(int B, int T, int feat_dim, int nfilt);
+size_t srf_cnnfe_fwd_workspace(int B, int T, int feat_dim, int nfilt);
+size_t srf_cnnfe_bwd_workspace(int B, int T, int feat_dim, int nfilt);
+int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat_dim, int nfilt,
+                  const float* k0a, const float* b0a, const float* k0b, const float* b0b, const float* gamma0,
+                  const float* beta0, const float* k1a, const float* b1a, const float* k1b, const float* b1b,
+                  const float* gamma1, const float* beta1, float* mmean0, float* mvar0, float* mmean1, float* mvar1,
+                  int training, float drop_p, unsigned long long seed, float* out, void* saved, size_t saved_bytes,
+                  void* workspace, size_t workspace_bytes, void* stream);
+/* Gradients (written) of every CNN-FE parameter from g_out = dL/d out. */
+int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat_dim, int nfilt, const float* gamma0,
+                  const float* k1a, const float* k1b, const float* gamma1, float drop_p, unsigned long long seed,
+                  const void* saved, const float* g_out, float* g_k0a, float* g_b0a, float* g_k0b, float* g_b0b,
+                  float* g_gamma0, float* g_beta0, float* g_k1a, float* g_b1a, float* g_k1b, float* g_b1b,
+                  float* g_gamma1, float* g_beta1, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- Primary capsules (sequence_router_naive.py:129-142) -------------------
+ * X = CNN-FE output viewed as [B*T][K] (K = F2*64, index f*64 + c as the
+ * reference's reshape, :131); Wp [K][PH], bp [PH]; encaps kernels [3][3][1][PD],
+ * biases [PD]; LN gamma/beta [PH*PD].  z [B*T][PH][PD] =
+ * drop_in(LN(squash_PD(mask(max(drop(encaps1(e)), drop(encaps2(e))))))).
+ * p_caps is the hard-coded 0.2 of naive:82, p_in = --train-inp-dropout. */
+size_t srf_primary_caps_saved_bytes(int B, int T, int PH, int PD);
+size_t srf_primary_caps_bwd_workspace(int B, int T, int K, int PH, int PD);
+int srf_primary_caps_fwd(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                         const float* bp, const float* K1, const float* b1, const float* K2, const float* b2,
+                         const float* gamma, const float* beta, int training, float p_caps, float p_in,
+                         unsigned long long seed, float* z, void* saved, size_t saved_bytes, void* stream);
+int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                         const float* K1, const float* K2, const float* gamma, const float* beta, int training,
+                         float p_caps, float p_in, unsigned long long seed, const void* saved, const float* g_z,
+                         float* g_X, float* g_Wp, float* g_bp, float* g_K1, float* g_b1, float* g_K2, float* g_b2,
+                         float* g_gamma, float* g_beta, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- Per-layer LayerNorm + dropout and the output head (naive:187-193) -----
+ * capsnorm: y = drop(LN(x)) per frame over n = J*D (ln_mid%d + dropout_mid_%d);
+ * head: logits[F][J] = LN_out(length_D(drop(LN_mid(v)))), lens[F][J] saved.
+ * stat [F][4] is written by the forward and read by the backward. */
+size_t srf_capsnorm_bwd_workspace(int F, int n, int J);
+int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
+                     unsigned long long seed, int layer, float* y, float* stat, void* stream);
+int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
+                     unsigned long long seed, int layer, const float* stat, const float* g_y, float* g_x,
+                     float* g_gamma, float* g_beta, void* workspace, size_t workspace_bytes, void* stream);
+int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
+                      const float* gamma_out, const float* beta_out, int training, float p, unsigned long long seed,
+                      int layer, float* logits, float* stat, float* lens, void* stream);
+int srf_caps_head_bwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
+                      const float* gamma_out, int training, float p, unsigned long long seed, int layer,
+                      const float* stat, const float* lens, const float* g_logits, float* g_v, float* g_gamma_mid,
+                      float* g_beta_mid, float* g_gamma_out, float* g_beta_out, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
+/* ---- CTC (tf.nn.ctc_loss at trainer_sr.py:64-66) ---------------------------
+ * logits [B][Tmax][C] batch-major, labels [B][Lmax] int32 (dense, padded),
+ * label_len / logit_len [B] int32 (logit_len = ceil(inp_len/4)).  nll [B]; if
+ * grad != NULL also d(grad_scale * nll_b)/d logits [B][Tmax][C] (zero past
+ * logit_len; zero for an infeasible utterance, whose nll is +inf). */
+size_t srf_ctc_workspace(int B, int Tmax, int C, int Lmax);
+int srf_ctc_loss(const float* logits, const int* labels, const int* label_len, const int* logit_len, int B, int Tmax,
+                 int C, int Lmax, int blank, float grad_scale, float* nll, float* grad, void* workspace,
+                 size_t workspace_bytes, void* stream);
+
 /* ---- Fused Adam over one flat parameter buffer ----------------------------
  * Replaces the Keras Adam apply of trainer_sr.py:71 / train_helper.py:60-70:
  * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= alpha m / (sqrt(v) + eps),

@@ -23,6 +23,34 @@ _SIGNATURES = {
     'srf_route_dr_bwd_workspace': (_c_size, [_c_int] * 10),
     'srf_route_dr_fwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _c_size, _vp]),
     'srf_route_dr_bwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    'srf_cnnfe_out_dims': (_c_int, [_c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
+    'srf_cnnfe_saved_bytes': (_c_size, [_c_int] * 4),
+    'srf_cnnfe_fwd_workspace': (_c_size, [_c_int] * 4),
+    'srf_cnnfe_bwd_workspace': (_c_size, [_c_int] * 4),
+    'srf_cnnfe_fwd': (_c_int, [_vp, _vp] + [_c_int] * 4 + [_vp] * 16 + [_c_int, ctypes.c_float, ctypes.c_ulonglong,
+                                                                       _vp, _vp, _c_size, _vp, _c_size, _vp]),
+    'srf_cnnfe_bwd': (_c_int, [_vp, _vp] + [_c_int] * 4 + [_vp] * 4 + [ctypes.c_float, ctypes.c_ulonglong]
+                      + [_vp] * 15 + [_c_size, _vp]),
+    'srf_primary_caps_saved_bytes': (_c_size, [_c_int] * 4),
+    'srf_primary_caps_bwd_workspace': (_c_size, [_c_int] * 5),
+    'srf_primary_caps_fwd': (_c_int, [_vp, _vp] + [_c_int] * 5 + [_vp] * 8 + [_c_int, ctypes.c_float, ctypes.c_float,
+                                                                           ctypes.c_ulonglong, _vp, _vp, _c_size, _vp]),
+    'srf_primary_caps_bwd': (_c_int, [_vp, _vp] + [_c_int] * 5 + [_vp] * 5 + [_c_int, ctypes.c_float, ctypes.c_float,
+                                                                           ctypes.c_ulonglong] + [_vp] * 12
+                             + [_c_size, _vp]),
+    'srf_capsnorm_bwd_workspace': (_c_size, [_c_int] * 3),
+    'srf_capsnorm_fwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong, _c_int,
+                                  _vp, _vp, _vp]),
+    'srf_capsnorm_bwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong, _c_int]
+                         + [_vp] * 6 + [_c_size, _vp]),
+    'srf_caps_head_fwd': (_c_int, [_vp, _c_int, _c_int, _c_int] + [_vp] * 4 + [_c_int, ctypes.c_float,
+                                                                              ctypes.c_ulonglong, _c_int]
+                          + [_vp] * 4),
+    'srf_caps_head_bwd': (_c_int, [_vp, _c_int, _c_int, _c_int] + [_vp] * 3 + [_c_int, ctypes.c_float,
+                                                                              ctypes.c_ulonglong, _c_int]
+                          + [_vp] * 9 + [_c_size, _vp]),
+    'srf_ctc_workspace': (_c_size, [_c_int] * 4),
+    'srf_ctc_loss': (_c_int, [_vp] * 4 + [_c_int] * 5 + [ctypes.c_float, _vp, _vp, _vp, _c_size, _vp]),
     'srf_adam_step': (_c_int, [_vp, _vp, _vp, _vp, _c_size, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                ctypes.c_float, _vp]),
 }

@@ -1,0 +1,735 @@
+// Capsule-side glue of SequenceRouter.call (sequence_router_naive.py:129-193):
+// primary capsules, the per-layer LayerNorm + dropout, and the output head.
+//
+//   proj        e[f][p] = X[f][:] . Wp[:, p] + bp[p]                   (:131-132)
+//   encaps      m = mask4(max(drop(conv3x3_1(e)), drop(conv3x3_2(e))))  (:133-135)
+//               z = drop_in(LN_in(squash_PD(m)))                        (:137-142)
+//   capsnorm    y = drop_mid(LN_mid(v)) between routing layers          (:187-191)
+//   head        logits = LN_out(length_D(drop_mid(LN_mid(v))))          (:187-193)
+// Every per-frame kernel is one 256-thread workgroup per frame (B*T' of them);
+// the frame's vector lives in LDS, reductions are wave shuffles + LDS.
+#include <algorithm>
+#include <cmath>
+
+#include "srf_common.h"
+#include "srf_rng.h"
+#include "../../include/srf.h"
+
+namespace {
+
+constexpr float kSquashEps = 1e-7f;
+constexpr float kLengthEps = 1e-7f;
+constexpr float kLnEps = 1e-3f;
+constexpr int kMaxVec = 4096;   // max per-frame vector (J*D or PH*PD) held in LDS
+
+__device__ __forceinline__ int ceil_div_len(int len, int div) { return (len + div - 1) / div; }
+
+// Sum of (a, b) over a 256-thread block; every thread gets the totals.
+__device__ __forceinline__ void block_sum2(float& a, float& b, float* red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) {
+    red[w] = a;
+    red[4 + w] = b;
+  }
+  __syncthreads();
+  a = red[0] + red[1] + red[2] + red[3];
+  b = red[4] + red[5] + red[6] + red[7];
+}
+
+__device__ __forceinline__ float drop_mult(bool on, unsigned long long seed, unsigned stream, size_t idx, float p) {
+  if (!on) return 1.f;
+  return srf_keep(seed, stream, idx, p) ? 1.f / (1.f - p) : 0.f;
+}
+
+// ---------------------------------------------------------------- proj
+// One wave per frame, outputs in groups of 8.
+__global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__ X, int F, int K, int PH,
+                                                       const float* __restrict__ Wp, const float* __restrict__ bp,
+                                                       float* __restrict__ e) {
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int l = threadIdx.x & 63;
+  if (f >= F) return;
+  const float* x = X + (size_t)f * K;
+  for (int p0 = 0; p0 < PH; p0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int k = l; k < K; k += 64) {
+      const float xv = x[k];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (p0 + q < PH) acc[q] += xv * Wp[(size_t)k * PH + p0 + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float s = wave_sum(acc[q]);
+      if (l == 0 && p0 + q < PH) e[(size_t)f * PH + p0 + q] = s + bp[p0 + q];
+    }
+  }
+}
+
+// g_X[f][k] = sum_p g_e[f][p] Wp[k][p]
+__global__ void proj_bwd_x_kernel(const float* __restrict__ g_e, const float* __restrict__ Wp, int F, int K, int PH,
+                                  float* __restrict__ g_X) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)F * K) return;
+  const int k = idx % K;
+  const size_t f = idx / K;
+  float s = 0.f;
+  for (int p = 0; p < PH; ++p) s += g_e[f * PH + p] * Wp[(size_t)k * PH + p];
+  g_X[idx] = s;
+}
+
+// part[chunk][k*PH + p] = sum_{f in chunk} X[f][k] g_e[f][p]; row K*PH holds the bias partials.
+__global__ void proj_bwd_w_kernel(const float* __restrict__ X, const float* __restrict__ g_e, int F, int K, int PH,
+                                  int fchunk, float* __restrict__ part) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ch = blockIdx.y;
+  const int f0 = ch * fchunk, f1 = min(F, f0 + fchunk);
+  const int cols = K * PH + PH;
+  if (k < K) {
+    for (int p0 = 0; p0 < PH; p0 += 8) {
+      float acc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+      for (int f = f0; f < f1; ++f) {
+        const float xv = X[(size_t)f * K + k];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (p0 + q < PH) acc[q] += xv * g_e[(size_t)f * PH + p0 + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (p0 + q < PH) part[(size_t)ch * cols + (size_t)k * PH + p0 + q] = acc[q];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < PH) {
+    float s = 0.f;
+    for (int f = f0; f < f1; ++f) s += g_e[(size_t)f * PH + threadIdx.x];
+    part[(size_t)ch * cols + (size_t)K * PH + threadIdx.x] = s;
+  }
+}
+
+__global__ void colsum_kernel2(const float* __restrict__ in, int rows, int cols, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += in[(size_t)r * cols + c];
+  out[c] = s;
+}
+
+// ---------------------------------------------------------------- encaps
+struct CapsDims {
+  int B, T, PH, PD;   // T = T' frames per utterance
+};
+
+__device__ __forceinline__ float encaps_conv(const float* __restrict__ e3, int PH, int p, int d,
+                                             const float* __restrict__ K, float bias, int PD) {
+  // e3: 3 x PH neighbourhood in LDS (rows t-1, t, t+1; zero when outside [0,T))
+  float v = bias;
+#pragma unroll
+  for (int dt = 0; dt < 3; ++dt)
+#pragma unroll
+    for (int dp = 0; dp < 3; ++dp) {
+      const int pp = p + dp - 1;
+      if (pp >= 0 && pp < PH) v += e3[dt * PH + pp] * K[(dt * 3 + dp) * PD + d];
+    }
+  return v;
+}
+
+__device__ __forceinline__ void load_e3(const float* __restrict__ e, int f, const CapsDims& cd, float* e3) {
+  const int t = f % cd.T;
+  for (int i = threadIdx.x; i < 3 * cd.PH; i += blockDim.x) {
+    const int dt = i / cd.PH, p = i - dt * cd.PH;
+    const int tt = t + dt - 1;
+    e3[i] = (tt >= 0 && tt < cd.T) ? e[(size_t)(f + dt - 1) * cd.PH + p] : 0.f;
+  }
+}
+
+// Per-frame squash factors over PD for every p (m in LDS), written to fac[p].
+__device__ __forceinline__ void squash_factors(const float* m, int PH, int PD, float* fac, float* n2s) {
+  for (int p = threadIdx.x; p < PH; p += blockDim.x) {
+    float n2 = 0.f;
+    for (int d = 0; d < PD; ++d) n2 += m[p * PD + d] * m[p * PD + d];
+    fac[p] = n2 / (1.f + n2) / sqrtf(n2 + kSquashEps);
+    n2s[p] = n2;
+  }
+}
+
+__global__ __launch_bounds__(256) void encaps_fwd_kernel(
+    const float* __restrict__ e, const int* __restrict__ inp_len, CapsDims cd, const float* __restrict__ K1,
+    const float* __restrict__ b1, const float* __restrict__ K2, const float* __restrict__ b2,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int training, float p_caps, float p_in,
+    unsigned long long seed, float* __restrict__ m_out, unsigned char* __restrict__ sel,
+    float* __restrict__ lnstat, float* __restrict__ z) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int E = cd.PH * cd.PD;
+  float* m = sm;                 // E
+  float* e3 = m + E;             // 3*PH
+  float* fac = e3 + 3 * cd.PH;   // PH
+  float* n2s = fac + cd.PH;      // PH
+  float* red = n2s + cd.PH;      // 8
+  const int f = blockIdx.x;
+  const int b = f / cd.T, t = f - b * cd.T;
+  const bool valid_t = t < ceil_div_len(inp_len[b], 4);
+  load_e3(e, f, cd, e3);
+  __syncthreads();
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const int p = i / cd.PD, d = i - p * cd.PD;
+    const size_t gi = (size_t)f * E + i;
+    const float v1 = encaps_conv(e3, cd.PH, p, d, K1, b1[d], cd.PD) *
+                     drop_mult(training && p_caps > 0.f, seed, kStreamEncaps1, gi, p_caps);
+    const float v2 = encaps_conv(e3, cd.PH, p, d, K2, b2[d], cd.PD) *
+                     drop_mult(training && p_caps > 0.f, seed, kStreamEncaps2, gi, p_caps);
+    const bool s = v1 >= v2;
+    const float mv = valid_t ? (s ? v1 : v2) : 0.f;
+    m[i] = mv;
+    m_out[gi] = mv;
+    sel[gi] = s ? 1 : 0;
+  }
+  __syncthreads();
+  squash_factors(m, cd.PH, cd.PD, fac, n2s);
+  __syncthreads();
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const float sq = m[i] * fac[i / cd.PD];
+    s1 += sq;
+  }
+  float dummy = 0.f;
+  block_sum2(s1, dummy, red);
+  const float mean = s1 / E;
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const float dv = m[i] * fac[i / cd.PD] - mean;
+    s2 += dv * dv;
+  }
+  dummy = 0.f;
+  block_sum2(s2, dummy, red);
+  const float rstd = 1.f / sqrtf(s2 / E + kLnEps);
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const size_t gi = (size_t)f * E + i;
+    const float y = (m[i] * fac[i / cd.PD] - mean) * rstd * gamma[i] + beta[i];
+    z[gi] = y * drop_mult(training && p_in > 0.f, seed, kStreamInput, gi, p_in);
+  }
+  if (threadIdx.x == 0) {
+    lnstat[2 * f] = mean;
+    lnstat[2 * f + 1] = rstd;
+  }
+}
+
+// squash backward for one capsule: gs = g*gv + 2 g'(n2) (s.gv) s, element d.
+__device__ __forceinline__ float squash_bwd_elem(float s_d, float gv_d, float n2, float sdotg) {
+  const float rs = 1.f / sqrtf(n2 + kSquashEps);
+  const float ip = 1.f / (1.f + n2);
+  const float gfac = n2 * ip * rs;
+  const float dg = rs * ip * (ip - 0.5f * n2 / (n2 + kSquashEps));
+  return gfac * gv_d + 2.f * dg * sdotg * s_d;
+}
+
+// Backward part A (per frame): through input dropout, LN_in, squash, mask,
+// maxout and encaps dropout to the two conv outputs g_v1, g_v2; LN gamma/beta
+// and encaps kernel/bias gradient partials per frame:
+//   wpart[f][0 .. 2E)                 g_gamma_in, g_beta_in contributions
+//   wpart[f][2E + k*10*PD + tap*PD+d] g_K_k  (tap 9 = bias)
+__global__ __launch_bounds__(256) void encaps_bwd_a_kernel(
+    const float* __restrict__ g_z, const float* __restrict__ e, const float* __restrict__ m_in,
+    const unsigned char* __restrict__ sel, const float* __restrict__ lnstat, const int* __restrict__ inp_len,
+    CapsDims cd, const float* __restrict__ gamma, const float* __restrict__ beta, int training, float p_caps,
+    float p_in, unsigned long long seed, float* __restrict__ g_v1, float* __restrict__ g_v2,
+    float* __restrict__ wpart) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int E = cd.PH * cd.PD;
+  float* m = sm;                 // E
+  float* gs = m + E;             // E   (grad wrt squash output, then wrt m)
+  float* gv = gs + E;            // 2E  (g_v1, g_v2 for the wgrad partials)
+  float* e3 = gv + 2 * E;        // 3*PH
+  float* fac = e3 + 3 * cd.PH;   // PH
+  float* n2s = fac + cd.PH;      // PH
+  float* sdg = n2s + cd.PH;      // PH
+  float* red = sdg + cd.PH;      // 8
+  const int f = blockIdx.x;
+  const int b = f / cd.T, t = f - b * cd.T;
+  const bool valid_t = t < ceil_div_len(inp_len[b], 4);
+  const float mean = lnstat[2 * f], rstd = lnstat[2 * f + 1];
+  for (int i = threadIdx.x; i < E; i += blockDim.x) m[i] = m_in[(size_t)f * E + i];
+  load_e3(e, f, cd, e3);
+  __syncthreads();
+  squash_factors(m, cd.PH, cd.PD, fac, n2s);
+  __syncthreads();
+  // LN backward: gy = g_z * drop; xh = (s - mean) * rstd
+  float a1 = 0.f, a2 = 0.f;
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const size_t gi = (size_t)f * E + i;
+    const float gy = g_z[gi] * drop_mult(training && p_in > 0.f, seed, kStreamInput, gi, p_in);
+    const float xh = (m[i] * fac[i / cd.PD] - mean) * rstd;
+    wpart[(size_t)f * (2 * E + 20 * cd.PD) + i] = gy * xh;       // g_gamma
+    wpart[(size_t)f * (2 * E + 20 * cd.PD) + E + i] = gy;        // g_beta
+    const float gx = gy * gamma[i];
+    gs[i] = gx;
+    a1 += gx;
+    a2 += gx * xh;
+  }
+  block_sum2(a1, a2, red);
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const float xh = (m[i] * fac[i / cd.PD] - mean) * rstd;
+    gs[i] = rstd * (gs[i] - a1 / E - xh * a2 / E);
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < cd.PH; p += blockDim.x) {
+    float sg = 0.f;
+    for (int d = 0; d < cd.PD; ++d) sg += m[p * cd.PD + d] * gs[p * cd.PD + d];
+    sdg[p] = sg;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const int p = i / cd.PD;
+    const size_t gi = (size_t)f * E + i;
+    float gm = valid_t ? squash_bwd_elem(m[i], gs[i], n2s[p], sdg[p]) : 0.f;
+    const bool s = sel[gi] != 0;
+    const float g1 = (s ? gm : 0.f) * drop_mult(training && p_caps > 0.f, seed, kStreamEncaps1, gi, p_caps);
+    const float g2 = (s ? 0.f : gm) * drop_mult(training && p_caps > 0.f, seed, kStreamEncaps2, gi, p_caps);
+    g_v1[gi] = g1;
+    g_v2[gi] = g2;
+    gv[i] = g1;
+    gv[E + i] = g2;
+  }
+  __syncthreads();
+  // kernel/bias partials: out j = (k, tap, d), tap 9 = bias
+  for (int j = threadIdx.x; j < 20 * cd.PD; j += blockDim.x) {
+    const int k = j / (10 * cd.PD);
+    const int tap = (j / cd.PD) % 10, d = j % cd.PD;
+    const float* g = gv + k * E;
+    float s = 0.f;
+    if (tap == 9) {
+      for (int p = 0; p < cd.PH; ++p) s += g[p * cd.PD + d];
+    } else {
+      const int dt = tap / 3, dp = tap % 3;
+      for (int p = 0; p < cd.PH; ++p) {
+        const int pp = p + dp - 1;
+        if (pp >= 0 && pp < cd.PH) s += g[p * cd.PD + d] * e3[dt * cd.PH + pp];
+      }
+    }
+    wpart[(size_t)f * (2 * E + 20 * cd.PD) + 2 * E + j] = s;
+  }
+}
+
+// Backward part B: g_e[t'][p'] = sum_{k,dt,dp,d} g_vk[t'-dt+1][p'-dp+1][d] K_k[dt][dp][d].
+__global__ void encaps_bwd_b_kernel(const float* __restrict__ g_v1, const float* __restrict__ g_v2, CapsDims cd,
+                                    const float* __restrict__ K1, const float* __restrict__ K2,
+                                    float* __restrict__ g_e) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int F = cd.B * cd.T;
+  if (idx >= F * cd.PH) return;
+  const int p = idx % cd.PH, f = idx / cd.PH;
+  const int t = f % cd.T;
+  const int E = cd.PH * cd.PD;
+  float s = 0.f;
+  for (int dt = 0; dt < 3; ++dt) {
+    const int tt = t - dt + 1;
+    if (tt < 0 || tt >= cd.T) continue;
+    const size_t fo = (size_t)(f - dt + 1) * E;
+    for (int dp = 0; dp < 3; ++dp) {
+      const int pp = p - dp + 1;
+      if (pp < 0 || pp >= cd.PH) continue;
+      for (int d = 0; d < cd.PD; ++d)
+        s += g_v1[fo + pp * cd.PD + d] * K1[(dt * 3 + dp) * cd.PD + d] +
+             g_v2[fo + pp * cd.PD + d] * K2[(dt * 3 + dp) * cd.PD + d];
+    }
+  }
+  g_e[idx] = s;
+}
+
+// ---------------------------------------------------------------- LN + dropout
+// y = drop(LN(x)) over vectors of length n (one frame per workgroup); also the
+// output head: logits = LN_out(length_D(drop(LN_mid(v)))) when head != 0.
+__global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restrict__ x, int n,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int training, float p,
+                                                           unsigned long long seed, unsigned stream,
+                                                           float* __restrict__ y, float* __restrict__ stat, int head,
+                                                           int J, int D, const float* __restrict__ gamma_o,
+                                                           const float* __restrict__ beta_o,
+                                                           float* __restrict__ logits, float* __restrict__ lens) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* v = sm;           // n
+  float* red = v + n;      // 8
+  const int f = blockIdx.x;
+  float s1 = 0.f, dummy = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float a = x[(size_t)f * n + i];
+    v[i] = a;
+    s1 += a;
+  }
+  block_sum2(s1, dummy, red);
+  const float mean = s1 / n;
+  float s2 = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float dv = v[i] - mean;
+    s2 += dv * dv;
+  }
+  dummy = 0.f;
+  block_sum2(s2, dummy, red);
+  const float rstd = 1.f / sqrtf(s2 / n + kLnEps);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const size_t gi = (size_t)f * n + i;
+    const float o = ((v[i] - mean) * rstd * gamma[i] + beta[i]) * drop_mult(training && p > 0.f, seed, stream, gi, p);
+    v[i] = o;
+    if (!head) y[gi] = o;
+  }
+  if (threadIdx.x == 0) {
+    stat[4 * f] = mean;
+    stat[4 * f + 1] = rstd;
+  }
+  if (!head) return;
+  __syncthreads();
+  // length over D (naive:255-258), then LN_out over the J capsules
+  float* L = v + n + 8;   // J
+  for (int j = threadIdx.x; j < J; j += blockDim.x) {
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += v[j * D + d] * v[j * D + d];
+    L[j] = sqrtf(s + kLengthEps);
+    lens[(size_t)f * J + j] = L[j];
+  }
+  __syncthreads();
+  float t1 = 0.f;
+  dummy = 0.f;
+  for (int j = threadIdx.x; j < J; j += blockDim.x) t1 += L[j];
+  block_sum2(t1, dummy, red);
+  const float mo = t1 / J;
+  float t2 = 0.f;
+  for (int j = threadIdx.x; j < J; j += blockDim.x) t2 += (L[j] - mo) * (L[j] - mo);
+  dummy = 0.f;
+  block_sum2(t2, dummy, red);
+  const float ro = 1.f / sqrtf(t2 / J + kLnEps);
+  for (int j = threadIdx.x; j < J; j += blockDim.x)
+    logits[(size_t)f * J + j] = (L[j] - mo) * ro * gamma_o[j] + beta_o[j];
+  if (threadIdx.x == 0) {
+    stat[4 * f + 2] = mo;
+    stat[4 * f + 3] = ro;
+  }
+}
+
+// Backward of capsnorm_fwd.  gpart[f][0..n) = g_gamma contributions, [n..2n) g_beta;
+// head: gpart[f][2n..2n+J) g_gamma_out, [2n+J..2n+2J) g_beta_out.
+//   head: o = drop(LN_mid(x)), L_j = sqrt(|o_j|^2 + eps), logits = LN_out(L)
+//         g_o = g_L_j * o / L_j (naive:255-258)
+__global__ __launch_bounds__(256) void capsnorm_bwd_kernel(
+    const float* __restrict__ x, int n, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int training, float p, unsigned long long seed, unsigned stream, const float* __restrict__ stat,
+    const float* __restrict__ g_in, int head, int J, int D, const float* __restrict__ gamma_o,
+    const float* __restrict__ lens, float* __restrict__ g_x, float* __restrict__ gpart) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* gy = sm;          // n
+  float* red = gy + n;     // 8
+  float* gl = red + 8;     // J
+  const int f = blockIdx.x;
+  const float mean = stat[4 * f], rstd = stat[4 * f + 1];
+  const size_t stride = head ? (size_t)2 * n + 2 * J : (size_t)2 * n;
+  if (head) {
+    const float mo = stat[4 * f + 2], ro = stat[4 * f + 3];
+    float a1 = 0.f, a2 = 0.f;
+    for (int j = threadIdx.x; j < J; j += blockDim.x) {
+      const float go = g_in[(size_t)f * J + j];
+      const float xh = (lens[(size_t)f * J + j] - mo) * ro;
+      gpart[(size_t)f * stride + 2 * n + j] = go * xh;
+      gpart[(size_t)f * stride + 2 * n + J + j] = go;
+      const float gx = go * gamma_o[j];
+      gl[j] = gx;
+      a1 += gx;
+      a2 += gx * xh;
+    }
+    block_sum2(a1, a2, red);
+    for (int j = threadIdx.x; j < J; j += blockDim.x) {
+      const float xh = (lens[(size_t)f * J + j] - mo) * ro;
+      gl[j] = ro * (gl[j] - a1 / J - xh * a2 / J) / lens[(size_t)f * J + j];
+    }
+    __syncthreads();
+  }
+  float a1 = 0.f, a2 = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const size_t gi = (size_t)f * n + i;
+    const float xh = (x[gi] - mean) * rstd;
+    const float dm = drop_mult(training && p > 0.f, seed, stream, gi, p);
+    float go;
+    if (head) {
+      const float o = (xh * gamma[i] + beta[i]) * dm;
+      go = gl[i / D] * o;
+    } else {
+      go = g_in[gi];
+    }
+    const float g = go * dm;   // gradient wrt the LN output
+    gpart[(size_t)f * stride + i] = g * xh;
+    gpart[(size_t)f * stride + n + i] = g;
+    const float t = g * gamma[i];
+    gy[i] = t;
+    a1 += t;
+    a2 += t * xh;
+  }
+  block_sum2(a1, a2, red);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const size_t gi = (size_t)f * n + i;
+    const float xh = (x[gi] - mean) * rstd;
+    g_x[gi] = rstd * (gy[i] - a1 / n - xh * a2 / n);
+  }
+}
+
+// ---------------------------------------------------------------- host
+struct CapsSaved {
+  float *e, *m, *lnstat;
+  unsigned char* sel;
+  size_t bytes;
+};
+
+CapsSaved caps_saved_layout(int F, int PH, int PD, void* base) {
+  const size_t E = (size_t)PH * PD;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += srf::align_up(bytes, 256);
+    return o;
+  };
+  const size_t oe = take((size_t)F * PH * 4), om = take((size_t)F * E * 4), os = take((size_t)F * 2 * 4),
+               osel = take((size_t)F * E);
+  char* b = static_cast<char*>(base);
+  CapsSaved c;
+  c.e = (float*)(b + oe);
+  c.m = (float*)(b + om);
+  c.lnstat = (float*)(b + os);
+  c.sel = (unsigned char*)(b + osel);
+  c.bytes = off;
+  return c;
+}
+
+struct CapsBwdWs {
+  float *gv1, *gv2, *wpart, *wsum, *g_e, *ppart, *psum;
+  size_t bytes;
+};
+
+constexpr int kProjChunks = 16;
+
+CapsBwdWs caps_bwd_layout(int F, int K, int PH, int PD, void* base) {
+  const size_t E = (size_t)PH * PD;
+  const size_t wcols = 2 * E + 20 * PD, pcols = (size_t)K * PH + PH;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += srf::align_up(bytes, 256);
+    return o;
+  };
+  const size_t o1 = take((size_t)F * E * 4), o2 = take((size_t)F * E * 4), ow = take((size_t)F * wcols * 4),
+               owsum = take(wcols * 4), oge = take((size_t)F * PH * 4), opp = take(kProjChunks * pcols * 4),
+               ops = take(pcols * 4);
+  char* b = static_cast<char*>(base);
+  CapsBwdWs w;
+  w.gv1 = (float*)(b + o1);
+  w.gv2 = (float*)(b + o2);
+  w.wpart = (float*)(b + ow);
+  w.wsum = (float*)(b + owsum);
+  w.g_e = (float*)(b + oge);
+  w.ppart = (float*)(b + opp);
+  w.psum = (float*)(b + ops);
+  w.bytes = off;
+  return w;
+}
+
+__global__ void scatter_encaps_grads(const float* __restrict__ wsum, int E, int PD, float* __restrict__ g_gamma,
+                                     float* __restrict__ g_beta, float* __restrict__ gK1, float* __restrict__ gb1,
+                                     float* __restrict__ gK2, float* __restrict__ gb2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < E) {
+    g_gamma[i] = wsum[i];
+    g_beta[i] = wsum[E + i];
+  }
+  if (i < 20 * PD) {
+    const int k = i / (10 * PD), tap = (i / PD) % 10, d = i % PD;
+    const float v = wsum[2 * E + i];
+    if (tap < 9)
+      (k == 0 ? gK1 : gK2)[tap * PD + d] = v;
+    else
+      (k == 0 ? gb1 : gb2)[d] = v;
+  }
+}
+
+__global__ void split_copy(const float* __restrict__ src, int n0, float* __restrict__ d0, int n1,
+                           float* __restrict__ d1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n0) d0[i] = src[i];
+  if (i < n1) d1[i] = src[n0 + i];
+}
+
+int check_caps(int B, int T, int PH, int PD) {
+  SRF_REQUIRE(B > 0 && T > 0 && PH > 0 && PD > 0, "bad primary capsule shape");
+  SRF_REQUIRE((size_t)PH * PD <= kMaxVec, "PH*PD = %d exceeds %d", PH * PD, kMaxVec);
+  return SRF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t srf_primary_caps_saved_bytes(int B, int T, int PH, int PD) {
+  return caps_saved_layout(B * T, PH, PD, nullptr).bytes;
+}
+
+size_t srf_primary_caps_bwd_workspace(int B, int T, int K, int PH, int PD) {
+  return caps_bwd_layout(B * T, K, PH, PD, nullptr).bytes;
+}
+
+int srf_primary_caps_fwd(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                         const float* bp, const float* K1, const float* b1, const float* K2, const float* b2,
+                         const float* gamma, const float* beta, int training, float p_caps, float p_in,
+                         unsigned long long seed, float* z, void* saved, size_t saved_bytes, void* stream) {
+  int rc = check_caps(B, T, PH, PD);
+  if (rc) return rc;
+  SRF_REQUIRE(X && inp_len && Wp && bp && K1 && b1 && K2 && b2 && gamma && beta && z && saved, "null pointer");
+  const int F = B * T;
+  CapsSaved sv = caps_saved_layout(F, PH, PD, saved);
+  if (saved_bytes < sv.bytes) {
+    srf::set_error("primary caps saved buffer too small: %zu < %zu", saved_bytes, sv.bytes);
+    return SRF_EWORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(proj_fwd_kernel, dim3((F + 3) / 4), dim3(256), 0, st, X, F, K, PH, Wp, bp, sv.e);
+  SRF_LAUNCH_CHECK("proj_fwd");
+  CapsDims cd{B, T, PH, PD};
+  const size_t sh = (size_t)(PH * PD + 5 * PH + 8) * sizeof(float);
+  hipLaunchKernelGGL(encaps_fwd_kernel, dim3(F), dim3(256), sh, st, sv.e, inp_len, cd, K1, b1, K2, b2, gamma, beta,
+                     training, p_caps, p_in, seed, sv.m, sv.sel, sv.lnstat, z);
+  SRF_LAUNCH_CHECK("encaps_fwd");
+  return SRF_OK;
+}
+
+int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                         const float* K1, const float* K2, const float* gamma, const float* beta, int training,
+                         float p_caps, float p_in, unsigned long long seed, const void* saved, const float* g_z,
+                         float* g_X, float* g_Wp, float* g_bp, float* g_K1, float* g_b1, float* g_K2, float* g_b2,
+                         float* g_gamma, float* g_beta, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_caps(B, T, PH, PD);
+  if (rc) return rc;
+  SRF_REQUIRE(X && inp_len && Wp && K1 && K2 && gamma && beta && saved && g_z && g_X && g_Wp && g_bp && g_K1 &&
+                  g_b1 && g_K2 && g_b2 && g_gamma && g_beta && workspace,
+              "null pointer");
+  const int F = B * T, E = PH * PD;
+  CapsSaved sv = caps_saved_layout(F, PH, PD, const_cast<void*>(saved));
+  CapsBwdWs w = caps_bwd_layout(F, K, PH, PD, workspace);
+  if (workspace_bytes < w.bytes) {
+    srf::set_error("primary caps workspace too small: %zu < %zu", workspace_bytes, w.bytes);
+    return SRF_EWORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  CapsDims cd{B, T, PH, PD};
+  const size_t sh = (size_t)(4 * E + 6 * PH + 8) * sizeof(float);
+  hipLaunchKernelGGL(encaps_bwd_a_kernel, dim3(F), dim3(256), sh, st, g_z, sv.e, sv.m, sv.sel, sv.lnstat, inp_len, cd,
+                     gamma, beta, training, p_caps, p_in, seed, w.gv1, w.gv2, w.wpart);
+  SRF_LAUNCH_CHECK("encaps_bwd_a");
+  const int wcols = 2 * E + 20 * PD;
+  hipLaunchKernelGGL(colsum_kernel2, dim3((wcols + 255) / 256), dim3(256), 0, st, w.wpart, F, wcols, w.wsum);
+  SRF_LAUNCH_CHECK("colsum(encaps)");
+  hipLaunchKernelGGL(scatter_encaps_grads, dim3((std::max(E, 20 * PD) + 255) / 256), dim3(256), 0, st, w.wsum, E, PD,
+                     g_gamma, g_beta, g_K1, g_b1, g_K2, g_b2);
+  SRF_LAUNCH_CHECK("scatter_encaps_grads");
+  hipLaunchKernelGGL(encaps_bwd_b_kernel, dim3((F * PH + 255) / 256), dim3(256), 0, st, w.gv1, w.gv2, cd, K1, K2,
+                     w.g_e);
+  SRF_LAUNCH_CHECK("encaps_bwd_b");
+  hipLaunchKernelGGL(proj_bwd_x_kernel, dim3(((size_t)F * K + 255) / 256), dim3(256), 0, st, w.g_e, Wp, F, K, PH,
+                     g_X);
+  SRF_LAUNCH_CHECK("proj_bwd_x");
+  const int fchunk = (F + kProjChunks - 1) / kProjChunks;
+  hipLaunchKernelGGL(proj_bwd_w_kernel, dim3((K + 255) / 256, kProjChunks), dim3(256), 0, st, X, w.g_e, F, K, PH,
+                     fchunk, w.ppart);
+  SRF_LAUNCH_CHECK("proj_bwd_w");
+  const int pcols = K * PH + PH;
+  hipLaunchKernelGGL(colsum_kernel2, dim3((pcols + 255) / 256), dim3(256), 0, st, w.ppart, kProjChunks, pcols,
+                     w.psum);
+  SRF_LAUNCH_CHECK("colsum(proj)");
+  hipLaunchKernelGGL(split_copy, dim3((K * PH + 255) / 256), dim3(256), 0, st, w.psum, K * PH, g_Wp, PH, g_bp);
+  SRF_LAUNCH_CHECK("split_copy(proj)");
+  return SRF_OK;
+}
+
+size_t srf_capsnorm_bwd_workspace(int F, int n, int J) {
+  return srf::align_up((size_t)F * (2 * n + 2 * J) * 4, 256) + srf::align_up((size_t)(2 * n + 2 * J) * 4, 256);
+}
+
+int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
+                     unsigned long long seed, int layer, float* y, float* stat, void* stream) {
+  SRF_REQUIRE(x && gamma && beta && y && stat && F > 0 && n > 0 && n <= kMaxVec, "bad capsnorm arguments");
+  hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, static_cast<hipStream_t>(stream),
+                     x, n, gamma, beta, training, p, seed, (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0,
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr);
+  SRF_LAUNCH_CHECK("capsnorm_fwd");
+  return SRF_OK;
+}
+
+int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
+                     unsigned long long seed, int layer, const float* stat, const float* g_y, float* g_x,
+                     float* g_gamma, float* g_beta, void* workspace, size_t workspace_bytes, void* stream) {
+  SRF_REQUIRE(x && gamma && beta && stat && g_y && g_x && g_gamma && g_beta && workspace && F > 0 && n > 0 &&
+                  n <= kMaxVec,
+              "bad capsnorm arguments");
+  if (workspace_bytes < srf_capsnorm_bwd_workspace(F, n, 0)) {
+    srf::set_error("capsnorm workspace too small");
+    return SRF_EWORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(workspace);
+  float* sum = part + srf::align_up((size_t)F * 2 * n * 4, 256) / 4;
+  hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, st, x, n, gamma, beta, training, p,
+                     seed, (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr,
+                     (const float*)nullptr, g_x, part);
+  SRF_LAUNCH_CHECK("capsnorm_bwd");
+  hipLaunchKernelGGL(colsum_kernel2, dim3((2 * n + 255) / 256), dim3(256), 0, st, part, F, 2 * n, sum);
+  SRF_LAUNCH_CHECK("colsum(capsnorm)");
+  hipLaunchKernelGGL(split_copy, dim3((n + 255) / 256), dim3(256), 0, st, sum, n, g_gamma, n, g_beta);
+  SRF_LAUNCH_CHECK("split_copy(capsnorm)");
+  return SRF_OK;
+}
+
+int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
+                      const float* gamma_out, const float* beta_out, int training, float p, unsigned long long seed,
+                      int layer, float* logits, float* stat, float* lens, void* stream) {
+  const int n = J * D;
+  SRF_REQUIRE(v && gamma_mid && beta_mid && gamma_out && beta_out && logits && stat && lens && F > 0 && n > 0 &&
+                  n <= kMaxVec,
+              "bad head arguments");
+  hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4,
+                     static_cast<hipStream_t>(stream), v, n, gamma_mid, beta_mid, training, p, seed,
+                     (unsigned)(kStreamMid0 + layer), (float*)nullptr, stat, 1, J, D, gamma_out, beta_out, logits,
+                     lens);
+  SRF_LAUNCH_CHECK("caps_head_fwd");
+  return SRF_OK;
+}
+
+int srf_caps_head_bwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
+                      const float* gamma_out, int training, float p, unsigned long long seed, int layer,
+                      const float* stat, const float* lens, const float* g_logits, float* g_v, float* g_gamma_mid,
+                      float* g_beta_mid, float* g_gamma_out, float* g_beta_out, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+  const int n = J * D;
+  SRF_REQUIRE(v && gamma_mid && beta_mid && gamma_out && stat && lens && g_logits && g_v && g_gamma_mid &&
+                  g_beta_mid && g_gamma_out && g_beta_out && workspace && F > 0 && n <= kMaxVec,
+              "bad head arguments");
+  if (workspace_bytes < srf_capsnorm_bwd_workspace(F, n, J)) {
+    srf::set_error("head workspace too small");
+    return SRF_EWORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int cols = 2 * n + 2 * J;
+  float* part = static_cast<float*>(workspace);
+  float* sum = part + srf::align_up((size_t)F * cols * 4, 256) / 4;
+  hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4, st, v, n, gamma_mid, beta_mid,
+                     training, p, seed, (unsigned)(kStreamMid0 + layer), stat, g_logits, 1, J, D, gamma_out, lens,
+                     g_v, part);
+  SRF_LAUNCH_CHECK("caps_head_bwd");
+  hipLaunchKernelGGL(colsum_kernel2, dim3((cols + 255) / 256), dim3(256), 0, st, part, F, cols, sum);
+  SRF_LAUNCH_CHECK("colsum(head)");
+  hipLaunchKernelGGL(split_copy, dim3((n + 255) / 256), dim3(256), 0, st, sum, n, g_gamma_mid, n, g_beta_mid);
+  SRF_LAUNCH_CHECK("split_copy(head mid)");
+  hipLaunchKernelGGL(split_copy, dim3((J + 255) / 256), dim3(256), 0, st, sum + 2 * n, J, g_gamma_out, J, g_beta_out);
+  SRF_LAUNCH_CHECK("split_copy(head out)");
+  return SRF_OK;
+}
+
+}  // extern "C"

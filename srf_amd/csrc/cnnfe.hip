@@ -1,0 +1,901 @@
+// CNN front end (CapsulationLayer, sequence_router.py:44-82) for gfx950.
+//
+// Two maxout stages over the NHWC fbank map (H = time, W = frequency):
+//   y_k = mask_k( max( drop(conv_ka(x)), drop(conv_kb(x)) ) )      (:76-77)
+//   x_{k+1} = mask_k( BN_k(y_k) )                                    (:78-79)
+// with 3x3 stride-2 'SAME' convolutions (TF padding: pad_before = total // 2),
+// mask_k zeroing frames t >= ceil(len / 2^(k+1)) (model_helper.py:125-140) and
+// Keras BatchNormalization (batch statistics over every position, eps 1e-3).
+//
+// Kernels:
+//   conv1_fwd    VALU direct conv (Cin = 1, K = 9) + maxout + dropout + mask,
+//                Welford per-channel partials for BN1, argmax byte per output;
+//   bn_finalize  Chan merge of the partials -> scale/shift, moving statistics;
+//   conv2_fwd    MFMA implicit GEMM (M = output pixels, N = 128 = both convs,
+//                K = 9 taps x 64 channels) whose A staging applies BN1 + mask1
+//                and whose epilogue does bias + dropout + maxout + mask2 + BN2
+//                partials;
+//   bn_apply     writes the CapsulationLayer output mask2(BN2(y2)).
+#include <algorithm>
+#include <cmath>
+
+#include "srf_common.h"
+#include "srf_rng.h"
+#include "../../include/srf.h"
+
+namespace {
+
+constexpr int C = 64;            // --model-conv-filter-num (reference default, required here)
+constexpr float kBnEps = 1e-3f;   // Keras BatchNormalization default
+constexpr float kBnMomentum = 0.99f;
+
+struct Dims {
+  int B, T, Fin;
+  int T1, F1, T2, F2;
+  int pt1, pf1, pt2, pf2;  // SAME pad_before of stage 1 / stage 2 (time, freq)
+};
+
+inline int same_out(int n) { return (n + 1) / 2; }
+inline int same_pad_before(int n) {
+  const int out = same_out(n);
+  const int total = std::max((out - 1) * 2 + 3 - n, 0);
+  return total / 2;
+}
+
+Dims make_dims(int B, int T, int Fin) {
+  Dims d;
+  d.B = B; d.T = T; d.Fin = Fin;
+  d.T1 = same_out(T); d.F1 = same_out(Fin);
+  d.T2 = same_out(d.T1); d.F2 = same_out(d.F1);
+  d.pt1 = same_pad_before(T); d.pf1 = same_pad_before(Fin);
+  d.pt2 = same_pad_before(d.T1); d.pf2 = same_pad_before(d.F1);
+  return d;
+}
+
+__device__ __forceinline__ int ceil_div_len(int len, int div) { return (len + div - 1) / div; }
+
+// Welford partial (count, mean, M2) merge (Chan et al.).
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  if (nb == 0.f) return;
+  const float nn = n + nb;
+  const float delta = meanb - mean;
+  mean += delta * (nb / nn);
+  m2 += m2b + delta * delta * (n * nb / nn);
+  n = nn;
+}
+
+// ---------------------------------------------------------------- conv1
+// One thread = one output channel c of a stream of output pixels (grid-stride).
+// Block 256 = 4 pixel rows x 64 channels.  Partials slab[block][c] = (n, mean, M2).
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(
+    const float* __restrict__ feats, const int* __restrict__ inp_len, Dims d, const float* __restrict__ ka,
+    const float* __restrict__ ba, const float* __restrict__ kb, const float* __restrict__ bb, int training,
+    float drop_p, unsigned long long seed, float* __restrict__ y1, unsigned char* __restrict__ sel1,
+    float* __restrict__ part) {
+  __shared__ float sh[3][4][C];
+  const int c = threadIdx.x & (C - 1);
+  const int row = threadIdx.x >> 6;
+  float wa[9], wb[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    wa[k] = ka[k * C + c];  // kernel [3][3][1][C]
+    wb[k] = kb[k * C + c];
+  }
+  const float bia = ba[c], bib = bb[c];
+  const float keep_scale = 1.f / (1.f - drop_p);
+  const long long P = (long long)d.B * d.T1 * d.F1;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+    const int f1 = p % d.F1;
+    const int t1 = (p / d.F1) % d.T1;
+    const int b = p / ((long long)d.F1 * d.T1);
+    float a = bia, bv = bib;
+#pragma unroll
+    for (int dt = 0; dt < 3; ++dt) {
+      const int t = 2 * t1 - d.pt1 + dt;
+#pragma unroll
+      for (int df = 0; df < 3; ++df) {
+        const int f = 2 * f1 - d.pf1 + df;
+        float x = 0.f;
+        if (t >= 0 && t < d.T && f >= 0 && f < d.Fin) x = feats[((size_t)b * d.T + t) * d.Fin + f];
+        a += x * wa[dt * 3 + df];
+        bv += x * wb[dt * 3 + df];
+      }
+    }
+    const size_t o = (size_t)p * C + c;
+    if (training && drop_p > 0.f) {
+      a *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
+      bv *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
+    }
+    const bool s = a >= bv;  // TF Maximum gradient: ties go to the first operand
+    float y = s ? a : bv;
+    if (t1 >= ceil_div_len(inp_len[b], 2)) y = 0.f;
+    y1[o] = y;
+    sel1[o] = s ? 1 : 0;
+    n += 1.f;
+    const float delta = y - mean;
+    mean += delta / n;
+    m2 += delta * (y - mean);
+  }
+  sh[0][row][c] = n; sh[1][row][c] = mean; sh[2][row][c] = m2;
+  __syncthreads();
+  if (row == 0) {
+    for (int r = 1; r < 4; ++r) chan_merge(n, mean, m2, sh[0][r][c], sh[1][r][c], sh[2][r][c]);
+    part[((size_t)blockIdx.x * 3 + 0) * C + c] = n;
+    part[((size_t)blockIdx.x * 3 + 1) * C + c] = mean;
+    part[((size_t)blockIdx.x * 3 + 2) * C + c] = m2;
+  }
+}
+
+// ---------------------------------------------------------------- BN finalize
+// stats[0][c] = mean, stats[1][c] = rstd, stats[2][c] = scale, stats[3][c] = shift.
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nparts, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float* __restrict__ mmean,
+                                   float* __restrict__ mvar, int training, float* __restrict__ stats) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    float n = 0.f, mu = 0.f, m2 = 0.f;
+    for (int k = 0; k < nparts; ++k)
+      chan_merge(n, mu, m2, part[((size_t)k * 3 + 0) * C + c], part[((size_t)k * 3 + 1) * C + c],
+                 part[((size_t)k * 3 + 2) * C + c]);
+    mean = mu;
+    var = m2 / n;
+    // moving averages; the fused NHWC kernel feeds the Bessel-corrected variance
+    mmean[c] = mmean[c] * kBnMomentum + mean * (1.f - kBnMomentum);
+    mvar[c] = mvar[c] * kBnMomentum + (n > 1.f ? var * n / (n - 1.f) : var) * (1.f - kBnMomentum);
+  } else {
+    mean = mmean[c];
+    var = mvar[c];
+  }
+  const float rstd = 1.f / sqrtf(var + kBnEps);
+  const float scale = gamma[c] * rstd;
+  stats[0 * C + c] = mean;
+  stats[1 * C + c] = rstd;
+  stats[2 * C + c] = scale;
+  stats[3 * C + c] = beta[c] - mean * scale;
+}
+
+// Pack both stage-2 kernels [3][3][C][C] (kh, kw, cin, cout) into the MFMA B
+// image wp[tap][n = ab*C + cout][cin].
+__global__ void pack_w2_kernel(const float* __restrict__ ka, const float* __restrict__ kb, float* __restrict__ wp) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 9 * 2 * C * C) return;
+  const int cin = idx % C;
+  const int n = (idx / C) % (2 * C);
+  const int tap = idx / (2 * C * C);
+  const float* k = n < C ? ka : kb;
+  wp[idx] = k[((size_t)tap * C + cin) * C + (n % C)];
+}
+
+// ---------------------------------------------------------------- conv2 (MFMA)
+// Workgroup = 4 waves = 64 output pixels x 128 outputs (conv a and b, 64 each).
+// Wave w owns output channels [16w, 16w+16) of both convs: N-tile 0 = conv a,
+// N-tile 1 = conv b, so the maxout pairs land in the same lane.
+constexpr int kLdsStride = C + 4;  // row padding against LDS bank conflicts
+
+__global__ __launch_bounds__(256) void conv2_fwd_kernel(
+    const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len, Dims d,
+    const float* __restrict__ wp, const float* __restrict__ ba, const float* __restrict__ bb, int training,
+    float drop_p, unsigned long long seed, float* __restrict__ y2, unsigned char* __restrict__ sel2,
+    float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float As[64 * kLdsStride];
+  __shared__ __attribute__((aligned(16))) float Bs[2 * C * kLdsStride];
+  __shared__ float red[3][4][4][16];   // [n|mean|M2][wave][lane group][channel]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int P2 = d.B * d.T2 * d.F2;
+  const int p0 = blockIdx.x * 64;
+
+  // per-thread staging coordinates: 4 float4 of A per thread
+  f4 acc[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int tap = 0; tap < 9; ++tap) {
+    const int dt = tap / 3, df = tap - dt * 3;
+    // stage A: BN1 + mask1 applied to the gathered input pixels (zero padding)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = q * 256 + tid;   // 1024 float4 = 64 px x 16
+      const int px = idx >> 4, c4 = (idx & 15) * 4;
+      const int p = p0 + px;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < P2) {
+        const int f2 = p % d.F2;
+        const int t2 = (p / d.F2) % d.T2;
+        const int b = p / (d.F2 * d.T2);
+        const int t1 = 2 * t2 - d.pt2 + dt;
+        const int f1 = 2 * f2 - d.pf2 + df;
+        if (t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < ceil_div_len(inp_len[b], 2)) {
+          const f4 x = *reinterpret_cast<const f4*>(y1 + (((size_t)b * d.T1 + t1) * d.F1 + f1) * C + c4);
+          const f4 sc = *reinterpret_cast<const f4*>(stats1 + 2 * C + c4);
+          const f4 sf = *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
+          v = x * sc + sf;
+        }
+      }
+      *reinterpret_cast<f4*>(&As[px * kLdsStride + c4]) = v;
+    }
+    // stage B: packed weights of this tap, [128][64] -> [128][68]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = q * 256 + tid;   // 2048 float4 = 128 rows x 16
+      const int n = idx >> 4, c4 = (idx & 15) * 4;
+      *reinterpret_cast<f4*>(&Bs[n * kLdsStride + c4]) =
+          *reinterpret_cast<const f4*>(wp + ((size_t)tap * 2 * C + n) * C + c4);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < C / 16; ++s) {
+      const int k0 = 16 * s + 4 * g;
+      const f4 b0 = *reinterpret_cast<const f4*>(&Bs[(0 * C + 16 * wv + l16) * kLdsStride + k0]);
+      const f4 b1 = *reinterpret_cast<const f4*>(&Bs[(1 * C + 16 * wv + l16) * kLdsStride + k0]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f4 a = *reinterpret_cast<const f4*>(&As[(mt * 16 + l16) * kLdsStride + k0]);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          acc[mt][0] = mfma16x16x4(a[kk], b0[kk], acc[mt][0]);
+          acc[mt][1] = mfma16x16x4(a[kk], b1[kk], acc[mt][1]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane (c = 16*wv + l16, g) holds pixels mt*16 + 4g + k
+  const int c = 16 * wv + l16;
+  const float bia = ba[c], bib = bb[c];
+  const float keep_scale = 1.f / (1.f - drop_p);
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = p0 + mt * 16 + 4 * g + k;
+      if (p >= P2) continue;
+      const size_t o = (size_t)p * C + c;
+      float a = acc[mt][0][k] + bia, bv = acc[mt][1][k] + bib;
+      if (training && drop_p > 0.f) {
+        a *= srf_keep(seed, kStreamConv1a, o, drop_p) ? keep_scale : 0.f;
+        bv *= srf_keep(seed, kStreamConv1b, o, drop_p) ? keep_scale : 0.f;
+      }
+      const bool s = a >= bv;
+      float y = s ? a : bv;
+      const int t2 = (p / d.F2) % d.T2;
+      const int b = p / (d.F2 * d.T2);
+      if (t2 >= ceil_div_len(inp_len[b], 4)) y = 0.f;
+      y2[o] = y;
+      sel2[o] = s ? 1 : 0;
+      n += 1.f;
+      const float delta = y - mean;
+      mean += delta / n;
+      m2 += delta * (y - mean);
+    }
+  }
+  red[0][wv][g][l16] = n; red[1][wv][g][l16] = mean; red[2][wv][g][l16] = m2;
+  // combine the 4 lane groups of this wave (same channel) through LDS
+  __syncthreads();
+  if (g == 0) {
+    for (int r = 1; r < 4; ++r)
+      chan_merge(n, mean, m2, red[0][wv][r][l16], red[1][wv][r][l16], red[2][wv][r][l16]);
+    part[((size_t)blockIdx.x * 3 + 0) * C + c] = n;
+    part[((size_t)blockIdx.x * 3 + 1) * C + c] = mean;
+    part[((size_t)blockIdx.x * 3 + 2) * C + c] = m2;
+  }
+}
+
+// out = mask2(BN2(y2)), the CapsulationLayer output.
+__global__ void bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ stats,
+                                const int* __restrict__ inp_len, int B, int Tk, int Fk, int div,
+                                float* __restrict__ out) {
+  const size_t n4 = (size_t)B * Tk * Fk * C / 4;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = (q * 4) % C;
+    const size_t p = q * 4 / C;
+    const int t = (p / Fk) % Tk;
+    const int b = p / ((size_t)Fk * Tk);
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (t < ceil_div_len(inp_len[b], div)) {
+      const f4 x = reinterpret_cast<const f4*>(y)[q];
+      v = x * *reinterpret_cast<const f4*>(stats + 2 * C + c4) + *reinterpret_cast<const f4*>(stats + 3 * C + c4);
+    }
+    reinterpret_cast<f4*>(out)[q] = v;
+  }
+}
+
+// ================================================================ backward
+// Gradient of the CapsulationLayer output g_out (of mask2(BN2(y2))).
+//
+// BN backward (training statistics): with dy = mask * g and xh = (y - mean) * rstd,
+//   g_y = mask_pre * gamma * rstd * (dy - sum(dy)/N - xh * sum(dy*xh)/N)
+// (mask_pre = the mask applied before BN; it equals the post-BN mask here).
+
+// Per-channel partial sums (sum dy, sum dy*xh) over a stream of positions.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                            const float* __restrict__ stats,
+                                                            const int* __restrict__ inp_len, int B, int Tk, int Fk,
+                                                            int div, float* __restrict__ part) {
+  __shared__ float sh[2][4][C];
+  const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
+  const float mean = stats[c], rstd = stats[C + c];
+  const long long P = (long long)B * Tk * Fk;
+  float s0 = 0.f, s1 = 0.f;
+  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+    const int t = (p / Fk) % Tk;
+    const int b = p / ((long long)Fk * Tk);
+    if (t >= ceil_div_len(inp_len[b], div)) continue;
+    const size_t o = (size_t)p * C + c;
+    const float dy = g[o];
+    s0 += dy;
+    s1 += dy * (y[o] - mean) * rstd;
+  }
+  sh[0][row][c] = s0; sh[1][row][c] = s1;
+  __syncthreads();
+  if (row == 0) {
+    for (int r = 1; r < 4; ++r) { s0 += sh[0][r][c]; s1 += sh[1][r][c]; }
+    part[((size_t)blockIdx.x * 2 + 0) * C + c] = s0;
+    part[((size_t)blockIdx.x * 2 + 1) * C + c] = s1;
+  }
+}
+
+// Column sums of a [rows][cols] slab: out[c] = sum_r in[r][c] (optionally into
+// two outputs split at `split`).
+__global__ void colsum_kernel(const float* __restrict__ in, int rows, int cols, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += in[(size_t)r * cols + c];
+  out[c] = s;
+}
+
+__device__ __forceinline__ float bn_bwd_elem(float gin, float y, float mask, float mean, float rstd, float gamma,
+                                             float sdy_n, float sdyxh_n) {
+  const float dy = mask * gin;
+  const float xh = (y - mean) * rstd;
+  return mask * gamma * rstd * (dy - sdy_n - xh * sdyxh_n);
+}
+
+// BN2 backward + maxout/dropout backward: g_ab[p][n] (n < C: conv a, else conv b);
+// bias-gradient partials per block.
+__global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
+    const float* __restrict__ g_out, const float* __restrict__ y2, const unsigned char* __restrict__ sel2,
+    const float* __restrict__ stats2, const float* __restrict__ gamma2, const float* __restrict__ bnsum2,
+    const int* __restrict__ inp_len, Dims d, float drop_p, unsigned long long seed, float* __restrict__ g_ab,
+    float* __restrict__ part) {
+  __shared__ float sh[2][4][C];
+  const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
+  const long long P = (long long)d.B * d.T2 * d.F2;
+  const float mean = stats2[c], rstd = stats2[C + c], gam = gamma2[c];
+  const float sdy_n = bnsum2[c] / (float)P, sdyxh_n = bnsum2[C + c] / (float)P;
+  const float keep_scale = 1.f / (1.f - drop_p);
+  float ga_s = 0.f, gb_s = 0.f;
+  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+    const int t = (p / d.F2) % d.T2;
+    const int b = p / ((long long)d.F2 * d.T2);
+    const float mask = t < ceil_div_len(inp_len[b], 4) ? 1.f : 0.f;
+    const size_t o = (size_t)p * C + c;
+    const float gy = bn_bwd_elem(g_out[o], y2[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
+    const bool s = sel2[o] != 0;
+    float ga = s ? gy : 0.f, gb = s ? 0.f : gy;
+    if (drop_p > 0.f) {
+      ga *= srf_keep(seed, kStreamConv1a, o, drop_p) ? keep_scale : 0.f;
+      gb *= srf_keep(seed, kStreamConv1b, o, drop_p) ? keep_scale : 0.f;
+    }
+    g_ab[(size_t)p * 2 * C + c] = ga;
+    g_ab[(size_t)p * 2 * C + C + c] = gb;
+    ga_s += ga;
+    gb_s += gb;
+  }
+  sh[0][row][c] = ga_s; sh[1][row][c] = gb_s;
+  __syncthreads();
+  if (row == 0) {
+    for (int r = 1; r < 4; ++r) { ga_s += sh[0][r][c]; gb_s += sh[1][r][c]; }
+    part[(size_t)blockIdx.x * 2 * C + c] = ga_s;
+    part[(size_t)blockIdx.x * 2 * C + C + c] = gb_s;
+  }
+}
+
+// Transposed weight image for the data gradient: wq[tap][cin][n].
+__global__ void pack_w2t_kernel(const float* __restrict__ ka, const float* __restrict__ kb, float* __restrict__ wq) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 9 * 2 * C * C) return;
+  const int n = idx % (2 * C);
+  const int cin = (idx / (2 * C)) % C;
+  const int tap = idx / (2 * C * C);
+  const float* k = n < C ? ka : kb;
+  wq[idx] = k[((size_t)tap * C + cin) * C + (n % C)];
+}
+
+constexpr int kNStride = 2 * C + 4;
+
+// Data gradient of stage 2 for the input pixels of one stride-parity class
+// (t1 % 2 == qt, f1 % 2 == qf): only taps with the matching parity reach such a
+// pixel, so the implicit GEMM (M = 64 pixels, N = 64 cin, K = taps x 128) runs
+// without zero taps.  g_x1[p1][cin] = sum_tap sum_n g_ab[o(p1,tap)][n] wq[tap][cin][n].
+__global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restrict__ g_ab,
+                                                          const float* __restrict__ wq, Dims d, int qt, int qf,
+                                                          float* __restrict__ g_x1) {
+  __shared__ __attribute__((aligned(16))) float As[64 * kNStride];
+  __shared__ __attribute__((aligned(16))) float Bs[C * kNStride];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int nkt = (d.T1 - qt + 1) / 2, nkf = (d.F1 - qf + 1) / 2;
+  const int Pc = d.B * nkt * nkf;
+  const int q0 = blockIdx.x * 64;
+  const int dt0 = (qt + d.pt2) & 1, df0 = (qf + d.pf2) & 1;
+  f4 acc[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int dt = dt0; dt < 3; dt += 2) {
+    for (int df = df0; df < 3; df += 2) {
+      const int tap = dt * 3 + df;
+      // stage A: g_ab at the output pixel this tap maps each input pixel to
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int idx = q * 256 + tid;   // 2048 float4 = 64 px x 32
+        const int px = idx >> 5, n4 = (idx & 31) * 4;
+        const int pc = q0 + px;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (pc < Pc) {
+          const int kf = pc % nkf, kt = (pc / nkf) % nkt, b = pc / (nkf * nkt);
+          const int t2 = (qt + 2 * kt + d.pt2 - dt) / 2, f2 = (qf + 2 * kf + d.pf2 - df) / 2;
+          if (t2 >= 0 && t2 < d.T2 && f2 >= 0 && f2 < d.F2)
+            v = *reinterpret_cast<const f4*>(g_ab + (((size_t)b * d.T2 + t2) * d.F2 + f2) * 2 * C + n4);
+        }
+        *reinterpret_cast<f4*>(&As[px * kNStride + n4]) = v;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int idx = q * 256 + tid;   // 2048 float4 = 64 cin x 32
+        const int ci = idx >> 5, n4 = (idx & 31) * 4;
+        *reinterpret_cast<f4*>(&Bs[ci * kNStride + n4]) =
+            *reinterpret_cast<const f4*>(wq + ((size_t)tap * C + ci) * 2 * C + n4);
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int s = 0; s < 2 * C / 16; ++s) {
+        const int k0 = 16 * s + 4 * g;
+        const f4 bw = *reinterpret_cast<const f4*>(&Bs[(16 * wv + l16) * kNStride + k0]);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const f4 a = *reinterpret_cast<const f4*>(&As[(mt * 16 + l16) * kNStride + k0]);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) acc[mt] = mfma16x16x4(a[kk], bw[kk], acc[mt]);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int ci = 16 * wv + l16;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pc = q0 + mt * 16 + 4 * g + k;
+      if (pc >= Pc) continue;
+      const int kf = pc % nkf, kt = (pc / nkf) % nkt, b = pc / (nkf * nkt);
+      const int t1 = qt + 2 * kt, f1 = qf + 2 * kf;
+      g_x1[(((size_t)b * d.T1 + t1) * d.F1 + f1) * C + ci] = acc[mt][k];
+    }
+  }
+}
+
+// Weight gradient of stage 2 for one tap and one pixel split:
+// part[s][tap][cin][n] = sum_{p in split} xbn1(p, tap)[cin] * g_ab[p][n].
+constexpr int kPxChunk = 32;
+constexpr int kPxStride = kPxChunk + 4;
+
+__global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restrict__ y1,
+                                                          const float* __restrict__ stats1,
+                                                          const int* __restrict__ inp_len,
+                                                          const float* __restrict__ g_ab, Dims d, int nsplit,
+                                                          int split_len, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float As[C * kPxStride];
+  __shared__ __attribute__((aligned(16))) float Bs[2 * C * kPxStride];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int tap = blockIdx.x / nsplit, sp = blockIdx.x - tap * nsplit;
+  const int dt = tap / 3, df = tap - dt * 3;
+  const int P2 = d.B * d.T2 * d.F2;
+  const int pbeg = sp * split_len, pend = min(P2, pbeg + split_len);
+  f4 acc[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int pc0 = pbeg; pc0 < pend; pc0 += kPxChunk) {
+    // A^T: xbn1 gathered for 32 output pixels x 64 cin, stored [cin][px]
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = q * 256 + tid;   // 512 float4 = 32 px x 16
+      const int px = idx >> 4, c4 = (idx & 15) * 4;
+      const int p = pc0 + px;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < pend) {
+        const int f2 = p % d.F2, t2 = (p / d.F2) % d.T2, b = p / (d.F2 * d.T2);
+        const int t1 = 2 * t2 - d.pt2 + dt, f1 = 2 * f2 - d.pf2 + df;
+        if (t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < ceil_div_len(inp_len[b], 2)) {
+          const f4 x = *reinterpret_cast<const f4*>(y1 + (((size_t)b * d.T1 + t1) * d.F1 + f1) * C + c4);
+          v = x * *reinterpret_cast<const f4*>(stats1 + 2 * C + c4) +
+              *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) As[(c4 + j) * kPxStride + px] = v[j];
+    }
+    // B^T: g_ab for 32 pixels x 128 outputs, stored [n][px]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = q * 256 + tid;   // 1024 float4 = 32 px x 32
+      const int px = idx >> 5, n4 = (idx & 31) * 4;
+      const int p = pc0 + px;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < pend) v = *reinterpret_cast<const f4*>(g_ab + (size_t)p * 2 * C + n4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Bs[(n4 + j) * kPxStride + px] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kPxChunk / 16; ++s) {
+      const int k0 = 16 * s + 4 * g;
+      const f4 b0 = *reinterpret_cast<const f4*>(&Bs[(32 * wv + l16) * kPxStride + k0]);
+      const f4 b1 = *reinterpret_cast<const f4*>(&Bs[(32 * wv + 16 + l16) * kPxStride + k0]);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f4 a = *reinterpret_cast<const f4*>(&As[(mt * 16 + l16) * kPxStride + k0]);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          acc[mt][0] = mfma16x16x4(a[kk], b0[kk], acc[mt][0]);
+          acc[mt][1] = mfma16x16x4(a[kk], b1[kk], acc[mt][1]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // C layout: col = n (l16 within the N-tile), rows = cin mt*16 + 4g + k
+  float* dst = part + ((size_t)sp * 9 + tap) * C * 2 * C;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        dst[(size_t)(mt * 16 + 4 * g + k) * 2 * C + 32 * wv + 16 * nt + l16] = acc[mt][nt][k];
+}
+
+// Sum the wgrad splits and unpack n -> (conv a|b, cout): gka/gkb [tap][cin][cout].
+__global__ void conv2_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit, float* __restrict__ gka,
+                                          float* __restrict__ gkb) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 9 * C * 2 * C) return;
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) s += part[(size_t)k * 9 * C * 2 * C + idx];
+  const int n = idx % (2 * C);
+  const int tc = idx / (2 * C);   // tap*C + cin
+  if (n < C)
+    gka[(size_t)tc * C + n] = s;
+  else
+    gkb[(size_t)tc * C + n - C] = s;
+}
+
+// BN1 backward + maxout/dropout backward + stage-1 weight/bias gradient partials.
+// part[block][j][c], j = 0..8 conv a taps, 9..17 conv b taps, 18 bias a, 19 bias b.
+__global__ __launch_bounds__(256) void conv1_bwd_kernel(
+    const float* __restrict__ feats, const int* __restrict__ inp_len, Dims d, const float* __restrict__ g_x1,
+    const float* __restrict__ y1, const unsigned char* __restrict__ sel1, const float* __restrict__ stats1,
+    const float* __restrict__ gamma1, const float* __restrict__ bnsum1, float drop_p, unsigned long long seed,
+    float* __restrict__ part) {
+  __shared__ float sh[4][20][C];
+  const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
+  const long long P = (long long)d.B * d.T1 * d.F1;
+  const float mean = stats1[c], rstd = stats1[C + c], gam = gamma1[c];
+  const float sdy_n = bnsum1[c] / (float)P, sdyxh_n = bnsum1[C + c] / (float)P;
+  const float keep_scale = 1.f / (1.f - drop_p);
+  float acc[20];
+#pragma unroll
+  for (int j = 0; j < 20; ++j) acc[j] = 0.f;
+  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+    const int f1 = p % d.F1;
+    const int t1 = (p / d.F1) % d.T1;
+    const int b = p / ((long long)d.F1 * d.T1);
+    const float mask = t1 < ceil_div_len(inp_len[b], 2) ? 1.f : 0.f;
+    const size_t o = (size_t)p * C + c;
+    const float gy = bn_bwd_elem(g_x1[o], y1[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
+    const bool s = sel1[o] != 0;
+    float ga = s ? gy : 0.f, gb = s ? 0.f : gy;
+    if (drop_p > 0.f) {
+      ga *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
+      gb *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
+    }
+    acc[18] += ga;
+    acc[19] += gb;
+#pragma unroll
+    for (int dt = 0; dt < 3; ++dt) {
+      const int t = 2 * t1 - d.pt1 + dt;
+#pragma unroll
+      for (int df = 0; df < 3; ++df) {
+        const int f = 2 * f1 - d.pf1 + df;
+        float x = 0.f;
+        if (t >= 0 && t < d.T && f >= 0 && f < d.Fin) x = feats[((size_t)b * d.T + t) * d.Fin + f];
+        acc[dt * 3 + df] += x * ga;
+        acc[9 + dt * 3 + df] += x * gb;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 20; ++j) sh[row][j][c] = acc[j];
+  __syncthreads();
+  for (int j = row; j < 20; j += 4) {
+    const float v = sh[0][j][c] + sh[1][j][c] + sh[2][j][c] + sh[3][j][c];
+    part[((size_t)blockIdx.x * 20 + j) * C + c] = v;
+  }
+}
+
+// ---------------------------------------------------------------- host
+constexpr int kConv1Blocks = 1024;
+
+struct FwdSaved {
+  float *y1, *y2, *stats1, *stats2;
+  unsigned char *sel1, *sel2;
+  size_t bytes;
+};
+
+FwdSaved saved_layout(const Dims& d, void* base) {
+  const size_t P1 = (size_t)d.B * d.T1 * d.F1, P2 = (size_t)d.B * d.T2 * d.F2;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += srf::align_up(bytes, 256);
+    return o;
+  };
+  const size_t oy1 = take(P1 * C * 4), oy2 = take(P2 * C * 4), os1 = take(4 * C * 4), os2 = take(4 * C * 4),
+               osel1 = take(P1 * C), osel2 = take(P2 * C);
+  char* b = static_cast<char*>(base);
+  FwdSaved s;
+  s.y1 = (float*)(b + oy1);
+  s.y2 = (float*)(b + oy2);
+  s.stats1 = (float*)(b + os1);
+  s.stats2 = (float*)(b + os2);
+  s.sel1 = (unsigned char*)(b + osel1);
+  s.sel2 = (unsigned char*)(b + osel2);
+  s.bytes = off;
+  return s;
+}
+
+struct FwdWs {
+  float *part1, *part2, *wp;
+  size_t bytes;
+};
+
+FwdWs fwd_ws_layout(const Dims& d, void* base) {
+  const size_t P2 = (size_t)d.B * d.T2 * d.F2;
+  const size_t nb2 = (P2 + 63) / 64;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += srf::align_up(bytes, 256);
+    return o;
+  };
+  const size_t op1 = take((size_t)kConv1Blocks * 3 * C * 4), op2 = take(nb2 * 3 * C * 4),
+               owp = take((size_t)9 * 2 * C * C * 4);
+  char* b = static_cast<char*>(base);
+  FwdWs w;
+  w.part1 = (float*)(b + op1);
+  w.part2 = (float*)(b + op2);
+  w.wp = (float*)(b + owp);
+  w.bytes = off;
+  return w;
+}
+
+int check_dims(int B, int T, int Fin, int nfilt) {
+  SRF_REQUIRE(B > 0 && T > 0 && Fin > 0, "bad CNN-FE shape B=%d T=%d F=%d", B, T, Fin);
+  SRF_REQUIRE(nfilt == C, "model-conv-filter-num must be %d (got %d)", C, nfilt);
+  return SRF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srf_cnnfe_out_dims(int T, int feat_dim, int* T2, int* F2) {
+  SRF_REQUIRE(T > 0 && feat_dim > 0 && T2 && F2, "bad arguments");
+  Dims d = make_dims(1, T, feat_dim);
+  *T2 = d.T2;
+  *F2 = d.F2;
+  return SRF_OK;
+}
+
+size_t srf_cnnfe_saved_bytes(int B, int T, int feat_dim, int nfilt) {
+  (void)nfilt;
+  return saved_layout(make_dims(B, T, feat_dim), nullptr).bytes;
+}
+
+size_t srf_cnnfe_fwd_workspace(int B, int T, int feat_dim, int nfilt) {
+  (void)nfilt;
+  return fwd_ws_layout(make_dims(B, T, feat_dim), nullptr).bytes;
+}
+
+int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat_dim, int nfilt,
+                  const float* k0a, const float* b0a, const float* k0b, const float* b0b, const float* gamma0,
+                  const float* beta0, const float* k1a, const float* b1a, const float* k1b, const float* b1b,
+                  const float* gamma1, const float* beta1, float* mmean0, float* mvar0, float* mmean1, float* mvar1,
+                  int training, float drop_p, unsigned long long seed, float* out, void* saved, size_t saved_bytes,
+                  void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_dims(B, T, feat_dim, nfilt);
+  if (rc) return rc;
+  SRF_REQUIRE(feats && inp_len && k0a && b0a && k0b && b0b && gamma0 && beta0 && k1a && b1a && k1b && b1b &&
+                  gamma1 && beta1 && mmean0 && mvar0 && mmean1 && mvar1 && out && saved && workspace,
+              "null pointer argument");
+  SRF_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "dropout rate %f out of [0,1)", drop_p);
+  const Dims d = make_dims(B, T, feat_dim);
+  FwdSaved sv = saved_layout(d, saved);
+  FwdWs w = fwd_ws_layout(d, workspace);
+  if (saved_bytes < sv.bytes || workspace_bytes < w.bytes) {
+    srf::set_error("CNN-FE buffers too small (saved %zu < %zu or workspace %zu < %zu)", saved_bytes, sv.bytes,
+                   workspace_bytes, w.bytes);
+    return SRF_EWORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t P2 = (size_t)d.B * d.T2 * d.F2;
+  const int nb2 = (int)((P2 + 63) / 64);
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(kConv1Blocks), dim3(256), 0, st, feats, inp_len, d, k0a, b0a, k0b, b0b,
+                     training, drop_p, seed, sv.y1, sv.sel1, w.part1);
+  SRF_LAUNCH_CHECK("conv1_fwd");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(C), 0, st, w.part1, kConv1Blocks, gamma0, beta0, mmean0,
+                     mvar0, training, sv.stats1);
+  SRF_LAUNCH_CHECK("bn_finalize(1)");
+  hipLaunchKernelGGL(pack_w2_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wp);
+  SRF_LAUNCH_CHECK("pack_w2");
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(nb2), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, d, w.wp, b1a, b1b,
+                     training, drop_p, seed, sv.y2, sv.sel2, w.part2);
+  SRF_LAUNCH_CHECK("conv2_fwd");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(C), 0, st, w.part2, nb2, gamma1, beta1, mmean1, mvar1,
+                     training, sv.stats2);
+  SRF_LAUNCH_CHECK("bn_finalize(2)");
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(1024), dim3(256), 0, st, sv.y2, sv.stats2, inp_len, d.B, d.T2, d.F2, 4,
+                     out);
+  SRF_LAUNCH_CHECK("bn_apply");
+  return SRF_OK;
+}
+
+}  // extern "C"
+
+namespace {
+struct BwdWs2 {
+  float *bnpart, *bnsum2, *bnsum1, *g_ab, *biaspart, *g_x1, *wq, *wpart, *c1part, *c1sum;
+  size_t bytes;
+};
+
+constexpr int kBnBlocks = 512;
+constexpr int kWgradSplits = 32;
+
+BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
+  const size_t P1 = (size_t)d.B * d.T1 * d.F1, P2 = (size_t)d.B * d.T2 * d.F2;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += srf::align_up(bytes, 256);
+    return o;
+  };
+  const size_t obp = take((size_t)kBnBlocks * 2 * C * 4), os2 = take(2 * C * 4), os1 = take(2 * C * 4),
+               oab = take(P2 * 2 * C * 4), obias = take((size_t)kBnBlocks * 2 * C * 4), ogx = take(P1 * C * 4),
+               owq = take((size_t)9 * 2 * C * C * 4), owp = take((size_t)kWgradSplits * 9 * C * 2 * C * 4),
+               oc1 = take((size_t)kConv1Blocks * 20 * C * 4), oc1s = take(20 * C * 4);
+  char* b = static_cast<char*>(base);
+  BwdWs2 w;
+  w.bnpart = (float*)(b + obp);
+  w.bnsum2 = (float*)(b + os2);
+  w.bnsum1 = (float*)(b + os1);
+  w.g_ab = (float*)(b + oab);
+  w.biaspart = (float*)(b + obias);
+  w.g_x1 = (float*)(b + ogx);
+  w.wq = (float*)(b + owq);
+  w.wpart = (float*)(b + owp);
+  w.c1part = (float*)(b + oc1);
+  w.c1sum = (float*)(b + oc1s);
+  w.bytes = off;
+  return w;
+}
+
+// Scatter the 20 x C stage-1 sums into the kernel/bias gradients.
+__global__ void conv1_grad_unpack_kernel(const float* __restrict__ sums, float* __restrict__ gka,
+                                         float* __restrict__ gkb, float* __restrict__ gba, float* __restrict__ gbb) {
+  const int idx = threadIdx.x + blockIdx.x * blockDim.x;
+  if (idx >= 20 * C) return;
+  const int j = idx / C, c = idx % C;
+  const float v = sums[idx];
+  if (j < 9)
+    gka[j * C + c] = v;
+  else if (j < 18)
+    gkb[(j - 9) * C + c] = v;
+  else if (j == 18)
+    gba[c] = v;
+  else
+    gbb[c] = v;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t srf_cnnfe_bwd_workspace(int B, int T, int feat_dim, int nfilt) {
+  (void)nfilt;
+  return bwd_ws_layout(make_dims(B, T, feat_dim), nullptr).bytes;
+}
+
+int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat_dim, int nfilt, const float* gamma0,
+                  const float* k1a, const float* k1b, const float* gamma1, float drop_p, unsigned long long seed,
+                  const void* saved, const float* g_out, float* g_k0a, float* g_b0a, float* g_k0b, float* g_b0b,
+                  float* g_gamma0, float* g_beta0, float* g_k1a, float* g_b1a, float* g_k1b, float* g_b1b,
+                  float* g_gamma1, float* g_beta1, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_dims(B, T, feat_dim, nfilt);
+  if (rc) return rc;
+  SRF_REQUIRE(feats && inp_len && gamma0 && k1a && k1b && gamma1 && saved && g_out && g_k0a && g_b0a && g_k0b &&
+                  g_b0b && g_gamma0 && g_beta0 && g_k1a && g_b1a && g_k1b && g_b1b && g_gamma1 && g_beta1 &&
+                  workspace,
+              "null pointer argument");
+  const Dims d = make_dims(B, T, feat_dim);
+  FwdSaved sv = saved_layout(d, const_cast<void*>(saved));
+  BwdWs2 w = bwd_ws_layout(d, workspace);
+  if (workspace_bytes < w.bytes) {
+    srf::set_error("CNN-FE backward workspace too small: %zu < %zu", workspace_bytes, w.bytes);
+    return SRF_EWORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int P2 = d.B * d.T2 * d.F2;
+  // BN2: sums -> d(beta2) = sum dy, d(gamma2) = sum dy*xh
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.stats2, inp_len, d.B,
+                     d.T2, d.F2, 4, w.bnpart);
+  SRF_LAUNCH_CHECK("bn_bwd_reduce(2)");
+  hipLaunchKernelGGL(colsum_kernel, dim3(1), dim3(2 * C), 0, st, w.bnpart, kBnBlocks, 2 * C, w.bnsum2);
+  SRF_LAUNCH_CHECK("colsum(bn2)");
+  SRF_HIP_TRY(hipMemcpyAsync(g_beta1, w.bnsum2, C * 4, hipMemcpyDeviceToDevice, st));
+  SRF_HIP_TRY(hipMemcpyAsync(g_gamma1, w.bnsum2 + C, C * 4, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.sel2, sv.stats2,
+                     gamma1, w.bnsum2, inp_len, d, drop_p, seed, w.g_ab, w.biaspart);
+  SRF_LAUNCH_CHECK("conv2_bwd_prep");
+  hipLaunchKernelGGL(colsum_kernel, dim3(1), dim3(2 * C), 0, st, w.biaspart, kBnBlocks, 2 * C, w.bnpart);
+  SRF_LAUNCH_CHECK("colsum(bias2)");
+  SRF_HIP_TRY(hipMemcpyAsync(g_b1a, w.bnpart, C * 4, hipMemcpyDeviceToDevice, st));
+  SRF_HIP_TRY(hipMemcpyAsync(g_b1b, w.bnpart + C, C * 4, hipMemcpyDeviceToDevice, st));
+  // stage-2 data gradient (4 stride-parity classes) and weight gradient
+  hipLaunchKernelGGL(pack_w2t_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wq);
+  SRF_LAUNCH_CHECK("pack_w2t");
+  for (int qt = 0; qt < 2; ++qt) {
+    for (int qf = 0; qf < 2; ++qf) {
+      const int Pc = d.B * ((d.T1 - qt + 1) / 2) * ((d.F1 - qf + 1) / 2);
+      if (Pc <= 0) continue;
+      hipLaunchKernelGGL(conv2_dgrad_kernel, dim3((Pc + 63) / 64), dim3(256), 0, st, w.g_ab, w.wq, d, qt, qf,
+                         w.g_x1);
+      SRF_LAUNCH_CHECK("conv2_dgrad");
+    }
+  }
+  const int split_len = ((P2 + kWgradSplits - 1) / kWgradSplits + kPxChunk - 1) / kPxChunk * kPxChunk;
+  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(9 * kWgradSplits), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, w.g_ab,
+                     d, kWgradSplits, split_len, w.wpart);
+  SRF_LAUNCH_CHECK("conv2_wgrad");
+  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((9 * C * 2 * C + 255) / 256), dim3(256), 0, st, w.wpart,
+                     kWgradSplits, g_k1a, g_k1b);
+  SRF_LAUNCH_CHECK("conv2_wgrad_reduce");
+  // BN1 backward sums, then stage-1 gradients
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, w.g_x1, sv.y1, sv.stats1, inp_len, d.B,
+                     d.T1, d.F1, 2, w.bnpart);
+  SRF_LAUNCH_CHECK("bn_bwd_reduce(1)");
+  hipLaunchKernelGGL(colsum_kernel, dim3(1), dim3(2 * C), 0, st, w.bnpart, kBnBlocks, 2 * C, w.bnsum1);
+  SRF_LAUNCH_CHECK("colsum(bn1)");
+  SRF_HIP_TRY(hipMemcpyAsync(g_beta0, w.bnsum1, C * 4, hipMemcpyDeviceToDevice, st));
+  SRF_HIP_TRY(hipMemcpyAsync(g_gamma0, w.bnsum1 + C, C * 4, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(conv1_bwd_kernel, dim3(kConv1Blocks), dim3(256), 0, st, feats, inp_len, d, w.g_x1, sv.y1,
+                     sv.sel1, sv.stats1, gamma0, w.bnsum1, drop_p, seed, w.c1part);
+  SRF_LAUNCH_CHECK("conv1_bwd");
+  hipLaunchKernelGGL(colsum_kernel, dim3((20 * C + 255) / 256), dim3(256), 0, st, w.c1part, kConv1Blocks, 20 * C,
+                     w.c1sum);
+  SRF_LAUNCH_CHECK("colsum(conv1)");
+  hipLaunchKernelGGL(conv1_grad_unpack_kernel, dim3((20 * C + 255) / 256), dim3(256), 0, st, w.c1sum, g_k0a, g_k0b,
+                     g_b0a, g_b0b);
+  SRF_LAUNCH_CHECK("conv1_grad_unpack");
+  return SRF_OK;
+}
+
+}  // extern "C"

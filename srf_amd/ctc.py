@@ -3,18 +3,17 @@
 ``ctc_loss`` keeps tf.nn.ctc_loss's calling convention as the reference uses it
 (dense labels, batch-major logits, explicit blank index) and returns the
 per-utterance negative log likelihood.  This revision computes it with
-torch's device CTC (a HIP CTC kernel is the next row in DESIGN.md).
+the HIP kernel srf_ctc_loss (loss and logit gradient in one launch).
 """
 import torch
-import torch.nn.functional as F
+
+from . import ops
 
 
 def ctc_loss(labels, logits, label_length, logit_length, logits_time_major=False, blank_index=0):
     if logits_time_major:
         logits = logits.transpose(0, 1)
-    log_probs = torch.log_softmax(logits, dim=-1).transpose(0, 1)   # [T, B, C]
-    return F.ctc_loss(log_probs, labels.long(), logit_length.long(), label_length.long(), blank=blank_index,
-                      reduction='none', zero_infinity=False)
+    return ops.ctc_loss(logits.contiguous(), labels, label_length, logit_length, blank_index)
 
 
 def greedy_decode(logits, lengths, blank_index):

@@ -101,3 +101,212 @@ class DynamicRouting(torch.autograd.Function):
 
 def dynamic_routing(emb, W, bias, geom):
     return DynamicRouting.apply(emb, W, bias, geom)
+
+
+# ---------------------------------------------------------------------------
+# CNN front end (CapsulationLayer)
+CNNFE_PARAMS = ('conv0a_kernel', 'conv0a_bias', 'conv0b_kernel', 'conv0b_bias', 'bn0_gamma', 'bn0_beta',
+                'conv1a_kernel', 'conv1a_bias', 'conv1b_kernel', 'conv1b_bias', 'bn1_gamma', 'bn1_beta')
+
+
+def cnnfe_out_dims(T, feat_dim):
+    import ctypes
+    t2, f2 = ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.lib().srf_cnnfe_out_dims(T, feat_dim, ctypes.byref(t2), ctypes.byref(f2)), 'srf_cnnfe_out_dims')
+    return t2.value, f2.value
+
+
+class CnnFe(torch.autograd.Function):
+    """feats [B,T,F] -> mask2(BN2(maxout2(mask1(BN1(maxout1(feats)))))) [B,T2,F2,64]."""
+
+    @staticmethod
+    def forward(ctx, feats, inp_len_i32, moving, training, drop_p, seed, *params):
+        B, T, Fd = feats.shape
+        _check_dev('feats', feats, (B, T, Fd))
+        L = _lib.lib()
+        T2, F2 = cnnfe_out_dims(T, Fd)
+        dev = feats.device
+        out = torch.empty((B, T2, F2, 64), device=dev, dtype=torch.float32)
+        sb = L.srf_cnnfe_saved_bytes(B, T, Fd, 64)
+        saved = torch.empty(sb, device=dev, dtype=torch.uint8)
+        wb = L.srf_cnnfe_fwd_workspace(B, T, Fd, 64)
+        ws = torch.empty(wb, device=dev, dtype=torch.uint8)
+        rc = L.srf_cnnfe_fwd(_ptr(feats), _ptr(inp_len_i32), B, T, Fd, 64, *[_ptr(p) for p in params],
+                             *[_ptr(m) for m in moving], int(bool(training)), float(drop_p), int(seed), _ptr(out),
+                             _ptr(saved), sb, _ptr(ws), wb, _stream())
+        _lib.check(rc, 'srf_cnnfe_fwd')
+        ctx.meta = (B, T, Fd, float(drop_p) if training else 0.0, int(seed))
+        ctx.save_for_backward(feats, inp_len_i32, saved, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        feats, inp_len, saved, *params = ctx.saved_tensors
+        B, T, Fd, drop_p, seed = ctx.meta
+        P = dict(zip(CNNFE_PARAMS, params))
+        grads = [torch.empty_like(p) for p in params]
+        G = dict(zip(CNNFE_PARAMS, grads))
+        L = _lib.lib()
+        wb = L.srf_cnnfe_bwd_workspace(B, T, Fd, 64)
+        ws = torch.empty(wb, device=feats.device, dtype=torch.uint8)
+        g_out = g_out.contiguous()
+        rc = L.srf_cnnfe_bwd(_ptr(feats), _ptr(inp_len), B, T, Fd, 64, _ptr(P['bn0_gamma']), _ptr(P['conv1a_kernel']),
+                             _ptr(P['conv1b_kernel']), _ptr(P['bn1_gamma']), drop_p, seed, _ptr(saved), _ptr(g_out),
+                             *[_ptr(G[k]) for k in CNNFE_PARAMS], _ptr(ws), wb, _stream())
+        _lib.check(rc, 'srf_cnnfe_bwd')
+        return (None, None, None, None, None, None, *grads)
+
+
+def cnnfe(feats, inp_len_i32, params, moving, training, drop_p, seed):
+    """params: the 12 tensors of CNNFE_PARAMS in order; moving: (mm0, mv0, mm1, mv1)."""
+    return CnnFe.apply(feats, inp_len_i32, moving, training, drop_p, seed, *params)
+
+
+# ---------------------------------------------------------------------------
+# Primary capsules
+CAPS_PARAMS = ('proj_kernel', 'proj_bias', 'encaps1_kernel', 'encaps1_bias', 'encaps2_kernel', 'encaps2_bias',
+               'ln_input_gamma', 'ln_input_beta')
+
+
+class PrimaryCaps(torch.autograd.Function):
+    """X [B,T,F2,64] -> z [B,T,PH,PD] (naive:129-142)."""
+
+    @staticmethod
+    def forward(ctx, X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, *params):
+        B, T = X.shape[:2]
+        K = X.shape[2] * X.shape[3]
+        _check_dev('X', X, tuple(X.shape))
+        L = _lib.lib()
+        z = torch.empty((B, T, PH, PD), device=X.device, dtype=torch.float32)
+        sb = L.srf_primary_caps_saved_bytes(B, T, PH, PD)
+        saved = torch.empty(sb, device=X.device, dtype=torch.uint8)
+        tr = int(bool(training))
+        rc = L.srf_primary_caps_fwd(_ptr(X), _ptr(inp_len_i32), B, T, K, PH, PD, *[_ptr(p) for p in params], tr,
+                                    float(p_caps), float(p_in), int(seed), _ptr(z), _ptr(saved), sb, _stream())
+        _lib.check(rc, 'srf_primary_caps_fwd')
+        ctx.meta = (B, T, K, PH, PD, tr, float(p_caps), float(p_in), int(seed))
+        ctx.save_for_backward(X, inp_len_i32, saved, *params)
+        return z
+
+    @staticmethod
+    def backward(ctx, g_z):
+        X, inp_len, saved, *params = ctx.saved_tensors
+        B, T, K, PH, PD, tr, p_caps, p_in, seed = ctx.meta
+        P = dict(zip(CAPS_PARAMS, params))
+        L = _lib.lib()
+        g_X = torch.empty_like(X)
+        grads = [torch.empty_like(p) for p in params]
+        G = dict(zip(CAPS_PARAMS, grads))
+        wb = L.srf_primary_caps_bwd_workspace(B, T, K, PH, PD)
+        ws = torch.empty(wb, device=X.device, dtype=torch.uint8)
+        rc = L.srf_primary_caps_bwd(_ptr(X), _ptr(inp_len), B, T, K, PH, PD, _ptr(P['proj_kernel']),
+                                    _ptr(P['encaps1_kernel']), _ptr(P['encaps2_kernel']), _ptr(P['ln_input_gamma']),
+                                    _ptr(P['ln_input_beta']), tr, p_caps, p_in, seed, _ptr(saved),
+                                    _ptr(g_z.contiguous()), _ptr(g_X), *[_ptr(G[k]) for k in CAPS_PARAMS], _ptr(ws),
+                                    wb, _stream())
+        _lib.check(rc, 'srf_primary_caps_bwd')
+        return (g_X, None, None, None, None, None, None, None, *grads)
+
+
+def primary_caps(X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, params):
+    return PrimaryCaps.apply(X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, *params)
+
+
+class CapsNorm(torch.autograd.Function):
+    """y = drop(LN(v)) per frame over J*D (naive:187-191)."""
+
+    @staticmethod
+    def forward(ctx, v, gamma, beta, training, p, seed, layer):
+        B, T, J, D = v.shape
+        F, n = B * T, J * D
+        L = _lib.lib()
+        y = torch.empty_like(v)
+        stat = torch.empty((F, 4), device=v.device, dtype=torch.float32)
+        tr = int(bool(training))
+        _lib.check(L.srf_capsnorm_fwd(_ptr(v), F, n, _ptr(gamma), _ptr(beta), tr, float(p), int(seed), int(layer),
+                                      _ptr(y), _ptr(stat), _stream()), 'srf_capsnorm_fwd')
+        ctx.meta = (F, n, tr, float(p), int(seed), int(layer))
+        ctx.save_for_backward(v, gamma, beta, stat)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        v, gamma, beta, stat = ctx.saved_tensors
+        F, n, tr, p, seed, layer = ctx.meta
+        L = _lib.lib()
+        g_v, g_g, g_b = torch.empty_like(v), torch.empty_like(gamma), torch.empty_like(beta)
+        wb = L.srf_capsnorm_bwd_workspace(F, n, 0)
+        ws = torch.empty(wb, device=v.device, dtype=torch.uint8)
+        _lib.check(L.srf_capsnorm_bwd(_ptr(v), F, n, _ptr(gamma), _ptr(beta), tr, p, seed, layer, _ptr(stat),
+                                      _ptr(g_y.contiguous()), _ptr(g_v), _ptr(g_g), _ptr(g_b), _ptr(ws), wb,
+                                      _stream()), 'srf_capsnorm_bwd')
+        return g_v, g_g, g_b, None, None, None, None
+
+
+class CapsHead(torch.autograd.Function):
+    """logits = LN_out(length_D(drop(LN_mid(v)))) (naive:187-193)."""
+
+    @staticmethod
+    def forward(ctx, v, gamma_mid, beta_mid, gamma_out, beta_out, training, p, seed, layer):
+        B, T, J, D = v.shape
+        F = B * T
+        L = _lib.lib()
+        logits = torch.empty((B, T, J), device=v.device, dtype=torch.float32)
+        stat = torch.empty((F, 4), device=v.device, dtype=torch.float32)
+        lens = torch.empty((F, J), device=v.device, dtype=torch.float32)
+        tr = int(bool(training))
+        _lib.check(L.srf_caps_head_fwd(_ptr(v), F, J, D, _ptr(gamma_mid), _ptr(beta_mid), _ptr(gamma_out),
+                                       _ptr(beta_out), tr, float(p), int(seed), int(layer), _ptr(logits), _ptr(stat),
+                                       _ptr(lens), _stream()), 'srf_caps_head_fwd')
+        ctx.meta = (F, J, D, tr, float(p), int(seed), int(layer))
+        ctx.save_for_backward(v, gamma_mid, beta_mid, gamma_out, beta_out, stat, lens)
+        return logits
+
+    @staticmethod
+    def backward(ctx, g_logits):
+        v, gm, bm, go, bo, stat, lens = ctx.saved_tensors
+        F, J, D, tr, p, seed, layer = ctx.meta
+        L = _lib.lib()
+        g_v = torch.empty_like(v)
+        g_gm, g_bm, g_go, g_bo = (torch.empty_like(t) for t in (gm, bm, go, bo))
+        wb = L.srf_capsnorm_bwd_workspace(F, J * D, J)
+        ws = torch.empty(wb, device=v.device, dtype=torch.uint8)
+        _lib.check(L.srf_caps_head_bwd(_ptr(v), F, J, D, _ptr(gm), _ptr(bm), _ptr(go), tr, p, seed, layer,
+                                       _ptr(stat), _ptr(lens), _ptr(g_logits.contiguous()), _ptr(g_v), _ptr(g_gm),
+                                       _ptr(g_bm), _ptr(g_go), _ptr(g_bo), _ptr(ws), wb, _stream()),
+                   'srf_caps_head_bwd')
+        return g_v, g_gm, g_bm, g_go, g_bo, None, None, None, None
+
+
+class CtcLoss(torch.autograd.Function):
+    """Per-utterance CTC NLL (blank = C-1 by the caller); the logit gradient is
+    produced by the same kernel launch and scaled by the incoming per-utterance
+    gradient in backward."""
+
+    @staticmethod
+    def forward(ctx, logits, labels_i32, label_len_i32, logit_len_i32, blank):
+        B, T, C = logits.shape
+        Lmax = labels_i32.shape[1]
+        L = _lib.lib()
+        nll = torch.empty(B, device=logits.device, dtype=torch.float32)
+        need_grad = logits.requires_grad
+        grad = torch.empty_like(logits) if need_grad else None
+        wb = L.srf_ctc_workspace(B, T, C, Lmax)
+        ws = torch.empty(wb, device=logits.device, dtype=torch.uint8)
+        _lib.check(L.srf_ctc_loss(_ptr(logits.contiguous()), _ptr(labels_i32), _ptr(label_len_i32),
+                                  _ptr(logit_len_i32), B, T, C, Lmax, int(blank), 1.0, _ptr(nll),
+                                  _ptr(grad) if need_grad else None, _ptr(ws), wb, _stream()), 'srf_ctc_loss')
+        if need_grad:
+            ctx.save_for_backward(grad)
+        return nll
+
+    @staticmethod
+    def backward(ctx, g_nll):
+        (grad,) = ctx.saved_tensors
+        return grad * g_nll[:, None, None], None, None, None, None
+
+
+def ctc_loss(logits, labels, label_len, logit_len, blank):
+    i32 = torch.int32
+    return CtcLoss.apply(logits, labels.to(i32).contiguous(), label_len.to(i32).contiguous(),
+                         logit_len.to(i32).contiguous(), blank)

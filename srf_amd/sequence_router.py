@@ -5,18 +5,18 @@ Same constructor ``SequenceRouter(config, logger, class_n)`` and call
 [B, ceil(T/4), class_n].  ``feats`` must already be cropped to max(inp_len)
 (trainer_sr.py:59-60), as in the reference.
 
-Compute placement: the routing layers (window + pose transform + DR) run in the
-HIP library through ``srf_amd.ops`` (no fallback); the CNN front end, primary
-capsules and the norms are assembled from torch device ops in this revision
-(DESIGN.md lists them as the next kernels).  All parameters are views into one
-flat fp32 buffer (``flat_params``) with a matching flat gradient buffer, so the
-data-parallel all-reduce and the Adam update are one launch each.
+Compute placement: every stage runs in the HIP library through ``srf_amd.ops``
+(CNN front end, primary capsules, the routing layers, the per-layer norms and
+the output head); there is no CPU or torch-op fallback.  All parameters are
+views into one flat fp32 buffer (``flat_params``) with a matching flat gradient
+buffer, so the data-parallel all-reduce and the Adam update are one launch each.
+Dropout masks come from a counter-based RNG keyed by a per-call seed, so the
+backward kernels regenerate them instead of storing them.
 """
 import math
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 from . import ops
 
@@ -26,36 +26,6 @@ LN_EPS = 1e-3       # Keras LayerNormalization default
 BN_EPS = 1e-3       # Keras BatchNormalization default
 BN_MOMENTUM = 0.99
 CNN_DROPOUT = 0.2   # hard-coded, sequence_router.py:62 and naive:82
-
-
-def same_pad(n, k, s):
-    out = -(-n // s)
-    total = max((out - 1) * s + k - n, 0)
-    return out, total // 2, total - total // 2
-
-
-def conv2d_same_nhwc(x, kern, bias, stride):
-    """Keras Conv2D(padding='same') on NHWC with kernel [kh, kw, Cin, Cout]."""
-    _, H, W, _ = x.shape
-    _, pt, pb = same_pad(H, kern.shape[0], stride)
-    _, pl, pr = same_pad(W, kern.shape[1], stride)
-    xn = F.pad(x.permute(0, 3, 1, 2), (pl, pr, pt, pb))
-    return F.conv2d(xn, kern.permute(3, 2, 0, 1), bias, stride=stride).permute(0, 2, 3, 1)
-
-
-def time_mask(inp_len, div, T, dtype):
-    """model_helper.py:125-140: 1 for t < ceil(len/div)."""
-    lens = (inp_len.to(torch.int64) + div - 1) // div
-    return (torch.arange(T, device=inp_len.device)[None, :] < lens[:, None]).to(dtype)
-
-
-def squash(s, dim=-1):
-    n2 = torch.sum(s * s, dim=dim, keepdim=True)
-    return n2 / (1.0 + n2) * (s / torch.sqrt(n2 + SQUASH_EPS))
-
-
-def layer_norm(x, gamma, beta):
-    return F.layer_norm(x, x.shape[-1:], gamma, beta, LN_EPS)
 
 
 class SequenceRouter(torch.nn.Module):
@@ -92,6 +62,8 @@ class SequenceRouter(torch.nn.Module):
         self.init = config.model_initializer
         self.dropout_enabled = True     # test hook: parity runs use BN batch stats without dropout
         self.n_chunks_override = {}     # layer -> n_chunks (tuning hook)
+        self._seed_base = int(np.random.default_rng(seed).integers(1, 2 ** 62))
+        self._calls = 0
 
         w = self.window
         if self.enc_num > 1:   # (in_n, out_n, out_d, in_d), naive:88-95
@@ -211,72 +183,36 @@ class SequenceRouter(torch.nn.Module):
             self._geoms[key] = g
         return g
 
-    def _dropout(self, x, p, training):
-        if training and self.dropout_enabled and p > 0:
-            return F.dropout(x, p, training=True)
-        return x
+    def _next_seed(self):
+        self._calls += 1
+        return (self._seed_base * 0x9E3779B1 + self._calls) % (1 << 63)
 
     # ---------------------------------------------------------------- forward
-    def cnn_fe(self, feats, inp_len, training):
-        """CapsulationLayer.call (sequence_router.py:69-82), NHWC."""
-        x = feats.unsqueeze(-1)
-        for k in range(self.cnn_n):
-            x1 = self._dropout(conv2d_same_nhwc(x, self.P(f'conv{k}a_kernel'), self.P(f'conv{k}a_bias'), 2),
-                               CNN_DROPOUT, training)
-            x2 = self._dropout(conv2d_same_nhwc(x, self.P(f'conv{k}b_kernel'), self.P(f'conv{k}b_bias'), 2),
-                               CNN_DROPOUT, training)
-            x = torch.maximum(x1, x2)
-            m = time_mask(inp_len, 2 ** (k + 1), x.shape[1], x.dtype)[:, :, None, None]
-            x = x * m
-            x = self._batch_norm(x, k, training)
-            x = x * m
-        return x
-
-    def _batch_norm(self, x, k, training):
-        gamma, beta = self.P(f'bn{k}_gamma'), self.P(f'bn{k}_beta')
-        mm, mv = getattr(self, f'bn{k}_moving_mean'), getattr(self, f'bn{k}_moving_var')
-        if training:
-            mu = x.mean(dim=(0, 1, 2))
-            var = x.var(dim=(0, 1, 2), unbiased=False)
-            with torch.no_grad():
-                n = x.numel() // x.shape[-1]
-                mm.mul_(BN_MOMENTUM).add_(mu.detach(), alpha=1 - BN_MOMENTUM)
-                mv.mul_(BN_MOMENTUM).add_(var.detach() * (n / max(n - 1, 1)), alpha=1 - BN_MOMENTUM)
-        else:
-            mu, var = mm, mv
-        return (x - mu) * torch.rsqrt(var + BN_EPS) * gamma + beta
-
-    def primary_caps(self, conv_out, inp_len, training):
-        """naive:129-142."""
-        B, T2, F2, C = conv_out.shape
-        emb = conv_out.reshape(B, T2, F2 * C) @ self.P('proj_kernel') + self.P('proj_bias')
-        emb = emb.unsqueeze(-1)
-        e1 = self._dropout(conv2d_same_nhwc(emb, self.P('encaps1_kernel'), self.P('encaps1_bias'), 1),
-                           CNN_DROPOUT, training)
-        e2 = self._dropout(conv2d_same_nhwc(emb, self.P('encaps2_kernel'), self.P('encaps2_bias'), 1),
-                           CNN_DROPOUT, training)
-        emb = torch.maximum(e1, e2) * time_mask(inp_len, 4, T2, emb.dtype)[:, :, None, None]
-        emb = squash(emb, -1)
-        flat = layer_norm(emb.reshape(B, T2, -1), self.P('ln_input_gamma'), self.P('ln_input_beta'))
-        flat = self._dropout(flat, self.inp_dropout, training)
-        return flat.reshape(B, T2, self.caps_inp_n, self.caps_inp_d)
-
     def forward(self, feats, input_lengths=None, training=False, **kwargs):
+        """naive:120-193.  Extra kwargs (mask=, att_mask=) are ignored like the
+        reference's Keras call."""
         inp_len = input_lengths
         if not torch.is_tensor(inp_len):
-            inp_len = torch.as_tensor(inp_len, device=feats.device)
-        inp_len = inp_len.to(feats.device)
+            inp_len = torch.as_tensor(inp_len)
+        il32 = inp_len.to(device=feats.device, dtype=torch.int32).contiguous()
         if self.is_context:
             raise NotImplementedError('SDR (model-caps-context=True) routing kernel is not built in this revision')
-        x = self.cnn_fe(feats, inp_len, training)
-        emb = self.primary_caps(x, inp_len, training)
+        drop = bool(training) and self.dropout_enabled
+        seed = self._next_seed() if drop else 0
+        moving = [getattr(self, n) for n in ('bn0_moving_mean', 'bn0_moving_var', 'bn1_moving_mean',
+                                             'bn1_moving_var')]
+        x = ops.cnnfe(feats.contiguous(), il32, [self.P(k) for k in ops.CNNFE_PARAMS], moving, training,
+                      CNN_DROPOUT if drop else 0.0, seed)
+        emb = ops.primary_caps(x, il32, self.caps_inp_n, self.caps_inp_d, training, CNN_DROPOUT if drop else 0.0,
+                               self.inp_dropout if drop else 0.0, seed, [self.P(k) for k in ops.CAPS_PARAMS])
         B, T2 = emb.shape[:2]
+        p_mid = self.inn_dropout if drop else 0.0
         for l in range(self.enc_num):
-            emb = emb.contiguous()
             v = ops.dynamic_routing(emb, self.P(f'W{l}'), self.P(f'b{l}'), self._geom(l, B, T2))
-            J, D = v.shape[2], v.shape[3]
-            flat = layer_norm(v.reshape(B, T2, J * D), self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'))
-            flat = self._dropout(flat, self.inn_dropout, training)
-            emb = flat.reshape(B, T2, J, D)
-        length = torch.sqrt(torch.sum(emb * emb, dim=-1) + LENGTH_EPS)
-        return layer_norm(length, self.P('ln_output_gamma'), self.P('ln_output_beta'))
+            if l < self.enc_num - 1:
+                emb = ops.CapsNorm.apply(v, self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'), training,
+                                         p_mid, seed, l)
+            else:
+                return ops.CapsHead.apply(v, self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'),
+                                          self.P('ln_output_gamma'), self.P('ln_output_beta'), training, p_mid,
+                                          seed, l)
