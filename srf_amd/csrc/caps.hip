@@ -12,6 +12,7 @@
 #include <cmath>
 
 #include "srf_common.h"
+#include "srf_reduce.h"
 #include "srf_rng.h"
 #include "../../include/srf.h"
 
@@ -45,7 +46,8 @@ __device__ __forceinline__ float drop_mult(bool on, unsigned long long seed, uns
 }
 
 // ---------------------------------------------------------------- proj
-// One wave per frame, outputs in groups of 8.
+// One wave per frame, outputs in groups of 8; the K loop is unrolled 4x with
+// independent loads so the wave keeps several row segments in flight.
 __global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__ X, int F, int K, int PH,
                                                        const float* __restrict__ Wp, const float* __restrict__ bp,
                                                        float* __restrict__ e) {
@@ -54,19 +56,21 @@ __global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__
   if (f >= F) return;
   const float* x = X + (size_t)f * K;
   for (int p0 = 0; p0 < PH; p0 += 8) {
+    const int np = min(8, PH - p0);
     float acc[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+#pragma unroll 4
     for (int k = l; k < K; k += 64) {
       const float xv = x[k];
+      const float* w = Wp + (size_t)k * PH + p0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (p0 + q < PH) acc[q] += xv * Wp[(size_t)k * PH + p0 + q];
+      for (int q = 0; q < 8; ++q) acc[q] += xv * (q < np ? w[q < np ? q : 0] : 0.f);
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const float s = wave_sum(acc[q]);
-      if (l == 0 && p0 + q < PH) e[(size_t)f * PH + p0 + q] = s + bp[p0 + q];
+      if (l == 0 && q < np) e[(size_t)f * PH + p0 + q] = s + bp[p0 + q];
     }
   }
 }
@@ -74,10 +78,10 @@ __global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__
 // g_X[f][k] = sum_p g_e[f][p] Wp[k][p]
 __global__ void proj_bwd_x_kernel(const float* __restrict__ g_e, const float* __restrict__ Wp, int F, int K, int PH,
                                   float* __restrict__ g_X) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)F * K) return;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= F * K) return;
   const int k = idx % K;
-  const size_t f = idx / K;
+  const int f = idx / K;
   float s = 0.f;
   for (int p = 0; p < PH; ++p) s += g_e[f * PH + p] * Wp[(size_t)k * PH + p];
   g_X[idx] = s;
@@ -111,14 +115,6 @@ __global__ void proj_bwd_w_kernel(const float* __restrict__ X, const float* __re
     for (int f = f0; f < f1; ++f) s += g_e[(size_t)f * PH + threadIdx.x];
     part[(size_t)ch * cols + (size_t)K * PH + threadIdx.x] = s;
   }
-}
-
-__global__ void colsum_kernel2(const float* __restrict__ in, int rows, int cols, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += in[(size_t)r * cols + c];
-  out[c] = s;
 }
 
 // ---------------------------------------------------------------- encaps
@@ -503,11 +499,11 @@ CapsSaved caps_saved_layout(int F, int PH, int PD, void* base) {
 }
 
 struct CapsBwdWs {
-  float *gv1, *gv2, *wpart, *wsum, *g_e, *ppart, *psum;
+  float *gv1, *gv2, *wpart, *wsum, *g_e, *ppart, *psum, *scratch;
   size_t bytes;
 };
 
-constexpr int kProjChunks = 16;
+constexpr int kProjChunks = 64;
 
 CapsBwdWs caps_bwd_layout(int F, int K, int PH, int PD, void* base) {
   const size_t E = (size_t)PH * PD;
@@ -520,7 +516,8 @@ CapsBwdWs caps_bwd_layout(int F, int K, int PH, int PD, void* base) {
   };
   const size_t o1 = take((size_t)F * E * 4), o2 = take((size_t)F * E * 4), ow = take((size_t)F * wcols * 4),
                owsum = take(wcols * 4), oge = take((size_t)F * PH * 4), opp = take(kProjChunks * pcols * 4),
-               ops = take(pcols * 4);
+               ops = take(pcols * 4),
+               osc = take(std::max(srf::colsum_scratch_floats(F, (int)wcols), srf::colsum_scratch_floats(kProjChunks, (int)pcols)) * 4);
   char* b = static_cast<char*>(base);
   CapsBwdWs w;
   w.gv1 = (float*)(b + o1);
@@ -530,6 +527,7 @@ CapsBwdWs caps_bwd_layout(int F, int K, int PH, int PD, void* base) {
   w.g_e = (float*)(b + oge);
   w.ppart = (float*)(b + opp);
   w.psum = (float*)(b + ops);
+  w.scratch = (float*)(b + osc);
   w.bytes = off;
   return w;
 }
@@ -625,8 +623,7 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
                      gamma, beta, training, p_caps, p_in, seed, w.gv1, w.gv2, w.wpart);
   SRF_LAUNCH_CHECK("encaps_bwd_a");
   const int wcols = 2 * E + 20 * PD;
-  hipLaunchKernelGGL(colsum_kernel2, dim3((wcols + 255) / 256), dim3(256), 0, st, w.wpart, F, wcols, w.wsum);
-  SRF_LAUNCH_CHECK("colsum(encaps)");
+  if ((rc = srf::colsum(w.wpart, F, wcols, w.wsum, w.scratch, st))) return rc;
   hipLaunchKernelGGL(scatter_encaps_grads, dim3((std::max(E, 20 * PD) + 255) / 256), dim3(256), 0, st, w.wsum, E, PD,
                      g_gamma, g_beta, g_K1, g_b1, g_K2, g_b2);
   SRF_LAUNCH_CHECK("scatter_encaps_grads");
@@ -641,16 +638,16 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
                      fchunk, w.ppart);
   SRF_LAUNCH_CHECK("proj_bwd_w");
   const int pcols = K * PH + PH;
-  hipLaunchKernelGGL(colsum_kernel2, dim3((pcols + 255) / 256), dim3(256), 0, st, w.ppart, kProjChunks, pcols,
-                     w.psum);
-  SRF_LAUNCH_CHECK("colsum(proj)");
+  if ((rc = srf::colsum(w.ppart, kProjChunks, pcols, w.psum, w.scratch, st))) return rc;
   hipLaunchKernelGGL(split_copy, dim3((K * PH + 255) / 256), dim3(256), 0, st, w.psum, K * PH, g_Wp, PH, g_bp);
   SRF_LAUNCH_CHECK("split_copy(proj)");
   return SRF_OK;
 }
 
 size_t srf_capsnorm_bwd_workspace(int F, int n, int J) {
-  return srf::align_up((size_t)F * (2 * n + 2 * J) * 4, 256) + srf::align_up((size_t)(2 * n + 2 * J) * 4, 256);
+  const int cols = 2 * n + 2 * J;
+  return srf::align_up((size_t)F * cols * 4, 256) + srf::align_up((size_t)cols * 4, 256) +
+         srf::colsum_scratch_floats(F, cols) * 4;
 }
 
 int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
@@ -676,12 +673,13 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* part = static_cast<float*>(workspace);
   float* sum = part + srf::align_up((size_t)F * 2 * n * 4, 256) / 4;
+  float* scratch = sum + srf::align_up((size_t)2 * n * 4, 256) / 4;
   hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, st, x, n, gamma, beta, training, p,
                      seed, (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr,
                      (const float*)nullptr, g_x, part);
   SRF_LAUNCH_CHECK("capsnorm_bwd");
-  hipLaunchKernelGGL(colsum_kernel2, dim3((2 * n + 255) / 256), dim3(256), 0, st, part, F, 2 * n, sum);
-  SRF_LAUNCH_CHECK("colsum(capsnorm)");
+  int rc = srf::colsum(part, F, 2 * n, sum, scratch, st);
+  if (rc) return rc;
   hipLaunchKernelGGL(split_copy, dim3((n + 255) / 256), dim3(256), 0, st, sum, n, g_gamma, n, g_beta);
   SRF_LAUNCH_CHECK("split_copy(capsnorm)");
   return SRF_OK;
@@ -719,12 +717,13 @@ int srf_caps_head_bwd(const float* v, int F, int J, int D, const float* gamma_mi
   const int cols = 2 * n + 2 * J;
   float* part = static_cast<float*>(workspace);
   float* sum = part + srf::align_up((size_t)F * cols * 4, 256) / 4;
+  float* scratch = sum + srf::align_up((size_t)cols * 4, 256) / 4;
   hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4, st, v, n, gamma_mid, beta_mid,
                      training, p, seed, (unsigned)(kStreamMid0 + layer), stat, g_logits, 1, J, D, gamma_out, lens,
                      g_v, part);
   SRF_LAUNCH_CHECK("caps_head_bwd");
-  hipLaunchKernelGGL(colsum_kernel2, dim3((cols + 255) / 256), dim3(256), 0, st, part, F, cols, sum);
-  SRF_LAUNCH_CHECK("colsum(head)");
+  int rc = srf::colsum(part, F, cols, sum, scratch, st);
+  if (rc) return rc;
   hipLaunchKernelGGL(split_copy, dim3((n + 255) / 256), dim3(256), 0, st, sum, n, g_gamma_mid, n, g_beta_mid);
   SRF_LAUNCH_CHECK("split_copy(head mid)");
   hipLaunchKernelGGL(split_copy, dim3((J + 255) / 256), dim3(256), 0, st, sum + 2 * n, J, g_gamma_out, J, g_beta_out);

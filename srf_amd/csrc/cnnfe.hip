@@ -20,6 +20,7 @@
 #include <cmath>
 
 #include "srf_common.h"
+#include "srf_reduce.h"
 #include "srf_rng.h"
 #include "../../include/srf.h"
 
@@ -83,12 +84,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
   }
   const float bia = ba[c], bib = bb[c];
   const float keep_scale = 1.f / (1.f - drop_p);
-  const long long P = (long long)d.B * d.T1 * d.F1;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+  const int P = d.B * d.T1 * d.F1;
+  // statistics as sums shifted by the channel biases (no per-element division)
+  float n = 0.f, s1 = 0.f, s2 = 0.f;
+  const float K = 0.5f * (bia + bib);
+#pragma unroll 4
+  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
     const int f1 = p % d.F1;
     const int t1 = (p / d.F1) % d.T1;
-    const int b = p / ((long long)d.F1 * d.T1);
+    const int b = p / (d.F1 * d.T1);
     float a = bia, bv = bib;
 #pragma unroll
     for (int dt = 0; dt < 3; ++dt) {
@@ -97,12 +101,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
       for (int df = 0; df < 3; ++df) {
         const int f = 2 * f1 - d.pf1 + df;
         float x = 0.f;
-        if (t >= 0 && t < d.T && f >= 0 && f < d.Fin) x = feats[((size_t)b * d.T + t) * d.Fin + f];
+        if (t >= 0 && t < d.T && f >= 0 && f < d.Fin) x = feats[(b * d.T + t) * d.Fin + f];
         a += x * wa[dt * 3 + df];
         bv += x * wb[dt * 3 + df];
       }
     }
-    const size_t o = (size_t)p * C + c;
+    const int o = p * C + c;
     if (training && drop_p > 0.f) {
       a *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
       bv *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
@@ -113,10 +117,11 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
     y1[o] = y;
     sel1[o] = s ? 1 : 0;
     n += 1.f;
-    const float delta = y - mean;
-    mean += delta / n;
-    m2 += delta * (y - mean);
+    s1 += y - K;
+    s2 += (y - K) * (y - K);
   }
+  float mean = n > 0.f ? K + s1 / n : 0.f;
+  float m2 = n > 0.f ? fmaxf(s2 - s1 * s1 / n, 0.f) : 0.f;
   sh[0][row][c] = n; sh[1][row][c] = mean; sh[2][row][c] = m2;
   __syncthreads();
   if (row == 0) {
@@ -129,17 +134,26 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
 
 // ---------------------------------------------------------------- BN finalize
 // stats[0][c] = mean, stats[1][c] = rstd, stats[2][c] = scale, stats[3][c] = shift.
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int nparts, const float* __restrict__ gamma,
-                                   const float* __restrict__ beta, float* __restrict__ mmean,
-                                   float* __restrict__ mvar, int training, float* __restrict__ stats) {
-  const int c = threadIdx.x;
-  if (c >= C) return;
-  float mean, var;
-  if (training) {
-    float n = 0.f, mu = 0.f, m2 = 0.f;
-    for (int k = 0; k < nparts; ++k)
+// 1024 threads = 16 partial streams x 64 channels, Chan-merged through LDS.
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ part, int nparts,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           float* __restrict__ mmean, float* __restrict__ mvar,
+                                                           int training, float* __restrict__ stats) {
+  __shared__ float sh[3][16][C];
+  const int c = threadIdx.x & (C - 1), r = threadIdx.x >> 6;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  if (training)
+#pragma unroll 8
+    for (int k = r; k < nparts; k += 16)
       chan_merge(n, mu, m2, part[((size_t)k * 3 + 0) * C + c], part[((size_t)k * 3 + 1) * C + c],
                  part[((size_t)k * 3 + 2) * C + c]);
+  sh[0][r][c] = n; sh[1][r][c] = mu; sh[2][r][c] = m2;
+  __syncthreads();
+  if (r != 0) return;
+  float mean, var;
+  if (training) {
+    for (int q = 1; q < 16; ++q) chan_merge(n, mu, m2, sh[0][q][c], sh[1][q][c], sh[2][q][c]);
     mean = mu;
     var = m2 / n;
     // moving averages; the fused NHWC kernel feeds the Bessel-corrected variance
@@ -291,12 +305,12 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
 __global__ void bn_apply_kernel(const float* __restrict__ y, const float* __restrict__ stats,
                                 const int* __restrict__ inp_len, int B, int Tk, int Fk, int div,
                                 float* __restrict__ out) {
-  const size_t n4 = (size_t)B * Tk * Fk * C / 4;
-  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (size_t)gridDim.x * blockDim.x) {
+  const int n4 = B * Tk * Fk * C / 4;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += gridDim.x * blockDim.x) {
     const int c4 = (q * 4) % C;
-    const size_t p = q * 4 / C;
+    const int p = q * 4 / C;
     const int t = (p / Fk) % Tk;
-    const int b = p / ((size_t)Fk * Tk);
+    const int b = p / (Fk * Tk);
     f4 v = {0.f, 0.f, 0.f, 0.f};
     if (t < ceil_div_len(inp_len[b], div)) {
       const f4 x = reinterpret_cast<const f4*>(y)[q];
@@ -321,11 +335,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
   __shared__ float sh[2][4][C];
   const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
   const float mean = stats[c], rstd = stats[C + c];
-  const long long P = (long long)B * Tk * Fk;
+  const int P = B * Tk * Fk;
   float s0 = 0.f, s1 = 0.f;
-  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+#pragma unroll 4
+  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
     const int t = (p / Fk) % Tk;
-    const int b = p / ((long long)Fk * Tk);
+    const int b = p / (Fk * Tk);
     if (t >= ceil_div_len(inp_len[b], div)) continue;
     const size_t o = (size_t)p * C + c;
     const float dy = g[o];
@@ -339,16 +354,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
     part[((size_t)blockIdx.x * 2 + 0) * C + c] = s0;
     part[((size_t)blockIdx.x * 2 + 1) * C + c] = s1;
   }
-}
-
-// Column sums of a [rows][cols] slab: out[c] = sum_r in[r][c] (optionally into
-// two outputs split at `split`).
-__global__ void colsum_kernel(const float* __restrict__ in, int rows, int cols, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += in[(size_t)r * cols + c];
-  out[c] = s;
 }
 
 __device__ __forceinline__ float bn_bwd_elem(float gin, float y, float mask, float mean, float rstd, float gamma,
@@ -367,14 +372,15 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     float* __restrict__ part) {
   __shared__ float sh[2][4][C];
   const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
-  const long long P = (long long)d.B * d.T2 * d.F2;
+  const int P = d.B * d.T2 * d.F2;
   const float mean = stats2[c], rstd = stats2[C + c], gam = gamma2[c];
   const float sdy_n = bnsum2[c] / (float)P, sdyxh_n = bnsum2[C + c] / (float)P;
   const float keep_scale = 1.f / (1.f - drop_p);
   float ga_s = 0.f, gb_s = 0.f;
-  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+#pragma unroll 4
+  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
     const int t = (p / d.F2) % d.T2;
-    const int b = p / ((long long)d.F2 * d.T2);
+    const int b = p / (d.F2 * d.T2);
     const float mask = t < ceil_div_len(inp_len[b], 4) ? 1.f : 0.f;
     const size_t o = (size_t)p * C + c;
     const float gy = bn_bwd_elem(g_out[o], y2[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
@@ -588,17 +594,18 @@ __global__ __launch_bounds__(256) void conv1_bwd_kernel(
     float* __restrict__ part) {
   __shared__ float sh[4][20][C];
   const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
-  const long long P = (long long)d.B * d.T1 * d.F1;
+  const int P = d.B * d.T1 * d.F1;
   const float mean = stats1[c], rstd = stats1[C + c], gam = gamma1[c];
   const float sdy_n = bnsum1[c] / (float)P, sdyxh_n = bnsum1[C + c] / (float)P;
   const float keep_scale = 1.f / (1.f - drop_p);
   float acc[20];
 #pragma unroll
   for (int j = 0; j < 20; ++j) acc[j] = 0.f;
-  for (long long p = (long long)blockIdx.x * 4 + row; p < P; p += (long long)gridDim.x * 4) {
+#pragma unroll 4
+  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
     const int f1 = p % d.F1;
     const int t1 = (p / d.F1) % d.T1;
-    const int b = p / ((long long)d.F1 * d.T1);
+    const int b = p / (d.F1 * d.T1);
     const float mask = t1 < ceil_div_len(inp_len[b], 2) ? 1.f : 0.f;
     const size_t o = (size_t)p * C + c;
     const float gy = bn_bwd_elem(g_x1[o], y1[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
@@ -742,7 +749,7 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3(kConv1Blocks), dim3(256), 0, st, feats, inp_len, d, k0a, b0a, k0b, b0b,
                      training, drop_p, seed, sv.y1, sv.sel1, w.part1);
   SRF_LAUNCH_CHECK("conv1_fwd");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(C), 0, st, w.part1, kConv1Blocks, gamma0, beta0, mmean0,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(1024), 0, st, w.part1, kConv1Blocks, gamma0, beta0, mmean0,
                      mvar0, training, sv.stats1);
   SRF_LAUNCH_CHECK("bn_finalize(1)");
   hipLaunchKernelGGL(pack_w2_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wp);
@@ -750,7 +757,7 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(conv2_fwd_kernel, dim3(nb2), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, d, w.wp, b1a, b1b,
                      training, drop_p, seed, sv.y2, sv.sel2, w.part2);
   SRF_LAUNCH_CHECK("conv2_fwd");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(C), 0, st, w.part2, nb2, gamma1, beta1, mmean1, mvar1,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(1024), 0, st, w.part2, nb2, gamma1, beta1, mmean1, mvar1,
                      training, sv.stats2);
   SRF_LAUNCH_CHECK("bn_finalize(2)");
   hipLaunchKernelGGL(bn_apply_kernel, dim3(1024), dim3(256), 0, st, sv.y2, sv.stats2, inp_len, d.B, d.T2, d.F2, 4,
@@ -763,11 +770,11 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
 
 namespace {
 struct BwdWs2 {
-  float *bnpart, *bnsum2, *bnsum1, *g_ab, *biaspart, *g_x1, *wq, *wpart, *c1part, *c1sum;
+  float *bnpart, *bnsum2, *bnsum1, *g_ab, *biaspart, *g_x1, *wq, *wpart, *c1part, *c1sum, *scratch;
   size_t bytes;
 };
 
-constexpr int kBnBlocks = 512;
+constexpr int kBnBlocks = 1024;
 constexpr int kWgradSplits = 32;
 
 BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
@@ -781,7 +788,8 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   const size_t obp = take((size_t)kBnBlocks * 2 * C * 4), os2 = take(2 * C * 4), os1 = take(2 * C * 4),
                oab = take(P2 * 2 * C * 4), obias = take((size_t)kBnBlocks * 2 * C * 4), ogx = take(P1 * C * 4),
                owq = take((size_t)9 * 2 * C * C * 4), owp = take((size_t)kWgradSplits * 9 * C * 2 * C * 4),
-               oc1 = take((size_t)kConv1Blocks * 20 * C * 4), oc1s = take(20 * C * 4);
+               oc1 = take((size_t)kConv1Blocks * 20 * C * 4), oc1s = take(20 * C * 4),
+               oscr = take(srf::colsum_scratch_floats(kConv1Blocks, 20 * C) * 4);
   char* b = static_cast<char*>(base);
   BwdWs2 w;
   w.bnpart = (float*)(b + obp);
@@ -794,6 +802,7 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   w.wpart = (float*)(b + owp);
   w.c1part = (float*)(b + oc1);
   w.c1sum = (float*)(b + oc1s);
+  w.scratch = (float*)(b + oscr);
   w.bytes = off;
   return w;
 }
@@ -848,15 +857,13 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.stats2, inp_len, d.B,
                      d.T2, d.F2, 4, w.bnpart);
   SRF_LAUNCH_CHECK("bn_bwd_reduce(2)");
-  hipLaunchKernelGGL(colsum_kernel, dim3(1), dim3(2 * C), 0, st, w.bnpart, kBnBlocks, 2 * C, w.bnsum2);
-  SRF_LAUNCH_CHECK("colsum(bn2)");
+  if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st))) return rc;
   SRF_HIP_TRY(hipMemcpyAsync(g_beta1, w.bnsum2, C * 4, hipMemcpyDeviceToDevice, st));
   SRF_HIP_TRY(hipMemcpyAsync(g_gamma1, w.bnsum2 + C, C * 4, hipMemcpyDeviceToDevice, st));
   hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.sel2, sv.stats2,
                      gamma1, w.bnsum2, inp_len, d, drop_p, seed, w.g_ab, w.biaspart);
   SRF_LAUNCH_CHECK("conv2_bwd_prep");
-  hipLaunchKernelGGL(colsum_kernel, dim3(1), dim3(2 * C), 0, st, w.biaspart, kBnBlocks, 2 * C, w.bnpart);
-  SRF_LAUNCH_CHECK("colsum(bias2)");
+  if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, w.bnpart, w.scratch, st))) return rc;
   SRF_HIP_TRY(hipMemcpyAsync(g_b1a, w.bnpart, C * 4, hipMemcpyDeviceToDevice, st));
   SRF_HIP_TRY(hipMemcpyAsync(g_b1b, w.bnpart + C, C * 4, hipMemcpyDeviceToDevice, st));
   // stage-2 data gradient (4 stride-parity classes) and weight gradient
@@ -882,16 +889,13 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, w.g_x1, sv.y1, sv.stats1, inp_len, d.B,
                      d.T1, d.F1, 2, w.bnpart);
   SRF_LAUNCH_CHECK("bn_bwd_reduce(1)");
-  hipLaunchKernelGGL(colsum_kernel, dim3(1), dim3(2 * C), 0, st, w.bnpart, kBnBlocks, 2 * C, w.bnsum1);
-  SRF_LAUNCH_CHECK("colsum(bn1)");
+  if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum1, w.scratch, st))) return rc;
   SRF_HIP_TRY(hipMemcpyAsync(g_beta0, w.bnsum1, C * 4, hipMemcpyDeviceToDevice, st));
   SRF_HIP_TRY(hipMemcpyAsync(g_gamma0, w.bnsum1 + C, C * 4, hipMemcpyDeviceToDevice, st));
   hipLaunchKernelGGL(conv1_bwd_kernel, dim3(kConv1Blocks), dim3(256), 0, st, feats, inp_len, d, w.g_x1, sv.y1,
                      sv.sel1, sv.stats1, gamma0, w.bnsum1, drop_p, seed, w.c1part);
   SRF_LAUNCH_CHECK("conv1_bwd");
-  hipLaunchKernelGGL(colsum_kernel, dim3((20 * C + 255) / 256), dim3(256), 0, st, w.c1part, kConv1Blocks, 20 * C,
-                     w.c1sum);
-  SRF_LAUNCH_CHECK("colsum(conv1)");
+  if ((rc = srf::colsum(w.c1part, kConv1Blocks, 20 * C, w.c1sum, w.scratch, st))) return rc;
   hipLaunchKernelGGL(conv1_grad_unpack_kernel, dim3((20 * C + 255) / 256), dim3(256), 0, st, w.c1sum, g_k0a, g_k0b,
                      g_b0a, g_b0b);
   SRF_LAUNCH_CHECK("conv1_grad_unpack");

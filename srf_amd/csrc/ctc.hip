@@ -20,85 +20,150 @@ __device__ __forceinline__ float lse2(float a, float b) {
   return m + __logf(__expf(a - m) + __expf(b - m));
 }
 
-__global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logits, const int* __restrict__ labels,
-                                                  const int* __restrict__ label_len,
-                                                  const int* __restrict__ logit_len, int Tmax, int C, int Lmax,
-                                                  int blank, float scale, float* __restrict__ nll,
-                                                  float* __restrict__ grad, float* __restrict__ ws) {
-  extern __shared__ int ext[];   // 2*Lmax+1
+// Recursion kernel: grid (B, 2).  Block (b, 0) runs the alpha recursion and
+// writes nll[b]; block (b, 1) runs beta.  Both recompute the log-softmax into
+// LDS (when it fits; else workspace) and stream their rows to workspace.
+// Dynamic LDS: ext[Smax] (int) | row[2][Smax] | lp[T*C].
+__global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restrict__ logits,
+                                                            const int* __restrict__ labels,
+                                                            const int* __restrict__ label_len,
+                                                            const int* __restrict__ logit_len, int Tmax, int C,
+                                                            int Lmax, int blank, int lp_in_lds, int want_beta,
+                                                            float* __restrict__ nll, float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Smax = 2 * Lmax + 1;
+  int* ext = reinterpret_cast<int*>(smem);
+  float* row = smem + Smax;
   const int b = blockIdx.x;
+  const bool is_beta = blockIdx.y == 1;
+  if (is_beta && !want_beta) return;
   const int L = label_len[b];
   const int Tb = min(logit_len[b], Tmax);
   const int S = 2 * L + 1;
-  const int Smax = 2 * Lmax + 1;
-  float* lp = ws + (size_t)b * Tmax * (C + 2 * Smax);
-  float* alpha = lp + (size_t)Tmax * C;
-  float* beta = alpha + (size_t)Tmax * Smax;
+  float* gws = ws + (size_t)b * Tmax * (C + 2 * Smax);
+  float* lpg = gws;                                       // [Tmax][C] (global copy, for the gradient)
+  float* lp = lp_in_lds ? (row + 2 * Smax) : lpg;
+  float* out = gws + (size_t)Tmax * C + (is_beta ? (size_t)Tmax * Smax : 0);
   const float* lg = logits + (size_t)b * Tmax * C;
   for (int s = threadIdx.x; s < S; s += blockDim.x) ext[s] = (s & 1) ? labels[(size_t)b * Lmax + (s >> 1)] : blank;
-  // log-softmax, one thread per frame
-  for (int t = threadIdx.x; t < Tb; t += blockDim.x) {
-    float m = -INFINITY;
-    for (int c = 0; c < C; ++c) m = fmaxf(m, lg[(size_t)t * C + c]);
-    float z = 0.f;
-    for (int c = 0; c < C; ++c) z += __expf(lg[(size_t)t * C + c] - m);
-    const float lz = m + __logf(z);
-    for (int c = 0; c < C; ++c) lp[(size_t)t * C + c] = lg[(size_t)t * C + c] - lz;
+  {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int t = w; t < Tb; t += nw) {
+      float m = -INFINITY;
+      for (int c = l; c < C; c += 64) m = fmaxf(m, lg[(size_t)t * C + c]);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      float z = 0.f;
+      for (int c = l; c < C; c += 64) z += __expf(lg[(size_t)t * C + c] - m);
+      z = wave_sum(z);
+      const float lz = m + __logf(z);
+      for (int c = l; c < C; c += 64) {
+        const float v = lg[(size_t)t * C + c] - lz;
+        lp[(size_t)t * C + c] = v;
+        if (!is_beta && lp_in_lds) lpg[(size_t)t * C + c] = v;
+      }
+    }
   }
   __syncthreads();
-  // alpha
-  for (int t = 0; t < Tb; ++t) {
-    for (int s = threadIdx.x; s < S; s += blockDim.x) {
-      float a;
-      if (t == 0) {
-        a = (s < 2) ? 0.f : -INFINITY;
-      } else {
-        const float* ap = alpha + (size_t)(t - 1) * Smax;
-        a = ap[s];
-        if (s >= 1) a = lse2(a, ap[s - 1]);
-        if (s >= 2 && ext[s] != blank && ext[s] != ext[s - 2]) a = lse2(a, ap[s - 2]);
+  if (!is_beta) {
+    for (int t = 0; t < Tb; ++t) {
+      const float* ap = row + ((t + 1) & 1) * Smax;
+      float* an = row + (t & 1) * Smax;
+      for (int s = threadIdx.x; s < S; s += blockDim.x) {
+        float a;
+        if (t == 0) {
+          a = (s < 2) ? 0.f : -INFINITY;
+        } else {
+          a = ap[s];
+          if (s >= 1) a = lse2(a, ap[s - 1]);
+          if (s >= 2 && ext[s] != blank && ext[s] != ext[s - 2]) a = lse2(a, ap[s - 2]);
+        }
+        a = (a == -INFINITY) ? -INFINITY : a + lp[(size_t)t * C + ext[s]];
+        an[s] = a;
+        out[(size_t)t * Smax + s] = a;
       }
-      alpha[(size_t)t * Smax + s] = (a == -INFINITY) ? -INFINITY : a + lp[(size_t)t * C + ext[s]];
+      __syncthreads();
     }
-    __syncthreads();
-  }
-  // beta
-  for (int t = Tb - 1; t >= 0; --t) {
-    for (int s = threadIdx.x; s < S; s += blockDim.x) {
-      float a;
-      if (t == Tb - 1) {
-        a = (s >= S - 2) ? 0.f : -INFINITY;
-      } else {
-        const float* bp = beta + (size_t)(t + 1) * Smax;
-        a = bp[s];
-        if (s + 1 < S) a = lse2(a, bp[s + 1]);
-        if (s + 2 < S && ext[s] != blank && ext[s] != ext[s + 2]) a = lse2(a, bp[s + 2]);
+    if (threadIdx.x == 0) {
+      float ll = -INFINITY;
+      if (Tb > 0) {
+        const float* al = row + ((Tb - 1) & 1) * Smax;
+        ll = al[S - 1];
+        if (S >= 2) ll = lse2(ll, al[S - 2]);
       }
-      beta[(size_t)t * Smax + s] = (a == -INFINITY) ? -INFINITY : a + lp[(size_t)t * C + ext[s]];
+      nll[b] = -ll;
     }
-    __syncthreads();
+  } else {
+    for (int t = Tb - 1; t >= 0; --t) {
+      const float* bp = row + ((t + 1) & 1) * Smax;
+      float* bn = row + (t & 1) * Smax;
+      for (int s = threadIdx.x; s < S; s += blockDim.x) {
+        float a;
+        if (t == Tb - 1) {
+          a = (s >= S - 2) ? 0.f : -INFINITY;
+        } else {
+          a = bp[s];
+          if (s + 1 < S) a = lse2(a, bp[s + 1]);
+          if (s + 2 < S && ext[s] != blank && ext[s] != ext[s + 2]) a = lse2(a, bp[s + 2]);
+        }
+        a = (a == -INFINITY) ? -INFINITY : a + lp[(size_t)t * C + ext[s]];
+        bn[s] = a;
+        out[(size_t)t * Smax + s] = a;
+      }
+      __syncthreads();
+    }
   }
-  float ll = -INFINITY;
-  if (Tb > 0) {
-    ll = alpha[(size_t)(Tb - 1) * Smax + S - 1];
-    if (S >= 2) ll = lse2(ll, alpha[(size_t)(Tb - 1) * Smax + S - 2]);
-  }
-  if (threadIdx.x == 0) nll[b] = -ll;
-  if (!grad) return;
-  float* gb = grad + (size_t)b * Tmax * C;
+}
+
+// Gradient kernel: grid (B, ceil(Tmax/16)), 256 threads = 16 frames x 16 class
+// lanes.  Per class the label positions are walked through a per-block
+// next-occurrence list (built in LDS), so a frame costs O(L + C), not O(C * L).
+__global__ __launch_bounds__(256) void ctc_grad_kernel(const int* __restrict__ labels,
+                                                       const int* __restrict__ label_len,
+                                                       const int* __restrict__ logit_len,
+                                                       const float* __restrict__ nll, int Tmax, int C, int Lmax,
+                                                       int blank, float scale, const float* __restrict__ ws,
+                                                       float* __restrict__ grad) {
+  extern __shared__ int lists[];   // head[C] | next[Lmax]
+  int* head = lists;
+  int* next = lists + C;
+  const int b = blockIdx.x;
+  const int L = label_len[b];
+  const int Tb = min(logit_len[b], Tmax);
+  const int Smax = 2 * Lmax + 1;
+  const float ll = -nll[b];
   const bool feasible = ll > -INFINITY;
-  for (int idx = threadIdx.x; idx < Tmax * C; idx += blockDim.x) {
-    const int t = idx / C, c = idx - t * C;
+  if (threadIdx.x == 0) {
+    for (int c = 0; c < C; ++c) head[c] = -1;
+    for (int k = L - 1; k >= 0; --k) {
+      const int c = labels[(size_t)b * Lmax + k];
+      next[k] = head[c];
+      head[c] = k;
+    }
+  }
+  __syncthreads();
+  const float* gws = ws + (size_t)b * Tmax * (C + 2 * Smax);
+  const float* lp = gws;
+  const float* alpha = gws + (size_t)Tmax * C;
+  const float* beta = alpha + (size_t)Tmax * Smax;
+  const int t = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (t >= Tmax) return;
+  float* gb = grad + ((size_t)b * Tmax + t) * C;
+  for (int c = threadIdx.x & 15; c < C; c += 16) {
     float g = 0.f;
     if (t < Tb && feasible) {
       float acc = -INFINITY;
-      for (int s = 0; s < S; ++s)
-        if (ext[s] == c) acc = lse2(acc, alpha[(size_t)t * Smax + s] + beta[(size_t)t * Smax + s]);
+      const float* at = alpha + (size_t)t * Smax;
+      const float* bt = beta + (size_t)t * Smax;
+      if (c == blank) {
+        for (int s = 0; s <= 2 * L; s += 2) acc = lse2(acc, at[s] + bt[s]);
+      } else {
+        for (int k = head[c]; k >= 0; k = next[k]) acc = lse2(acc, at[2 * k + 1] + bt[2 * k + 1]);
+      }
       const float l = lp[(size_t)t * C + c];
-      g = __expf(l) - (acc == -INFINITY ? 0.f : __expf(acc - l - ll));
-      g *= scale;
+      g = (__expf(l) - (acc == -INFINITY ? 0.f : __expf(acc - l - ll))) * scale;
     }
-    gb[idx] = g;
+    gb[c] = g;
   }
 }
 
@@ -119,9 +184,20 @@ int srf_ctc_loss(const float* logits, const int* labels, const int* label_len, c
     srf::set_error("CTC workspace too small");
     return SRF_EWORKSPACE;
   }
-  hipLaunchKernelGGL(ctc_kernel, dim3(B), dim3(256), (size_t)(2 * Lmax + 1) * sizeof(int),
-                     static_cast<hipStream_t>(stream), logits, labels, label_len, logit_len, Tmax, C, Lmax, blank,
-                     grad_scale, nll, grad, static_cast<float*>(workspace));
+  const size_t Smax = 2 * (size_t)Lmax + 1;
+  size_t shmem = 3 * Smax * sizeof(float);
+  const size_t lp_bytes = (size_t)Tmax * C * sizeof(float);
+  const int lp_in_lds = (shmem + lp_bytes) <= 96 * 1024;
+  if (lp_in_lds) shmem += lp_bytes;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(ctc_recursion_kernel, dim3(B, 2), dim3(256), shmem, st, logits, labels, label_len, logit_len,
+                     Tmax, C, Lmax, blank, lp_in_lds, grad ? 1 : 0, nll, static_cast<float*>(workspace));
+  SRF_LAUNCH_CHECK("ctc_recursion");
+  if (grad) {
+    hipLaunchKernelGGL(ctc_grad_kernel, dim3(B, (Tmax + 15) / 16), dim3(256), (size_t)(C + Lmax + 1) * sizeof(int),
+                       st, labels, label_len, logit_len, nll, Tmax, C, Lmax, blank, grad_scale,
+                       static_cast<const float*>(workspace), grad);
+  }
   SRF_LAUNCH_CHECK("ctc");
   return SRF_OK;
 }

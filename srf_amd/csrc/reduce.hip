@@ -1,0 +1,58 @@
+// Deterministic column sums shared by the backward passes:
+// out[c] = sum_r in[r][c] over a [rows][cols] slab of per-block partials.
+// Stage 1: blocks of 4 row-lanes x 64 columns stream a slice of rows (coalesced
+// along columns) into part[slice][cols]; stage 2: one thread per column adds the
+// slices in order.  Fixed order => bitwise reproducible.
+#include "srf_common.h"
+#include "srf_reduce.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ in, int rows, int cols,
+                                                     int rows_per_slice, float* __restrict__ part) {
+  __shared__ float sh[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_slice, r1 = min(rows, r0 + rows_per_slice);
+  float s = 0.f;
+  if (c < cols) {
+#pragma unroll 8
+    for (int r = r0 + rg; r < r1; r += 4) s += in[(size_t)r * cols + c];
+  }
+  sh[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < cols) {
+    const int l = threadIdx.x & 63;
+    part[(size_t)blockIdx.y * cols + c] = sh[0][l] + sh[1][l] + sh[2][l] + sh[3][l];
+  }
+}
+
+__global__ void colsum_stage2(const float* __restrict__ part, int slices, int cols, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < slices; ++k) s += part[(size_t)k * cols + c];
+  out[c] = s;
+}
+
+}  // namespace
+
+namespace srf {
+
+size_t colsum_scratch_floats(int rows, int cols) { return (size_t)kColsumMaxSlices * cols; (void)rows; }
+
+int colsum(const float* in, int rows, int cols, float* out, float* scratch, hipStream_t st) {
+  const int cblocks = (cols + 63) / 64;
+  int slices = std::max(1, std::min(kColsumMaxSlices, (1024 + cblocks - 1) / cblocks));
+  slices = std::min(slices, std::max(1, rows / 16));
+  const int rps = (rows + slices - 1) / slices;
+  slices = (rows + rps - 1) / rps;
+  hipLaunchKernelGGL(colsum_stage1, dim3(cblocks, slices), dim3(256), 0, st, in, rows, cols, rps, scratch);
+  SRF_LAUNCH_CHECK("colsum_stage1");
+  hipLaunchKernelGGL(colsum_stage2, dim3((cols + 255) / 256), dim3(256), 0, st, scratch, slices, cols, out);
+  SRF_LAUNCH_CHECK("colsum_stage2");
+  return SRF_OK;
+}
+
+}  // namespace srf

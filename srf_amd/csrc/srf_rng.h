@@ -1,7 +1,8 @@
 // Counter-based dropout RNG shared by forward and backward kernels: the keep
 // mask of element idx in stream s is a pure function of (seed, s, idx), so the
-// backward regenerates it instead of storing it.  splitmix64 finaliser; the
-// same function is restated in numpy by the tests (tests/torch_ref.py).
+// backward regenerates it instead of storing it.  32-bit arithmetic only
+// (lowbias32 mixer, two rounds keyed by the seed); the same function is restated
+// in numpy by the tests (tests/torch_ref.py).
 #pragma once
 #include <cstdint>
 
@@ -16,16 +17,24 @@ enum SrfRngStream : unsigned {
   kStreamMid0 = 7,   // + routing layer index
 };
 
-__device__ __forceinline__ uint64_t srf_mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
+__host__ __device__ __forceinline__ uint32_t srf_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t srf_stream_key(uint64_t seed, unsigned stream) {
+  return srf_mix32((uint32_t)seed ^ srf_mix32((uint32_t)(seed >> 32) ^ (stream * 0x9E3779B9u + 0x7F4A7C15u)));
 }
 
 // uniform in [0, 1) with 24 random bits
 __device__ __forceinline__ float srf_uniform(uint64_t seed, unsigned stream, uint64_t idx) {
-  const uint64_t z = srf_mix64(seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(stream + 1))) + idx * 0xD1B54A32D192ED03ull;
-  return (float)(srf_mix64(z) >> 40) * (1.0f / 16777216.0f);
+  const uint32_t k = srf_stream_key(seed, stream);
+  const uint32_t h = srf_mix32(srf_mix32((uint32_t)idx + k) ^ k);
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
 // Keras/TF inverted dropout keeps an element with probability 1 - p.

@@ -29,6 +29,19 @@ def _check_dev(name, t, shape):
         raise ValueError(f'{name} must be contiguous')
 
 
+def _grad_target(p):
+    """Where a backward kernel writes the gradient of parameter p: straight into
+    the model's flat gradient buffer when p is one of its views (then autograd is
+    handed None and adds nothing), else a fresh tensor returned to autograd."""
+    if getattr(p, '_srf_flat', False) and p.grad is not None:
+        return p.grad, True
+    return torch.empty_like(p), False
+
+
+def _returned(target_flags):
+    return [None if inplace else t for t, inplace in target_flags]
+
+
 class RouteGeom:
     """Static geometry of one DR layer (sequence_router_naive.py:146-147)."""
 
@@ -79,6 +92,7 @@ class DynamicRouting(torch.autograd.Function):
                                 ws_bytes, _stream())
         _lib.check(rc, 'srf_route_dr_fwd')
         ctx.geom = g
+        ctx.params = (W, bias)
         ctx.save_for_backward(emb, W, bias, saved)
         return v
 
@@ -89,14 +103,14 @@ class DynamicRouting(torch.autograd.Function):
         g_v = g_v.contiguous()
         L = _lib.lib()
         g_emb = torch.empty_like(emb)
-        g_W = torch.empty_like(W)
-        g_b = torch.empty_like(bias)
+        tW, tb = _grad_target(ctx.params[0]), _grad_target(ctx.params[1])
+        g_W, g_b = tW[0], tb[0]
         ws_bytes = L.srf_route_dr_bwd_workspace(*g.ws_args())
         ws = torch.empty(ws_bytes, device=emb.device, dtype=torch.uint8)
         rc = L.srf_route_dr_bwd(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), _ptr(g_v), _ptr(g_emb),
                                 _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
         _lib.check(rc, 'srf_route_dr_bwd')
-        return g_emb, g_W, g_b, None
+        return (g_emb, *_returned([tW, tb]), None)
 
 
 def dynamic_routing(emb, W, bias, geom):
@@ -136,6 +150,7 @@ class CnnFe(torch.autograd.Function):
                              _ptr(saved), sb, _ptr(ws), wb, _stream())
         _lib.check(rc, 'srf_cnnfe_fwd')
         ctx.meta = (B, T, Fd, float(drop_p) if training else 0.0, int(seed))
+        ctx.params = params
         ctx.save_for_backward(feats, inp_len_i32, saved, *params)
         return out
 
@@ -144,8 +159,8 @@ class CnnFe(torch.autograd.Function):
         feats, inp_len, saved, *params = ctx.saved_tensors
         B, T, Fd, drop_p, seed = ctx.meta
         P = dict(zip(CNNFE_PARAMS, params))
-        grads = [torch.empty_like(p) for p in params]
-        G = dict(zip(CNNFE_PARAMS, grads))
+        targets = [_grad_target(p) for p in ctx.params]
+        G = dict(zip(CNNFE_PARAMS, [t for t, _ in targets]))
         L = _lib.lib()
         wb = L.srf_cnnfe_bwd_workspace(B, T, Fd, 64)
         ws = torch.empty(wb, device=feats.device, dtype=torch.uint8)
@@ -154,7 +169,7 @@ class CnnFe(torch.autograd.Function):
                              _ptr(P['conv1b_kernel']), _ptr(P['bn1_gamma']), drop_p, seed, _ptr(saved), _ptr(g_out),
                              *[_ptr(G[k]) for k in CNNFE_PARAMS], _ptr(ws), wb, _stream())
         _lib.check(rc, 'srf_cnnfe_bwd')
-        return (None, None, None, None, None, None, *grads)
+        return (None, None, None, None, None, None, *_returned(targets))
 
 
 def cnnfe(feats, inp_len_i32, params, moving, training, drop_p, seed):
@@ -185,6 +200,7 @@ class PrimaryCaps(torch.autograd.Function):
                                     float(p_caps), float(p_in), int(seed), _ptr(z), _ptr(saved), sb, _stream())
         _lib.check(rc, 'srf_primary_caps_fwd')
         ctx.meta = (B, T, K, PH, PD, tr, float(p_caps), float(p_in), int(seed))
+        ctx.params = params
         ctx.save_for_backward(X, inp_len_i32, saved, *params)
         return z
 
@@ -195,8 +211,8 @@ class PrimaryCaps(torch.autograd.Function):
         P = dict(zip(CAPS_PARAMS, params))
         L = _lib.lib()
         g_X = torch.empty_like(X)
-        grads = [torch.empty_like(p) for p in params]
-        G = dict(zip(CAPS_PARAMS, grads))
+        targets = [_grad_target(p) for p in ctx.params]
+        G = dict(zip(CAPS_PARAMS, [t for t, _ in targets]))
         wb = L.srf_primary_caps_bwd_workspace(B, T, K, PH, PD)
         ws = torch.empty(wb, device=X.device, dtype=torch.uint8)
         rc = L.srf_primary_caps_bwd(_ptr(X), _ptr(inp_len), B, T, K, PH, PD, _ptr(P['proj_kernel']),
@@ -205,7 +221,7 @@ class PrimaryCaps(torch.autograd.Function):
                                     _ptr(g_z.contiguous()), _ptr(g_X), *[_ptr(G[k]) for k in CAPS_PARAMS], _ptr(ws),
                                     wb, _stream())
         _lib.check(rc, 'srf_primary_caps_bwd')
-        return (g_X, None, None, None, None, None, None, None, *grads)
+        return (g_X, None, None, None, None, None, None, None, *_returned(targets))
 
 
 def primary_caps(X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, params):
@@ -226,6 +242,7 @@ class CapsNorm(torch.autograd.Function):
         _lib.check(L.srf_capsnorm_fwd(_ptr(v), F, n, _ptr(gamma), _ptr(beta), tr, float(p), int(seed), int(layer),
                                       _ptr(y), _ptr(stat), _stream()), 'srf_capsnorm_fwd')
         ctx.meta = (F, n, tr, float(p), int(seed), int(layer))
+        ctx.params = (gamma, beta)
         ctx.save_for_backward(v, gamma, beta, stat)
         return y
 
@@ -234,13 +251,15 @@ class CapsNorm(torch.autograd.Function):
         v, gamma, beta, stat = ctx.saved_tensors
         F, n, tr, p, seed, layer = ctx.meta
         L = _lib.lib()
-        g_v, g_g, g_b = torch.empty_like(v), torch.empty_like(gamma), torch.empty_like(beta)
+        g_v = torch.empty_like(v)
+        targets = [_grad_target(p) for p in ctx.params]
+        g_g, g_b = targets[0][0], targets[1][0]
         wb = L.srf_capsnorm_bwd_workspace(F, n, 0)
         ws = torch.empty(wb, device=v.device, dtype=torch.uint8)
         _lib.check(L.srf_capsnorm_bwd(_ptr(v), F, n, _ptr(gamma), _ptr(beta), tr, p, seed, layer, _ptr(stat),
                                       _ptr(g_y.contiguous()), _ptr(g_v), _ptr(g_g), _ptr(g_b), _ptr(ws), wb,
                                       _stream()), 'srf_capsnorm_bwd')
-        return g_v, g_g, g_b, None, None, None, None
+        return (g_v, *_returned(targets), None, None, None, None)
 
 
 class CapsHead(torch.autograd.Function):
@@ -259,6 +278,7 @@ class CapsHead(torch.autograd.Function):
                                        _ptr(beta_out), tr, float(p), int(seed), int(layer), _ptr(logits), _ptr(stat),
                                        _ptr(lens), _stream()), 'srf_caps_head_fwd')
         ctx.meta = (F, J, D, tr, float(p), int(seed), int(layer))
+        ctx.params = (gamma_mid, beta_mid, gamma_out, beta_out)
         ctx.save_for_backward(v, gamma_mid, beta_mid, gamma_out, beta_out, stat, lens)
         return logits
 
@@ -268,14 +288,15 @@ class CapsHead(torch.autograd.Function):
         F, J, D, tr, p, seed, layer = ctx.meta
         L = _lib.lib()
         g_v = torch.empty_like(v)
-        g_gm, g_bm, g_go, g_bo = (torch.empty_like(t) for t in (gm, bm, go, bo))
+        targets = [_grad_target(p) for p in ctx.params]
+        g_gm, g_bm, g_go, g_bo = (t for t, _ in targets)
         wb = L.srf_capsnorm_bwd_workspace(F, J * D, J)
         ws = torch.empty(wb, device=v.device, dtype=torch.uint8)
         _lib.check(L.srf_caps_head_bwd(_ptr(v), F, J, D, _ptr(gm), _ptr(bm), _ptr(go), tr, p, seed, layer,
                                        _ptr(stat), _ptr(lens), _ptr(g_logits.contiguous()), _ptr(g_v), _ptr(g_gm),
                                        _ptr(g_bm), _ptr(g_go), _ptr(g_bo), _ptr(ws), wb, _stream()),
                    'srf_caps_head_bwd')
-        return g_v, g_gm, g_bm, g_go, g_bo, None, None, None, None
+        return (g_v, *_returned(targets), None, None, None, None)
 
 
 class CtcLoss(torch.autograd.Function):

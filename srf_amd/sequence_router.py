@@ -115,6 +115,7 @@ class SequenceRouter(torch.nn.Module):
                 view.copy_(torch.from_numpy(self._init_value(rng, shape, init)))
             p = torch.nn.Parameter(view)
             p.grad = self.flat_grad[offsets[name]:offsets[name] + n].view(shape)
+            p._srf_flat = True    # backward kernels write this gradient in place (overwrite)
             self.params[name] = p
         self.offsets = offsets
         for k in range(self.cnn_n):

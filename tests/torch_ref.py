@@ -9,24 +9,27 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-M64 = (1 << 64) - 1
 STREAMS = dict(conv0a=0, conv0b=1, conv1a=2, conv1b=3, encaps1=4, encaps2=5, input=6, mid0=7)
+M32 = 0xFFFFFFFF
 
 
-def _mix64(z):
-    z = np.asarray(z, dtype=np.uint64)
-    with np.errstate(over='ignore'):
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return z ^ (z >> np.uint64(31))
+def _mix32(x):
+    x = np.asarray(x, dtype=np.uint64) & np.uint64(M32)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7feb352d)) & np.uint64(M32)
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846ca68b)) & np.uint64(M32)
+    x ^= x >> np.uint64(16)
+    return x
 
 
 def rng_uniform(seed, stream, n):
-    """srf_uniform(seed, stream, idx) for idx in [0, n)."""
-    with np.errstate(over='ignore'):
-        k = _mix64(np.uint64(seed) ^ np.uint64((0x9E3779B97F4A7C15 * (stream + 1)) & M64))
-        z = k + np.arange(n, dtype=np.uint64) * np.uint64(0xD1B54A32D192ED03)
-    return (_mix64(z) >> np.uint64(40)).astype(np.float64) * (1.0 / 16777216.0)
+    """srf_uniform(seed, stream, idx) of srf_rng.h for idx in [0, n)."""
+    seed = int(seed)
+    k = int(_mix32((seed & M32) ^ int(_mix32(((seed >> 32) & M32) ^ ((stream * 0x9E3779B9 + 0x7F4A7C15) & M32)))))
+    idx = np.arange(n, dtype=np.uint64)
+    h = _mix32(_mix32((idx + np.uint64(k)) & np.uint64(M32)) ^ np.uint64(k))
+    return (h >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
 
 
 def dropout_mult(seed, stream, shape, p):
