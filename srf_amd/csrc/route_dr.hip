@@ -123,8 +123,8 @@ template <int DOUT, int TW>
 __device__ __forceinline__ void jreduce(float (&p)[TW]) {
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
-    p[t] += __shfl_xor(p[t], 16, 64);
-    if constexpr (DOUT >= 16) p[t] += __shfl_xor(p[t], 32, 64);
+    p[t] = xor16_sum(p[t]);
+    if constexpr (DOUT >= 16) p[t] = xor32_sum(p[t]);
   }
   if constexpr (DOUT > 16) {
     constexpr int TPJ = DOUT / 16;
@@ -270,12 +270,15 @@ __device__ __forceinline__ void pass_step(Frags<DIN, TW>& fr, PassState<TW>& st,
     }
     if constexpr (DOUT == 8) {
       // lane groups {0,1} and {2,3} hold different capsules: combine
-      const float mo = __shfl_xor(m, 32, 64), zo = __shfl_xor(z, 32, 64), yo = __shfl_xor(y, 32, 64);
-      const float M = fmaxf(m, mo);
-      const float s1 = (m == -INFINITY) ? 0.f : __expf(m - M);
-      const float s2 = (mo == -INFINITY) ? 0.f : __expf(mo - M);
-      z = z * s1 + zo * s2;
-      y = y * s1 + yo * s2;
+      float ma, mb, za, zb, ya, yb;
+      xpair32(m, ma, mb);
+      xpair32(z, za, zb);
+      xpair32(y, ya, yb);
+      const float M = fmaxf(ma, mb);
+      const float s1 = (ma == -INFINITY) ? 0.f : __expf(ma - M);
+      const float s2 = (mb == -INFINITY) ? 0.f : __expf(mb - M);
+      z = za * s1 + zb * s2;
+      y = ya * s1 + yb * s2;
       m = M;
     }
     if (NW > 1) {
@@ -385,25 +388,33 @@ __global__ __launch_bounds__(512) void route_pass_kernel(
 }
 
 // ---------------------------------------------------------------- gu pass
-// gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j with c^r = exp(L^r - logZ^r) and
-// gL^r = c^r (<gs^r_j, u_ij> - sigma^r): only per-(frame,i) scalars are shared
-// across output capsules, so j tiles are independent.  A workgroup = 4 waves
-// (4 x TW row tiles) of one frame tile and i-chunk.  Per i it
-//   * stores gu frame-contiguous, gu_t[i][row][f] (f padded to Fp), for the gW pass;
-//   * contracts gx^T[e][f] = sum_row W[i][row][e] gu[row][f] on the matrix cores
-//     straight from the gu registers, reduces it over the 4 waves in LDS and
-//     scatter-adds it into g_emb through the window adjoint (naive:150-151).
-template <int DIN, int DOUT, int TW, int R>
+// gu_ij = c^0_ij gs^0_j + sum_{r>=1} c^r_ij gs^r_j + gL^r_ij Vc^r_j with
+// c^r = exp(L^r - logZ^r), gL^r = c^r (<gs^r_j, u_ij> - sigma^r).  Vc^0 = 0, so
+// iteration 0 has uniform c^0 = 1/J_eff and no logit term.  Only per-(frame,i)
+// scalars are shared across output capsules, so the waves of a workgroup (one
+// frame tile, TW row tiles each) are independent.  Per input capsule i a wave
+//   * stores gu for the gW pass in 16x16 blocks, gu_t[i][frame tile][row tile][f][row]
+//     (one contiguous 1 KiB float4 store per block);
+//   * contracts gx^T[e][f] = sum_row W^T[i][e][row] gu[row][f] on the matrix cores
+//     straight from the gu registers (float4 loads of the transposed W) and adds
+//     it, through the window adjoint (naive:150-151), into an LDS accumulator of
+//     the workgroup's output frames (ds_add, no barrier per capsule);
+// the accumulator is flushed into g_emb with one atomic add per element at the end.
+// When the accumulator does not fit in LDS (wide windows) the adds go to g_emb.
+template <int DIN, int DOUT, int TW, int R, bool LDSACC>
 __global__ __launch_bounds__(256) void route_gu_kernel(
-    const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ bias, int F, int Fp,
-    int T, int N, int lpad, int in_n, int J, int mask_first, int n_wgroups, int n_chunks, int chunk_len,
-    const float* __restrict__ saved, const float* __restrict__ gs, const float* __restrict__ stats,
-    float* __restrict__ gu_t, float* __restrict__ g_emb) {
+    const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ WT,
+    const float* __restrict__ bias, int F, int Fp, int T, int N, int lpad, int rpad, int in_n, int J,
+    int mask_first, int n_wgroups, int n_chunks, int chunk_len, const float* __restrict__ saved,
+    const float* __restrict__ gs, const float* __restrict__ stats, float* __restrict__ gu_t,
+    float* __restrict__ g_emb) {
   constexpr int NCT = (DIN + 15) / 16;
-  __shared__ __attribute__((aligned(16))) float red[2][4][16 * DIN];
+  constexpr int RV = R > 1 ? R - 1 : 1;
+  extern __shared__ __attribute__((aligned(16))) float gacc[];
   const int JD = J * DOUT;
   const int NT = (JD + 15) / 16;
   const size_t FJD = (size_t)F * JD;
+  const int NW = blockDim.x >> 6;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fl = lane & 15, g = lane >> 4;
   const int chunk = blockIdx.x % n_chunks;
@@ -412,116 +423,142 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
   const int ft = rest / n_wgroups;
   const int f = ft * 16 + fl;
   const FrameLoc loc = frame_loc(f, F, T);
-  const int tbase = (wgrp * 4 + wv) * TW;
+  const int tbase = __builtin_amdgcn_readfirstlane((wgrp * NW + wv) * TW);
   const int i0 = chunk * chunk_len, i1 = min(in_n, i0 + chunk_len);
+  const int Jeff = J - (mask_first ? 1 : 0);
+  const int ND = N * DIN;
+  const int SROW = ND + 1;                       // LDS frame-slot stride (odd: spreads banks)
+  const int nslots = 16 + lpad + rpad;
 
-  float vcr[R][TW][4], gsr[R][TW][4];
+  if constexpr (LDSACC) {
+    for (int k = threadIdx.x; k < nslots * SROW; k += blockDim.x) gacc[k] = 0.f;
+    __syncthreads();
+  }
+
+  float vcr[RV][TW][4], gsr[R][TW][4];
+  float c0[TW];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
+  for (int t = 0; t < TW; ++t) {
+    const int j = tile_j<DOUT>(tbase + t, g);
+    c0[t] = (j < J && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
 #pragma unroll
-    for (int t = 0; t < TW; ++t) {
-      // Vc^r (r >= 1) is stored after iteration r-1 at saved[(r-1)*2+1]
-      if (r > 0) {
-        load_rows(saved + (size_t)(2 * (r - 1) + 1) * FJD, f, loc.valid, JD, tbase + t, g, vcr[r][t]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) vcr[r][t][k] = 0.f;
-      }
+    for (int r = 0; r < R; ++r) {
+      if (r > 0) load_rows(saved + (size_t)(2 * (r - 1) + 1) * FJD, f, loc.valid, JD, tbase + t, g, vcr[r - 1][t]);
       load_rows(gs + (size_t)r * FJD, f, loc.valid, JD, tbase + t, g, gsr[r][t]);
     }
   }
 
-  int parity = 0;
-  for (int i = i0; i < i1; ++i) {
-    float x[DIN / 4];
-    load_x<DIN>(emb, loc, T, N, lpad, i, g, x);
-    float u[TW][4], ga[TW][4];
+  if (i0 < i1) {
+    Frags<DIN, TW> fr;
+    fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, i0, JD, NT, tbase, lane, fr);
+    for (int i = i0; i < i1; ++i) {
+      // transposed W rows for the gx contraction and this capsule's softmax stats
+      f4 wt[NCT][TW];
 #pragma unroll
-    for (int t = 0; t < TW; ++t) {
-      const f4 v = pose_tile<DIN>(W, bias, i, JD, NT, tbase + t, lane, x);
-      u[t][0] = v.x; u[t][1] = v.y; u[t][2] = v.z; u[t][3] = v.w;
+      for (int ct = 0; ct < NCT; ++ct) {
+        const int e = min(ct * 16 + fl, DIN - 1);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) ga[t][k] = 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float p[TW], q[TW];
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        float s = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          s += u[t][k] * vcr[r][t][k];
-          s2 += u[t][k] * gsr[r][t][k];
+        for (int t = 0; t < TW; ++t) {
+          const int tc = min(tbase + t, NT - 1);
+          wt[ct][t] = ld4(WT + ((size_t)i * DIN + e) * JD + min(tc * 16 + 4 * g, JD - 4));
         }
-        p[t] = s;
-        q[t] = s2;
       }
-      if (r > 0) jreduce<DOUT, TW>(p);
-      jreduce<DOUT, TW>(q);
-      const size_t si = (((size_t)r * F + (loc.valid ? f : 0)) * in_n + i) * 2;
-      const float logz = loc.valid ? stats[si] : 0.f;
-      const float sigma = loc.valid ? stats[si + 1] : 0.f;
+      float logz[RV], sig[RV];
 #pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        const int j = tile_j<DOUT>(tbase + t, g);
-        const bool valid = j < J && !(mask_first && j == 0);
-        const float c = valid ? __expf(p[t] - logz) : 0.f;
-        const float gl = c * (q[t] - sigma);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ga[t][k] += c * gsr[r][t][k] + gl * vcr[r][t][k];
+      for (int r = 1; r < R; ++r) {
+        const f2 st = *reinterpret_cast<const f2*>(stats + (((size_t)(r - 1) * F + (loc.valid ? f : 0)) * in_n + i) * 2);
+        logz[r - 1] = st.x;
+        sig[r - 1] = st.y;
       }
-    }
-    // gu, frame-contiguous (rows past JD are skipped; frames past F carry 0)
+      float u[TW][4];
+      pose_tiles<DIN, TW>(fr, u);
+      fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, min(i + 1, i1 - 1), JD, NT, tbase, lane, fr);
+      float ga[TW][4];
 #pragma unroll
-    for (int t = 0; t < TW; ++t) {
+      for (int t = 0; t < TW; ++t)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int row = (tbase + t) * 16 + 4 * g + k;
-        if (row < JD) gu_t[((size_t)i * JD + row) * Fp + f] = ga[t][k];
+        for (int k = 0; k < 4; ++k) ga[t][k] = c0[t] * gsr[0][t][k];
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        float p[TW], q[TW];
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          float s = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            s += u[t][k] * vcr[r - 1][t][k];
+            s2 += u[t][k] * gsr[r][t][k];
+          }
+          p[t] = s;
+          q[t] = s2;
+        }
+        jreduce<DOUT, TW>(p);
+        jreduce<DOUT, TW>(q);
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          const float c = c0[t] != 0.f ? __expf(p[t] - logz[r - 1]) : 0.f;
+          const float gl = c * (q[t] - sig[r - 1]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ga[t][k] += c * gsr[r][t][k] + gl * vcr[r - 1][t][k];
+        }
       }
-    }
-    // gx^T[e][f] over this wave's rows (rows past JD carry ga == 0)
-    f4 gx[NCT];
+      // gu blocks (rows past JD and frames past F carry 0)
+      {
+        float* blk = gu_t + (((size_t)i * (Fp >> 4) + ft) * NT) * 256 + fl * 16 + 4 * g;
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) gx[ct] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < TW; ++t)
+          if (tbase + t < NT) st4(blk + (tbase + t) * 256, f4{ga[t][0], ga[t][1], ga[t][2], ga[t][3]});
+      }
+      // gx^T[e][f] over this wave's rows (rows past JD carry ga == 0)
+      f4 gx[NCT];
 #pragma unroll
-    for (int t = 0; t < TW; ++t) {
+      for (int ct = 0; ct < NCT; ++ct) {
+        gx[ct] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int row = min(min(tbase + t, NT - 1) * 16 + 4 * g + k, JD - 1);
+        for (int t = 0; t < TW; ++t)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) gx[ct] = mfma16x16x4(wt[ct][t][k], ga[t][k], gx[ct]);
+      }
+      const int w = i / N, n = i - w * N;
+      const int ts = loc.t + w - lpad;
+      if (loc.valid && ts >= 0 && ts < T) {
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) {
-          const int e = min(ct * 16 + fl, DIN - 1);
-          gx[ct] = mfma16x16x4(W[((size_t)i * JD + row) * DIN + e], ga[t][k], gx[ct]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int e = ct * 16 + 4 * g + k;
+            if (e < DIN) {
+              if constexpr (LDSACC)
+                atomicAdd(gacc + (fl + w) * SROW + n * DIN + e, gx[ct][k]);
+              else
+                atomicAdd(g_emb + ((size_t)(f + w - lpad) * N + n) * DIN + e, gx[ct][k]);
+            }
+          }
         }
       }
     }
-    float* buf = &red[parity][0][0];
-#pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = ct * 16 + 4 * g + k;
-        if (e < DIN) buf[wv * 16 * DIN + fl * DIN + e] = gx[ct][k];
-      }
-    }
-    __syncthreads();
-    {
-      const int w = i / N, n = i - w * N;
-      for (int idx = threadIdx.x; idx < 16 * DIN; idx += 256) {
-        const float sum = buf[idx] + buf[16 * DIN + idx] + buf[32 * DIN + idx] + buf[48 * DIN + idx];
-        const int flo = idx / DIN, e = idx - flo * DIN;
-        const int fo = ft * 16 + flo;
-        if (fo < F) {
-          const int bo = fo / T, to = fo - bo * T;
-          const int ts = to + w - lpad;
-          if (ts >= 0 && ts < T) atomicAdd(g_emb + ((size_t)(bo * T + ts) * N + n) * DIN + e, sum);
-        }
-      }
-    }
-    parity ^= 1;
   }
+  if constexpr (LDSACC) {
+    __syncthreads();
+    const int f0 = ft * 16 - lpad;
+    for (int k = threadIdx.x; k < nslots * ND; k += blockDim.x) {
+      const int slot = k / ND, rem = k - slot * ND;
+      const int fo = f0 + slot;
+      const float v = gacc[slot * SROW + rem];
+      if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + (size_t)fo * ND + rem, v);
+    }
+  }
+}
+
+// W [in_n][JD][din] -> WT [in_n][din][JD] (A operand of the gx contraction).
+__global__ void transpose_w_kernel(const float* __restrict__ W, int in_n, int JD, int din, float* __restrict__ WT) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)in_n * JD * din) return;
+  const int row = idx % JD;
+  const size_t rest = idx / JD;
+  const int e = rest % din;
+  const size_t i = rest / din;
+  WT[idx] = W[(i * JD + row) * din + e];
 }
 
 // Windowed input, transposed and frame-padded: xT[i][e][f] (f < Fp), the B
@@ -544,22 +581,24 @@ __global__ void window_xt_kernel(const float* __restrict__ emb, int F, int Fp, i
 }
 
 // ---------------------------------------------------------------- gW, gbias
-// gW[i][row][e] = sum_f gu[i][row][f] x[f][i][e]  (MFMA, K = frames, float4
-// loads of both frame-contiguous operands); gbias[i][row] = sum_f gu[i][row][f].
-// One wave per (i, row tile).
+// gW[i][row][e] = sum_f gu[i][row][f] x[f][i][e]  (MFMA, K = frames) and
+// gbias[i][row] = sum_f gu[i][row][f].  One wave per (i, row tile); per frame
+// tile it reads one 1 KiB gu block (4 dword loads per lane, frames 4g..4g+3)
+// and float4 frame runs of the transposed window xT.
 template <int DIN>
 __global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__ gu_t,
                                                        const float* __restrict__ xT, int Fp, int in_n, int JD,
                                                        float* __restrict__ gW, float* __restrict__ gbias) {
   constexpr int NCT = (DIN + 15) / 16;
   const int NT = (JD + 15) / 16;
+  const int NFT = Fp >> 4;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, l16 = lane & 15;
   const int task = blockIdx.x * 4 + wv;
   if (task >= in_n * NT) return;
   const int i = task / NT, tg = task - i * NT;
-  const int arow = tg * 16 + l16;
-  const float* ap = gu_t + ((size_t)i * JD + min(arow, JD - 1)) * Fp + 4 * g;
+  const float* ap = gu_t + ((size_t)i * NFT * NT + tg) * 256 + (4 * g) * 16 + l16;
+  const size_t astride = (size_t)NT * 256;   // next frame tile
   const float* bp[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) bp[ct] = xT + ((size_t)i * DIN + min(ct * 16 + l16, DIN - 1)) * Fp + 4 * g;
@@ -567,21 +606,41 @@ __global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) acc[ct][0] = acc[ct][1] = f4{0.f, 0.f, 0.f, 0.f};
   float gb = 0.f;
-#pragma unroll 2
-  for (int s = 0; s < Fp; s += 16) {
-    const f4 a = ld4(ap + s);
+  auto step = [&](const f4& a, const f4 (&b)[NCT]) {
     gb += (a.x + a.y) + (a.z + a.w);
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
-      const f4 b = ld4(bp[ct] + s);
-      acc[ct][0] = mfma16x16x4(a.x, b.x, acc[ct][0]);
-      acc[ct][1] = mfma16x16x4(a.y, b.y, acc[ct][1]);
-      acc[ct][0] = mfma16x16x4(a.z, b.z, acc[ct][0]);
-      acc[ct][1] = mfma16x16x4(a.w, b.w, acc[ct][1]);
+      acc[ct][0] = mfma16x16x4(a.x, b[ct].x, acc[ct][0]);
+      acc[ct][1] = mfma16x16x4(a.y, b[ct].y, acc[ct][1]);
+      acc[ct][0] = mfma16x16x4(a.z, b[ct].z, acc[ct][0]);
+      acc[ct][1] = mfma16x16x4(a.w, b[ct].w, acc[ct][1]);
     }
+  };
+  auto load_a = [&](int ft) {
+    const float* q = ap + (size_t)ft * astride;
+    return f4{q[0], q[16], q[32], q[48]};
+  };
+  int ft = 0;
+  // 4 frame tiles per trip: all loads issue before the MFMAs
+  for (; ft + 4 <= NFT; ft += 4) {
+    f4 a[4], b[4][NCT];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = load_a(ft + q);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) b[q][ct] = ld4(bp[ct] + (ft + q) * 16);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) step(a[q], b[q]);
   }
-  gb += __shfl_xor(gb, 16, 64);
-  gb += __shfl_xor(gb, 32, 64);
+  for (; ft < NFT; ++ft) {
+    f4 b[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) b[ct] = ld4(bp[ct] + ft * 16);
+    step(load_a(ft), b);
+  }
+  gb = xor32_sum(xor16_sum(gb));
+  const int arow = tg * 16 + l16;
   if (g == 0 && arow < JD) gbias[(size_t)i * JD + arow] = gb;
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {
@@ -762,31 +821,61 @@ void launch_bwd_finish(const Geom& g, const float* slab, int n_chunks, const flo
                      a_init, A, s, gs);
 }
 
-constexpr int kGuTW = 4;  // row tiles per wave in the gu pass
+constexpr int kGuTW = 2;  // row tiles per wave in the gu pass
+constexpr int kGuNW = 4;  // waves per gu workgroup
 
-inline int gu_wgroups(const Geom& g) { return (g.NT() + 4 * kGuTW - 1) / (4 * kGuTW); }
+inline int gu_wgroups(const Geom& g) { return (g.NT() + kGuNW * kGuTW - 1) / (kGuNW * kGuTW); }
 inline int padded_frames(const Geom& g) { return (g.F() + 15) / 16 * 16; }
+inline size_t gu_lds_bytes(const Geom& g) {
+  return (size_t)(16 + g.lpad + g.rpad) * (g.N * g.din + 1) * sizeof(float);
+}
+constexpr size_t kGuLdsMax = 64 * 1024;
+
+// i-chunks of the gu pass: fill ~4 workgroups per CU, then fewest capsules per workgroup.
+int gu_chunks(const Geom& g) {
+  const int base = (g.F() + 15) / 16 * gu_wgroups(g);
+  const int slots = 256 * 4;
+  int best = 1;
+  double best_cost = 1e30;
+  for (int c = 1; c <= std::min(g.in_n(), 64); ++c) {
+    const int rounds = (base * c + slots - 1) / slots;
+    const double cost = (double)rounds * ((g.in_n() + c - 1) / c + 4);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
+}
 
 template <int D, int R>
-void launch_gu(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias, const float* saved,
-               const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
+void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
+               const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
   const int n_ftiles = (g.F() + 15) / 16;
   const int n_wgroups = gu_wgroups(g);
+  const int n_chunks = gu_chunks(g);
   const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
-  hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R>), dim3(n_ftiles * n_wgroups * n_chunks), dim3(256), 0, st, emb,
-                     W, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups,
-                     n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb);
+  const int nw = std::min(kGuNW, (g.NT() + kGuTW - 1) / kGuTW);
+  const size_t lds = gu_lds_bytes(g);
+  if (lds <= kGuLdsMax)
+    hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R, true>), dim3(n_ftiles * n_wgroups * n_chunks),
+                       dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb);
+  else
+    hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R, false>), dim3(n_ftiles * n_wgroups * n_chunks),
+                       dim3(64 * nw), 0, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb);
 }
 
 template <int D>
-void launch_gu_r(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias,
+void launch_gu_r(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
                  const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
   switch (g.iters) {
-    case 1: launch_gu<D, 1>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    case 2: launch_gu<D, 2>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    case 3: launch_gu<D, 3>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    case 4: launch_gu<D, 4>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    default: launch_gu<D, 5>(g, n_chunks, emb, W, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 1: launch_gu<D, 1>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 2: launch_gu<D, 2>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 3: launch_gu<D, 3>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 4: launch_gu<D, 4>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    default: launch_gu<D, 5>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
   }
 }
 
@@ -814,7 +903,7 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
 }
 
 struct BwdWs {
-  float *A, *gs, *slab, *stats, *gu_t, *xT;
+  float *A, *gs, *slab, *stats, *gu_t, *xT, *WT;
   size_t bytes;
 };
 
@@ -827,8 +916,8 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
     return o;
   };
   const size_t oA = take(F * JD), ogs = take((size_t)g.iters * F * JD), oslab = take((size_t)n_chunks * F * JD),
-               ostats = take((size_t)g.iters * F * in_n * 2), ogu = take(in_n * JD * Fp),
-               oxt = take(in_n * g.din * Fp);
+               ostats = take((size_t)(g.iters - 1) * F * in_n * 2), ogu = take(in_n * (size_t)g.NT() * 16 * Fp),
+               oxt = take(in_n * g.din * Fp), owt = take(in_n * JD * g.din);
   char* b = static_cast<char*>(base);
   BwdWs w;
   w.A = (float*)(b + oA);
@@ -837,6 +926,7 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   w.stats = (float*)(b + ostats);
   w.gu_t = (float*)(b + ogu);
   w.xT = (float*)(b + oxt);
+  w.WT = (float*)(b + owt);
   w.bytes = off;
   return w;
 }
@@ -854,21 +944,26 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   launch_bwd_finish<D>(g, nullptr, n_chunks, g_v, w.A, saved + (size_t)(2 * (R - 1)) * FJD,
                        w.gs + (size_t)(R - 1) * FJD, st);
   SRF_LAUNCH_CHECK("bwd_finish");
-  for (int r = R - 1; r >= 0; --r) {
-    const float* vc = r > 0 ? saved + (size_t)(2 * (r - 1) + 1) * FJD : nullptr;
-    float* stats_r = w.stats + (size_t)r * g.F() * g.in_n() * 2;
-    dispatch_pass<D, MODE_BWD>(g, pc, n_chunks, emb, W, bias, r, vc, w.gs + (size_t)r * FJD, w.slab, stats_r,
-                               r > 0 ? 1 : 0, st);
+  // Iteration 0 needs no backward pass: Vc^0 = 0, so its couplings are uniform
+  // and its logits carry no gradient.
+  for (int r = R - 1; r >= 1; --r) {
+    const float* vc = saved + (size_t)(2 * (r - 1) + 1) * FJD;
+    float* stats_r = w.stats + (size_t)(r - 1) * g.F() * g.in_n() * 2;
+    dispatch_pass<D, MODE_BWD>(g, pc, n_chunks, emb, W, bias, r, vc, w.gs + (size_t)r * FJD, w.slab, stats_r, 1, st);
     SRF_LAUNCH_CHECK("route_pass(bwd)");
-    if (r > 0) {
-      launch_bwd_finish<D>(g, w.slab, n_chunks, nullptr, w.A, saved + (size_t)(2 * (r - 1)) * FJD,
-                           w.gs + (size_t)(r - 1) * FJD, st);
-      SRF_LAUNCH_CHECK("bwd_finish");
-    }
+    launch_bwd_finish<D>(g, w.slab, n_chunks, nullptr, w.A, saved + (size_t)(2 * (r - 1)) * FJD,
+                         w.gs + (size_t)(r - 1) * FJD, st);
+    SRF_LAUNCH_CHECK("bwd_finish");
+  }
+  {
+    const size_t total = (size_t)g.in_n() * g.JD() * g.din;
+    hipLaunchKernelGGL(transpose_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, g.in_n(), g.JD(), g.din,
+                       w.WT);
+    SRF_LAUNCH_CHECK("transpose_w");
   }
   // g_emb is accumulated by the gu pass (window adjoint folded into its scatter-add)
   SRF_HIP_TRY(hipMemsetAsync(g_emb, 0, (size_t)g.F() * g.N * g.din * sizeof(float), st));
-  launch_gu_r<D>(g, n_chunks, emb, W, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
+  launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");
   {
     const size_t total = (size_t)g.in_n() * g.din * Fp;

@@ -50,6 +50,31 @@ __device__ __forceinline__ f4 mfma16x16x4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Cross-row exchanges on the VALU (gfx950 v_permlane16/32_swap, no LDS round trip).
+// Both lanes of an exchanged pair receive the two values in the same order, so
+// symmetric combinations (sum, max) are bit-identical across the pair.
+__device__ __forceinline__ void xpair16(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void xpair32(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+// v + v of lane ^ 16 / lane ^ 32
+__device__ __forceinline__ float xor16_sum(float v) {
+  float a, b;
+  xpair16(v, a, b);
+  return a + b;
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  float a, b;
+  xpair32(v, a, b);
+  return a + b;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
