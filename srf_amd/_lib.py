@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libsrf.so')
+LIB_PATH = os.environ.get('SRF_LIB_PATH') or os.path.join(_HERE, 'libsrf.so')   # override: A/B builds
 
 _c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
 

@@ -17,6 +17,7 @@
 // Layouts (HBM, fp32): emb [F=B*T][N][Din]; W [in_n][J*Dout][Din] (row = j*Dout+d);
 // bias [in_n][J*Dout]; per-frame vectors [F][J*Dout].
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 
 #include "srf_common.h"
@@ -25,6 +26,7 @@
 namespace {
 
 constexpr float kSquashEps = 1e-7f;  // naive:248
+__constant__ int g_dbg = 0;   // experiment knobs (bitmask), 0 in production
 
 // Opt-in profiling hook (srf_route_dr_set_timing_events): events recorded on the
 // launch stream around each forward routing-pass kernel of the next
@@ -402,12 +404,12 @@ __global__ __launch_bounds__(512) void route_pass_kernel(
 // the accumulator is flushed into g_emb with one atomic add per element at the end.
 // When the accumulator does not fit in LDS (wide windows) the adds go to g_emb.
 template <int DIN, int DOUT, int TW, int R, bool LDSACC>
-__global__ __launch_bounds__(256) void route_gu_kernel(
+__global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
     const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ WT,
     const float* __restrict__ bias, int F, int Fp, int T, int N, int lpad, int rpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int chunk_len, const float* __restrict__ saved,
     const float* __restrict__ gs, const float* __restrict__ stats, float* __restrict__ gu_t,
-    float* __restrict__ g_emb) {
+    float* __restrict__ g_emb, int nslots_max) {
   constexpr int NCT = (DIN + 15) / 16;
   constexpr int RV = R > 1 ? R - 1 : 1;
   extern __shared__ __attribute__((aligned(16))) float gacc[];
@@ -427,11 +429,15 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
   const int i0 = chunk * chunk_len, i1 = min(in_n, i0 + chunk_len);
   const int Jeff = J - (mask_first ? 1 : 0);
   const int ND = N * DIN;
-  const int SROW = ND + 1;                       // LDS frame-slot stride (odd: spreads banks)
-  const int nslots = 16 + lpad + rpad;
+  // Per-wave gx accumulators (no LDS atomics): frame slot s <-> emb frame
+  // ft*16 - lpad + w_lo + s; the stride ND + 4 keeps float4 rows bank-conflict free.
+  const int SROW = ND + 4;
+  const int w_lo = i0 / N;
+  const int nslots = 16 + (max(i1 - 1, i0) / N - w_lo);
+  float* gw_acc = gacc + (size_t)wv * nslots_max * SROW;
 
   if constexpr (LDSACC) {
-    for (int k = threadIdx.x; k < nslots * SROW; k += blockDim.x) gacc[k] = 0.f;
+    for (int k = threadIdx.x; k < NW * nslots_max * SROW; k += blockDim.x) gacc[k] = 0.f;
     __syncthreads();
   }
 
@@ -448,31 +454,37 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
     }
   }
 
+  // transposed W rows for the gx contraction and the softmax stats of capsule i
+  auto fetch_side = [&](int i, f4 (&wt)[NCT][TW], float (&logz)[RV], float (&sig)[RV]) {
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const int e = min(ct * 16 + fl, DIN - 1);
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const int tc = min(tbase + t, NT - 1);
+        wt[ct][t] = ld4(WT + ((size_t)i * DIN + e) * JD + min(tc * 16 + 4 * g, JD - 4));
+      }
+    }
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      const f2 st = *reinterpret_cast<const f2*>(stats + (((size_t)(r - 1) * F + (loc.valid ? f : 0)) * in_n + i) * 2);
+      logz[r - 1] = st.x;
+      sig[r - 1] = st.y;
+    }
+  };
+
   if (i0 < i1) {
     Frags<DIN, TW> fr;
+    f4 wt[NCT][TW];
+    float logz[RV], sig[RV];
     fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, i0, JD, NT, tbase, lane, fr);
     for (int i = i0; i < i1; ++i) {
-      // transposed W rows for the gx contraction and this capsule's softmax stats
-      f4 wt[NCT][TW];
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) {
-        const int e = min(ct * 16 + fl, DIN - 1);
-#pragma unroll
-        for (int t = 0; t < TW; ++t) {
-          const int tc = min(tbase + t, NT - 1);
-          wt[ct][t] = ld4(WT + ((size_t)i * DIN + e) * JD + min(tc * 16 + 4 * g, JD - 4));
-        }
-      }
-      float logz[RV], sig[RV];
-#pragma unroll
-      for (int r = 1; r < R; ++r) {
-        const f2 st = *reinterpret_cast<const f2*>(stats + (((size_t)(r - 1) * F + (loc.valid ? f : 0)) * in_n + i) * 2);
-        logz[r - 1] = st.x;
-        sig[r - 1] = st.y;
-      }
+      fetch_side(i, wt, logz, sig);
       float u[TW][4];
       pose_tiles<DIN, TW>(fr, u);
-      fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, min(i + 1, i1 - 1), JD, NT, tbase, lane, fr);
+      // operands of capsule i+1 are fetched now and land while capsule i is processed
+      const int inext = min(i + 1, i1 - 1);
+      fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
       float ga[TW][4];
 #pragma unroll
       for (int t = 0; t < TW; ++t)
@@ -480,6 +492,13 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
         for (int k = 0; k < 4; ++k) ga[t][k] = c0[t] * gsr[0][t][k];
 #pragma unroll
       for (int r = 1; r < R; ++r) {
+        if (g_dbg & 8) {
+#pragma unroll
+          for (int t = 0; t < TW; ++t)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ga[t][k] += u[t][k];
+          continue;
+        }
         float p[TW], q[TW];
 #pragma unroll
         for (int t = 0; t < TW; ++t) {
@@ -507,9 +526,10 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
         float* blk = gu_t + (((size_t)i * (Fp >> 4) + ft) * NT) * 256 + fl * 16 + 4 * g;
 #pragma unroll
         for (int t = 0; t < TW; ++t)
-          if (tbase + t < NT) st4(blk + (tbase + t) * 256, f4{ga[t][0], ga[t][1], ga[t][2], ga[t][3]});
+          if (tbase + t < NT && !(g_dbg & 1)) st4(blk + (tbase + t) * 256, f4{ga[t][0], ga[t][1], ga[t][2], ga[t][3]});
       }
       // gx^T[e][f] over this wave's rows (rows past JD carry ga == 0)
+      if (g_dbg & 4) continue;
       f4 gx[NCT];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
@@ -521,18 +541,17 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
       }
       const int w = i / N, n = i - w * N;
       const int ts = loc.t + w - lpad;
-      if (loc.valid && ts >= 0 && ts < T) {
+      if (loc.valid && ts >= 0 && ts < T && !(g_dbg & 2)) {
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) {
+          if (ct * 16 + 4 * g >= DIN) continue;
+          if constexpr (LDSACC) {
+            float* a = gw_acc + (fl + w - w_lo) * SROW + n * DIN + ct * 16 + 4 * g;
+            st4(a, ld4(a) + gx[ct]);
+          } else {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int e = ct * 16 + 4 * g + k;
-            if (e < DIN) {
-              if constexpr (LDSACC)
-                atomicAdd(gacc + (fl + w) * SROW + n * DIN + e, gx[ct][k]);
-              else
-                atomicAdd(g_emb + ((size_t)(f + w - lpad) * N + n) * DIN + e, gx[ct][k]);
-            }
+            for (int k = 0; k < 4; ++k)
+              atomicAdd(g_emb + ((size_t)(f + w - lpad) * N + n) * DIN + ct * 16 + 4 * g + k, gx[ct][k]);
           }
         }
       }
@@ -540,11 +559,12 @@ __global__ __launch_bounds__(256) void route_gu_kernel(
   }
   if constexpr (LDSACC) {
     __syncthreads();
-    const int f0 = ft * 16 - lpad;
+    const int f0 = ft * 16 - lpad + w_lo;
     for (int k = threadIdx.x; k < nslots * ND; k += blockDim.x) {
       const int slot = k / ND, rem = k - slot * ND;
       const int fo = f0 + slot;
-      const float v = gacc[slot * SROW + rem];
+      float v = 0.f;
+      for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots_max + slot) * SROW + rem];
       if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + (size_t)fo * ND + rem, v);
     }
   }
@@ -826,8 +846,17 @@ constexpr int kGuNW = 4;  // waves per gu workgroup
 
 inline int gu_wgroups(const Geom& g) { return (g.NT() + kGuNW * kGuTW - 1) / (kGuNW * kGuTW); }
 inline int padded_frames(const Geom& g) { return (g.F() + 15) / 16 * 16; }
-inline size_t gu_lds_bytes(const Geom& g) {
-  return (size_t)(16 + g.lpad + g.rpad) * (g.N * g.din + 1) * sizeof(float);
+// Frame slots of the widest i-chunk's gx accumulator (16 + its window-offset span).
+inline int gu_nslots(const Geom& g, int chunk_len) {
+  int span = 0;
+  for (int i0 = 0; i0 < g.in_n(); i0 += chunk_len) {
+    const int i1 = std::min(g.in_n(), i0 + chunk_len);
+    span = std::max(span, (i1 - 1) / g.N - i0 / g.N);
+  }
+  return 16 + span;
+}
+inline size_t gu_lds_bytes(const Geom& g, int nw, int nslots) {
+  return (size_t)nw * nslots * (g.N * g.din + 4) * sizeof(float);
 }
 constexpr size_t kGuLdsMax = 64 * 1024;
 
@@ -856,15 +885,18 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
   const int n_chunks = gu_chunks(g);
   const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
   const int nw = std::min(kGuNW, (g.NT() + kGuTW - 1) / kGuTW);
-  const size_t lds = gu_lds_bytes(g);
+  const int nslots = gu_nslots(g, chunk_len);
+  const size_t lds = gu_lds_bytes(g, nw, nslots);
+  static int dbg = getenv("SRF_DBG") ? atoi(getenv("SRF_DBG")) : 0;
+  if (dbg) hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, st);
   if (lds <= kGuLdsMax)
     hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R, true>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
-                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb);
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb, nslots);
   else
     hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R, false>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), 0, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
-                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb);
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb, nslots);
 }
 
 template <int D>
