@@ -17,7 +17,6 @@
 // Layouts (HBM, fp32): emb [F=B*T][N][Din]; W [in_n][J*Dout][Din] (row = j*Dout+d);
 // bias [in_n][J*Dout]; per-frame vectors [F][J*Dout].
 #include <algorithm>
-#include <cstdlib>
 #include <cmath>
 
 #include "srf_common.h"
@@ -26,7 +25,6 @@
 namespace {
 
 constexpr float kSquashEps = 1e-7f;  // naive:248
-__constant__ int g_dbg = 0;   // experiment knobs (bitmask), 0 in production
 
 // Opt-in profiling hook (srf_route_dr_set_timing_events): events recorded on the
 // launch stream around each forward routing-pass kernel of the next
@@ -492,13 +490,6 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
         for (int k = 0; k < 4; ++k) ga[t][k] = c0[t] * gsr[0][t][k];
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        if (g_dbg & 8) {
-#pragma unroll
-          for (int t = 0; t < TW; ++t)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ga[t][k] += u[t][k];
-          continue;
-        }
         float p[TW], q[TW];
 #pragma unroll
         for (int t = 0; t < TW; ++t) {
@@ -526,10 +517,9 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
         float* blk = gu_t + (((size_t)i * (Fp >> 4) + ft) * NT) * 256 + fl * 16 + 4 * g;
 #pragma unroll
         for (int t = 0; t < TW; ++t)
-          if (tbase + t < NT && !(g_dbg & 1)) st4(blk + (tbase + t) * 256, f4{ga[t][0], ga[t][1], ga[t][2], ga[t][3]});
+          if (tbase + t < NT) st4(blk + (tbase + t) * 256, f4{ga[t][0], ga[t][1], ga[t][2], ga[t][3]});
       }
       // gx^T[e][f] over this wave's rows (rows past JD carry ga == 0)
-      if (g_dbg & 4) continue;
       f4 gx[NCT];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
@@ -541,7 +531,7 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
       }
       const int w = i / N, n = i - w * N;
       const int ts = loc.t + w - lpad;
-      if (loc.valid && ts >= 0 && ts < T && !(g_dbg & 2)) {
+      if (loc.valid && ts >= 0 && ts < T) {
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) {
           if (ct * 16 + 4 * g >= DIN) continue;
@@ -677,82 +667,67 @@ __global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------- finish kernels
+// One thread per float4 of a capsule (Q = DOUT/4 adjacent lanes per capsule);
+// squash norms are reduced across the Q lanes.
+template <int Q>
+__device__ __forceinline__ float qsum(float v) {
+#pragma unroll
+  for (int o = 1; o < Q; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ f4 sum_slab4(const float* __restrict__ slab, int n, size_t FJD, size_t off) {
+  f4 a = ld4(slab + off);
+#pragma unroll 4
+  for (int c = 1; c < n; ++c) a += ld4(slab + (size_t)c * FJD + off);
+  return a;
+}
+
 // s^r = sum over i-chunks; v^r = squash(s^r) (naive:204); Vc^{r+1} = Vc^r + v^r.
 template <int DOUT>
-__global__ void fwd_finish_kernel(const float* __restrict__ slab, int n_chunks, int F, int J,
+__global__ void fwd_finish_kernel(const float* __restrict__ slab, int n_chunks, size_t FJD,
                                   const float* __restrict__ vc_in, float* __restrict__ s_out,
                                   float* __restrict__ vc_out, float* __restrict__ v_out) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= F * J) return;
-  const size_t JD = (size_t)J * DOUT;
-  const size_t base = (size_t)idx * DOUT;  // = f*JD + j*DOUT
-  const size_t FJD = (size_t)F * JD;
-  float s[DOUT];
-#pragma unroll
-  for (int d = 0; d < DOUT; d += 4) {
-    f4 a = ld4(slab + base + d);
-    for (int c = 1; c < n_chunks; ++c) a += ld4(slab + (size_t)c * FJD + base + d);
-    s[d] = a.x; s[d + 1] = a.y; s[d + 2] = a.z; s[d + 3] = a.w;
-  }
-  float n2 = 0.f;
-#pragma unroll
-  for (int d = 0; d < DOUT; ++d) n2 += s[d] * s[d];
+  constexpr int Q = DOUT / 4;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // float4 index; FJD/4 % Q == 0
+  const bool ok = idx < FJD / 4;
+  const size_t off = (ok ? idx : 0) * 4;
+  const f4 sv = sum_slab4(slab, n_chunks, FJD, off);
+  const float n2 = qsum<Q>((sv.x * sv.x + sv.y * sv.y) + (sv.z * sv.z + sv.w * sv.w));
+  if (!ok) return;
   const float fac = n2 / (1.f + n2) / sqrtf(n2 + kSquashEps);
-#pragma unroll
-  for (int d = 0; d < DOUT; d += 4) {
-    const f4 sv = {s[d], s[d + 1], s[d + 2], s[d + 3]};
-    const f4 v = sv * fac;
-    st4(s_out + base + d, sv);
-    f4 vc = v;
-    if (vc_in) vc += ld4(vc_in + base + d);
-    st4(vc_out + base + d, vc);
-    if (v_out) st4(v_out + base + d, v);
-  }
+  const f4 v = sv * fac;
+  st4(s_out + off, sv);
+  st4(vc_out + off, vc_in ? v + ld4(vc_in + off) : v);
+  if (v_out) st4(v_out + off, v);
 }
 
 // gs = squash'(s)^T a with a = a_init (the upstream gradient of the last
 // iteration's v) or, for earlier iterations, a = A += sum of gVc slabs.
 template <int DOUT>
-__global__ void bwd_finish_kernel(const float* __restrict__ slab, int n_chunks, int F, int J,
+__global__ void bwd_finish_kernel(const float* __restrict__ slab, int n_chunks, size_t FJD,
                                   const float* __restrict__ a_init, float* __restrict__ A,
                                   const float* __restrict__ s, float* __restrict__ gs) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= F * J) return;
-  const size_t JD = (size_t)J * DOUT;
-  const size_t base = (size_t)idx * DOUT;
-  const size_t FJD = (size_t)F * JD;
-  float a[DOUT], sv[DOUT];
-#pragma unroll
-  for (int d = 0; d < DOUT; d += 4) {
-    f4 v;
-    if (a_init) {
-      v = ld4(a_init + base + d);
-    } else {
-      v = ld4(A + base + d);
-      for (int c = 0; c < n_chunks; ++c) v += ld4(slab + (size_t)c * FJD + base + d);
-      st4(A + base + d, v);
-    }
-    const f4 q = ld4(s + base + d);
-    a[d] = v.x; a[d + 1] = v.y; a[d + 2] = v.z; a[d + 3] = v.w;
-    sv[d] = q.x; sv[d + 1] = q.y; sv[d + 2] = q.z; sv[d + 3] = q.w;
+  constexpr int Q = DOUT / 4;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = idx < FJD / 4;
+  const size_t off = (ok ? idx : 0) * 4;
+  f4 a;
+  if (a_init) {
+    a = ld4(a_init + off);
+  } else {
+    a = ld4(A + off) + sum_slab4(slab, n_chunks, FJD, off);
+    if (ok) st4(A + off, a);
   }
-  float n2 = 0.f, sa = 0.f;
-#pragma unroll
-  for (int d = 0; d < DOUT; ++d) {
-    n2 += sv[d] * sv[d];
-    sa += sv[d] * a[d];
-  }
+  const f4 sv = ld4(s + off);
+  const float n2 = qsum<Q>((sv.x * sv.x + sv.y * sv.y) + (sv.z * sv.z + sv.w * sv.w));
+  const float sa = qsum<Q>((sv.x * a.x + sv.y * a.y) + (sv.z * a.z + sv.w * a.w));
+  if (!ok) return;
   const float rs = 1.f / sqrtf(n2 + kSquashEps);
   const float ip = 1.f / (1.f + n2);
   const float gfac = n2 * ip * rs;
-  const float dg = rs * ip * (ip - 0.5f * n2 / (n2 + kSquashEps));
-#pragma unroll
-  for (int d = 0; d < DOUT; d += 4) {
-    f4 o;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = gfac * a[d + k] + 2.f * dg * sa * sv[d + k];
-    st4(gs + base + d, o);
-  }
+  const float dg2 = 2.f * rs * ip * (ip - 0.5f * n2 / (n2 + kSquashEps)) * sa;
+  st4(gs + off, a * gfac + sv * dg2);
 }
 
 // ---------------------------------------------------------------- host side
@@ -828,23 +803,24 @@ void dispatch_pass(const Geom& g, const PassCfg& pc, int n_chunks, const float* 
 template <int D>
 void launch_fwd_finish(const Geom& g, const float* slab, int n_chunks, const float* vc_in, float* s_out,
                        float* vc_out, float* v_out, hipStream_t st) {
-  const int n = g.F() * g.J;
-  hipLaunchKernelGGL((fwd_finish_kernel<D>), dim3((n + 255) / 256), dim3(256), 0, st, slab, n_chunks, g.F(), g.J,
+  const size_t FJD = (size_t)g.F() * g.JD();
+  hipLaunchKernelGGL((fwd_finish_kernel<D>), dim3((FJD / 4 + 255) / 256), dim3(256), 0, st, slab, n_chunks, FJD,
                      vc_in, s_out, vc_out, v_out);
 }
 
 template <int D>
 void launch_bwd_finish(const Geom& g, const float* slab, int n_chunks, const float* a_init, float* A,
                        const float* s, float* gs, hipStream_t st) {
-  const int n = g.F() * g.J;
-  hipLaunchKernelGGL((bwd_finish_kernel<D>), dim3((n + 255) / 256), dim3(256), 0, st, slab, n_chunks, g.F(), g.J,
+  const size_t FJD = (size_t)g.F() * g.JD();
+  hipLaunchKernelGGL((bwd_finish_kernel<D>), dim3((FJD / 4 + 255) / 256), dim3(256), 0, st, slab, n_chunks, FJD,
                      a_init, A, s, gs);
 }
 
-constexpr int kGuTW = 2;  // row tiles per wave in the gu pass
+// row tiles per wave in the gu pass (a wave must hold whole output capsules)
+constexpr int gu_tw(int d) { return d >= 64 ? 4 : 2; }
 constexpr int kGuNW = 4;  // waves per gu workgroup
 
-inline int gu_wgroups(const Geom& g) { return (g.NT() + kGuNW * kGuTW - 1) / (kGuNW * kGuTW); }
+inline int gu_wgroups(const Geom& g) { return (g.NT() + kGuNW * gu_tw(g.dout) - 1) / (kGuNW * gu_tw(g.dout)); }
 inline int padded_frames(const Geom& g) { return (g.F() + 15) / 16 * 16; }
 // Frame slots of the widest i-chunk's gx accumulator (16 + its window-offset span).
 inline int gu_nslots(const Geom& g, int chunk_len) {
@@ -884,17 +860,16 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
   const int n_wgroups = gu_wgroups(g);
   const int n_chunks = gu_chunks(g);
   const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
-  const int nw = std::min(kGuNW, (g.NT() + kGuTW - 1) / kGuTW);
+  constexpr int TW = gu_tw(D);
+  const int nw = std::min(kGuNW, (g.NT() + TW - 1) / TW);
   const int nslots = gu_nslots(g, chunk_len);
   const size_t lds = gu_lds_bytes(g, nw, nslots);
-  static int dbg = getenv("SRF_DBG") ? atoi(getenv("SRF_DBG")) : 0;
-  if (dbg) hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, st);
   if (lds <= kGuLdsMax)
-    hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R, true>), dim3(n_ftiles * n_wgroups * n_chunks),
+    hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, true>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
                        g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb, nslots);
   else
-    hipLaunchKernelGGL((route_gu_kernel<D, D, kGuTW, R, false>), dim3(n_ftiles * n_wgroups * n_chunks),
+    hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, false>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), 0, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
                        g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb, nslots);
 }

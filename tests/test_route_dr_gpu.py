@@ -23,6 +23,8 @@ CASES = [
     (3, 9, 16, 32, 2, 2, 16, 3, False),   # C3/C4 inner layer
     (2, 6, 16, 32, 2, 2, 32, 3, True),    # C3/C4 last layer
     (1, 5, 3, 16, 1, 2, 5, 2, True),      # ragged odd sizes
+    (1, 5, 2, 64, 1, 1, 4, 2, True),      # C5-width capsules (DIM=64)
+    (2, 7, 4, 8, 1, 1, 6, 5, False),      # 5 routing iterations
 ]
 
 
