@@ -75,6 +75,75 @@ __global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__
   }
 }
 
+// Vectorised forms for PH in {4, 8, 16} (K % 256 == 0 is not required, K % 4 == 0 is):
+// a wave owns FW frames; lane l covers k = 4l + 256j, reading X and the Wp rows as
+// float4, so each Wp row fetched serves FW frames.
+template <int PH, int FW>
+__global__ __launch_bounds__(256) void proj_fwd_vec_kernel(const float* __restrict__ X, int F, int K,
+                                                           const float* __restrict__ Wp,
+                                                           const float* __restrict__ bp, float* __restrict__ e) {
+  constexpr int PQ = PH / 4;
+  const int l = threadIdx.x & 63;
+  const int f0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * FW;
+  if (f0 >= F) return;
+  float acc[FW][PH];
+#pragma unroll
+  for (int u = 0; u < FW; ++u)
+#pragma unroll
+    for (int p = 0; p < PH; ++p) acc[u][p] = 0.f;
+#pragma unroll 2
+  for (int k0 = 4 * l; k0 < K; k0 += 256) {
+    f4 x[FW], w[4][PQ];
+#pragma unroll
+    for (int u = 0; u < FW; ++u) x[u] = *reinterpret_cast<const f4*>(X + (size_t)min(f0 + u, F - 1) * K + k0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) w[kk][q] = *reinterpret_cast<const f4*>(Wp + (size_t)(k0 + kk) * PH + 4 * q);
+#pragma unroll
+    for (int u = 0; u < FW; ++u)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int p = 0; p < PH; ++p) acc[u][p] += x[u][kk] * w[kk][p >> 2][p & 3];
+  }
+#pragma unroll
+  for (int u = 0; u < FW; ++u)
+#pragma unroll
+    for (int p = 0; p < PH; ++p) {
+      const float sum = wave_sum(acc[u][p]);
+      if (l == 0 && f0 + u < F) e[(size_t)(f0 + u) * PH + p] = sum + bp[p];
+    }
+}
+
+// g_X[f][k..k+3] = sum_p g_e[f][p] Wp[k..k+3][p], one float4 of g_X per thread.
+template <int PH>
+__global__ __launch_bounds__(256) void proj_bwd_x_vec_kernel(const float* __restrict__ g_e,
+                                                             const float* __restrict__ Wp, int F, int K,
+                                                             float* __restrict__ g_X) {
+  constexpr int PQ = PH / 4;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K4 = K / 4;
+  if (idx >= (size_t)F * K4) return;
+  const int f = (int)(idx / K4);
+  const int k0 = (int)(idx - (size_t)f * K4) * 4;
+  f4 ge[PQ];
+#pragma unroll
+  for (int q = 0; q < PQ; ++q) ge[q] = *reinterpret_cast<const f4*>(g_e + (size_t)f * PH + 4 * q);
+  f4 out;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      const f4 w = *reinterpret_cast<const f4*>(Wp + (size_t)(k0 + kk) * PH + 4 * q);
+      sacc += (w.x * ge[q].x + w.y * ge[q].y) + (w.z * ge[q].z + w.w * ge[q].w);
+    }
+    out[kk] = sacc;
+  }
+  *reinterpret_cast<f4*>(g_X + (size_t)f * K + k0) = out;
+}
+
 // g_X[f][k] = sum_p g_e[f][p] Wp[k][p]
 __global__ void proj_bwd_x_kernel(const float* __restrict__ g_e, const float* __restrict__ Wp, int F, int K, int PH,
                                   float* __restrict__ g_X) {
@@ -589,7 +658,16 @@ int srf_primary_caps_fwd(const float* X, const int* inp_len, int B, int T, int K
     return SRF_EWORKSPACE;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(proj_fwd_kernel, dim3((F + 3) / 4), dim3(256), 0, st, X, F, K, PH, Wp, bp, sv.e);
+  constexpr int FW = 2;
+  const dim3 gvec((F + 4 * FW - 1) / (4 * FW));
+  if (K % 4 == 0 && PH == 4)
+    hipLaunchKernelGGL((proj_fwd_vec_kernel<4, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e);
+  else if (K % 4 == 0 && PH == 8)
+    hipLaunchKernelGGL((proj_fwd_vec_kernel<8, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e);
+  else if (K % 4 == 0 && PH == 16)
+    hipLaunchKernelGGL((proj_fwd_vec_kernel<16, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e);
+  else
+    hipLaunchKernelGGL(proj_fwd_kernel, dim3((F + 3) / 4), dim3(256), 0, st, X, F, K, PH, Wp, bp, sv.e);
   SRF_LAUNCH_CHECK("proj_fwd");
   CapsDims cd{B, T, PH, PD};
   const size_t sh = (size_t)(PH * PD + 5 * PH + 8) * sizeof(float);
@@ -630,8 +708,16 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
   hipLaunchKernelGGL(encaps_bwd_b_kernel, dim3((F * PH + 255) / 256), dim3(256), 0, st, w.gv1, w.gv2, cd, K1, K2,
                      w.g_e);
   SRF_LAUNCH_CHECK("encaps_bwd_b");
-  hipLaunchKernelGGL(proj_bwd_x_kernel, dim3(((size_t)F * K + 255) / 256), dim3(256), 0, st, w.g_e, Wp, F, K, PH,
-                     g_X);
+  const dim3 gx4(((size_t)F * (K / 4) + 255) / 256);
+  if (K % 4 == 0 && PH == 4)
+    hipLaunchKernelGGL(proj_bwd_x_vec_kernel<4>, gx4, dim3(256), 0, st, w.g_e, Wp, F, K, g_X);
+  else if (K % 4 == 0 && PH == 8)
+    hipLaunchKernelGGL(proj_bwd_x_vec_kernel<8>, gx4, dim3(256), 0, st, w.g_e, Wp, F, K, g_X);
+  else if (K % 4 == 0 && PH == 16)
+    hipLaunchKernelGGL(proj_bwd_x_vec_kernel<16>, gx4, dim3(256), 0, st, w.g_e, Wp, F, K, g_X);
+  else
+    hipLaunchKernelGGL(proj_bwd_x_kernel, dim3(((size_t)F * K + 255) / 256), dim3(256), 0, st, w.g_e, Wp, F, K, PH,
+                       g_X);
   SRF_LAUNCH_CHECK("proj_bwd_x");
   const int fchunk = (F + kProjChunks - 1) / kProjChunks;
   hipLaunchKernelGGL(proj_bwd_w_kernel, dim3((K + 255) / 256, kProjChunks), dim3(256), 0, st, X, w.g_e, F, K, PH,

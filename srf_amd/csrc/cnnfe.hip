@@ -66,16 +66,54 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
 }
 
 // ---------------------------------------------------------------- conv1
-// One thread = one output channel c of a stream of output pixels (grid-stride).
-// Block 256 = 4 pixel rows x 64 channels.  Partials slab[block][c] = (n, mean, M2).
+// A workgroup = kRows1 consecutive output rows t1 of one utterance (one wave per
+// row), a lane = one output channel c.  The 2*kRows1+1 input rows the tile reads
+// are staged in LDS with the SAME zero padding materialised, so each pixel's
+// 3x3 window is 9 broadcast LDS reads and no bounds checks.
+constexpr int kRows1 = 4;
+
+struct Tile1 {
+  int b, t1_0, fpad;   // fpad = row stride of the staged input (Fin + 2)
+};
+
+__device__ __forceinline__ Tile1 stage_rows1(const float* __restrict__ feats, const Dims& d, float* win) {
+  const int tiles_per_b = (d.T1 + kRows1 - 1) / kRows1;
+  Tile1 tl;
+  tl.b = blockIdx.x / tiles_per_b;
+  tl.t1_0 = (blockIdx.x - tl.b * tiles_per_b) * kRows1;
+  tl.fpad = d.Fin + 2;
+  const int nrows = 2 * kRows1 + 1;
+  const int t_base = 2 * tl.t1_0 - d.pt1;
+  for (int k = threadIdx.x; k < nrows * tl.fpad; k += blockDim.x) {
+    const int r = k / tl.fpad, col = k - r * tl.fpad;
+    const int t = t_base + r, f = col - 1;   // staged column 0 is f = -1
+    const bool ok = t >= 0 && t < d.T && f >= 0 && f < d.Fin;
+    const float v = feats[((size_t)tl.b * d.T + min(max(t, 0), d.T - 1)) * d.Fin + min(max(f, 0), d.Fin - 1)];
+    win[k] = ok ? v : 0.f;
+  }
+  __syncthreads();
+  return tl;
+}
+
+// x[dt*3+df] of output pixel (row wave w, column f1); requires pf1 <= 1 (3x3, stride 2)
+__device__ __forceinline__ void window9_lds(const float* win, const Tile1& tl, const Dims& d, int w, int f1,
+                                            float (&x)[9]) {
+#pragma unroll
+  for (int dt = 0; dt < 3; ++dt)
+#pragma unroll
+    for (int df = 0; df < 3; ++df) x[dt * 3 + df] = win[(2 * w + dt) * tl.fpad + 2 * f1 - d.pf1 + df + 1];
+}
+
+// Partials slab[block][c] = (n, mean, M2).
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(
     const float* __restrict__ feats, const int* __restrict__ inp_len, Dims d, const float* __restrict__ ka,
     const float* __restrict__ ba, const float* __restrict__ kb, const float* __restrict__ bb, int training,
     float drop_p, unsigned long long seed, float* __restrict__ y1, unsigned char* __restrict__ sel1,
     float* __restrict__ part) {
-  __shared__ float sh[3][4][C];
+  extern __shared__ __attribute__((aligned(16))) float win[];
+  __shared__ float sh[3][kRows1][C];
   const int c = threadIdx.x & (C - 1);
-  const int row = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float wa[9], wb[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
@@ -84,52 +122,69 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
   }
   const float bia = ba[c], bib = bb[c];
   const float keep_scale = 1.f / (1.f - drop_p);
-  const int P = d.B * d.T1 * d.F1;
+  const bool drop = training && drop_p > 0.f;
+  const Tile1 tl = stage_rows1(feats, d, win);
+  const int t1 = tl.t1_0 + w;
   // statistics as sums shifted by the channel biases (no per-element division)
   float n = 0.f, s1 = 0.f, s2 = 0.f;
   const float K = 0.5f * (bia + bib);
-#pragma unroll 4
-  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
-    const int f1 = p % d.F1;
-    const int t1 = (p / d.F1) % d.T1;
-    const int b = p / (d.F1 * d.T1);
-    float a = bia, bv = bib;
+  if (t1 < d.T1) {
+    const bool live = t1 < ceil_div_len(inp_len[tl.b], 2);
+    const int pbase = (tl.b * d.T1 + t1) * d.F1;
+#pragma unroll 2
+    for (int f1 = 0; f1 < d.F1; ++f1) {
+      float x[9];
+      window9_lds(win, tl, d, w, f1, x);
+      float a = bia, bv = bib;
 #pragma unroll
-    for (int dt = 0; dt < 3; ++dt) {
-      const int t = 2 * t1 - d.pt1 + dt;
-#pragma unroll
-      for (int df = 0; df < 3; ++df) {
-        const int f = 2 * f1 - d.pf1 + df;
-        float x = 0.f;
-        if (t >= 0 && t < d.T && f >= 0 && f < d.Fin) x = feats[(b * d.T + t) * d.Fin + f];
-        a += x * wa[dt * 3 + df];
-        bv += x * wb[dt * 3 + df];
+      for (int k = 0; k < 9; ++k) {
+        a += x[k] * wa[k];
+        bv += x[k] * wb[k];
       }
+      const int o = (pbase + f1) * C + c;
+      if (drop) {
+        a *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
+        bv *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
+      }
+      const bool sl = a >= bv;  // TF Maximum gradient: ties go to the first operand
+      const float y = live ? (sl ? a : bv) : 0.f;
+      y1[o] = y;
+      sel1[o] = sl ? 1 : 0;
+      n += 1.f;
+      s1 += y - K;
+      s2 += (y - K) * (y - K);
     }
-    const int o = p * C + c;
-    if (training && drop_p > 0.f) {
-      a *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
-      bv *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
-    }
-    const bool s = a >= bv;  // TF Maximum gradient: ties go to the first operand
-    float y = s ? a : bv;
-    if (t1 >= ceil_div_len(inp_len[b], 2)) y = 0.f;
-    y1[o] = y;
-    sel1[o] = s ? 1 : 0;
-    n += 1.f;
-    s1 += y - K;
-    s2 += (y - K) * (y - K);
   }
   float mean = n > 0.f ? K + s1 / n : 0.f;
   float m2 = n > 0.f ? fmaxf(s2 - s1 * s1 / n, 0.f) : 0.f;
-  sh[0][row][c] = n; sh[1][row][c] = mean; sh[2][row][c] = m2;
+  sh[0][w][c] = n; sh[1][w][c] = mean; sh[2][w][c] = m2;
   __syncthreads();
-  if (row == 0) {
-    for (int r = 1; r < 4; ++r) chan_merge(n, mean, m2, sh[0][r][c], sh[1][r][c], sh[2][r][c]);
+  if (w == 0) {
+    for (int r = 1; r < kRows1; ++r) chan_merge(n, mean, m2, sh[0][r][c], sh[1][r][c], sh[2][r][c]);
     part[((size_t)blockIdx.x * 3 + 0) * C + c] = n;
     part[((size_t)blockIdx.x * 3 + 1) * C + c] = mean;
     part[((size_t)blockIdx.x * 3 + 2) * C + c] = m2;
   }
+}
+
+// Merge groups of Welford partials: block k merges parts [k*per, (k+1)*per) of
+// every channel into out[k] (the first stage of the BN finalize).
+__global__ __launch_bounds__(256) void bn_merge_kernel(const float* __restrict__ part, int nparts, int per,
+                                                       float* __restrict__ out) {
+  __shared__ float sh[3][4][C];
+  const int c = threadIdx.x & (C - 1), r = threadIdx.x >> 6;
+  const int k0 = blockIdx.x * per, k1 = min(nparts, k0 + per);
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int k = k0 + r; k < k1; k += 4)
+    chan_merge(n, mu, m2, part[((size_t)k * 3 + 0) * C + c], part[((size_t)k * 3 + 1) * C + c],
+               part[((size_t)k * 3 + 2) * C + c]);
+  sh[0][r][c] = n; sh[1][r][c] = mu; sh[2][r][c] = m2;
+  __syncthreads();
+  if (r != 0) return;
+  for (int q = 1; q < 4; ++q) chan_merge(n, mu, m2, sh[0][q][c], sh[1][q][c], sh[2][q][c]);
+  out[((size_t)blockIdx.x * 3 + 0) * C + c] = n;
+  out[((size_t)blockIdx.x * 3 + 1) * C + c] = mu;
+  out[((size_t)blockIdx.x * 3 + 2) * C + c] = m2;
 }
 
 // ---------------------------------------------------------------- BN finalize
@@ -333,19 +388,30 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restr
                                                             const int* __restrict__ inp_len, int B, int Tk, int Fk,
                                                             int div, float* __restrict__ part) {
   __shared__ float sh[2][4][C];
-  const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
+  const int c = threadIdx.x & (C - 1);
+  const int row = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // pixels are wave-uniform
   const float mean = stats[c], rstd = stats[C + c];
   const int P = B * Tk * Fk;
+  constexpr int PX = 4;
   float s0 = 0.f, s1 = 0.f;
-#pragma unroll 4
-  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
-    const int t = (p / Fk) % Tk;
-    const int b = p / (Fk * Tk);
-    if (t >= ceil_div_len(inp_len[b], div)) continue;
-    const size_t o = (size_t)p * C + c;
-    const float dy = g[o];
-    s0 += dy;
-    s1 += dy * (y[o] - mean) * rstd;
+  for (int p0 = (blockIdx.x * 4 + row) * PX; p0 < P; p0 += gridDim.x * 4 * PX) {
+    float dy[PX], yv[PX], m[PX];
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const int p = min(p0 + u, P - 1);
+      const int t = (p / Fk) % Tk;
+      const int b = p / (Fk * Tk);
+      m[u] = (p0 + u < P && t < ceil_div_len(inp_len[b], div)) ? 1.f : 0.f;
+      const size_t o = (size_t)p * C + c;
+      dy[u] = g[o];
+      yv[u] = y[o];
+    }
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const float d = dy[u] * m[u];
+      s0 += d;
+      s1 += d * (yv[u] - mean) * rstd;
+    }
   }
   sh[0][row][c] = s0; sh[1][row][c] = s1;
   __syncthreads();
@@ -371,7 +437,7 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     const int* __restrict__ inp_len, Dims d, float drop_p, unsigned long long seed, float* __restrict__ g_ab,
     float* __restrict__ part) {
   __shared__ float sh[2][4][C];
-  const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
+  const int c = threadIdx.x & (C - 1), row = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = d.B * d.T2 * d.F2;
   const float mean = stats2[c], rstd = stats2[C + c], gam = gamma2[c];
   const float sdy_n = bnsum2[c] / (float)P, sdyxh_n = bnsum2[C + c] / (float)P;
@@ -592,8 +658,10 @@ __global__ __launch_bounds__(256) void conv1_bwd_kernel(
     const float* __restrict__ y1, const unsigned char* __restrict__ sel1, const float* __restrict__ stats1,
     const float* __restrict__ gamma1, const float* __restrict__ bnsum1, float drop_p, unsigned long long seed,
     float* __restrict__ part) {
-  __shared__ float sh[4][20][C];
-  const int c = threadIdx.x & (C - 1), row = threadIdx.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) float win[];
+  __shared__ float sh[kRows1][20][C];
+  const int c = threadIdx.x & (C - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = d.B * d.T1 * d.F1;
   const float mean = stats1[c], rstd = stats1[C + c], gam = gamma1[c];
   const float sdy_n = bnsum1[c] / (float)P, sdyxh_n = bnsum1[C + c] / (float)P;
@@ -601,46 +669,47 @@ __global__ __launch_bounds__(256) void conv1_bwd_kernel(
   float acc[20];
 #pragma unroll
   for (int j = 0; j < 20; ++j) acc[j] = 0.f;
-#pragma unroll 4
-  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
-    const int f1 = p % d.F1;
-    const int t1 = (p / d.F1) % d.T1;
-    const int b = p / (d.F1 * d.T1);
-    const float mask = t1 < ceil_div_len(inp_len[b], 2) ? 1.f : 0.f;
-    const size_t o = (size_t)p * C + c;
-    const float gy = bn_bwd_elem(g_x1[o], y1[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
-    const bool s = sel1[o] != 0;
-    float ga = s ? gy : 0.f, gb = s ? 0.f : gy;
-    if (drop_p > 0.f) {
-      ga *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
-      gb *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
-    }
-    acc[18] += ga;
-    acc[19] += gb;
+  const Tile1 tl = stage_rows1(feats, d, win);
+  const int t1 = tl.t1_0 + w;
+  if (t1 < d.T1) {
+    const float mask = t1 < ceil_div_len(inp_len[tl.b], 2) ? 1.f : 0.f;
+    const int pbase = (tl.b * d.T1 + t1) * d.F1;
+#pragma unroll 2
+    for (int f1 = 0; f1 < d.F1; ++f1) {
+      const int o = (pbase + f1) * C + c;
+      const float gy = bn_bwd_elem(g_x1[o], y1[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
+      const bool sl = sel1[o] != 0;
+      float ga = sl ? gy : 0.f, gb = sl ? 0.f : gy;
+      if (drop_p > 0.f) {
+        ga *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
+        gb *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
+      }
+      float x[9];
+      window9_lds(win, tl, d, w, f1, x);
+      acc[18] += ga;
+      acc[19] += gb;
 #pragma unroll
-    for (int dt = 0; dt < 3; ++dt) {
-      const int t = 2 * t1 - d.pt1 + dt;
-#pragma unroll
-      for (int df = 0; df < 3; ++df) {
-        const int f = 2 * f1 - d.pf1 + df;
-        float x = 0.f;
-        if (t >= 0 && t < d.T && f >= 0 && f < d.Fin) x = feats[((size_t)b * d.T + t) * d.Fin + f];
-        acc[dt * 3 + df] += x * ga;
-        acc[9 + dt * 3 + df] += x * gb;
+      for (int k = 0; k < 9; ++k) {
+        acc[k] += x[k] * ga;
+        acc[9 + k] += x[k] * gb;
       }
     }
   }
 #pragma unroll
-  for (int j = 0; j < 20; ++j) sh[row][j][c] = acc[j];
+  for (int j = 0; j < 20; ++j) sh[w][j][c] = acc[j];
   __syncthreads();
-  for (int j = row; j < 20; j += 4) {
-    const float v = sh[0][j][c] + sh[1][j][c] + sh[2][j][c] + sh[3][j][c];
+  for (int j = w; j < 20; j += kRows1) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < kRows1; ++r) v += sh[r][j][c];
     part[((size_t)blockIdx.x * 20 + j) * C + c] = v;
   }
 }
 
 // ---------------------------------------------------------------- host
-constexpr int kConv1Blocks = 1024;
+// conv1 workgroups: kRows1 output rows of one utterance each
+inline int conv1_blocks(const Dims& d) { return d.B * ((d.T1 + kRows1 - 1) / kRows1); }
+inline size_t conv1_lds(const Dims& d) { return (size_t)(2 * kRows1 + 1) * (d.Fin + 2) * sizeof(float); }
 
 struct FwdSaved {
   float *y1, *y2, *stats1, *stats2;
@@ -670,8 +739,22 @@ FwdSaved saved_layout(const Dims& d, void* base) {
   return s;
 }
 
+constexpr int kBnMerge = 32;   // first-stage groups of the BN finalize
+
+// Two-stage finalize: kBnMerge groups of partials, then one block over the groups.
+int bn_finalize(const float* part, int nparts, float* merged, const float* gamma, const float* beta, float* mmean,
+                float* mvar, int training, float* stats, hipStream_t st) {
+  const int per = (nparts + kBnMerge - 1) / kBnMerge;
+  hipLaunchKernelGGL(bn_merge_kernel, dim3(kBnMerge), dim3(256), 0, st, part, nparts, per, merged);
+  SRF_LAUNCH_CHECK("bn_merge");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(1024), 0, st, merged, kBnMerge, gamma, beta, mmean, mvar,
+                     training, stats);
+  SRF_LAUNCH_CHECK("bn_finalize");
+  return SRF_OK;
+}
+
 struct FwdWs {
-  float *part1, *part2, *wp;
+  float *part1, *part2, *wp, *merged;
   size_t bytes;
 };
 
@@ -684,10 +767,11 @@ FwdWs fwd_ws_layout(const Dims& d, void* base) {
     off += srf::align_up(bytes, 256);
     return o;
   };
-  const size_t op1 = take((size_t)kConv1Blocks * 3 * C * 4), op2 = take(nb2 * 3 * C * 4),
-               owp = take((size_t)9 * 2 * C * C * 4);
+  const size_t op1 = take((size_t)conv1_blocks(d) * 3 * C * 4), op2 = take(nb2 * 3 * C * 4),
+               owp = take((size_t)9 * 2 * C * C * 4), omg = take((size_t)kBnMerge * 3 * C * 4);
   char* b = static_cast<char*>(base);
   FwdWs w;
+  w.merged = (float*)(b + omg);
   w.part1 = (float*)(b + op1);
   w.part2 = (float*)(b + op2);
   w.wp = (float*)(b + owp);
@@ -746,19 +830,18 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t P2 = (size_t)d.B * d.T2 * d.F2;
   const int nb2 = (int)((P2 + 63) / 64);
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(kConv1Blocks), dim3(256), 0, st, feats, inp_len, d, k0a, b0a, k0b, b0b,
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, k0a, b0a, k0b, b0b,
                      training, drop_p, seed, sv.y1, sv.sel1, w.part1);
   SRF_LAUNCH_CHECK("conv1_fwd");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(1024), 0, st, w.part1, kConv1Blocks, gamma0, beta0, mmean0,
-                     mvar0, training, sv.stats1);
+  if ((rc = bn_finalize(w.part1, conv1_blocks(d), w.merged, gamma0, beta0, mmean0, mvar0, training, sv.stats1, st)))
+    return rc;
   SRF_LAUNCH_CHECK("bn_finalize(1)");
   hipLaunchKernelGGL(pack_w2_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wp);
   SRF_LAUNCH_CHECK("pack_w2");
   hipLaunchKernelGGL(conv2_fwd_kernel, dim3(nb2), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, d, w.wp, b1a, b1b,
                      training, drop_p, seed, sv.y2, sv.sel2, w.part2);
   SRF_LAUNCH_CHECK("conv2_fwd");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(1024), 0, st, w.part2, nb2, gamma1, beta1, mmean1, mvar1,
-                     training, sv.stats2);
+  if ((rc = bn_finalize(w.part2, nb2, w.merged, gamma1, beta1, mmean1, mvar1, training, sv.stats2, st))) return rc;
   SRF_LAUNCH_CHECK("bn_finalize(2)");
   hipLaunchKernelGGL(bn_apply_kernel, dim3(1024), dim3(256), 0, st, sv.y2, sv.stats2, inp_len, d.B, d.T2, d.F2, 4,
                      out);
@@ -788,8 +871,8 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   const size_t obp = take((size_t)kBnBlocks * 2 * C * 4), os2 = take(2 * C * 4), os1 = take(2 * C * 4),
                oab = take(P2 * 2 * C * 4), obias = take((size_t)kBnBlocks * 2 * C * 4), ogx = take(P1 * C * 4),
                owq = take((size_t)9 * 2 * C * C * 4), owp = take((size_t)kWgradSplits * 9 * C * 2 * C * 4),
-               oc1 = take((size_t)kConv1Blocks * 20 * C * 4), oc1s = take(20 * C * 4),
-               oscr = take(srf::colsum_scratch_floats(kConv1Blocks, 20 * C) * 4);
+               oc1 = take((size_t)conv1_blocks(d) * 20 * C * 4), oc1s = take(20 * C * 4),
+               oscr = take(srf::colsum_scratch_floats(std::max(conv1_blocks(d), kBnBlocks), 20 * C) * 4);
   char* b = static_cast<char*>(base);
   BwdWs2 w;
   w.bnpart = (float*)(b + obp);
@@ -892,10 +975,10 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum1, w.scratch, st))) return rc;
   SRF_HIP_TRY(hipMemcpyAsync(g_beta0, w.bnsum1, C * 4, hipMemcpyDeviceToDevice, st));
   SRF_HIP_TRY(hipMemcpyAsync(g_gamma0, w.bnsum1 + C, C * 4, hipMemcpyDeviceToDevice, st));
-  hipLaunchKernelGGL(conv1_bwd_kernel, dim3(kConv1Blocks), dim3(256), 0, st, feats, inp_len, d, w.g_x1, sv.y1,
+  hipLaunchKernelGGL(conv1_bwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, w.g_x1, sv.y1,
                      sv.sel1, sv.stats1, gamma0, w.bnsum1, drop_p, seed, w.c1part);
   SRF_LAUNCH_CHECK("conv1_bwd");
-  if ((rc = srf::colsum(w.c1part, kConv1Blocks, 20 * C, w.c1sum, w.scratch, st))) return rc;
+  if ((rc = srf::colsum(w.c1part, conv1_blocks(d), 20 * C, w.c1sum, w.scratch, st))) return rc;
   hipLaunchKernelGGL(conv1_grad_unpack_kernel, dim3((20 * C + 255) / 256), dim3(256), 0, st, w.c1sum, g_k0a, g_k0b,
                      g_b0a, g_b0b);
   SRF_LAUNCH_CHECK("conv1_grad_unpack");
