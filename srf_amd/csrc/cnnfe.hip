@@ -244,13 +244,83 @@ __global__ void pack_w2_kernel(const float* __restrict__ ka, const float* __rest
 // N-tile 1 = conv b, so the maxout pairs land in the same lane.
 constexpr int kLdsStride = C + 4;  // row padding against LDS bank conflicts
 
+// Per tap: the A tile (64 px x 64 cin, BN1 + mask1 applied) is staged in LDS,
+// double-buffered (the next tap's gather is in flight during this tap's MFMAs);
+// each wave streams its own B columns (the packed weights) straight into
+// registers, one tap ahead, since no other wave reads them.
+struct A2Gather {
+  f4 x[4];
+  unsigned ok;   // bit q: slot q holds a live pixel
+};
+
+// Tap-independent coordinates of the 4 A slots a thread stages (no divisions per tap).
+struct A2Slots {
+  int b[4], t2[4], f2[4], len1[4];
+  unsigned live;
+};
+
+__device__ __forceinline__ A2Slots a2_slots(const int* __restrict__ inp_len, const Dims& d, int p0, int tid) {
+  const int P2 = d.B * d.T2 * d.F2;
+  A2Slots sl;
+  sl.live = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int px = (q * 256 + tid) >> 4;
+    const int p = min(p0 + px, P2 - 1);
+    sl.f2[q] = p % d.F2;
+    sl.t2[q] = (p / d.F2) % d.T2;
+    sl.b[q] = p / (d.F2 * d.T2);
+    sl.len1[q] = ceil_div_len(inp_len[sl.b[q]], 2);
+    sl.live |= (p0 + px < P2 ? 1u : 0u) << q;
+  }
+  return sl;
+}
+
+__device__ __forceinline__ A2Gather gather_a2(const float* __restrict__ y1, const A2Slots& sl, const Dims& d,
+                                              int tap, int tid) {
+  const int dt = tap / 3, df = tap - dt * 3;
+  A2Gather r;
+  r.ok = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c4 = ((q * 256 + tid) & 15) * 4;
+    const int t1 = 2 * sl.t2[q] - d.pt2 + dt;
+    const int f1 = 2 * sl.f2[q] - d.pf2 + df;
+    const bool ok = ((sl.live >> q) & 1u) && t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < sl.len1[q];
+    const int t1c = min(max(t1, 0), d.T1 - 1), f1c = min(max(f1, 0), d.F1 - 1);
+    r.x[q] = *reinterpret_cast<const f4*>(y1 + (((size_t)sl.b[q] * d.T1 + t1c) * d.F1 + f1c) * C + c4);
+    r.ok |= (ok ? 1u : 0u) << q;
+  }
+  return r;
+}
+
+__device__ __forceinline__ void put_a2(float* As, const A2Gather& r, const float* __restrict__ stats1, int tid) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = q * 256 + tid;
+    const int px = idx >> 4, c4 = (idx & 15) * 4;
+    const f4 sc = *reinterpret_cast<const f4*>(stats1 + 2 * C + c4);
+    const f4 sf = *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
+    const f4 v = ((r.ok >> q) & 1u) ? r.x[q] * sc + sf : f4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f4*>(&As[px * kLdsStride + c4]) = v;
+  }
+}
+
+__device__ __forceinline__ void load_b2(const float* __restrict__ wp, int tap, int wv, int l16, int g,
+                                        f4 (&b)[4][2]) {
+#pragma unroll
+  for (int s = 0; s < C / 16; ++s)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      b[s][nt] = *reinterpret_cast<const f4*>(wp + ((size_t)tap * 2 * C + nt * C + 16 * wv + l16) * C + 16 * s + 4 * g);
+}
+
 __global__ __launch_bounds__(256) void conv2_fwd_kernel(
     const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len, Dims d,
     const float* __restrict__ wp, const float* __restrict__ ba, const float* __restrict__ bb, int training,
     float drop_p, unsigned long long seed, float* __restrict__ y2, unsigned char* __restrict__ sel2,
     float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float As[64 * kLdsStride];
-  __shared__ __attribute__((aligned(16))) float Bs[2 * C * kLdsStride];
+  __shared__ __attribute__((aligned(16))) float As[2][64 * kLdsStride];
   __shared__ float red[3][4][4][16];   // [n|mean|M2][wave][lane group][channel]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
@@ -258,58 +328,43 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
   const int P2 = d.B * d.T2 * d.F2;
   const int p0 = blockIdx.x * 64;
 
-  // per-thread staging coordinates: 4 float4 of A per thread
   f4 acc[4][2];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
 
+  f4 bcur[4][2], bnxt[4][2];
+  load_b2(wp, 0, wv, l16, g, bcur);
+  const A2Slots slots = a2_slots(inp_len, d, p0, tid);
+  {
+    const A2Gather r = gather_a2(y1, slots, d, 0, tid);
+    put_a2(As[0], r, stats1, tid);
+  }
+  __syncthreads();
   for (int tap = 0; tap < 9; ++tap) {
-    const int dt = tap / 3, df = tap - dt * 3;
-    // stage A: BN1 + mask1 applied to the gathered input pixels (zero padding)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int idx = q * 256 + tid;   // 1024 float4 = 64 px x 16
-      const int px = idx >> 4, c4 = (idx & 15) * 4;
-      const int p = p0 + px;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (p < P2) {
-        const int f2 = p % d.F2;
-        const int t2 = (p / d.F2) % d.T2;
-        const int b = p / (d.F2 * d.T2);
-        const int t1 = 2 * t2 - d.pt2 + dt;
-        const int f1 = 2 * f2 - d.pf2 + df;
-        if (t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < ceil_div_len(inp_len[b], 2)) {
-          const f4 x = *reinterpret_cast<const f4*>(y1 + (((size_t)b * d.T1 + t1) * d.F1 + f1) * C + c4);
-          const f4 sc = *reinterpret_cast<const f4*>(stats1 + 2 * C + c4);
-          const f4 sf = *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
-          v = x * sc + sf;
-        }
-      }
-      *reinterpret_cast<f4*>(&As[px * kLdsStride + c4]) = v;
+    const bool more = tap + 1 < 9;
+    A2Gather r;
+    if (more) {
+      r = gather_a2(y1, slots, d, tap + 1, tid);
+      load_b2(wp, tap + 1, wv, l16, g, bnxt);
     }
-    // stage B: packed weights of this tap, [128][64] -> [128][68]
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int idx = q * 256 + tid;   // 2048 float4 = 128 rows x 16
-      const int n = idx >> 4, c4 = (idx & 15) * 4;
-      *reinterpret_cast<f4*>(&Bs[n * kLdsStride + c4]) =
-          *reinterpret_cast<const f4*>(wp + ((size_t)tap * 2 * C + n) * C + c4);
-    }
-    __syncthreads();
+    const float* Ab = As[tap & 1];
 #pragma unroll
     for (int s = 0; s < C / 16; ++s) {
       const int k0 = 16 * s + 4 * g;
-      const f4 b0 = *reinterpret_cast<const f4*>(&Bs[(0 * C + 16 * wv + l16) * kLdsStride + k0]);
-      const f4 b1 = *reinterpret_cast<const f4*>(&Bs[(1 * C + 16 * wv + l16) * kLdsStride + k0]);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const f4 a = *reinterpret_cast<const f4*>(&As[(mt * 16 + l16) * kLdsStride + k0]);
+        const f4 a = *reinterpret_cast<const f4*>(&Ab[(mt * 16 + l16) * kLdsStride + k0]);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
-          acc[mt][0] = mfma16x16x4(a[kk], b0[kk], acc[mt][0]);
-          acc[mt][1] = mfma16x16x4(a[kk], b1[kk], acc[mt][1]);
+          acc[mt][0] = mfma16x16x4(a[kk], bcur[s][0][kk], acc[mt][0]);
+          acc[mt][1] = mfma16x16x4(a[kk], bcur[s][1][kk], acc[mt][1]);
         }
       }
+    }
+    if (more) {
+      put_a2(As[(tap + 1) & 1], r, stats1, tid);
+#pragma unroll
+      for (int s = 0; s < C / 16; ++s) bcur[s][0] = bnxt[s][0], bcur[s][1] = bnxt[s][1];
     }
     __syncthreads();
   }
@@ -321,9 +376,19 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
   float n = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
+    // coordinates of the first of the 4 consecutive pixels, then stepped
+    const int pb = min(p0 + mt * 16 + 4 * g, P2 - 1);
+    int f2 = pb % d.F2, t2 = (pb / d.F2) % d.T2, b = pb / (d.F2 * d.T2);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int p = p0 + mt * 16 + 4 * g + k;
+      if (k > 0 && ++f2 == d.F2) {
+        f2 = 0;
+        if (++t2 == d.T2) {
+          t2 = 0;
+          ++b;
+        }
+      }
       if (p >= P2) continue;
       const size_t o = (size_t)p * C + c;
       float a = acc[mt][0][k] + bia, bv = acc[mt][1][k] + bib;
@@ -331,13 +396,11 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
         a *= srf_keep(seed, kStreamConv1a, o, drop_p) ? keep_scale : 0.f;
         bv *= srf_keep(seed, kStreamConv1b, o, drop_p) ? keep_scale : 0.f;
       }
-      const bool s = a >= bv;
-      float y = s ? a : bv;
-      const int t2 = (p / d.F2) % d.T2;
-      const int b = p / (d.F2 * d.T2);
+      const bool sel = a >= bv;
+      float y = sel ? a : bv;
       if (t2 >= ceil_div_len(inp_len[b], 4)) y = 0.f;
       y2[o] = y;
-      sel2[o] = s ? 1 : 0;
+      sel2[o] = sel ? 1 : 0;
       n += 1.f;
       const float delta = y - mean;
       mean += delta / n;
@@ -487,68 +550,110 @@ constexpr int kNStride = 2 * C + 4;
 // (t1 % 2 == qt, f1 % 2 == qf): only taps with the matching parity reach such a
 // pixel, so the implicit GEMM (M = 64 pixels, N = 64 cin, K = taps x 128) runs
 // without zero taps.  g_x1[p1][cin] = sum_tap sum_n g_ab[o(p1,tap)][n] wq[tap][cin][n].
+// A (64 px x 128 n, gathered from g_ab) is double-buffered in LDS with the next
+// tap's gather in flight; each wave streams its 16 cin rows of wq into registers.
 __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restrict__ g_ab,
                                                           const float* __restrict__ wq, Dims d, int qt, int qf,
                                                           float* __restrict__ g_x1) {
-  __shared__ __attribute__((aligned(16))) float As[64 * kNStride];
-  __shared__ __attribute__((aligned(16))) float Bs[C * kNStride];
+  __shared__ __attribute__((aligned(16))) float As[2][64 * kNStride];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int nkt = (d.T1 - qt + 1) / 2, nkf = (d.F1 - qf + 1) / 2;
   const int Pc = d.B * nkt * nkf;
   const int q0 = blockIdx.x * 64;
   const int dt0 = (qt + d.pt2) & 1, df0 = (qf + d.pf2) & 1;
+  const int ntf = (3 - df0 + 1) / 2;                       // taps per parity class: ntt x ntf
+  const int ntaps = ((3 - dt0 + 1) / 2) * ntf;
+  // tap-independent slot coordinates: slot q = pixel (q*256 + tid) >> 5
+  int sb[8], skt[8], skf[8];
+  unsigned live = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int pc = q0 + ((q * 256 + tid) >> 5);
+    const int pcc = min(pc, Pc - 1);
+    skf[q] = pcc % nkf;
+    skt[q] = (pcc / nkf) % nkt;
+    sb[q] = pcc / (nkf * nkt);
+    live |= (pc < Pc ? 1u : 0u) << q;
+  }
+  const int n4 = (tid & 31) * 4;
+  auto tap_of = [&](int k) {
+    const int dt = dt0 + 2 * (k / ntf), df = df0 + 2 * (k % ntf);
+    return dt * 3 + df;
+  };
+  auto gather = [&](int tap, f4 (&v)[8], unsigned& ok) {
+    const int dt = tap / 3, df = tap - dt * 3;
+    ok = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int t2 = (qt + 2 * skt[q] + d.pt2 - dt) / 2, f2 = (qf + 2 * skf[q] + d.pf2 - df) / 2;
+      const bool in = ((live >> q) & 1u) && t2 >= 0 && t2 < d.T2 && f2 >= 0 && f2 < d.F2;
+      const int t2c = min(max(t2, 0), d.T2 - 1), f2c = min(max(f2, 0), d.F2 - 1);
+      v[q] = *reinterpret_cast<const f4*>(g_ab + (((size_t)sb[q] * d.T2 + t2c) * d.F2 + f2c) * 2 * C + n4);
+      ok |= (in ? 1u : 0u) << q;
+    }
+  };
+  auto put = [&](float* A, const f4 (&v)[8], unsigned ok) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int px = (q * 256 + tid) >> 5;
+      *reinterpret_cast<f4*>(&A[px * kNStride + n4]) = ((ok >> q) & 1u) ? v[q] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto load_b = [&](int tap, f4 (&bw)[8]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2)
+      bw[s2] = *reinterpret_cast<const f4*>(wq + ((size_t)tap * C + 16 * wv + l16) * 2 * C + 16 * s2 + 4 * g);
+  };
   f4 acc[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int dt = dt0; dt < 3; dt += 2) {
-    for (int df = df0; df < 3; df += 2) {
-      const int tap = dt * 3 + df;
-      // stage A: g_ab at the output pixel this tap maps each input pixel to
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int idx = q * 256 + tid;   // 2048 float4 = 64 px x 32
-        const int px = idx >> 5, n4 = (idx & 31) * 4;
-        const int pc = q0 + px;
-        f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (pc < Pc) {
-          const int kf = pc % nkf, kt = (pc / nkf) % nkt, b = pc / (nkf * nkt);
-          const int t2 = (qt + 2 * kt + d.pt2 - dt) / 2, f2 = (qf + 2 * kf + d.pf2 - df) / 2;
-          if (t2 >= 0 && t2 < d.T2 && f2 >= 0 && f2 < d.F2)
-            v = *reinterpret_cast<const f4*>(g_ab + (((size_t)b * d.T2 + t2) * d.F2 + f2) * 2 * C + n4);
-        }
-        *reinterpret_cast<f4*>(&As[px * kNStride + n4]) = v;
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int idx = q * 256 + tid;   // 2048 float4 = 64 cin x 32
-        const int ci = idx >> 5, n4 = (idx & 31) * 4;
-        *reinterpret_cast<f4*>(&Bs[ci * kNStride + n4]) =
-            *reinterpret_cast<const f4*>(wq + ((size_t)tap * C + ci) * 2 * C + n4);
-      }
-      __syncthreads();
-#pragma unroll 4
-      for (int s = 0; s < 2 * C / 16; ++s) {
-        const int k0 = 16 * s + 4 * g;
-        const f4 bw = *reinterpret_cast<const f4*>(&Bs[(16 * wv + l16) * kNStride + k0]);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const f4 a = *reinterpret_cast<const f4*>(&As[(mt * 16 + l16) * kNStride + k0]);
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) acc[mt] = mfma16x16x4(a[kk], bw[kk], acc[mt]);
-        }
-      }
-      __syncthreads();
+  f4 bcur[8], bnxt[8], av[8];
+  unsigned aok;
+  load_b(tap_of(0), bcur);
+  gather(tap_of(0), av, aok);
+  put(As[0], av, aok);
+  __syncthreads();
+  for (int k = 0; k < ntaps; ++k) {
+    const bool more = k + 1 < ntaps;
+    if (more) {
+      gather(tap_of(k + 1), av, aok);
+      load_b(tap_of(k + 1), bnxt);
     }
+    const float* Ab = As[k & 1];
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2) {
+      const int k0 = 16 * s2 + 4 * g;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f4 a = *reinterpret_cast<const f4*>(&Ab[(mt * 16 + l16) * kNStride + k0]);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) acc[mt] = mfma16x16x4(a[kk], bcur[s2][kk], acc[mt]);
+      }
+    }
+    if (more) {
+      put(As[(k + 1) & 1], av, aok);
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) bcur[s2] = bnxt[s2];
+    }
+    __syncthreads();
   }
   const int ci = 16 * wv + l16;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
+    const int pb = min(q0 + mt * 16 + 4 * g, Pc - 1);
+    int kf = pb % nkf, kt = (pb / nkf) % nkt, b = pb / (nkf * nkt);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int pc = q0 + mt * 16 + 4 * g + k;
+      if (k > 0 && ++kf == nkf) {
+        kf = 0;
+        if (++kt == nkt) {
+          kt = 0;
+          ++b;
+        }
+      }
       if (pc >= Pc) continue;
-      const int kf = pc % nkf, kt = (pc / nkf) % nkt, b = pc / (nkf * nkt);
       const int t1 = qt + 2 * kt, f1 = qf + 2 * kf;
       g_x1[(((size_t)b * d.T1 + t1) * d.F1 + f1) * C + ci] = acc[mt][k];
     }
@@ -557,72 +662,104 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
 
 // Weight gradient of stage 2 for one tap and one pixel split:
 // part[s][tap][cin][n] = sum_{p in split} xbn1(p, tap)[cin] * g_ab[p][n].
-constexpr int kPxChunk = 32;
-constexpr int kPxStride = kPxChunk + 4;
+// K = pixels in chunks of kWgChunk, staged row-major (A [px][cin] with BN1 + mask1
+// applied, B [px][n]) and double-buffered; a wave owns n in [32w, 32w+32) for all
+// 64 cin.  Row strides = 16 mod 64 words keep the per-lane b32 operand reads
+// (lane group g = pixel) bank-conflict free.
+constexpr int kWgChunk = 32;
+constexpr int kWgAStr = C + 16;
+constexpr int kWgBStr = 2 * C + 16;
+
+struct WgDiv {
+  FastDiv f2, t2;
+};
 
 __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restrict__ y1,
                                                           const float* __restrict__ stats1,
                                                           const int* __restrict__ inp_len,
-                                                          const float* __restrict__ g_ab, Dims d, int nsplit,
-                                                          int split_len, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float As[C * kPxStride];
-  __shared__ __attribute__((aligned(16))) float Bs[2 * C * kPxStride];
+                                                          const float* __restrict__ g_ab, Dims d, WgDiv dv,
+                                                          int nsplit, int split_len, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float As[2][kWgChunk * kWgAStr];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kWgChunk * kWgBStr];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int tap = blockIdx.x / nsplit, sp = blockIdx.x - tap * nsplit;
   const int dt = tap / 3, df = tap - dt * 3;
   const int P2 = d.B * d.T2 * d.F2;
   const int pbeg = sp * split_len, pend = min(P2, pbeg + split_len);
+  const int c4 = (tid & 15) * 4;                       // A slot channel (both A slots)
+  const f4 sc = *reinterpret_cast<const f4*>(stats1 + 2 * C + c4);
+  const f4 sf = *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
+  const int n4 = (tid & 31) * 4;                       // B slot column (all B slots)
+
+  f4 xa[2], xb[4];
+  unsigned oka = 0, okb = 0;
+  auto gather = [&](int pc0) {
+    oka = okb = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = pc0 + ((q * 256 + tid) >> 4);
+      const unsigned pcl = (unsigned)min(p, P2 - 1);
+      const unsigned r1 = fdiv(pcl, dv.f2);
+      const int f2 = (int)(pcl - r1 * d.F2);
+      const unsigned b = fdiv(r1, dv.t2);
+      const int t2 = (int)(r1 - b * d.T2);
+      const int t1 = 2 * t2 - d.pt2 + dt, f1 = 2 * f2 - d.pf2 + df;
+      const bool ok = p < pend && t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 &&
+                      t1 < ceil_div_len(inp_len[b], 2);
+      const int t1c = min(max(t1, 0), d.T1 - 1), f1c = min(max(f1, 0), d.F1 - 1);
+      xa[q] = *reinterpret_cast<const f4*>(y1 + (((size_t)b * d.T1 + t1c) * d.F1 + f1c) * C + c4);
+      oka |= (ok ? 1u : 0u) << q;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = pc0 + ((q * 256 + tid) >> 5);
+      xb[q] = *reinterpret_cast<const f4*>(g_ab + (size_t)min(p, P2 - 1) * 2 * C + n4);
+      okb |= (p < pend ? 1u : 0u) << q;
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int px = (q * 256 + tid) >> 4;
+      *reinterpret_cast<f4*>(&As[buf][px * kWgAStr + c4]) =
+          ((oka >> q) & 1u) ? xa[q] * sc + sf : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int px = (q * 256 + tid) >> 5;
+      *reinterpret_cast<f4*>(&Bs[buf][px * kWgBStr + n4]) = ((okb >> q) & 1u) ? xb[q] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
   f4 acc[4][2];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int pc0 = pbeg; pc0 < pend; pc0 += kPxChunk) {
-    // A^T: xbn1 gathered for 32 output pixels x 64 cin, stored [cin][px]
+  const int nch = (pend - pbeg + kWgChunk - 1) / kWgChunk;
+  if (nch > 0) {
+    gather(pbeg);
+    put(0);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const bool more = ch + 1 < nch;
+    if (more) gather(pbeg + (ch + 1) * kWgChunk);
+    const float* A = As[ch & 1];
+    const float* Bm = Bs[ch & 1];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int idx = q * 256 + tid;   // 512 float4 = 32 px x 16
-      const int px = idx >> 4, c4 = (idx & 15) * 4;
-      const int p = pc0 + px;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (p < pend) {
-        const int f2 = p % d.F2, t2 = (p / d.F2) % d.T2, b = p / (d.F2 * d.T2);
-        const int t1 = 2 * t2 - d.pt2 + dt, f1 = 2 * f2 - d.pf2 + df;
-        if (t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < ceil_div_len(inp_len[b], 2)) {
-          const f4 x = *reinterpret_cast<const f4*>(y1 + (((size_t)b * d.T1 + t1) * d.F1 + f1) * C + c4);
-          v = x * *reinterpret_cast<const f4*>(stats1 + 2 * C + c4) +
-              *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
-        }
-      }
+    for (int ks = 0; ks < kWgChunk / 4; ++ks) {
+      const int px = ks * 4 + g;
+      float a[4], bv[2];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) As[(c4 + j) * kPxStride + px] = v[j];
+      for (int mt = 0; mt < 4; ++mt) a[mt] = A[px * kWgAStr + mt * 16 + l16];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) bv[nt] = Bm[px * kWgBStr + 32 * wv + nt * 16 + l16];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x4(a[mt], bv[nt], acc[mt][nt]);
     }
-    // B^T: g_ab for 32 pixels x 128 outputs, stored [n][px]
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int idx = q * 256 + tid;   // 1024 float4 = 32 px x 32
-      const int px = idx >> 5, n4 = (idx & 31) * 4;
-      const int p = pc0 + px;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (p < pend) v = *reinterpret_cast<const f4*>(g_ab + (size_t)p * 2 * C + n4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) Bs[(n4 + j) * kPxStride + px] = v[j];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < kPxChunk / 16; ++s) {
-      const int k0 = 16 * s + 4 * g;
-      const f4 b0 = *reinterpret_cast<const f4*>(&Bs[(32 * wv + l16) * kPxStride + k0]);
-      const f4 b1 = *reinterpret_cast<const f4*>(&Bs[(32 * wv + 16 + l16) * kPxStride + k0]);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const f4 a = *reinterpret_cast<const f4*>(&As[(mt * 16 + l16) * kPxStride + k0]);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          acc[mt][0] = mfma16x16x4(a[kk], b0[kk], acc[mt][0]);
-          acc[mt][1] = mfma16x16x4(a[kk], b1[kk], acc[mt][1]);
-        }
-      }
-    }
+    if (more) put((ch + 1) & 1);
     __syncthreads();
   }
   // C layout: col = n (l16 within the N-tile), rows = cin mt*16 + 4g + k
@@ -642,6 +779,7 @@ __global__ void conv2_wgrad_reduce_kernel(const float* __restrict__ part, int ns
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= 9 * C * 2 * C) return;
   float s = 0.f;
+#pragma unroll 8
   for (int k = 0; k < nsplit; ++k) s += part[(size_t)k * 9 * C * 2 * C + idx];
   const int n = idx % (2 * C);
   const int tc = idx / (2 * C);   // tap*C + cin
@@ -858,7 +996,7 @@ struct BwdWs2 {
 };
 
 constexpr int kBnBlocks = 1024;
-constexpr int kWgradSplits = 32;
+constexpr int kWgradSplits = 64;
 
 BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   const size_t P1 = (size_t)d.B * d.T1 * d.F1, P2 = (size_t)d.B * d.T2 * d.F2;
@@ -961,9 +1099,10 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
       SRF_LAUNCH_CHECK("conv2_dgrad");
     }
   }
-  const int split_len = ((P2 + kWgradSplits - 1) / kWgradSplits + kPxChunk - 1) / kPxChunk * kPxChunk;
+  const int split_len = ((P2 + kWgradSplits - 1) / kWgradSplits + kWgChunk - 1) / kWgChunk * kWgChunk;
+  const WgDiv dv{make_fastdiv(d.F2), make_fastdiv(d.T2)};
   hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(9 * kWgradSplits), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, w.g_ab,
-                     d, kWgradSplits, split_len, w.wpart);
+                     d, dv, kWgradSplits, split_len, w.wpart);
   SRF_LAUNCH_CHECK("conv2_wgrad");
   hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((9 * C * 2 * C + 255) / 256), dim3(256), 0, st, w.wpart,
                      kWgradSplits, g_k1a, g_k1b);

@@ -41,6 +41,27 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
     }                                                                          \
   } while (0)
 
+// Exact unsigned division by a runtime-constant divisor d >= 1 (Granlund-Montgomery):
+// q = (t + ((n - t) >> 1)) >> (l - 1), t = umulhi(n, m).  Built on the host.
+struct FastDiv {
+  unsigned m, d;
+  int l;
+};
+inline FastDiv make_fastdiv(unsigned d) {
+  FastDiv f;
+  f.d = d;
+  f.l = 0;
+  while ((1ull << f.l) < d) ++f.l;
+  f.m = d > 1 ? (unsigned)((((1ull << 32) * ((1ull << f.l) - d)) / d) + 1) : 0u;
+  if (f.l == 0) f.l = 1;
+  return f;
+}
+__device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) {
+  const unsigned t = __umulhi(n, f.m);
+  const unsigned q = (t + ((n - t) >> 1)) >> (f.l - 1);
+  return f.d == 1 ? n : q;
+}
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 
