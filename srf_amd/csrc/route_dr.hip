@@ -211,22 +211,30 @@ struct PassState {
 
 // One input capsule i of a routing pass: u tile -> logits <u, Vc> -> softmax
 // over all output capsules (cross-wave through LDS) -> accumulate.
-template <int DIN, int DOUT, int TW, int MODE>
-__device__ __forceinline__ void pass_step(Frags<DIN, TW>& fr, PassState<TW>& st, float* red, int& parity, int i,
+template <int DIN, int DOUT, int TW, int MODE, bool FIRST>
+__device__ __forceinline__ void pass_step(float (&u)[TW][4], Frags<DIN, TW>& fr, PassState<TW>& st, float* red,
+                                          int& parity, int i,
                                           int r, int J, int Jeff, int mask_first, int tbase, int wv, int NW, int lane,
                                           int in_n, int f, bool fvalid, float* __restrict__ stats,
                                           const float* __restrict__ emb, const float* __restrict__ W,
                                           const float* __restrict__ bias, const FrameLoc& loc, int T, int N,
                                           int lpad, int inext, int JD, int NT) {
   const int fl = lane & 15, g = lane >> 4;
-  float u[TW][4];
-  pose_tiles<DIN, TW>(fr, u);
-  // the MFMAs have consumed the fragments: refill them with capsule inext now,
-  // so the loads are in flight across the softmax and its barrier
+  // software pipeline: u holds capsule i; the MFMAs for capsule i+1 issue now and
+  // run on the matrix cores while this capsule's softmax runs on the VALU; the
+  // fragments they consumed are refilled with capsule inext (= i+2)
+  // (forward only: the backward pass has no registers to spare for it)
+  constexpr bool PIPE = MODE == MODE_FWD && DIN <= 16;
+  float unx[TW][4];
+  if constexpr (PIPE) {
+    pose_tiles<DIN, TW>(fr, unx);
+  } else {
+    pose_tiles<DIN, TW>(fr, u);
+  }
   fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
   float c[TW];
   float gL[TW];
-  if (MODE == MODE_FWD && r == 0) {
+  if constexpr (MODE == MODE_FWD && FIRST) {
     // iteration 0: logits are 0 (+ the mask), so c is uniform (naive:172-181)
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
@@ -281,6 +289,14 @@ __device__ __forceinline__ void pass_step(Frags<DIN, TW>& fr, PassState<TW>& st,
       y = ya * s1 + yb * s2;
       m = M;
     }
+    if constexpr (PIPE) {
+      // interleave the next capsule's MFMAs with this capsule's softmax VALU work
+#pragma unroll
+      for (int k = 0; k < TW * DIN / 4; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+    }
     if (NW > 1) {
       float* slot = red + parity * (NW * 48);
       if (g == 0) {
@@ -321,7 +337,10 @@ __device__ __forceinline__ void pass_step(Frags<DIN, TW>& fr, PassState<TW>& st,
   for (int t = 0; t < TW; ++t) {
     const float w = (MODE == MODE_FWD) ? c[t] : gL[t];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) st.acc[t][k] += w * u[t][k];
+    for (int k = 0; k < 4; ++k) {
+      st.acc[t][k] += w * u[t][k];
+      if constexpr (PIPE) u[t][k] = unx[t][k];
+    }
   }
 }
 
@@ -330,7 +349,7 @@ __device__ __forceinline__ void pass_step(Frags<DIN, TW>& fr, PassState<TW>& st,
 // block: NW waves, wave w owns row tiles [w*TW, (w+1)*TW).  The fragments of
 // capsule i+1 are fetched before capsule i is processed (two register sets,
 // loop unrolled by 2), so the loads fly across the softmax barrier.
-template <int DIN, int DOUT, int TW, int MODE>
+template <int DIN, int DOUT, int TW, int MODE, bool FIRST>
 __global__ __launch_bounds__(512) void route_pass_kernel(
     const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ bias,
     int F, int T, int N, int lpad, int in_n, int J, int n_chunks, int chunk_len, int mask_first, int r,
@@ -369,11 +388,17 @@ __global__ __launch_bounds__(512) void route_pass_kernel(
 
   int parity = 0;
   if (i0 < i1) {
+    constexpr int AHEAD = (MODE == MODE_FWD && DIN <= 16) ? 2 : 1;   // capsules between a fetch and its use
     Frags<DIN, TW> fr;
+    float u[TW][4];
     fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, i0, JD, NT, tbase, lane, fr);
+    if constexpr (AHEAD == 2) {
+      pose_tiles<DIN, TW>(fr, u);
+      fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, min(i0 + 1, i1 - 1), JD, NT, tbase, lane, fr);
+    }
     for (int i = i0; i < i1; ++i) {
-      pass_step<DIN, DOUT, TW, MODE>(fr, st, red, parity, i, r, J, Jeff, mask_first, tbase, wv, NW, lane, in_n, f,
-                                     loc.valid, stats, emb, W, bias, loc, T, N, lpad, min(i + 1, i1 - 1), JD, NT);
+      pass_step<DIN, DOUT, TW, MODE, FIRST>(u, fr, st, red, parity, i, r, J, Jeff, mask_first, tbase, wv, NW, lane, in_n, f,
+                                     loc.valid, stats, emb, W, bias, loc, T, N, lpad, min(i + AHEAD, i1 - 1), JD, NT);
     }
   }
   if (!want_acc) return;
@@ -785,7 +810,8 @@ void launch_pass(const Geom& g, int NW, int n_chunks, const float* emb, const fl
   const int n_ftiles = (g.F() + 15) / 16;
   const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
   const size_t shmem = (NW > 1) ? (size_t)2 * NW * 48 * sizeof(float) : 16;
-  hipLaunchKernelGGL((route_pass_kernel<D, D, TW, MODE>), dim3(n_ftiles * n_chunks), dim3(64 * NW), shmem, st,
+  auto kern = r == 0 ? route_pass_kernel<D, D, TW, MODE, true> : route_pass_kernel<D, D, TW, MODE, false>;
+  hipLaunchKernelGGL(kern, dim3(n_ftiles * n_chunks), dim3(64 * NW), shmem, st,
                      emb, W, bias, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, n_chunks, chunk_len, g.mask_first, r,
                      vc, gsv, slab, stats, want_acc);
 }
