@@ -62,10 +62,13 @@ def synthetic_batch(B, T, class_n, rank, dev):
     Tp = (T + 3) // 4
     L = Tp // 2
     gl = torch.Generator().manual_seed(4321 + rank)
-    labels = torch.randint(1, class_n - 1, (B, L), generator=gl)
+    labels = torch.randint(1, class_n - 1, (B, L), generator=gl, dtype=torch.int32)
     inp_len = torch.full((B,), T, dtype=torch.int32)
     tar_len = torch.full((B,), L, dtype=torch.int32)
-    return tuple(t.to(dev) for t in (feats, labels, inp_len, tar_len))
+    # lengths stay host-side, as the input pipeline yields them (crop without a device sync)
+    if str(dev) != 'cpu':
+        inp_len = inp_len.pin_memory()
+    return feats.to(dev), labels.to(dev), inp_len, tar_len.to(dev)
 
 
 class HipEvents:

@@ -619,13 +619,6 @@ __global__ void scatter_encaps_grads(const float* __restrict__ wsum, int E, int 
   }
 }
 
-__global__ void split_copy(const float* __restrict__ src, int n0, float* __restrict__ d0, int n1,
-                           float* __restrict__ d1) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n0) d0[i] = src[i];
-  if (i < n1) d1[i] = src[n0 + i];
-}
-
 int check_caps(int B, int T, int PH, int PD) {
   SRF_REQUIRE(B > 0 && T > 0 && PH > 0 && PD > 0, "bad primary capsule shape");
   SRF_REQUIRE((size_t)PH * PD <= kMaxVec, "PH*PD = %d exceeds %d", PH * PD, kMaxVec);
@@ -724,9 +717,9 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
                      fchunk, w.ppart);
   SRF_LAUNCH_CHECK("proj_bwd_w");
   const int pcols = K * PH + PH;
-  if ((rc = srf::colsum(w.ppart, kProjChunks, pcols, w.psum, w.scratch, st))) return rc;
-  hipLaunchKernelGGL(split_copy, dim3((K * PH + 255) / 256), dim3(256), 0, st, w.psum, K * PH, g_Wp, PH, g_bp);
-  SRF_LAUNCH_CHECK("split_copy(proj)");
+  if ((rc = srf::colsum(w.ppart, kProjChunks, pcols, nullptr, w.scratch, st,
+                        srf::ColSplit{{g_Wp, g_bp, nullptr, nullptr}, {K * PH, PH, 0, 0}})))
+    return rc;
   return SRF_OK;
 }
 
@@ -764,11 +757,8 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
                      seed, (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr,
                      (const float*)nullptr, g_x, part);
   SRF_LAUNCH_CHECK("capsnorm_bwd");
-  int rc = srf::colsum(part, F, 2 * n, sum, scratch, st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(split_copy, dim3((n + 255) / 256), dim3(256), 0, st, sum, n, g_gamma, n, g_beta);
-  SRF_LAUNCH_CHECK("split_copy(capsnorm)");
-  return SRF_OK;
+  (void)sum;
+  return srf::colsum(part, F, 2 * n, nullptr, scratch, st, srf::ColSplit{{g_gamma, g_beta, nullptr, nullptr}, {n, n, 0, 0}});
 }
 
 int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
@@ -808,13 +798,9 @@ int srf_caps_head_bwd(const float* v, int F, int J, int D, const float* gamma_mi
                      training, p, seed, (unsigned)(kStreamMid0 + layer), stat, g_logits, 1, J, D, gamma_out, lens,
                      g_v, part);
   SRF_LAUNCH_CHECK("caps_head_bwd");
-  int rc = srf::colsum(part, F, cols, sum, scratch, st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(split_copy, dim3((n + 255) / 256), dim3(256), 0, st, sum, n, g_gamma_mid, n, g_beta_mid);
-  SRF_LAUNCH_CHECK("split_copy(head mid)");
-  hipLaunchKernelGGL(split_copy, dim3((J + 255) / 256), dim3(256), 0, st, sum + 2 * n, J, g_gamma_out, J, g_beta_out);
-  SRF_LAUNCH_CHECK("split_copy(head out)");
-  return SRF_OK;
+  (void)sum;
+  return srf::colsum(part, F, cols, nullptr, scratch, st,
+                     srf::ColSplit{{g_gamma_mid, g_beta_mid, g_gamma_out, g_beta_out}, {n, n, J, J}});
 }
 
 }  // extern "C"

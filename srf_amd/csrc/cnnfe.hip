@@ -1078,15 +1078,13 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.stats2, inp_len, d.B,
                      d.T2, d.F2, 4, w.bnpart);
   SRF_LAUNCH_CHECK("bn_bwd_reduce(2)");
-  if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st))) return rc;
-  SRF_HIP_TRY(hipMemcpyAsync(g_beta1, w.bnsum2, C * 4, hipMemcpyDeviceToDevice, st));
-  SRF_HIP_TRY(hipMemcpyAsync(g_gamma1, w.bnsum2 + C, C * 4, hipMemcpyDeviceToDevice, st));
+  if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st, srf::ColSplit{{g_beta1, g_gamma1, nullptr, nullptr}, {C, C, 0, 0}})))
+    return rc;
   hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.sel2, sv.stats2,
                      gamma1, w.bnsum2, inp_len, d, drop_p, seed, w.g_ab, w.biaspart);
   SRF_LAUNCH_CHECK("conv2_bwd_prep");
-  if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, w.bnpart, w.scratch, st))) return rc;
-  SRF_HIP_TRY(hipMemcpyAsync(g_b1a, w.bnpart, C * 4, hipMemcpyDeviceToDevice, st));
-  SRF_HIP_TRY(hipMemcpyAsync(g_b1b, w.bnpart + C, C * 4, hipMemcpyDeviceToDevice, st));
+  if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, nullptr, w.scratch, st, srf::ColSplit{{g_b1a, g_b1b, nullptr, nullptr}, {C, C, 0, 0}})))
+    return rc;
   // stage-2 data gradient (4 stride-parity classes) and weight gradient
   hipLaunchKernelGGL(pack_w2t_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wq);
   SRF_LAUNCH_CHECK("pack_w2t");
@@ -1111,9 +1109,8 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, w.g_x1, sv.y1, sv.stats1, inp_len, d.B,
                      d.T1, d.F1, 2, w.bnpart);
   SRF_LAUNCH_CHECK("bn_bwd_reduce(1)");
-  if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum1, w.scratch, st))) return rc;
-  SRF_HIP_TRY(hipMemcpyAsync(g_beta0, w.bnsum1, C * 4, hipMemcpyDeviceToDevice, st));
-  SRF_HIP_TRY(hipMemcpyAsync(g_gamma0, w.bnsum1 + C, C * 4, hipMemcpyDeviceToDevice, st));
+  if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum1, w.scratch, st, srf::ColSplit{{g_beta0, g_gamma0, nullptr, nullptr}, {C, C, 0, 0}})))
+    return rc;
   hipLaunchKernelGGL(conv1_bwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, w.g_x1, sv.y1,
                      sv.sel1, sv.stats1, gamma0, w.bnsum1, drop_p, seed, w.c1part);
   SRF_LAUNCH_CHECK("conv1_bwd");

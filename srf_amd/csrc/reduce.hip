@@ -7,6 +7,7 @@
 #include "srf_reduce.h"
 
 namespace {
+using srf::ColSplit;
 
 __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ in, int rows, int cols,
                                                      int rows_per_slice, float* __restrict__ part) {
@@ -27,13 +28,20 @@ __global__ __launch_bounds__(256) void colsum_stage1(const float* __restrict__ i
   }
 }
 
-__global__ void colsum_stage2(const float* __restrict__ part, int slices, int cols, float* __restrict__ out) {
+__global__ void colsum_stage2(const float* __restrict__ part, int slices, int cols, float* __restrict__ out,
+                              ColSplit split) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cols) return;
   float s = 0.f;
 #pragma unroll 8
   for (int k = 0; k < slices; ++k) s += part[(size_t)k * cols + c];
-  out[c] = s;
+  if (out) out[c] = s;
+  int start = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (split.dst[k] && c >= start && c < start + split.width[k]) split.dst[k][c - start] = s;
+    start += split.width[k];
+  }
 }
 
 }  // namespace
@@ -42,7 +50,12 @@ namespace srf {
 
 size_t colsum_scratch_floats(int rows, int cols) { return (size_t)kColsumMaxSlices * cols; (void)rows; }
 
-int colsum(const float* in, int rows, int cols, float* out, float* scratch, hipStream_t st) {
+int colsum(const float* in, int rows, int cols, float* out, float* scratch, hipStream_t st, const ColSplit& split) {
+  if (rows <= 128) {   // few partial rows: one pass, one thread per column
+    hipLaunchKernelGGL(colsum_stage2, dim3((cols + 255) / 256), dim3(256), 0, st, in, rows, cols, out, split);
+    SRF_LAUNCH_CHECK("colsum_stage2");
+    return SRF_OK;
+  }
   const int cblocks = (cols + 63) / 64;
   int slices = std::max(1, std::min(kColsumMaxSlices, (1024 + cblocks - 1) / cblocks));
   slices = std::min(slices, std::max(1, rows / 16));
@@ -50,7 +63,7 @@ int colsum(const float* in, int rows, int cols, float* out, float* scratch, hipS
   slices = (rows + rps - 1) / rps;
   hipLaunchKernelGGL(colsum_stage1, dim3(cblocks, slices), dim3(256), 0, st, in, rows, cols, rps, scratch);
   SRF_LAUNCH_CHECK("colsum_stage1");
-  hipLaunchKernelGGL(colsum_stage2, dim3((cols + 255) / 256), dim3(256), 0, st, scratch, slices, cols, out);
+  hipLaunchKernelGGL(colsum_stage2, dim3((cols + 255) / 256), dim3(256), 0, st, scratch, slices, cols, out, split);
   SRF_LAUNCH_CHECK("colsum_stage2");
   return SRF_OK;
 }

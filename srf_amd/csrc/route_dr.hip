@@ -585,10 +585,16 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
   }
 }
 
-// W [in_n][JD][din] -> WT [in_n][din][JD] (A operand of the gx contraction).
-__global__ void transpose_w_kernel(const float* __restrict__ W, int in_n, int JD, int din, float* __restrict__ WT) {
+// W [in_n][JD][din] -> WT [in_n][din][JD] (A operand of the gx contraction); the
+// same launch zeroes g_emb ([n_zero] floats), which the gu pass accumulates into.
+__global__ void transpose_w_kernel(const float* __restrict__ W, int in_n, int JD, int din, float* __restrict__ WT,
+                                   float* __restrict__ zero, size_t n_zero) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)in_n * JD * din) return;
+  const size_t nw = (size_t)in_n * JD * din;
+  if (idx >= nw) {
+    if (idx - nw < n_zero) zero[idx - nw] = 0.f;
+    return;
+  }
   const int row = idx % JD;
   const size_t rest = idx / JD;
   const int e = rest % din;
@@ -740,6 +746,7 @@ __global__ void bwd_finish_kernel(const float* __restrict__ slab, int n_chunks, 
   f4 a;
   if (a_init) {
     a = ld4(a_init + off);
+    if (ok) st4(A + off, f4{0.f, 0.f, 0.f, 0.f});   // A starts at 0 (gradient via later logits)
   } else {
     a = ld4(A + off) + sum_slab4(slab, n_chunks, FJD, off);
     if (ok) st4(A + off, a);
@@ -973,7 +980,6 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   const int Fp = padded_frames(g);
   // gs^{R-1} = squash'(s^{R-1}) g_v.  A accumulates sum_{r'>r} gVc^{r'}, the
   // gradient of v^r for r < R-1 (those v reach the loss only through the logits).
-  SRF_HIP_TRY(hipMemsetAsync(w.A, 0, FJD * sizeof(float), st));
   launch_bwd_finish<D>(g, nullptr, n_chunks, g_v, w.A, saved + (size_t)(2 * (R - 1)) * FJD,
                        w.gs + (size_t)(R - 1) * FJD, st);
   SRF_LAUNCH_CHECK("bwd_finish");
@@ -989,13 +995,14 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     SRF_LAUNCH_CHECK("bwd_finish");
   }
   {
-    const size_t total = (size_t)g.in_n() * g.JD() * g.din;
+    // W^T for the gu pass; the same launch zeroes g_emb (accumulated by the gu pass
+    // through the window adjoint)
+    const size_t n_emb = (size_t)g.F() * g.N * g.din;
+    const size_t total = (size_t)g.in_n() * g.JD() * g.din + n_emb;
     hipLaunchKernelGGL(transpose_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, g.in_n(), g.JD(), g.din,
-                       w.WT);
+                       w.WT, g_emb, n_emb);
     SRF_LAUNCH_CHECK("transpose_w");
   }
-  // g_emb is accumulated by the gu pass (window adjoint folded into its scatter-add)
-  SRF_HIP_TRY(hipMemsetAsync(g_emb, 0, (size_t)g.F() * g.N * g.din * sizeof(float), st));
   launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");
   {

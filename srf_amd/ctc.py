@@ -16,6 +16,12 @@ def ctc_loss(labels, logits, label_length, logit_length, logits_time_major=False
     return ops.ctc_loss(logits.contiguous(), labels, label_length, logit_length, blank_index)
 
 
+def ctc_loss_and_grad(labels, logits, label_length, logit_length, blank_index, grad_scale):
+    """Per-utterance NLL and grad_scale * d(sum nll)/d logits from one launch
+    (batch-major logits); the training step's loss head."""
+    return ops.ctc_loss_and_grad(logits.contiguous(), labels, label_length, logit_length, blank_index, grad_scale)
+
+
 def greedy_decode(logits, lengths, blank_index):
     """Best-path decoding: per-frame argmax, merge repeats, drop blanks.
     logits [B, T, C] batch-major; returns a list of label lists."""

@@ -327,7 +327,25 @@ class CtcLoss(torch.autograd.Function):
         return grad * g_nll[:, None, None], None, None, None, None
 
 
+def _i32(t):
+    return t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
+
+
+def ctc_loss_and_grad(logits, labels, label_len, logit_len, blank, grad_scale):
+    """(nll [B], grad_scale * d(sum nll)/d logits) without autograd."""
+    B, T, C = logits.shape
+    labels, label_len, logit_len = _i32(labels), _i32(label_len), _i32(logit_len)
+    Lmax = labels.shape[1]
+    L = _lib.lib()
+    nll = torch.empty(B, device=logits.device, dtype=torch.float32)
+    grad = torch.empty_like(logits)
+    wb = L.srf_ctc_workspace(B, T, C, Lmax)
+    ws = torch.empty(wb, device=logits.device, dtype=torch.uint8)
+    _lib.check(L.srf_ctc_loss(_ptr(logits.detach()), _ptr(labels), _ptr(label_len), _ptr(logit_len), B, T, C, Lmax,
+                              int(blank), float(grad_scale), _ptr(nll), _ptr(grad), _ptr(ws), wb, _stream()),
+               'srf_ctc_loss')
+    return nll, grad
+
+
 def ctc_loss(logits, labels, label_len, logit_len, blank):
-    i32 = torch.int32
-    return CtcLoss.apply(logits, labels.to(i32).contiguous(), label_len.to(i32).contiguous(),
-                         logit_len.to(i32).contiguous(), blank)
+    return CtcLoss.apply(logits, _i32(labels), _i32(label_len), _i32(logit_len), blank)

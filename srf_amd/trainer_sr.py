@@ -15,7 +15,8 @@ from . import ctc
 
 
 class Mean:
-    """tf.keras.metrics.Mean (trainer_sr.py:161-163)."""
+    """tf.keras.metrics.Mean (trainer_sr.py:161-163).  Device tensors are summed on
+    their device (no host synchronisation per step); result() reads the total."""
 
     def __init__(self, name=''):
         self.name = name
@@ -26,29 +27,38 @@ class Mean:
         self.count = 0
 
     def update_state(self, values):
-        v = torch.as_tensor(values).detach().double().reshape(-1)
-        self.total += float(v.sum())
-        self.count += v.numel()
+        if torch.is_tensor(values):
+            v = values.detach()
+            self.total = self.total + v.sum(dtype=torch.float64)
+            self.count += v.numel()
+        else:
+            v = torch.as_tensor(values, dtype=torch.float64).reshape(-1)
+            self.total = self.total + float(v.sum())
+            self.count += v.numel()
+
+    def _total(self):
+        return float(self.total) if torch.is_tensor(self.total) else self.total
 
     def result(self):
-        return self.total / self.count if self.count else 0.0
+        return self._total() / self.count if self.count else 0.0
 
 
 class Sum(Mean):
     """tf.keras.metrics.Sum (trainer_sr.py:164)."""
 
     def result(self):
-        return self.total
+        return self._total()
 
 
 def _crop(feats, inp_len):
-    """trainer_sr.py:59-60: crop the padded batch to the longest utterance."""
+    """trainer_sr.py:59-60: crop the padded batch to the longest utterance.  With
+    host-resident lengths (what the data pipeline yields) this needs no device sync."""
     T = int(inp_len.max())
-    return feats[:, :T, :].contiguous()
+    return feats if T == feats.shape[1] else feats[:, :T, :].contiguous()
 
 
 def ceil_div(inp_len, div):
-    return (inp_len.to(torch.int64) + div - 1) // div
+    return torch.div(inp_len + (div - 1), div, rounding_mode='floor').to(torch.int32)
 
 
 def allreduce_grads(model):
@@ -61,17 +71,20 @@ def process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_s
     feats, labels, inp_len, tar_len = inputs
     batch = feats.shape[0]
     feats = _crop(feats, inp_len)
-    model.zero_grad()
+    host_len = inp_len
+    inp_len = inp_len.to(feats.device, non_blocking=True)
     y_pred = model(feats, input_lengths=inp_len, training=True)
-    pe_loss = ctc.ctc_loss(labels, y_pred, tar_len, ceil_div(inp_len, in_len_div), blank_index=blank_idx)
-    loss = pe_loss.sum() / float(batch * n_gpus)
-    loss.backward()
+    # loss = sum(nll) / (B * n_gpus): its logit gradient comes out of the CTC launch
+    # already scaled, and seeds the backward directly (no scalar autograd ops)
+    pe_loss, g_logits = ctc.ctc_loss_and_grad(labels, y_pred, tar_len, ceil_div(inp_len, in_len_div), blank_idx,
+                                              1.0 / float(batch * n_gpus))
+    y_pred.backward(g_logits)
     allreduce_grads(model)
     optimizer.apply_gradients(model)
     if loss_state is not None:
         loss_state.update_state(pe_loss)
     if frame_state is not None:
-        frame_state.update_state(inp_len.sum())
+        frame_state.update_state(host_len.sum())
     if samples is not None:
         samples.update_state(batch)
     return pe_loss

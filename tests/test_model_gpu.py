@@ -90,3 +90,55 @@ def test_train_step_runs_and_updates(cuda):
     assert not torch.equal(model.flat_params, p0)
     assert np.isfinite(loss_state.result())
     assert samples.result() == 4
+
+
+def test_backward_overwrites_every_gradient(cuda):
+    """The train step never zeroes grads: every parameter's gradient must be
+    written (not accumulated) by the backward kernels.  Poison the flat gradient
+    buffer, run one backward, and require every slice finite and equal to a
+    backward from zeroed grads."""
+    from srf_amd import ctc, trainer_sr
+    model, sh, z = _build('c2_mini', cuda)
+    feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
+    inp_len = torch.tensor(z['inp_len'], dtype=torch.int32, device=cuda)
+    labels = torch.tensor(z['labels'], device=cuda)
+    tar_len = torch.tensor(z['tar_len'], device=cuda)
+
+    def grads(poison):
+        model.flat_grad.fill_(float('nan') if poison else 0.0)
+        logits = model(feats, input_lengths=inp_len, training=True)
+        _, g = ctc.ctc_loss_and_grad(labels, logits, tar_len, trainer_sr.ceil_div(inp_len, 4), sh.class_n - 1,
+                                     1.0 / feats.shape[0])
+        logits.backward(g)
+        return {k: p.grad.detach().clone() for k, p in model.params.items()}
+
+    clean = grads(False)
+    poisoned = grads(True)
+    for k in clean:
+        assert torch.isfinite(poisoned[k]).all(), k
+        # equal up to float-atomic reassociation in the routing backward (an
+        # accumulation into stale values would be off by O(1) relative)
+        err = (poisoned[k] - clean[k]).abs().max().item()
+        assert err <= 1e-4 * clean[k].abs().max().item() + 1e-7, (k, err)
+
+
+def test_fused_loss_head_matches_autograd(cuda):
+    """ctc_loss_and_grad + logits.backward(g) == autograd of sum(nll)/B."""
+    from srf_amd import ctc, trainer_sr
+    model, sh, z = _build('c2_mini', cuda)
+    feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
+    inp_len = torch.tensor(z['inp_len'], dtype=torch.int32, device=cuda)
+    labels = torch.tensor(z['labels'], device=cuda)
+    tar_len = torch.tensor(z['tar_len'], device=cuda)
+    lens4 = trainer_sr.ceil_div(inp_len, 4)
+    model.zero_grad()
+    logits = model(feats, input_lengths=inp_len, training=True)
+    nll = ctc.ctc_loss(labels, logits, tar_len, lens4, blank_index=sh.class_n - 1)
+    (nll.sum() / feats.shape[0]).backward()
+    ref = model.flat_grad.clone()
+    model.zero_grad()
+    logits = model(feats, input_lengths=inp_len, training=True)
+    nll2, g = ctc.ctc_loss_and_grad(labels, logits, tar_len, lens4, sh.class_n - 1, 1.0 / feats.shape[0])
+    logits.backward(g)
+    assert torch.allclose(nll2, nll.detach())
+    assert (model.flat_grad - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
