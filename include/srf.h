@@ -55,6 +55,25 @@ int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B,
                      const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* ---- Sequential dynamic routing layer: window + pose transform + SDR -------
+ * Replaces tfsr/model/sequence_router_naive.py:162-170 (tf.while_loop over the
+ * frames) with body_context :231-245 and, for the last layer, pad_body_context
+ * :212-229; and their TF autodiff.  Frames of an utterance are routed in order,
+ * the previous frame's final v seeding the next frame's logits.  saved: the
+ * per-frame v (srf_route_sdr_saved_floats), written by the forward, read by the
+ * backward.  Returns SRF_EUNSUPPORTED when one frame's routing state exceeds a
+ * CU's LDS. */
+size_t srf_route_sdr_saved_floats(int B, int T, int J, int dout);
+size_t srf_route_sdr_fwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout);
+size_t srf_route_sdr_bwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters);
+int srf_route_sdr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                      int rpad, int J, int dout, int iters, int mask_first, float* v_out, float* saved,
+                      void* workspace, size_t workspace_bytes, void* stream);
+int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                      int rpad, int J, int dout, int iters, int mask_first, const float* saved, const float* g_v,
+                      float* g_emb, float* g_W, float* g_bias, void* workspace, size_t workspace_bytes,
+                      void* stream);
+
 /* ---- CNN front end (CapsulationLayer, tfsr/model/sequence_router.py:44-82) ---
  * feats [B][T][feat_dim] fp32 (already cropped to max(inp_len), trainer_sr.py:59-60),
  * inp_len [B] int32 (device).  Kernels [3][3][Cin][64] (kh, kw, cin, cout), as the

@@ -23,6 +23,11 @@ _SIGNATURES = {
     'srf_route_dr_bwd_workspace': (_c_size, [_c_int] * 10),
     'srf_route_dr_fwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _c_size, _vp]),
     'srf_route_dr_bwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    'srf_route_sdr_saved_floats': (_c_size, [_c_int] * 4),
+    'srf_route_sdr_fwd_workspace': (_c_size, [_c_int] * 8),
+    'srf_route_sdr_bwd_workspace': (_c_size, [_c_int] * 9),
+    'srf_route_sdr_fwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _vp, _vp, _c_size, _vp]),
+    'srf_route_sdr_bwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     'srf_cnnfe_out_dims': (_c_int, [_c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
     'srf_cnnfe_saved_bytes': (_c_size, [_c_int] * 4),
     'srf_cnnfe_fwd_workspace': (_c_size, [_c_int] * 4),

@@ -1,0 +1,540 @@
+// Windowed pose transform + sequential dynamic routing (SDR) for one capsule
+// layer, gfx950.  Replaces sequence_router_naive.py:162-170 (the tf.while_loop
+// over frames) with body_context :231-245 / pad_body_context :212-229, and its
+// autodiff.
+//
+// Frame t of an utterance is routed after frame t-1: its logits start from
+// <u_t, v_{t-1}> (v_{-1} = 0), then R iterations of
+//   b += <u, w> (+ mask), c = softmax_j(b), s = sum_i c u, v = squash(s)
+// with w = v_{t-1} in iteration 0 and the previous iteration's v after.  With
+// Vc^r = v_{t-1} + sum_{k<r} v^k the logits are b^r = <u, Vc^r> + (r+1) m, so
+// the backward is the DR backward of routing.hip with Vc^0 = v_{t-1} plus the
+// carried gradient dL/dv_{t-1} = sum_r gVc^r.
+//
+// Kernels:
+//   sdr_pose_kernel   u[f][i][row] = W_i x_i(f) + b_i for every frame (MFMA), the
+//                     frame-parallel part, kept in HBM for the sequential pass;
+//   sdr_fwd_kernel    one workgroup per utterance walks its frames in order;
+//   sdr_bwd_kernel    one workgroup per utterance walks them backwards,
+//                     recomputing each frame's iterations, and writes gu;
+//   sdr_gx_kernel     gx = W^T gu (MFMA) scattered into g_emb via the window adjoint;
+//   sdr_gw_kernel     gW = sum_f gu x^T (MFMA, K = frames); gbias = column sums of gu.
+// Layouts (HBM, fp32): emb [F][N][din]; W [in_n][J*Dout][din]; bias [in_n][J*Dout];
+// u, gu [F][in_n][J*Dout]; v [F][J*Dout].
+#include <algorithm>
+#include <cmath>
+
+#include "srf_common.h"
+#include "srf_reduce.h"
+#include "../../include/srf.h"
+
+namespace {
+
+constexpr float kSquashEps = 1e-7f;   // naive:248
+constexpr float kMaskLogit = -1e9f;   // naive:216-217
+constexpr int kSeqThreads = 256;
+
+struct SGeom {
+  int B, T, N, din, lpad, rpad, J, dout, iters, mask_first;
+  int F() const { return B * T; }
+  int in_n() const { return N * (lpad + rpad + 1); }
+  int JD() const { return J * dout; }
+  int NT() const { return (J * dout + 15) / 16; }
+};
+
+// ------------------------------------------------------------------ pose
+// Workgroup = 4 waves over one frame tile (16 frames) and one capsule i; wave w
+// takes row tiles w, w+4, ...  Operands as in the DR pass (k-permuted MFMA).
+template <int DIN>
+__global__ __launch_bounds__(256) void sdr_pose_kernel(const float* __restrict__ emb, const float* __restrict__ W,
+                                                       const float* __restrict__ bias, int F, int T, int N, int lpad,
+                                                       int in_n, int JD, float* __restrict__ u) {
+  constexpr int KS = DIN / 4;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int fl = lane & 15, g = lane >> 4;
+  const int i = blockIdx.y;
+  const int f = blockIdx.x * 16 + fl;
+  const int fc = min(f, F - 1);
+  const int b = fc / T, t = fc - b * T;
+  const int w = i / N, n = i - w * N;
+  const int ts = t + w - lpad;
+  const bool ok = f < F && ts >= 0 && ts < T;
+  float x[KS];
+  const float* xp = emb + ((size_t)(b * T + min(max(ts, 0), T - 1)) * N + n) * DIN + g * KS;
+#pragma unroll
+  for (int k = 0; k < KS; ++k) x[k] = ok ? xp[k] : 0.f;
+  const int NT = (JD + 15) / 16;
+  for (int tile = wv; tile < NT; tile += 4) {
+    const int arow = min(tile * 16 + fl, JD - 1);
+    const float* wp = W + ((size_t)i * JD + arow) * DIN + g * KS;
+    const int crow = min(tile * 16 + 4 * g, JD - 4);
+    f4 acc = *reinterpret_cast<const f4*>(bias + (size_t)i * JD + crow);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) acc = mfma16x16x4(wp[k], x[k], acc);
+    const int row = tile * 16 + 4 * g;
+    if (f < F && row < JD) *reinterpret_cast<f4*>(u + ((size_t)f * in_n + i) * JD + row) = acc;
+  }
+}
+
+// ------------------------------------------------------------------ shared helpers
+// Shared-memory views of the per-frame routing state.
+struct SeqSmem {
+  float* v;      // [JD]   agreement vector of the current iteration (carry at r = 0)
+  float* bl;     // [P]    logits b_ij (P = in_n*J)
+  float* c;      // [P]    couplings
+  float* s;      // [JD]
+  float* red;    // [2*in_n] softmax max / 1/sum per i
+};
+
+// b += <u, w> (+ mask); c = softmax_j(b); s = sum_i c u; v = squash(s).
+// On return sm.v holds v^r and sm.s holds s^r.
+__device__ __forceinline__ void sdr_iteration(const float* __restrict__ ut, const SeqSmem& sm, int in_n, int J,
+                                              int D, int mask_first, float* c_keep, float* s_keep) {
+  const int P = in_n * J, JD = J * D;
+  const int tid = threadIdx.x;
+  for (int p = tid; p < P; p += kSeqThreads) {
+    const int i = p / J, j = p - i * J;
+    const float* up = ut + (size_t)i * JD + j * D;
+    const float* vp = sm.v + j * D;
+    float d0 = 0.f, d1 = 0.f;
+    for (int d = 0; d < D; d += 4) {
+      const f4 a = *reinterpret_cast<const f4*>(up + d);
+      d0 += a.x * vp[d] + a.y * vp[d + 1];
+      d1 += a.z * vp[d + 2] + a.w * vp[d + 3];
+    }
+    sm.bl[p] += (d0 + d1) + ((mask_first && j == 0) ? kMaskLogit : 0.f);
+  }
+  __syncthreads();
+  for (int i = tid; i < in_n; i += kSeqThreads) {
+    float m = -INFINITY;
+    for (int j = 0; j < J; ++j) m = fmaxf(m, sm.bl[i * J + j]);
+    float z = 0.f;
+    for (int j = 0; j < J; ++j) z += __expf(sm.bl[i * J + j] - m);
+    const float iz = 1.f / z;
+    for (int j = 0; j < J; ++j) {
+      const float cv = __expf(sm.bl[i * J + j] - m) * iz;
+      sm.c[i * J + j] = cv;
+      if (c_keep) c_keep[i * J + j] = cv;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < JD; e += kSeqThreads) {
+    const int j = e / D;
+    float acc = 0.f;
+    for (int i = 0; i < in_n; ++i) acc += sm.c[i * J + j] * ut[(size_t)i * JD + e];
+    sm.s[e] = acc;
+    if (s_keep) s_keep[e] = acc;
+  }
+  __syncthreads();
+  for (int j = tid; j < J; j += kSeqThreads) {
+    float n2 = 0.f;
+    for (int d = 0; d < D; ++d) n2 += sm.s[j * D + d] * sm.s[j * D + d];
+    const float fac = n2 / (1.f + n2) / sqrtf(n2 + kSquashEps);
+    for (int d = 0; d < D; ++d) sm.v[j * D + d] = sm.s[j * D + d] * fac;
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ forward
+// One workgroup per utterance; v_out[f] = v^{R-1} of frame f.
+__global__ __launch_bounds__(kSeqThreads) void sdr_fwd_kernel(const float* __restrict__ u, int T, int in_n, int J,
+                                                              int D, int iters, int mask_first,
+                                                              float* __restrict__ v_out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int JD = J * D, P = in_n * J;
+  SeqSmem sm{smem, smem + JD, smem + JD + P, smem + JD + 2 * P, smem + 2 * JD + 2 * P};
+  const int b = blockIdx.x;
+  for (int e = threadIdx.x; e < JD; e += kSeqThreads) sm.v[e] = 0.f;   // v_{-1} = 0
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const size_t f = (size_t)b * T + t;
+    const float* ut = u + f * in_n * JD;
+    for (int p = threadIdx.x; p < P; p += kSeqThreads) sm.bl[p] = 0.f;
+    __syncthreads();
+    for (int r = 0; r < iters; ++r) sdr_iteration(ut, sm, in_n, J, D, mask_first, nullptr, nullptr);
+    for (int e = threadIdx.x; e < JD; e += kSeqThreads) v_out[f * JD + e] = sm.v[e];
+  }
+}
+
+size_t sdr_fwd_smem(int in_n, int J, int D) {
+  return (size_t)(3 * J * D + 2 * in_n * J + 2 * in_n) * sizeof(float);
+}
+
+// ------------------------------------------------------------------ backward
+// One workgroup per utterance, frames in reverse.  Per frame: recompute the R
+// iterations from v_{t-1} (keeping c^r, s^r, Vc^r), then for r = R-1..0
+//   gs^r = squash'(s^r)^T a^r with a^{R-1} = g_v[t] + carry and, below the top,
+//          a^{r-1} = sum_{r' >= r} gVc^{r'} (v^{r-1} reaches the loss only via later logits),
+//   q_ij = <u_ij, gs_j>, sigma_i = sum_j c_ij q_ij, gL_ij = c_ij (q_ij - sigma_i),
+//   gVc^r_j = sum_i gL_ij u_ij;
+// gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j, written to HBM; carry = sum_r gVc^r.
+struct BwdSmem {
+  float *v, *bl, *c, *s, *red;      // forward scratch (SeqSmem)
+  float *ck, *gl;                   // [R][P]
+  float *sk, *vck, *gsk;            // [R][JD]
+  float *acc, *carry, *gv;          // [JD]
+};
+
+__global__ __launch_bounds__(kSeqThreads) void sdr_bwd_kernel(const float* __restrict__ u,
+                                                              const float* __restrict__ v_saved,
+                                                              const float* __restrict__ g_v, int T, int in_n, int J,
+                                                              int D, int iters, int mask_first,
+                                                              float* __restrict__ gu) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int JD = J * D, P = in_n * J, R = iters;
+  const int tid = threadIdx.x;
+  BwdSmem bs;
+  float* q = smem;
+  bs.v = q; q += JD;
+  bs.bl = q; q += P;
+  bs.c = q; q += P;
+  bs.s = q; q += JD;
+  bs.red = q; q += 2 * in_n;
+  bs.ck = q; q += (size_t)R * P;
+  bs.gl = q; q += (size_t)R * P;
+  bs.sk = q; q += (size_t)R * JD;
+  bs.vck = q; q += (size_t)R * JD;
+  bs.gsk = q; q += (size_t)R * JD;
+  bs.acc = q; q += JD;
+  bs.carry = q; q += JD;
+  bs.gv = q; q += JD;
+  const SeqSmem sm{bs.v, bs.bl, bs.c, bs.s, bs.red};
+  const int b = blockIdx.x;
+  for (int e = tid; e < JD; e += kSeqThreads) bs.carry[e] = 0.f;
+  __syncthreads();
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t f = (size_t)b * T + t;
+    const float* ut = u + f * in_n * JD;
+    // ---- recompute the frame's iterations from v_{t-1}
+    for (int e = tid; e < JD; e += kSeqThreads) {
+      const float vp = t > 0 ? v_saved[(f - 1) * JD + e] : 0.f;
+      sm.v[e] = vp;
+      bs.vck[e] = vp;                               // Vc^0 = v_{t-1}
+      bs.acc[e] = g_v[f * JD + e] + bs.carry[e];   // dL/dv^{R-1}
+      bs.carry[e] = 0.f;
+    }
+    for (int p = tid; p < P; p += kSeqThreads) sm.bl[p] = 0.f;
+    __syncthreads();
+    for (int r = 0; r < R; ++r) {
+      sdr_iteration(ut, sm, in_n, J, D, mask_first, bs.ck + (size_t)r * P, bs.sk + (size_t)r * JD);
+      if (r + 1 < R) {
+        for (int e = tid; e < JD; e += kSeqThreads) bs.vck[(size_t)(r + 1) * JD + e] = bs.vck[(size_t)r * JD + e] + sm.v[e];
+        __syncthreads();
+      }
+    }
+    // ---- backward through the iterations; bs.acc holds dL/dv^r
+    for (int r = R - 1; r >= 0; --r) {
+      const float* sr = bs.sk + (size_t)r * JD;
+      float* gsr = bs.gsk + (size_t)r * JD;
+      for (int j = tid; j < J; j += kSeqThreads) {
+        float n2 = 0.f, sa = 0.f;
+        for (int d = 0; d < D; ++d) {
+          n2 += sr[j * D + d] * sr[j * D + d];
+          sa += sr[j * D + d] * bs.acc[j * D + d];
+        }
+        const float rs = 1.f / sqrtf(n2 + kSquashEps);
+        const float ip = 1.f / (1.f + n2);
+        const float gfac = n2 * ip * rs;
+        const float dg2 = 2.f * rs * ip * (ip - 0.5f * n2 / (n2 + kSquashEps)) * sa;
+        for (int d = 0; d < D; ++d) gsr[j * D + d] = gfac * bs.acc[j * D + d] + dg2 * sr[j * D + d];
+      }
+      __syncthreads();
+      // q_ij = <u_ij, gs_j> into gl (temporarily)
+      const float* cr = bs.ck + (size_t)r * P;
+      float* glr = bs.gl + (size_t)r * P;
+      for (int p = tid; p < P; p += kSeqThreads) {
+        const int i = p / J, j = p - i * J;
+        const float* up = ut + (size_t)i * JD + j * D;
+        float d0 = 0.f, d1 = 0.f;
+        for (int d = 0; d < D; d += 4) {
+          const f4 a = *reinterpret_cast<const f4*>(up + d);
+          d0 += a.x * gsr[j * D + d] + a.y * gsr[j * D + d + 1];
+          d1 += a.z * gsr[j * D + d + 2] + a.w * gsr[j * D + d + 3];
+        }
+        glr[p] = d0 + d1;
+      }
+      __syncthreads();
+      for (int i = tid; i < in_n; i += kSeqThreads) {
+        float sg = 0.f;
+        for (int j = 0; j < J; ++j) sg += cr[i * J + j] * glr[i * J + j];
+        for (int j = 0; j < J; ++j) glr[i * J + j] = cr[i * J + j] * (glr[i * J + j] - sg);
+      }
+      __syncthreads();
+      // gVc^r_j = sum_i gL_ij u_ij: the gradient of every v^k with k < r and of v_{t-1}
+      for (int e = tid; e < JD; e += kSeqThreads) {
+        const int j = e / D;
+        float g = 0.f;
+        for (int i = 0; i < in_n; ++i) g += glr[i * J + j] * ut[(size_t)i * JD + e];
+        bs.carry[e] += g;
+        // dL/dv^{r-1} = sum_{r' >= r} gVc^{r'} (v^{R-1} only reaches the loss directly)
+        bs.gv[e] = (r == R - 1) ? g : bs.gv[e] + g;
+        bs.acc[e] = bs.gv[e];
+      }
+      __syncthreads();
+    }
+    // ---- gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j
+    for (int idx = tid; idx < in_n * JD; idx += kSeqThreads) {
+      const int i = idx / JD, e = idx - i * JD, j = e / D;
+      float g = 0.f;
+      for (int r = 0; r < R; ++r)
+        g += bs.ck[(size_t)r * P + i * J + j] * bs.gsk[(size_t)r * JD + e] +
+             bs.gl[(size_t)r * P + i * J + j] * bs.vck[(size_t)r * JD + e];
+      gu[f * in_n * JD + idx] = g;
+    }
+    __syncthreads();
+  }
+}
+
+size_t sdr_bwd_smem(int in_n, int J, int D, int R) {
+  const size_t JD = (size_t)J * D, P = (size_t)in_n * J;
+  return (3 * JD + 2 * P + 2 * in_n + 2 * R * P + 3 * R * JD + 3 * JD) * sizeof(float);
+}
+
+// ------------------------------------------------------------------ gx, gW
+// gx^T[e][f] = sum_row W^T[i][e][row] gu[f][i][row] for one frame tile and capsule
+// (K = rows, float4 operands), scattered into g_emb through the window adjoint.
+template <int DIN>
+__global__ __launch_bounds__(64) void sdr_gx_kernel(const float* __restrict__ gu, const float* __restrict__ WT,
+                                                    int F, int T, int N, int lpad, int in_n, int JD,
+                                                    float* __restrict__ g_emb) {
+  constexpr int NCT = (DIN + 15) / 16;
+  const int lane = threadIdx.x, fl = lane & 15, g = lane >> 4;
+  const int i = blockIdx.y;
+  const int f = blockIdx.x * 16 + fl;
+  const int fc = min(f, F - 1);
+  f4 acc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) acc[ct] = f4{0.f, 0.f, 0.f, 0.f};
+  const float* bp = gu + ((size_t)fc * in_n + i) * JD + 4 * g;
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < JD; k0 += 16) {
+    const bool kin = k0 + 4 * g < JD;   // JD % 4 == 0: a float4 is wholly in or out
+    const f4 bv = kin ? *reinterpret_cast<const f4*>(bp + k0) : z4;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const int e = min(ct * 16 + fl, DIN - 1);
+      const f4 av = kin ? *reinterpret_cast<const f4*>(WT + ((size_t)i * DIN + e) * JD + k0 + 4 * g) : z4;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) acc[ct] = mfma16x16x4(av[kk], bv[kk], acc[ct]);
+    }
+  }
+  // C layout: col = frame (fl), rows e = ct*16 + 4g + k
+  const int b = fc / T, t = fc - b * T;
+  const int w = i / N, n = i - w * N;
+  const int ts = t + w - lpad;
+  if (f >= F || ts < 0 || ts >= T) return;
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = ct * 16 + 4 * g + k;
+      if (e < DIN) atomicAdd(g_emb + ((size_t)(b * T + ts) * N + n) * DIN + e, acc[ct][k]);
+    }
+}
+
+// W [in_n][JD][din] -> WT [in_n][din][JD]; the same launch zeroes g_emb.
+__global__ void sdr_transpose_w_kernel(const float* __restrict__ W, int in_n, int JD, int din,
+                                       float* __restrict__ WT, float* __restrict__ zero, size_t n_zero) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t nw = (size_t)in_n * JD * din;
+  if (idx >= nw) {
+    if (idx - nw < n_zero) zero[idx - nw] = 0.f;
+    return;
+  }
+  const int row = idx % JD;
+  const size_t rest = idx / JD;
+  const int e = rest % din;
+  const size_t i = rest / din;
+  WT[idx] = W[(i * JD + row) * din + e];
+}
+
+// gW[i][row][e] = sum_f gu[f][i][row] x_i(f)[e]: one wave per (i, row tile); K =
+// frames in steps of 4 (lane group g = frame), x read through the window.
+template <int DIN>
+__global__ __launch_bounds__(256) void sdr_gw_kernel(const float* __restrict__ gu, const float* __restrict__ emb,
+                                                     int F, int T, int N, int lpad, int in_n, int JD,
+                                                     float* __restrict__ gW) {
+  constexpr int NCT = (DIN + 15) / 16;
+  const int NT = (JD + 15) / 16;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int task = blockIdx.x * 4 + wv;
+  if (task >= in_n * NT) return;
+  const int i = task / NT, tg = task - i * NT;
+  const int row = min(tg * 16 + l16, JD - 1);
+  const int w = i / N, n = i - w * N;
+  f4 acc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) acc[ct] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int f0 = 0; f0 < F; f0 += 4) {
+    const int f = f0 + g;
+    const int fc = min(f, F - 1);
+    const float a = f < F ? gu[((size_t)fc * in_n + i) * JD + row] : 0.f;
+    const int b = fc / T, t = fc - b * T;
+    const int ts = t + w - lpad;
+    const bool ok = f < F && ts >= 0 && ts < T;
+    const float* xp = emb + ((size_t)(b * T + min(max(ts, 0), T - 1)) * N + n) * DIN;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      const float xv = ok ? xp[min(ct * 16 + l16, DIN - 1)] : 0.f;
+      acc[ct] = mfma16x16x4(a, xv, acc[ct]);
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int e = ct * 16 + l16;
+    if (e >= DIN) continue;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = tg * 16 + 4 * g + k;
+      if (r < JD) gW[((size_t)i * JD + r) * DIN + e] = acc[ct][k];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host
+int check_sgeom(const SGeom& g) {
+  SRF_REQUIRE(g.B > 0 && g.T > 0 && g.N > 0 && g.J > 1, "bad shape B=%d T=%d N=%d J=%d", g.B, g.T, g.N, g.J);
+  SRF_REQUIRE(g.lpad >= 0 && g.rpad >= 0, "negative window pad");
+  SRF_REQUIRE(g.iters >= 1 && g.iters <= 5, "routing iterations must be in [1,5], got %d", g.iters);
+  SRF_REQUIRE(g.din == 8 || g.din == 16 || g.din == 32 || g.din == 64, "unsupported in_d %d", g.din);
+  SRF_REQUIRE(g.dout % 4 == 0, "out_d must be a multiple of 4");
+  return SRF_OK;
+}
+
+int sdr_smem_check(size_t bytes) {
+  if (bytes > 160 * 1024) {
+    srf::set_error("SDR frame state (%zu B) exceeds the 160 KiB LDS of one CU", bytes);
+    return SRF_EUNSUPPORTED;
+  }
+  return SRF_OK;
+}
+
+template <int D>
+void launch_pose(const SGeom& g, const float* emb, const float* W, const float* bias, float* u, hipStream_t st) {
+  hipLaunchKernelGGL(sdr_pose_kernel<D>, dim3((g.F() + 15) / 16, g.in_n()), dim3(256), 0, st, emb, W, bias, g.F(),
+                     g.T, g.N, g.lpad, g.in_n(), g.JD(), u);
+}
+
+int pose_dispatch(const SGeom& g, const float* emb, const float* W, const float* bias, float* u, hipStream_t st) {
+  switch (g.din) {
+    case 8: launch_pose<8>(g, emb, W, bias, u, st); break;
+    case 16: launch_pose<16>(g, emb, W, bias, u, st); break;
+    case 32: launch_pose<32>(g, emb, W, bias, u, st); break;
+    default: launch_pose<64>(g, emb, W, bias, u, st); break;
+  }
+  SRF_LAUNCH_CHECK("sdr_pose");
+  return SRF_OK;
+}
+
+struct SdrBwdWs {
+  float *u, *gu, *WT, *scratch;
+  size_t bytes;
+};
+
+SdrBwdWs sdr_bwd_layout(const SGeom& g, void* base) {
+  const size_t FU = (size_t)g.F() * g.in_n() * g.JD();
+  size_t off = 0;
+  auto take = [&](size_t nfloat) {
+    size_t o = off;
+    off += srf::align_up(nfloat * sizeof(float), 256);
+    return o;
+  };
+  const size_t ou = take(FU), ogu = take(FU), owt = take((size_t)g.in_n() * g.JD() * g.din),
+               osc = take(srf::colsum_scratch_floats(g.F(), g.in_n() * g.JD()));
+  char* b = static_cast<char*>(base);
+  SdrBwdWs w;
+  w.u = (float*)(b + ou);
+  w.gu = (float*)(b + ogu);
+  w.WT = (float*)(b + owt);
+  w.scratch = (float*)(b + osc);
+  w.bytes = off;
+  return w;
+}
+
+template <int D>
+void launch_gx_gw(const SGeom& g, const float* emb, const SdrBwdWs& w, float* g_emb, float* g_W, hipStream_t st) {
+  hipLaunchKernelGGL(sdr_gx_kernel<D>, dim3((g.F() + 15) / 16, g.in_n()), dim3(64), 0, st, w.gu, w.WT, g.F(), g.T,
+                     g.N, g.lpad, g.in_n(), g.JD(), g_emb);
+  const int tasks = g.in_n() * g.NT();
+  hipLaunchKernelGGL(sdr_gw_kernel<D>, dim3((tasks + 3) / 4), dim3(256), 0, st, w.gu, emb, g.F(), g.T, g.N, g.lpad,
+                     g.in_n(), g.JD(), g_W);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t srf_route_sdr_saved_floats(int B, int T, int J, int dout) { return (size_t)B * T * J * dout; }
+
+size_t srf_route_sdr_fwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout) {
+  (void)din;
+  return srf::align_up((size_t)B * T * N * (lpad + rpad + 1) * J * dout * sizeof(float), 256);
+}
+
+size_t srf_route_sdr_bwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, iters, 0};
+  return sdr_bwd_layout(g, nullptr).bytes;
+}
+
+int srf_route_sdr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                      int rpad, int J, int dout, int iters, int mask_first, float* v_out, float* saved,
+                      void* workspace, size_t workspace_bytes, void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, iters, mask_first ? 1 : 0};
+  int rc = check_sgeom(g);
+  if (rc) return rc;
+  SRF_REQUIRE(emb && W && bias && v_out && saved && workspace, "null pointer argument");
+  if (workspace_bytes < srf_route_sdr_fwd_workspace(B, T, N, din, lpad, rpad, J, dout)) {
+    srf::set_error("SDR forward workspace too small");
+    return SRF_EWORKSPACE;
+  }
+  const size_t sm = sdr_fwd_smem(g.in_n(), J, dout);
+  if ((rc = sdr_smem_check(sm))) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* u = static_cast<float*>(workspace);
+  if ((rc = pose_dispatch(g, emb, W, bias, u, st))) return rc;
+  hipLaunchKernelGGL(sdr_fwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, u, T, g.in_n(), J, dout, iters,
+                     g.mask_first, v_out);
+  SRF_LAUNCH_CHECK("sdr_fwd");
+  SRF_HIP_TRY(hipMemcpyAsync(saved, v_out, (size_t)g.F() * g.JD() * sizeof(float), hipMemcpyDeviceToDevice, st));
+  return SRF_OK;
+}
+
+int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                      int rpad, int J, int dout, int iters, int mask_first, const float* saved, const float* g_v,
+                      float* g_emb, float* g_W, float* g_bias, void* workspace, size_t workspace_bytes,
+                      void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, iters, mask_first ? 1 : 0};
+  int rc = check_sgeom(g);
+  if (rc) return rc;
+  SRF_REQUIRE(emb && W && bias && saved && g_v && g_emb && g_W && g_bias && workspace, "null pointer argument");
+  const SdrBwdWs w = sdr_bwd_layout(g, workspace);
+  if (workspace_bytes < w.bytes) {
+    srf::set_error("SDR backward workspace too small");
+    return SRF_EWORKSPACE;
+  }
+  const size_t sm = sdr_bwd_smem(g.in_n(), J, dout, iters);
+  if ((rc = sdr_smem_check(sm))) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if ((rc = pose_dispatch(g, emb, W, bias, w.u, st))) return rc;
+  hipLaunchKernelGGL(sdr_bwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, w.u, saved, g_v, T, g.in_n(), J, dout,
+                     iters, g.mask_first, w.gu);
+  SRF_LAUNCH_CHECK("sdr_bwd");
+  {
+    const size_t n_emb = (size_t)g.F() * N * din;
+    const size_t total = (size_t)g.in_n() * g.JD() * din + n_emb;
+    hipLaunchKernelGGL(sdr_transpose_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, g.in_n(), g.JD(), din,
+                       w.WT, g_emb, n_emb);
+    SRF_LAUNCH_CHECK("sdr_transpose_w");
+  }
+  switch (din) {
+    case 8: launch_gx_gw<8>(g, emb, w, g_emb, g_W, st); break;
+    case 16: launch_gx_gw<16>(g, emb, w, g_emb, g_W, st); break;
+    case 32: launch_gx_gw<32>(g, emb, w, g_emb, g_W, st); break;
+    default: launch_gx_gw<64>(g, emb, w, g_emb, g_W, st); break;
+  }
+  SRF_LAUNCH_CHECK("sdr_gx_gw");
+  return srf::colsum(w.gu, g.F(), g.in_n() * g.JD(), g_bias, w.scratch, st);
+}
+
+}  // extern "C"

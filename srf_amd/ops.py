@@ -117,6 +117,52 @@ def dynamic_routing(emb, W, bias, geom):
     return DynamicRouting.apply(emb, W, bias, geom)
 
 
+class SequentialRouting(torch.autograd.Function):
+    """window -> pose -> SDR (frames routed in order, naive:162-170 with
+    body_context / pad_body_context), one layer.  emb [B,T,N,din] -> v [B,T,J,dout]."""
+
+    @staticmethod
+    def forward(ctx, emb, W, bias, geom):
+        g = geom
+        _check_dev('emb', emb, (g.B, g.T, g.N, g.din))
+        _check_dev('W', W, (g.in_n, g.J, g.dout, g.din))
+        _check_dev('bias', bias, (g.in_n, g.J, g.dout))
+        L = _lib.lib()
+        dev = emb.device
+        v = torch.empty((g.B, g.T, g.J, g.dout), device=dev, dtype=torch.float32)
+        saved = torch.empty(L.srf_route_sdr_saved_floats(g.B, g.T, g.J, g.dout), device=dev, dtype=torch.float32)
+        geo = (g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout)
+        ws_bytes = L.srf_route_sdr_fwd_workspace(*geo)
+        ws = torch.empty(ws_bytes, device=dev, dtype=torch.uint8)
+        rc = L.srf_route_sdr_fwd(_ptr(emb), _ptr(W), _ptr(bias), *geo, g.iters, g.mask_first, _ptr(v), _ptr(saved),
+                                 _ptr(ws), ws_bytes, _stream())
+        _lib.check(rc, 'srf_route_sdr_fwd')
+        ctx.geom = g
+        ctx.params = (W, bias)
+        ctx.save_for_backward(emb, W, bias, saved)
+        return v
+
+    @staticmethod
+    def backward(ctx, g_v):
+        emb, W, bias, saved = ctx.saved_tensors
+        g = ctx.geom
+        g_v = g_v.contiguous()
+        L = _lib.lib()
+        g_emb = torch.empty_like(emb)
+        tW, tb = _grad_target(ctx.params[0]), _grad_target(ctx.params[1])
+        geo = (g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout)
+        ws_bytes = L.srf_route_sdr_bwd_workspace(*geo, g.iters)
+        ws = torch.empty(ws_bytes, device=emb.device, dtype=torch.uint8)
+        rc = L.srf_route_sdr_bwd(_ptr(emb), _ptr(W), _ptr(bias), *geo, g.iters, g.mask_first, _ptr(saved),
+                                 _ptr(g_v), _ptr(g_emb), _ptr(tW[0]), _ptr(tb[0]), _ptr(ws), ws_bytes, _stream())
+        _lib.check(rc, 'srf_route_sdr_bwd')
+        return (g_emb, *_returned([tW, tb]), None)
+
+
+def sequential_routing(emb, W, bias, geom):
+    return SequentialRouting.apply(emb, W, bias, geom)
+
+
 # ---------------------------------------------------------------------------
 # CNN front end (CapsulationLayer)
 CNNFE_PARAMS = ('conv0a_kernel', 'conv0a_bias', 'conv0b_kernel', 'conv0b_bias', 'bn0_gamma', 'bn0_beta',

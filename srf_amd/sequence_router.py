@@ -196,8 +196,6 @@ class SequenceRouter(torch.nn.Module):
         if not torch.is_tensor(inp_len):
             inp_len = torch.as_tensor(inp_len)
         il32 = inp_len.to(device=feats.device, dtype=torch.int32).contiguous()
-        if self.is_context:
-            raise NotImplementedError('SDR (model-caps-context=True) routing kernel is not built in this revision')
         drop = bool(training) and self.dropout_enabled
         seed = self._next_seed() if drop else 0
         moving = [getattr(self, n) for n in ('bn0_moving_mean', 'bn0_moving_var', 'bn1_moving_mean',
@@ -209,7 +207,8 @@ class SequenceRouter(torch.nn.Module):
         B, T2 = emb.shape[:2]
         p_mid = self.inn_dropout if drop else 0.0
         for l in range(self.enc_num):
-            v = ops.dynamic_routing(emb, self.P(f'W{l}'), self.P(f'b{l}'), self._geom(l, B, T2))
+            route = ops.sequential_routing if self.is_context else ops.dynamic_routing
+            v = route(emb, self.P(f'W{l}'), self.P(f'b{l}'), self._geom(l, B, T2))
             if l < self.enc_num - 1:
                 emb = ops.CapsNorm.apply(v, self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'), training,
                                          p_mid, seed, l)

@@ -15,7 +15,7 @@ from tests.helpers import config_from_shape, load_model_fixture
 
 pytestmark = pytest.mark.gpu
 
-DR_FIXTURES = ['c1_mini', 'c2_mini']
+DR_FIXTURES = ['c1_mini', 'c2_mini', 'c3_mini_sdr']   # c3: SDR routing
 
 
 def _build(name, dev):

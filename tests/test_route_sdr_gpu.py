@@ -1,0 +1,101 @@
+"""GPU parity of the sequential dynamic routing layer (srf_route_sdr_fwd/bwd,
+through the C ABI) against the CPU oracle.
+
+Forward: numpy float64 restatement of sequence_router_naive.py:162-170 with
+body_context :231-245 / pad_body_context :212-229 (oracle/srf_oracle.py).
+Backward: float64 autograd of the op-for-op torch mirror (oracle/naive_mirror.py).
+Tolerances (fp32 kernel vs fp64 oracle): forward |err| <= 2e-5 * (1 + |ref|),
+gradients |err| <= 1e-4 * max(1, max|ref|) -- the carried agreement vector makes
+later frames depend on all earlier ones, so fp32 reassociation accumulates
+along the utterance.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import srf_oracle as so
+from oracle import naive_mirror as nm
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # B, T, N, D, lpad, rpad, J, iters, mask_first
+    (2, 9, 4, 16, 1, 1, 5, 3, True),      # small, last-layer mask
+    (1, 7, 8, 8, 2, 2, 16, 3, False),     # D = 8
+    (3, 6, 16, 32, 2, 2, 16, 3, False),   # C3 inner layer shape (short)
+    (2, 5, 16, 32, 2, 2, 32, 3, True),    # C3 last layer shape (short)
+    (2, 8, 3, 16, 0, 1, 7, 1, False),     # one iteration, asymmetric window
+    (1, 6, 2, 16, 1, 0, 4, 5, True),      # five iterations
+]
+
+
+def _mk(case, seed):
+    B, T, N, D, lp, rp, J, it, mf = case
+    rng = np.random.default_rng(seed)
+    in_n = N * (lp + rp + 1)
+    emb = rng.standard_normal((B, T, N, D)) * 0.5
+    W = rng.standard_normal((in_n, J, D, D)) * 0.1
+    bias = rng.standard_normal((in_n, J, D)) * 0.1
+    return emb, W, bias
+
+
+def _run_gpu(case, emb, W, bias, dev):
+    from srf_amd.ops import RouteGeom, sequential_routing
+    B, T, N, D, lp, rp, J, it, mf = case
+    g = RouteGeom(B, T, N, D, lp, rp, J, D, it, mf)
+    te = torch.tensor(emb, dtype=torch.float32, device=dev, requires_grad=True)
+    tW = torch.tensor(W, dtype=torch.float32, device=dev, requires_grad=True)
+    tb = torch.tensor(bias, dtype=torch.float32, device=dev, requires_grad=True)
+    return te, tW, tb, sequential_routing(te, tW, tb, g)
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_route_sdr_forward(cuda, case):
+    emb, W, bias = _mk(case, 11)
+    _, _, _, v = _run_gpu(case, emb, W, bias, cuda)
+    B, T, N, D, lp, rp, J, it, mf = case
+    ref = so.sequential_routing(so.pose(so.window(emb, lp, rp), W, bias), it, mf)
+    got = v.detach().cpu().double().numpy()
+    assert np.all(np.abs(got - ref) <= 2e-5 * (1 + np.abs(ref))), np.abs(got - ref).max()
+
+
+@pytest.mark.parametrize('case', CASES)
+def test_route_sdr_backward(cuda, case):
+    emb, W, bias = _mk(case, 12)
+    te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
+    gv = np.random.default_rng(13).standard_normal(v.shape)
+    v.backward(torch.tensor(gv, dtype=torch.float32, device=cuda))
+    B, T, N, D, lp, rp, J, it, mf = case
+    ce = torch.tensor(emb, requires_grad=True)
+    cW = torch.tensor(W, requires_grad=True)
+    cb = torch.tensor(bias, requires_grad=True)
+    ep = torch.nn.functional.pad(ce, (0, 0, 0, 0, lp, rp))
+    xw = torch.cat([ep[:, w:w + T] for w in range(lp + rp + 1)], dim=2)
+    vr = nm.sequential_routing(nm.pose_tiled(xw, cW, cb), it, mf)
+    vr.backward(torch.tensor(gv))
+    for name, got, ref in (('g_emb', te.grad, ce.grad), ('g_W', tW.grad, cW.grad), ('g_bias', tb.grad, cb.grad)):
+        got = got.cpu().double().numpy()
+        ref = ref.numpy()
+        err = np.abs(got - ref).max()
+        assert err <= 1e-4 * max(1.0, np.abs(ref).max()), (name, err, np.abs(ref).max())
+
+
+def test_route_sdr_rejects_oversized_frame_state(cuda):
+    """A frame whose routing state exceeds one CU's LDS is refused, not mis-run."""
+    from srf_amd import _lib
+    L = _lib.lib()
+    # C5-like last layer: in_n = 16*41, J = 32, D = 64, 5 iterations
+    B, T, N, D, lp, rp, J, it = 1, 2, 16, 64, 20, 20, 32, 5
+    dev = cuda
+    in_n = N * (lp + rp + 1)
+    emb = torch.zeros(B, T, N, D, device=dev)
+    W = torch.zeros(in_n, J, D, D, device=dev)
+    bias = torch.zeros(in_n, J, D, device=dev)
+    v = torch.empty(B, T, J, D, device=dev)
+    saved = torch.empty(B * T * J * D, device=dev)
+    wb = L.srf_route_sdr_fwd_workspace(B, T, N, D, lp, rp, J, D)
+    ws = torch.empty(wb, dtype=torch.uint8, device=dev)
+    rc = L.srf_route_sdr_fwd(emb.data_ptr(), W.data_ptr(), bias.data_ptr(), B, T, N, D, lp, rp, J, D, it, 1,
+                             v.data_ptr(), saved.data_ptr(), ws.data_ptr(), wb,
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == -3 and b'LDS' in L.srf_last_error()
