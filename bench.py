@@ -34,6 +34,7 @@ WORKLOADS = {
     # name: (config kwargs, class_n, per-GPU B, T)
     'timit_c2': (dict(enc=3, iters=3, lpad=4, rpad=4, ph=8, pd=16, ch=8, cd=16, vd=16, context=False), 63, 17, 320),
     'wsj_c4': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=False), 32, 28, 800),
+    'wsj_c3': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=True), 32, 28, 800),
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 HBM_PEAK_GBS = 8000.0
@@ -167,8 +168,10 @@ def main():
     last = model.enc_num - 1
     geom = model._geom(last, B, Tp)
     R = model.iter
-    ev_pairs = [(ev.create(R), ev.create(R)) for _ in range(args.steps)]
-    geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
+    dr = not model.is_context    # the event hook times DR passes; SDR runs no such pass
+    ev_pairs = [(ev.create(R), ev.create(R)) for _ in range(args.steps)] if dr else []
+    if dr:
+        geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
 
     if world > 1:
         dist.barrier()
@@ -187,7 +190,7 @@ def main():
         elapsed = float(t.item())
 
     kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
-    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
     in_n, J, D, Din = model.layer_shapes[last]
     frames_prime = B * Tp
     # algorithmic FLOPs per launch: the layer's pose contraction (once per
@@ -205,15 +208,16 @@ def main():
         'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic (N(0,1) 123-d fbank, random init)',
         'config': {'workload': f'{args.workload}: SRF L={cfg.model_encoder_num} PH=CH={cfg.model_caps_primary_num} '
-                               f'DIM={cfg.model_caps_primary_dim} LPAD=RPAD={cfg.model_caps_window_lpad} DR iter='
-                               f'{cfg.model_caps_iter}, train step (fwd+bwd+allreduce+Adam)',
+                               f'DIM={cfg.model_caps_primary_dim} LPAD=RPAD={cfg.model_caps_window_lpad} '
+                               f'{"SDR" if model.is_context else "DR"} iter={cfg.model_caps_iter}, '
+                               f'train step (fwd+bwd+allreduce+Adam)',
                    'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
                    'parallelism': f'dp{world}'},
-        'roofline': {'kernel': f'route_pass_kernel<16,16,8,FWD> (layer {last + 1} DR forward pass)', 'bound': 'mfma',
-                     'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+        'roofline': {'kernel': f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)',
+                     'bound': 'mfma', 'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
                      'avg_launch_us': round(kern_avg_ms * 1e3, 2),
-                     'flops_per_launch': flops_launch},
+                     'flops_per_launch': flops_launch} if dr else None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)
