@@ -430,7 +430,7 @@ template <int DIN, int DOUT, int TW, int R, bool LDSACC>
 __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
     const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ WT,
     const float* __restrict__ bias, int F, int Fp, int T, int N, int lpad, int rpad, int in_n, int J,
-    int mask_first, int n_wgroups, int n_chunks, int chunk_len, const float* __restrict__ saved,
+    int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
     const float* __restrict__ gs, const float* __restrict__ stats, float* __restrict__ gu_t,
     float* __restrict__ g_emb, int nslots_max) {
   constexpr int NCT = (DIN + 15) / 16;
@@ -449,14 +449,17 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
   const int f = ft * 16 + fl;
   const FrameLoc loc = frame_loc(f, F, T);
   const int tbase = __builtin_amdgcn_readfirstlane((wgrp * NW + wv) * TW);
-  const int i0 = chunk * chunk_len, i1 = min(in_n, i0 + chunk_len);
+  // i-chunk = input capsules (w, n) with n in [n0, n1) and every window offset w,
+  // visited w-major; capsule k of the chunk is i = w*N + n.
+  const int n0 = chunk * n_per, nn = min(N, n0 + n_per) - n0;
+  const int Wn = in_n / N;
+  const int ncap = Wn * nn;
+  auto cap = [&](int k) { return (k / nn) * N + n0 + k % nn; };
   const int Jeff = J - (mask_first ? 1 : 0);
-  const int ND = N * DIN;
   // Per-wave gx accumulators (no LDS atomics): frame slot s <-> emb frame
-  // ft*16 - lpad + w_lo + s; the stride ND + 4 keeps float4 rows bank-conflict free.
-  const int SROW = ND + 4;
-  const int w_lo = i0 / N;
-  const int nslots = 16 + (max(i1 - 1, i0) / N - w_lo);
+  // ft*16 - lpad + s, row (n - n0, e); the stride keeps float4 rows bank-conflict free.
+  const int SROW = n_per * DIN + 4;
+  const int nslots = 15 + Wn;
   float* gw_acc = gacc + (size_t)wv * nslots_max * SROW;
 
   if constexpr (LDSACC) {
@@ -496,17 +499,18 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
     }
   };
 
-  if (i0 < i1) {
+  if (ncap > 0) {
     Frags<DIN, TW> fr;
     f4 wt[NCT][TW];
     float logz[RV], sig[RV];
-    fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, i0, JD, NT, tbase, lane, fr);
-    for (int i = i0; i < i1; ++i) {
+    fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, cap(0), JD, NT, tbase, lane, fr);
+    for (int k = 0; k < ncap; ++k) {
+      const int i = cap(k);
       fetch_side(i, wt, logz, sig);
       float u[TW][4];
       pose_tiles<DIN, TW>(fr, u);
-      // operands of capsule i+1 are fetched now and land while capsule i is processed
-      const int inext = min(i + 1, i1 - 1);
+      // operands of the next capsule are fetched now and land while this one is processed
+      const int inext = cap(min(k + 1, ncap - 1));
       fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
       float ga[TW][4];
 #pragma unroll
@@ -561,7 +565,7 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
         for (int ct = 0; ct < NCT; ++ct) {
           if (ct * 16 + 4 * g >= DIN) continue;
           if constexpr (LDSACC) {
-            float* a = gw_acc + (fl + w - w_lo) * SROW + n * DIN + ct * 16 + 4 * g;
+            float* a = gw_acc + (fl + w) * SROW + (n - n0) * DIN + ct * 16 + 4 * g;
             st4(a, ld4(a) + gx[ct]);
           } else {
 #pragma unroll
@@ -574,13 +578,14 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
   }
   if constexpr (LDSACC) {
     __syncthreads();
-    const int f0 = ft * 16 - lpad + w_lo;
-    for (int k = threadIdx.x; k < nslots * ND; k += blockDim.x) {
-      const int slot = k / ND, rem = k - slot * ND;
+    const int f0 = ft * 16 - lpad;
+    const int row = nn * DIN;
+    for (int k = threadIdx.x; k < nslots * row; k += blockDim.x) {
+      const int slot = k / row, rem = k - slot * row;
       const int fo = f0 + slot;
       float v = 0.f;
       for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots_max + slot) * SROW + rem];
-      if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + (size_t)fo * ND + rem, v);
+      if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
     }
   }
 }
@@ -855,32 +860,27 @@ constexpr int kGuNW = 4;  // waves per gu workgroup
 
 inline int gu_wgroups(const Geom& g) { return (g.NT() + kGuNW * gu_tw(g.dout) - 1) / (kGuNW * gu_tw(g.dout)); }
 inline int padded_frames(const Geom& g) { return (g.F() + 15) / 16 * 16; }
-// Frame slots of the widest i-chunk's gx accumulator (16 + its window-offset span).
-inline int gu_nslots(const Geom& g, int chunk_len) {
-  int span = 0;
-  for (int i0 = 0; i0 < g.in_n(); i0 += chunk_len) {
-    const int i1 = std::min(g.in_n(), i0 + chunk_len);
-    span = std::max(span, (i1 - 1) / g.N - i0 / g.N);
-  }
-  return 16 + span;
-}
-inline size_t gu_lds_bytes(const Geom& g, int nw, int nslots) {
-  return (size_t)nw * nslots * (g.N * g.din + 4) * sizeof(float);
+inline int gu_window(const Geom& g) { return g.lpad + g.rpad + 1; }
+inline size_t gu_lds_bytes(const Geom& g, int nw, int n_per) {
+  return (size_t)nw * (15 + gu_window(g)) * (n_per * g.din + 4) * sizeof(float);
 }
 constexpr size_t kGuLdsMax = 64 * 1024;
 
-// i-chunks of the gu pass: fill ~4 workgroups per CU, then fewest capsules per workgroup.
-int gu_chunks(const Geom& g) {
+// gu i-chunks are ranges of n (all window offsets each): fill ~4 workgroups per CU,
+// then fewest capsules per workgroup, with the gx accumulator inside kGuLdsMax.
+int gu_n_per(const Geom& g, int nw) {
   const int base = (g.F() + 15) / 16 * gu_wgroups(g);
   const int slots = 256 * 4;
   int best = 1;
   double best_cost = 1e30;
-  for (int c = 1; c <= std::min(g.in_n(), 64); ++c) {
-    const int rounds = (base * c + slots - 1) / slots;
-    const double cost = (double)rounds * ((g.in_n() + c - 1) / c + 4);
+  for (int n_per = 1; n_per <= g.N; ++n_per) {
+    if (n_per > 1 && gu_lds_bytes(g, nw, n_per) > kGuLdsMax) break;
+    const int chunks = (g.N + n_per - 1) / n_per;
+    const int rounds = (base * chunks + slots - 1) / slots;
+    const double cost = (double)rounds * (gu_window(g) * n_per + 4);
     if (cost < best_cost) {
       best_cost = cost;
-      best = c;
+      best = n_per;
     }
   }
   return best;
@@ -891,20 +891,20 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
                const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
   const int n_ftiles = (g.F() + 15) / 16;
   const int n_wgroups = gu_wgroups(g);
-  const int n_chunks = gu_chunks(g);
-  const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
   constexpr int TW = gu_tw(D);
   const int nw = std::min(kGuNW, (g.NT() + TW - 1) / TW);
-  const int nslots = gu_nslots(g, chunk_len);
-  const size_t lds = gu_lds_bytes(g, nw, nslots);
+  const int n_per = gu_n_per(g, nw);
+  const int n_chunks = (g.N + n_per - 1) / n_per;
+  const int nslots = 15 + gu_window(g);
+  const size_t lds = gu_lds_bytes(g, nw, n_per);
   if (lds <= kGuLdsMax)
     hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, true>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
-                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb, nslots);
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots);
   else
     hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, false>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), 0, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
-                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, chunk_len, saved, gs, stats, gu_t, g_emb, nslots);
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots);
 }
 
 template <int D>
