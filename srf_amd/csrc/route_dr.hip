@@ -166,7 +166,9 @@ struct Frags {
   f4 b[TW];
 };
 
-template <int DIN, int TW>
+// NOBIAS: fragments without the bias (the accumulators start at 0); the
+// iteration-0 forward pass adds the i-chunk's bias sum once at the end instead.
+template <int DIN, int TW, bool NOBIAS = false>
 __device__ __forceinline__ void fetch_frags(const float* __restrict__ emb, const float* __restrict__ W,
                                             const float* __restrict__ bias, const FrameLoc& loc, int T, int N,
                                             int lpad, int i, int JD, int NT, int tbase, int lane,
@@ -188,7 +190,11 @@ __device__ __forceinline__ void fetch_frags(const float* __restrict__ emb, const
       brow = min(tc * 16 + 4 * g, JD - 4) - tc * 16;
     }
     load_vec<KS>(Wi + (size_t)tc * 16 * DIN + lrow * DIN + g * KS, fr.w[t]);
-    fr.b[t] = ld4(bi + tc * 16 + brow);
+    if constexpr (NOBIAS) {
+      fr.b[t] = f4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      fr.b[t] = ld4(bi + tc * 16 + brow);
+    }
   }
 }
 
@@ -231,7 +237,7 @@ __device__ __forceinline__ void pass_step(float (&u)[TW][4], Frags<DIN, TW>& fr,
   } else {
     pose_tiles<DIN, TW>(fr, u);
   }
-  fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
+  fetch_frags<DIN, TW, MODE == MODE_FWD && FIRST>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
   float c[TW];
   float gL[TW];
   if constexpr (MODE == MODE_FWD && FIRST) {
@@ -391,10 +397,11 @@ __global__ __launch_bounds__(512) void route_pass_kernel(
     constexpr int AHEAD = (MODE == MODE_FWD && DIN <= 16) ? 2 : 1;   // capsules between a fetch and its use
     Frags<DIN, TW> fr;
     float u[TW][4];
-    fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, i0, JD, NT, tbase, lane, fr);
+    constexpr bool NB = MODE == MODE_FWD && FIRST;
+    fetch_frags<DIN, TW, NB>(emb, W, bias, loc, T, N, lpad, i0, JD, NT, tbase, lane, fr);
     if constexpr (AHEAD == 2) {
       pose_tiles<DIN, TW>(fr, u);
-      fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, min(i0 + 1, i1 - 1), JD, NT, tbase, lane, fr);
+      fetch_frags<DIN, TW, NB>(emb, W, bias, loc, T, N, lpad, min(i0 + 1, i1 - 1), JD, NT, tbase, lane, fr);
     }
     for (int i = i0; i < i1; ++i) {
       pass_step<DIN, DOUT, TW, MODE, FIRST>(u, fr, st, red, parity, i, r, J, Jeff, mask_first, tbase, wv, NW, lane, in_n, f,
@@ -402,6 +409,18 @@ __global__ __launch_bounds__(512) void route_pass_kernel(
     }
   }
   if (!want_acc) return;
+  if constexpr (MODE == MODE_FWD && FIRST) {
+    // uniform couplings: the bias enters once, as c * (sum of the chunk's biases), gsv = that sum
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int j = tile_j<DOUT>(tbase + t, g);
+      const float c0 = (j < J && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+      float bs[4];
+      load_rows(gsv + (size_t)chunk * JD, 0, true, JD, tbase + t, g, bs);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) st.acc[t][k] += c0 * bs[k];
+    }
+  }
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
     const int row = (tbase + t) * 16 + 4 * g;
@@ -410,6 +429,18 @@ __global__ __launch_bounds__(512) void route_pass_kernel(
       st4(slab + ((size_t)chunk * F + f) * JD + row, v);
     }
   }
+}
+
+// bsum[c][row] = sum of bias[i][row] over the capsules i of i-chunk c.
+__global__ void bias_chunk_sum_kernel(const float* __restrict__ bias, int in_n, int JD, int n_chunks,
+                                      int chunk_len, float* __restrict__ bsum) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_chunks * JD) return;
+  const int c = idx / JD, row = idx - c * JD;
+  const int i0 = c * chunk_len, i1 = min(in_n, i0 + chunk_len);
+  float acc = 0.f;
+  for (int i = i0; i < i1; ++i) acc += bias[(size_t)i * JD + row];
+  bsum[idx] = acc;
 }
 
 // ---------------------------------------------------------------- gu pass
@@ -929,10 +960,17 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   const int nev = t_ev_n;
   t_ev_start = t_ev_stop = nullptr;
   t_ev_n = 0;
+  float* bsum = slab + (size_t)n_chunks * FJD;
+  {
+    const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
+    hipLaunchKernelGGL(bias_chunk_sum_kernel, dim3((n_chunks * g.JD() + 255) / 256), dim3(256), 0, st, bias,
+                       g.in_n(), g.JD(), n_chunks, chunk_len, bsum);
+    SRF_LAUNCH_CHECK("bias_chunk_sum");
+  }
   for (int r = 0; r < g.iters; ++r) {
     const float* vc = r > 0 ? saved + (size_t)(2 * (r - 1) + 1) * FJD : nullptr;
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev0[r], st));
-    dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, nullptr, slab, nullptr, 1, st);
+    dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, r == 0 ? bsum : nullptr, slab, nullptr, 1, st);
     SRF_LAUNCH_CHECK("route_pass(fwd)");
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev1[r], st));
     launch_fwd_finish<D>(g, slab, n_chunks, vc, saved + (size_t)(2 * r) * FJD, saved + (size_t)(2 * r + 1) * FJD,
@@ -1044,7 +1082,8 @@ size_t srf_route_dr_saved_floats(int B, int T, int J, int dout, int iters) {
 size_t srf_route_dr_fwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters,
                                   int n_chunks) {
   (void)N; (void)din; (void)lpad; (void)rpad; (void)iters;
-  return (size_t)n_chunks * B * T * J * dout * sizeof(float);
+  // partial slabs + the i-chunk bias sums of the iteration-0 pass
+  return (size_t)n_chunks * ((size_t)B * T + 1) * J * dout * sizeof(float);
 }
 
 size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters,
