@@ -37,6 +37,7 @@ WORKLOADS = {
     'wsj_c3': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=True), 32, 28, 800),
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak
 HBM_PEAK_GBS = 8000.0
 
 
@@ -192,6 +193,7 @@ def main():
     kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
     kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
     in_n, J, D, Din = model.layer_shapes[last]
+    fwd32 = Din in (8, 16) and D in (8, 16, 32) and J * D <= 1024 and os.environ.get('SRF_ROUTE_FWD32', '1') != '0'
     frames_prime = B * Tp
     # algorithmic FLOPs per launch: the layer's pose contraction (once per
     # forward, spread over its R pass launches) + one routing iteration
@@ -213,11 +215,20 @@ def main():
                                f'train step (fwd+bwd+allreduce+Adam)',
                    'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
                    'parallelism': f'dp{world}'},
-        'roofline': {'kernel': f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)',
+        'roofline': {'kernel': (f'route_fwd32_first_kernel + route_fwd32_kernel<{Din},{D}> (layer {last + 1} DR forward '
+                                f'passes, R={R}; pose on v_mfma_f32_32x32x16_bf16 as 3-term bf16 splits = fp32-accurate)'
+                                if fwd32 else f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)'),
                      'bound': 'mfma', 'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
                      'avg_launch_us': round(kern_avg_ms * 1e3, 2),
-                     'flops_per_launch': flops_launch} if dr else None,
+                     'flops_per_launch': flops_launch,
+                     # what the matrix cores execute: the full pose every pass, as 6 bf16 products
+                     # (+1 bias product) per fp32 product on the split path
+                     'executed_mfma': ({'dtype': 'bf16', 'peak_tflops': BF16_MFMA_PEAK_TFLOPS,
+                                        'frac': round(frames_prime * 2.0 * in_n * (J * D + 31) // 32 * 32 * Din
+                                                      * (7 if Din == 16 else 4) / (kern_avg_ms * 1e-3) / 1e12
+                                                      / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
+                    if dr else None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)

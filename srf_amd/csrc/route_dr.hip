@@ -20,6 +20,7 @@
 #include <cmath>
 
 #include "srf_common.h"
+#include "route_fwd32.h"
 #include "../../include/srf.h"
 
 namespace {
@@ -950,6 +951,14 @@ void launch_gu_r(const Geom& g, const float* emb, const float* W, const float* W
   }
 }
 
+// The 32x32 split-bf16 pass (route_fwd32.hip) serves the shapes it supports;
+// SRF_ROUTE_FWD32=0 in the environment selects route_pass_kernel instead (A/B runs).
+inline bool use_fwd32(const Geom& g) {
+  const char* e = getenv("SRF_ROUTE_FWD32");
+  if (e && e[0] == '0') return false;
+  return srf::fwd32_supported(g.din, g.dout, g.J);
+}
+
 template <int D>
 int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias, float* v_out,
              float* saved, float* slab, hipStream_t st) {
@@ -960,8 +969,14 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   const int nev = t_ev_n;
   t_ev_start = t_ev_stop = nullptr;
   t_ev_n = 0;
+  const bool p32 = use_fwd32(g);
+  srf::Fwd32Plan plan{};
   float* bsum = slab + (size_t)n_chunks * FJD;
-  {
+  if (p32) {
+    plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    const int rc = srf::fwd32_prepare(plan, emb, W, bias, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, slab, st);
+    if (rc) return rc;
+  } else {
     const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
     hipLaunchKernelGGL(bias_chunk_sum_kernel, dim3((n_chunks * g.JD() + 255) / 256), dim3(256), 0, st, bias,
                        g.in_n(), g.JD(), n_chunks, chunk_len, bsum);
@@ -970,10 +985,17 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   for (int r = 0; r < g.iters; ++r) {
     const float* vc = r > 0 ? saved + (size_t)(2 * (r - 1) + 1) * FJD : nullptr;
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev0[r], st));
-    dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, r == 0 ? bsum : nullptr, slab, nullptr, 1, st);
+    if (p32) {
+      const int rc = srf::fwd32_pass(plan, r == 0, slab, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout,
+                                     g.mask_first, vc, st);
+      if (rc) return rc;
+    } else {
+      dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, r == 0 ? bsum : nullptr, slab, nullptr, 1, st);
+    }
     SRF_LAUNCH_CHECK("route_pass(fwd)");
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev1[r], st));
-    launch_fwd_finish<D>(g, slab, n_chunks, vc, saved + (size_t)(2 * r) * FJD, saved + (size_t)(2 * r + 1) * FJD,
+    launch_fwd_finish<D>(g, p32 ? srf::fwd32_slab(plan, slab) : slab, p32 ? plan.n_chunks : n_chunks, vc,
+                         saved + (size_t)(2 * r) * FJD, saved + (size_t)(2 * r + 1) * FJD,
                          r == g.iters - 1 ? v_out : nullptr, st);
     SRF_LAUNCH_CHECK("fwd_finish");
   }
@@ -1081,9 +1103,13 @@ size_t srf_route_dr_saved_floats(int B, int T, int J, int dout, int iters) {
 
 size_t srf_route_dr_fwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters,
                                   int n_chunks) {
-  (void)N; (void)din; (void)lpad; (void)rpad; (void)iters;
+  (void)iters;
   // partial slabs + the i-chunk bias sums of the iteration-0 pass
-  return (size_t)n_chunks * ((size_t)B * T + 1) * J * dout * sizeof(float);
+  size_t need = (size_t)n_chunks * ((size_t)B * T + 1) * J * dout * sizeof(float);
+  Geom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  if (use_fwd32(g))
+    need = std::max(need, srf::fwd32_workspace(srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout)));
+  return need;
 }
 
 size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters,

@@ -1,0 +1,724 @@
+// DR routing forward pass on 32x32 tiles with fp32-accurate split-bf16 MFMA, gfx950.
+//
+// Replaces, like route_dr.hip's route_pass_kernel, the forward routing iteration of
+// sequence_router_naive.py:171-185 / _loop_body :199-206 (pose :154-159 recomputed
+// per pass, window :150-151).  This variant is the forward pass for din in {8, 16}
+// and dout in {8, 16, 32} with J*dout <= 1024 (BASELINE C1 and C2); other shapes
+// keep route_pass_kernel.
+//
+// Pose product.  u = W x + b is formed on v_mfma_f32_32x32x16_bf16 from 3-term
+// bf16 splits a = a1 + a2 + a3 (a1 = bf16(a), a2 = bf16(a - a1), a3 = bf16(a - a1 - a2)),
+// keeping the six products whose size is >= 2^-18 |a b|:
+//     W x ~ W1x1 + W1x2 + W2x1 + W2x2 + W1x3 + W3x1      (dropped terms <= 2^-26 |W x|)
+// and the bias through one more MFMA against a ones column (b1 + b2 + b3 exact to
+// 2^-27).  bf16 x bf16 products are exact in the fp32 accumulator, so the pose is
+// as accurate as an fp32 FMA chain (tests/test_route_dr_gpu.py holds it to the
+// same tolerances) at 6/16 of the fp32 MFMA time.
+//
+// Tiles.  A workgroup owns 32 frames x all J*dout rows (32-row tiles, TW per wave)
+// and an i-chunk of input capsules.  Lane l holds frame (l & 31) and, per tile,
+// the 16 rows 8q + 4h + (0..3) (q = 0..3, h = l >> 5) of the MFMA's C/D map.  A
+// lane therefore holds a whole 4- or 8-row piece of each output capsule, so the
+// agreement logit of a capsule needs ONE cross-half exchange: v_permlane32_swap
+// reduce-scatters two capsules' partial dots at once and leaves each lane half
+// the logit of one of them.  Softmax over j: per-lane stats -> lane-half combine
+// -> per-wave stats through LDS (one barrier per input capsule).  Vc (the
+// agreement vector, naive:205 by linearity) lives in each wave's private LDS slab
+// in fragment order (conflict-free ds_read_b128).
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <algorithm>
+
+#include "srf_common.h"
+#include "route_fwd32.h"
+
+// Timing-experiment variants (never in the shipped build): 1 = no next-capsule
+// loads, 2 = no cross-wave exchange, 3 = no softmax (acc += u only),
+// 4 = s_memtime phase breakdown printed by two waves.
+#ifndef SRF_FWD32_DBG
+#define SRF_FWD32_DBG 0
+#endif
+// 1: issue the next capsule's loads right after the MFMAs (they then wait for the
+// queued MFMAs to read their operand registers); 0: after the softmax barrier.
+#ifndef SRF_FWD32_FETCH_EARLY
+#define SRF_FWD32_FETCH_EARLY 0
+#endif
+
+namespace {
+
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v mfma32(const bf8& a, const bf8& b, const f16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+
+// ------------------------------------------------------------------ splits
+// a -> (a1, a2, a3), each round-to-nearest bf16.
+__device__ __forceinline__ void split3(float a, __bf16& a1, __bf16& a2, __bf16& a3) {
+  a1 = (__bf16)a;
+  const float r = a - (float)a1;
+  a2 = (__bf16)r;
+  a3 = (__bf16)(r - (float)a2);
+}
+
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+
+// 8 consecutive floats -> their three bf16 planes (16 bytes each)
+__device__ __forceinline__ void split8(const float* __restrict__ src, bool ok, __bf16* d1, __bf16* d2, __bf16* d3) {
+  f4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
+  if (ok) {
+    lo = *reinterpret_cast<const f4*>(src);
+    hi = *reinterpret_cast<const f4*>(src + 4);
+  }
+  const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  bf8v p1, p2, p3;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    __bf16 a1, a2, a3;
+    split3(v[k], a1, a2, a3);
+    p1[k] = a1;
+    p2[k] = a2;
+    p3[k] = a3;
+  }
+  *reinterpret_cast<bf8v*>(d1) = p1;
+  *reinterpret_cast<bf8v*>(d2) = p2;
+  *reinterpret_cast<bf8v*>(d3) = p3;
+}
+
+// One launch prepares every operand of a forward (thread ranges in this order):
+//   W [in_n][JD][din]   -> Ws [3][in_n][JDp][din] bf16 planes (rows past JD = 0), 8 per thread;
+//   bias [in_n][JD]     -> bs [in_n][JDp][4] = (b1, b2, b3, 0);
+//   bsum[c][row]        =  sum of bias[i][row] over the capsules of i-chunk c (iteration-0 pass);
+//   emb [F][N][din]     -> xs [3][plane], plane = [N][F][din] capsule-major + 16 zeros.
+struct PrepArgs {
+  const float *W, *bias, *emb;
+  __bf16 *Ws, *bs, *xs;
+  float* bsum;
+  int in_n, JD, JDp, din, n_chunks, chunk_len, F, N;
+  size_t xplane;
+  size_t n_a, n_b, n_c, n_d;   // thread counts of the four ranges
+};
+
+__global__ void prep32_kernel(PrepArgs P) {
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < P.n_a) {
+    const size_t e0 = idx * 8;
+    const int e = e0 % P.din;
+    const size_t rr = e0 / P.din;
+    const int row = rr % P.JDp;
+    const size_t i = rr / P.JDp;
+    const size_t nw = (size_t)P.in_n * P.JDp * P.din;
+    split8(P.W + (i * P.JD + min(row, P.JD - 1)) * P.din + e, row < P.JD, P.Ws + e0, P.Ws + nw + e0,
+           P.Ws + 2 * nw + e0);
+    return;
+  }
+  idx -= P.n_a;
+  if (idx < P.n_b) {
+    const int row = idx % P.JDp;
+    const size_t i = idx / P.JDp;
+    const float b = row < P.JD ? P.bias[i * P.JD + row] : 0.f;
+    __bf16 b1, b2, b3;
+    split3(b, b1, b2, b3);
+    bf4 v = {b1, b2, b3, (__bf16)0.f};
+    *reinterpret_cast<bf4*>(P.bs + idx * 4) = v;
+    return;
+  }
+  idx -= P.n_b;
+  if (idx < P.n_c) {
+    const int c = idx / P.JD, row = idx - (size_t)c * P.JD;
+    const int i0 = c * P.chunk_len, i1 = min(P.in_n, i0 + P.chunk_len);
+    float acc = 0.f;
+    for (int i = i0; i < i1; ++i) acc += P.bias[(size_t)i * P.JD + row];
+    P.bsum[idx] = acc;
+    return;
+  }
+  idx -= P.n_c;
+  if (idx < P.n_d) {
+    const size_t e0 = idx * 8;
+    const size_t n_data = (size_t)P.F * P.N * P.din;
+    const int e = e0 % P.din;
+    const size_t rr = e0 / P.din;
+    const int f = rr % P.F;
+    const int n = rr / P.F;
+    const bool ok = e0 < n_data;
+    split8(P.emb + ((size_t)(ok ? f : 0) * P.N + (ok ? n : 0)) * P.din + (ok ? e : 0), ok, P.xs + e0,
+           P.xs + P.xplane + e0, P.xs + 2 * P.xplane + e0);
+  }
+}
+
+// ------------------------------------------------------------------ fragments
+// Per input capsule: A fragments (W splits) per tile, the bias fragment per tile,
+// B fragments (x splits) shared by the tiles.
+//   DIN 16: one MFMA covers din; A_p = W plane p (k = 8h + j), B_q = x plane q.
+//   DIN  8: K = 16 packs two planes: A1 = [W1 | W2], A2 = [W1 | W3],
+//           B1 = [x1 | x1], B2 = [x2 | x2], B3 = [x3 | x1] (lane half h holds k = 8h..8h+7):
+//           A1 B1 = W1x1 + W2x1, A1 B2 = W1x2 + W2x2, A2 B3 = W1x3 + W3x1.
+// Bias: A = (b1, b2, b3, 0, 0, 0, 0, 0) of the row, B = ones at k = 0..2 of lane
+// half 0 and zero elsewhere, so only (b1 + b2 + b3) reaches the accumulator.
+// All operands come through buffer loads: one descriptor per array, the per-lane
+// byte offset in voffset (fixed per tile), the per-capsule / per-plane offset in
+// soffset.  Invalid window frames read the zero row at the end of each x plane.
+#ifndef SRF_FWD32_TW
+#define SRF_FWD32_TW 4
+#endif
+constexpr int kTW = SRF_FWD32_TW;        // 32-row tiles per wave
+constexpr int kMaxNW = 32 / kTW;         // J*dout <= 1024
+constexpr int kWavesPerEU = 8 / kTW;
+
+template <int DIN>
+struct SplitFrags {
+  static constexpr int NA = DIN == 16 ? 3 : 2;
+};
+
+template <int DIN, int TW>
+struct Frags32 {
+  bf8 a[TW][SplitFrags<DIN>::NA];
+  bf8 bias[TW];
+  bf8 b[3];
+};
+
+struct Rsrc3 {
+  __amdgpu_buffer_rsrc_t w, b, x;
+};
+
+__device__ __forceinline__ bf8 bload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(bf8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+
+// Window source of capsule i = w*N + n for this lane (naive:150-151): frame
+// t + w - lpad of the same utterance, i.e. row f + w - lpad of capsule n's plane,
+// or the zero row when it falls outside [0, T).
+template <int DIN>
+__device__ __forceinline__ uint32_t x_voff(int i, int N, int lpad, int T, int F, int f, int ft, bool fvalid, int h,
+                                           uint32_t zero_off) {
+  const int w = i / N, n = i - w * N;
+  const int ts = ft + w - lpad;
+  const bool ok = fvalid && ts >= 0 && ts < T;
+  const uint32_t o = (uint32_t)(((n * F + f + w - lpad) * DIN) * 2 + (DIN == 16 ? 16 * h : 0));
+  return ok ? o : zero_off;
+}
+
+template <int DIN, int TW, bool BIAS>
+__device__ __forceinline__ void fetch32(const Rsrc3& rs, uint32_t wvo, uint32_t bvo, uint32_t xvo, int h,
+                                        uint32_t wplane_b, uint32_t xplane_b, uint32_t wcap_b, uint32_t bcap_b,
+                                        Frags32<DIN, TW>& fr) {
+  constexpr uint32_t TSTEP = 32 * DIN * 2;   // bytes between row tiles
+  if constexpr (DIN == 16) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fr.b[p] = bload(rs.x, xvo, p * xplane_b);
+  } else {
+    fr.b[0] = bload(rs.x, xvo, 0);
+    fr.b[1] = bload(rs.x, xvo, xplane_b);
+    fr.b[2] = bload(rs.x, xvo + (h == 0 ? 2 * xplane_b : 0), 0);   // [x3 | x1]: lane-dependent plane
+  }
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const uint32_t vo = wvo + t * TSTEP;
+    if constexpr (DIN == 16) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fr.a[t][p] = bload(rs.w, vo, wcap_b + p * wplane_b);
+    } else {
+      // lane half 1 reads plane 2 / plane 3 through a voffset shift
+      fr.a[t][0] = bload(rs.w, vo + (h ? wplane_b : 0), wcap_b);
+      fr.a[t][1] = bload(rs.w, vo + (h ? 2 * wplane_b : 0), wcap_b);
+    }
+    if constexpr (BIAS) {
+      // (b1, b2, b3, 0) of the row; the upper half of the fragment stays zero
+      const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap_b, 0);
+      fr.bias[t] = __builtin_bit_cast(bf8, (unsigned __attribute__((ext_vector_type(4)))){v2[0], v2[1], 0u, 0u});
+    }
+  }
+}
+
+template <int DIN>
+__device__ __forceinline__ f16v pose_chain(const bf8 (&a)[SplitFrags<DIN>::NA], const bf8 (&b)[3], f16v acc) {
+  if constexpr (DIN == 16) {   // small terms first
+    acc = mfma32(a[2], b[0], acc);   // W3 x1
+    acc = mfma32(a[0], b[2], acc);   // W1 x3
+    acc = mfma32(a[1], b[1], acc);   // W2 x2
+    acc = mfma32(a[1], b[0], acc);   // W2 x1
+    acc = mfma32(a[0], b[1], acc);   // W1 x2
+    acc = mfma32(a[0], b[0], acc);   // W1 x1
+  } else {
+    acc = mfma32(a[1], b[2], acc);   // W1 x3 + W3 x1
+    acc = mfma32(a[0], b[1], acc);   // W1 x2 + W2 x2
+    acc = mfma32(a[0], b[0], acc);   // W1 x1 + W2 x1
+  }
+  return acc;
+}
+
+// ones column of the bias MFMA: k = 0, 1, 2 of lane half 0
+__device__ __forceinline__ bf8 ones_frag(int h) {
+  const __bf16 o = (__bf16)(h == 0 ? 1.f : 0.f), z = (__bf16)0.f;
+  bf8 v = {o, o, o, z, z, z, z, z};
+  return v;
+}
+
+// capsule partial k of a wave's tile t / register v (rows 8(v>>2) + 4h + (v&3))
+template <int DOUT>
+__device__ __forceinline__ constexpr int kpart(int t, int v) {
+  return DOUT == 8 ? 4 * t + (v >> 2) : DOUT == 16 ? 2 * t + (v >> 3) : t;
+}
+
+struct Args32 {
+  const __bf16 *Ws, *bs, *xs;
+  size_t ws_bytes, bs_bytes, xs_bytes;
+  uint32_t wplane_b, xplane_b, zero_off;
+  int F, T, N, lpad, in_n, J, JDp, n_chunks, chunk_len, mask_first, n_tgroups;
+  const float* vc;
+  const float* bsum;
+  float* slab;
+};
+
+// ------------------------------------------------------------------ kernels
+// Iteration-0 pass (naive:172-181: logits 0 + mask, so c is uniform):
+// s = c0 (sum_i W_i x_i + sum_i b_i).  A pure GEMM: each wave owns
+// (32 frames, kFTW row tiles, i-chunk) and accumulates the pose sum in its MFMA
+// accumulators; the chunk's bias sum is added at the end.  Operands are double
+// buffered: capsule k+1's loads are issued before capsule k's MFMAs, into the
+// registers capsule k-1 used, so no load waits on a queued MFMA's operand read.
+constexpr int kFTW = 2;
+
+template <int DIN>
+struct FirstFrags {
+  bf8 a[kFTW][SplitFrags<DIN>::NA];
+  bf8 b[3];
+};
+
+template <int DIN>
+__device__ __forceinline__ void fetch_first(const Rsrc3& rs, uint32_t wvo, uint32_t xvo, int h, uint32_t wplane_b,
+                                            uint32_t xplane_b, uint32_t wcap_b, FirstFrags<DIN>& fr) {
+  constexpr uint32_t TSTEP = 32 * DIN * 2;
+  if constexpr (DIN == 16) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fr.b[p] = bload(rs.x, xvo, p * xplane_b);
+  } else {
+    fr.b[0] = bload(rs.x, xvo, 0);
+    fr.b[1] = bload(rs.x, xvo, xplane_b);
+    fr.b[2] = bload(rs.x, xvo + (h == 0 ? 2 * xplane_b : 0), 0);
+  }
+#pragma unroll
+  for (int t = 0; t < kFTW; ++t) {
+    const uint32_t vo = wvo + t * TSTEP;
+    if constexpr (DIN == 16) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fr.a[t][p] = bload(rs.w, vo, wcap_b + p * wplane_b);
+    } else {
+      fr.a[t][0] = bload(rs.w, vo + (h ? wplane_b : 0), wcap_b);
+      fr.a[t][1] = bload(rs.w, vo + (h ? 2 * wplane_b : 0), wcap_b);
+    }
+  }
+}
+
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void route_fwd32_first_kernel(Args32 A) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int chunk = task % A.n_chunks;
+  const int rest = task / A.n_chunks;
+  const int tg = rest % A.n_tgroups, ft = rest / A.n_tgroups;
+  if (ft * 32 >= A.F) return;
+  const int tbase = tg * kFTW;
+  const int JD = A.J * DOUT;
+  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+  const int f = ft * 32 + r;
+  const int fc = min(f, A.F - 1);
+  const int fb = fc / A.T, ftt = fc - fb * A.T;
+  const bool fv = f < A.F;
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
+  const uint32_t capb = (uint32_t)A.JDp * DIN * 2;
+  f16v acc[kFTW];
+#pragma unroll
+  for (int t = 0; t < kFTW; ++t) acc[t] = f16v{};
+  auto fetch = [&](int i, FirstFrags<DIN>& fr) {
+    fetch_first<DIN>(rs, wvo, x_voff<DIN>(i, A.N, A.lpad, A.T, A.F, f, ftt, fv, h, A.zero_off), h, A.wplane_b,
+                     A.xplane_b, (uint32_t)i * capb, fr);
+  };
+  auto mfmas = [&](const FirstFrags<DIN>& fr) {
+#pragma unroll
+    for (int t = 0; t < kFTW; ++t) acc[t] = pose_chain<DIN>(fr.a[t], fr.b, acc[t]);
+  };
+  if (i0 < i1) {
+    FirstFrags<DIN> f0, f1;
+    fetch(i0, f0);
+    int i = i0;
+    for (; i + 1 < i1; i += 2) {
+      fetch(i + 1, f1);
+      mfmas(f0);
+      if (i + 2 < i1) fetch(i + 2, f0);
+      mfmas(f1);
+    }
+    if (i < i1) mfmas(f0);
+  }
+  const int Jeff = A.J - (A.mask_first ? 1 : 0);
+#pragma unroll
+  for (int t = 0; t < kFTW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      const int j = row / DOUT;
+      const float c0 = (j < A.J && !(A.mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+      if (fv && row < JD) {
+        const f4 bsv = *reinterpret_cast<const f4*>(A.bsum + (size_t)chunk * JD + row);
+        f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = (v + bsv) * c0;
+      }
+    }
+}
+
+// Routing pass r >= 1.  grid: n_ftiles * n_chunks (chunk = blockIdx % n_chunks);
+// block: NW waves of kTW row tiles.  LDS: NW * kTW * 4 KiB of Vc fragments, then
+// 2 x NW x 32 float2 of per-wave softmax stats.
+template <int DIN, int DOUT, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesPerEU))) void route_fwd32_kernel(Args32 A) {
+  constexpr int TW = kTW;
+  constexpr int CP = TW * 32 / DOUT;   // capsule partials per lane
+  constexpr int OWN = CP / 2;          // capsules whose logit this lane owns
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int JD = A.J * DOUT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int ft = blockIdx.x / A.n_chunks, chunk = blockIdx.x - ft * A.n_chunks;
+  const int f = ft * 32 + r;
+  const int fc = min(f, A.F - 1);
+  const int fb = fc / A.T, ftt = fc - fb * A.T;
+  const bool fvalid = f < A.F;
+  const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
+  const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
+  const int j0 = tbase * 32 / DOUT;
+  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
+
+  f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
+  float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
+  // Vc rows of this wave's tiles -> private LDS in fragment order
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (fvalid && row < JD) v = *reinterpret_cast<const f4*>(A.vc + (size_t)f * JD + row);
+      vcl[(t * 4 + q) * 64 + lane] = v;
+    }
+  // owned-capsule masks: 0 or -inf added to the logit
+  float mk[OWN];
+#pragma unroll
+  for (int a = 0; a < OWN; ++a) {
+    const int j = j0 + 2 * a + h;
+    mk[a] = (j < A.J && !(A.mask_first && j == 0)) ? 0.f : -INFINITY;
+  }
+  const bf8 ones = ones_frag(h);
+  f16v acc[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) acc[t] = f16v{};
+  int par = 0;
+  if (i0 < i1) {
+    Frags32<DIN, TW> fr;
+    fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8, fr);
+#if SRF_FWD32_DBG == 4
+    unsigned long long tph[5] = {0, 0, 0, 0, 0};
+    unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#define SRF_TMARK(k) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); tph[k] += tn - tlast; tlast = tn; }
+#else
+#define SRF_TMARK(k)
+#endif
+    for (int i = i0; i < i1; ++i) {
+      f16v u[TW];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
+      SRF_TMARK(0)
+      if (SRF_FWD32_FETCH_EARLY && i + 1 < i1)
+        fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                               A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
+                               (uint32_t)(i + 1) * A.JDp * 8, fr);
+      if (SRF_FWD32_FETCH_EARLY) __builtin_amdgcn_sched_barrier(0);
+      // partial agreement dots <u_ij, Vc_j> over this lane's rows (packed FMA pairs)
+      f2 P2[CP];
+#pragma unroll
+      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 vv = vcl[(t * 4 + q) * 64 + lane];
+          const int k = kpart<DOUT>(t, 4 * q);
+          P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv.x, vv.y};
+          P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv.z, vv.w};
+        }
+      // reduce-scatter over lane halves: half h owns capsule partial 2a + h
+      float L[OWN], e[OWN];
+      float m = -1e30f;
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        const float pa = P2[2 * a].x + P2[2 * a].y, pb = P2[2 * a + 1].x + P2[2 * a + 1].y;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa), __float_as_uint(pb), false, false);
+        L[a] = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + mk[a];
+        m = fmaxf(m, L[a]);
+      }
+      float z = 0.f;
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        e[a] = __expf(L[a] - m);
+        z += e[a];
+      }
+      // combine the two lane halves (same order on both: bit-identical)
+      float M, Z;
+      {
+        float m0, m1, z0, z1;
+        xpair32(m, m0, m1);
+        xpair32(z, z0, z1);
+        M = fmaxf(m0, m1);
+        Z = z0 * __expf(m0 - M) + z1 * __expf(m1 - M);
+      }
+      if constexpr (SRF_FWD32_DBG == 3) {
+#pragma unroll
+        for (int t = 0; t < TW; ++t) acc[t] += u[t];
+        continue;
+      }
+      if constexpr (NW > 1 && SRF_FWD32_DBG != 2) {
+        // per-wave stats of the 32 frames -> LDS; half h combines waves [h*NW/2, (h+1)*NW/2)
+        float2* slot = st + par * NW * 32;
+        if (h == 0) slot[wv * 32 + r] = make_float2(M, Z);
+        SRF_TMARK(2)
+        __syncthreads();
+        SRF_TMARK(3)
+        constexpr int HW = NW / 2;
+        float2 sv[HW];
+#pragma unroll
+        for (int w = 0; w < HW; ++w) sv[w] = slot[(h * HW + w) * 32 + r];
+        float mh = sv[0].x;
+#pragma unroll
+        for (int w = 1; w < HW; ++w) mh = fmaxf(mh, sv[w].x);
+        float zh = 0.f;
+#pragma unroll
+        for (int w = 0; w < HW; ++w) zh += sv[w].y * __expf(sv[w].x - mh);
+        float m0, m1, z0, z1;
+        xpair32(mh, m0, m1);
+        xpair32(zh, z0, z1);
+        const float MM = fmaxf(m0, m1);
+        Z = z0 * __expf(m0 - MM) + z1 * __expf(m1 - MM);
+        M = MM;
+        par ^= 1;
+      }
+      // next capsule's operands: issued once every MFMA result has been consumed
+      // (the dots), so no load waits on a queued MFMA's operand read
+      __builtin_amdgcn_sched_barrier(0);
+      if (!SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
+        fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                               A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
+                               (uint32_t)(i + 1) * A.JDp * 8, fr);
+      __builtin_amdgcn_sched_barrier(0);
+      SRF_TMARK(1)
+      // c = exp(L - M) / Z = e * exp(m - M) / Z; then all-gather over the halves
+      const float sc = __expf(m - M) / Z;
+      float c[CP];
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        float c0, c1;
+        xpair32(e[a] * sc, c0, c1);
+        c[2 * a] = c0;
+        c[2 * a + 1] = c1;
+      }
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const float cv = c[kpart<DOUT>(t, v)];
+          f2 a2 = {acc[t][v], acc[t][v + 1]};
+          a2 += f2{cv, cv} * f2{u[t][v], u[t][v + 1]};
+          acc[t][v] = a2.x;
+          acc[t][v + 1] = a2.y;
+        }
+      SRF_TMARK(4)
+    }
+#if SRF_FWD32_DBG == 4
+    if (lane == 0 && (blockIdx.x == 100 || blockIdx.x == 7) && (wv == 0 || wv == NW - 1))
+      printf("fwd32 blk %d wv %d caps %d: mfma-issue %llu loads-issue %llu softmax1 %llu barrier %llu softmax2+acc %llu\n",
+             blockIdx.x, wv, i1 - i0, tph[0], tph[1], tph[2], tph[3], tph[4]);
+#endif
+  }
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      if (fvalid && row < JD) {
+        f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v;
+      }
+    }
+}
+
+
+}  // namespace
+
+namespace srf {
+
+bool fwd32_supported(int din, int dout, int J) {
+  return (din == 8 || din == 16) && (dout == 8 || dout == 16 || dout == 32) && din <= dout &&
+         J * dout <= 32 * kTW * kMaxNW && (J * dout) % 8 == 0;
+}
+
+Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout) {
+  Fwd32Plan p;
+  const int in_n = N * (lpad + rpad + 1);
+  const int JD = J * dout;
+  const int NT = (JD + 31) / 32;
+  p.NW = 1;
+  while (p.NW * kTW < NT) p.NW *= 2;
+  p.JDp = p.NW * kTW * 32;
+  const int F = B * T;
+  const int n_ftiles = (F + 31) / 32;
+  // one workgroup per CU when NW > 1 (the Vc slabs fill most of the LDS);
+  // single-wave workgroups: up to 4 per CU.
+  const int slots = p.NW > 1 ? 256 : 1024;
+  int best = 1;
+  double best_cost = 1e30;
+  const char* env = getenv("SRF_FWD32_CHUNKS");
+  const int forced = env ? atoi(env) : 0;
+  for (int c = 1; c <= std::min(in_n, 96); ++c) {
+    const int rounds = (n_ftiles * c + slots - 1) / slots;
+    const int len = (in_n + c - 1) / c;
+    double cost = (double)rounds * (len + 3) * (1.0 + 0.002 * c);
+    if (forced > 0) cost = (c == std::min(forced, in_n)) ? 0.0 : 1.0;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  p.n_chunks = best;
+  p.chunk_len = (in_n + best - 1) / best;
+  p.n_ftiles = n_ftiles;
+  p.xplane = (size_t)F * N * din + 16;
+  p.ws_w = srf::align_up((size_t)3 * in_n * p.JDp * din * 2, 256);
+  p.ws_b = srf::align_up((size_t)in_n * p.JDp * 4 * 2, 256);
+  p.ws_x = srf::align_up((size_t)3 * p.xplane * 2, 256);
+  p.ws_bsum = srf::align_up((size_t)best * JD * 4, 256);
+  p.ws_slab = srf::align_up((size_t)best * F * JD * 4, 256);
+  return p;
+}
+
+float* fwd32_slab(const Fwd32Plan& p, void* ws) {
+  return reinterpret_cast<float*>(static_cast<char*>(ws) + p.ws_w + p.ws_b + p.ws_x + p.ws_bsum);
+}
+
+size_t fwd32_workspace(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x + p.ws_bsum + p.ws_slab; }
+
+size_t fwd32_lds(const Fwd32Plan& p) {
+  return (size_t)p.NW * kTW * 4 * 64 * 16 + (p.NW > 1 ? (size_t)2 * 32 * p.NW * 8 : 0);
+}
+
+int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
+                  int din, int lpad, int rpad, int J, int dout, void* ws, hipStream_t st) {
+  char* base = static_cast<char*>(ws);
+  PrepArgs P;
+  P.W = W;
+  P.bias = bias;
+  P.emb = emb;
+  P.Ws = reinterpret_cast<__bf16*>(base);
+  P.bs = reinterpret_cast<__bf16*>(base + p.ws_w);
+  P.xs = reinterpret_cast<__bf16*>(base + p.ws_w + p.ws_b);
+  P.bsum = reinterpret_cast<float*>(base + p.ws_w + p.ws_b + p.ws_x);
+  P.in_n = N * (lpad + rpad + 1);
+  P.JD = J * dout;
+  P.JDp = p.JDp;
+  P.din = din;
+  P.n_chunks = p.n_chunks;
+  P.chunk_len = p.chunk_len;
+  P.F = B * T;
+  P.N = N;
+  P.xplane = p.xplane;
+  P.n_a = (size_t)P.in_n * p.JDp * din / 8;
+  P.n_b = (size_t)P.in_n * p.JDp;
+  P.n_c = (size_t)p.n_chunks * P.JD;
+  P.n_d = p.xplane / 8;
+  const size_t total = P.n_a + P.n_b + P.n_c + P.n_d;
+  hipLaunchKernelGGL(prep32_kernel, dim3((total + 255) / 256), dim3(256), 0, st, P);
+  SRF_LAUNCH_CHECK("prep32");
+  return SRF_OK;
+}
+
+template <int DIN, int DOUT, int NW>
+static int launch_rpass(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
+  const size_t lds = fwd32_lds(p);
+  auto kern = route_fwd32_kernel<DIN, DOUT, NW>;
+  if (lds > 64 * 1024)
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a);
+  SRF_LAUNCH_CHECK("route_fwd32");
+  return SRF_OK;
+}
+
+template <int DIN, int DOUT>
+static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipStream_t st) {
+  if (first) {
+    Args32 b = a;
+    b.n_tgroups = p.JDp / (32 * kFTW);
+    const int tasks = p.n_ftiles * b.n_tgroups * p.n_chunks;
+    hipLaunchKernelGGL((route_fwd32_first_kernel<DIN, DOUT>), dim3((tasks + 3) / 4), dim3(256), 0, st, b);
+    SRF_LAUNCH_CHECK("route_fwd32_first");
+    return SRF_OK;
+  }
+  switch (p.NW) {
+    case 1: return launch_rpass<DIN, DOUT, 1>(p, a, st);
+    case 2: return launch_rpass<DIN, DOUT, 2>(p, a, st);
+    case 4: return launch_rpass<DIN, DOUT, 4>(p, a, st);
+    case 8: return launch_rpass<DIN, DOUT, 8>(p, a, st);
+    default: return launch_rpass<DIN, DOUT, kMaxNW>(p, a, st);
+  }
+}
+
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
+               int J, int dout, int mask_first, const float* vc, hipStream_t st) {
+  const int in_n = N * (lpad + rpad + 1);
+  const char* base = static_cast<const char*>(ws);
+  Args32 a;
+  a.Ws = reinterpret_cast<const __bf16*>(base);
+  a.bs = reinterpret_cast<const __bf16*>(base + p.ws_w);
+  a.xs = reinterpret_cast<const __bf16*>(base + p.ws_w + p.ws_b);
+  a.ws_bytes = p.ws_w;
+  a.bs_bytes = (size_t)in_n * p.JDp * 8;
+  a.xs_bytes = 3 * p.xplane * 2;
+  a.wplane_b = (uint32_t)((size_t)in_n * p.JDp * din * 2);
+  a.xplane_b = (uint32_t)(p.xplane * 2);
+  a.zero_off = (uint32_t)((p.xplane - 16) * 2);
+  a.F = B * T;
+  a.T = T;
+  a.N = N;
+  a.lpad = lpad;
+  a.in_n = in_n;
+  a.J = J;
+  a.JDp = p.JDp;
+  a.n_chunks = p.n_chunks;
+  a.chunk_len = p.chunk_len;
+  a.mask_first = mask_first;
+  a.n_tgroups = p.NW;
+  a.vc = vc;
+  a.bsum = reinterpret_cast<const float*>(base + p.ws_w + p.ws_b + p.ws_x);
+  a.slab = fwd32_slab(p, const_cast<void*>(ws));
+  SRF_REQUIRE(3 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
+#define SRF_P32(DI, DO) \
+  if (din == DI && dout == DO) return launch_pass32_t<DI, DO>(p, first, a, st);
+  SRF_P32(8, 8)
+  SRF_P32(8, 16)
+  SRF_P32(8, 32)
+  SRF_P32(16, 16)
+  SRF_P32(16, 32)
+#undef SRF_P32
+  srf::set_error("fwd32: unsupported din %d dout %d", din, dout);
+  return SRF_EUNSUPPORTED;
+}
+
+}  // namespace srf

@@ -25,6 +25,8 @@ CASES = [
     (1, 5, 3, 16, 1, 2, 5, 2, True),      # ragged odd sizes
     (1, 5, 2, 64, 1, 1, 4, 2, True),      # C5-width capsules (DIM=64)
     (2, 7, 4, 8, 1, 1, 6, 5, False),      # 5 routing iterations
+    (3, 37, 8, 16, 4, 4, 63, 3, True),    # several 32-frame tiles, ragged last tile
+    (2, 21, 4, 8, 2, 1, 12, 3, False),    # din 8 -> dout 8 with a partial 32-row tile
 ]
 
 
@@ -91,3 +93,17 @@ def test_route_dr_chunking_invariant(cuda):
         outs.append(v.detach().cpu().numpy())
     assert np.abs(outs[0] - outs[1]).max() < 1e-5
     assert np.abs(outs[0] - outs[2]).max() < 1e-5
+
+
+@pytest.mark.parametrize('case', [(3, 37, 8, 16, 4, 4, 63, 3, True), (2, 19, 8, 16, 4, 4, 8, 3, False),
+                                  (1, 33, 4, 8, 0, 0, 63, 1, True)])
+def test_route_dr_fwd32_matches_fp32_mfma_path(cuda, case, monkeypatch):
+    """The split-bf16 32x32 forward (route_fwd32.hip) against the exact-fp32
+    16x16x4 MFMA forward (route_pass_kernel): same routing to fp32 accuracy."""
+    emb, W, bias = _mk(case, 5)
+    _, _, _, v32 = _run_gpu(case, emb, W, bias, cuda)
+    monkeypatch.setenv('SRF_ROUTE_FWD32', '0')
+    _, _, _, v16 = _run_gpu(case, emb, W, bias, cuda)
+    a = v32.detach().cpu().double().numpy()
+    b = v16.detach().cpu().double().numpy()
+    assert np.all(np.abs(a - b) <= 1e-5 * (1 + np.abs(b))), np.abs(a - b).max()
