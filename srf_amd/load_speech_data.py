@@ -1,0 +1,381 @@
+"""TF-free speech input pipeline with the reference's dataset surface.
+
+Mirrors tfsr/data/load_speech_data.py (create_ds :24-115, finalize_ds :118-126,
+create_ds_batch_for_test :129-147, create_ds_batch_for_train :150-161,
+create_ds_bucket :164-181, map_data_for_transformer_fn :184-198) on top of the
+C++ TFRecord / tf.train.Example codec in ``libsrf_data.so`` (include/srf_data.h).
+
+A dataset here is a re-iterable object; iterating it yields tuples of numpy
+arrays in the reference's element structure:
+  * ``create_ds``: (inputs [T*F] f32, targets [L] i64, input_length i64, target_length i64[, utt_id bytes]);
+  * batched datasets: the same components padded to the longest element of the
+    batch (zeros), as ``padded_batch`` does;
+  * ``map(map_data_for_transformer_fn, feat_dim)``: ([B, T, F] f32, [B, L] i32, [B] i32, [B] i32).
+
+Order semantics: with shuffle=False the order is deterministic (files sorted,
+records interleaved round-robin with block length 1, as tf.data interleave
+visits its cycle).  The reference interleaves with deterministic=False and
+shuffles with unseeded TF RNGs, so shuffled orders are equal in distribution,
+not in sequence; ``seed`` makes ours reproducible.
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+DATA_LIB_PATH = os.environ.get('SRF_DATA_LIB_PATH') or os.path.join(_HERE, 'libsrf_data.so')
+
+
+class SpeechExample(ctypes.Structure):
+    _fields_ = [('input_speech', ctypes.POINTER(ctypes.c_float)), ('n_input_speech', ctypes.c_int64),
+                ('target_label', ctypes.POINTER(ctypes.c_int64)), ('n_target_label', ctypes.c_int64),
+                ('input_length', ctypes.c_int64), ('target_length', ctypes.c_int64),
+                ('utt_id', ctypes.c_void_p), ('utt_id_len', ctypes.c_int64)]
+
+
+_vp, _sz = ctypes.c_void_p, ctypes.c_size_t
+_SIGNATURES = {
+    'srf_data_last_error': (ctypes.c_char_p, []),
+    'srf_crc32c': (ctypes.c_uint32, [_vp, _sz]),
+    'srf_crc32c_masked': (ctypes.c_uint32, [_vp, _sz]),
+    'srf_tfr_open': (_vp, [ctypes.c_char_p, ctypes.c_int]),
+    'srf_tfr_next': (ctypes.c_int, [_vp, ctypes.POINTER(SpeechExample)]),
+    'srf_tfr_record': (ctypes.POINTER(ctypes.c_uint8), [_vp, ctypes.POINTER(_sz)]),
+    'srf_tfr_close': (ctypes.c_int, [_vp]),
+    'srf_example_parser_new': (_vp, []),
+    'srf_example_parse': (ctypes.c_int, [_vp, _vp, _sz, ctypes.POINTER(SpeechExample)]),
+    'srf_tfr_writer_open': (_vp, [ctypes.c_char_p]),
+    'srf_tfr_write_example': (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64]),
+    'srf_tfr_write_record': (ctypes.c_int, [_vp, _vp, _sz]),
+    'srf_tfr_writer_close': (ctypes.c_int, [_vp]),
+}
+
+_lib = None
+
+
+class TFRecordError(IOError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(DATA_LIB_PATH):
+            raise ImportError(f'{DATA_LIB_PATH} is missing: build it with `make -C srf_amd/csrc`')
+        h = ctypes.CDLL(DATA_LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def _err(what, rc=None):
+    msg = lib().srf_data_last_error().decode(errors='replace')
+    return TFRecordError(f'{what} failed{"" if rc is None else f" (rc={rc})"}: {msg}')
+
+
+def _to_numpy(ex, with_utt):
+    feats = np.ctypeslib.as_array(ex.input_speech, (ex.n_input_speech,)).copy() if ex.n_input_speech else \
+        np.zeros(0, np.float32)
+    labels = np.ctypeslib.as_array(ex.target_label, (ex.n_target_label,)).copy() if ex.n_target_label else \
+        np.zeros(0, np.int64)
+    out = (feats, labels, np.int64(ex.input_length), np.int64(ex.target_length))
+    if with_utt:
+        utt = ctypes.string_at(ex.utt_id, ex.utt_id_len) if ex.utt_id else b''
+        out = out + (utt,)
+    return out
+
+
+def read_tfrecord(path, is_utt_id=False, verify_crc=True):
+    """Yield the parsed speech Examples of one TFRecord file, in file order."""
+    L = lib()
+    h = L.srf_tfr_open(path.encode(), 1 if verify_crc else 0)
+    if not h:
+        raise _err('srf_tfr_open')
+    try:
+        ex = SpeechExample()
+        while True:
+            rc = L.srf_tfr_next(h, ctypes.byref(ex))
+            if rc == 1:
+                return
+            if rc != 0:
+                raise _err(f'reading {path}', rc)
+            yield _to_numpy(ex, is_utt_id)
+    finally:
+        L.srf_tfr_close(h)
+
+
+def parse_example(serialized, is_utt_id=True):
+    """tf.io.parse_single_example with the reference's feature spec."""
+    L = lib()
+    h = L.srf_example_parser_new()
+    try:
+        buf = ctypes.create_string_buffer(bytes(serialized), len(serialized))
+        ex = SpeechExample()
+        rc = L.srf_example_parse(h, buf, len(serialized), ctypes.byref(ex))
+        if rc != 0:
+            raise _err('parse_example', rc)
+        return _to_numpy(ex, is_utt_id)
+    finally:
+        L.srf_tfr_close(h)
+
+
+class TFRecordWriter:
+    """tf.io.TFRecordWriter for speech Examples (save_speech_data.py:119-120,178-186)."""
+
+    def __init__(self, path):
+        self._h = lib().srf_tfr_writer_open(path.encode())
+        if not self._h:
+            raise _err('srf_tfr_writer_open')
+
+    def write_example(self, input_speech, target_label, input_length=None, target_length=None, utt_id=None):
+        feats = np.ascontiguousarray(np.asarray(input_speech, np.float32).reshape(-1))
+        labels = np.ascontiguousarray(np.asarray(target_label, np.int64).reshape(-1))
+        if input_length is None:
+            input_length = np.asarray(input_speech).shape[0]
+        if target_length is None:
+            target_length = labels.size
+        if isinstance(utt_id, str):
+            utt_id = utt_id.encode('utf-8')
+        rc = lib().srf_tfr_write_example(self._h, feats.ctypes.data, feats.size, labels.ctypes.data, labels.size,
+                                         int(input_length), int(target_length), utt_id,
+                                         len(utt_id) if utt_id is not None else 0)
+        if rc != 0:
+            raise _err('write_example', rc)
+
+    def write(self, record):
+        buf = ctypes.create_string_buffer(bytes(record), len(record))
+        rc = lib().srf_tfr_write_record(self._h, buf, len(record))
+        if rc != 0:
+            raise _err('write', rc)
+
+    def close(self):
+        if self._h:
+            lib().srf_tfr_writer_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def tfrecord_shard_paths(data_path, tfrecord_dir, data_name, tf_record_name, feat_type, feat_dim, total_shards):
+    """Shard file names of save_speech_data.py:103-109."""
+    return [os.path.join(data_path + '/' + tfrecord_dir,
+                         '%s-%s-%s-%d-%.5d-of-%.5d' % (data_name, tf_record_name, feat_type, feat_dim, k + 1,
+                                                       total_shards)) for k in range(total_shards)]
+
+
+# ---------------------------------------------------------------- datasets
+class Dataset:
+    """A re-iterable element stream with the few tf.data transformations the
+    reference pipeline uses."""
+
+    def __init__(self, gen_fn):
+        self._gen_fn = gen_fn
+
+    def __iter__(self):
+        return iter(self._gen_fn())
+
+    def map(self, fn, *args):
+        src = self
+        return Dataset(lambda: (fn(*el, *args) for el in src))
+
+    def filter(self, pred):
+        src = self
+        return Dataset(lambda: (el for el in src if pred(*el)))
+
+    def cache(self):
+        src = self
+        store = []
+
+        def gen():
+            if store and store[-1] is _DONE:
+                yield from store[:-1]
+                return
+            store.clear()
+            for el in src:
+                store.append(el)
+                yield el
+            store.append(_DONE)
+        return Dataset(gen)
+
+    def shuffle(self, buffer_size, seed=None):
+        src = self
+        state = {'epoch': 0}
+
+        def gen():
+            rng = np.random.default_rng(None if seed is None else seed + state['epoch'])
+            state['epoch'] += 1
+            buf = []
+            for el in src:
+                if len(buf) < buffer_size:
+                    buf.append(el)
+                    continue
+                k = int(rng.integers(len(buf)))
+                yield buf[k]
+                buf[k] = el
+            while buf:
+                yield buf.pop(int(rng.integers(len(buf))))
+        return Dataset(gen)
+
+    def repeat(self, count=None):
+        src = self
+
+        def gen():
+            k = 0
+            while count is None or count < 0 or k < count:
+                yield from src
+                k += 1
+        return Dataset(gen)
+
+    def prefetch(self, buffer_size=None):
+        return self
+
+    def padded_batch(self, batch_size, drop_remainder=False):
+        src = self
+
+        def gen():
+            batch = []
+            for el in src:
+                batch.append(el)
+                if len(batch) == batch_size:
+                    yield pad_batch(batch)
+                    batch = []
+            if batch and not drop_remainder:
+                yield pad_batch(batch)
+        return Dataset(gen)
+
+    def bucket_by_sequence_length(self, element_length_func, bucket_boundaries, bucket_batch_sizes,
+                                  drop_remainder=True):
+        """tf.data.experimental.bucket_by_sequence_length(pad_to_bucket_boundary=False,
+        no_padding=False): bucket k holds lengths in [b_{k-1}, b_k) (b_{-1} = -inf,
+        b_K = +inf); a bucket emits a padded batch as soon as it holds its batch size;
+        at end of input the partial batches are dropped (drop_remainder=True) or
+        emitted in bucket order."""
+        if len(bucket_batch_sizes) != len(bucket_boundaries) + 1:
+            raise ValueError('len(bucket_batch_sizes) must equal len(bucket_boundaries) + 1')
+        src = self
+        bounds = list(bucket_boundaries)
+
+        def gen():
+            pending = [[] for _ in bucket_batch_sizes]
+            for el in src:
+                k = int(np.searchsorted(bounds, int(element_length_func(*el)), side='right'))
+                pending[k].append(el)
+                if len(pending[k]) == bucket_batch_sizes[k]:
+                    yield pad_batch(pending[k])
+                    pending[k] = []
+            if not drop_remainder:
+                for p in pending:
+                    if p:
+                        yield pad_batch(p)
+        return Dataset(gen)
+
+
+_DONE = object()
+
+
+def pad_batch(elements):
+    """padded_batch: stack each component, zero-padding 1-D components to the longest."""
+    out = []
+    for comp in zip(*elements):
+        first = comp[0]
+        if isinstance(first, (bytes, str)):
+            out.append(np.array(comp, dtype=object))
+        elif np.ndim(first) == 0:
+            out.append(np.array(comp))
+        else:
+            n = max(c.shape[0] for c in comp)
+            arr = np.zeros((len(comp), n), dtype=first.dtype)
+            for i, c in enumerate(comp):
+                arr[i, :c.shape[0]] = c
+            out.append(arr)
+    return tuple(out)
+
+
+def _interleave_files(files, is_utt_id, verify_crc=True):
+    """Round-robin over the files, one record at a time (interleave, block 1)."""
+    def gen():
+        iters = [read_tfrecord(f, is_utt_id, verify_crc) for f in files]
+        while iters:
+            alive = []
+            for it in iters:
+                try:
+                    yield next(it)
+                    alive.append(it)
+                except StopIteration:
+                    pass
+            iters = alive
+    return gen
+
+
+def create_ds(file_pattern, shuffle, max_inp, max_tar, is_utt_id=False, seed=None):
+    """load_speech_data.py:24-115: files -> records -> parsed -> length-filtered."""
+    files = sorted(glob.glob(file_pattern))
+    if not files:
+        raise FileNotFoundError(f'no TFRecord files match {file_pattern}')
+    if shuffle:
+        np.random.default_rng(seed).shuffle(files)
+    ds = Dataset(_interleave_files(files, is_utt_id))
+
+    def keep(length, limit):
+        return limit < 1 or length <= limit   # _filter_max_length (:48-50)
+    return ds.filter(lambda *el: keep(el[2], max_inp)).filter(lambda *el: keep(el[3], max_tar))
+
+
+def finalize_ds(dataset, repeat, shuffle, seed=None):
+    """load_speech_data.py:118-126."""
+    dataset = dataset.cache()
+    if shuffle:
+        dataset = dataset.shuffle(buffer_size=5000, seed=seed)
+    dataset = dataset.repeat(repeat)
+    return dataset.prefetch()
+
+
+def create_ds_batch_for_test(file_pattern, batch_size, max_inp, max_tar):
+    """load_speech_data.py:129-147: batch size falls back to 1 unless it divides
+    the number of utterances."""
+    utt_num = sum(sum(1 for _ in read_tfrecord(f)) for f in glob.glob(file_pattern))
+    if utt_num % batch_size != 0:
+        batch_size = 1
+    ds = create_ds(file_pattern, False, max_inp, max_tar, True).padded_batch(batch_size, drop_remainder=False)
+    return finalize_ds(ds, 1, False)
+
+
+def create_ds_batch_for_train(file_pattern, shuffle, repeat, batch_size, max_inp, max_tar, seed=None):
+    """load_speech_data.py:150-161."""
+    ds = create_ds(file_pattern, shuffle, max_inp, max_tar, seed=seed).padded_batch(batch_size, drop_remainder=True)
+    return finalize_ds(ds, repeat, shuffle, seed)
+
+
+def create_ds_bucket(file_pattern, shuffle, repeat, bucket_boundaries, bucket_batch_sizes, max_inp, max_tar,
+                     seed=None):
+    """load_speech_data.py:164-181: length buckets on input_length."""
+    ds = create_ds(file_pattern, shuffle, max_inp, max_tar, seed=seed)
+    ds = ds.bucket_by_sequence_length(lambda x, y, a, b: a, bucket_boundaries, bucket_batch_sizes,
+                                      drop_remainder=True)
+    return finalize_ds(ds, repeat, shuffle, seed)
+
+
+def map_data_for_transformer_fn(inputs, targets, input_length, target_length, arg):
+    """load_speech_data.py:184-198: [B, T*F] -> [B, T, F], ints to int32."""
+    inputs = np.asarray(inputs, np.float32)
+    return (inputs.reshape(inputs.shape[0], -1, arg), np.asarray(targets).astype(np.int32),
+            np.asarray(input_length).astype(np.int32), np.asarray(target_length).astype(np.int32))
+
+
+def map_data_for_transformer_utt_id_fn(inputs, targets, input_length, target_length, utt_id, arg):
+    """load_speech_data.py:201-210."""
+    return map_data_for_transformer_fn(inputs, targets, input_length, target_length, arg) + (utt_id,)
