@@ -1,0 +1,141 @@
+"""Checkpoint surface of the SRF path (srf_amd/checkpoint.py) on CPU tensors:
+TF object-path naming and shapes (naive:68-118, sequence_router.py:44-63),
+CheckpointManager semantics (ckpt-N, max_to_keep, the `checkpoint` state file,
+misc_helper.py:139-163) and averaging (average_ckpt_sr.py:135-179)."""
+import argparse
+import os
+
+import numpy as np
+import torch
+
+from srf_amd import checkpoint as ck
+from srf_amd.sequence_router import SequenceRouter
+from srf_amd.train_helper import CustomSchedule, SrfAdam
+from tests.helpers import config_from_shape
+
+KW = dict(feat_dim=40, enc_num=2, iters=2, lpad=1, rpad=1, ph=4, pd=8, ch=4, cd=8, vd=8, context=False)
+
+
+def _model(seed):
+    return SequenceRouter(config_from_shape(KW), None, 12, device=torch.device('cpu'), seed=seed)
+
+
+def test_tf_names_and_shapes():
+    m = _model(0)
+    st = ck.model_state(m)
+    in_n = 4 * 3
+    assert st['model/wgt/0/.ATTRIBUTES/VARIABLE_VALUE'].shape == (1, 1, in_n, 4, 8, 8)
+    assert st['model/bias/1/.ATTRIBUTES/VARIABLE_VALUE'].shape == (1, 1, in_n, 12, 8, 1)
+    assert st['model/conv/conv_layers/1/0/kernel/.ATTRIBUTES/VARIABLE_VALUE'].shape == (3, 3, 1, 64)
+    assert st['model/conv/bn_layers/1/moving_variance/.ATTRIBUTES/VARIABLE_VALUE'].shape == (64,)
+    assert st['model/ln_m/1/gamma/.ATTRIBUTES/VARIABLE_VALUE'].shape == (12 * 8,)
+    assert st['model/proj_pe/kernel/.ATTRIBUTES/VARIABLE_VALUE'].shape == (10 * 64, 4)
+    # every parameter and BN statistic is named exactly once
+    assert len(st) == len(m.params) + 2 * m.cnn_n
+    np.testing.assert_array_equal(st['model/wgt/0/.ATTRIBUTES/VARIABLE_VALUE'].reshape(in_n, 4, 8, 8),
+                                  m.params['W0'].detach().numpy())
+
+
+def test_manager_save_restore_rotation(tmp_path):
+    m, opt = _model(1), SrfAdam(CustomSchedule(0.5, 1, 1200))
+    opt._m = torch.randn(m.n_flat)
+    opt._v = torch.rand(m.n_flat)
+    opt.iterations = 17
+    mgr = ck.CheckpointManager(m, opt, str(tmp_path), max_to_keep=2)
+    for _ in range(3):
+        with torch.no_grad():
+            m.flat_params.add_(1.0)
+        path = mgr.save()
+    assert path.endswith('ckpt-3') and mgr.latest_checkpoint == path
+    assert sorted(os.listdir(tmp_path)) == ['checkpoint', 'ckpt-2.srf.safetensors', 'ckpt-3.srf.safetensors']
+    state_file = open(tmp_path / 'checkpoint').read()
+    assert 'model_checkpoint_path: "ckpt-3"' in state_file and 'all_model_checkpoint_paths: "ckpt-2"' in state_file
+    m2, opt2 = _model(2), SrfAdam(CustomSchedule(0.5, 1, 1200))
+    cfg = argparse.Namespace(model_ckpt_max_to_keep=-1, path_ckpt=str(tmp_path), path_ckpt_epoch=0)
+    mgr2, epoch = ck.load_checkpoint(cfg, None, m2, opt2)
+    assert epoch == 3 and opt2.iterations == 17
+    for k in m.params:
+        torch.testing.assert_close(m2.params[k], m.params[k], rtol=0, atol=0)
+    for a, b in ((opt2._m, opt._m), (opt2._v, opt._v)):
+        for name in m.params:
+            off, n = m.offsets[name], m.params[name].numel()
+            torch.testing.assert_close(a[off:off + n], b[off:off + n], rtol=0, atol=0)
+    cfg.path_ckpt_epoch = 2
+    m3 = _model(3)
+    assert ck.load_checkpoint(cfg, None, m3, None)[1] == 2
+    torch.testing.assert_close(m3.params['W1'], m.params['W1'] - 1.0, rtol=0, atol=1e-6)
+
+
+def test_average_checkpoints(tmp_path):
+    models = [_model(10 + k) for k in range(3)]
+    mgr = ck.CheckpointManager(models[0], None, str(tmp_path), max_to_keep=None)
+    for mk in models:
+        mgr.model = mk
+        mgr.save()
+    cfg = argparse.Namespace(path_ckpt=str(tmp_path), model_average_num=2)
+    path, avg = ck.average_checkpoints(cfg, None, lambda: _model(99))
+    assert path == os.path.join(str(tmp_path), 'avg', 'ckpt-1')
+    for k in avg.params:
+        want = (models[1].params[k].detach() + models[2].params[k].detach()) / 2
+        torch.testing.assert_close(avg.params[k].detach(), want, rtol=1e-6, atol=1e-7)
+    back = _model(5)
+    ck.restore(path, back)
+    torch.testing.assert_close(back.params['b0'], avg.params['b0'], rtol=0, atol=0)
+
+
+def _masked_crc(b):
+    from tests.test_data_cpu import crc32c_py, masked
+    return masked(crc32c_py(b))
+
+
+def test_tf_bundle_reads_hand_built_table(tmp_path):
+    """A LevelDB-format table assembled byte by byte from the format spec
+    (entries: varint shared/non_shared/value_len + key delta + value; restart
+    array; block trailer type + masked CRC; index block of BlockHandles; 48-byte
+    footer with magic) and a BundleEntryProto written field by field."""
+    import struct
+    from srf_amd import tf_bundle as tb
+    val = np.arange(6, dtype=np.float32).reshape(2, 3)
+    raw = val.tobytes()
+    dims = bytes([0x12, 2, 0x08, 2]) + bytes([0x12, 2, 0x08, 3])          # dim{size:2} dim{size:3}
+    entry = (bytes([0x08, 1]) + bytes([0x12, len(dims)]) + dims            # dtype=DT_FLOAT, shape
+             + bytes([0x28, len(raw)]) + bytes([0x35]) + struct.pack('<I', _masked_crc(raw)))
+    header = bytes([0x08, 1])                                              # num_shards=1
+    # data block: key "" -> header, key "w" -> entry (shared 0, restart at 0 only)
+    body = bytes([0, 0, len(header)]) + header + bytes([0, 1, len(entry)]) + b'w' + entry
+    body += struct.pack('<I', 0) + struct.pack('<I', 1)
+    f = bytearray(body)
+    f += b'\x00' + struct.pack('<I', _masked_crc(body + b'\x00'))
+    meta_off = len(f)
+    meta = struct.pack('<I', 0) + struct.pack('<I', 1)
+    f += meta + b'\x00' + struct.pack('<I', _masked_crc(meta + b'\x00'))
+    idx_off = len(f)
+    handle = bytes([0, len(body)])
+    idx = bytes([0, 1, len(handle)]) + b'w' + handle + struct.pack('<I', 0) + struct.pack('<I', 1)
+    f += idx + b'\x00' + struct.pack('<I', _masked_crc(idx + b'\x00'))
+    footer = bytes([meta_off, len(meta), idx_off, len(idx)])
+    f += footer + b'\x00' * (40 - len(footer)) + struct.pack('<Q', 0xdb4775248b80fb57)
+    prefix = str(tmp_path / 'hand')
+    open(prefix + '.index', 'wb').write(bytes(f))
+    open(prefix + '.data-00000-of-00001', 'wb').write(raw)
+    assert tb.list_variables(prefix) == [('w', [2, 3], 1)]
+    np.testing.assert_array_equal(tb.load_checkpoint(prefix)['w'], val)
+
+
+def test_tf_bundle_export_import_round_trip(tmp_path):
+    from srf_amd import tf_bundle as tb
+    m, opt = _model(7), SrfAdam(CustomSchedule(0.5, 1, 1200))
+    opt._m = torch.randn(m.n_flat)
+    opt._v = torch.rand(m.n_flat)
+    opt.iterations = 5
+    prefix = str(tmp_path / 'tf' / 'ckpt-4')
+    tb.export_to_tf(prefix, m, opt)
+    names = [n for n, _, _ in tb.list_variables(prefix)]
+    assert names == sorted(names) and 'model/wgt/1/.ATTRIBUTES/VARIABLE_VALUE' in names
+    m2, opt2 = _model(8), SrfAdam(CustomSchedule(0.5, 1, 1200))
+    unused = tb.restore_from_tf(prefix, m2, opt2)
+    assert unused and all(k.startswith('optimizer/') or '.OPTIMIZER_SLOT/' in k for k in unused)
+    for k in m.params:
+        torch.testing.assert_close(m2.params[k], m.params[k], rtol=0, atol=0)
+    assert opt2.iterations == 5
+    torch.testing.assert_close(opt2._v[m.offsets['W0']:m.offsets['W0'] + 10], opt._v[m.offsets['W0']:m.offsets['W0'] + 10])
