@@ -14,9 +14,12 @@
 // Kernels:
 //   sdr_pose_kernel   u[f][i][row] = W_i x_i(f) + b_i for every frame (MFMA), the
 //                     frame-parallel part, kept in HBM for the sequential pass;
-//   sdr_fwd_kernel    one workgroup per utterance walks its frames in order;
-//   sdr_bwd_kernel    one workgroup per utterance walks them backwards,
-//                     recomputing each frame's iterations, and writes gu;
+//   sdr_seq_*         (route_sdr_seq*.hip) the recurrence itself: one 1024-thread
+//                     workgroup per utterance holds the frame's u in registers and
+//                     walks the frames in order (forward) or in reverse,
+//                     recomputing each frame's iterations, writing gu (backward);
+//   sdr_fwd_kernel /  the first, 256-thread LDS version of the recurrence, kept for
+//   sdr_bwd_kernel    shapes outside the register budget (and SRF_SDR_SEQ=0);
 //   sdr_gx_kernel     gx = W^T gu (MFMA) scattered into g_emb via the window adjoint;
 //   sdr_gw_kernel     gW = sum_f gu x^T (MFMA, K = frames); gbias = column sums of gu.
 // Layouts (HBM, fp32): emb [F][N][din]; W [in_n][J*Dout][din]; bias [in_n][J*Dout];
@@ -26,6 +29,7 @@
 
 #include "srf_common.h"
 #include "srf_reduce.h"
+#include "route_sdr_seq.h"
 #include "../../include/srf.h"
 
 namespace {
@@ -488,14 +492,19 @@ int srf_route_sdr_fwd(const float* emb, const float* W, const float* bias, int B
     srf::set_error("SDR forward workspace too small");
     return SRF_EWORKSPACE;
   }
+  const bool seq = srf::sdr_seq_supported(g.in_n(), J, dout, iters);
   const size_t sm = sdr_fwd_smem(g.in_n(), J, dout);
-  if ((rc = sdr_smem_check(sm))) return rc;
+  if (!seq && (rc = sdr_smem_check(sm))) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* u = static_cast<float*>(workspace);
   if ((rc = pose_dispatch(g, emb, W, bias, u, st))) return rc;
-  hipLaunchKernelGGL(sdr_fwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, u, T, g.in_n(), J, dout, iters,
-                     g.mask_first, v_out);
-  SRF_LAUNCH_CHECK("sdr_fwd");
+  if (seq) {
+    if ((rc = srf::sdr_seq_fwd(u, B, T, g.in_n(), J, dout, iters, g.mask_first, v_out, st))) return rc;
+  } else {
+    hipLaunchKernelGGL(sdr_fwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, u, T, g.in_n(), J, dout, iters,
+                       g.mask_first, v_out);
+    SRF_LAUNCH_CHECK("sdr_fwd");
+  }
   SRF_HIP_TRY(hipMemcpyAsync(saved, v_out, (size_t)g.F() * g.JD() * sizeof(float), hipMemcpyDeviceToDevice, st));
   return SRF_OK;
 }
@@ -513,13 +522,18 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
     srf::set_error("SDR backward workspace too small");
     return SRF_EWORKSPACE;
   }
+  const bool seq = srf::sdr_seq_supported(g.in_n(), J, dout, iters);
   const size_t sm = sdr_bwd_smem(g.in_n(), J, dout, iters);
-  if ((rc = sdr_smem_check(sm))) return rc;
+  if (!seq && (rc = sdr_smem_check(sm))) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if ((rc = pose_dispatch(g, emb, W, bias, w.u, st))) return rc;
-  hipLaunchKernelGGL(sdr_bwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, w.u, saved, g_v, T, g.in_n(), J, dout,
-                     iters, g.mask_first, w.gu);
-  SRF_LAUNCH_CHECK("sdr_bwd");
+  if (seq) {
+    if ((rc = srf::sdr_seq_bwd(w.u, saved, g_v, B, T, g.in_n(), J, dout, iters, g.mask_first, w.gu, st))) return rc;
+  } else {
+    hipLaunchKernelGGL(sdr_bwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, w.u, saved, g_v, T, g.in_n(), J, dout,
+                       iters, g.mask_first, w.gu);
+    SRF_LAUNCH_CHECK("sdr_bwd");
+  }
   {
     const size_t n_emb = (size_t)g.F() * N * din;
     const size_t total = (size_t)g.in_n() * g.JD() * din + n_emb;

@@ -1,0 +1,144 @@
+// Sequential dynamic routing (SDR) recurrence with register-resident frames, gfx950.
+//
+// Replaces the frame loop of sequence_router_naive.py:162-170 (tf.while_loop over
+// T' with body_context :231-245 / pad_body_context :212-229), one utterance per
+// workgroup.  route_sdr.hip forms u = W x + b for every frame on MFMA first; this
+// file walks the frames (forward here, backward in route_sdr_seq_bwd.hip).
+//
+// Mapping (route_sdr_seq_dev.h).  A 1024-thread workgroup holds the frame's whole
+// u_t [in_n][J][D] in registers.  J is padded to JP (a power of two); a capsule's
+// D values are split over Q lanes of KD values, so one input capsule is a "row" of
+// ROWL = JP*Q lanes and a wave holds SUB = 64/ROWL rows.  The G = 16*SUB row slots
+// take input capsules i = g, g + G, ... (at most NIM per lane).  Per iteration:
+//   logits  b_ij += <u_ij, w_j>: KD FMAs per lane + a butterfly over the Q lanes;
+//   softmax over j: butterflies over the JP capsules of the row;
+//   s_j = sum_i c_ij u_ij: in-lane over the lane's rows, a butterfly over the
+//         wave's rows, then the 16 wave partials through LDS;
+//   squash: thread e = j*D + d owns element e; the norm is a butterfly over D lanes.
+// Every butterfly is an xor exchange (DPP quad_perm, ds_swizzle, permlane swaps),
+// so all lanes of a group hold bit-identical sums.  Two barriers per iteration;
+// the next frame's u is loaded while the last reduction and squash of the
+// current frame run.  HBM traffic per frame: u_t once (in_n*J*D floats) + v_t.
+#include <cstdlib>
+
+#include "route_sdr_seq.h"
+#include "route_sdr_seq_dev.h"
+
+namespace {
+
+using namespace srf_seq;
+
+// LDS: w [JD] (agreement input of the iteration: v_{t-1} at r = 0, then v^{r-1}),
+// part [16][JD].
+template <int D, int JP, int NIM>
+__global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __restrict__ u, int T, int in_n, int J,
+                                                               int iters, int mask_first, float* __restrict__ v_out) {
+  using C = Cfg<D, JP, NIM>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int JD = J * D;
+  float* wl = lds;
+  float* part = lds + ((JD + 3) & ~3);
+  const int tid = threadIdx.x;
+  const Lane L = lane_map<C>(in_n, J, mask_first);
+  const size_t ff = (size_t)in_n * JD;
+  const float* ub = u + (size_t)blockIdx.x * T * ff;
+  float* vo = v_out + (size_t)blockIdx.x * T * JD;
+  const bool owner_wave = (tid >> 6) * 64 < JD;   // waves holding elements e = tid < JD
+  const bool ev = tid < JD;
+  if (ev) wl[tid] = 0.f;   // v_{-1} = 0
+  float ur[C::NIM][C::KD];
+  load_frame<C>(ub, JD, L, ur);
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    float b[C::NIM], c[C::NIM];
+#pragma unroll
+    for (int k = 0; k < C::NIM; ++k) b[k] = 0.f;
+    for (int r = 0; r < iters; ++r) {
+      float w[C::KD];
+      lds_slice<C::KD>(wl + L.eoff, L.jv, w);
+      logits_softmax<C>(ur, w, L, b, c);
+      row_partial<C>(c, ur, L, JD, part);
+      if (r == iters - 1 && t + 1 < T) load_frame<C>(ub + (size_t)(t + 1) * ff, JD, L, ur);   // u_t is dead
+      __syncthreads();
+      if (owner_wave) {
+        const float v = squash_elem<D>(ev ? sum_parts(part, JD, tid) : 0.f);
+        if (ev) {
+          wl[tid] = v;
+          if (r == iters - 1) vo[(size_t)t * JD + tid] = v;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+size_t fwd_lds(int J, int D) {
+  return ((((size_t)J * D + 3) & ~(size_t)3) + (size_t)kWaves * J * D) * sizeof(float);
+}
+
+template <int D, int JP, int NIM>
+int launch_fwd(const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
+               hipStream_t st) {
+  const size_t lds = fwd_lds(J, D);
+  auto k = sdr_seq_fwd_kernel<D, JP, NIM>;
+  if (lds > 64 * 1024)
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, T, in_n, J, iters, mask_first, v_out);
+  SRF_LAUNCH_CHECK("sdr_seq_fwd");
+  return SRF_OK;
+}
+
+template <int D, int JP>
+int fwd_nim(int nim, const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
+            hipStream_t st) {
+  if (nim == 2) return launch_fwd<D, JP, 2>(u, B, T, in_n, J, iters, mask_first, v_out, st);
+  if (nim == 5) return launch_fwd<D, JP, 5>(u, B, T, in_n, J, iters, mask_first, v_out, st);
+  if constexpr (seq_kd(D, JP) <= 8) return launch_fwd<D, JP, 10>(u, B, T, in_n, J, iters, mask_first, v_out, st);
+  srf::set_error("sdr_seq: no forward kernel for %d input capsules per lane", nim);
+  return SRF_EUNSUPPORTED;
+}
+
+}  // namespace
+
+namespace srf {
+
+bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm) {
+  const char* e = getenv("SRF_SDR_SEQ");
+  if (e && e[0] == '0') return false;
+  if (J < 2 || J > 64 || iters < 1 || iters > 5 || in_n < 1) return false;
+  if (dout != 8 && dout != 16 && dout != 32) return false;
+  const int JP = srf_seq::pow2_at_least(J);
+  if (dout * JP > 1024) return false;
+  const int KD = srf_seq::seq_kd(dout, JP);
+  const int G = srf_seq::seq_slots(dout, JP);
+  const int NI = (in_n + G - 1) / G;
+  const int m = NI <= 2 ? 2 : NI <= 5 ? 5 : (NI <= 10 && KD <= 8) ? 10 : 0;
+  if (m == 0) return false;
+  const int r = iters <= 3 ? 3 : 5;
+  if (r == 5 && m != 2) return false;   // five-iteration backward kept for small layers only
+  if (nim) *nim = m;
+  if (rm) *rm = r;
+  return true;
+}
+
+bool sdr_seq_supported(int in_n, int J, int dout, int iters) {
+  return sdr_seq_plan(in_n, J, dout, iters, nullptr, nullptr);
+}
+
+int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
+                hipStream_t st) {
+  int nim = 0, rm = 0;
+  if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
+    srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
+    return SRF_EUNSUPPORTED;
+  }
+  const int JP = srf_seq::pow2_at_least(J);
+#define SRF_SEQ_F(DD, PP) \
+  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, u, B, T, in_n, J, iters, mask_first, v_out, st);
+  SRF_SEQ_CASES(SRF_SEQ_F)
+#undef SRF_SEQ_F
+  srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);
+  return SRF_EUNSUPPORTED;
+}
+
+}  // namespace srf

@@ -1,0 +1,217 @@
+// Backward of the SDR recurrence (route_sdr_seq.hip) with register-resident
+// frames, gfx950: the autodiff of sequence_router_naive.py:162-170 / 212-245.
+//
+// One workgroup per utterance walks its frames in reverse.  Per frame it
+// recomputes the R routing iterations from v_{t-1} (the forward's saved v), with
+// Vc^r = v_{t-1} + sum_{k<r} v^k so that b^r = <u, Vc^r> (+ mask) by linearity of
+// the b += <u, v> update, then runs the routing adjoint:
+//   gs^r  = squash'(s^r)^T a^r,        a^{R-1} = g_v[t] + carry,
+//   q_ij  = <u_ij, gs^r_j>,  sigma_i = sum_j c_ij q_ij,  gL_ij = c_ij (q_ij - sigma_i),
+//   gVc^r = sum_i gL_ij u_ij,          a^{r-1} = sum_{r' >= r} gVc^{r'},
+//   gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j,
+//   carry (dL/dv_{t-1} for frame t-1) = sum_r gVc^r.
+// u stays in registers (lane map of route_sdr_seq_dev.h); c^r and gL^r are per
+// (lane, row) registers; s^r, the running adjoints and the carry live in the
+// registers of the thread that owns element e = j*D + d; Vc^r and gs^r go through
+// LDS because every row reads them.  gu is formed in place of the dead u.
+#include <cstdlib>
+
+#include "route_sdr_seq.h"
+#include "route_sdr_seq_dev.h"
+
+namespace {
+
+using namespace srf_seq;
+
+// LDS: w [JDa], Vc [RM][JDa], gs [RM][JDa], part [16][JD].
+template <int D, int JP, int NIM, int RM>
+__global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __restrict__ u,
+                                                               const float* __restrict__ v_saved,
+                                                               const float* __restrict__ g_v, int T, int in_n, int J,
+                                                               int iters, int mask_first, float* __restrict__ gu) {
+  using C = Cfg<D, JP, NIM>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int JD = J * D;
+  const int JDa = (JD + 3) & ~3;
+  const int R = iters;
+  float* wl = lds;
+  float* vcl = wl + JDa;
+  float* gsl = vcl + RM * JDa;
+  float* part = gsl + RM * JDa;
+  const int tid = threadIdx.x;
+  const Lane L = lane_map<C>(in_n, J, mask_first);
+  const size_t ff = (size_t)in_n * JD;
+  const size_t f0 = (size_t)blockIdx.x * T;
+  const bool owner_wave = (tid >> 6) * 64 < JD;
+  const bool ev = tid < JD;
+  float carry = 0.f;   // dL/dv_t carried back from frame t+1 (owner threads)
+  float ur[C::NIM][C::KD];
+  float cr[RM][C::NIM], gl[RM][C::NIM];
+  float sr[RM];        // s^r of the owned element
+#pragma unroll
+  for (int r = 0; r < RM; ++r) sr[r] = 0.f;
+  load_frame<C>(u + (f0 + T - 1) * ff, JD, L, ur);
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t f = f0 + t;
+    float a = 0.f;
+    if (ev) {
+      const float vp = t > 0 ? v_saved[(f - 1) * JD + tid] : 0.f;
+      wl[tid] = vp;
+      vcl[tid] = vp;                       // Vc^0 = v_{t-1}
+      a = g_v[f * JD + tid] + carry;       // dL/dv^{R-1}
+      carry = 0.f;
+    }
+    __syncthreads();
+    // ---- recompute the frame's iterations: c^r, s^r, Vc^r
+    float b[C::NIM];
+#pragma unroll
+    for (int k = 0; k < C::NIM; ++k) b[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      if (r < R) {
+        float w[C::KD];
+        lds_slice<C::KD>(wl + L.eoff, L.jv, w);
+        logits_softmax<C>(ur, w, L, b, cr[r]);
+        row_partial<C>(cr[r], ur, L, JD, part);
+        __syncthreads();
+        if (owner_wave) {
+          const float s = ev ? sum_parts(part, JD, tid) : 0.f;
+          sr[r] = s;
+          const float v = squash_elem<D>(s);
+          if (ev) {
+            wl[tid] = v;
+            if (r + 1 < R) vcl[(r + 1) * JDa + tid] = vcl[r * JDa + tid] + v;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // ---- adjoint, r = R-1 .. 0 (a = dL/dv^r)
+    float grun = 0.f;
+#pragma unroll
+    for (int r = RM - 1; r >= 0; --r) {
+      if (r < R) {
+        if (owner_wave) {
+          const float s = sr[r];
+          const float n2 = group_sum<1, D>(s * s);
+          const float sa = group_sum<1, D>(s * a);
+          const float rs = 1.f / sqrtf(n2 + kSquashEps);
+          const float ip = 1.f / (1.f + n2);
+          const float gfac = n2 * ip * rs;
+          const float dg2 = 2.f * rs * ip * (ip - 0.5f * n2 / (n2 + kSquashEps)) * sa;
+          if (ev) gsl[r * JDa + tid] = gfac * a + dg2 * s;
+        }
+        __syncthreads();
+        float gsv[C::KD];
+        lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
+#pragma unroll
+        for (int k = 0; k < C::NIM; ++k) {
+          gl[r][k] = 0.f;
+          if (k < L.NI) {
+            float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+            for (int d = 0; d < C::KD; d += 2) {
+              p0 += ur[k][d] * gsv[d];
+              p1 += ur[k][d + 1] * gsv[d + 1];
+            }
+            const float q = group_sum<1, C::Q>(p0 + p1);
+            const float sig = group_sum<C::Q, C::ROWL>(cr[r][k] * q);
+            gl[r][k] = cr[r][k] * (q - sig);
+          }
+        }
+        row_partial<C>(gl[r], ur, L, JD, part);
+        __syncthreads();
+        if (ev) {
+          const float g = sum_parts(part, JD, tid);   // gVc^r_e
+          carry += g;
+          grun = (r == R - 1) ? g : grun + g;
+          a = grun;
+        }
+      }
+    }
+    // ---- gu (in place of u, which is dead now)
+#pragma unroll
+    for (int k = 0; k < C::NIM; ++k)
+#pragma unroll
+      for (int d = 0; d < C::KD; ++d) ur[k][d] = 0.f;
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      if (r < R) {
+        float gsv[C::KD], vcv[C::KD];
+        lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
+        lds_slice<C::KD>(vcl + r * JDa + L.eoff, L.jv, vcv);
+#pragma unroll
+        for (int k = 0; k < C::NIM; ++k)
+#pragma unroll
+          for (int d = 0; d < C::KD; ++d) ur[k][d] += cr[r][k] * gsv[d] + gl[r][k] * vcv[d];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < C::NIM; ++k) {
+      if (L.jv && k < L.NI) {
+        float* dst = gu + f * ff + (size_t)(L.g + k * C::G) * JD + L.eoff;
+#pragma unroll
+        for (int c = 0; c < C::KD; c += 4)
+          *reinterpret_cast<f4*>(dst + c) = f4{ur[k][c], ur[k][c + 1], ur[k][c + 2], ur[k][c + 3]};
+      }
+    }
+    if (t > 0) load_frame<C>(u + (f - 1) * ff, JD, L, ur);
+    __syncthreads();   // the next frame overwrites w and Vc^0
+  }
+}
+
+size_t bwd_lds(int J, int D, int RM) {
+  const size_t JDa = ((size_t)J * D + 3) & ~(size_t)3;
+  return (JDa * (1 + 2 * (size_t)RM) + (size_t)kWaves * J * D) * sizeof(float);
+}
+
+template <int D, int JP, int NIM, int RM>
+int launch_bwd(const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J, int iters,
+               int mask_first, float* gu, hipStream_t st) {
+  const size_t lds = bwd_lds(J, D, RM);
+  auto k = sdr_seq_bwd_kernel<D, JP, NIM, RM>;
+  if (lds > 64 * 1024)
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, vs, gv, T, in_n, J, iters, mask_first, gu);
+  SRF_LAUNCH_CHECK("sdr_seq_bwd");
+  return SRF_OK;
+}
+
+template <int D, int JP>
+int bwd_nim(int nim, int rm, const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J,
+            int iters, int mask_first, float* gu, hipStream_t st) {
+  if (rm == 5) return launch_bwd<D, JP, 2, 5>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
+  if (nim == 2) return launch_bwd<D, JP, 2, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
+  if (nim == 5) return launch_bwd<D, JP, 5, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
+  if constexpr (seq_kd(D, JP) <= 8)
+    return launch_bwd<D, JP, 10, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
+  srf::set_error("sdr_seq: no backward kernel for %d input capsules per lane", nim);
+  return SRF_EUNSUPPORTED;
+}
+
+}  // namespace
+
+namespace srf {
+
+int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
+                int iters, int mask_first, float* gu, hipStream_t st) {
+  int nim = 0, rm = 0;
+  if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
+    srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
+    return SRF_EUNSUPPORTED;
+  }
+  if (bwd_lds(J, dout, rm) > 160 * 1024) {
+    srf::set_error("sdr_seq: backward LDS exceeds 160 KiB");
+    return SRF_EUNSUPPORTED;
+  }
+  const int JP = srf_seq::pow2_at_least(J);
+#define SRF_SEQ_B(DD, PP)     \
+  if (dout == DD && JP == PP) \
+    return bwd_nim<DD, PP>(nim, rm, u, v_saved, g_v, B, T, in_n, J, iters, mask_first, gu, st);
+  SRF_SEQ_CASES(SRF_SEQ_B)
+#undef SRF_SEQ_B
+  srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);
+  return SRF_EUNSUPPORTED;
+}
+
+}  // namespace srf

@@ -26,7 +26,12 @@ CASES = [
     (2, 5, 16, 32, 2, 2, 32, 3, True),    # C3 last layer shape (short)
     (2, 8, 3, 16, 0, 1, 7, 1, False),     # one iteration, asymmetric window
     (1, 6, 2, 16, 1, 0, 4, 5, True),      # five iterations
+    (2, 16, 16, 32, 2, 2, 16, 3, False),  # C3 inner layer shape, 16 frames of recurrence
+    (1, 10, 8, 16, 4, 4, 63, 3, True),    # TIMIT-sized last layer: J = 63 (padded to 64), in_n = 72
+    (2, 6, 4, 8, 0, 0, 3, 2, True),       # J = 3 (padded to 4), D = 8, no window
 ]
+# shapes run again through the first (256-thread LDS) recurrence kernels
+LEGACY = [CASES[0], CASES[2], CASES[3], CASES[5]]
 
 
 def _mk(case, seed):
@@ -49,10 +54,9 @@ def _run_gpu(case, emb, W, bias, dev):
     return te, tW, tb, sequential_routing(te, tW, tb, g)
 
 
-@pytest.mark.parametrize('case', CASES)
-def test_route_sdr_forward(cuda, case):
+def _check_forward(case, dev):
     emb, W, bias = _mk(case, 11)
-    _, _, _, v = _run_gpu(case, emb, W, bias, cuda)
+    _, _, _, v = _run_gpu(case, emb, W, bias, dev)
     B, T, N, D, lp, rp, J, it, mf = case
     ref = so.sequential_routing(so.pose(so.window(emb, lp, rp), W, bias), it, mf)
     got = v.detach().cpu().double().numpy()
@@ -60,7 +64,25 @@ def test_route_sdr_forward(cuda, case):
 
 
 @pytest.mark.parametrize('case', CASES)
+def test_route_sdr_forward(cuda, case):
+    _check_forward(case, cuda)
+
+
+@pytest.mark.parametrize('case', LEGACY)
+def test_route_sdr_legacy_kernels(cuda, case, monkeypatch):
+    """SRF_SDR_SEQ=0 selects the 256-thread LDS recurrence kernels (the path for
+    shapes beyond the register-resident kernels' budget)."""
+    monkeypatch.setenv('SRF_SDR_SEQ', '0')
+    _check_forward(case, cuda)
+    _check_backward(case, cuda)
+
+
+@pytest.mark.parametrize('case', CASES)
 def test_route_sdr_backward(cuda, case):
+    _check_backward(case, cuda)
+
+
+def _check_backward(case, cuda):
     emb, W, bias = _mk(case, 12)
     te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
     gv = np.random.default_rng(13).standard_normal(v.shape)
