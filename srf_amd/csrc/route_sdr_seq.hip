@@ -15,8 +15,8 @@
 //   s_j = sum_i c_ij u_ij: in-lane over the lane's rows, a butterfly over the
 //         wave's rows, then the 16 wave partials through LDS;
 //   squash: thread e = j*D + d owns element e; the norm is a butterfly over D lanes.
-// Every butterfly is an xor exchange (DPP quad_perm, ds_swizzle, permlane swaps),
-// so all lanes of a group hold bit-identical sums.  Two barriers per iteration;
+// Butterflies stay on the VALU where they can (DPP quad_perm / row_ror, permlane
+// swaps; ds_swizzle only for a lone xor 4).  Two barriers per iteration;
 // the next frame's u is loaded while the last reduction and squash of the
 // current frame run.  HBM traffic per frame: u_t once (in_n*J*D floats) + v_t.
 #include <cstdlib>

@@ -11,9 +11,9 @@
 //   gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j,
 //   carry (dL/dv_{t-1} for frame t-1) = sum_r gVc^r.
 // u stays in registers (lane map of route_sdr_seq_dev.h); c^r and gL^r are per
-// (lane, row) registers; s^r, the running adjoints and the carry live in the
+// (lane, row) registers or LDS slabs; s^r, the running adjoints and the carry live in the
 // registers of the thread that owns element e = j*D + d; Vc^r and gs^r go through
-// LDS because every row reads them.  gu is formed in place of the dead u.
+// LDS because every row reads them.
 #include <cstdlib>
 
 #include "route_sdr_seq.h"
@@ -23,13 +23,19 @@ namespace {
 
 using namespace srf_seq;
 
-// LDS: w [JDa], Vc [RM][JDa], gs [RM][JDa], part [16][JD].
-template <int D, int JP, int NIM, int RM>
+// c^r and gL^r of the lane's rows live in registers or, with CL (chosen when u
+// already takes most of the lane's register budget and the slabs fit), in LDS
+// [RM][in_n][JP] (written by the first lane of each capsule, read by all Q lanes).
+constexpr bool cl_wanted(int nim, int kd) { return nim * kd >= 40; }
+
+// LDS: w [JDa], Vc [RM][JDa], gs [RM][JDa], part [16][JD] (+ c, gL [RM][in_n][JP]).
+template <int D, int JP, int NIM, int RM, bool CL>
 __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __restrict__ u,
                                                                const float* __restrict__ v_saved,
                                                                const float* __restrict__ g_v, int T, int in_n, int J,
                                                                int iters, int mask_first, float* __restrict__ gu) {
   using C = Cfg<D, JP, NIM>;
+  constexpr int RR = CL ? 1 : RM;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = J * D;
   const int JDa = (JD + 3) & ~3;
@@ -38,6 +44,8 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
   float* vcl = wl + JDa;
   float* gsl = vcl + RM * JDa;
   float* part = gsl + RM * JDa;
+  float* cl = part + kWaves * JD;          // [RM][in_n][JP] (CL only)
+  float* gll = cl + RM * in_n * JP;        // [RM][in_n][JP] (CL only)
   const int tid = threadIdx.x;
   const Lane L = lane_map<C>(in_n, J, mask_first);
   const size_t ff = (size_t)in_n * JD;
@@ -46,7 +54,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
   const bool ev = tid < JD;
   float carry = 0.f;   // dL/dv_t carried back from frame t+1 (owner threads)
   float ur[C::NIM][C::KD];
-  float cr[RM][C::NIM], gl[RM][C::NIM];
+  float cr[RR][C::NIM], gl[RR][C::NIM];
   float sr[RM];        // s^r of the owned element
 #pragma unroll
   for (int r = 0; r < RM; ++r) sr[r] = 0.f;
@@ -69,10 +77,16 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       if (r < R) {
-        float w[C::KD];
+        float w[C::KD], cc[C::NIM];
         lds_slice<C::KD>(wl + L.eoff, L.jv, w);
-        logits_softmax<C>(ur, w, L, b, cr[r]);
-        row_partial<C>(cr[r], ur, L, JD, part);
+        logits_softmax<C>(ur, w, L, b, cc);
+        row_partial<C>(cc, ur, L, JD, part);
+        if constexpr (CL) {
+          store_ij<C>(cc, L, cl + r * in_n * JP);
+        } else {
+#pragma unroll
+          for (int k = 0; k < C::NIM; ++k) cr[r][k] = cc[k];
+        }
         __syncthreads();
         if (owner_wave) {
           const float s = ev ? sum_parts(part, JD, tid) : 0.f;
@@ -102,11 +116,17 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
           if (ev) gsl[r * JDa + tid] = gfac * a + dg2 * s;
         }
         __syncthreads();
-        float gsv[C::KD];
+        float gsv[C::KD], cc[C::NIM], gg[C::NIM];
         lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
+        if constexpr (CL) {
+          load_ij<C>(cl + r * in_n * JP, L, cc);
+        } else {
+#pragma unroll
+          for (int k = 0; k < C::NIM; ++k) cc[k] = cr[r][k];
+        }
 #pragma unroll
         for (int k = 0; k < C::NIM; ++k) {
-          gl[r][k] = 0.f;
+          gg[k] = 0.f;
           if (k < L.NI) {
             float p0 = 0.f, p1 = 0.f;
 #pragma unroll
@@ -115,11 +135,17 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
               p1 += ur[k][d + 1] * gsv[d + 1];
             }
             const float q = group_sum<1, C::Q>(p0 + p1);
-            const float sig = group_sum<C::Q, C::ROWL>(cr[r][k] * q);
-            gl[r][k] = cr[r][k] * (q - sig);
+            const float sig = group_sum<C::Q, C::ROWL>(cc[k] * q);
+            gg[k] = cc[k] * (q - sig);
           }
         }
-        row_partial<C>(gl[r], ur, L, JD, part);
+        row_partial<C>(gg, ur, L, JD, part);
+        if constexpr (CL) {
+          store_ij<C>(gg, L, gll + r * in_n * JP);
+        } else {
+#pragma unroll
+          for (int k = 0; k < C::NIM; ++k) gl[r][k] = gg[k];
+        }
         __syncthreads();
         if (ev) {
           const float g = sum_parts(part, JD, tid);   // gVc^r_e
@@ -129,47 +155,59 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
         }
       }
     }
-    // ---- gu (in place of u, which is dead now)
-#pragma unroll
-    for (int k = 0; k < C::NIM; ++k)
-#pragma unroll
-      for (int d = 0; d < C::KD; ++d) ur[k][d] = 0.f;
-#pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      if (r < R) {
-        float gsv[C::KD], vcv[C::KD];
-        lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
-        lds_slice<C::KD>(vcl + r * JDa + L.eoff, L.jv, vcv);
-#pragma unroll
-        for (int k = 0; k < C::NIM; ++k)
-#pragma unroll
-          for (int d = 0; d < C::KD; ++d) ur[k][d] += cr[r][k] * gsv[d] + gl[r][k] * vcv[d];
-      }
-    }
+    // ---- gu, one input capsule of the lane at a time (u is dead: its registers
+    // take the next frame's loads, issued right after)
 #pragma unroll
     for (int k = 0; k < C::NIM; ++k) {
-      if (L.jv && k < L.NI) {
-        float* dst = gu + f * ff + (size_t)(L.g + k * C::G) * JD + L.eoff;
+      if (k < L.NI) {
+        float acc[C::KD];
 #pragma unroll
-        for (int c = 0; c < C::KD; c += 4)
-          *reinterpret_cast<f4*>(dst + c) = f4{ur[k][c], ur[k][c + 1], ur[k][c + 2], ur[k][c + 3]};
+        for (int d = 0; d < C::KD; ++d) acc[d] = 0.f;
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          if (r < R) {
+            float gsv[C::KD], vcv[C::KD];
+            lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
+            lds_slice<C::KD>(vcl + r * JDa + L.eoff, L.jv, vcv);
+            float ck, gk;
+            if constexpr (CL) {
+              const int idx = (L.g + k * C::G) * JP + L.j;
+              ck = cl[r * in_n * JP + idx];
+              gk = gll[r * in_n * JP + idx];
+            } else {
+              ck = cr[r][k];
+              gk = gl[r][k];
+            }
+#pragma unroll
+            for (int d = 0; d < C::KD; ++d) acc[d] += ck * gsv[d] + gk * vcv[d];
+          }
+        }
+        if (L.jv) {
+          float* dst = gu + f * ff + (size_t)(L.g + k * C::G) * JD + L.eoff;
+#pragma unroll
+          for (int c = 0; c < C::KD; c += 4) *reinterpret_cast<f4*>(dst + c) = f4{acc[c], acc[c + 1], acc[c + 2], acc[c + 3]};
+        }
       }
     }
     if (t > 0) load_frame<C>(u + (f - 1) * ff, JD, L, ur);
-    __syncthreads();   // the next frame overwrites w and Vc^0
+    __syncthreads();   // the next frame overwrites w, Vc^0 and the c / gL slabs
   }
 }
 
-size_t bwd_lds(int J, int D, int RM) {
+size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
   const size_t JDa = ((size_t)J * D + 3) & ~(size_t)3;
-  return (JDa * (1 + 2 * (size_t)RM) + (size_t)kWaves * J * D) * sizeof(float);
+  const size_t JP = (size_t)pow2_at_least(J);
+  return (JDa * (1 + 2 * (size_t)RM) + (size_t)kWaves * J * D + (cl ? 2 * (size_t)RM * in_n * JP : 0)) *
+         sizeof(float);
 }
 
 template <int D, int JP, int NIM, int RM>
 int launch_bwd(const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J, int iters,
                int mask_first, float* gu, hipStream_t st) {
-  const size_t lds = bwd_lds(J, D, RM);
-  auto k = sdr_seq_bwd_kernel<D, JP, NIM, RM>;
+  constexpr bool want = cl_wanted(NIM, seq_kd(D, JP));
+  const bool cl = want && bwd_lds(J, D, RM, in_n, true) <= 160 * 1024;
+  const size_t lds = bwd_lds(J, D, RM, in_n, cl);
+  auto k = cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want> : sdr_seq_bwd_kernel<D, JP, NIM, RM, false>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, vs, gv, T, in_n, J, iters, mask_first, gu);
@@ -198,10 +236,6 @@ int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, i
   int nim = 0, rm = 0;
   if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
-    return SRF_EUNSUPPORTED;
-  }
-  if (bwd_lds(J, dout, rm) > 160 * 1024) {
-    srf::set_error("sdr_seq: backward LDS exceeds 160 KiB");
     return SRF_EUNSUPPORTED;
   }
   const int JP = srf_seq::pow2_at_least(J);

@@ -40,7 +40,7 @@ __device__ __forceinline__ float partner(float v) {
 }
 
 // v (+) value of lane ^ O; IEEE + and max are commutative, so both lanes of the
-// pair hold the same bits and a full butterfly leaves a group bit-identical.
+// pair hold the same bits.
 template <int O>
 __device__ __forceinline__ float pair_sum(float v) {
   if constexpr (O == 16) return xor16_sum(v);
@@ -60,16 +60,43 @@ __device__ __forceinline__ float pair_max(float v) {
   }
 }
 
-// all-reduce over the lanes whose index differs only in bits [LO, HI)
+// value of lane (l - N) mod 16 within the lane's 16-lane row (DPP row_ror, VALU only)
+template <int N>
+__device__ __forceinline__ float row_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 | N, 0xF, 0xF, false));
+}
+
+// all-reduce over the lanes whose index differs only in bits [LO, HI).  Bits 2
+// and 3 together go through two DPP row rotations (VALU) instead of two
+// ds_swizzle round trips; max stays bit-identical over the group, a sum may
+// differ in its last bit between lanes (different association order).
 template <int LO, int HI>
 __device__ __forceinline__ float group_sum(float v) {
-  if constexpr (LO < HI) return group_sum<2 * LO, HI>(pair_sum<LO>(v));
-  else return v;
+  if constexpr (LO >= HI) {
+    return v;
+  } else if constexpr (LO == 4 && HI >= 16) {
+    v += row_ror<4>(v);
+    v += row_ror<8>(v);
+    return group_sum<16, HI>(v);
+  } else if constexpr (LO == 8) {
+    return group_sum<16, HI>(v + row_ror<8>(v));   // (l - 8) mod 16 == l ^ 8
+  } else {
+    return group_sum<2 * LO, HI>(pair_sum<LO>(v));
+  }
 }
 template <int LO, int HI>
 __device__ __forceinline__ float group_max(float v) {
-  if constexpr (LO < HI) return group_max<2 * LO, HI>(pair_max<LO>(v));
-  else return v;
+  if constexpr (LO >= HI) {
+    return v;
+  } else if constexpr (LO == 4 && HI >= 16) {
+    v = fmaxf(v, row_ror<4>(v));
+    v = fmaxf(v, row_ror<8>(v));
+    return group_max<16, HI>(v);
+  } else if constexpr (LO == 8) {
+    return group_max<16, HI>(fmaxf(v, row_ror<8>(v)));
+  } else {
+    return group_max<2 * LO, HI>(pair_max<LO>(v));
+  }
 }
 
 // ------------------------------------------------------------------ lane map
@@ -92,6 +119,7 @@ struct Lane {
   int eoff;     // offset of the lane's KD values in a [J*D] vector
   int NI;       // input capsules of the row slot
   bool jv, jm;  // j < J; j < J and not the masked class 0 (naive:174-178, 216-220)
+  bool q0;      // first of the Q lanes of its capsule
 };
 
 template <class C>
@@ -105,7 +133,21 @@ __device__ __forceinline__ Lane lane_map(int in_n, int J, int mask_first) {
   L.NI = L.g < in_n ? (in_n - L.g + C::G - 1) / C::G : 0;
   L.jv = L.j < J;
   L.jm = L.jv && !(mask_first && L.j == 0);
+  L.q0 = (rl % C::Q) == 0;
   return L;
+}
+
+// per-(input capsule, output capsule) scalars of the lane's rows <-> LDS [in_n][JP]
+template <class C>
+__device__ __forceinline__ void store_ij(const float (&v)[C::NIM], const Lane& L, float* __restrict__ dst) {
+#pragma unroll
+  for (int k = 0; k < C::NIM; ++k)
+    if (k < L.NI && L.q0) dst[(L.g + k * C::G) * C::JP + L.j] = v[k];
+}
+template <class C>
+__device__ __forceinline__ void load_ij(const float* __restrict__ src, const Lane& L, float (&v)[C::NIM]) {
+#pragma unroll
+  for (int k = 0; k < C::NIM; ++k) v[k] = k < L.NI ? src[(L.g + k * C::G) * C::JP + L.j] : 0.f;
 }
 
 // the lane's rows of u_t -> registers (zeros for padded capsules and rows)
