@@ -24,6 +24,12 @@
 #include "route_sdr_seq.h"
 #include "route_sdr_seq_dev.h"
 
+// Timing experiments (never in the shipped build): 1 = next frame's loads hit the
+// cache (wrong results), 2 = uniform couplings (no softmax reductions).
+#ifndef SRF_SEQ_DBG
+#define SRF_SEQ_DBG 0
+#endif
+
 namespace {
 
 using namespace srf_seq;
@@ -58,7 +64,11 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
       lds_slice<C::KD>(wl + L.eoff, L.jv, w);
       logits_softmax<C>(ur, w, L, b, c);
       row_partial<C>(c, ur, L, JD, part);
+#if SRF_SEQ_DBG == 1   // timing experiment: re-load the current (cache-hot) frame
+      if (r == iters - 1 && t + 1 < T) load_frame<C>(ub + (size_t)t * ff, JD, L, ur);
+#else
       if (r == iters - 1 && t + 1 < T) load_frame<C>(ub + (size_t)(t + 1) * ff, JD, L, ur);   // u_t is dead
+#endif
       __syncthreads();
       if (owner_wave) {
         const float v = squash_elem<D>(ev ? sum_parts(part, JD, tid) : 0.f);

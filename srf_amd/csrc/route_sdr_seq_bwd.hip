@@ -109,10 +109,10 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
           const float s = sr[r];
           const float n2 = group_sum<1, D>(s * s);
           const float sa = group_sum<1, D>(s * a);
-          const float rs = 1.f / sqrtf(n2 + kSquashEps);
-          const float ip = 1.f / (1.f + n2);
+          const float rs = __builtin_amdgcn_rsqf(n2 + kSquashEps);
+          const float ip = __builtin_amdgcn_rcpf(1.f + n2);
           const float gfac = n2 * ip * rs;
-          const float dg2 = 2.f * rs * ip * (ip - 0.5f * n2 / (n2 + kSquashEps)) * sa;
+          const float dg2 = 2.f * rs * ip * (ip - 0.5f * n2 * rs * rs) * sa;
           if (ev) gsl[r * JDa + tid] = gfac * a + dg2 * s;
         }
         __syncthreads();

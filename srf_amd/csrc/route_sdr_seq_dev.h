@@ -199,10 +199,14 @@ __device__ __forceinline__ void logits_softmax(const float (&ur)[C::NIM][C::KD],
         p1 += ur[k][d + 1] * w[d + 1];
       }
       b[k] += group_sum<1, C::Q>(p0 + p1);
+#if defined(SRF_SEQ_DBG) && SRF_SEQ_DBG == 2
+      c[k] = L.jm ? b[k] * 1e-30f + 0.0625f : 0.f;
+      continue;
+#endif
       const float x = L.jm ? b[k] : -INFINITY;
       const float m = group_max<C::Q, C::ROWL>(x);
       const float e = __expf(x - m);
-      c[k] = e / group_sum<C::Q, C::ROWL>(e);
+      c[k] = e * __builtin_amdgcn_rcpf(group_sum<C::Q, C::ROWL>(e));
     }
   }
 }
@@ -236,11 +240,12 @@ __device__ __forceinline__ float sum_parts(const float* __restrict__ part, int J
   return s;
 }
 
-// squash over the D consecutive owner lanes of a capsule (naive:247-252)
+// squash over the D consecutive owner lanes of a capsule (naive:247-252); the
+// recurrence is VALU-issue bound, so 1-ulp v_rcp / v_rsq replace IEEE div / sqrt
 template <int D>
 __device__ __forceinline__ float squash_elem(float s) {
   const float n2 = group_sum<1, D>(s * s);
-  return s * (n2 / (1.f + n2) / sqrtf(n2 + kSquashEps));
+  return s * (n2 * __builtin_amdgcn_rcpf(1.f + n2) * __builtin_amdgcn_rsqf(n2 + kSquashEps));
 }
 
 }  // namespace srf_seq
