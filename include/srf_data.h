@@ -1,4 +1,5 @@
-/* srf_data.h -- C ABI of the TF-free input pipeline of the SRF path (host only).
+/* srf_data.h -- C ABI of the TF-free host side of the SRF path: the input
+ * pipeline and the CTC beam-search decoder (host only).
  *
  * Replaces the TFRecord I/O the reference does through TensorFlow:
  *   tf.data.TFRecordDataset + tf.io.parse_single_example of
@@ -64,6 +65,15 @@ int srf_tfr_write_example(void* writer, const float* input_speech, int64_t n_inp
                           int64_t target_length, const char* utt_id, int64_t utt_id_len);
 int srf_tfr_write_record(void* writer, const uint8_t* data, size_t n);
 int srf_tfr_writer_close(void* writer);
+
+/* CTC prefix beam search of one utterance, replacing tf.nn.ctc_beam_search_decoder
+ * in process_test_step (trainer_sr.py:109-112; top_paths = 1, no re-merge of repeats).
+ * logits [T][C] row-major fp32 (a log-softmax is applied per frame), blank index
+ * `blank`.  Writes the most probable labelling (at most T labels) to out_labels, its
+ * length to *out_len and its log probability to *out_log_prob (may be NULL).
+ * Returns 0, or -1 on a bad argument. */
+int srf_ctc_beam_search(const float* logits, int T, int C, int blank, int beam_width, int32_t* out_labels,
+                        int* out_len, float* out_log_prob);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,9 @@
 per-utterance negative log likelihood.  This revision computes it with
 the HIP kernel srf_ctc_loss (loss and logit gradient in one launch).
 """
+import ctypes
+
+import numpy as np
 import torch
 
 from . import ops
@@ -36,3 +39,29 @@ def greedy_decode(logits, lengths, blank_index):
             prev = k
         out.append(seq)
     return out
+
+
+def beam_search_decode(logits, lengths, blank_index, beam_width=100):
+    """tf.nn.ctc_beam_search_decoder(time-major logits, lengths, beam_width,
+    top_paths=1) as process_test_step calls it (trainer_sr.py:109-112), on the host
+    prefix beam search of libsrf_data.so.  logits [B, T, C] batch-major (device or
+    host); returns (list of label lists, numpy log probabilities)."""
+    from . import load_speech_data as lsd
+    L = lsd.lib()
+    x = np.ascontiguousarray(logits.detach().float().cpu().numpy())
+    lens = [int(v) for v in torch.as_tensor(lengths).cpu().tolist()]
+    B, T, C = x.shape
+    out, logp = [], np.zeros(B, np.float64)
+    buf = np.zeros(max(T, 1), np.int32)
+    n = ctypes.c_int()
+    lp = ctypes.c_float()
+    for b in range(B):
+        t = max(0, min(lens[b], T))
+        row = x[b]
+        rc = L.srf_ctc_beam_search(row.ctypes.data, t, C, int(blank_index), int(beam_width), buf.ctypes.data,
+                                   ctypes.byref(n), ctypes.byref(lp))
+        if rc != 0:
+            raise ValueError(f'srf_ctc_beam_search: bad argument (T={t}, C={C}, blank={blank_index}, beam={beam_width})')
+        out.append(buf[:n.value].tolist())
+        logp[b] = lp.value
+    return out, logp

@@ -51,6 +51,7 @@ _SIGNATURES = {
                                              ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64]),
     'srf_tfr_write_record': (ctypes.c_int, [_vp, _vp, _sz]),
     'srf_tfr_writer_close': (ctypes.c_int, [_vp]),
+    'srf_ctc_beam_search': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
 }
 
 _lib = None

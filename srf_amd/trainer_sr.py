@@ -104,12 +104,18 @@ def process_valid_step(in_len_div, inputs, model, loss_state, blank_idx):
 
 @torch.no_grad()
 def process_test_step(in_len_div, inputs, model, beam_width=None):
-    """trainer_sr.py:96-117 with best-path decoding (beam search is a next row).
-    Decode lengths use floor division, as the reference does (:110)."""
+    """trainer_sr.py:96-117: forward, then tf.nn.ctc_beam_search_decoder(beam_width,
+    top_paths=1) on the host (srf_amd.ctc.beam_search_decode); best-path decoding
+    when no beam width is configured.  Decode lengths use floor division, as the
+    reference does (:110)."""
     feats, _, inp_len, _, utt_id = inputs
     feats = _crop(feats, inp_len)
     y_pred = model(feats, input_lengths=inp_len, training=False)
-    hyps = ctc.greedy_decode(y_pred, inp_len.to(torch.int64) // in_len_div, y_pred.shape[-1] - 1)
+    lens = inp_len.to(torch.int64) // in_len_div
+    if beam_width:
+        hyps, _ = ctc.beam_search_decode(y_pred, lens, y_pred.shape[-1] - 1, beam_width)
+    else:
+        hyps = ctc.greedy_decode(y_pred, lens, y_pred.shape[-1] - 1)
     for u, h in zip(utt_id, hyps):
         print('UTTID:', u)
         print(h)
