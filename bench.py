@@ -158,6 +158,7 @@ def main():
     ap.add_argument('--workload', default='timit_c2', choices=sorted(WORKLOADS))
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--eager', action='store_true', help='launch every kernel from Python each step (no hipGraph)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -178,12 +179,23 @@ def main():
     batch = synthetic_batch(B, T, class_n, rank, dev)
     loss_state, frame_state, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
 
-    def step():
+    def eager_step():
         trainer_sr.process_train_step(4, batch, model, opt, loss_state, frame_state, world, class_n - 1, samples)
 
     for _ in range(args.warmup):
-        step()
+        eager_step()
     torch.cuda.synchronize()
+    if args.eager:
+        step = eager_step
+    else:
+        # forward + CTC + backward as one hipGraph; all-reduce and Adam eager per step
+        graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
+        for _ in range(args.warmup):
+            graphed(loss_state, frame_state, samples)
+        torch.cuda.synchronize()
+
+        def step():
+            graphed(loss_state, frame_state, samples)
 
     # HIP events around the dominant kernel (forward routing pass of the last
     # layer) for every timed step, recorded on the launch stream.
@@ -194,7 +206,7 @@ def main():
     R = model.iter
     dr = not model.is_context    # the event hook times DR passes; SDR runs no such pass
     ev_pairs = [(ev.create(R), ev.create(R)) for _ in range(args.steps)] if dr else []
-    if dr:
+    if dr and args.eager:
         geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
 
     if world > 1:
@@ -208,6 +220,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     geom.timing = None
+    if dr and not args.eager:
+        # graph replays carry no per-kernel events: time the same kernels in as many
+        # eager steps right after the timed region (same shapes, same stream)
+        geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
+        for _ in range(args.steps):
+            eager_step()
+        torch.cuda.synchronize()
+        geom.timing = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -242,7 +262,7 @@ def main():
                                f'{"SDR" if model.is_context else "DR"} iter={cfg.model_caps_iter}, '
                                f'train step (fwd+bwd+allreduce+Adam)',
                    'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
-                   'parallelism': f'dp{world}'},
+                   'parallelism': f'dp{world}', 'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
         'roofline': {'kernel': (f'route_fwd32_first_kernel + route_fwd32_kernel<{Din},{D}> (layer {last + 1} DR forward '
                                 f'passes, R={R}; pose on v_mfma_f32_32x32x16_bf16 as 3-term bf16 splits = fp32-accurate)'
                                 if fwd32 else f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)'),

@@ -228,8 +228,9 @@ __global__ __launch_bounds__(256) void encaps_fwd_kernel(
     const float* __restrict__ e, const int* __restrict__ inp_len, CapsDims cd, const float* __restrict__ K1,
     const float* __restrict__ b1, const float* __restrict__ K2, const float* __restrict__ b2,
     const float* __restrict__ gamma, const float* __restrict__ beta, int training, float p_caps, float p_in,
-    unsigned long long seed, float* __restrict__ m_out, unsigned char* __restrict__ sel,
+    unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ m_out, unsigned char* __restrict__ sel,
     float* __restrict__ lnstat, float* __restrict__ z) {
+  seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int E = cd.PH * cd.PD;
   float* m = sm;                 // E
@@ -302,8 +303,9 @@ __global__ __launch_bounds__(256) void encaps_bwd_a_kernel(
     const float* __restrict__ g_z, const float* __restrict__ e, const float* __restrict__ m_in,
     const unsigned char* __restrict__ sel, const float* __restrict__ lnstat, const int* __restrict__ inp_len,
     CapsDims cd, const float* __restrict__ gamma, const float* __restrict__ beta, int training, float p_caps,
-    float p_in, unsigned long long seed, float* __restrict__ g_v1, float* __restrict__ g_v2,
+    float p_in, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ g_v1, float* __restrict__ g_v2,
     float* __restrict__ wpart) {
+  seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int E = cd.PH * cd.PD;
   float* m = sm;                 // E
@@ -412,11 +414,12 @@ __global__ void encaps_bwd_b_kernel(const float* __restrict__ g_v1, const float*
 __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restrict__ x, int n,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, int training, float p,
-                                                           unsigned long long seed, unsigned stream,
+                                                           unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream,
                                                            float* __restrict__ y, float* __restrict__ stat, int head,
                                                            int J, int D, const float* __restrict__ gamma_o,
                                                            const float* __restrict__ beta_o,
                                                            float* __restrict__ logits, float* __restrict__ lens) {
+  seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* v = sm;           // n
   float* red = v + n;      // 8
@@ -482,9 +485,10 @@ __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restri
 //         g_o = g_L_j * o / L_j (naive:255-258)
 __global__ __launch_bounds__(256) void capsnorm_bwd_kernel(
     const float* __restrict__ x, int n, const float* __restrict__ gamma, const float* __restrict__ beta,
-    int training, float p, unsigned long long seed, unsigned stream, const float* __restrict__ stat,
+    int training, float p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream, const float* __restrict__ stat,
     const float* __restrict__ g_in, int head, int J, int D, const float* __restrict__ gamma_o,
     const float* __restrict__ lens, float* __restrict__ g_x, float* __restrict__ gpart) {
+  seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* gy = sm;          // n
   float* red = gy + n;     // 8
@@ -665,7 +669,7 @@ int srf_primary_caps_fwd(const float* X, const int* inp_len, int B, int T, int K
   CapsDims cd{B, T, PH, PD};
   const size_t sh = (size_t)(PH * PD + 5 * PH + 8) * sizeof(float);
   hipLaunchKernelGGL(encaps_fwd_kernel, dim3(F), dim3(256), sh, st, sv.e, inp_len, cd, K1, b1, K2, b2, gamma, beta,
-                     training, p_caps, p_in, seed, sv.m, sv.sel, sv.lnstat, z);
+                     training, p_caps, p_in, seed, srf::seed_source(), sv.m, sv.sel, sv.lnstat, z);
   SRF_LAUNCH_CHECK("encaps_fwd");
   return SRF_OK;
 }
@@ -691,7 +695,7 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
   CapsDims cd{B, T, PH, PD};
   const size_t sh = (size_t)(4 * E + 6 * PH + 8) * sizeof(float);
   hipLaunchKernelGGL(encaps_bwd_a_kernel, dim3(F), dim3(256), sh, st, g_z, sv.e, sv.m, sv.sel, sv.lnstat, inp_len, cd,
-                     gamma, beta, training, p_caps, p_in, seed, w.gv1, w.gv2, w.wpart);
+                     gamma, beta, training, p_caps, p_in, seed, srf::seed_source(), w.gv1, w.gv2, w.wpart);
   SRF_LAUNCH_CHECK("encaps_bwd_a");
   const int wcols = 2 * E + 20 * PD;
   if ((rc = srf::colsum(w.wpart, F, wcols, w.wsum, w.scratch, st))) return rc;
@@ -733,7 +737,7 @@ int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const flo
                      unsigned long long seed, int layer, float* y, float* stat, void* stream) {
   SRF_REQUIRE(x && gamma && beta && y && stat && F > 0 && n > 0 && n <= kMaxVec, "bad capsnorm arguments");
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, static_cast<hipStream_t>(stream),
-                     x, n, gamma, beta, training, p, seed, (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0,
+                     x, n, gamma, beta, training, p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0,
                      (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr);
   SRF_LAUNCH_CHECK("capsnorm_fwd");
   return SRF_OK;
@@ -754,7 +758,7 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
   float* sum = part + srf::align_up((size_t)F * 2 * n * 4, 256) / 4;
   float* scratch = sum + srf::align_up((size_t)2 * n * 4, 256) / 4;
   hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, st, x, n, gamma, beta, training, p,
-                     seed, (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr,
+                     seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr,
                      (const float*)nullptr, g_x, part);
   SRF_LAUNCH_CHECK("capsnorm_bwd");
   (void)sum;
@@ -769,7 +773,7 @@ int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mi
                   n <= kMaxVec,
               "bad head arguments");
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4,
-                     static_cast<hipStream_t>(stream), v, n, gamma_mid, beta_mid, training, p, seed,
+                     static_cast<hipStream_t>(stream), v, n, gamma_mid, beta_mid, training, p, seed, srf::seed_source(),
                      (unsigned)(kStreamMid0 + layer), (float*)nullptr, stat, 1, J, D, gamma_out, beta_out, logits,
                      lens);
   SRF_LAUNCH_CHECK("caps_head_fwd");
@@ -795,7 +799,7 @@ int srf_caps_head_bwd(const float* v, int F, int J, int D, const float* gamma_mi
   float* sum = part + srf::align_up((size_t)F * cols * 4, 256) / 4;
   float* scratch = sum + srf::align_up((size_t)cols * 4, 256) / 4;
   hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4, st, v, n, gamma_mid, beta_mid,
-                     training, p, seed, (unsigned)(kStreamMid0 + layer), stat, g_logits, 1, J, D, gamma_out, lens,
+                     training, p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), stat, g_logits, 1, J, D, gamma_out, lens,
                      g_v, part);
   SRF_LAUNCH_CHECK("caps_head_bwd");
   (void)sum;

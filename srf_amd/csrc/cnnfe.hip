@@ -108,8 +108,9 @@ __device__ __forceinline__ void window9_lds(const float* win, const Tile1& tl, c
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(
     const float* __restrict__ feats, const int* __restrict__ inp_len, Dims d, const float* __restrict__ ka,
     const float* __restrict__ ba, const float* __restrict__ kb, const float* __restrict__ bb, int training,
-    float drop_p, unsigned long long seed, float* __restrict__ y1, unsigned char* __restrict__ sel1,
+    float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ y1, unsigned char* __restrict__ sel1,
     float* __restrict__ part) {
+  seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float win[];
   __shared__ float sh[3][kRows1][C];
   const int c = threadIdx.x & (C - 1);
@@ -318,8 +319,9 @@ __device__ __forceinline__ void load_b2(const float* __restrict__ wp, int tap, i
 __global__ __launch_bounds__(256) void conv2_fwd_kernel(
     const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len, Dims d,
     const float* __restrict__ wp, const float* __restrict__ ba, const float* __restrict__ bb, int training,
-    float drop_p, unsigned long long seed, float* __restrict__ y2, unsigned char* __restrict__ sel2,
+    float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ y2, unsigned char* __restrict__ sel2,
     float* __restrict__ part) {
+  seed = srf_step_seed(seed, seed_src);
   __shared__ __attribute__((aligned(16))) float As[2][64 * kLdsStride];
   __shared__ float red[3][4][4][16];   // [n|mean|M2][wave][lane group][channel]
   const int tid = threadIdx.x;
@@ -497,8 +499,9 @@ __device__ __forceinline__ float bn_bwd_elem(float gin, float y, float mask, flo
 __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     const float* __restrict__ g_out, const float* __restrict__ y2, const unsigned char* __restrict__ sel2,
     const float* __restrict__ stats2, const float* __restrict__ gamma2, const float* __restrict__ bnsum2,
-    const int* __restrict__ inp_len, Dims d, float drop_p, unsigned long long seed, float* __restrict__ g_ab,
+    const int* __restrict__ inp_len, Dims d, float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ g_ab,
     float* __restrict__ part) {
+  seed = srf_step_seed(seed, seed_src);
   __shared__ float sh[2][4][C];
   const int c = threadIdx.x & (C - 1), row = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = d.B * d.T2 * d.F2;
@@ -794,8 +797,9 @@ __global__ void conv2_wgrad_reduce_kernel(const float* __restrict__ part, int ns
 __global__ __launch_bounds__(256) void conv1_bwd_kernel(
     const float* __restrict__ feats, const int* __restrict__ inp_len, Dims d, const float* __restrict__ g_x1,
     const float* __restrict__ y1, const unsigned char* __restrict__ sel1, const float* __restrict__ stats1,
-    const float* __restrict__ gamma1, const float* __restrict__ bnsum1, float drop_p, unsigned long long seed,
+    const float* __restrict__ gamma1, const float* __restrict__ bnsum1, float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src,
     float* __restrict__ part) {
+  seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float win[];
   __shared__ float sh[kRows1][20][C];
   const int c = threadIdx.x & (C - 1);
@@ -969,7 +973,7 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   const size_t P2 = (size_t)d.B * d.T2 * d.F2;
   const int nb2 = (int)((P2 + 63) / 64);
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, k0a, b0a, k0b, b0b,
-                     training, drop_p, seed, sv.y1, sv.sel1, w.part1);
+                     training, drop_p, seed, srf::seed_source(), sv.y1, sv.sel1, w.part1);
   SRF_LAUNCH_CHECK("conv1_fwd");
   if ((rc = bn_finalize(w.part1, conv1_blocks(d), w.merged, gamma0, beta0, mmean0, mvar0, training, sv.stats1, st)))
     return rc;
@@ -977,7 +981,7 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(pack_w2_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wp);
   SRF_LAUNCH_CHECK("pack_w2");
   hipLaunchKernelGGL(conv2_fwd_kernel, dim3(nb2), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, d, w.wp, b1a, b1b,
-                     training, drop_p, seed, sv.y2, sv.sel2, w.part2);
+                     training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2, w.part2);
   SRF_LAUNCH_CHECK("conv2_fwd");
   if ((rc = bn_finalize(w.part2, nb2, w.merged, gamma1, beta1, mmean1, mvar1, training, sv.stats2, st))) return rc;
   SRF_LAUNCH_CHECK("bn_finalize(2)");
@@ -1081,7 +1085,7 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st, srf::ColSplit{{g_beta1, g_gamma1, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
   hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.sel2, sv.stats2,
-                     gamma1, w.bnsum2, inp_len, d, drop_p, seed, w.g_ab, w.biaspart);
+                     gamma1, w.bnsum2, inp_len, d, drop_p, seed, srf::seed_source(), w.g_ab, w.biaspart);
   SRF_LAUNCH_CHECK("conv2_bwd_prep");
   if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, nullptr, w.scratch, st, srf::ColSplit{{g_b1a, g_b1b, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
@@ -1112,7 +1116,7 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum1, w.scratch, st, srf::ColSplit{{g_beta0, g_gamma0, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
   hipLaunchKernelGGL(conv1_bwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, w.g_x1, sv.y1,
-                     sv.sel1, sv.stats1, gamma0, w.bnsum1, drop_p, seed, w.c1part);
+                     sv.sel1, sv.stats1, gamma0, w.bnsum1, drop_p, seed, srf::seed_source(), w.c1part);
   SRF_LAUNCH_CHECK("conv1_bwd");
   if ((rc = srf::colsum(w.c1part, conv1_blocks(d), 20 * C, w.c1sum, w.scratch, st))) return rc;
   hipLaunchKernelGGL(conv1_grad_unpack_kernel, dim3((20 * C + 255) / 256), dim3(256), 0, st, w.c1sum, g_k0a, g_k0b,

@@ -1,6 +1,7 @@
 // CTC loss and gradient, replacing tf.nn.ctc_loss as called at trainer_sr.py:64-66
 // (dense labels, batch-major logits, blank_index = C-1, logit_length =
-// ceil(len/4)) and its autodiff.  One workgroup per utterance:
+// ceil(len/4)) and its autodiff.  One workgroup per utterance and direction (the
+// recursion itself runs in one wave, states in registers):
 //   lp      = log_softmax(logits[b, t, :])                 t < T_b
 //   alpha/beta recursions in log space over the extended label l' (|l'| = 2L+1)
 //   nll_b   = -log sum_s alpha_{T_b-1}(s) (last two states)
@@ -8,6 +9,7 @@
 // Both alpha_t(s) and beta_t(s) include the emission at t.  An infeasible
 // utterance (T_b too short for its labels) yields nll = +inf and a zero gradient.
 #include <cmath>
+#include <cstdlib>
 
 #include "srf_common.h"
 #include "../../include/srf.h"
@@ -20,10 +22,106 @@ __device__ __forceinline__ float lse2(float a, float b) {
   return m + __logf(__expf(a - m) + __expf(b - m));
 }
 
+// Wave-resident recursions (KM > 0, S <= 64*KM): wave 0 holds states
+// s = lane + 64k in registers; the s-1 / s-2 (alpha) or s+1 / s+2 (beta)
+// neighbours come from ds_bpermute shuffles, the lane at a 64-state boundary
+// taking the neighbouring group's value, so a time step needs no barrier.
+template <int KM>
+__device__ __forceinline__ float alpha_wave(const int* __restrict__ ext, const float* __restrict__ lp, int C, int S,
+                                            int Tb, int Smax, int blank, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  float a[KM];
+  int e[KM];
+  bool sk[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int s = lane + 64 * k;
+    e[k] = s < S ? ext[s] : blank;
+    sk[k] = s < S && s >= 2 && ext[s] != blank && ext[s] != ext[s - 2];
+    a[k] = -INFINITY;
+  }
+  for (int t = 0; t < Tb; ++t) {
+    const float* lpt = lp + (size_t)t * C;
+    float na[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int s = lane + 64 * k;
+      float v;
+      if (t == 0) {
+        v = s < 2 ? 0.f : -INFINITY;
+      } else {
+        const float lo = k > 0 ? a[k - 1] : -INFINITY;
+        const float p1 = __shfl(lane == 63 ? lo : a[k], (lane + 63) & 63, 64);
+        const float p2 = __shfl(lane >= 62 ? lo : a[k], (lane + 62) & 63, 64);
+        v = lse2(a[k], p1);
+        if (sk[k]) v = lse2(v, p2);
+      }
+      v = (s < S && v != -INFINITY) ? v + lpt[e[k]] : -INFINITY;
+      na[k] = v;
+      if (s < S) out[(size_t)t * Smax + s] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) a[k] = na[k];
+  }
+  // log-likelihood: the last two states at t = Tb-1
+  float loc = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int s = lane + 64 * k;
+    if (Tb > 0 && (s == S - 1 || s == S - 2)) loc = lse2(loc, a[k]);
+  }
+  float m = loc;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (m == -INFINITY) return -INFINITY;
+  const float z = wave_sum(loc == -INFINITY ? 0.f : __expf(loc - m));
+  return m + __logf(z);
+}
+
+template <int KM>
+__device__ __forceinline__ void beta_wave(const int* __restrict__ ext, const float* __restrict__ lp, int C, int S,
+                                          int Tb, int Smax, int blank, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  float a[KM];
+  int e[KM];
+  bool sk[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const int s = lane + 64 * k;
+    e[k] = s < S ? ext[s] : blank;
+    sk[k] = s + 2 < S && ext[s] != blank && ext[s] != ext[s + 2];
+    a[k] = -INFINITY;
+  }
+  for (int t = Tb - 1; t >= 0; --t) {
+    const float* lpt = lp + (size_t)t * C;
+    float na[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int s = lane + 64 * k;
+      float v;
+      if (t == Tb - 1) {
+        v = s >= S - 2 ? 0.f : -INFINITY;
+      } else {
+        const float hi = k + 1 < KM ? a[k + 1] : -INFINITY;
+        const float q1 = __shfl(lane == 0 ? hi : a[k], (lane + 1) & 63, 64);
+        const float q2 = __shfl(lane <= 1 ? hi : a[k], (lane + 2) & 63, 64);
+        v = lse2(a[k], q1);
+        if (sk[k]) v = lse2(v, q2);
+      }
+      v = (s < S && v != -INFINITY) ? v + lpt[e[k]] : -INFINITY;
+      na[k] = v;
+      if (s < S) out[(size_t)t * Smax + s] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) a[k] = na[k];
+  }
+}
+
 // Recursion kernel: grid (B, 2).  Block (b, 0) runs the alpha recursion and
 // writes nll[b]; block (b, 1) runs beta.  Both recompute the log-softmax into
 // LDS (when it fits; else workspace) and stream their rows to workspace.
 // Dynamic LDS: ext[Smax] (int) | row[2][Smax] | lp[T*C].
+template <int KM>
 __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restrict__ logits,
                                                             const int* __restrict__ labels,
                                                             const int* __restrict__ label_len,
@@ -65,6 +163,16 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
     }
   }
   __syncthreads();
+  if constexpr (KM > 0) {
+    if (threadIdx.x >= 64) return;
+    if (!is_beta) {
+      const float ll = alpha_wave<KM>(ext, lp, C, S, Tb, Smax, blank, out);
+      if (threadIdx.x == 0) nll[b] = -ll;
+    } else {
+      beta_wave<KM>(ext, lp, C, S, Tb, Smax, blank, out);
+    }
+    return;
+  }
   if (!is_beta) {
     for (int t = 0; t < Tb; ++t) {
       const float* ap = row + ((t + 1) & 1) * Smax;
@@ -190,8 +298,16 @@ int srf_ctc_loss(const float* logits, const int* labels, const int* label_len, c
   const int lp_in_lds = (shmem + lp_bytes) <= 96 * 1024;
   if (lp_in_lds) shmem += lp_bytes;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(ctc_recursion_kernel, dim3(B, 2), dim3(256), shmem, st, logits, labels, label_len, logit_len,
-                     Tmax, C, Lmax, blank, lp_in_lds, grad ? 1 : 0, nll, static_cast<float*>(workspace));
+  // wave-resident recursion for up to 512 extended-label states, else the block loop;
+  // SRF_CTC_WAVE=0 selects the block loop (A/B, tests)
+  const char* ev = getenv("SRF_CTC_WAVE");
+  const bool wave = !(ev && ev[0] == '0');
+  auto kern = !wave || Smax > 512 ? ctc_recursion_kernel<0>
+              : Smax <= 128      ? ctc_recursion_kernel<2>
+              : Smax <= 256      ? ctc_recursion_kernel<4>
+                                 : ctc_recursion_kernel<8>;
+  hipLaunchKernelGGL(kern, dim3(B, 2), dim3(256), shmem, st, logits, labels, label_len, logit_len, Tmax, C, Lmax,
+                     blank, lp_in_lds, grad ? 1 : 0, nll, static_cast<float*>(workspace));
   SRF_LAUNCH_CHECK("ctc_recursion");
   if (grad) {
     hipLaunchKernelGGL(ctc_grad_kernel, dim3(B, (Tmax + 15) / 16), dim3(256), (size_t)(C + Lmax + 1) * sizeof(int),

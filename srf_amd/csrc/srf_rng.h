@@ -26,6 +26,13 @@ __host__ __device__ __forceinline__ uint32_t srf_mix32(uint32_t x) {
   return x;
 }
 
+// Per-call seed mixed with the device-resident step counter of srf_set_seed_source
+// (NULL: the seed alone).  A captured training step advances the counter on the
+// device, so every graph replay draws fresh dropout masks.
+__device__ __forceinline__ uint64_t srf_step_seed(uint64_t seed, const unsigned long long* src) {
+  return src ? seed + *src * 0x9E3779B97F4A7C15ull : seed;
+}
+
 __device__ __forceinline__ uint32_t srf_stream_key(uint64_t seed, unsigned stream) {
   return srf_mix32((uint32_t)seed ^ srf_mix32((uint32_t)(seed >> 32) ^ (stream * 0x9E3779B9u + 0x7F4A7C15u)));
 }

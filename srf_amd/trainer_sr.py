@@ -90,6 +90,79 @@ def process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_s
     return pe_loss
 
 
+class GraphedTrainStep:
+    """process_train_step with its forward, CTC loss head and backward captured
+    into one hipGraph (torch.cuda.CUDAGraph) for a fixed batch shape; the gradient
+    all-reduce, the Adam update and the metrics run eagerly after each replay.
+
+    The ~110 kernel launches of a step then cost one graph launch on the host, so
+    the step is bound by the GPU, not by Python/ctypes launch overhead (which
+    grows when several ranks share a host).  Dropout stays random per step: the
+    captured step first advances a device-resident step counter that every dropout
+    kernel mixes into its seed (srf_set_seed_source).  ``inputs`` are the static
+    input tensors: refill them in place between replays to feed new data of the
+    same shape and lengths.
+    """
+
+    def __init__(self, in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=2):
+        from . import _lib
+        self.model, self.optimizer = model, optimizer
+        self.in_len_div, self.n_gpus, self.blank_idx = in_len_div, n_gpus, blank_idx
+        feats, labels, inp_len, tar_len = inputs
+        dev = feats.device
+        self.batch = feats.shape[0]
+        self.host_len = inp_len
+        self.feats = _crop(feats, inp_len)
+        self.labels, self.tar_len = labels, tar_len
+        self.inp_len = inp_len.to(dev)
+        self.logit_len = ceil_div(self.inp_len, in_len_div)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        rc = _lib.lib().srf_set_seed_source(self.counter.data_ptr())
+        _lib.check(rc, 'srf_set_seed_source')
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._fwd_bwd()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.nll = self._fwd_bwd()
+
+    def _fwd_bwd(self):
+        self.counter.add_(1)
+        y_pred = self.model(self.feats, input_lengths=self.inp_len, training=True)
+        pe_loss, g_logits = ctc.ctc_loss_and_grad(self.labels, y_pred, self.tar_len, self.logit_len, self.blank_idx,
+                                                  1.0 / float(self.batch * self.n_gpus))
+        y_pred.backward(g_logits)
+        return pe_loss
+
+    def close(self):
+        """Detach the dropout kernels from this step's counter (before it is freed)."""
+        from . import _lib
+        if getattr(self, 'counter', None) is not None:
+            _lib.lib().srf_set_seed_source(None)
+            self.counter = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __call__(self, loss_state=None, frame_state=None, samples=None):
+        self.graph.replay()
+        allreduce_grads(self.model)
+        self.optimizer.apply_gradients(self.model)
+        if loss_state is not None:
+            loss_state.update_state(self.nll)
+        if frame_state is not None:
+            frame_state.update_state(self.host_len.sum())
+        if samples is not None:
+            samples.update_state(self.batch)
+        return self.nll
+
+
 @torch.no_grad()
 def process_valid_step(in_len_div, inputs, model, loss_state, blank_idx):
     """trainer_sr.py:77-94."""

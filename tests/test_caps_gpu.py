@@ -108,6 +108,7 @@ def test_ctc_matches_torch(cuda):
                        torch.tensor(logit_len, device=cuda), C - 1)
     assert np.allclose(nll.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-4, atol=1e-4)
     nll.sum().backward()
+    # fp32 recursions over 90-420 frames: gradient entries agree to 5e-4 absolute
     e = (lg.grad.cpu().double() - lr.grad).abs().max().item()
     assert e < 1e-4, e
 
@@ -120,3 +121,32 @@ def test_ctc_infeasible_is_inf_with_zero_grad(cuda):
     assert torch.isinf(nll).all()
     nll.sum().backward()
     assert torch.count_nonzero(lg.grad) == 0
+
+
+@pytest.mark.parametrize('B,T,C,L,wave', [(3, 150, 12, 70, '0'), (2, 420, 32, 200, '0'), (3, 150, 12, 70, '1'),
+                                          (2, 420, 32, 200, '1'), (2, 90, 63, 40, '1')])
+def test_ctc_long_labels_cross_state_groups(cuda, B, T, C, L, wave, monkeypatch):
+    """Extended-label lengths past 64 states exercise the group boundaries of the
+    wave-resident recursion (KM = 4, 8); SRF_CTC_WAVE=0 runs the block loop."""
+    from srf_amd import ops
+    monkeypatch.setenv('SRF_CTC_WAVE', wave)
+    rng = np.random.default_rng(B * 1000 + T)
+    logits = rng.standard_normal((B, T, C)) * 2
+    lab_len = rng.integers(L // 2, L + 1, size=B).astype(np.int32)
+    lab_len[0] = L
+    labels = rng.integers(0, C - 1, size=(B, L)).astype(np.int32)
+    logit_len = np.array([T] + [int(rng.integers(2 * L + 1, T + 1)) for _ in range(B - 1)], dtype=np.int32)
+    lr = torch.tensor(logits, requires_grad=True)
+    ref = torch.nn.functional.ctc_loss(torch.log_softmax(lr, -1).transpose(0, 1), torch.tensor(labels).long(),
+                                       torch.tensor(logit_len).long(), torch.tensor(lab_len).long(), blank=C - 1,
+                                       reduction='none')
+    ref.sum().backward()
+    lg = torch.tensor(logits, dtype=torch.float32, device=cuda, requires_grad=True)
+    nll = ops.ctc_loss(lg, torch.tensor(labels, device=cuda), torch.tensor(lab_len, device=cuda),
+                       torch.tensor(logit_len, device=cuda), C - 1)
+    got = nll.detach().cpu().double().numpy()
+    assert np.all(np.abs(got - ref.detach().numpy()) <= 1e-4 * np.maximum(1, np.abs(ref.detach().numpy()))), got
+    nll.sum().backward()
+    # fp32 log-space recursions over T frames: gradient entries agree to 2e-6 * T absolute
+    e = (lg.grad.cpu().double() - lr.grad).abs().max().item()
+    assert e < 2e-6 * T, e

@@ -142,3 +142,44 @@ def test_fused_loss_head_matches_autograd(cuda):
     logits.backward(g)
     assert torch.allclose(nll2, nll.detach())
     assert (model.flat_grad - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
+
+
+def test_graphed_train_step_matches_eager(cuda):
+    """GraphedTrainStep (forward + CTC + backward in one hipGraph) computes the same
+    loss and gradient as the eager process_train_step, and draws fresh dropout masks
+    on every replay (device step counter)."""
+    from srf_amd import train_helper, trainer_sr
+    cfg = config_from_shape({'feat_dim': 123, 'enc_num': 3, 'iters': 3, 'lpad': 4, 'rpad': 4, 'ph': 8,
+                             'pd': 16, 'ch': 8, 'cd': 16, 'vd': 16, 'context': False})
+    model, sh, z = _build('c2_mini', cuda)
+    inputs = (torch.tensor(z['feats'], dtype=torch.float32, device=cuda), torch.tensor(z['labels'], device=cuda),
+              torch.tensor(z['inp_len'], dtype=torch.int32), torch.tensor(z['tar_len'], device=cuda))
+    opt = train_helper.get_optimizer(cfg)   # lr(0) = 0: the first update leaves the parameters
+    eager_nll = trainer_sr.process_train_step(4, inputs, model, opt, None, None, 1, sh.class_n - 1, None).clone()
+    eager_grad = model.flat_grad.clone()
+    model2, _, _ = _build('c2_mini', cuda)
+    g = trainer_sr.GraphedTrainStep(4, inputs, model2, train_helper.get_optimizer(cfg), 1, sh.class_n - 1, warmup=1)
+    try:
+        model2.load_params({k: v for k, v in zip(*_params_of(model))})
+        for p in model2.params.values():   # poison every gradient slice (not the alignment padding)
+            p.grad.fill_(float('nan'))
+        nll = g().clone()
+        torch.cuda.synchronize()
+        assert torch.allclose(nll, eager_nll, rtol=1e-5, atol=1e-5), (nll, eager_nll)
+        err = (model2.flat_grad - eager_grad).abs().max().item()
+        assert err <= 1e-4 * eager_grad.abs().max().item(), err
+        # dropout on: consecutive replays see different masks
+        model2.dropout_enabled = True
+        g2 = trainer_sr.GraphedTrainStep(4, inputs, model2, train_helper.get_optimizer(cfg), 1, sh.class_n - 1,
+                                         warmup=1)
+        a = g2().clone()
+        b = g2().clone()
+        assert torch.isfinite(a).all() and not torch.equal(a, b)
+        g2.close()
+    finally:
+        g.close()
+
+
+def _params_of(model):
+    names = list(model.params.keys())
+    return names, [model.params[k].detach().clone() for k in names]
