@@ -144,7 +144,29 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
   float* out = gws + (size_t)Tmax * C + (is_beta ? (size_t)Tmax * Smax : 0);
   const float* lg = logits + (size_t)b * Tmax * C;
   for (int s = threadIdx.x; s < S; s += blockDim.x) ext[s] = (s & 1) ? labels[(size_t)b * Lmax + (s >> 1)] : blank;
-  {
+  if (C <= 64) {
+    // one class per lane; 8 rows per wave in flight, so the row loads overlap
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+    constexpr int RB = 8;
+    for (int t0 = w * RB; t0 < Tb; t0 += nw * RB) {
+      float v[RB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) v[r] = (l < C && t0 + r < Tb) ? lg[(size_t)(t0 + r) * C + l] : -INFINITY;
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        float m = v[r];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        const float z = wave_sum(l < C ? __expf(v[r] - m) : 0.f);
+        const float lz = m + __logf(z);
+        if (l < C && t0 + r < Tb) {
+          const size_t o = (size_t)(t0 + r) * C + l;
+          lp[o] = v[r] - lz;
+          if (!is_beta && lp_in_lds) lpg[o] = v[r] - lz;
+        }
+      }
+    }
+  } else {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
     for (int t = w; t < Tb; t += nw) {
       float m = -INFINITY;
