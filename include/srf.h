@@ -126,6 +126,21 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
                          float p_caps, float p_in, unsigned long long seed, const void* saved, const float* g_z,
                          float* g_X, float* g_Wp, float* g_bp, float* g_K1, float* g_b1, float* g_K2, float* g_b2,
                          float* g_gamma, float* g_beta, void* workspace, size_t workspace_bytes, void* stream);
+/* The einsum variant (sequence_router_einsum.py:129-131): e = (X Wp + bp) * proj_scale
+ * (+ get_pos_enc(T, PH), model_helper.py:30-58, when pos_enc != 0; PH even, >= 4)
+ * before the encaps convs.  The plain entry points are proj_scale = 1, pos_enc = 0
+ * (naive and lowmemory, naive:131-132 / lowmemory:133-135). */
+int srf_primary_caps_fwd_ex(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                            const float* bp, const float* K1, const float* b1, const float* K2, const float* b2,
+                            const float* gamma, const float* beta, int training, float p_caps, float p_in,
+                            unsigned long long seed, float proj_scale, int pos_enc, float* z, void* saved,
+                            size_t saved_bytes, void* stream);
+int srf_primary_caps_bwd_ex(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                            const float* K1, const float* K2, const float* gamma, const float* beta, int training,
+                            float p_caps, float p_in, unsigned long long seed, float proj_scale, const void* saved,
+                            const float* g_z, float* g_X, float* g_Wp, float* g_bp, float* g_K1, float* g_b1,
+                            float* g_K2, float* g_b2, float* g_gamma, float* g_beta, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 /* ---- Per-layer LayerNorm + dropout and the output head (naive:187-193) -----
  * capsnorm: y = drop(LN(x)) per frame over n = J*D (ln_mid%d + dropout_mid_%d);
@@ -140,6 +155,12 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
 int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
                       const float* gamma_out, const float* beta_out, int training, float p, unsigned long long seed,
                       int layer, float* logits, float* stat, float* lens, void* stream);
+/* length_eps of the output length: 1e-7 for naive / lowmemory (naive:256,
+ * sequence_router.py:39), 1e-9 for einsum (sequence_router_einsum.py:238).  The
+ * backward reads the saved lens, so it is the same for every variant. */
+int srf_caps_head_fwd_ex(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
+                         const float* gamma_out, const float* beta_out, int training, float p, unsigned long long seed,
+                         int layer, float length_eps, float* logits, float* stat, float* lens, void* stream);
 int srf_caps_head_bwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
                       const float* gamma_out, int training, float p, unsigned long long seed, int layer,
                       const float* stat, const float* lens, const float* g_logits, float* g_v, float* g_gamma_mid,

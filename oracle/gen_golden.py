@@ -53,6 +53,13 @@ MODEL_CASES = {
                      class_n=63, context=False), 2, [37, 29], [5, 3], 12),
     'c3_mini_sdr': (dict(feat_dim=123, enc_num=2, iters=3, lpad=2, rpad=2, ph=4, pd=8, ch=4, cd=8, vd=8,
                          class_n=32, context=True), 2, [26, 19], [4, 2], 13),
+    # the other two reference variants (trainer_sr.py:188-199), C2-shaped but smaller
+    'c2_mini_einsum': (dict(feat_dim=123, enc_num=2, iters=3, lpad=2, rpad=2, ph=8, pd=8, ch=8, cd=8, vd=8,
+                            class_n=63, context=False, caps_type='einsum'), 2, [37, 29], [5, 3], 14),
+    'c2_mini_lowmemory': (dict(feat_dim=123, enc_num=2, iters=3, lpad=2, rpad=2, ph=8, pd=8, ch=8, cd=8, vd=8,
+                               class_n=63, context=False, caps_type='lowmemory'), 2, [37, 29], [5, 3], 15),
+    'c3_mini_sdr_lowmemory': (dict(feat_dim=123, enc_num=2, iters=3, lpad=2, rpad=2, ph=4, pd=8, ch=4, cd=8, vd=8,
+                                   class_n=32, context=True, caps_type='lowmemory'), 2, [26, 19], [4, 2], 16),
 }
 
 
@@ -73,8 +80,10 @@ def gen_flags():
             json.dump({'argv': argv, 'parsed': args}, fh, indent=1, sort_keys=True)
 
 
-def gen_models():
+def gen_models(only=()):
     for name, (kw, B, lens, tlens, seed) in MODEL_CASES.items():
+        if only and name not in only:
+            continue
         sh = so.SrfShape(**kw)
         P = so.init_params(sh, seed=seed)
         rng = np.random.default_rng(seed + 100)
@@ -98,7 +107,9 @@ def gen_models():
         pe = nm.ctc_per_utt(lt, torch.tensor(labels), torch.tensor(inp_len), torch.tensor(tar_len), sh.class_n)
         assert np.abs(pe.detach().numpy() - nll).max() < 1e-9, 'ctc oracle/torch disagree'
         (pe.sum() / B).backward()
-        grads = {'grad.' + k.replace('__', '.'): p.grad.numpy() for k, p in m.p.items()}
+        # no gradient (lowmemory DR W/b, unused by the graph): TF's apply_gradients skips them, stored as 0
+        grads = {'grad.' + k.replace('__', '.'): (p.grad.numpy() if p.grad is not None else np.zeros(p.shape))
+                 for k, p in m.p.items()}
         out = {'shape_json': np.array(json.dumps(kw)), 'feats': feats, 'inp_len': inp_len, 'labels': labels,
                'tar_len': tar_len, 'logits': logits, 'nll': nll,
                'greedy_json': np.array(json.dumps(greedy))}
@@ -113,5 +124,7 @@ def gen_models():
 
 if __name__ == '__main__':
     os.makedirs(GOLD, exist_ok=True)
-    gen_flags()
-    gen_models()
+    only = sys.argv[1:]   # optional model case names: regenerate just those
+    if not only:
+        gen_flags()
+    gen_models(only)

@@ -58,9 +58,9 @@ def squash(s, dim=-1):
     return n2 / (1.0 + n2) * (s / torch.sqrt(n2 + so.SQUASH_EPS))
 
 
-def length(s, dim=-1):
-    """naive:255-258."""
-    return torch.sqrt(torch.sum(torch.square(s), dim=dim) + so.LENGTH_EPS)
+def length(s, dim=-1, eps=so.LENGTH_EPS):
+    """naive:255-258 (einsum:238 uses eps 1e-9)."""
+    return torch.sqrt(torch.sum(torch.square(s), dim=dim) + eps)
 
 
 def pose_tiled(emb_win, W, bias):
@@ -146,6 +146,9 @@ class NaiveMirror(torch.nn.Module):
             x = feat_mask(x, inp_len, 2 ** (k + 1))
         B, T2, F2, C = x.shape
         emb = x.reshape(B, T2, F2 * C) @ self.P('proj.kernel') + self.P('proj.bias')
+        if sh.caps_type == 'einsum':   # sequence_router_einsum.py:130-131
+            pe = torch.as_tensor(so.pos_enc(T2, sh.ph), dtype=emb.dtype)
+            emb = emb * so.einsum_scale(sh.ph) + pe
         emb = emb.unsqueeze(-1)
         e1 = conv2d_same(emb, self.P('encaps1.kernel'), self.P('encaps1.bias'), 1)
         e2 = conv2d_same(emb, self.P('encaps2.kernel'), self.P('encaps2.bias'), 1)
@@ -163,18 +166,22 @@ class NaiveMirror(torch.nn.Module):
             Tn = emb.shape[1]
             ep = F.pad(emb, (0, 0, 0, 0, sh.lpad, sh.rpad))
             xw = torch.cat([ep[:, w:w + Tn] for w in range(sh.window)], dim=2)
-            u = pose_tiled(xw, self.P(f'W{l}'), self.P(f'b{l}'))
-            if sh.context:
-                v = sequential_routing(u, sh.iters, l == L - 1)
+            if sh.caps_type == 'lowmemory' and not sh.context:
+                J = self.P(f'W{l}').shape[1]
+                u = xw.unsqueeze(3).repeat(1, 1, 1, J, 1)              # lowmemory:162, no W / bias
             else:
-                v = dynamic_routing(u, sh.iters, l == L - 1)
+                u = pose_tiled(xw, self.P(f'W{l}'), self.P(f'b{l}'))
+            if sh.context:
+                v = sequential_routing(u, sh.route_iters, l == L - 1)
+            else:
+                v = dynamic_routing(u, sh.route_iters, l == L - 1)
             J, Dv = v.shape[2], v.shape[3]
             flat = layer_norm(v.reshape(B, Tn, J * Dv), self.P(f'ln_mid{l + 1}.gamma'),
                               self.P(f'ln_mid{l + 1}.beta'))
             if drop is not None and f'mid{l}' in drop:
                 flat = flat * drop[f'mid{l}']
             emb = flat.reshape(B, Tn, J, Dv)
-        return layer_norm(length(emb, -1), self.P('ln_output.gamma'), self.P('ln_output.beta'))
+        return layer_norm(length(emb, -1, sh.length_eps), self.P('ln_output.gamma'), self.P('ln_output.beta'))
 
 
 def ctc_per_utt(logits, labels, inp_len, tar_len, class_n, div=4):

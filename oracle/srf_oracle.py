@@ -176,12 +176,16 @@ class SrfShape:
     """Static shape of a SequenceRouter (``sequence_router_naive.py:42-103``)."""
 
     def __init__(self, feat_dim=123, nfilt=64, cnn_n=2, enc_num=3, iters=3, lpad=4, rpad=4,
-                 ph=8, pd=8, ch=8, cd=8, vd=8, class_n=63, context=False):
+                 ph=8, pd=8, ch=8, cd=8, vd=8, class_n=63, context=False, caps_type='naive'):
         self.feat_dim, self.nfilt, self.cnn_n = feat_dim, nfilt, cnn_n
+        self.caps_type = caps_type   # trainer_sr.py:188-199: lowmemory | einsum | naive
         self.enc_num, self.iters, self.lpad, self.rpad = enc_num, iters, lpad, rpad
         self.ph, self.pd, self.ch, self.cd, self.vd = ph, pd, ch, cd, vd
         self.class_n, self.context = class_n, context
         self.window = lpad + rpad + 1
+        # lowmemory routes once whatever --model-caps-iter says (lowmemory:107-109,190)
+        self.route_iters = 1 if caps_type == 'lowmemory' else iters
+        self.length_eps = 1e-9 if caps_type == 'einsum' else LENGTH_EPS   # einsum:238 / naive:256
         self.feat_out = math.ceil(feat_dim / (2 * cnn_n))   # naive:50 (quirk: only right for cnn_n=2)
 
     def layer_shapes(self):
@@ -267,10 +271,29 @@ def cnn_fe(P, shape, feats, inp_len, bn_training=True, drop=None):
     return x, stats
 
 
+def pos_enc(length, hidden):
+    """``get_pos_enc`` (model_helper.py:30-58), computed in float32 as the reference
+    does: [sin(t * inv_k) | cos(t * inv_k)], inv_k = exp(-k * log(1e4) / (hidden/2 - 1))."""
+    f32 = np.float32
+    nts = hidden // 2
+    inc = f32(math.log(1e4 / 1.0)) / (f32(nts) - f32(1))
+    inv = np.exp(np.arange(nts, dtype=f32) * -inc).astype(f32)
+    st = np.arange(length, dtype=f32)[:, None] * inv[None, :]
+    return np.concatenate([np.sin(st), np.cos(st)], axis=1).astype(f32)
+
+
+def einsum_scale(ph):
+    """tf.math.sqrt(tf.cast(ph, tf.float32)) (einsum:130), the float32 value."""
+    return float(np.sqrt(np.float32(ph)))
+
+
 def primary_caps(P, shape, conv_out, inp_len, drop=None):
-    """``sequence_router_naive.py:129-142``."""
+    """``sequence_router_naive.py:129-142``; einsum variant adds the sqrt(PH) scale
+    and positional encoding after proj_pe (``sequence_router_einsum.py:129-131``)."""
     B, T2, F2, C = conv_out.shape
     emb = conv_out.reshape(B, T2, F2 * C) @ P['proj.kernel'] + P['proj.bias']   # :131-132
+    if shape.caps_type == 'einsum':
+        emb = emb * einsum_scale(shape.ph) + pos_enc(T2, shape.ph)
     emb = emb[..., None]                                                        # [B,T',PH,1]
     e1 = conv2d_same(emb, P['encaps1.kernel'], P['encaps1.bias'], 1)
     e2 = conv2d_same(emb, P['encaps2.kernel'], P['encaps2.bias'], 1)
@@ -288,18 +311,23 @@ def primary_caps(P, shape, conv_out, inp_len, drop=None):
 
 
 def routing_layers(P, shape, emb, drop=None, return_all=False):
-    """Per-layer window -> pose -> DR/SDR -> LN (+dropout); ``naive:145-193``."""
+    """Per-layer window -> pose -> DR/SDR -> LN (+dropout); ``naive:145-193``.
+    lowmemory: one iteration, and DR without W / bias, u_ij = x_i (lowmemory:162-164)."""
     outs = []
     L = shape.enc_num
     for l in range(L):
         B, T, N, D = emb.shape
         x = window(emb, shape.lpad, shape.rpad)
-        u = pose(x, P[f'W{l}'], P[f'b{l}'])
         last = l == L - 1
-        if shape.context:
-            v = sequential_routing(u, shape.iters, last)
+        if shape.caps_type == 'lowmemory' and not shape.context:
+            J = P[f'W{l}'].shape[1]
+            u = np.broadcast_to(x[:, :, :, None, :], x.shape[:3] + (J, x.shape[3]))   # tf.tile :162
         else:
-            v = dynamic_routing(u, shape.iters, last)
+            u = pose(x, P[f'W{l}'], P[f'b{l}'])
+        if shape.context:
+            v = sequential_routing(u, shape.route_iters, last)
+        else:
+            v = dynamic_routing(u, shape.route_iters, last)
         J, Dv = v.shape[2], v.shape[3]
         outs.append(v)
         # every layer, the last included, is LN'd (ln_mid%d, :187-191) before length/ln_o
@@ -307,7 +335,7 @@ def routing_layers(P, shape, emb, drop=None, return_all=False):
         if drop is not None and f'mid{l}' in drop:
             flat = flat * drop[f'mid{l}']
         emb = flat.reshape(B, T, J, Dv)
-    logits = layer_norm(length(emb, -1), P['ln_output.gamma'], P['ln_output.beta'])  # :193
+    logits = layer_norm(length(emb, -1, shape.length_eps), P['ln_output.gamma'], P['ln_output.beta'])  # :193
     return (logits, outs) if return_all else logits
 
 

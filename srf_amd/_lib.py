@@ -44,6 +44,12 @@ _SIGNATURES = {
     'srf_primary_caps_bwd': (_c_int, [_vp, _vp] + [_c_int] * 5 + [_vp] * 5 + [_c_int, ctypes.c_float, ctypes.c_float,
                                                                            ctypes.c_ulonglong] + [_vp] * 12
                              + [_c_size, _vp]),
+    'srf_primary_caps_fwd_ex': (_c_int, [_vp, _vp] + [_c_int] * 5 + [_vp] * 8
+                                + [_c_int, ctypes.c_float, ctypes.c_float, ctypes.c_ulonglong, ctypes.c_float, _c_int,
+                                   _vp, _vp, _c_size, _vp]),
+    'srf_primary_caps_bwd_ex': (_c_int, [_vp, _vp] + [_c_int] * 5 + [_vp] * 5
+                                + [_c_int, ctypes.c_float, ctypes.c_float, ctypes.c_ulonglong, ctypes.c_float]
+                                + [_vp] * 12 + [_c_size, _vp]),
     'srf_capsnorm_bwd_workspace': (_c_size, [_c_int] * 3),
     'srf_capsnorm_fwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong, _c_int,
                                   _vp, _vp, _vp]),
@@ -52,6 +58,8 @@ _SIGNATURES = {
     'srf_caps_head_fwd': (_c_int, [_vp, _c_int, _c_int, _c_int] + [_vp] * 4 + [_c_int, ctypes.c_float,
                                                                               ctypes.c_ulonglong, _c_int]
                           + [_vp] * 4),
+    'srf_caps_head_fwd_ex': (_c_int, [_vp, _c_int, _c_int, _c_int] + [_vp] * 4
+                             + [_c_int, ctypes.c_float, ctypes.c_ulonglong, _c_int, ctypes.c_float] + [_vp] * 4),
     'srf_caps_head_bwd': (_c_int, [_vp, _c_int, _c_int, _c_int] + [_vp] * 3 + [_c_int, ctypes.c_float,
                                                                               ctypes.c_ulonglong, _c_int]
                           + [_vp] * 9 + [_c_size, _vp]),

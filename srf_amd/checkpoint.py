@@ -37,7 +37,10 @@ def tf_variable_map(model):
     conv_layers[1][k] for the two maxout halves of conv stage k
     (sequence_router.py:52-60, 76-77): ours conv{k}a / conv{k}b.
     W%d / b%d carry the reference's leading (1, 1) and trailing 1 axes
-    (naive:97-103)."""
+    (naive:97-103); the einsum variant stores W as (in, out, od, id) and the bias as
+    (1, 1, in, out, od) (einsum:93-97), lowmemory as (1, in, out, od, id) and
+    (1, in, out, od, 1) (lowmemory:94-98).  Same values in the same order."""
+    caps_type = getattr(model, 'caps_type', 'naive')
     m = {}
     for k in range(model.cnn_n):
         for j, ab in enumerate('ab'):
@@ -55,8 +58,14 @@ def tf_variable_map(model):
         m[f'ln_input_{t}'] = (f'model/ln_i/{t}/{VALUE}', None)
         m[f'ln_output_{t}'] = (f'model/ln_o/{t}/{VALUE}', None)
     for l, (in_n, out_n, out_d, in_d) in enumerate(model.layer_shapes):
-        m[f'W{l}'] = (f'model/wgt/{l}/{VALUE}', (1, 1, in_n, out_n, out_d, in_d))
-        m[f'b{l}'] = (f'model/bias/{l}/{VALUE}', (1, 1, in_n, out_n, out_d, 1))
+        if caps_type == 'einsum':
+            ws, bs = (in_n, out_n, out_d, in_d), (1, 1, in_n, out_n, out_d)
+        elif caps_type == 'lowmemory':
+            ws, bs = (1, in_n, out_n, out_d, in_d), (1, in_n, out_n, out_d, 1)
+        else:
+            ws, bs = (1, 1, in_n, out_n, out_d, in_d), (1, 1, in_n, out_n, out_d, 1)
+        m[f'W{l}'] = (f'model/wgt/{l}/{VALUE}', ws)
+        m[f'b{l}'] = (f'model/bias/{l}/{VALUE}', bs)
         for t in ('gamma', 'beta'):
             m[f'ln_mid{l + 1}_{t}'] = (f'model/ln_m/{l}/{t}/{VALUE}', None)
     return m

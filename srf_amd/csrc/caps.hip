@@ -45,12 +45,31 @@ __device__ __forceinline__ float drop_mult(bool on, unsigned long long seed, uns
   return srf_keep(seed, stream, idx, p) ? 1.f / (1.f - p) : 0.f;
 }
 
+// get_pos_enc (model_helper.py:30-58), evaluated in float32 like the reference:
+// columns [0, PH/2) are sin(t * inv_k), [PH/2, PH) cos(t * inv_k), with
+// inv_k = exp(-k * log(1e4) / (PH/2 - 1)).
+__device__ __forceinline__ float pos_enc(int t, int p, int PH) {
+  const int nts = PH >> 1;
+  const float inc = 9.210340371976184f / (float)(nts - 1);
+  const int k = p < nts ? p : p - nts;
+  const float st = (float)t * expf((float)k * -inc);
+  return p < nts ? sinf(st) : cosf(st);
+}
+
+// Epilogue of the projection: e = (x W + b) * scale (+ pos_enc) -- the einsum
+// variant's sqrt(PH) scaling and positional encoding (sequence_router_einsum.py:129-131);
+// scale = 1 and no encoding for naive / lowmemory.
+__device__ __forceinline__ float proj_epilogue(float acc, int f, int T, int p, int PH, float scale, int pe) {
+  const float y = acc * scale;
+  return pe ? y + pos_enc(f % T, p, PH) : y;
+}
+
 // ---------------------------------------------------------------- proj
 // One wave per frame, outputs in groups of 8; the K loop is unrolled 4x with
 // independent loads so the wave keeps several row segments in flight.
 __global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__ X, int F, int K, int PH,
                                                        const float* __restrict__ Wp, const float* __restrict__ bp,
-                                                       float* __restrict__ e) {
+                                                       float* __restrict__ e, int T, float scale, int pe) {
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int l = threadIdx.x & 63;
   if (f >= F) return;
@@ -70,7 +89,7 @@ __global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const float s = wave_sum(acc[q]);
-      if (l == 0 && q < np) e[(size_t)f * PH + p0 + q] = s + bp[p0 + q];
+      if (l == 0 && q < np) e[(size_t)f * PH + p0 + q] = proj_epilogue(s + bp[p0 + q], f, T, p0 + q, PH, scale, pe);
     }
   }
 }
@@ -81,7 +100,8 @@ __global__ __launch_bounds__(256) void proj_fwd_kernel(const float* __restrict__
 template <int PH, int FW>
 __global__ __launch_bounds__(256) void proj_fwd_vec_kernel(const float* __restrict__ X, int F, int K,
                                                            const float* __restrict__ Wp,
-                                                           const float* __restrict__ bp, float* __restrict__ e) {
+                                                           const float* __restrict__ bp, float* __restrict__ e,
+                                                           int T, float scale, int pe) {
   constexpr int PQ = PH / 4;
   const int l = threadIdx.x & 63;
   const int f0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * FW;
@@ -112,7 +132,7 @@ __global__ __launch_bounds__(256) void proj_fwd_vec_kernel(const float* __restri
 #pragma unroll
     for (int p = 0; p < PH; ++p) {
       const float sum = wave_sum(acc[u][p]);
-      if (l == 0 && f0 + u < F) e[(size_t)(f0 + u) * PH + p] = sum + bp[p];
+      if (l == 0 && f0 + u < F) e[(size_t)(f0 + u) * PH + p] = proj_epilogue(sum + bp[p], f0 + u, T, p, PH, scale, pe);
     }
 }
 
@@ -385,7 +405,7 @@ __global__ __launch_bounds__(256) void encaps_bwd_a_kernel(
 // Backward part B: g_e[t'][p'] = sum_{k,dt,dp,d} g_vk[t'-dt+1][p'-dp+1][d] K_k[dt][dp][d].
 __global__ void encaps_bwd_b_kernel(const float* __restrict__ g_v1, const float* __restrict__ g_v2, CapsDims cd,
                                     const float* __restrict__ K1, const float* __restrict__ K2,
-                                    float* __restrict__ g_e) {
+                                    float* __restrict__ g_e, float scale) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int F = cd.B * cd.T;
   if (idx >= F * cd.PH) return;
@@ -405,7 +425,7 @@ __global__ void encaps_bwd_b_kernel(const float* __restrict__ g_v1, const float*
              g_v2[fo + pp * cd.PD + d] * K2[(dt * 3 + dp) * cd.PD + d];
     }
   }
-  g_e[idx] = s;
+  g_e[idx] = s * scale;   // through the einsum variant's sqrt(PH) scaling (1 otherwise)
 }
 
 // ---------------------------------------------------------------- LN + dropout
@@ -418,7 +438,8 @@ __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restri
                                                            float* __restrict__ y, float* __restrict__ stat, int head,
                                                            int J, int D, const float* __restrict__ gamma_o,
                                                            const float* __restrict__ beta_o,
-                                                           float* __restrict__ logits, float* __restrict__ lens) {
+                                                           float* __restrict__ logits, float* __restrict__ lens,
+                                                           float len_eps) {
   seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* v = sm;           // n
@@ -457,7 +478,7 @@ __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restri
   for (int j = threadIdx.x; j < J; j += blockDim.x) {
     float s = 0.f;
     for (int d = 0; d < D; ++d) s += v[j * D + d] * v[j * D + d];
-    L[j] = sqrtf(s + kLengthEps);
+    L[j] = sqrtf(s + len_eps);
     lens[(size_t)f * J + j] = L[j];
   }
   __syncthreads();
@@ -645,8 +666,18 @@ int srf_primary_caps_fwd(const float* X, const int* inp_len, int B, int T, int K
                          const float* bp, const float* K1, const float* b1, const float* K2, const float* b2,
                          const float* gamma, const float* beta, int training, float p_caps, float p_in,
                          unsigned long long seed, float* z, void* saved, size_t saved_bytes, void* stream) {
+  return srf_primary_caps_fwd_ex(X, inp_len, B, T, K, PH, PD, Wp, bp, K1, b1, K2, b2, gamma, beta, training, p_caps,
+                                 p_in, seed, 1.f, 0, z, saved, saved_bytes, stream);
+}
+
+int srf_primary_caps_fwd_ex(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                            const float* bp, const float* K1, const float* b1, const float* K2, const float* b2,
+                            const float* gamma, const float* beta, int training, float p_caps, float p_in,
+                            unsigned long long seed, float proj_scale, int pos_enc, float* z, void* saved,
+                            size_t saved_bytes, void* stream) {
   int rc = check_caps(B, T, PH, PD);
   if (rc) return rc;
+  SRF_REQUIRE(!pos_enc || (PH >= 4 && PH % 2 == 0), "positional encoding needs an even PH >= 4, got %d", PH);
   SRF_REQUIRE(X && inp_len && Wp && bp && K1 && b1 && K2 && b2 && gamma && beta && z && saved, "null pointer");
   const int F = B * T;
   CapsSaved sv = caps_saved_layout(F, PH, PD, saved);
@@ -658,13 +689,17 @@ int srf_primary_caps_fwd(const float* X, const int* inp_len, int B, int T, int K
   constexpr int FW = 2;
   const dim3 gvec((F + 4 * FW - 1) / (4 * FW));
   if (K % 4 == 0 && PH == 4)
-    hipLaunchKernelGGL((proj_fwd_vec_kernel<4, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e);
+    hipLaunchKernelGGL((proj_fwd_vec_kernel<4, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e, T,
+                       proj_scale, pos_enc);
   else if (K % 4 == 0 && PH == 8)
-    hipLaunchKernelGGL((proj_fwd_vec_kernel<8, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e);
+    hipLaunchKernelGGL((proj_fwd_vec_kernel<8, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e, T,
+                       proj_scale, pos_enc);
   else if (K % 4 == 0 && PH == 16)
-    hipLaunchKernelGGL((proj_fwd_vec_kernel<16, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e);
+    hipLaunchKernelGGL((proj_fwd_vec_kernel<16, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e, T,
+                       proj_scale, pos_enc);
   else
-    hipLaunchKernelGGL(proj_fwd_kernel, dim3((F + 3) / 4), dim3(256), 0, st, X, F, K, PH, Wp, bp, sv.e);
+    hipLaunchKernelGGL(proj_fwd_kernel, dim3((F + 3) / 4), dim3(256), 0, st, X, F, K, PH, Wp, bp, sv.e, T, proj_scale,
+                       pos_enc);
   SRF_LAUNCH_CHECK("proj_fwd");
   CapsDims cd{B, T, PH, PD};
   const size_t sh = (size_t)(PH * PD + 5 * PH + 8) * sizeof(float);
@@ -679,6 +714,17 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
                          float p_caps, float p_in, unsigned long long seed, const void* saved, const float* g_z,
                          float* g_X, float* g_Wp, float* g_bp, float* g_K1, float* g_b1, float* g_K2, float* g_b2,
                          float* g_gamma, float* g_beta, void* workspace, size_t workspace_bytes, void* stream) {
+  return srf_primary_caps_bwd_ex(X, inp_len, B, T, K, PH, PD, Wp, K1, K2, gamma, beta, training, p_caps, p_in, seed,
+                                 1.f, saved, g_z, g_X, g_Wp, g_bp, g_K1, g_b1, g_K2, g_b2, g_gamma, g_beta, workspace,
+                                 workspace_bytes, stream);
+}
+
+int srf_primary_caps_bwd_ex(const float* X, const int* inp_len, int B, int T, int K, int PH, int PD, const float* Wp,
+                            const float* K1, const float* K2, const float* gamma, const float* beta, int training,
+                            float p_caps, float p_in, unsigned long long seed, float proj_scale, const void* saved,
+                            const float* g_z, float* g_X, float* g_Wp, float* g_bp, float* g_K1, float* g_b1,
+                            float* g_K2, float* g_b2, float* g_gamma, float* g_beta, void* workspace,
+                            size_t workspace_bytes, void* stream) {
   int rc = check_caps(B, T, PH, PD);
   if (rc) return rc;
   SRF_REQUIRE(X && inp_len && Wp && K1 && K2 && gamma && beta && saved && g_z && g_X && g_Wp && g_bp && g_K1 &&
@@ -703,7 +749,7 @@ int srf_primary_caps_bwd(const float* X, const int* inp_len, int B, int T, int K
                      g_gamma, g_beta, g_K1, g_b1, g_K2, g_b2);
   SRF_LAUNCH_CHECK("scatter_encaps_grads");
   hipLaunchKernelGGL(encaps_bwd_b_kernel, dim3((F * PH + 255) / 256), dim3(256), 0, st, w.gv1, w.gv2, cd, K1, K2,
-                     w.g_e);
+                     w.g_e, proj_scale);
   SRF_LAUNCH_CHECK("encaps_bwd_b");
   const dim3 gx4(((size_t)F * (K / 4) + 255) / 256);
   if (K % 4 == 0 && PH == 4)
@@ -738,7 +784,7 @@ int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const flo
   SRF_REQUIRE(x && gamma && beta && y && stat && F > 0 && n > 0 && n <= kMaxVec, "bad capsnorm arguments");
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, static_cast<hipStream_t>(stream),
                      x, n, gamma, beta, training, p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0,
-                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr);
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr, kLengthEps);
   SRF_LAUNCH_CHECK("capsnorm_fwd");
   return SRF_OK;
 }
@@ -768,6 +814,13 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
 int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
                       const float* gamma_out, const float* beta_out, int training, float p, unsigned long long seed,
                       int layer, float* logits, float* stat, float* lens, void* stream) {
+  return srf_caps_head_fwd_ex(v, F, J, D, gamma_mid, beta_mid, gamma_out, beta_out, training, p, seed, layer, kLengthEps,
+                              logits, stat, lens, stream);
+}
+
+int srf_caps_head_fwd_ex(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
+                         const float* gamma_out, const float* beta_out, int training, float p, unsigned long long seed,
+                         int layer, float length_eps, float* logits, float* stat, float* lens, void* stream) {
   const int n = J * D;
   SRF_REQUIRE(v && gamma_mid && beta_mid && gamma_out && beta_out && logits && stat && lens && F > 0 && n > 0 &&
                   n <= kMaxVec,
@@ -775,7 +828,7 @@ int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mi
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4,
                      static_cast<hipStream_t>(stream), v, n, gamma_mid, beta_mid, training, p, seed, srf::seed_source(),
                      (unsigned)(kStreamMid0 + layer), (float*)nullptr, stat, 1, J, D, gamma_out, beta_out, logits,
-                     lens);
+                     lens, length_eps);
   SRF_LAUNCH_CHECK("caps_head_fwd");
   return SRF_OK;
 }

@@ -233,7 +233,8 @@ class PrimaryCaps(torch.autograd.Function):
     """X [B,T,F2,64] -> z [B,T,PH,PD] (naive:129-142)."""
 
     @staticmethod
-    def forward(ctx, X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, *params):
+    def forward(ctx, X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, variant, *params):
+        proj_scale, pos_enc = variant
         B, T = X.shape[:2]
         K = X.shape[2] * X.shape[3]
         _check_dev('X', X, tuple(X.shape))
@@ -242,10 +243,11 @@ class PrimaryCaps(torch.autograd.Function):
         sb = L.srf_primary_caps_saved_bytes(B, T, PH, PD)
         saved = torch.empty(sb, device=X.device, dtype=torch.uint8)
         tr = int(bool(training))
-        rc = L.srf_primary_caps_fwd(_ptr(X), _ptr(inp_len_i32), B, T, K, PH, PD, *[_ptr(p) for p in params], tr,
-                                    float(p_caps), float(p_in), int(seed), _ptr(z), _ptr(saved), sb, _stream())
-        _lib.check(rc, 'srf_primary_caps_fwd')
-        ctx.meta = (B, T, K, PH, PD, tr, float(p_caps), float(p_in), int(seed))
+        rc = L.srf_primary_caps_fwd_ex(_ptr(X), _ptr(inp_len_i32), B, T, K, PH, PD, *[_ptr(p) for p in params], tr,
+                                       float(p_caps), float(p_in), int(seed), float(proj_scale), int(bool(pos_enc)),
+                                       _ptr(z), _ptr(saved), sb, _stream())
+        _lib.check(rc, 'srf_primary_caps_fwd_ex')
+        ctx.meta = (B, T, K, PH, PD, tr, float(p_caps), float(p_in), int(seed), float(proj_scale))
         ctx.params = params
         ctx.save_for_backward(X, inp_len_i32, saved, *params)
         return z
@@ -253,7 +255,7 @@ class PrimaryCaps(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_z):
         X, inp_len, saved, *params = ctx.saved_tensors
-        B, T, K, PH, PD, tr, p_caps, p_in, seed = ctx.meta
+        B, T, K, PH, PD, tr, p_caps, p_in, seed, proj_scale = ctx.meta
         P = dict(zip(CAPS_PARAMS, params))
         L = _lib.lib()
         g_X = torch.empty_like(X)
@@ -261,17 +263,19 @@ class PrimaryCaps(torch.autograd.Function):
         G = dict(zip(CAPS_PARAMS, [t for t, _ in targets]))
         wb = L.srf_primary_caps_bwd_workspace(B, T, K, PH, PD)
         ws = torch.empty(wb, device=X.device, dtype=torch.uint8)
-        rc = L.srf_primary_caps_bwd(_ptr(X), _ptr(inp_len), B, T, K, PH, PD, _ptr(P['proj_kernel']),
-                                    _ptr(P['encaps1_kernel']), _ptr(P['encaps2_kernel']), _ptr(P['ln_input_gamma']),
-                                    _ptr(P['ln_input_beta']), tr, p_caps, p_in, seed, _ptr(saved),
-                                    _ptr(g_z.contiguous()), _ptr(g_X), *[_ptr(G[k]) for k in CAPS_PARAMS], _ptr(ws),
-                                    wb, _stream())
-        _lib.check(rc, 'srf_primary_caps_bwd')
-        return (g_X, None, None, None, None, None, None, None, *_returned(targets))
+        rc = L.srf_primary_caps_bwd_ex(_ptr(X), _ptr(inp_len), B, T, K, PH, PD, _ptr(P['proj_kernel']),
+                                       _ptr(P['encaps1_kernel']), _ptr(P['encaps2_kernel']),
+                                       _ptr(P['ln_input_gamma']), _ptr(P['ln_input_beta']), tr, p_caps, p_in, seed,
+                                       proj_scale, _ptr(saved), _ptr(g_z.contiguous()), _ptr(g_X),
+                                       *[_ptr(G[k]) for k in CAPS_PARAMS], _ptr(ws), wb, _stream())
+        _lib.check(rc, 'srf_primary_caps_bwd_ex')
+        return (g_X, None, None, None, None, None, None, None, None, *_returned(targets))
 
 
-def primary_caps(X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, params):
-    return PrimaryCaps.apply(X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, *params)
+def primary_caps(X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, params, proj_scale=1.0, pos_enc=False):
+    """proj_scale / pos_enc: the einsum variant's sqrt(PH) scaling and positional
+    encoding after proj_pe (sequence_router_einsum.py:129-131); 1 / off otherwise."""
+    return PrimaryCaps.apply(X, inp_len_i32, PH, PD, training, p_caps, p_in, seed, (proj_scale, pos_enc), *params)
 
 
 class CapsNorm(torch.autograd.Function):
@@ -312,7 +316,7 @@ class CapsHead(torch.autograd.Function):
     """logits = LN_out(length_D(drop(LN_mid(v)))) (naive:187-193)."""
 
     @staticmethod
-    def forward(ctx, v, gamma_mid, beta_mid, gamma_out, beta_out, training, p, seed, layer):
+    def forward(ctx, v, gamma_mid, beta_mid, gamma_out, beta_out, training, p, seed, layer, length_eps=1e-7):
         B, T, J, D = v.shape
         F = B * T
         L = _lib.lib()
@@ -320,9 +324,9 @@ class CapsHead(torch.autograd.Function):
         stat = torch.empty((F, 4), device=v.device, dtype=torch.float32)
         lens = torch.empty((F, J), device=v.device, dtype=torch.float32)
         tr = int(bool(training))
-        _lib.check(L.srf_caps_head_fwd(_ptr(v), F, J, D, _ptr(gamma_mid), _ptr(beta_mid), _ptr(gamma_out),
-                                       _ptr(beta_out), tr, float(p), int(seed), int(layer), _ptr(logits), _ptr(stat),
-                                       _ptr(lens), _stream()), 'srf_caps_head_fwd')
+        _lib.check(L.srf_caps_head_fwd_ex(_ptr(v), F, J, D, _ptr(gamma_mid), _ptr(beta_mid), _ptr(gamma_out),
+                                          _ptr(beta_out), tr, float(p), int(seed), int(layer), float(length_eps),
+                                          _ptr(logits), _ptr(stat), _ptr(lens), _stream()), 'srf_caps_head_fwd_ex')
         ctx.meta = (F, J, D, tr, float(p), int(seed), int(layer))
         ctx.params = (gamma_mid, beta_mid, gamma_out, beta_out)
         ctx.save_for_backward(v, gamma_mid, beta_mid, gamma_out, beta_out, stat, lens)
@@ -342,7 +346,7 @@ class CapsHead(torch.autograd.Function):
                                        _ptr(stat), _ptr(lens), _ptr(g_logits.contiguous()), _ptr(g_v), _ptr(g_gm),
                                        _ptr(g_bm), _ptr(g_go), _ptr(g_bo), _ptr(ws), wb, _stream()),
                    'srf_caps_head_bwd')
-        return (g_v, *_returned(targets), None, None, None, None)
+        return (g_v, *_returned(targets), None, None, None, None, None)
 
 
 class CtcLoss(torch.autograd.Function):

@@ -22,6 +22,8 @@ from . import ops
 
 SQUASH_EPS = 1e-7   # naive:248
 LENGTH_EPS = 1e-7   # naive:256
+LENGTH_EPS_EINSUM = 1e-9   # sequence_router_einsum.py:238
+CAPS_TYPES = ('lowmemory', 'einsum', 'naive')   # trainer_sr.py:188-199, common_helper.py:228-231
 LN_EPS = 1e-3       # Keras LayerNormalization default
 BN_EPS = 1e-3       # Keras BatchNormalization default
 BN_MOMENTUM = 0.99
@@ -29,7 +31,19 @@ CNN_DROPOUT = 0.2   # hard-coded, sequence_router.py:62 and naive:82
 
 
 class SequenceRouter(torch.nn.Module):
-    """SRF acoustic model (naive variant semantics)."""
+    """SRF acoustic model.  ``config.model_caps_type`` picks the reference variant
+    (trainer_sr.py:188-199); all three run on the same HIP kernels:
+
+    * ``naive`` (sequence_router_naive.py): the semantics everything else is built to;
+    * ``einsum`` (sequence_router_einsum.py): proj_pe output scaled by sqrt(PH) plus the
+      sinusoidal positional encoding (:129-131), output length eps 1e-9 (:238);
+    * ``lowmemory`` (sequence_router_lowmemory.py): one routing iteration whatever
+      --model-caps-iter says (:107-109,190); its DR layers route the windowed input
+      capsules themselves, u_ij = x_i, without W or bias (:162-164), so W%d / b%d of a
+      DR layer get no gradient (TF's apply_gradients skips them).  The DR kernels run
+      with an identity W and zero bias for that; the SDR layers keep W and bias
+      (lowmemory:226-250).
+    """
 
     iter = -1  # class-level like the reference (naive:40,56): shared by every instance
 
@@ -60,6 +74,12 @@ class SequenceRouter(torch.nn.Module):
         self.inp_dropout = float(config.train_inp_dropout)
         self.inn_dropout = float(config.train_inn_dropout)
         self.init = config.model_initializer
+        self.caps_type = getattr(config, 'model_caps_type', 'naive')
+        if self.caps_type not in CAPS_TYPES:
+            raise ValueError('model-caps-type must be lowmemory, einsum or naive but %s' % self.caps_type)
+        self.route_iters = 1 if self.caps_type == 'lowmemory' else self.iter
+        self.proj_scale = math.sqrt(self.caps_inp_n) if self.caps_type == 'einsum' else 1.0
+        self.length_eps = LENGTH_EPS_EINSUM if self.caps_type == 'einsum' else LENGTH_EPS
         self.dropout_enabled = True     # test hook: parity runs use BN batch stats without dropout
         self.n_chunks_override = {}     # layer -> n_chunks (tuning hook)
         self._seed_base = int(np.random.default_rng(seed).integers(1, 2 ** 62))
@@ -122,6 +142,15 @@ class SequenceRouter(torch.nn.Module):
             self.register_buffer(f'bn{k}_moving_mean', torch.zeros(self.nfilt, device=dev))
             self.register_buffer(f'bn{k}_moving_var', torch.ones(self.nfilt, device=dev))
         self._geoms = {}
+        self._identity = {}
+        if self.caps_type == 'lowmemory' and not self.is_context:
+            for l, (in_n, out_n, out_d, in_d) in enumerate(shapes):
+                if out_d != in_d:
+                    # u_hat = tile(x) has in_d components; the reshape to out_n*out_d
+                    # (lowmemory:196-197) only works when they agree
+                    raise ValueError(f'lowmemory DR needs equal capsule dims, layer {l}: {in_d} -> {out_d}')
+                eye = torch.eye(in_d, device=dev, dtype=torch.float32).expand(in_n, out_n, in_d, in_d)
+                self._identity[l] = (eye.contiguous(), torch.zeros((in_n, out_n, out_d), device=dev))
         if logger is not None:
             logger.info('Layer x %d, Iter x %d, Init %s, Win %d (l:%d, r:%d), ' % (
                 self.enc_num, SequenceRouter.iter, 'SDR' if self.is_context else 'DR', self.window, self.lpad,
@@ -179,7 +208,7 @@ class SequenceRouter(torch.nn.Module):
         if g is None:
             in_n, out_n, out_d, in_d = self.layer_shapes[l]
             N = in_n // self.window
-            g = ops.RouteGeom(B, T, N, in_d, self.lpad, self.rpad, out_n, out_d, self.iter,
+            g = ops.RouteGeom(B, T, N, in_d, self.lpad, self.rpad, out_n, out_d, self.route_iters,
                               l == self.enc_num - 1, self.n_chunks_override.get(l, 0))
             self._geoms[key] = g
         return g
@@ -203,16 +232,18 @@ class SequenceRouter(torch.nn.Module):
         x = ops.cnnfe(feats.contiguous(), il32, [self.P(k) for k in ops.CNNFE_PARAMS], moving, training,
                       CNN_DROPOUT if drop else 0.0, seed)
         emb = ops.primary_caps(x, il32, self.caps_inp_n, self.caps_inp_d, training, CNN_DROPOUT if drop else 0.0,
-                               self.inp_dropout if drop else 0.0, seed, [self.P(k) for k in ops.CAPS_PARAMS])
+                               self.inp_dropout if drop else 0.0, seed, [self.P(k) for k in ops.CAPS_PARAMS],
+                               self.proj_scale, self.caps_type == 'einsum')
         B, T2 = emb.shape[:2]
         p_mid = self.inn_dropout if drop else 0.0
         for l in range(self.enc_num):
             route = ops.sequential_routing if self.is_context else ops.dynamic_routing
-            v = route(emb, self.P(f'W{l}'), self.P(f'b{l}'), self._geom(l, B, T2))
+            W, bias = self._identity.get(l, (self.P(f'W{l}'), self.P(f'b{l}')))
+            v = route(emb, W, bias, self._geom(l, B, T2))
             if l < self.enc_num - 1:
                 emb = ops.CapsNorm.apply(v, self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'), training,
                                          p_mid, seed, l)
             else:
                 return ops.CapsHead.apply(v, self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'),
                                           self.P('ln_output_gamma'), self.P('ln_output_beta'), training, p_mid,
-                                          seed, l)
+                                          seed, l, self.length_eps)

@@ -15,7 +15,7 @@ def config_from_shape(kw, **over):
         model_encoder_num=kw['enc_num'], model_caps_iter=kw['iters'], model_caps_window_lpad=kw['lpad'],
         model_caps_window_rpad=kw['rpad'], model_caps_context=kw['context'], model_caps_primary_num=kw['ph'],
         model_caps_primary_dim=kw['pd'], model_caps_convolution_num=kw['ch'], model_caps_convolution_dim=kw['cd'],
-        model_caps_class_dim=kw['vd'], model_caps_type='naive', model_initializer='fan_avg',
+        model_caps_class_dim=kw['vd'], model_caps_type=kw.get('caps_type', 'naive'), model_initializer='fan_avg',
         train_inp_dropout=0.1, train_inn_dropout=0.1, model_dimension=1, train_lr_param_k=0.5,
         train_warmup_n=1200, train_lr_max=1e3, train_adam_beta1=0.9, train_adam_beta2=0.98,
         train_adam_epsilon=1e-9, train_opti_type=None)

@@ -36,6 +36,23 @@ def test_tf_names_and_shapes():
                                   m.params['W0'].detach().numpy())
 
 
+def test_tf_shapes_per_variant():
+    """einsum:91-97 and lowmemory:94-98 store W / bias without the naive (1, 1)
+    prefix or with a single leading 1; values keep the same order."""
+    in_n = 4 * 3
+    for caps_type, ws, bs in (('einsum', (in_n, 4, 8, 8), (1, 1, in_n, 12, 8)),
+                              ('lowmemory', (1, in_n, 4, 8, 8), (1, in_n, 12, 8, 1))):
+        m = SequenceRouter(config_from_shape(dict(KW, caps_type=caps_type)), None, 12, device=torch.device('cpu'),
+                           seed=0)
+        st = ck.model_state(m)
+        assert st['model/wgt/0/.ATTRIBUTES/VARIABLE_VALUE'].shape == ws
+        assert st['model/bias/1/.ATTRIBUTES/VARIABLE_VALUE'].shape == bs
+        m2 = SequenceRouter(config_from_shape(dict(KW, caps_type=caps_type)), None, 12, device=torch.device('cpu'),
+                            seed=5)
+        ck.load_model_state(m2, st)
+        assert torch.equal(m2.params['b1'], m.params['b1'])
+
+
 def test_manager_save_restore_rotation(tmp_path):
     m, opt = _model(1), SrfAdam(CustomSchedule(0.5, 1, 1200))
     opt._m = torch.randn(m.n_flat)

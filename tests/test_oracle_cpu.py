@@ -11,7 +11,8 @@ from oracle import srf_oracle as so
 from tests.helpers import load_model_fixture
 
 
-@pytest.mark.parametrize('name', ['c1_mini', 'c2_mini', 'c3_mini_sdr'])
+@pytest.mark.parametrize('name', ['c1_mini', 'c2_mini', 'c3_mini_sdr', 'c2_mini_einsum', 'c2_mini_lowmemory',
+                                  'c3_mini_sdr_lowmemory'])
 def test_oracle_reproduces_fixture(name):
     kw, sh, P, z = load_model_fixture(name)
     logits = so.srf_forward(P, sh, z['feats'], z['inp_len'])
@@ -21,9 +22,11 @@ def test_oracle_reproduces_fixture(name):
     assert so.greedy_decode(logits, np.ceil(z['inp_len'] / 4).astype(int), sh.class_n - 1) == z['greedy']
 
 
-def test_mirror_matches_oracle_sdr_and_dr():
+@pytest.mark.parametrize('caps_type', ['naive', 'einsum', 'lowmemory'])
+def test_mirror_matches_oracle_sdr_and_dr(caps_type):
     for ctx in (False, True):
-        sh = so.SrfShape(enc_num=2, iters=2, lpad=1, rpad=2, ph=4, pd=8, ch=4, cd=8, vd=8, class_n=9, context=ctx)
+        sh = so.SrfShape(enc_num=2, iters=2, lpad=1, rpad=2, ph=4, pd=8, ch=4, cd=8, vd=8, class_n=9, context=ctx,
+                         caps_type=caps_type)
         P = so.init_params(sh, seed=5)
         rng = np.random.default_rng(6)
         feats = rng.standard_normal((2, 23, 123))
@@ -91,3 +94,34 @@ def test_mirror_gradient_finite_difference():
             minus = val
     fd = (plus - minus) / (2 * eps)
     assert abs(fd - g[idx]) < 1e-6 * max(1.0, abs(fd))
+
+
+def test_pos_enc_matches_closed_form():
+    """get_pos_enc (model_helper.py:30-58): row 0 is [0..0 | 1..1]; float32 values
+    agree with the float64 closed form to float32 rounding of t * inv_k."""
+    pe = so.pos_enc(200, 16)
+    assert pe.dtype == np.float32 and pe.shape == (200, 16)
+    assert np.all(pe[0, :8] == 0) and np.all(pe[0, 8:] == 1)
+    t = np.arange(200)[:, None]
+    inv = np.exp(-np.arange(8) * np.log(1e4) / 7)[None, :]
+    ref = np.concatenate([np.sin(t * inv), np.cos(t * inv)], 1)
+    assert np.abs(pe - ref).max() < 5e-5
+
+
+def test_lowmemory_routes_once_and_ignores_W_in_dr():
+    """lowmemory: --model-caps-iter is ignored (lowmemory:107-109,190) and its DR
+    layers do not read W / bias (lowmemory:162-164)."""
+    rng = np.random.default_rng(3)
+    feats = rng.standard_normal((2, 21, 123))
+    inp_len = np.array([21, 16])
+    outs = []
+    for iters in (1, 3):
+        sh = so.SrfShape(enc_num=2, iters=iters, lpad=1, rpad=1, ph=4, pd=8, ch=4, cd=8, vd=8, class_n=9,
+                         caps_type='lowmemory')
+        P = so.init_params(sh, seed=7)
+        outs.append(so.srf_forward(P, sh, feats, inp_len))
+    assert np.abs(outs[0] - outs[1]).max() == 0
+    P2 = dict(P, W0=P['W0'] * 3.0, b1=P['b1'] + 1.0)
+    assert np.abs(so.srf_forward(P2, sh, feats, inp_len) - outs[1]).max() == 0
+    sh_n = so.SrfShape(enc_num=2, iters=3, lpad=1, rpad=1, ph=4, pd=8, ch=4, cd=8, vd=8, class_n=9)
+    assert np.abs(so.srf_forward(P, sh_n, feats, inp_len) - outs[1]).max() > 1e-3
