@@ -240,6 +240,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # forward-only frames/s: model(feats, training=False) as in
+    # process_valid_step (BN moving statistics, no dropout), eager launches, outside
+    # the training-step timed region, same barrier + max-over-ranks timing
+    feats_b, il_b = batch[0], batch[2]
+    with torch.no_grad():
+        for _ in range(max(1, args.warmup)):
+            model(feats_b, input_lengths=il_b, training=False)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tf0 = time.perf_counter()
+        for _ in range(args.steps):
+            model(feats_b, input_lengths=il_b, training=False)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        fwd_elapsed = time.perf_counter() - tf0
+    if world > 1:
+        t = torch.tensor([fwd_elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        fwd_elapsed = float(t.item())
+
     kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
     kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
     in_n, J, D, Din = model.layer_shapes[last]
@@ -288,6 +310,9 @@ def main():
                                                       / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
                     if dr else None,
     }
+    line['forward_only'] = {'value': round(B * T * world * args.steps / fwd_elapsed, 1), 'unit': 'frames/s',
+                            'ms_per_step': round(fwd_elapsed / args.steps * 1e3, 4),
+                            'mode': 'model(feats, training=False), eager launches'}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)
     if rank == 0:

@@ -403,29 +403,39 @@ __global__ __launch_bounds__(256) void encaps_bwd_a_kernel(
 }
 
 // Backward part B: g_e[t'][p'] = sum_{k,dt,dp,d} g_vk[t'-dt+1][p'-dp+1][d] K_k[dt][dp][d].
-__global__ void encaps_bwd_b_kernel(const float* __restrict__ g_v1, const float* __restrict__ g_v2, CapsDims cd,
-                                    const float* __restrict__ K1, const float* __restrict__ K2,
-                                    float* __restrict__ g_e, float scale) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+// 16 lanes per output (f, p'): lane q takes d = q, q+16, ... (coalesced along d), and
+// the 16 partial sums meet in an xor butterfly.
+constexpr int kEbLanes = 16;
+__global__ __launch_bounds__(256) void encaps_bwd_b_kernel(const float* __restrict__ g_v1,
+                                                           const float* __restrict__ g_v2, CapsDims cd,
+                                                           const float* __restrict__ K1,
+                                                           const float* __restrict__ K2, float* __restrict__ g_e,
+                                                           float scale) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = gid / kEbLanes, q = gid % kEbLanes;
   const int F = cd.B * cd.T;
-  if (idx >= F * cd.PH) return;
-  const int p = idx % cd.PH, f = idx / cd.PH;
+  const bool live = idx < F * cd.PH;   // the whole 16-lane group agrees
+  const int p = live ? idx % cd.PH : 0, f = live ? idx / cd.PH : 0;
   const int t = f % cd.T;
   const int E = cd.PH * cd.PD;
   float s = 0.f;
-  for (int dt = 0; dt < 3; ++dt) {
-    const int tt = t - dt + 1;
-    if (tt < 0 || tt >= cd.T) continue;
-    const size_t fo = (size_t)(f - dt + 1) * E;
-    for (int dp = 0; dp < 3; ++dp) {
-      const int pp = p - dp + 1;
-      if (pp < 0 || pp >= cd.PH) continue;
-      for (int d = 0; d < cd.PD; ++d)
-        s += g_v1[fo + pp * cd.PD + d] * K1[(dt * 3 + dp) * cd.PD + d] +
-             g_v2[fo + pp * cd.PD + d] * K2[(dt * 3 + dp) * cd.PD + d];
+  if (live) {
+    for (int dt = 0; dt < 3; ++dt) {
+      const int tt = t - dt + 1;
+      if (tt < 0 || tt >= cd.T) continue;
+      const size_t fo = (size_t)(f - dt + 1) * E;
+      for (int dp = 0; dp < 3; ++dp) {
+        const int pp = p - dp + 1;
+        if (pp < 0 || pp >= cd.PH) continue;
+        for (int d = q; d < cd.PD; d += kEbLanes)
+          s += g_v1[fo + pp * cd.PD + d] * K1[(dt * 3 + dp) * cd.PD + d] +
+               g_v2[fo + pp * cd.PD + d] * K2[(dt * 3 + dp) * cd.PD + d];
+      }
     }
   }
-  g_e[idx] = s * scale;   // through the einsum variant's sqrt(PH) scaling (1 otherwise)
+#pragma unroll
+  for (int o = kEbLanes / 2; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (live && q == 0) g_e[idx] = s * scale;   // through the einsum variant's sqrt(PH) scaling (1 otherwise)
 }
 
 // ---------------------------------------------------------------- LN + dropout
@@ -748,8 +758,8 @@ int srf_primary_caps_bwd_ex(const float* X, const int* inp_len, int B, int T, in
   hipLaunchKernelGGL(scatter_encaps_grads, dim3((std::max(E, 20 * PD) + 255) / 256), dim3(256), 0, st, w.wsum, E, PD,
                      g_gamma, g_beta, g_K1, g_b1, g_K2, g_b2);
   SRF_LAUNCH_CHECK("scatter_encaps_grads");
-  hipLaunchKernelGGL(encaps_bwd_b_kernel, dim3((F * PH + 255) / 256), dim3(256), 0, st, w.gv1, w.gv2, cd, K1, K2,
-                     w.g_e, proj_scale);
+  hipLaunchKernelGGL(encaps_bwd_b_kernel, dim3(((size_t)F * PH * kEbLanes + 255) / 256), dim3(256), 0, st, w.gv1,
+                     w.gv2, cd, K1, K2, w.g_e, proj_scale);
   SRF_LAUNCH_CHECK("encaps_bwd_b");
   const dim3 gx4(((size_t)F * (K / 4) + 255) / 256);
   if (K % 4 == 0 && PH == 4)
