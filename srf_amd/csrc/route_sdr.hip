@@ -140,11 +140,16 @@ __device__ __forceinline__ void sdr_iteration(const float* __restrict__ ut, cons
 }
 
 // ------------------------------------------------------------------ forward
-// One workgroup per utterance; v_out[f] = v^{R-1} of frame f.
+// One workgroup per utterance; v_out[f] = v^{R-1} of frame f.  GS: the frame state
+// does not fit one CU's LDS (C5: in_n = 16*41 capsules), so it lives in a per-workgroup
+// slice of global memory (gstate, stride gstride floats) instead -- L2-resident, same code.
+template <bool GS>
 __global__ __launch_bounds__(kSeqThreads) void sdr_fwd_kernel(const float* __restrict__ u, int T, int in_n, int J,
                                                               int D, int iters, int mask_first,
-                                                              float* __restrict__ v_out) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+                                                              float* __restrict__ v_out, float* __restrict__ gstate,
+                                                              size_t gstride) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* smem = GS ? gstate + blockIdx.x * gstride : lds;
   const int JD = J * D, P = in_n * J;
   SeqSmem sm{smem, smem + JD, smem + JD + P, smem + JD + 2 * P, smem + 2 * JD + 2 * P};
   const int b = blockIdx.x;
@@ -179,12 +184,15 @@ struct BwdSmem {
   float *acc, *carry, *gv;          // [JD]
 };
 
+template <bool GS>
 __global__ __launch_bounds__(kSeqThreads) void sdr_bwd_kernel(const float* __restrict__ u,
                                                               const float* __restrict__ v_saved,
                                                               const float* __restrict__ g_v, int T, int in_n, int J,
                                                               int D, int iters, int mask_first,
-                                                              float* __restrict__ gu) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+                                                              float* __restrict__ gu, float* __restrict__ gstate,
+                                                              size_t gstride) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* smem = GS ? gstate + blockIdx.x * gstride : lds;
   const int JD = J * D, P = in_n * J, R = iters;
   const int tid = threadIdx.x;
   BwdSmem bs;
@@ -406,12 +414,19 @@ int check_sgeom(const SGeom& g) {
   return SRF_OK;
 }
 
-int sdr_smem_check(size_t bytes) {
-  if (bytes > 160 * 1024) {
-    srf::set_error("SDR frame state (%zu B) exceeds the 160 KiB LDS of one CU", bytes);
-    return SRF_EUNSUPPORTED;
-  }
-  return SRF_OK;
+// Frame state beyond one CU's 160 KiB LDS goes to global memory (workspace); so does
+// every state when SRF_SDR_GSTATE=1 (test hook for the global-state kernels).
+bool sdr_gstate(size_t bytes) {
+  if (bytes > 160 * 1024) return true;
+  const char* e = getenv("SRF_SDR_GSTATE");
+  return e && e[0] == '1';
+}
+
+// per-workgroup slice of the global frame state, in floats (256-B aligned slices)
+size_t gstate_stride(size_t state_bytes) { return srf::align_up(state_bytes, 256) / sizeof(float); }
+
+size_t gstate_bytes(const SGeom& g, size_t state_bytes) {
+  return sdr_gstate(state_bytes) ? (size_t)g.B * gstate_stride(state_bytes) * sizeof(float) : 0;
 }
 
 template <int D>
@@ -432,7 +447,7 @@ int pose_dispatch(const SGeom& g, const float* emb, const float* W, const float*
 }
 
 struct SdrBwdWs {
-  float *u, *gu, *WT, *scratch;
+  float *u, *gu, *WT, *scratch, *gstate;
   size_t bytes;
 };
 
@@ -445,13 +460,15 @@ SdrBwdWs sdr_bwd_layout(const SGeom& g, void* base) {
     return o;
   };
   const size_t ou = take(FU), ogu = take(FU), owt = take((size_t)g.in_n() * g.JD() * g.din),
-               osc = take(srf::colsum_scratch_floats(g.F(), g.in_n() * g.JD()));
+               osc = take(srf::colsum_scratch_floats(g.F(), g.in_n() * g.JD())),
+               ogs = take(gstate_bytes(g, sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters)) / sizeof(float));
   char* b = static_cast<char*>(base);
   SdrBwdWs w;
   w.u = (float*)(b + ou);
   w.gu = (float*)(b + ogu);
   w.WT = (float*)(b + owt);
   w.scratch = (float*)(b + osc);
+  w.gstate = (float*)(b + ogs);
   w.bytes = off;
   return w;
 }
@@ -472,8 +489,9 @@ extern "C" {
 size_t srf_route_sdr_saved_floats(int B, int T, int J, int dout) { return (size_t)B * T * J * dout; }
 
 size_t srf_route_sdr_fwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout) {
-  (void)din;
-  return srf::align_up((size_t)B * T * N * (lpad + rpad + 1) * J * dout * sizeof(float), 256);
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  return srf::align_up((size_t)B * T * N * (lpad + rpad + 1) * J * dout * sizeof(float), 256) +
+         gstate_bytes(g, sdr_fwd_smem(g.in_n(), J, dout));
 }
 
 size_t srf_route_sdr_bwd_workspace(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters) {
@@ -494,15 +512,19 @@ int srf_route_sdr_fwd(const float* emb, const float* W, const float* bias, int B
   }
   const bool seq = srf::sdr_seq_supported(g.in_n(), J, dout, iters);
   const size_t sm = sdr_fwd_smem(g.in_n(), J, dout);
-  if (!seq && (rc = sdr_smem_check(sm))) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* u = static_cast<float*>(workspace);
+  float* gstate = u + srf::align_up((size_t)g.F() * g.in_n() * g.JD() * sizeof(float), 256) / sizeof(float);
   if ((rc = pose_dispatch(g, emb, W, bias, u, st))) return rc;
   if (seq) {
     if ((rc = srf::sdr_seq_fwd(u, B, T, g.in_n(), J, dout, iters, g.mask_first, v_out, st))) return rc;
   } else {
-    hipLaunchKernelGGL(sdr_fwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, u, T, g.in_n(), J, dout, iters,
-                       g.mask_first, v_out);
+    if (sdr_gstate(sm))
+      hipLaunchKernelGGL(sdr_fwd_kernel<true>, dim3(B), dim3(kSeqThreads), 0, st, u, T, g.in_n(), J, dout, iters,
+                         g.mask_first, v_out, gstate, gstate_stride(sm));
+    else
+      hipLaunchKernelGGL(sdr_fwd_kernel<false>, dim3(B), dim3(kSeqThreads), sm, st, u, T, g.in_n(), J, dout, iters,
+                         g.mask_first, v_out, (float*)nullptr, (size_t)0);
     SRF_LAUNCH_CHECK("sdr_fwd");
   }
   SRF_HIP_TRY(hipMemcpyAsync(saved, v_out, (size_t)g.F() * g.JD() * sizeof(float), hipMemcpyDeviceToDevice, st));
@@ -524,14 +546,17 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
   }
   const bool seq = srf::sdr_seq_supported(g.in_n(), J, dout, iters);
   const size_t sm = sdr_bwd_smem(g.in_n(), J, dout, iters);
-  if (!seq && (rc = sdr_smem_check(sm))) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if ((rc = pose_dispatch(g, emb, W, bias, w.u, st))) return rc;
   if (seq) {
     if ((rc = srf::sdr_seq_bwd(w.u, saved, g_v, B, T, g.in_n(), J, dout, iters, g.mask_first, w.gu, st))) return rc;
   } else {
-    hipLaunchKernelGGL(sdr_bwd_kernel, dim3(B), dim3(kSeqThreads), sm, st, w.u, saved, g_v, T, g.in_n(), J, dout,
-                       iters, g.mask_first, w.gu);
+    if (sdr_gstate(sm))
+      hipLaunchKernelGGL(sdr_bwd_kernel<true>, dim3(B), dim3(kSeqThreads), 0, st, w.u, saved, g_v, T, g.in_n(), J,
+                         dout, iters, g.mask_first, w.gu, w.gstate, gstate_stride(sm));
+    else
+      hipLaunchKernelGGL(sdr_bwd_kernel<false>, dim3(B), dim3(kSeqThreads), sm, st, w.u, saved, g_v, T, g.in_n(), J,
+                         dout, iters, g.mask_first, w.gu, (float*)nullptr, (size_t)0);
     SRF_LAUNCH_CHECK("sdr_bwd");
   }
   {

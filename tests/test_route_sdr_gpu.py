@@ -102,22 +102,21 @@ def _check_backward(case, cuda):
         assert err <= 1e-4 * max(1.0, np.abs(ref).max()), (name, err, np.abs(ref).max())
 
 
-def test_route_sdr_rejects_oversized_frame_state(cuda):
-    """A frame whose routing state exceeds one CU's LDS is refused, not mis-run."""
-    from srf_amd import _lib
-    L = _lib.lib()
-    # C5-like last layer: in_n = 16*41, J = 32, D = 64, 5 iterations
-    B, T, N, D, lp, rp, J, it = 1, 2, 16, 64, 20, 20, 32, 5
-    dev = cuda
-    in_n = N * (lp + rp + 1)
-    emb = torch.zeros(B, T, N, D, device=dev)
-    W = torch.zeros(in_n, J, D, D, device=dev)
-    bias = torch.zeros(in_n, J, D, device=dev)
-    v = torch.empty(B, T, J, D, device=dev)
-    saved = torch.empty(B * T * J * D, device=dev)
-    wb = L.srf_route_sdr_fwd_workspace(B, T, N, D, lp, rp, J, D)
-    ws = torch.empty(wb, dtype=torch.uint8, device=dev)
-    rc = L.srf_route_sdr_fwd(emb.data_ptr(), W.data_ptr(), bias.data_ptr(), B, T, N, D, lp, rp, J, D, it, 1,
-                             v.data_ptr(), saved.data_ptr(), ws.data_ptr(), wb,
-                             torch.cuda.current_stream().cuda_stream)
-    assert rc == -3 and b'LDS' in L.srf_last_error()
+@pytest.mark.parametrize('case', LEGACY[:2])
+def test_route_sdr_global_state_kernels(cuda, case, monkeypatch):
+    """SRF_SDR_GSTATE=1 moves the legacy kernels' frame state from LDS to the
+    global-memory workspace (the path of shapes whose state exceeds one CU's LDS)."""
+    monkeypatch.setenv('SRF_SDR_SEQ', '0')
+    monkeypatch.setenv('SRF_SDR_GSTATE', '1')
+    _check_forward(case, cuda)
+    _check_backward(case, cuda)
+
+
+def test_route_sdr_c5_last_layer_shape(cuda):
+    """BASELINE C5's last layer (in_n = 16*41 = 656, J = 32, D = 64, 5 iterations,
+    lpad = rpad = 20): the frame state (198 KB forward, 2.3 MB backward) exceeds
+    one CU's LDS, so it runs on the global-state kernels.  Two frames, forward and
+    backward against the oracle."""
+    case = (1, 2, 16, 64, 20, 20, 32, 5, True)
+    _check_forward(case, cuda)
+    _check_backward(case, cuda)
