@@ -35,6 +35,9 @@ WORKLOADS = {
     'timit_c2': (dict(enc=3, iters=3, lpad=4, rpad=4, ph=8, pd=16, ch=8, cd=16, vd=16, context=False), 63, 17, 320),
     'wsj_c4': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=False), 32, 28, 800),
     'wsj_c3': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=True), 32, 28, 800),
+    # BASELINE C5 (HBM-bound stress): PH=CH=16 assumed as in C3; fp32 here --
+    # the fp8 pose MFMA the config names is not built
+    'wsj_c5': (dict(enc=8, iters=5, lpad=20, rpad=20, ph=16, pd=64, ch=16, cd=64, vd=64, context=True), 32, 28, 800),
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak
