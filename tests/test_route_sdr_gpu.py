@@ -30,7 +30,7 @@ CASES = [
     (1, 10, 8, 16, 4, 4, 63, 3, True),    # TIMIT-sized last layer: J = 63 (padded to 64), in_n = 72
     (2, 6, 4, 8, 0, 0, 3, 2, True),       # J = 3 (padded to 4), D = 8, no window
 ]
-# shapes run again through the first (256-thread LDS) recurrence kernels
+# shapes run again through the first (LDS-state, one workgroup per utterance) recurrence kernels
 LEGACY = [CASES[0], CASES[2], CASES[3], CASES[5]]
 
 
@@ -70,7 +70,7 @@ def test_route_sdr_forward(cuda, case):
 
 @pytest.mark.parametrize('case', LEGACY)
 def test_route_sdr_legacy_kernels(cuda, case, monkeypatch):
-    """SRF_SDR_SEQ=0 selects the 256-thread LDS recurrence kernels (the path for
+    """SRF_SDR_SEQ=0 selects the LDS-state recurrence kernels (the path for
     shapes beyond the register-resident kernels' budget)."""
     monkeypatch.setenv('SRF_SDR_SEQ', '0')
     _check_forward(case, cuda)
