@@ -61,6 +61,19 @@ int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
                      const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
                      size_t workspace_bytes, void* stream);
+/* The same backward in two stream-ordered parts.  _data writes g_emb and leaves the
+ * gu blocks in the workspace; _weights (same workspace, same geometry) then writes
+ * g_W and g_bias.  _weights depends on nothing else, so a caller may launch it on a
+ * second stream that waits for _data, and join that stream before reading g_W /
+ * g_bias or reusing the workspace: the weight contraction then overlaps the
+ * backward of the layers below.  srf_route_dr_bwd = _data + _weights on one stream. */
+int srf_route_dr_bwd_data(const float* emb, const float* W, const float* bias, int B, int T, int N, int din,
+                          int lpad, int rpad, int J, int dout, int iters, int mask_first, int n_chunks,
+                          const float* saved, const float* g_v, float* g_emb, void* workspace,
+                          size_t workspace_bytes, void* stream);
+int srf_route_dr_bwd_weights(const float* emb, int B, int T, int N, int din, int lpad, int rpad, int J, int dout,
+                             int iters, int mask_first, int n_chunks, float* g_W, float* g_bias, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* ---- Sequential dynamic routing layer: window + pose transform + SDR -------
  * Replaces tfsr/model/sequence_router_naive.py:162-170 (tf.while_loop over the

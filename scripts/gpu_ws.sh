@@ -1,0 +1,14 @@
+# Weight-gradient side stream: GPU tests, then C2 bench with and without it.
+set -e
+cd $GRAFT_REPO_ROOT
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-ws}
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/ -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+tail -1 $OUT/smoke.log
+timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench_ws1.json 2> $OUT/bench_ws1.err || { tail -20 $OUT/bench_ws1.err; exit 1; }
+SRF_WEIGHT_STREAM=0 timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench_ws0.json 2> $OUT/bench_ws0.err
+timeout -k 10 300 python bench.py --no-cpu-baseline --workload wsj_c4 --steps 10 --warmup 3 > $OUT/bench_c4_ws1.json 2> $OUT/bench_c4_ws1.err
+SRF_WEIGHT_STREAM=0 timeout -k 10 300 python bench.py --no-cpu-baseline --workload wsj_c4 --steps 10 --warmup 3 > $OUT/bench_c4_ws0.json 2> $OUT/bench_c4_ws0.err
+for f in bench_ws1 bench_ws0 bench_c4_ws1 bench_c4_ws0; do python -c "import json; d=json.load(open('$OUT/$f.json')); print('$f', d['ms_per_step'], d['value'])"; done

@@ -1031,9 +1031,31 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   return w;
 }
 
+// gW = gu x^T and gbias from the gu blocks the data pass left in the workspace; needs
+// nothing else of the backward, so a caller may run it on a second stream (after the
+// data pass, joined before g_W / g_bias or the workspace are used again).
+template <int D>
+int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st) {
+  const int Fp = padded_frames(g);
+  {
+    const size_t total = (size_t)g.in_n() * g.din * Fp;
+    hipLaunchKernelGGL(window_xt_kernel, dim3((total + 255) / 256), dim3(256), 0, st, emb, g.F(), Fp, g.T, g.N,
+                       g.din, g.lpad, g.in_n(), w.xT);
+    SRF_LAUNCH_CHECK("window_xt");
+  }
+  {
+    const int tasks = g.in_n() * g.NT();
+    hipLaunchKernelGGL((route_gw_kernel<D>), dim3((tasks + 3) / 4), dim3(256), 0, st, w.gu_t, w.xT, Fp, g.in_n(),
+                       g.JD(), g_W, g_bias);
+    SRF_LAUNCH_CHECK("route_gw");
+  }
+  return SRF_OK;
+}
+
 template <int D>
 int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias, const float* saved,
-             const float* g_v, float* g_emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st) {
+             const float* g_v, float* g_emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st,
+             bool with_weights) {
   const PassCfg pc = pass_cfg(g);
   const size_t FJD = (size_t)g.F() * g.JD();
   const int R = g.iters;
@@ -1065,19 +1087,8 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   }
   launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");
-  {
-    const size_t total = (size_t)g.in_n() * g.din * Fp;
-    hipLaunchKernelGGL(window_xt_kernel, dim3((total + 255) / 256), dim3(256), 0, st, emb, g.F(), Fp, g.T, g.N,
-                       g.din, g.lpad, g.in_n(), w.xT);
-    SRF_LAUNCH_CHECK("window_xt");
-  }
-  {
-    const int tasks = g.in_n() * g.NT();
-    hipLaunchKernelGGL((route_gw_kernel<D>), dim3((tasks + 3) / 4), dim3(256), 0, st, w.gu_t, w.xT, Fp, g.in_n(),
-                       g.JD(), g_W, g_bias);
-    SRF_LAUNCH_CHECK("route_gw");
-  }
-  return SRF_OK;
+  (void)Fp;
+  return with_weights ? bwd_weights_impl<D>(g, emb, g_W, g_bias, w, st) : SRF_OK;
 }
 
 }  // namespace
@@ -1141,10 +1152,11 @@ int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B,
   }
 }
 
-int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
-                     int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
-                     const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
-                     size_t workspace_bytes, void* stream) {
+namespace {
+int route_dr_bwd_entry(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                       int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
+                       const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
+                       size_t workspace_bytes, void* stream, bool with_weights) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, iters, mask_first ? 1 : 0};
   int rc = check_geom(g);
   if (rc) return rc;
@@ -1157,10 +1169,51 @@ int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B,
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   switch (din) {
-    case 8: return bwd_impl<8>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st);
-    case 16: return bwd_impl<16>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st);
-    case 32: return bwd_impl<32>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st);
-    default: return bwd_impl<64>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st);
+    case 8: return bwd_impl<8>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+    case 16: return bwd_impl<16>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+    case 32: return bwd_impl<32>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+    default: return bwd_impl<64>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+  }
+}
+}  // namespace
+
+int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
+                     const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
+                     size_t workspace_bytes, void* stream) {
+  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved, g_v,
+                            g_emb, g_W, g_bias, workspace, workspace_bytes, stream, true);
+}
+
+int srf_route_dr_bwd_data(const float* emb, const float* W, const float* bias, int B, int T, int N, int din,
+                          int lpad, int rpad, int J, int dout, int iters, int mask_first, int n_chunks,
+                          const float* saved, const float* g_v, float* g_emb, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  // g_W / g_bias are not touched by the data pass; the checks want non-null pointers
+  float* unused = reinterpret_cast<float*>(workspace);
+  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved, g_v,
+                            g_emb, unused, unused, workspace, workspace_bytes, stream, false);
+}
+
+int srf_route_dr_bwd_weights(const float* emb, int B, int T, int N, int din, int lpad, int rpad, int J, int dout,
+                             int iters, int mask_first, int n_chunks, float* g_W, float* g_bias, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  Geom g{B, T, N, din, lpad, rpad, J, dout, iters, mask_first ? 1 : 0};
+  int rc = check_geom(g);
+  if (rc) return rc;
+  SRF_REQUIRE(emb && g_W && g_bias && workspace, "null pointer argument");
+  SRF_REQUIRE(n_chunks >= 1 && n_chunks <= g.in_n(), "n_chunks %d out of [1, %d]", n_chunks, g.in_n());
+  BwdWs w = bwd_layout(g, n_chunks, workspace);
+  if (workspace_bytes < w.bytes) {
+    srf::set_error("backward workspace too small: %zu < %zu", workspace_bytes, w.bytes);
+    return SRF_EWORKSPACE;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (din) {
+    case 8: return bwd_weights_impl<8>(g, emb, g_W, g_bias, w, st);
+    case 16: return bwd_weights_impl<16>(g, emb, g_W, g_bias, w, st);
+    case 32: return bwd_weights_impl<32>(g, emb, g_W, g_bias, w, st);
+    default: return bwd_weights_impl<64>(g, emb, g_W, g_bias, w, st);
   }
 }
 

@@ -42,6 +42,27 @@ def _returned(target_flags):
     return [None if inplace else t for t, inplace in target_flags]
 
 
+# Side stream for the DR weight-gradient pass (srf_route_dr_bwd_weights): forked from
+# the autograd stream after a layer's data pass, joined by join_weight_streams() --
+# PrimaryCaps.backward calls it, which runs after every routing layer's backward.
+_side_streams = {}
+_pending_joins = []
+
+
+def _weight_stream(dev):
+    s = _side_streams.get(dev)
+    if s is None:
+        s = _side_streams[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def join_weight_streams():
+    """Make the current stream wait for every forked weight-gradient pass."""
+    cur = torch.cuda.current_stream()
+    while _pending_joins:
+        cur.wait_stream(_pending_joins.pop())
+
+
 class RouteGeom:
     """Static geometry of one DR layer (sequence_router_naive.py:146-147)."""
 
@@ -51,6 +72,7 @@ class RouteGeom:
         self.iters, self.mask_first = iters, int(bool(mask_first))
         self.in_n = N * (lpad + rpad + 1)
         self.timing = None   # optional (starts, stops) hipEvent_t arrays for the profiling hook
+        self.side_stream = False   # run the weight-gradient pass on a forked stream (SequenceRouter sets it)
         L = _lib.lib()
         if n_chunks <= 0:
             n_chunks = L.srf_route_dr_auto_chunks(B, T, N, din, lpad, rpad, J, dout)
@@ -107,9 +129,23 @@ class DynamicRouting(torch.autograd.Function):
         g_W, g_b = tW[0], tb[0]
         ws_bytes = L.srf_route_dr_bwd_workspace(*g.ws_args())
         ws = torch.empty(ws_bytes, device=emb.device, dtype=torch.uint8)
-        rc = L.srf_route_dr_bwd(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), _ptr(g_v), _ptr(g_emb),
-                                _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
-        _lib.check(rc, 'srf_route_dr_bwd')
+        if not g.side_stream:
+            rc = L.srf_route_dr_bwd(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), _ptr(g_v), _ptr(g_emb),
+                                    _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
+            _lib.check(rc, 'srf_route_dr_bwd')
+            return (g_emb, *_returned([tW, tb]), None)
+        rc = L.srf_route_dr_bwd_data(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), _ptr(g_v),
+                                     _ptr(g_emb), _ptr(ws), ws_bytes, _stream())
+        _lib.check(rc, 'srf_route_dr_bwd_data')
+        side = _weight_stream(emb.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            rc = L.srf_route_dr_bwd_weights(_ptr(emb), *g.args(), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes,
+                                            ctypes_void(side.cuda_stream))
+        _lib.check(rc, 'srf_route_dr_bwd_weights')
+        for t in (ws, emb, g_W, g_b):
+            t.record_stream(side)
+        _pending_joins.append(side)
         return (g_emb, *_returned([tW, tb]), None)
 
 
@@ -269,6 +305,7 @@ class PrimaryCaps(torch.autograd.Function):
                                        proj_scale, _ptr(saved), _ptr(g_z.contiguous()), _ptr(g_X),
                                        *[_ptr(G[k]) for k in CAPS_PARAMS], _ptr(ws), wb, _stream())
         _lib.check(rc, 'srf_primary_caps_bwd_ex')
+        join_weight_streams()
         return (g_X, None, None, None, None, None, None, None, None, *_returned(targets))
 
 
