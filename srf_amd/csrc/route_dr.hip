@@ -640,22 +640,33 @@ __global__ void transpose_w_kernel(const float* __restrict__ W, int in_n, int JD
 }
 
 // Windowed input, transposed and frame-padded: xT[i][e][f] (f < Fp), the B
-// operand of the gW contraction.
-__global__ void window_xt_kernel(const float* __restrict__ emb, int F, int Fp, int T, int N, int din, int lpad,
-                                 int in_n, float* __restrict__ xT) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)in_n * din * Fp) return;
-  const int f = idx % Fp;
-  const int e = (idx / Fp) % din;
-  const int i = idx / ((size_t)Fp * din);
-  float v = 0.f;
-  if (f < F) {
-    const int w = i / N, n = i - w * N;
-    const int b = f / T, t = f - b * T;
-    const int ts = t + w - lpad;
-    if (ts >= 0 && ts < T) v = emb[((size_t)(b * T + ts) * N + n) * din + e];
+// operand of the gW contraction.  One workgroup per (capsule i, 64-frame tile):
+// the tile's 64 x din window rows are read along e (coalesced), transposed through
+// LDS, and written as din runs of 64 consecutive frames.
+constexpr int kXtFrames = 64;
+__global__ __launch_bounds__(256) void window_xt_kernel(const float* __restrict__ emb, int F, int Fp, int T, int N,
+                                                        int din, int lpad, int in_n, float* __restrict__ xT) {
+  __shared__ float tile[kXtFrames][64 + 1];
+  const int i = blockIdx.x / ((Fp + kXtFrames - 1) / kXtFrames);
+  const int f0 = (blockIdx.x - i * ((Fp + kXtFrames - 1) / kXtFrames)) * kXtFrames;
+  const int w = i / N, n = i - w * N;
+  for (int k = threadIdx.x; k < kXtFrames * din; k += blockDim.x) {
+    const int fl = k / din, e = k - fl * din;
+    const int f = f0 + fl;
+    float v = 0.f;
+    if (f < F) {
+      const int b = f / T, t = f - b * T;
+      const int ts = t + w - lpad;
+      if (ts >= 0 && ts < T) v = emb[((size_t)(b * T + ts) * N + n) * din + e];
+    }
+    tile[fl][e] = v;
   }
-  xT[idx] = v;
+  __syncthreads();
+  for (int k = threadIdx.x; k < kXtFrames * din; k += blockDim.x) {
+    const int e = k / kXtFrames, fl = k - e * kXtFrames;
+    const int f = f0 + fl;
+    if (f < Fp) xT[((size_t)i * din + e) * Fp + f] = tile[fl][e];
+  }
 }
 
 // ---------------------------------------------------------------- gW, gbias
@@ -1038,9 +1049,10 @@ template <int D>
 int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st) {
   const int Fp = padded_frames(g);
   {
-    const size_t total = (size_t)g.in_n() * g.din * Fp;
-    hipLaunchKernelGGL(window_xt_kernel, dim3((total + 255) / 256), dim3(256), 0, st, emb, g.F(), Fp, g.T, g.N,
-                       g.din, g.lpad, g.in_n(), w.xT);
+    SRF_REQUIRE(g.din <= 64, "window_xt tile holds din <= 64, got %d", g.din);
+    const int tiles = (Fp + kXtFrames - 1) / kXtFrames;
+    hipLaunchKernelGGL(window_xt_kernel, dim3(g.in_n() * tiles), dim3(256), 0, st, emb, g.F(), Fp, g.T, g.N, g.din,
+                       g.lpad, g.in_n(), w.xT);
     SRF_LAUNCH_CHECK("window_xt");
   }
   {
