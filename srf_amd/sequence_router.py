@@ -245,6 +245,11 @@ class SequenceRouter(torch.nn.Module):
         for l in range(self.enc_num):
             route = ops.sequential_routing if self.is_context else ops.dynamic_routing
             W, bias = self._identity.get(l, (self.P(f'W{l}'), self.P(f'b{l}')))
+            if l in self._identity and torch.is_grad_enabled():
+                # lowmemory DR reads no W / bias: their gradients are zero, written here
+                # so that "backward writes every gradient" holds for this variant too
+                self.P(f'W{l}').grad.zero_()
+                self.P(f'b{l}').grad.zero_()
             v = route(emb, W, bias, self._geom(l, B, T2))
             if l < self.enc_num - 1:
                 emb = ops.CapsNorm.apply(v, self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'), training,

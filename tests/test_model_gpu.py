@@ -101,13 +101,14 @@ def test_train_step_runs_and_updates(cuda):
     assert samples.result() == 4
 
 
-def test_backward_overwrites_every_gradient(cuda):
+@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c3_mini_sdr_lowmemory'])
+def test_backward_overwrites_every_gradient(cuda, name):
     """The train step never zeroes grads: every parameter's gradient must be
     written (not accumulated) by the backward kernels.  Poison the flat gradient
     buffer, run one backward, and require every slice finite and equal to a
     backward from zeroed grads."""
     from srf_amd import ctc, trainer_sr
-    model, sh, z = _build('c2_mini', cuda)
+    model, sh, z = _build(name, cuda)
     feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
     inp_len = torch.tensor(z['inp_len'], dtype=torch.int32, device=cuda)
     labels = torch.tensor(z['labels'], device=cuda)
@@ -153,20 +154,21 @@ def test_fused_loss_head_matches_autograd(cuda):
     assert (model.flat_grad - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
 
 
-def test_graphed_train_step_matches_eager(cuda):
+@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c2_mini_einsum'])
+def test_graphed_train_step_matches_eager(cuda, name):
     """GraphedTrainStep (forward + CTC + backward in one hipGraph) computes the same
     loss and gradient as the eager process_train_step, and draws fresh dropout masks
     on every replay (device step counter)."""
     from srf_amd import train_helper, trainer_sr
     cfg = config_from_shape({'feat_dim': 123, 'enc_num': 3, 'iters': 3, 'lpad': 4, 'rpad': 4, 'ph': 8,
                              'pd': 16, 'ch': 8, 'cd': 16, 'vd': 16, 'context': False})
-    model, sh, z = _build('c2_mini', cuda)
+    model, sh, z = _build(name, cuda)
     inputs = (torch.tensor(z['feats'], dtype=torch.float32, device=cuda), torch.tensor(z['labels'], device=cuda),
               torch.tensor(z['inp_len'], dtype=torch.int32), torch.tensor(z['tar_len'], device=cuda))
     opt = train_helper.get_optimizer(cfg)   # lr(0) = 0: the first update leaves the parameters
     eager_nll = trainer_sr.process_train_step(4, inputs, model, opt, None, None, 1, sh.class_n - 1, None).clone()
     eager_grad = model.flat_grad.clone()
-    model2, _, _ = _build('c2_mini', cuda)
+    model2, _, _ = _build(name, cuda)
     g = trainer_sr.GraphedTrainStep(4, inputs, model2, train_helper.get_optimizer(cfg), 1, sh.class_n - 1, warmup=1)
     try:
         model2.load_params({k: v for k, v in zip(*_params_of(model))})
