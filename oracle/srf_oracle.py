@@ -9,6 +9,10 @@ Layouts follow the reference: activations NHWC (H = time, W = frequency /
 capsule index), conv kernels ``[kh, kw, Cin, Cout]``, routing weight
 ``W[in_n, out_n, out_d, in_d]`` and bias ``[in_n, out_n, out_d]`` (the reference
 variables carry extra singleton axes, ``sequence_router_naive.py:88-103``).
+
+``SrfShape.caps_type`` selects the reference variant (``trainer_sr.py:188-199``):
+naive (the default), einsum (``sequence_router_einsum.py:129-131,238``) or lowmemory
+(``sequence_router_lowmemory.py:107-109,162-164,190``).
 """
 import math
 
