@@ -44,11 +44,13 @@ size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rp
 int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, float* v_out,
                      float* saved, void* workspace, size_t workspace_bytes, void* stream);
-/* Dropout step counter (this thread): a device uint64 that every dropout kernel
- * launched afterwards by this thread mixes into its seed (NULL restores the
+/* Dropout step counter (process-wide): a device uint64 that every dropout kernel
+ * launched afterwards, from any thread, mixes into its seed (NULL restores the
  * per-call seeds alone).  It lets a training step captured into a hipGraph draw
  * fresh masks on every replay: the step advances the counter on the device.
- * Forward and backward of one step must see the same counter value. */
+ * Forward and backward of one step must see the same counter value (the autograd
+ * backward runs on torch's device worker thread, hence process-wide, not per
+ * thread; one process drives one GPU). */
 int srf_set_seed_source(const void* step_counter);
 
 /* Profiling hook (opt-in, this thread only): the next srf_route_dr_fwd call

@@ -28,6 +28,7 @@ import torch
 from safetensors.numpy import load_file, save_file
 
 VALUE = '.ATTRIBUTES/VARIABLE_VALUE'
+SAVE_COUNTER = 'save_counter/' + VALUE
 
 
 def tf_variable_map(model):
@@ -75,11 +76,16 @@ def _slot_key(tf_key, slot):
     return tf_key.replace(VALUE, f'.OPTIMIZER_SLOT/optimizer/{slot}/{VALUE}')
 
 
-def model_state(model):
-    """All model tensors (parameters + BN moving statistics) under TF names."""
+def model_state(model, overrides=None):
+    """All model tensors (parameters + BN moving statistics) under TF names.
+    ``overrides`` maps our names to tensors saved in place of the model's own (the
+    replica-mean BN moving statistics of trainer_sr.replica_mean_moving_statistics)."""
     out = {}
+    overrides = overrides or {}
     for name, (key, shape) in tf_variable_map(model).items():
-        t = model.params[name] if name in model.params else getattr(model, name)
+        t = overrides.get(name)
+        if t is None:
+            t = model.params[name] if name in model.params else getattr(model, name)
         a = t.detach().cpu().numpy().astype(np.float32)
         out[key] = a.reshape(shape) if shape else a
     return out
@@ -138,13 +144,20 @@ def load_optimizer_state(model, optimizer, state):
 class CheckpointManager:
     """tf.train.CheckpointManager(ckpt, directory, max_to_keep): ``ckpt-N``
     prefixes, N = save counter; the ``checkpoint`` text file lists them like TF's
-    CheckpointState (model_checkpoint_path / all_model_checkpoint_paths)."""
+    CheckpointState (model_checkpoint_path / all_model_checkpoint_paths).
+
+    ``save_counter`` is tf.train.Checkpoint's save_counter: 0 for a fresh
+    checkpoint object, set by a restore to the value stored in the restored
+    checkpoint, and advanced by one on every save, which numbers the file unless
+    an explicit checkpoint_number is given.  Resuming from ckpt-3 while ckpt-5
+    exists therefore writes ckpt-4 next, as TF does."""
 
     SUFFIX = '.srf.safetensors'
 
     def __init__(self, model, optimizer, directory, max_to_keep=5):
         self.model, self.optimizer, self.directory = model, optimizer, directory
         self.max_to_keep = max_to_keep
+        self.save_counter = 0
         os.makedirs(directory, exist_ok=True)
         self._ckpts = self._read_state()
 
@@ -171,15 +184,16 @@ class CheckpointManager:
         with open(os.path.join(self.directory, 'checkpoint'), 'w') as f:
             f.write('\n'.join(lines) + '\n')
 
-    def save(self, checkpoint_number=None):
-        n = checkpoint_number
-        if n is None:
-            n = 1 + max([int(c.split('-')[-1]) for c in self._ckpts] + [0])
+    def save(self, checkpoint_number=None, overrides=None):
+        """``overrides``: see model_state (data-parallel runs pass the replica-mean
+        BN moving statistics, which is what a MirroredStrategy checkpoint holds)."""
+        self.save_counter += 1
+        n = self.save_counter if checkpoint_number is None else int(checkpoint_number)
         name = f'ckpt-{n}'
-        state = model_state(self.model)
+        state = model_state(self.model, overrides)
         if self.optimizer is not None:
             state.update(optimizer_state(self.model, self.optimizer))
-        state['save_counter/' + VALUE] = np.array(n, np.int64)
+        state[SAVE_COUNTER] = np.array(self.save_counter, np.int64)
         save_file(state, os.path.join(self.directory, name) + self.SUFFIX)
         self._ckpts = [c for c in self._ckpts if c != name] + [name]
         if self.max_to_keep is not None and self.max_to_keep > 0:
@@ -195,11 +209,13 @@ def read_checkpoint(prefix):
 
 
 def restore(prefix, model, optimizer=None, expect_partial=True):
-    """tf.train.Checkpoint(...).restore(prefix).expect_partial()."""
+    """tf.train.Checkpoint(...).restore(prefix).expect_partial(); returns the
+    restored save_counter (0 when the checkpoint holds none)."""
     state = read_checkpoint(prefix)
     load_model_state(model, state, strict=not expect_partial)
     if optimizer is not None:
         load_optimizer_state(model, optimizer, state)
+    return int(np.asarray(state[SAVE_COUNTER]).reshape(-1)[0]) if SAVE_COUNTER in state else 0
 
 
 def load_checkpoint(config, logger, model, optimizer):
@@ -216,7 +232,7 @@ def load_checkpoint(config, logger, model, optimizer):
         loaded = manager.latest_checkpoint
     if 'ckpt' in loaded:
         epoch_offset = int(loaded.split('-')[-1])
-        restore(loaded, model, optimizer)
+        manager.save_counter = restore(loaded, model, optimizer)
     else:
         epoch_offset = 0
         loaded = None
@@ -226,11 +242,14 @@ def load_checkpoint(config, logger, model, optimizer):
 
 
 def average_checkpoints(config, logger, model_fn, optimizer=None):
-    """average_ckpt_sr.py:100-179: element-wise mean of the model weights of the
-    last ``model_average_num`` checkpoints in ``path_ckpt``, saved through a
+    """average_ckpt_sr.py:91-179: element-wise mean of the model weights of the
+    last ``model_average_num`` checkpoints in ``path_ckpt`` among those numbered
+    <= ``train_max_epoch`` (all of them when it is 0, :91-96), saved through a
     max_to_keep=1 manager into ``path_ckpt/avg`` (replaced if present)."""
     import shutil
     ckpts = CheckpointManager(model_fn(), None, config.path_ckpt, max_to_keep=None).checkpoints
+    max_epoch = getattr(config, 'train_max_epoch', 0) or 0
+    ckpts = [c for c in ckpts if max_epoch == 0 or int(c.split('-')[-1]) <= max_epoch]
     chosen = ckpts[-config.model_average_num:]
     if not chosen:
         raise FileNotFoundError(f'no checkpoints in {config.path_ckpt}')

@@ -1,4 +1,5 @@
 // Library identity, thread-local error reporting and the dropout step counter of the C ABI.
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 
@@ -7,7 +8,10 @@
 
 namespace {
 thread_local char g_err[512] = "";
-thread_local const unsigned long long* t_seed_src = nullptr;
+// Process-global, not thread-local: torch runs the autograd backward of device
+// tensors on its own per-device worker thread, and the backward kernels must
+// rebuild the forward's dropout masks from the same counter.
+std::atomic<const unsigned long long*> g_seed_src{nullptr};
 }
 
 namespace srf {
@@ -17,14 +21,14 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
-const unsigned long long* seed_source() { return t_seed_src; }
+const unsigned long long* seed_source() { return g_seed_src.load(std::memory_order_acquire); }
 }  // namespace srf
 
 extern "C" {
 int srf_version(void) { return 1; }
 
 int srf_set_seed_source(const void* step_counter) {
-  t_seed_src = static_cast<const unsigned long long*>(step_counter);
+  g_seed_src.store(static_cast<const unsigned long long*>(step_counter), std::memory_order_release);
   return 0;
 }
 const char* srf_last_error(void) { return g_err; }

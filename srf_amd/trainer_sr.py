@@ -61,9 +61,36 @@ def ceil_div(inp_len, div):
     return torch.div(inp_len + (div - 1), div, rounding_mode='floor').to(torch.int32)
 
 
+def _world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
 def allreduce_grads(model):
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _world() > 1:
         dist.all_reduce(model.flat_grad, op=dist.ReduceOp.SUM)
+
+
+def replica_mean_moving_statistics(model):
+    """BatchNorm moving statistics as a MirroredStrategy checkpoint holds them.
+
+    Batch statistics stay per replica (Keras BN is not SyncBN), so each rank's
+    moving mean / variance drift apart.  Under MirroredStrategy they are SyncOnRead
+    variables with MEAN aggregation: a replica reads its own value (validation runs
+    inside strategy.run, trainer_sr.py:224-228), while a cross-replica read -- the
+    checkpoint save (trainer_sr.py:281-288) -- sees the mean over replicas.  Every
+    rank calls this (one all-reduce of 4*64 floats); it returns {buffer name: mean}
+    for CheckpointManager.save(overrides=...) and leaves the local buffers alone."""
+    names = [f'bn{k}_moving_{s}' for k in range(model.cnn_n) for s in ('mean', 'var')]
+    bufs = [getattr(model, n) for n in names]
+    flat = torch.cat([b.detach().reshape(-1) for b in bufs])
+    if _world() > 1:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        flat /= _world()
+    out, off = {}, 0
+    for n, b in zip(names, bufs):
+        out[n] = flat[off:off + b.numel()].view_as(b)
+        off += b.numel()
+    return out
 
 
 def process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_state, n_gpus, blank_idx, samples):
@@ -99,9 +126,14 @@ class GraphedTrainStep:
     the step is bound by the GPU, not by Python/ctypes launch overhead (which
     grows when several ranks share a host).  Dropout stays random per step: the
     captured step first advances a device-resident step counter that every dropout
-    kernel mixes into its seed (srf_set_seed_source).  ``inputs`` are the static
-    input tensors: refill them in place between replays to feed new data of the
-    same shape and lengths.
+    kernel mixes into its seed (srf_set_seed_source).
+
+    The graph reads the static tensors ``self.feats`` (cropped to max(inp_len),
+    which may be a private copy of the caller's feats), ``self.labels``,
+    ``self.inp_len`` (device copy) and ``self.tar_len``, not the caller's
+    ``inputs``.  Feed a new batch of the same shape and lengths with
+    ``refill(...)``, which copies into those tensors and refuses any other shape
+    or lengths.
     """
 
     def __init__(self, in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=2):
@@ -128,6 +160,18 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.nll = self._fwd_bwd()
+
+    def refill(self, feats, labels, inp_len, tar_len):
+        """Copy a new batch into the tensors the captured graph reads."""
+        if not torch.equal(torch.as_tensor(inp_len).cpu().to(torch.int64),
+                           torch.as_tensor(self.host_len).cpu().to(torch.int64)):
+            raise ValueError('GraphedTrainStep.refill: input lengths differ from the captured batch')
+        feats = feats[:, :self.feats.shape[1], :]
+        for dst, src, what in ((self.feats, feats, 'feats'), (self.labels, labels, 'labels'),
+                               (self.tar_len, tar_len, 'tar_len')):
+            if tuple(src.shape) != tuple(dst.shape):
+                raise ValueError(f'GraphedTrainStep.refill: {what} shape {tuple(src.shape)} != {tuple(dst.shape)}')
+            dst.copy_(src, non_blocking=True)
 
     def _fwd_bwd(self):
         self.counter.add_(1)

@@ -83,13 +83,31 @@ def test_manager_save_restore_rotation(tmp_path):
     torch.testing.assert_close(m3.params['W1'], m.params['W1'] - 1.0, rtol=0, atol=1e-6)
 
 
+def test_resume_numbers_from_restored_save_counter(tmp_path):
+    """tf.train.Checkpoint restores save_counter with the model: resuming from
+    ckpt-3 while ckpt-5 exists writes ckpt-4 next (and the epoch offset of the
+    following resume is 4, not 6)."""
+    m = _model(1)
+    mgr = ck.CheckpointManager(m, None, str(tmp_path), max_to_keep=None)
+    for _ in range(5):
+        mgr.save()
+    assert mgr.save_counter == 5
+    cfg = argparse.Namespace(model_ckpt_max_to_keep=-1, path_ckpt=str(tmp_path), path_ckpt_epoch=3)
+    mgr2, epoch = ck.load_checkpoint(cfg, None, _model(2), None)
+    assert epoch == 3 and mgr2.save_counter == 3
+    assert mgr2.save().endswith('ckpt-4')
+    assert int(ck.read_checkpoint(os.path.join(str(tmp_path), 'ckpt-4'))[ck.SAVE_COUNTER]) == 4
+    # a fresh checkpoint object (no restore) counts from 0, as TF's does
+    assert ck.CheckpointManager(m, None, str(tmp_path / 'other'), max_to_keep=None).save().endswith('ckpt-1')
+
+
 def test_average_checkpoints(tmp_path):
     models = [_model(10 + k) for k in range(3)]
     mgr = ck.CheckpointManager(models[0], None, str(tmp_path), max_to_keep=None)
     for mk in models:
         mgr.model = mk
         mgr.save()
-    cfg = argparse.Namespace(path_ckpt=str(tmp_path), model_average_num=2)
+    cfg = argparse.Namespace(path_ckpt=str(tmp_path), model_average_num=2, train_max_epoch=0)
     path, avg = ck.average_checkpoints(cfg, None, lambda: _model(99))
     assert path == os.path.join(str(tmp_path), 'avg', 'ckpt-1')
     for k in avg.params:
@@ -98,6 +116,12 @@ def test_average_checkpoints(tmp_path):
     back = _model(5)
     ck.restore(path, back)
     torch.testing.assert_close(back.params['b0'], avg.params['b0'], rtol=0, atol=0)
+    # average_ckpt_sr.py:91-96: only ckpt-N with N <= train_max_epoch take part
+    cfg.train_max_epoch = 2
+    _, avg2 = ck.average_checkpoints(cfg, None, lambda: _model(99))
+    for k in avg2.params:
+        want = (models[0].params[k].detach() + models[1].params[k].detach()) / 2
+        torch.testing.assert_close(avg2.params[k].detach(), want, rtol=1e-6, atol=1e-7)
 
 
 def _masked_crc(b):

@@ -68,3 +68,44 @@ def test_gloo_allreduce_gives_global_gradient():
     total = sum(((X @ w) ** 2).sum() / float(B * world) for _, _, X, B in res)
     total.backward()
     assert torch.allclose(g0, w.grad, atol=1e-6)
+
+
+def _bn_worker(rank, world, port, ckdir, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from srf_amd import checkpoint as ck
+    from tests.test_checkpoint_cpu import _model
+    model = _model(0)
+    with torch.no_grad():     # per-replica batch statistics drift apart
+        model.bn0_moving_mean.fill_(1.0 + rank)
+        model.bn1_moving_var.fill_(2.0 * (rank + 1))
+    means = trainer_sr.replica_mean_moving_statistics(model)
+    if rank == 0:
+        ck.CheckpointManager(model, None, ckdir, max_to_keep=None).save(overrides=means)
+    dist.barrier()
+    q.put((rank, float(model.bn0_moving_mean[0]), float(means['bn0_moving_mean'][0]),
+           float(means['bn1_moving_var'][0])))
+    dist.destroy_process_group()
+
+
+def test_gloo_checkpoint_holds_replica_mean_bn_statistics(tmp_path):
+    """MirroredStrategy saves SyncOnRead(MEAN) BN moving statistics: the checkpoint
+    holds the mean over ranks, each rank keeps its own local values."""
+    from srf_amd import checkpoint as ck
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bn_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [1.0, 2.0]                 # local values untouched
+    assert all(r[2] == 1.5 and r[3] == 3.0 for r in res)     # mean over replicas
+    st = ck.read_checkpoint(os.path.join(str(tmp_path), 'ckpt-1'))
+    assert float(st['model/conv/bn_layers/0/moving_mean/' + ck.VALUE][0]) == 1.5
+    assert float(st['model/conv/bn_layers/1/moving_variance/' + ck.VALUE][0]) == 3.0

@@ -194,3 +194,50 @@ def test_graphed_train_step_matches_eager(cuda, name):
 def _params_of(model):
     names = list(model.params.keys())
     return names, [model.params[k].detach().clone() for k in names]
+
+
+def test_graphed_dropout_gradient_matches_finite_difference(cuda):
+    """Dropout on, GraphedTrainStep: the replayed gradient must be the gradient of
+    the loss under the SAME dropout masks.  The forward and the backward kernels
+    both rebuild their masks from (per-call seed, device step counter); the
+    backward runs on torch's autograd device thread, so the counter must be seen
+    there too (a per-thread counter would leave the backward on other masks).
+    Checked with central differences of the graphed step's own loss along the
+    gradient direction and along a random direction (fp32, 2 % tolerance)."""
+    from srf_amd import ctc, train_helper, trainer_sr
+    cfg = config_from_shape({'feat_dim': 123, 'enc_num': 3, 'iters': 3, 'lpad': 4, 'rpad': 4, 'ph': 8,
+                             'pd': 16, 'ch': 8, 'cd': 16, 'vd': 16, 'context': False})
+    model, sh, z = _build('c2_mini', cuda)
+    model.dropout_enabled = True
+    inputs = (torch.tensor(z['feats'], dtype=torch.float32, device=cuda), torch.tensor(z['labels'], device=cuda),
+              torch.tensor(z['inp_len'], dtype=torch.int32), torch.tensor(z['tar_len'], device=cuda))
+    g = trainer_sr.GraphedTrainStep(4, inputs, model, train_helper.get_optimizer(cfg), 1, sh.class_n - 1, warmup=1)
+    try:
+        cap_calls = model._calls             # the captured forward drew seed number cap_calls
+        g.graph.replay()                     # counter -> c + 1; gradient into flat_grad
+        torch.cuda.synchronize()
+        grad = model.flat_grad.clone()
+        B = inputs[0].shape[0]
+
+        @torch.no_grad()
+        def loss():
+            model._calls = cap_calls - 1     # same per-call seed as the captured step
+            logits = model(g.feats, input_lengths=g.inp_len, training=True)
+            nll = ctc.ctc_loss(g.labels, logits, g.tar_len, g.logit_len, blank_index=sh.class_n - 1)
+            return float(nll.double().sum()) / B
+
+        assert abs(loss() - float(g.nll.double().sum()) / B) <= 1e-4 * abs(loss())
+        p0 = model.flat_params.clone()
+        gen = torch.Generator(device=cuda).manual_seed(7)
+        rnd = torch.randn(p0.shape, device=cuda, generator=gen) * (grad != 0)
+        for d in (grad / grad.norm(), rnd / rnd.norm()):
+            h = 1e-3    # calibrated (scripts/dbg_fd.py): |p| ~ 131, |g| ~ 160; h = 1e-1 is too coarse
+            model.flat_params.copy_(p0 + h * d)
+            lp = loss()
+            model.flat_params.copy_(p0 - h * d)
+            lm = loss()
+            model.flat_params.copy_(p0)
+            fd, an = (lp - lm) / (2 * h), float((grad * d).sum())
+            assert abs(fd - an) <= 0.02 * abs(float(grad.norm())), (fd, an, float(grad.norm()))
+    finally:
+        g.close()
