@@ -44,6 +44,25 @@ size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rp
 int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, float* v_out,
                      float* saved, void* workspace, size_t workspace_bytes, void* stream);
+/* Coupling storage (the 32x32 split-bf16 path: din in {8, 16}, dout in {8, 16, 32},
+ * J*dout <= 1024; 0 for other shapes or iters < 2): the couplings c^r and logZ^r
+ * of the routing iterations r >= 1, written by srf_route_dr_fwd_ex when
+ * couplings != NULL and read by srf_route_dr_bwd_ex / _bwd_data_ex, whose
+ * backward routing passes then skip the logit and softmax recompute.  NULL
+ * couplings: the plain entry points' behaviour (forward stores nothing, backward
+ * recomputes).  Inference passes NULL. */
+size_t srf_route_dr_coupling_floats(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters);
+int srf_route_dr_fwd_ex(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                        int rpad, int J, int dout, int iters, int mask_first, int n_chunks, float* v_out,
+                        float* saved, float* couplings, void* workspace, size_t workspace_bytes, void* stream);
+int srf_route_dr_bwd_ex(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                        int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
+                        const float* couplings, const float* g_v, float* g_emb, float* g_W, float* g_bias,
+                        void* workspace, size_t workspace_bytes, void* stream);
+int srf_route_dr_bwd_data_ex(const float* emb, const float* W, const float* bias, int B, int T, int N, int din,
+                             int lpad, int rpad, int J, int dout, int iters, int mask_first, int n_chunks,
+                             const float* saved, const float* couplings, const float* g_v, float* g_emb,
+                             void* workspace, size_t workspace_bytes, void* stream);
 /* Dropout step counter (process-wide): a device uint64 that every dropout kernel
  * launched afterwards, from any thread, mixes into its seed (NULL restores the
  * per-call seeds alone).  It lets a training step captured into a hipGraph draw

@@ -972,7 +972,7 @@ inline bool use_fwd32(const Geom& g) {
 
 template <int D>
 int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias, float* v_out,
-             float* saved, float* slab, hipStream_t st) {
+             float* saved, float* couplings, float* slab, hipStream_t st) {
   const PassCfg pc = pass_cfg(g);
   const size_t FJD = (size_t)g.F() * g.JD();
   hipEvent_t* ev0 = t_ev_start;
@@ -997,8 +997,14 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     const float* vc = r > 0 ? saved + (size_t)(2 * (r - 1) + 1) * FJD : nullptr;
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev0[r], st));
     if (p32) {
+      float *cst = nullptr, *lzst = nullptr;
+      if (couplings != nullptr && r > 0) {
+        const size_t blk = (size_t)g.F() * g.in_n();
+        cst = couplings + (size_t)(r - 1) * blk * (plan.JDp / g.dout);
+        lzst = couplings + (size_t)(g.iters - 1) * blk * (plan.JDp / g.dout) + (size_t)(r - 1) * blk;
+      }
       const int rc = srf::fwd32_pass(plan, r == 0, slab, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout,
-                                     g.mask_first, vc, st);
+                                     g.mask_first, vc, cst, lzst, st);
       if (rc) return rc;
     } else {
       dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, r == 0 ? bsum : nullptr, slab, nullptr, 1, st);
@@ -1015,6 +1021,7 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
 
 struct BwdWs {
   float *A, *gs, *slab, *stats, *gu_t, *xT, *WT;
+  void* p32;          // split-bf16 operand planes + slab of the B1 passes from stored couplings
   size_t bytes;
 };
 
@@ -1029,6 +1036,11 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   const size_t oA = take(F * JD), ogs = take((size_t)g.iters * F * JD), oslab = take((size_t)n_chunks * F * JD),
                ostats = take((size_t)(g.iters - 1) * F * in_n * 2), ogu = take(in_n * (size_t)g.NT() * 16 * Fp),
                oxt = take(in_n * g.din * Fp), owt = take(in_n * JD * g.din);
+  size_t op32 = 0;
+  if (use_fwd32(g)) {
+    const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    op32 = take((srf::fwd32_workspace(plan) + 3) / 4);
+  }
   char* b = static_cast<char*>(base);
   BwdWs w;
   w.A = (float*)(b + oA);
@@ -1038,6 +1050,7 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   w.gu_t = (float*)(b + ogu);
   w.xT = (float*)(b + oxt);
   w.WT = (float*)(b + owt);
+  w.p32 = op32 ? (void*)(b + op32) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -1066,8 +1079,8 @@ int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias,
 
 template <int D>
 int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias, const float* saved,
-             const float* g_v, float* g_emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st,
-             bool with_weights) {
+             const float* couplings, const float* g_v, float* g_emb, float* g_W, float* g_bias, const BwdWs& w,
+             hipStream_t st, bool with_weights) {
   const PassCfg pc = pass_cfg(g);
   const size_t FJD = (size_t)g.F() * g.JD();
   const int R = g.iters;
@@ -1079,13 +1092,35 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   SRF_LAUNCH_CHECK("bwd_finish");
   // Iteration 0 needs no backward pass: Vc^0 = 0, so its couplings are uniform
   // and its logits carry no gradient.
+  const bool p32 = couplings != nullptr && w.p32 != nullptr && R > 1;
+  srf::Fwd32Plan plan{};
+  if (p32) {
+    // B1 from the forward's stored couplings on the split-bf16 32x32 tiles
+    plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    const int rc = srf::fwd32_prepare(plan, emb, W, bias, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, w.p32,
+                                      st);
+    if (rc) return rc;
+  }
   for (int r = R - 1; r >= 1; --r) {
     const float* vc = saved + (size_t)(2 * (r - 1) + 1) * FJD;
     float* stats_r = w.stats + (size_t)(r - 1) * g.F() * g.in_n() * 2;
-    dispatch_pass<D, MODE_BWD>(g, pc, n_chunks, emb, W, bias, r, vc, w.gs + (size_t)r * FJD, w.slab, stats_r, 1, st);
-    SRF_LAUNCH_CHECK("route_pass(bwd)");
-    launch_bwd_finish<D>(g, w.slab, n_chunks, nullptr, w.A, saved + (size_t)(2 * (r - 1)) * FJD,
-                         w.gs + (size_t)(r - 1) * FJD, st);
+    if (p32) {
+      const size_t blk = (size_t)g.F() * g.in_n();
+      const int JP = plan.JDp / g.dout;
+      const int rc = srf::bwd32_pass(plan, w.p32, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout,
+                                     couplings + (size_t)(r - 1) * blk * JP,
+                                     couplings + (size_t)(R - 1) * blk * JP + (size_t)(r - 1) * blk,
+                                     w.gs + (size_t)r * FJD, stats_r, st);
+      if (rc) return rc;
+      launch_bwd_finish<D>(g, srf::fwd32_slab(plan, w.p32), plan.n_chunks, nullptr, w.A,
+                           saved + (size_t)(2 * (r - 1)) * FJD, w.gs + (size_t)(r - 1) * FJD, st);
+    } else {
+      dispatch_pass<D, MODE_BWD>(g, pc, n_chunks, emb, W, bias, r, vc, w.gs + (size_t)r * FJD, w.slab, stats_r, 1,
+                                 st);
+      SRF_LAUNCH_CHECK("route_pass(bwd)");
+      launch_bwd_finish<D>(g, w.slab, n_chunks, nullptr, w.A, saved + (size_t)(2 * (r - 1)) * FJD,
+                           w.gs + (size_t)(r - 1) * FJD, st);
+    }
     SRF_LAUNCH_CHECK("bwd_finish");
   }
   {
@@ -1141,9 +1176,22 @@ size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rp
   return bwd_layout(g, n_chunks, nullptr).bytes;
 }
 
+size_t srf_route_dr_coupling_floats(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters) {
+  Geom g{B, T, N, din, lpad, rpad, J, dout, iters, 0};
+  if (!use_fwd32(g) || iters < 2) return 0;
+  return srf::fwd32_coupling_floats(srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout), B * T, g.in_n(), dout, iters);
+}
+
 int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, float* v_out, float* saved,
                      void* workspace, size_t workspace_bytes, void* stream) {
+  return srf_route_dr_fwd_ex(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, v_out,
+                             saved, nullptr, workspace, workspace_bytes, stream);
+}
+
+int srf_route_dr_fwd_ex(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                        int rpad, int J, int dout, int iters, int mask_first, int n_chunks, float* v_out,
+                        float* saved, float* couplings, void* workspace, size_t workspace_bytes, void* stream) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, iters, mask_first ? 1 : 0};
   int rc = check_geom(g);
   if (rc) return rc;
@@ -1156,19 +1204,20 @@ int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B,
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* slab = static_cast<float*>(workspace);
+  if (couplings != nullptr && (!use_fwd32(g) || iters < 2)) couplings = nullptr;   // nothing to store
   switch (din) {
-    case 8: return fwd_impl<8>(g, n_chunks, emb, W, bias, v_out, saved, slab, st);
-    case 16: return fwd_impl<16>(g, n_chunks, emb, W, bias, v_out, saved, slab, st);
-    case 32: return fwd_impl<32>(g, n_chunks, emb, W, bias, v_out, saved, slab, st);
-    default: return fwd_impl<64>(g, n_chunks, emb, W, bias, v_out, saved, slab, st);
+    case 8: return fwd_impl<8>(g, n_chunks, emb, W, bias, v_out, saved, couplings, slab, st);
+    case 16: return fwd_impl<16>(g, n_chunks, emb, W, bias, v_out, saved, couplings, slab, st);
+    case 32: return fwd_impl<32>(g, n_chunks, emb, W, bias, v_out, saved, couplings, slab, st);
+    default: return fwd_impl<64>(g, n_chunks, emb, W, bias, v_out, saved, couplings, slab, st);
   }
 }
 
 namespace {
 int route_dr_bwd_entry(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                        int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
-                       const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
-                       size_t workspace_bytes, void* stream, bool with_weights) {
+                       const float* couplings, const float* g_v, float* g_emb, float* g_W, float* g_bias,
+                       void* workspace, size_t workspace_bytes, void* stream, bool with_weights) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, iters, mask_first ? 1 : 0};
   int rc = check_geom(g);
   if (rc) return rc;
@@ -1180,11 +1229,16 @@ int route_dr_bwd_entry(const float* emb, const float* W, const float* bias, int 
     return SRF_EWORKSPACE;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (couplings != nullptr && (!use_fwd32(g) || iters < 2)) couplings = nullptr;
   switch (din) {
-    case 8: return bwd_impl<8>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
-    case 16: return bwd_impl<16>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
-    case 32: return bwd_impl<32>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
-    default: return bwd_impl<64>(g, n_chunks, emb, W, bias, saved, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+    case 8:
+      return bwd_impl<8>(g, n_chunks, emb, W, bias, saved, couplings, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+    case 16:
+      return bwd_impl<16>(g, n_chunks, emb, W, bias, saved, couplings, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+    case 32:
+      return bwd_impl<32>(g, n_chunks, emb, W, bias, saved, couplings, g_v, g_emb, g_W, g_bias, w, st, with_weights);
+    default:
+      return bwd_impl<64>(g, n_chunks, emb, W, bias, saved, couplings, g_v, g_emb, g_W, g_bias, w, st, with_weights);
   }
 }
 }  // namespace
@@ -1193,8 +1247,16 @@ int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
                      const float* g_v, float* g_emb, float* g_W, float* g_bias, void* workspace,
                      size_t workspace_bytes, void* stream) {
-  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved, g_v,
-                            g_emb, g_W, g_bias, workspace, workspace_bytes, stream, true);
+  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved,
+                            nullptr, g_v, g_emb, g_W, g_bias, workspace, workspace_bytes, stream, true);
+}
+
+int srf_route_dr_bwd_ex(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                        int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
+                        const float* couplings, const float* g_v, float* g_emb, float* g_W, float* g_bias,
+                        void* workspace, size_t workspace_bytes, void* stream) {
+  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved,
+                            couplings, g_v, g_emb, g_W, g_bias, workspace, workspace_bytes, stream, true);
 }
 
 int srf_route_dr_bwd_data(const float* emb, const float* W, const float* bias, int B, int T, int N, int din,
@@ -1203,8 +1265,17 @@ int srf_route_dr_bwd_data(const float* emb, const float* W, const float* bias, i
                           size_t workspace_bytes, void* stream) {
   // g_W / g_bias are not touched by the data pass; the checks want non-null pointers
   float* unused = reinterpret_cast<float*>(workspace);
-  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved, g_v,
-                            g_emb, unused, unused, workspace, workspace_bytes, stream, false);
+  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved,
+                            nullptr, g_v, g_emb, unused, unused, workspace, workspace_bytes, stream, false);
+}
+
+int srf_route_dr_bwd_data_ex(const float* emb, const float* W, const float* bias, int B, int T, int N, int din,
+                             int lpad, int rpad, int J, int dout, int iters, int mask_first, int n_chunks,
+                             const float* saved, const float* couplings, const float* g_v, float* g_emb,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  float* unused = reinterpret_cast<float*>(workspace);
+  return route_dr_bwd_entry(emb, W, bias, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, saved,
+                            couplings, g_v, g_emb, unused, unused, workspace, workspace_bytes, stream, false);
 }
 
 int srf_route_dr_bwd_weights(const float* emb, int B, int T, int N, int din, int lpad, int rpad, int J, int dout,

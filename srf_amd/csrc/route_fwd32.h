@@ -22,8 +22,16 @@ float* fwd32_slab(const Fwd32Plan& p, void* ws);
 // split W / bias / emb into bf16 planes and the i-chunk bias sums (once per forward)
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
                   int din, int lpad, int rpad, int J, int dout, void* ws, hipStream_t st);
-// one routing pass: partial s over i-chunks into fwd32_slab(p, ws)
+// one routing pass: partial s over i-chunks into fwd32_slab(p, ws); passes r >= 1
+// also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr
 int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
-               int J, int dout, int mask_first, const float* vc, hipStream_t st);
+               int J, int dout, int mask_first, const float* vc, float* cst, float* lzst, hipStream_t st);
+// coupling storage of one forward: (iters - 1) blocks of c^r [F][in_n][JP] followed by
+// (iters - 1) blocks of logZ^r [F][in_n]; JP = JDp / dout
+size_t fwd32_coupling_floats(const Fwd32Plan& p, int F, int in_n, int dout, int iters);
+// one backward routing pass r >= 1 from the stored couplings: partial gVc^r over
+// i-chunks into fwd32_slab(p, ws) and the (logZ, sigma) stats of the gu pass
+int bwd32_pass(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad, int J,
+               int dout, const float* cst, const float* lz, const float* gs, float* stats, hipStream_t st);
 
 }  // namespace srf

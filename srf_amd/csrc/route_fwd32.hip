@@ -276,7 +276,20 @@ struct Args32 {
   const float* vc;
   const float* bsum;
   float* slab;
+  // forward passes r >= 1: when cst != nullptr, the couplings c^r [F][in_n][JP]
+  // (each lane's owned capsules contiguous, see c_slot) and logZ^r [F][in_n] are
+  // stored for the backward (route_bwd32_kernel reads them instead of recomputing
+  // the logits)
+  float* cst;
+  float* lzst;
+  int JP;
 };
+
+// Position of a wave's owned capsule in the stored coupling row: lane half h owns
+// capsules j0 + 2a + h (a < OWN) after the logit reduce-scatter, stored at
+// j0 + h*OWN + a so that a lane's OWN values are one contiguous vector.
+template <int DOUT>
+__host__ __device__ constexpr int c_cp() { return kTW * 32 / DOUT; }
 
 // ------------------------------------------------------------------ kernels
 // Iteration-0 pass (naive:172-181: logits 0 + mask, so c is uniform):
@@ -523,6 +536,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       SRF_TMARK(1)
       // c = exp(L - M) / Z = e * exp(m - M) / Z; then all-gather over the halves
       const float sc = __expf(m - M) / Z;
+      if (A.cst != nullptr && fvalid) {
+        float* dst = A.cst + ((size_t)f * A.in_n + i) * A.JP + j0 + h * OWN;
+        if constexpr (OWN % 4 == 0) {
+#pragma unroll
+          for (int a = 0; a < OWN; a += 4)
+            *reinterpret_cast<f4*>(dst + a) = f4{e[a] * sc, e[a + 1] * sc, e[a + 2] * sc, e[a + 3] * sc};
+        } else {
+          *reinterpret_cast<f2*>(dst) = f2{e[0] * sc, e[1] * sc};
+        }
+        if (h == 0 && wv == 0) A.lzst[(size_t)f * A.in_n + i] = M + __logf(Z);
+      }
       float c[CP];
 #pragma unroll
       for (int a = 0; a < OWN; ++a) {
@@ -561,6 +585,174 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     }
 }
 
+
+// ------------------------------------------------------------------ backward pass
+// Backward routing pass r >= 1 (the adjoint of _loop_body, naive:199-206), on the
+// forward's tiles and split-bf16 pose.  The couplings c^r come from the forward
+// (Args32::cst), so no logit is recomputed:
+//   q_ij = <gs_j, u_ij>,  sigma_i = sum_j c_ij q_ij,  gL_ij = c_ij (q_ij - sigma_i),
+//   gVc_j (partial over the i-chunk) = sum_i gL_ij u_ij      -> slab
+//   stats[f][i] = (logZ_i, sigma_i)                            (for the gu pass)
+// gs^r rows live in each wave's private LDS slab in fragment order (as Vc in the
+// forward); sigma needs one cross-wave sum per input capsule (one barrier).
+struct Bwd32Args {
+  const float* cst;   // c^r [F][in_n][JP]
+  const float* lz;    // logZ^r [F][in_n]
+  const float* gs;    // gs^r [F][JD]
+  float* stats;       // [F][in_n][2]
+};
+
+template <int OWN>
+__device__ __forceinline__ void load_c(const float* __restrict__ p, float (&c)[OWN]) {
+  if constexpr (OWN % 4 == 0) {
+#pragma unroll
+    for (int a = 0; a < OWN; a += 4) {
+      const f4 v = *reinterpret_cast<const f4*>(p + a);
+      c[a] = v.x; c[a + 1] = v.y; c[a + 2] = v.z; c[a + 3] = v.w;
+    }
+  } else {
+    const f2 v = *reinterpret_cast<const f2*>(p);
+    c[0] = v.x; c[1] = v.y;
+  }
+}
+
+template <int DIN, int DOUT, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesPerEU))) void route_bwd32_kernel(
+    Args32 A, Bwd32Args Bk) {
+  constexpr int TW = kTW;
+  constexpr int CP = TW * 32 / DOUT;
+  constexpr int OWN = CP / 2;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int JD = A.J * DOUT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int ft = blockIdx.x / A.n_chunks, chunk = blockIdx.x - ft * A.n_chunks;
+  const int f = ft * 32 + r;
+  const int fc = min(f, A.F - 1);
+  const int fb = fc / A.T, ftt = fc - fb * A.T;
+  const bool fvalid = f < A.F;
+  const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
+  const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
+  const int j0 = tbase * 32 / DOUT;
+  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
+
+  f4* gsl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
+  float* st = lds + (size_t)NW * TW * 4 * 64 * 4;
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (fvalid && row < JD) v = *reinterpret_cast<const f4*>(Bk.gs + (size_t)f * JD + row);
+      gsl[(t * 4 + q) * 64 + lane] = v;
+    }
+  const bf8 ones = ones_frag(h);
+  f16v acc[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) acc[t] = f16v{};
+  const float* crow = Bk.cst + (size_t)fc * A.in_n * A.JP + j0 + h * OWN;
+  int par = 0;
+  if (i0 < i1) {
+    Frags32<DIN, TW> fr;
+    float cn[OWN];
+    fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8, fr);
+    load_c<OWN>(crow + (size_t)i0 * A.JP, cn);
+    for (int i = i0; i < i1; ++i) {
+      f16v u[TW];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
+      float cc[OWN];
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) cc[a] = cn[a];
+      // partial dots <u_ij, gs_j> over this lane's rows
+      f2 P2[CP];
+#pragma unroll
+      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 gv = gsl[(t * 4 + q) * 64 + lane];
+          const int k = kpart<DOUT>(t, 4 * q);
+          P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{gv.x, gv.y};
+          P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{gv.z, gv.w};
+        }
+      float Q[OWN];
+      float sp = 0.f;
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        const float pa = P2[2 * a].x + P2[2 * a].y, pb = P2[2 * a + 1].x + P2[2 * a + 1].y;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa), __float_as_uint(pb), false, false);
+        Q[a] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        sp += cc[a] * Q[a];
+      }
+      float S;
+      {
+        float s0, s1;
+        xpair32(sp, s0, s1);
+        S = s0 + s1;
+      }
+      if constexpr (NW > 1) {
+        float* slot = st + par * NW * 32;
+        if (h == 0) slot[wv * 32 + r] = S;
+        __syncthreads();
+        constexpr int HW = NW / 2;
+        float sh = 0.f;
+#pragma unroll
+        for (int w = 0; w < HW; ++w) sh += slot[(h * HW + w) * 32 + r];
+        float s0, s1;
+        xpair32(sh, s0, s1);
+        S = s0 + s1;
+        par ^= 1;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < i1) {
+        fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
+                               h, A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
+                               (uint32_t)(i + 1) * A.JDp * 8, fr);
+        load_c<OWN>(crow + (size_t)(i + 1) * A.JP, cn);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (wv == 0 && h == 0 && fvalid) {
+        const size_t fi = (size_t)f * A.in_n + i;
+        *reinterpret_cast<f2*>(Bk.stats + fi * 2) = f2{Bk.lz[fi], S};
+      }
+      // gL of the owned capsules, then all-gather over the lane halves
+      float g[CP];
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        float g0, g1;
+        xpair32(cc[a] * (Q[a] - S), g0, g1);
+        g[2 * a] = g0;
+        g[2 * a + 1] = g1;
+      }
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const float gv = g[kpart<DOUT>(t, v)];
+          f2 a2 = {acc[t][v], acc[t][v + 1]};
+          a2 += f2{gv, gv} * f2{u[t][v], u[t][v + 1]};
+          acc[t][v] = a2.x;
+          acc[t][v + 1] = a2.y;
+        }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      if (fvalid && row < JD) {
+        f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v;
+      }
+    }
+}
 
 }  // namespace
 
@@ -680,8 +872,8 @@ static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipS
   }
 }
 
-int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
-               int J, int dout, int mask_first, const float* vc, hipStream_t st) {
+static Args32 make_args32(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
+                          int J, int dout, int mask_first) {
   const int in_n = N * (lpad + rpad + 1);
   const char* base = static_cast<const char*>(ws);
   Args32 a;
@@ -705,9 +897,26 @@ int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int
   a.chunk_len = p.chunk_len;
   a.mask_first = mask_first;
   a.n_tgroups = p.NW;
-  a.vc = vc;
+  a.vc = nullptr;
   a.bsum = reinterpret_cast<const float*>(base + p.ws_w + p.ws_b + p.ws_x);
   a.slab = fwd32_slab(p, const_cast<void*>(ws));
+  a.cst = nullptr;
+  a.lzst = nullptr;
+  a.JP = p.JDp / dout;
+  return a;
+}
+
+size_t fwd32_coupling_floats(const Fwd32Plan& p, int F, int in_n, int dout, int iters) {
+  if (iters < 2) return 0;
+  return (size_t)(iters - 1) * F * in_n * (p.JDp / dout + 1);
+}
+
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
+               int J, int dout, int mask_first, const float* vc, float* cst, float* lzst, hipStream_t st) {
+  Args32 a = make_args32(p, ws, B, T, N, din, lpad, rpad, J, dout, mask_first);
+  a.vc = vc;
+  a.cst = first ? nullptr : cst;
+  a.lzst = first ? nullptr : lzst;
   SRF_REQUIRE(3 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
 #define SRF_P32(DI, DO) \
   if (din == DI && dout == DO) return launch_pass32_t<DI, DO>(p, first, a, st);
@@ -718,6 +927,44 @@ int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int
   SRF_P32(16, 32)
 #undef SRF_P32
   srf::set_error("fwd32: unsupported din %d dout %d", din, dout);
+  return SRF_EUNSUPPORTED;
+}
+
+template <int DIN, int DOUT, int NW>
+static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b, hipStream_t st) {
+  const size_t lds = fwd32_lds(p);
+  auto kern = route_bwd32_kernel<DIN, DOUT, NW>;
+  if (lds > 64 * 1024)
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a, b);
+  SRF_LAUNCH_CHECK("route_bwd32");
+  return SRF_OK;
+}
+
+template <int DIN, int DOUT>
+static int launch_bpass_t(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b, hipStream_t st) {
+  switch (p.NW) {
+    case 1: return launch_bpass<DIN, DOUT, 1>(p, a, b, st);
+    case 2: return launch_bpass<DIN, DOUT, 2>(p, a, b, st);
+    case 4: return launch_bpass<DIN, DOUT, 4>(p, a, b, st);
+    case 8: return launch_bpass<DIN, DOUT, 8>(p, a, b, st);
+    default: return launch_bpass<DIN, DOUT, kMaxNW>(p, a, b, st);
+  }
+}
+
+int bwd32_pass(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad, int J,
+               int dout, const float* cst, const float* lz, const float* gs, float* stats, hipStream_t st) {
+  Args32 a = make_args32(p, ws, B, T, N, din, lpad, rpad, J, dout, 0);
+  Bwd32Args b{cst, lz, gs, stats};
+#define SRF_B32(DI, DO) \
+  if (din == DI && dout == DO) return launch_bpass_t<DI, DO>(p, a, b, st);
+  SRF_B32(8, 8)
+  SRF_B32(8, 16)
+  SRF_B32(8, 32)
+  SRF_B32(16, 16)
+  SRF_B32(16, 32)
+#undef SRF_B32
+  srf::set_error("bwd32: unsupported din %d dout %d", din, dout);
   return SRF_EUNSUPPORTED;
 }
 

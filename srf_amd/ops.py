@@ -1,5 +1,7 @@
 """torch.autograd wrappers around the C ABI (device memory from torch's caching
 allocator, launches on torch's current HIP stream)."""
+import os
+
 import torch
 
 from . import _lib
@@ -93,7 +95,7 @@ class DynamicRouting(torch.autograd.Function):
     emb [B,T,N,din] -> v [B,T,J,dout] (the last iteration's squashed capsules)."""
 
     @staticmethod
-    def forward(ctx, emb, W, bias, geom):
+    def forward(ctx, emb, W, bias, geom, need_bwd=True):
         g = geom
         _check_dev('emb', emb, (g.B, g.T, g.N, g.din))
         _check_dev('W', W, (g.in_n, g.J, g.dout, g.din))
@@ -110,11 +112,18 @@ class DynamicRouting(torch.autograd.Function):
             _lib.check(L.srf_route_dr_set_timing_events(starts, stops, n), 'set_timing_events')
             if not g.timing:
                 g.timing = None
-        rc = L.srf_route_dr_fwd(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(v), _ptr(saved), _ptr(ws),
-                                ws_bytes, _stream())
-        _lib.check(rc, 'srf_route_dr_fwd')
+        # couplings of iterations r >= 1 for the backward (training only: a forward
+        # under no_grad or on non-trainable inputs stores nothing; grad mode is off
+        # inside Function.forward, so the caller decides, see dynamic_routing)
+        nc = L.srf_route_dr_coupling_floats(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, g.iters) \
+            if need_bwd and os.environ.get('SRF_ROUTE_COUPLINGS', '1') != '0' else 0
+        cpl = torch.empty(nc, device=dev, dtype=torch.float32) if nc else None
+        rc = L.srf_route_dr_fwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(v), _ptr(saved),
+                                   _ptr(cpl) if cpl is not None else None, _ptr(ws), ws_bytes, _stream())
+        _lib.check(rc, 'srf_route_dr_fwd_ex')
         ctx.geom = g
         ctx.params = (W, bias)
+        ctx.couplings = cpl
         ctx.save_for_backward(emb, W, bias, saved)
         return v
 
@@ -129,14 +138,17 @@ class DynamicRouting(torch.autograd.Function):
         g_W, g_b = tW[0], tb[0]
         ws_bytes = L.srf_route_dr_bwd_workspace(*g.ws_args())
         ws = torch.empty(ws_bytes, device=emb.device, dtype=torch.uint8)
+        cpl = ctx.couplings
+        ctx.couplings = None
+        cp = _ptr(cpl) if cpl is not None else None
         if not g.side_stream:
-            rc = L.srf_route_dr_bwd(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), _ptr(g_v), _ptr(g_emb),
-                                    _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
-            _lib.check(rc, 'srf_route_dr_bwd')
-            return (g_emb, *_returned([tW, tb]), None)
-        rc = L.srf_route_dr_bwd_data(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), _ptr(g_v),
-                                     _ptr(g_emb), _ptr(ws), ws_bytes, _stream())
-        _lib.check(rc, 'srf_route_dr_bwd_data')
+            rc = L.srf_route_dr_bwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
+                                       _ptr(g_emb), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
+            _lib.check(rc, 'srf_route_dr_bwd_ex')
+            return (g_emb, *_returned([tW, tb]), None, None)
+        rc = L.srf_route_dr_bwd_data_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
+                                        _ptr(g_emb), _ptr(ws), ws_bytes, _stream())
+        _lib.check(rc, 'srf_route_dr_bwd_data_ex')
         side = _weight_stream(emb.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -146,11 +158,12 @@ class DynamicRouting(torch.autograd.Function):
         for t in (ws, emb, g_W, g_b):
             t.record_stream(side)
         _pending_joins.append(side)
-        return (g_emb, *_returned([tW, tb]), None)
+        return (g_emb, *_returned([tW, tb]), None, None)
 
 
 def dynamic_routing(emb, W, bias, geom):
-    return DynamicRouting.apply(emb, W, bias, geom)
+    need_bwd = torch.is_grad_enabled() and (emb.requires_grad or W.requires_grad or bias.requires_grad)
+    return DynamicRouting.apply(emb, W, bias, geom, need_bwd)
 
 
 class SequentialRouting(torch.autograd.Function):

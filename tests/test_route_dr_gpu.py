@@ -107,3 +107,22 @@ def test_route_dr_fwd32_matches_fp32_mfma_path(cuda, case, monkeypatch):
     a = v32.detach().cpu().double().numpy()
     b = v16.detach().cpu().double().numpy()
     assert np.all(np.abs(a - b) <= 1e-5 * (1 + np.abs(b))), np.abs(a - b).max()
+
+
+@pytest.mark.parametrize('case', [(3, 37, 8, 16, 4, 4, 63, 3, True), (2, 19, 8, 16, 4, 4, 8, 3, False),
+                                  (2, 21, 4, 8, 2, 1, 12, 3, False), (2, 7, 4, 8, 1, 1, 6, 5, False)])
+def test_route_dr_backward_from_stored_couplings(cuda, case, monkeypatch):
+    """The backward routing passes that read the forward's stored couplings
+    (route_bwd32_kernel) against the ones that recompute the logits
+    (route_pass_kernel, SRF_ROUTE_COUPLINGS=0): same gradients to fp32 accuracy."""
+    emb, W, bias = _mk(case, 6)
+    gv = torch.tensor(np.random.default_rng(7).standard_normal(case[:2] + (case[6], case[3])), dtype=torch.float32,
+                      device=cuda)
+    grads = []
+    for flag in ('1', '0'):
+        monkeypatch.setenv('SRF_ROUTE_COUPLINGS', flag)
+        te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
+        v.backward(gv)
+        grads.append([t.grad.detach().cpu().double().numpy() for t in (te, tW, tb)])
+    for a, b, name in zip(grads[0], grads[1], ('g_emb', 'g_W', 'g_bias')):
+        assert np.abs(a - b).max() <= 2e-5 * max(1.0, np.abs(b).max()), (name, np.abs(a - b).max())
