@@ -59,6 +59,11 @@ int srf_route_dr_bwd_ex(const float* emb, const float* W, const float* bias, int
                         int rpad, int J, int dout, int iters, int mask_first, int n_chunks, const float* saved,
                         const float* couplings, const float* g_v, float* g_emb, float* g_W, float* g_bias,
                         void* workspace, size_t workspace_bytes, void* stream);
+/* _bwd_weights of a backward whose _bwd_data_ex was given couplings: the same
+ * saved and couplings buffers. */
+int srf_route_dr_bwd_weights_ex(const float* emb, int B, int T, int N, int din, int lpad, int rpad, int J, int dout,
+                                int iters, int mask_first, int n_chunks, const float* saved, const float* couplings,
+                                float* g_W, float* g_bias, void* workspace, size_t workspace_bytes, void* stream);
 int srf_route_dr_bwd_data_ex(const float* emb, const float* W, const float* bias, int B, int T, int N, int din,
                              int lpad, int rpad, int J, int dout, int iters, int mask_first, int n_chunks,
                              const float* saved, const float* couplings, const float* g_v, float* g_emb,

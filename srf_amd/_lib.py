@@ -30,6 +30,7 @@ _SIGNATURES = {
     'srf_route_dr_fwd_ex': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp, _vp, _vp, _vp, _c_size, _vp]),
     'srf_route_dr_bwd_ex': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp] * 7 + [_c_size, _vp]),
     'srf_route_dr_bwd_data_ex': (_c_int, [_vp, _vp, _vp] + [_c_int] * 11 + [_vp] * 5 + [_c_size, _vp]),
+    'srf_route_dr_bwd_weights_ex': (_c_int, [_vp] + [_c_int] * 11 + [_vp] * 5 + [_c_size, _vp]),
     'srf_route_sdr_saved_floats': (_c_size, [_c_int] * 4),
     'srf_route_sdr_fwd_workspace': (_c_size, [_c_int] * 8),
     'srf_route_sdr_bwd_workspace': (_c_size, [_c_int] * 9),

@@ -458,13 +458,17 @@ __global__ void bias_chunk_sum_kernel(const float* __restrict__ bias, int in_n, 
 //     the workgroup's output frames (ds_add, no barrier per capsule);
 // the accumulator is flushed into g_emb with one atomic add per element at the end.
 // When the accumulator does not fit in LDS (wide windows) the adds go to g_emb.
-template <int DIN, int DOUT, int TW, int R, bool LDSACC>
+// CPL: the couplings c^r and logit gradients gL^r of the 32x32 passes are given
+// (cst, glst: [r-1][in_n][JP][Fs], frame-minor), so gu needs
+// neither the pose nor any logit: gu_ij = c^0 gs^0_j + sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j.
+template <int DIN, int DOUT, int TW, int R, bool LDSACC, bool CPL = false>
 __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
     const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ WT,
     const float* __restrict__ bias, int F, int Fp, int T, int N, int lpad, int rpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
     const float* __restrict__ gs, const float* __restrict__ stats, float* __restrict__ gu_t,
-    float* __restrict__ g_emb, int nslots_max) {
+    float* __restrict__ g_emb, int nslots_max, const float* __restrict__ cst = nullptr,
+    const float* __restrict__ glst = nullptr, int JP = 0) {
   constexpr int NCT = (DIN + 15) / 16;
   constexpr int RV = R > 1 ? R - 1 : 1;
   extern __shared__ __attribute__((aligned(16))) float gacc[];
@@ -523,32 +527,54 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
         wt[ct][t] = ld4(WT + ((size_t)i * DIN + e) * JD + min(tc * 16 + 4 * g, JD - 4));
       }
     }
+    if constexpr (!CPL) {
 #pragma unroll
-    for (int r = 1; r < R; ++r) {
-      const f2 st = *reinterpret_cast<const f2*>(stats + (((size_t)(r - 1) * F + (loc.valid ? f : 0)) * in_n + i) * 2);
-      logz[r - 1] = st.x;
-      sig[r - 1] = st.y;
+      for (int r = 1; r < R; ++r) {
+        const f2 st = *reinterpret_cast<const f2*>(stats + (((size_t)(r - 1) * F + (loc.valid ? f : 0)) * in_n + i) * 2);
+        logz[r - 1] = st.x;
+        sig[r - 1] = st.y;
+      }
     }
   };
 
+  // stored couplings / logit gradients: [r-1][in_n][JP][Fs], frame-minor
+  const int Fs = srf::fwd32_frame_stride(F);
+  int cpos[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) cpos[t] = min(tile_j<DOUT>(tbase + t, g), J - 1);
+  const size_t cblk = (size_t)in_n * JP * Fs;
   if (ncap > 0) {
     Frags<DIN, TW> fr;
     f4 wt[NCT][TW];
     float logz[RV], sig[RV];
-    fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, cap(0), JD, NT, tbase, lane, fr);
+    if constexpr (!CPL) fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, cap(0), JD, NT, tbase, lane, fr);
     for (int k = 0; k < ncap; ++k) {
       const int i = cap(k);
       fetch_side(i, wt, logz, sig);
-      float u[TW][4];
-      pose_tiles<DIN, TW>(fr, u);
-      // operands of the next capsule are fetched now and land while this one is processed
-      const int inext = cap(min(k + 1, ncap - 1));
-      fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
       float ga[TW][4];
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
         for (int k = 0; k < 4; ++k) ga[t][k] = c0[t] * gsr[0][t][k];
+      if constexpr (CPL) {
+        const size_t fi = (size_t)i * JP * Fs + (loc.valid ? f : 0);
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+#pragma unroll
+          for (int t = 0; t < TW; ++t) {
+            const size_t o = (size_t)(r - 1) * cblk + fi + (size_t)cpos[t] * Fs;
+            const float c = cst[o];
+            const float gl = glst[o];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ga[t][k] += c * gsr[r][t][k] + gl * vcr[r - 1][t][k];
+          }
+      }
+      if constexpr (!CPL) {
+      float u[TW][4];
+      pose_tiles<DIN, TW>(fr, u);
+      // operands of the next capsule are fetched now and land while this one is processed
+      const int inext = cap(min(k + 1, ncap - 1));
+      fetch_frags<DIN, TW>(emb, W, bias, loc, T, N, lpad, inext, JD, NT, tbase, lane, fr);
 #pragma unroll
       for (int r = 1; r < R; ++r) {
         float p[TW], q[TW];
@@ -573,8 +599,10 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
           for (int k = 0; k < 4; ++k) ga[t][k] += c * gsr[r][t][k] + gl * vcr[r - 1][t][k];
         }
       }
-      // gu blocks (rows past JD and frames past F carry 0)
-      {
+      }
+      // gu blocks (rows past JD and frames past F carry 0); with stored scalars the
+      // gW pass (route_gw2_kernel) forms gu itself and nothing is stored
+      if constexpr (!CPL) {
         float* blk = gu_t + (((size_t)i * (Fp >> 4) + ft) * NT) * 256 + fl * 16 + 4 * g;
 #pragma unroll
         for (int t = 0; t < TW; ++t)
@@ -743,6 +771,204 @@ __global__ __launch_bounds__(256) void route_gw_kernel(const float* __restrict__
       }
     }
   }
+}
+
+
+// ---------------------------------------------------------------- gW from stored scalars
+// gW^T_i[e][row] = sum_f x_i^T[e][f] gu_i[f][row], with gu formed on the fly (never
+// stored) from the per-frame vectors and the stored per-(i, j, f) scalars:
+//   gu_fij = c^0_j gs^0_fj + sum_{r>=1} c^r_ijf gs^r_fj + gL^r_ijf Vc^r_fj.
+// v_mfma_f32_16x16x4_f32 with K = frames: lane (row = l & 15, kk = l >> 4) builds gu
+// for frames 4kk + v (v = 0..3, MFMA v) of its wave's 16-row tile; A = x^T.
+// A workgroup = 4 waves (4 row tiles) x GCAP capsules x one of S frame splits; its
+// gW / gbias sums stay in registers over the frame range.  Per 16-frame tile the
+// workgroup stages the capsules' couplings, logit gradients and transposed window
+// (xT) in LDS, one tile ahead (global loads of tile t+1 in flight during tile t),
+// and each lane prefetches its per-frame vectors one tile ahead.  Partials: S slabs
+// of [in_n][JD][D] (gW) + [in_n][JD] (gbias), or the gradients when S = 1.
+template <int D>
+constexpr int gw2_cap() { return D <= 16 ? 8 : (D == 32 ? 4 : 2); }
+template <int D>
+constexpr int gw2_jw() { return D >= 64 ? 1 : 64 / D; }   // capsules j per workgroup row group
+template <int D, int R>
+constexpr int gw2_stage_floats() {
+  return gw2_cap<D>() * ((R > 1 ? R - 1 : 1) * 2 * gw2_jw<D>() * 16 + D * 16);
+}
+
+template <int D, int R>
+__global__ __launch_bounds__(256) void route_gw2_kernel(
+    const float* __restrict__ xT, const float* __restrict__ saved, const float* __restrict__ gs,
+    const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp, int in_n, int J, int mask_first,
+    int JP, int n_rt, int n_cc, int S, int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride) {
+  constexpr int NCT = (D + 15) / 16;
+  constexpr int CAP = gw2_cap<D>();
+  constexpr int RV = R > 1 ? R - 1 : 1;
+  constexpr int JW = gw2_jw<D>();
+  constexpr int CG = RV * 2 * JW * 16;             // per capsule: [r][c|gl][jw][16 frames]
+  constexpr int SF = gw2_stage_floats<D, R>();     // per buffer: CAP x (CG + D x 16)
+  constexpr int NQ = (SF / 4 + 255) / 256;         // float4 staging loads per thread
+  __shared__ __attribute__((aligned(16))) float stg[2][SF];
+  const int JD = J * D;
+  const int NT = (JD + 15) / 16;
+  const size_t FJD = (size_t)F * JD;
+  const int Fs = srf::fwd32_frame_stride(F);
+  const size_t cblk = (size_t)in_n * JP * Fs;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l16 = lane & 15, kk = lane >> 4;
+  int b = blockIdx.x;
+  const int s = b % S;
+  b /= S;
+  const int rtg = b % n_rt;
+  const int cc = b / n_rt;
+  const int tg = rtg * 4 + wv;                     // this wave's 16-row tile
+  const int row = min(tg * 16 + l16, JD - 1);
+  const bool rvalid = tg < NT && tg * 16 + l16 < JD;
+  const int j = row / D;
+  const int jg0 = (rtg * 64) / D;                  // first capsule j of the row group
+  const int jl = min(j - jg0, JW - 1);
+  const int Jeff = J - (mask_first ? 1 : 0);
+  const float c0 = (rvalid && j < J && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+  const int i0 = cc * CAP, ncap = min(in_n, i0 + CAP) - i0;
+  const int NFT = Fp >> 4;
+  const int ft0 = s * ft_per, ft1 = min(NFT, ft0 + ft_per);
+
+  // staging: float4 q of the buffer <-> (capsule k, part) with parts
+  //   [0, CG/4): couplings/logit gradients (r, c|gl, jw, frame quad)
+  //   [CG/4, CG/4 + 4D): xT (e, frame quad)
+  f4 sv[NQ];
+  auto stage_load = [&](int ft) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int idx = q * 256 + threadIdx.x;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (idx < SF / 4) {
+        const int k = idx / (CG / 4 + 4 * D), rem = idx - k * (CG / 4 + 4 * D);
+        const int i = i0 + min(k, ncap - 1);
+        if (rem < CG / 4) {
+          const int fq = rem & 3, jw = (rem >> 2) % JW, cg = (rem >> 2) / JW;   // cg = r * 2 + (0: c, 1: gL)
+          const int r = cg >> 1;
+          const int jj = min(jg0 + jw, JP - 1);
+          const int f = ft * 16 + 4 * fq;
+          const float* src = (cg & 1) ? glst : cst;
+          if (R > 1 && f < F) v = ld4(src + (size_t)r * cblk + ((size_t)i * JP + jj) * Fs + f);
+          if (f + 4 > F) {   // frames past F hold no stored scalars
+            if (f + 0 >= F) v.x = 0.f;
+            if (f + 1 >= F) v.y = 0.f;
+            if (f + 2 >= F) v.z = 0.f;
+            if (f + 3 >= F) v.w = 0.f;
+          }
+        } else {
+          const int x = rem - CG / 4, e = x >> 2, fq = x & 3;
+          v = ld4(xT + ((size_t)i * D + e) * Fp + ft * 16 + 4 * fq);
+        }
+        if (k >= ncap) v = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      sv[q] = v;
+    }
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int idx = q * 256 + threadIdx.x;
+      if (idx < SF / 4) st4(&stg[buf][idx * 4], sv[q]);
+    }
+  };
+  float g0[4], gr[RV][4], vr[RV][4];
+  float n0[4], nr[RV][4], nvr[RV][4];
+  auto vec_load = [&](int ft) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int f = ft * 16 + 4 * kk + v;
+      const bool ok = rvalid && f < F;
+      const size_t o = (size_t)(ok ? f : 0) * JD + row;
+      n0[v] = ok ? gs[o] : 0.f;
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        nr[r - 1][v] = ok ? gs[(size_t)r * FJD + o] : 0.f;
+        nvr[r - 1][v] = ok ? saved[(size_t)(2 * (r - 1) + 1) * FJD + o] : 0.f;
+      }
+    }
+  };
+
+  f4 acc[CAP][NCT];
+  float gb[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    gb[k] = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[k][ct] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (ft0 < ft1) {
+    stage_load(ft0);
+    vec_load(ft0);
+    stage_store(0);
+  }
+  for (int ft = ft0; ft < ft1; ++ft) {
+    const int buf = (ft - ft0) & 1;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      g0[v] = n0[v];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) gr[r][v] = nr[r][v], vr[r][v] = nvr[r][v];
+    }
+    __syncthreads();   // buffer buf staged; the other buffer is free
+    const bool more = ft + 1 < ft1;
+    if (more) {
+      stage_load(ft + 1);
+      vec_load(ft + 1);
+    }
+    const float* sb = stg[buf];
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) {
+      const float* ck = sb + k * (CG + D * 16);
+      float gu[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) gu[v] = c0 * g0[v];
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        const f4 c = ld4(ck + (((r - 1) * 2 + 0) * JW + jl) * 16 + 4 * kk);
+        const f4 gl = ld4(ck + (((r - 1) * 2 + 1) * JW + jl) * 16 + 4 * kk);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) gu[v] += c[v] * gr[r - 1][v] + gl[v] * vr[r - 1][v];
+      }
+      gb[k] += (gu[0] + gu[1]) + (gu[2] + gu[3]);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const int e = ct * 16 + l16;
+        const f4 xa = e < D ? ld4(ck + CG + min(e, D - 1) * 16 + 4 * kk) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[k][ct] = mfma16x16x4(xa[v], gu[v], acc[k][ct]);
+      }
+    }
+    if (more) stage_store(buf ^ 1);
+  }
+  float* gw = gwp + (size_t)s * pstride;
+  float* gbo = gbp + (size_t)s * pstride;
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    if (k >= ncap) continue;
+    const int i = i0 + k;
+    const float t = xor32_sum(xor16_sum(gb[k]));
+    if (rvalid) {
+      if (kk == 0) gbo[(size_t)i * JD + row] = t;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        if (ct * 16 + 4 * kk < D) st4(gw + ((size_t)i * JD + row) * D + ct * 16 + 4 * kk, acc[k][ct]);
+    }
+  }
+}
+
+// gW | gbias = sum of the S partial slabs (float4 per thread).
+__global__ void gw_reduce_kernel(const float* __restrict__ part, int S, size_t n4, size_t stride, float* __restrict__ gW,
+                                 size_t nw4, float* __restrict__ gb) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n4) return;
+  f4 a = ld4(part + idx * 4);
+  for (int s = 1; s < S; ++s) a += ld4(part + (size_t)s * stride + idx * 4);
+  if (idx < nw4)
+    st4(gW + idx * 4, a);
+  else
+    st4(gb + (idx - nw4) * 4, a);
 }
 
 // ---------------------------------------------------------------- finish kernels
@@ -931,7 +1157,8 @@ int gu_n_per(const Geom& g, int nw) {
 
 template <int D, int R>
 void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
-               const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
+               const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st,
+               const float* cst, const float* glst, int JP) {
   const int n_ftiles = (g.F() + 15) / 16;
   const int n_wgroups = gu_wgroups(g);
   constexpr int TW = gu_tw(D);
@@ -940,26 +1167,91 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
   const int n_chunks = (g.N + n_per - 1) / n_per;
   const int nslots = 15 + gu_window(g);
   const size_t lds = gu_lds_bytes(g, nw, n_per);
-  if (lds <= kGuLdsMax)
+  if (lds <= kGuLdsMax && cst != nullptr)
+    hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, true, true>), dim3(n_ftiles * n_wgroups * n_chunks),
+                       dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots,
+                       cst, glst, JP);
+  else if (lds <= kGuLdsMax)
     hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, true>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
-                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots);
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots,
+                       nullptr, nullptr, 0);
   else
     hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, false>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), 0, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
-                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots);
+                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots,
+                       nullptr, nullptr, 0);
 }
 
 template <int D>
 void launch_gu_r(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
-                 const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st) {
+                 const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st,
+                 const float* cst = nullptr, const float* glst = nullptr, int JP = 0) {
   switch (g.iters) {
-    case 1: launch_gu<D, 1>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    case 2: launch_gu<D, 2>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    case 3: launch_gu<D, 3>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    case 4: launch_gu<D, 4>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
-    default: launch_gu<D, 5>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st); break;
+    case 1: launch_gu<D, 1>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, nullptr, nullptr, 0); break;
+    case 2: launch_gu<D, 2>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
+    case 3: launch_gu<D, 3>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
+    case 4: launch_gu<D, 4>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
+    default: launch_gu<D, 5>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
   }
+}
+
+
+// gW-from-scalars plan: capsule chunk, frame splits.  SRF_GW2_SPLITS forces S.
+struct Gw2Plan {
+  int cap, n_rt, n_cc, S, ft_per;
+  size_t pstride;
+};
+
+inline int gw2_cap_rt(int d) { return d <= 16 ? 8 : (d == 32 ? 4 : 2); }
+
+Gw2Plan gw2_plan(const Geom& g) {
+  Gw2Plan p{};
+  const int NT = g.NT();
+  const int NCT = (g.din + 15) / 16;
+  p.n_rt = (NT + 3) / 4;
+  p.cap = gw2_cap_rt(g.din);
+  p.n_cc = (g.in_n() + p.cap - 1) / p.cap;
+  const int NFT = padded_frames(g) / 16;
+  p.pstride = (size_t)g.in_n() * g.JD() * (g.din + 1);
+  const char* fs = getenv("SRF_GW2_SPLITS");
+  const int forced = fs ? atoi(fs) : 0;
+  const int base = p.n_rt * p.n_cc;
+  double best = 1e30;
+  for (int S0 = 1; S0 <= NFT; ++S0) {
+    if (forced > 0 && S0 != std::min(forced, NFT)) continue;
+    const int ft_per = (NFT + S0 - 1) / S0;
+    const int S = (NFT + ft_per - 1) / ft_per;
+    const int rounds = (base * S + 767) / 768;   // ~3 workgroups per CU
+    const double work = (double)rounds * ft_per * p.cap * NCT * 200.0 / 2.4e9;
+    const double slab = S > 1 ? 2.0 * S * p.pstride * 4 / 4e12 : 0.0;
+    if (work + slab < best) {
+      best = work + slab;
+      p.S = S;
+      p.ft_per = ft_per;
+    }
+  }
+  return p;
+}
+
+template <int D>
+int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* saved, const float* gs,
+               const float* cst, const float* glst, int JP, float* gwp, float* gbp, hipStream_t st) {
+  const int grid = p.n_rt * p.n_cc * p.S;
+#define SRF_GW2(R_)                                                                                              \
+  hipLaunchKernelGGL((route_gw2_kernel<D, R_>), dim3(grid), dim3(256), 0, st, xT, saved, gs, cst, glst, g.F(),    \
+                     padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.n_cc, p.S, p.ft_per, gwp, gbp,   \
+                     p.pstride)
+  switch (g.iters) {
+    case 2: SRF_GW2(2); break;
+    case 3: SRF_GW2(3); break;
+    case 4: SRF_GW2(4); break;
+    default: SRF_GW2(5); break;
+  }
+#undef SRF_GW2
+  SRF_LAUNCH_CHECK("route_gw2");
+  return SRF_OK;
 }
 
 // The 32x32 split-bf16 pass (route_fwd32.hip) serves the shapes it supports;
@@ -999,7 +1291,7 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     if (p32) {
       float *cst = nullptr, *lzst = nullptr;
       if (couplings != nullptr && r > 0) {
-        const size_t blk = (size_t)g.F() * g.in_n();
+        const size_t blk = (size_t)srf::fwd32_frame_stride(g.F()) * g.in_n();
         cst = couplings + (size_t)(r - 1) * blk * (plan.JDp / g.dout);
         lzst = couplings + (size_t)(g.iters - 1) * blk * (plan.JDp / g.dout) + (size_t)(r - 1) * blk;
       }
@@ -1022,6 +1314,8 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
 struct BwdWs {
   float *A, *gs, *slab, *stats, *gu_t, *xT, *WT;
   void* p32;          // split-bf16 operand planes + slab of the B1 passes from stored couplings
+  float* gl;          // gL^r of those passes [iters-1][in_n][JP][Fs], read by the gu / gW passes
+  float* gwpart;      // partial gW | gbias slabs of route_gw2_kernel (S frame splits)
   size_t bytes;
 };
 
@@ -1036,10 +1330,13 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   const size_t oA = take(F * JD), ogs = take((size_t)g.iters * F * JD), oslab = take((size_t)n_chunks * F * JD),
                ostats = take((size_t)(g.iters - 1) * F * in_n * 2), ogu = take(in_n * (size_t)g.NT() * 16 * Fp),
                oxt = take(in_n * g.din * Fp), owt = take(in_n * JD * g.din);
-  size_t op32 = 0;
+  size_t op32 = 0, ogl = 0, ogwp = 0;
   if (use_fwd32(g)) {
     const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
     op32 = take((srf::fwd32_workspace(plan) + 3) / 4);
+    ogl = take((size_t)std::max(g.iters - 1, 1) * srf::fwd32_frame_stride(g.F()) * in_n * (plan.JDp / g.dout));
+    const Gw2Plan gp = gw2_plan(g);
+    ogwp = take(gp.S * gp.pstride);
   }
   char* b = static_cast<char*>(base);
   BwdWs w;
@@ -1051,6 +1348,8 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   w.xT = (float*)(b + oxt);
   w.WT = (float*)(b + owt);
   w.p32 = op32 ? (void*)(b + op32) : nullptr;
+  w.gl = ogl ? (float*)(b + ogl) : nullptr;
+  w.gwpart = ogwp ? (float*)(b + ogwp) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -1059,8 +1358,28 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
 // nothing else of the backward, so a caller may run it on a second stream (after the
 // data pass, joined before g_W / g_bias or the workspace are used again).
 template <int D>
-int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st) {
+int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st,
+                     const float* saved = nullptr, const float* couplings = nullptr) {
   const int Fp = padded_frames(g);
+  if (couplings != nullptr && w.gl != nullptr && g.iters > 1) {
+    // gu formed from the stored couplings / logit gradients (never materialised)
+    const int tiles = (Fp + kXtFrames - 1) / kXtFrames;
+    hipLaunchKernelGGL(window_xt_kernel, dim3(g.in_n() * tiles), dim3(256), 0, st, emb, g.F(), Fp, g.T, g.N, g.din,
+                       g.lpad, g.in_n(), w.xT);
+    SRF_LAUNCH_CHECK("window_xt");
+    const Gw2Plan p = gw2_plan(g);
+    const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    const bool direct = p.S == 1;
+    float* gwp = direct ? g_W : w.gwpart;
+    float* gbp = direct ? g_bias : w.gwpart + (size_t)g.in_n() * g.JD() * g.din;
+    int rc = launch_gw2<D>(g, p, w.xT, saved, w.gs, couplings, w.gl, plan.JDp / g.dout, gwp, gbp, st);
+    if (rc || direct) return rc;
+    const size_t nw4 = (size_t)g.in_n() * g.JD() * g.din / 4, n4 = p.pstride / 4;
+    hipLaunchKernelGGL(gw_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, w.gwpart, p.S, n4, p.pstride, g_W,
+                       nw4, g_bias);
+    SRF_LAUNCH_CHECK("gw_reduce");
+    return SRF_OK;
+  }
   {
     SRF_REQUIRE(g.din <= 64, "window_xt tile holds din <= 64, got %d", g.din);
     const int tiles = (Fp + kXtFrames - 1) / kXtFrames;
@@ -1105,12 +1424,12 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     const float* vc = saved + (size_t)(2 * (r - 1) + 1) * FJD;
     float* stats_r = w.stats + (size_t)(r - 1) * g.F() * g.in_n() * 2;
     if (p32) {
-      const size_t blk = (size_t)g.F() * g.in_n();
+      const size_t blk = (size_t)srf::fwd32_frame_stride(g.F()) * g.in_n();
       const int JP = plan.JDp / g.dout;
       const int rc = srf::bwd32_pass(plan, w.p32, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout,
                                      couplings + (size_t)(r - 1) * blk * JP,
                                      couplings + (size_t)(R - 1) * blk * JP + (size_t)(r - 1) * blk,
-                                     w.gs + (size_t)r * FJD, stats_r, st);
+                                     w.gs + (size_t)r * FJD, stats_r, w.gl + (size_t)(r - 1) * blk * JP, st);
       if (rc) return rc;
       launch_bwd_finish<D>(g, srf::fwd32_slab(plan, w.p32), plan.n_chunks, nullptr, w.A,
                            saved + (size_t)(2 * (r - 1)) * FJD, w.gs + (size_t)(r - 1) * FJD, st);
@@ -1132,10 +1451,14 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
                        w.WT, g_emb, n_emb);
     SRF_LAUNCH_CHECK("transpose_w");
   }
-  launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
+  if (p32)
+    launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st, couplings, w.gl,
+                   plan.JDp / g.dout);
+  else
+    launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");
   (void)Fp;
-  return with_weights ? bwd_weights_impl<D>(g, emb, g_W, g_bias, w, st) : SRF_OK;
+  return with_weights ? bwd_weights_impl<D>(g, emb, g_W, g_bias, w, st, saved, p32 ? couplings : nullptr) : SRF_OK;
 }
 
 }  // namespace
@@ -1281,6 +1604,13 @@ int srf_route_dr_bwd_data_ex(const float* emb, const float* W, const float* bias
 int srf_route_dr_bwd_weights(const float* emb, int B, int T, int N, int din, int lpad, int rpad, int J, int dout,
                              int iters, int mask_first, int n_chunks, float* g_W, float* g_bias, void* workspace,
                              size_t workspace_bytes, void* stream) {
+  return srf_route_dr_bwd_weights_ex(emb, B, T, N, din, lpad, rpad, J, dout, iters, mask_first, n_chunks, nullptr,
+                                     nullptr, g_W, g_bias, workspace, workspace_bytes, stream);
+}
+
+int srf_route_dr_bwd_weights_ex(const float* emb, int B, int T, int N, int din, int lpad, int rpad, int J, int dout,
+                                int iters, int mask_first, int n_chunks, const float* saved, const float* couplings,
+                                float* g_W, float* g_bias, void* workspace, size_t workspace_bytes, void* stream) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, iters, mask_first ? 1 : 0};
   int rc = check_geom(g);
   if (rc) return rc;
@@ -1292,11 +1622,12 @@ int srf_route_dr_bwd_weights(const float* emb, int B, int T, int N, int din, int
     return SRF_EWORKSPACE;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (couplings != nullptr && (!use_fwd32(g) || iters < 2 || saved == nullptr)) couplings = nullptr;
   switch (din) {
-    case 8: return bwd_weights_impl<8>(g, emb, g_W, g_bias, w, st);
-    case 16: return bwd_weights_impl<16>(g, emb, g_W, g_bias, w, st);
-    case 32: return bwd_weights_impl<32>(g, emb, g_W, g_bias, w, st);
-    default: return bwd_weights_impl<64>(g, emb, g_W, g_bias, w, st);
+    case 8: return bwd_weights_impl<8>(g, emb, g_W, g_bias, w, st, saved, couplings);
+    case 16: return bwd_weights_impl<16>(g, emb, g_W, g_bias, w, st, saved, couplings);
+    case 32: return bwd_weights_impl<32>(g, emb, g_W, g_bias, w, st, saved, couplings);
+    default: return bwd_weights_impl<64>(g, emb, g_W, g_bias, w, st, saved, couplings);
   }
 }
 

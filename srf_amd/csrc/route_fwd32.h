@@ -6,6 +6,11 @@
 
 namespace srf {
 
+// Row tiles (of 32 rows) per wave of route_fwd32 / route_bwd32.
+constexpr int kFwd32TW = 4;
+// Frame stride of the stored couplings (frame-minor layout, 32-frame aligned).
+__host__ __device__ inline int fwd32_frame_stride(int F) { return (F + 31) / 32 * 32; }
+
 struct Fwd32Plan {
   int NW;              // waves per workgroup (TW = 4 row tiles of 32 each)
   int JDp;             // J*dout padded to NW*4*32 rows
@@ -26,12 +31,14 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
 // also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr
 int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
                int J, int dout, int mask_first, const float* vc, float* cst, float* lzst, hipStream_t st);
-// coupling storage of one forward: (iters - 1) blocks of c^r [F][in_n][JP] followed by
-// (iters - 1) blocks of logZ^r [F][in_n]; JP = JDp / dout
+// coupling storage of one forward: (iters - 1) blocks of c^r [in_n][JP][Fs] followed by
+// (iters - 1) blocks of logZ^r [in_n][Fs]; JP = JDp / dout, Fs = fwd32_frame_stride(F)
 size_t fwd32_coupling_floats(const Fwd32Plan& p, int F, int in_n, int dout, int iters);
 // one backward routing pass r >= 1 from the stored couplings: partial gVc^r over
-// i-chunks into fwd32_slab(p, ws) and the (logZ, sigma) stats of the gu pass
+// i-chunks into fwd32_slab(p, ws), the (logZ, sigma) stats and the logit
+// gradients gL^r (glst, laid out as the couplings) of the gu pass
 int bwd32_pass(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad, int J,
-               int dout, const float* cst, const float* lz, const float* gs, float* stats, hipStream_t st);
+               int dout, const float* cst, const float* lz, const float* gs, float* stats, float* glst,
+               hipStream_t st);
 
 }  // namespace srf

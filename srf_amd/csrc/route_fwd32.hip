@@ -166,6 +166,7 @@ __global__ void prep32_kernel(PrepArgs P) {
 #define SRF_FWD32_TW 4
 #endif
 constexpr int kTW = SRF_FWD32_TW;        // 32-row tiles per wave
+static_assert(kTW == srf::kFwd32TW, "stored-coupling layout (route_fwd32.h) assumes kFwd32TW row tiles per wave");
 constexpr int kMaxNW = 32 / kTW;         // J*dout <= 1024
 constexpr int kWavesPerEU = 8 / kTW;
 
@@ -276,20 +277,15 @@ struct Args32 {
   const float* vc;
   const float* bsum;
   float* slab;
-  // forward passes r >= 1: when cst != nullptr, the couplings c^r [F][in_n][JP]
-  // (each lane's owned capsules contiguous, see c_slot) and logZ^r [F][in_n] are
-  // stored for the backward (route_bwd32_kernel reads them instead of recomputing
-  // the logits)
+  // forward passes r >= 1: when cst != nullptr, the couplings c^r [in_n][JP][Fs]
+  // and logZ^r [in_n][Fs] (frame-minor: coalesced for every reader) are stored for
+  // the backward (route_bwd32_kernel reads them instead of recomputing the logits)
   float* cst;
   float* lzst;
-  int JP;
+  int JP, Fs;
 };
 
-// Position of a wave's owned capsule in the stored coupling row: lane half h owns
-// capsules j0 + 2a + h (a < OWN) after the logit reduce-scatter, stored at
-// j0 + h*OWN + a so that a lane's OWN values are one contiguous vector.
-template <int DOUT>
-__host__ __device__ constexpr int c_cp() { return kTW * 32 / DOUT; }
+
 
 // ------------------------------------------------------------------ kernels
 // Iteration-0 pass (naive:172-181: logits 0 + mask, so c is uniform):
@@ -537,15 +533,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       // c = exp(L - M) / Z = e * exp(m - M) / Z; then all-gather over the halves
       const float sc = __expf(m - M) / Z;
       if (A.cst != nullptr && fvalid) {
-        float* dst = A.cst + ((size_t)f * A.in_n + i) * A.JP + j0 + h * OWN;
-        if constexpr (OWN % 4 == 0) {
+        // lane half h owns capsules j0 + 2a + h after the logit reduce-scatter
+        float* dst = A.cst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
 #pragma unroll
-          for (int a = 0; a < OWN; a += 4)
-            *reinterpret_cast<f4*>(dst + a) = f4{e[a] * sc, e[a + 1] * sc, e[a + 2] * sc, e[a + 3] * sc};
-        } else {
-          *reinterpret_cast<f2*>(dst) = f2{e[0] * sc, e[1] * sc};
-        }
-        if (h == 0 && wv == 0) A.lzst[(size_t)f * A.in_n + i] = M + __logf(Z);
+        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = e[a] * sc;
+        if (h == 0 && wv == 0) A.lzst[(size_t)i * A.Fs + f] = M + __logf(Z);
       }
       float c[CP];
 #pragma unroll
@@ -596,24 +588,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 // gs^r rows live in each wave's private LDS slab in fragment order (as Vc in the
 // forward); sigma needs one cross-wave sum per input capsule (one barrier).
 struct Bwd32Args {
-  const float* cst;   // c^r [F][in_n][JP]
-  const float* lz;    // logZ^r [F][in_n]
+  const float* cst;   // c^r [in_n][JP][Fs]
+  const float* lz;    // logZ^r [in_n][Fs]
   const float* gs;    // gs^r [F][JD]
   float* stats;       // [F][in_n][2]
+  float* glst;        // gL^r [in_n][JP][Fs] (laid out as c^r), for the gu pass
 };
 
+// the owned couplings j0 + 2a + h of one capsule i (p points at capsule j0 + h, frame f)
 template <int OWN>
-__device__ __forceinline__ void load_c(const float* __restrict__ p, float (&c)[OWN]) {
-  if constexpr (OWN % 4 == 0) {
+__device__ __forceinline__ void load_c(const float* __restrict__ p, size_t fs, float (&c)[OWN]) {
 #pragma unroll
-    for (int a = 0; a < OWN; a += 4) {
-      const f4 v = *reinterpret_cast<const f4*>(p + a);
-      c[a] = v.x; c[a + 1] = v.y; c[a + 2] = v.z; c[a + 3] = v.w;
-    }
-  } else {
-    const f2 v = *reinterpret_cast<const f2*>(p);
-    c[0] = v.x; c[1] = v.y;
-  }
+  for (int a = 0; a < OWN; ++a) c[a] = p[2 * a * fs];
 }
 
 template <int DIN, int DOUT, int NW>
@@ -653,14 +639,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   f16v acc[TW];
 #pragma unroll
   for (int t = 0; t < TW; ++t) acc[t] = f16v{};
-  const float* crow = Bk.cst + (size_t)fc * A.in_n * A.JP + j0 + h * OWN;
+  const float* crow = Bk.cst + (size_t)(j0 + h) * A.Fs + fc;
+  const size_t cstep = (size_t)A.JP * A.Fs;   // next capsule i
   int par = 0;
   if (i0 < i1) {
     Frags32<DIN, TW> fr;
     float cn[OWN];
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                            A.wplane_b, A.xplane_b, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8, fr);
-    load_c<OWN>(crow + (size_t)i0 * A.JP, cn);
+    load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cn);
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
 #pragma unroll
@@ -714,19 +701,27 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
                                h, A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
-        load_c<OWN>(crow + (size_t)(i + 1) * A.JP, cn);
+        load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
       }
       __builtin_amdgcn_sched_barrier(0);
       if (wv == 0 && h == 0 && fvalid) {
         const size_t fi = (size_t)f * A.in_n + i;
-        *reinterpret_cast<f2*>(Bk.stats + fi * 2) = f2{Bk.lz[fi], S};
+        *reinterpret_cast<f2*>(Bk.stats + fi * 2) = f2{Bk.lz[(size_t)i * A.Fs + f], S};
       }
-      // gL of the owned capsules, then all-gather over the lane halves
+      // gL of the owned capsules (stored for the gu pass), then all-gather over the lane halves
+      float gown[OWN];
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) gown[a] = cc[a] * (Q[a] - S);
+      if (fvalid) {
+        float* dst = Bk.glst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
+#pragma unroll
+        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = gown[a];
+      }
       float g[CP];
 #pragma unroll
       for (int a = 0; a < OWN; ++a) {
         float g0, g1;
-        xpair32(cc[a] * (Q[a] - S), g0, g1);
+        xpair32(gown[a], g0, g1);
         g[2 * a] = g0;
         g[2 * a + 1] = g1;
       }
@@ -903,12 +898,13 @@ static Args32 make_args32(const Fwd32Plan& p, const void* ws, int B, int T, int 
   a.cst = nullptr;
   a.lzst = nullptr;
   a.JP = p.JDp / dout;
+  a.Fs = fwd32_frame_stride(B * T);
   return a;
 }
 
 size_t fwd32_coupling_floats(const Fwd32Plan& p, int F, int in_n, int dout, int iters) {
   if (iters < 2) return 0;
-  return (size_t)(iters - 1) * F * in_n * (p.JDp / dout + 1);
+  return (size_t)(iters - 1) * fwd32_frame_stride(F) * in_n * (p.JDp / dout + 1);
 }
 
 int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
@@ -953,9 +949,10 @@ static int launch_bpass_t(const Fwd32Plan& p, const Args32& a, const Bwd32Args& 
 }
 
 int bwd32_pass(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad, int J,
-               int dout, const float* cst, const float* lz, const float* gs, float* stats, hipStream_t st) {
+               int dout, const float* cst, const float* lz, const float* gs, float* stats, float* glst,
+               hipStream_t st) {
   Args32 a = make_args32(p, ws, B, T, N, din, lpad, rpad, J, dout, 0);
-  Bwd32Args b{cst, lz, gs, stats};
+  Bwd32Args b{cst, lz, gs, stats, glst};
 #define SRF_B32(DI, DO) \
   if (din == DI && dout == DO) return launch_bpass_t<DI, DO>(p, a, b, st);
   SRF_B32(8, 8)

@@ -152,10 +152,10 @@ class DynamicRouting(torch.autograd.Function):
         side = _weight_stream(emb.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            rc = L.srf_route_dr_bwd_weights(_ptr(emb), *g.args(), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes,
-                                            ctypes_void(side.cuda_stream))
-        _lib.check(rc, 'srf_route_dr_bwd_weights')
-        for t in (ws, emb, g_W, g_b):
+            rc = L.srf_route_dr_bwd_weights_ex(_ptr(emb), *g.args(), _ptr(saved), cp, _ptr(g_W), _ptr(g_b), _ptr(ws),
+                                               ws_bytes, ctypes_void(side.cuda_stream))
+        _lib.check(rc, 'srf_route_dr_bwd_weights_ex')
+        for t in (ws, emb, g_W, g_b, saved) + ((cpl,) if cpl is not None else ()):
             t.record_stream(side)
         _pending_joins.append(side)
         return (g_emb, *_returned([tW, tb]), None, None)
