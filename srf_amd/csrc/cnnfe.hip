@@ -18,6 +18,7 @@
 //   bn_apply     writes the CapsulationLayer output mask2(BN2(y2)).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "srf_common.h"
 #include "srf_reduce.h"
@@ -418,6 +419,245 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
     part[((size_t)blockIdx.x * 3 + 0) * C + c] = n;
     part[((size_t)blockIdx.x * 3 + 1) * C + c] = mean;
     part[((size_t)blockIdx.x * 3 + 2) * C + c] = m2;
+  }
+}
+
+
+// ---------------------------------------------------------------- conv2 (split-bf16 MFMA)
+// The same implicit GEMM on v_mfma_f32_32x32x16_bf16 with fp32-accurate 3-term
+// bf16 splits (a = a1 + a2 + a3; the six products >= 2^-18 |ab|, as the routing
+// pose, route_fwd32.hip): 16/6 of the fp32-MFMA rate.  Workgroup = 2 waves = 64
+// output pixels x 128 outputs; a wave owns 32 pixels x all 128 outputs (conv a
+// channels 0-31 / 32-63, conv b channels 0-31 / 32-63: the maxout pairs share a
+// lane).  Per k-block (one tap, 16 input channels) the A fragments are gathered
+// straight into registers (BN1 + mask1 + split on the VALU, one k-block ahead) and
+// the B fragments (packed, pre-split weights, shared by both waves) are staged in
+// LDS, double-buffered, one k-block ahead.  Epilogue as conv2_fwd_kernel.
+typedef __bf16 cbf8 __attribute__((ext_vector_type(8)));
+typedef float cf16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ cf16 mfma32bf(const cbf8& a, const cbf8& b, const cf16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void split8v(const float (&v)[8], cbf8& p1, cbf8& p2, cbf8& p3) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 a1 = (__bf16)v[k];
+    const float r = v[k] - (float)a1;
+    const __bf16 a2 = (__bf16)r;
+    p1[k] = a1;
+    p2[k] = a2;
+    p3[k] = (__bf16)(r - (float)a2);
+  }
+}
+
+// Packed split weights wp3[plane][tap][n][cin] (n = ab*C + cout), one thread per 8 cin.
+__global__ void pack_w2_split_kernel(const float* __restrict__ ka, const float* __restrict__ kb,
+                                     __bf16* __restrict__ wp3) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;   // (tap, n, cin/8)
+  if (idx >= 9 * 2 * C * (C / 8)) return;
+  const int c8 = idx % (C / 8), n = (idx / (C / 8)) % (2 * C), tap = idx / (2 * C * (C / 8));
+  const float* k = n < C ? ka : kb;
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = k[((size_t)tap * C + 8 * c8 + q) * C + (n % C)];
+  cbf8 p1, p2, p3;
+  split8v(v, p1, p2, p3);
+  const size_t plane = (size_t)9 * 2 * C * C;
+  const size_t o = ((size_t)tap * 2 * C + n) * C + 8 * c8;
+  *reinterpret_cast<cbf8*>(wp3 + o) = p1;
+  *reinterpret_cast<cbf8*>(wp3 + plane + o) = p2;
+  *reinterpret_cast<cbf8*>(wp3 + 2 * plane + o) = p3;
+}
+
+constexpr int kC2BStride = 24;   // bf16 per output row of an LDS B k-block (16 + 8: conflict-free b128 reads)
+constexpr int kC2Waves = 4;      // 32 pixels each: 128 pixels per workgroup
+constexpr int kC2Px = 32 * kC2Waves;
+constexpr int kC2BLoads = 3 * 2 * C * 2 / (64 * kC2Waves);   // 16-byte B loads per thread per k-block
+
+__global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2))) void conv2_fwd32_kernel(
+    const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len, Dims d,
+    const __bf16* __restrict__ wp3, const float* __restrict__ ba, const float* __restrict__ bb, int training,
+    float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ y2,
+    unsigned char* __restrict__ sel2, float* __restrict__ part) {
+  seed = srf_step_seed(seed, seed_src);
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][2 * C * kC2BStride];
+  __shared__ __attribute__((aligned(16))) float ss[2][C];
+  __shared__ float red[3][kC2Waves][2 * 32];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int P2 = d.B * d.T2 * d.F2;
+  const int p0 = blockIdx.x * kC2Px;
+  const size_t plane = (size_t)9 * 2 * C * C;
+  if (tid < 2 * C) ss[tid >> 6][tid & 63] = stats1[(2 + (tid >> 6)) * C + (tid & 63)];
+
+  // A row of this lane: pixel p0 + 32 wv + r
+  const int pa = p0 + 32 * wv + r;
+  const bool alive = pa < P2;
+  const int pc = min(pa, P2 - 1);
+  const int af2 = pc % d.F2, at2 = (pc / d.F2) % d.T2, ab = pc / (d.F2 * d.T2);
+  const int alen1 = ceil_div_len(inp_len[ab], 2);
+
+  // k-block kk = tap * 4 + kb: input channels [16 kb, 16 kb + 16)
+  auto load_b = [&](int kk, cbf8 (&bv)[kC2BLoads]) {
+    const int tap = kk >> 2, kb = kk & 3;
+#pragma unroll
+    for (int q = 0; q < kC2BLoads; ++q) {
+      const int idx = q * 64 * kC2Waves + tid;
+      const int pl = idx >> 8, rem = idx & 255, n = rem >> 1, half = rem & 1;
+      bv[q] = *reinterpret_cast<const cbf8*>(wp3 + pl * plane + ((size_t)tap * 2 * C + n) * C + 16 * kb + 8 * half);
+    }
+  };
+  auto store_b = [&](int buf, const cbf8 (&bv)[kC2BLoads]) {
+#pragma unroll
+    for (int q = 0; q < kC2BLoads; ++q) {
+      const int idx = q * 64 * kC2Waves + tid;
+      const int pl = idx >> 8, rem = idx & 255, n = rem >> 1, half = rem & 1;
+      *reinterpret_cast<cbf8*>(&Bs[buf][pl][n * kC2BStride + 8 * half]) = bv[q];
+    }
+  };
+  auto load_a = [&](int kk, f4 (&av)[2], bool& ok) {
+    const int tap = kk >> 2, kb = kk & 3;
+    const int dt = tap / 3, df = tap - dt * 3;
+    const int t1 = 2 * at2 - d.pt2 + dt, f1 = 2 * af2 - d.pf2 + df;
+    ok = alive && t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < alen1;
+    const int t1c = min(max(t1, 0), d.T1 - 1), f1c = min(max(f1, 0), d.F1 - 1);
+    const float* src = y1 + (((size_t)ab * d.T1 + t1c) * d.F1 + f1c) * C + 16 * kb + 8 * h;
+    av[0] = *reinterpret_cast<const f4*>(src);
+    av[1] = *reinterpret_cast<const f4*>(src + 4);
+  };
+
+  cf16 acc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) acc[nt] = cf16{};
+  // one k-block: A split from registers, B from LDS buffer buf, 24 MFMAs
+  auto compute = [&](int kk, int buf, const f4 (&av)[2], bool aok) {
+    cbf8 a1, a2, a3;
+    {
+      const int c0 = 16 * (kk & 3) + 8 * h;
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float x = q < 4 ? av[0][q] : av[1][q - 4];
+        v[q] = aok ? x * ss[0][c0 + q] + ss[1][c0 + q] : 0.f;
+      }
+      split8v(v, a1, a2, a3);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int nrow = (nt >> 1) * C + 32 * (nt & 1) + r;   // nt: 0/1 conv a, 2/3 conv b
+      const cbf8 b1 = *reinterpret_cast<const cbf8*>(&Bs[buf][0][nrow * kC2BStride + 8 * h]);
+      const cbf8 b2 = *reinterpret_cast<const cbf8*>(&Bs[buf][1][nrow * kC2BStride + 8 * h]);
+      const cbf8 b3 = *reinterpret_cast<const cbf8*>(&Bs[buf][2][nrow * kC2BStride + 8 * h]);
+      cf16 c = acc[nt];
+      c = mfma32bf(a3, b1, c);
+      c = mfma32bf(a1, b3, c);
+      c = mfma32bf(a2, b2, c);
+      c = mfma32bf(a2, b1, c);
+      c = mfma32bf(a1, b2, c);
+      c = mfma32bf(a1, b1, c);
+      acc[nt] = c;
+    }
+  };
+  // software pipeline, two k-blocks ahead: at k-block kk the registers hold the
+  // operands of kk + 1 (stored to LDS at the end of kk) and receive those of kk + 2
+  cbf8 bvA[kC2BLoads], bvB[kC2BLoads];
+  f4 avA[2], avB[2], avC[2];
+  bool okA, okB, okC;
+  load_b(0, bvA);
+  load_a(0, avA, okA);
+  load_b(1, bvB);
+  load_a(1, avB, okB);
+  store_b(0, bvA);
+  __syncthreads();
+  // kk even: A-set = kk, B-set = kk + 1; loads of kk + 2 go to the A registers
+  for (int kk = 0; kk < 36; kk += 2) {
+    // even step kk
+    {
+      const f4 a0[2] = {avA[0], avA[1]};
+      const bool ok0 = okA;
+      if (kk + 2 < 36) {
+        load_b(kk + 2, bvA);
+        load_a(kk + 2, avA, okA);
+      }
+      compute(kk, 0, a0, ok0);
+      store_b(1, bvB);
+      __syncthreads();
+    }
+    // odd step kk + 1
+    {
+      const f4 a1v[2] = {avB[0], avB[1]};
+      const bool ok1 = okB;
+      if (kk + 3 < 36) {
+        load_b(kk + 3, bvB);
+        load_a(kk + 3, avB, okB);
+      }
+      compute(kk + 1, 1, a1v, ok1);
+      if (kk + 2 < 36) store_b(0, bvA);
+      __syncthreads();
+    }
+  }
+  (void)avC;
+  (void)okC;
+
+  // epilogue: lane column r = channel (32 g + r), rows = pixels 8q + 4h + v of the wave
+  const float keep_scale = 1.f / (1.f - drop_p);
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int c = 32 * g + r;
+    const float bia = ba[c], bib = bb[c];
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int p = p0 + 32 * wv + 8 * q + 4 * h + v;
+        if (p >= P2) continue;
+        const int t2 = (p / d.F2) % d.T2, b = p / (d.F2 * d.T2);
+        const size_t o = (size_t)p * C + c;
+        float a = acc[g][4 * q + v] + bia, bvv = acc[2 + g][4 * q + v] + bib;
+        if (training && drop_p > 0.f) {
+          a *= srf_keep(seed, kStreamConv1a, o, drop_p) ? keep_scale : 0.f;
+          bvv *= srf_keep(seed, kStreamConv1b, o, drop_p) ? keep_scale : 0.f;
+        }
+        const bool sel = a >= bvv;
+        float y = sel ? a : bvv;
+        if (t2 >= ceil_div_len(inp_len[b], 4)) y = 0.f;
+        y2[o] = y;
+        sel2[o] = sel ? 1 : 0;
+        n += 1.f;
+        const float delta = y - mean;
+        mean += delta / n;
+        m2 += delta * (y - mean);
+      }
+    // combine the two lane halves (same channel), then the waves through LDS
+    {
+      float nb, mb, qb, x;
+      xpair32(n, x, nb);
+      nb = h ? x : nb;
+      xpair32(mean, x, mb);
+      mb = h ? x : mb;
+      xpair32(m2, x, qb);
+      qb = h ? x : qb;
+      if (h == 0) chan_merge(n, mean, m2, nb, mb, qb);
+    }
+    if (h == 0) {
+      red[0][wv][g * 32 + r] = n;
+      red[1][wv][g * 32 + r] = mean;
+      red[2][wv][g * 32 + r] = m2;
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * 32) {
+    const int gc = tid;   // channel 0..63 (g * 32 + r)
+    float n = red[0][0][gc], mean = red[1][0][gc], m2 = red[2][0][gc];
+#pragma unroll
+    for (int w = 1; w < kC2Waves; ++w) chan_merge(n, mean, m2, red[0][w][gc], red[1][w][gc], red[2][w][gc]);
+    part[((size_t)blockIdx.x * 3 + 0) * C + gc] = n;
+    part[((size_t)blockIdx.x * 3 + 1) * C + gc] = mean;
+    part[((size_t)blockIdx.x * 3 + 2) * C + gc] = m2;
   }
 }
 
@@ -897,6 +1137,7 @@ int bn_finalize(const float* part, int nparts, float* merged, const float* gamma
 
 struct FwdWs {
   float *part1, *part2, *wp, *merged;
+  __bf16* wp3;   // split-bf16 packed stage-2 weights [3][tap][n][cin]
   size_t bytes;
 };
 
@@ -910,15 +1151,24 @@ FwdWs fwd_ws_layout(const Dims& d, void* base) {
     return o;
   };
   const size_t op1 = take((size_t)conv1_blocks(d) * 3 * C * 4), op2 = take(nb2 * 3 * C * 4),
-               owp = take((size_t)9 * 2 * C * C * 4), omg = take((size_t)kBnMerge * 3 * C * 4);
+               owp = take((size_t)9 * 2 * C * C * 4), omg = take((size_t)kBnMerge * 3 * C * 4),
+               owp3 = take((size_t)3 * 9 * 2 * C * C * 2);
   char* b = static_cast<char*>(base);
   FwdWs w;
+  w.wp3 = (__bf16*)(b + owp3);
   w.merged = (float*)(b + omg);
   w.part1 = (float*)(b + op1);
   w.part2 = (float*)(b + op2);
   w.wp = (float*)(b + owp);
   w.bytes = off;
   return w;
+}
+
+// The split-bf16 stage-2 kernels serve by default; SRF_CONV2_32=0 selects the
+// fp32-MFMA ones (A/B runs).
+inline bool use_conv2_32() {
+  const char* e = getenv("SRF_CONV2_32");
+  return !(e && e[0] == '0');
 }
 
 int check_dims(int B, int T, int Fin, int nfilt) {
@@ -972,18 +1222,31 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t P2 = (size_t)d.B * d.T2 * d.F2;
   const int nb2 = (int)((P2 + 63) / 64);
+  int nparts2 = nb2;
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, k0a, b0a, k0b, b0b,
                      training, drop_p, seed, srf::seed_source(), sv.y1, sv.sel1, w.part1);
   SRF_LAUNCH_CHECK("conv1_fwd");
   if ((rc = bn_finalize(w.part1, conv1_blocks(d), w.merged, gamma0, beta0, mmean0, mvar0, training, sv.stats1, st)))
     return rc;
   SRF_LAUNCH_CHECK("bn_finalize(1)");
-  hipLaunchKernelGGL(pack_w2_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wp);
-  SRF_LAUNCH_CHECK("pack_w2");
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(nb2), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, d, w.wp, b1a, b1b,
-                     training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2, w.part2);
-  SRF_LAUNCH_CHECK("conv2_fwd");
-  if ((rc = bn_finalize(w.part2, nb2, w.merged, gamma1, beta1, mmean1, mvar1, training, sv.stats2, st))) return rc;
+  if (use_conv2_32()) {
+    hipLaunchKernelGGL(pack_w2_split_kernel, dim3((9 * 2 * C * (C / 8) + 255) / 256), dim3(256), 0, st, k1a, k1b,
+                       w.wp3);
+    SRF_LAUNCH_CHECK("pack_w2_split");
+    const int nb32 = (int)((P2 + kC2Px - 1) / kC2Px);
+    hipLaunchKernelGGL(conv2_fwd32_kernel, dim3(nb32), dim3(64 * kC2Waves), 0, st, sv.y1, sv.stats1, inp_len, d,
+                       w.wp3, b1a, b1b, training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2, w.part2);
+    SRF_LAUNCH_CHECK("conv2_fwd32");
+    nparts2 = nb32;
+  } else {
+    hipLaunchKernelGGL(pack_w2_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wp);
+    SRF_LAUNCH_CHECK("pack_w2");
+    hipLaunchKernelGGL(conv2_fwd_kernel, dim3(nb2), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, d, w.wp, b1a, b1b,
+                       training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2, w.part2);
+    SRF_LAUNCH_CHECK("conv2_fwd");
+  }
+  if ((rc = bn_finalize(w.part2, nparts2, w.merged, gamma1, beta1, mmean1, mvar1, training, sv.stats2, st)))
+    return rc;
   SRF_LAUNCH_CHECK("bn_finalize(2)");
   hipLaunchKernelGGL(bn_apply_kernel, dim3(1024), dim3(256), 0, st, sv.y2, sv.stats2, inp_len, d.B, d.T2, d.F2, 4,
                      out);

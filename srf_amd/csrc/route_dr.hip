@@ -26,6 +26,9 @@
 namespace {
 
 constexpr float kSquashEps = 1e-7f;  // naive:248
+#ifndef SRF_GU_SPLITGX
+#define SRF_GU_SPLITGX 0
+#endif
 
 // Opt-in profiling hook (srf_route_dr_set_timing_events): events recorded on the
 // launch stream around each forward routing-pass kernel of the next
@@ -612,11 +615,24 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
       f4 gx[NCT];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
+#if SRF_GU_SPLITGX
+        // two independent accumulator chains (A/B variant)
+        f4 ga0 = f4{0.f, 0.f, 0.f, 0.f}, ga1 = ga0;
+#pragma unroll
+        for (int t = 0; t < TW; ++t)
+#pragma unroll
+          for (int k = 0; k < 4; k += 2) {
+            ga0 = mfma16x16x4(wt[ct][t][k], ga[t][k], ga0);
+            ga1 = mfma16x16x4(wt[ct][t][k + 1], ga[t][k + 1], ga1);
+          }
+        gx[ct] = ga0 + ga1;
+#else
         gx[ct] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < TW; ++t)
 #pragma unroll
           for (int k = 0; k < 4; ++k) gx[ct] = mfma16x16x4(wt[ct][t][k], ga[t][k], gx[ct]);
+#endif
       }
       const int w = i / N, n = i - w * N;
       const int ts = loc.t + w - lpad;
@@ -1223,7 +1239,7 @@ Gw2Plan gw2_plan(const Geom& g) {
     if (forced > 0 && S0 != std::min(forced, NFT)) continue;
     const int ft_per = (NFT + S0 - 1) / S0;
     const int S = (NFT + ft_per - 1) / ft_per;
-    const int rounds = (base * S + 767) / 768;   // ~3 workgroups per CU
+    const int rounds = (base * S + 511) / 512;   // 2 workgroups per CU (8 waves at ~180 VGPRs)
     const double work = (double)rounds * ft_per * p.cap * NCT * 200.0 / 2.4e9;
     const double slab = S > 1 ? 2.0 * S * p.pstride * 4 / 4e12 : 0.0;
     if (work + slab < best) {

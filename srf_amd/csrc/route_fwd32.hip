@@ -44,6 +44,14 @@
 #ifndef SRF_FWD32_FETCH_EARLY
 #define SRF_FWD32_FETCH_EARLY 0
 #endif
+// 1: the second half of a workgroup's waves runs at s_setprio 1 (pass kernels)
+#ifndef SRF_FWD32_PRIO
+#define SRF_FWD32_PRIO 0
+#endif
+// 1: softmax normaliser by the fast reciprocal instead of an IEEE division
+#ifndef SRF_FWD32_FASTDIV
+#define SRF_FWD32_FASTDIV 0
+#endif
 
 namespace {
 
@@ -405,6 +413,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
   const int j0 = tbase * 32 / DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+#if SRF_FWD32_PRIO
+  if (NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
 
@@ -531,7 +542,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       __builtin_amdgcn_sched_barrier(0);
       SRF_TMARK(1)
       // c = exp(L - M) / Z = e * exp(m - M) / Z; then all-gather over the halves
+#if SRF_FWD32_FASTDIV
+      const float sc = __expf(m - M) * __builtin_amdgcn_rcpf(Z);
+#else
       const float sc = __expf(m - M) / Z;
+#endif
       if (A.cst != nullptr && fvalid) {
         // lane half h owns capsules j0 + 2a + h after the logit reduce-scatter
         float* dst = A.cst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
@@ -621,6 +636,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
   const int j0 = tbase * 32 / DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+#if SRF_FWD32_PRIO
+  if (NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
 
@@ -655,6 +673,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       float cc[OWN];
 #pragma unroll
       for (int a = 0; a < OWN; ++a) cc[a] = cn[a];
+      // the next capsule's couplings: a whole capsule of work hides their latency
+      if (i + 1 < i1) load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
       // partial dots <u_ij, gs_j> over this lane's rows
       f2 P2[CP];
 #pragma unroll
@@ -701,7 +721,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
                                h, A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
-        load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
       }
       __builtin_amdgcn_sched_barrier(0);
       if (wv == 0 && h == 0 && fvalid) {

@@ -103,3 +103,28 @@ def test_cnnfe_inference_uses_moving_stats(cuda):
                     [P[k].float().to(cuda) for k in ops.CNNFE_PARAMS], moving, False, 0.2, 1)
     assert np.abs(out.cpu().double().numpy() - x.numpy()).max() < 2e-4 * (1 + np.abs(x.numpy()).max())
     assert torch.allclose(moving[0].cpu().double(), mm[0].float().double())   # untouched
+
+
+def test_conv2_split_bf16_matches_fp32_mfma(cuda, monkeypatch):
+    """The split-bf16 stage-2 convolution (conv2_fwd32_kernel, 3-term bf16 splits on
+    32x32x16 MFMA) against the fp32-MFMA one (SRF_CONV2_32=0): same CNN-FE output
+    to fp32 accuracy, dropout included (same counter-based masks)."""
+    from srf_amd import ops
+    torch.manual_seed(3)
+    B, T, Fd = 3, 45, 123
+    feats = torch.randn(B, T, Fd, device=cuda)
+    il = torch.tensor([45, 31, 12], dtype=torch.int32, device=cuda)
+    params = []
+    for k in range(2):
+        cin = 1 if k == 0 else 64
+        for _ in range(2):
+            params += [torch.randn(3, 3, cin, 64, device=cuda) * 0.1, torch.randn(64, device=cuda) * 0.1]
+        params += [1 + 0.1 * torch.randn(64, device=cuda), 0.1 * torch.randn(64, device=cuda)]
+    outs = []
+    for flag in ('1', '0'):
+        monkeypatch.setenv('SRF_CONV2_32', flag)
+        moving = [torch.zeros(64, device=cuda), torch.ones(64, device=cuda), torch.zeros(64, device=cuda),
+                  torch.ones(64, device=cuda)]
+        outs.append(ops.cnnfe(feats, il, params, moving, True, 0.2, 1234).cpu().double().numpy())
+    err = np.abs(outs[0] - outs[1]).max()
+    assert err <= 2e-5 * max(1.0, np.abs(outs[1]).max()), err
