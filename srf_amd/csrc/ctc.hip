@@ -24,8 +24,19 @@ __device__ __forceinline__ float lse2(float a, float b) {
 
 // Wave-resident recursions (KM > 0, S <= 64*KM): wave 0 holds states
 // s = lane + 64k in registers; the s-1 / s-2 (alpha) or s+1 / s+2 (beta)
-// neighbours come from ds_bpermute shuffles, the lane at a 64-state boundary
-// taking the neighbouring group's value, so a time step needs no barrier.
+// neighbours come from DPP whole-wave shifts (wave_shr:1 / wave_shl:1, a VALU
+// move instead of an LDS-crossbar shuffle on the serial path), the lanes at a
+// 64-state boundary taking the neighbouring group's values (v_readlane), so a
+// time step needs no barrier.
+__device__ __forceinline__ float dpp_wave_shr1(float old, float src) {   // lane l <- src[l-1], lane 0 <- old
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_wave_shl1(float old, float src) {   // lane l <- src[l+1], lane 63 <- old
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x130, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float read_lane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 template <int KM>
 __device__ __forceinline__ float alpha_wave(const int* __restrict__ ext, const float* __restrict__ lp, int C, int S,
                                             int Tb, int Smax, int blank, float* __restrict__ out) {
@@ -50,9 +61,10 @@ __device__ __forceinline__ float alpha_wave(const int* __restrict__ ext, const f
       if (t == 0) {
         v = s < 2 ? 0.f : -INFINITY;
       } else {
-        const float lo = k > 0 ? a[k - 1] : -INFINITY;
-        const float p1 = __shfl(lane == 63 ? lo : a[k], (lane + 63) & 63, 64);
-        const float p2 = __shfl(lane >= 62 ? lo : a[k], (lane + 62) & 63, 64);
+        const float l63 = k > 0 ? read_lane(a[k - 1], 63) : -INFINITY;
+        const float l62 = k > 0 ? read_lane(a[k - 1], 62) : -INFINITY;
+        const float p1 = dpp_wave_shr1(l63, a[k]);    // state s - 1
+        const float p2 = dpp_wave_shr1(l62, p1);      // state s - 2
         v = lse2(a[k], p1);
         if (sk[k]) v = lse2(v, p2);
       }
@@ -102,9 +114,10 @@ __device__ __forceinline__ void beta_wave(const int* __restrict__ ext, const flo
       if (t == Tb - 1) {
         v = s >= S - 2 ? 0.f : -INFINITY;
       } else {
-        const float hi = k + 1 < KM ? a[k + 1] : -INFINITY;
-        const float q1 = __shfl(lane == 0 ? hi : a[k], (lane + 1) & 63, 64);
-        const float q2 = __shfl(lane <= 1 ? hi : a[k], (lane + 2) & 63, 64);
+        const float h0 = k + 1 < KM ? read_lane(a[k + 1], 0) : -INFINITY;
+        const float h1 = k + 1 < KM ? read_lane(a[k + 1], 1) : -INFINITY;
+        const float q1 = dpp_wave_shl1(h0, a[k]);     // state s + 1
+        const float q2 = dpp_wave_shl1(h1, q1);       // state s + 2
         v = lse2(a[k], q1);
         if (sk[k]) v = lse2(v, q2);
       }
