@@ -1290,10 +1290,24 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   t_ev_n = 0;
   const bool p32 = use_fwd32(g);
   srf::Fwd32Plan plan{};
+  srf::Fwd32Cpl cl{};
   float* bsum = slab + (size_t)n_chunks * FJD;
+  // split operand planes: in the coupling storage when the backward will reuse them
+  void* planes = slab;
+  void* scratch = slab;
   if (p32) {
     plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
-    const int rc = srf::fwd32_prepare(plan, emb, W, bias, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, slab, st);
+    float *WT = nullptr, *xT = nullptr;
+    if (couplings != nullptr) {
+      cl = srf::fwd32_cpl_layout(plan, g.F(), g.in_n(), g.din, g.dout, g.J, g.iters);
+      planes = couplings + cl.planes;
+      WT = couplings + cl.WT;
+      xT = couplings + cl.xT;
+    } else {
+      scratch = static_cast<char*>(static_cast<void*>(slab)) + srf::fwd32_planes_bytes(plan);
+    }
+    const int rc = srf::fwd32_prepare(plan, emb, W, bias, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, planes,
+                                      scratch, WT, xT, st);
     if (rc) return rc;
   } else {
     const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
@@ -1308,18 +1322,18 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
       float *cst = nullptr, *lzst = nullptr;
       if (couplings != nullptr && r > 0) {
         const size_t blk = (size_t)srf::fwd32_frame_stride(g.F()) * g.in_n();
-        cst = couplings + (size_t)(r - 1) * blk * (plan.JDp / g.dout);
-        lzst = couplings + (size_t)(g.iters - 1) * blk * (plan.JDp / g.dout) + (size_t)(r - 1) * blk;
+        cst = couplings + cl.c + (size_t)(r - 1) * blk * (plan.JDp / g.dout);
+        lzst = couplings + cl.lz + (size_t)(r - 1) * blk;
       }
-      const int rc = srf::fwd32_pass(plan, r == 0, slab, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout,
-                                     g.mask_first, vc, cst, lzst, st);
+      const int rc = srf::fwd32_pass(plan, r == 0, planes, scratch, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J,
+                                     g.dout, g.mask_first, vc, cst, lzst, st);
       if (rc) return rc;
     } else {
       dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, r == 0 ? bsum : nullptr, slab, nullptr, 1, st);
     }
     SRF_LAUNCH_CHECK("route_pass(fwd)");
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev1[r], st));
-    launch_fwd_finish<D>(g, p32 ? srf::fwd32_slab(plan, slab) : slab, p32 ? plan.n_chunks : n_chunks, vc,
+    launch_fwd_finish<D>(g, p32 ? srf::fwd32_slab(plan, scratch) : slab, p32 ? plan.n_chunks : n_chunks, vc,
                          saved + (size_t)(2 * r) * FJD, saved + (size_t)(2 * r + 1) * FJD,
                          r == g.iters - 1 ? v_out : nullptr, st);
     SRF_LAUNCH_CHECK("fwd_finish");
@@ -1329,7 +1343,7 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
 
 struct BwdWs {
   float *A, *gs, *slab, *stats, *gu_t, *xT, *WT;
-  void* p32;          // split-bf16 operand planes + slab of the B1 passes from stored couplings
+  void* p32;          // scratch (bias sums + partial slabs) of the B1 passes from stored couplings
   float* gl;          // gL^r of those passes [iters-1][in_n][JP][Fs], read by the gu / gW passes
   float* gwpart;      // partial gW | gbias slabs of route_gw2_kernel (S frame splits)
   size_t bytes;
@@ -1349,7 +1363,7 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   size_t op32 = 0, ogl = 0, ogwp = 0;
   if (use_fwd32(g)) {
     const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
-    op32 = take((srf::fwd32_workspace(plan) + 3) / 4);
+    op32 = take((srf::fwd32_scratch_bytes(plan) + 3) / 4);
     ogl = take((size_t)std::max(g.iters - 1, 1) * srf::fwd32_frame_stride(g.F()) * in_n * (plan.JDp / g.dout));
     const Gw2Plan gp = gw2_plan(g);
     ogwp = take(gp.S * gp.pstride);
@@ -1378,17 +1392,16 @@ int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias,
                      const float* saved = nullptr, const float* couplings = nullptr) {
   const int Fp = padded_frames(g);
   if (couplings != nullptr && w.gl != nullptr && g.iters > 1) {
-    // gu formed from the stored couplings / logit gradients (never materialised)
-    const int tiles = (Fp + kXtFrames - 1) / kXtFrames;
-    hipLaunchKernelGGL(window_xt_kernel, dim3(g.in_n() * tiles), dim3(256), 0, st, emb, g.F(), Fp, g.T, g.N, g.din,
-                       g.lpad, g.in_n(), w.xT);
-    SRF_LAUNCH_CHECK("window_xt");
+    // gu formed from the stored couplings / logit gradients (never materialised);
+    // the forward left the windowed x^T in the coupling storage
     const Gw2Plan p = gw2_plan(g);
     const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    const srf::Fwd32Cpl cl = srf::fwd32_cpl_layout(plan, g.F(), g.in_n(), g.din, g.dout, g.J, g.iters);
     const bool direct = p.S == 1;
     float* gwp = direct ? g_W : w.gwpart;
     float* gbp = direct ? g_bias : w.gwpart + (size_t)g.in_n() * g.JD() * g.din;
-    int rc = launch_gw2<D>(g, p, w.xT, saved, w.gs, couplings, w.gl, plan.JDp / g.dout, gwp, gbp, st);
+    int rc = launch_gw2<D>(g, p, couplings + cl.xT, saved, w.gs, couplings + cl.c, w.gl, plan.JDp / g.dout, gwp, gbp,
+                           st);
     if (rc || direct) return rc;
     const size_t nw4 = (size_t)g.in_n() * g.JD() * g.din / 4, n4 = p.pstride / 4;
     hipLaunchKernelGGL(gw_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, w.gwpart, p.S, n4, p.pstride, g_W,
@@ -1429,12 +1442,11 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   // and its logits carry no gradient.
   const bool p32 = couplings != nullptr && w.p32 != nullptr && R > 1;
   srf::Fwd32Plan plan{};
+  srf::Fwd32Cpl cl{};
   if (p32) {
-    // B1 from the forward's stored couplings on the split-bf16 32x32 tiles
+    // B1 from the forward's stored couplings and operand planes on the split-bf16 32x32 tiles
     plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
-    const int rc = srf::fwd32_prepare(plan, emb, W, bias, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, w.p32,
-                                      st);
-    if (rc) return rc;
+    cl = srf::fwd32_cpl_layout(plan, g.F(), g.in_n(), g.din, g.dout, g.J, g.iters);
   }
   for (int r = R - 1; r >= 1; --r) {
     const float* vc = saved + (size_t)(2 * (r - 1) + 1) * FJD;
@@ -1442,9 +1454,9 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     if (p32) {
       const size_t blk = (size_t)srf::fwd32_frame_stride(g.F()) * g.in_n();
       const int JP = plan.JDp / g.dout;
-      const int rc = srf::bwd32_pass(plan, w.p32, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout,
-                                     couplings + (size_t)(r - 1) * blk * JP,
-                                     couplings + (size_t)(R - 1) * blk * JP + (size_t)(r - 1) * blk,
+      const int rc = srf::bwd32_pass(plan, couplings + cl.planes, w.p32, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J,
+                                     g.dout, couplings + cl.c + (size_t)(r - 1) * blk * JP,
+                                     couplings + cl.lz + (size_t)(r - 1) * blk,
                                      w.gs + (size_t)r * FJD, stats_r, w.gl + (size_t)(r - 1) * blk * JP, st);
       if (rc) return rc;
       launch_bwd_finish<D>(g, srf::fwd32_slab(plan, w.p32), plan.n_chunks, nullptr, w.A,
@@ -1458,18 +1470,20 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     }
     SRF_LAUNCH_CHECK("bwd_finish");
   }
-  {
-    // W^T for the gu pass; the same launch zeroes g_emb (accumulated by the gu pass
-    // through the window adjoint)
-    const size_t n_emb = (size_t)g.F() * g.N * g.din;
+  const size_t n_emb = (size_t)g.F() * g.N * g.din;
+  if (p32) {
+    // W^T is in the coupling storage; g_emb is accumulated by the gu pass through the window adjoint
+    SRF_HIP_TRY(hipMemsetAsync(g_emb, 0, n_emb * sizeof(float), st));
+  } else {
+    // W^T for the gu pass; the same launch zeroes g_emb
     const size_t total = (size_t)g.in_n() * g.JD() * g.din + n_emb;
     hipLaunchKernelGGL(transpose_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, g.in_n(), g.JD(), g.din,
                        w.WT, g_emb, n_emb);
     SRF_LAUNCH_CHECK("transpose_w");
   }
   if (p32)
-    launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st, couplings, w.gl,
-                   plan.JDp / g.dout);
+    launch_gu_r<D>(g, emb, W, couplings + cl.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st, couplings + cl.c,
+                   w.gl, plan.JDp / g.dout);
   else
     launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");
@@ -1518,7 +1532,8 @@ size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rp
 size_t srf_route_dr_coupling_floats(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, iters, 0};
   if (!use_fwd32(g) || iters < 2) return 0;
-  return srf::fwd32_coupling_floats(srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout), B * T, g.in_n(), dout, iters);
+  return srf::fwd32_cpl_layout(srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout), B * T, g.in_n(), din, dout, J, iters)
+      .total;
 }
 
 int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,

@@ -21,24 +21,37 @@ struct Fwd32Plan {
 
 bool fwd32_supported(int din, int dout, int J);
 Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout);
-size_t fwd32_workspace(const Fwd32Plan& p);
+// Operand planes (split W, bias, x: written by fwd32_prepare, read by every pass)
+// and per-pass scratch (i-chunk bias sums + partial slabs) may live apart: a
+// training forward keeps its planes for the backward (coupling storage).
+size_t fwd32_planes_bytes(const Fwd32Plan& p);
+size_t fwd32_scratch_bytes(const Fwd32Plan& p);
+size_t fwd32_workspace(const Fwd32Plan& p);   // planes + scratch
 size_t fwd32_lds(const Fwd32Plan& p);
-float* fwd32_slab(const Fwd32Plan& p, void* ws);
-// split W / bias / emb into bf16 planes and the i-chunk bias sums (once per forward)
+float* fwd32_slab(const Fwd32Plan& p, void* scratch);
+// split W / bias / emb into bf16 planes and the i-chunk bias sums (once per forward);
+// WT / xT (nullable): also the fp32 W^T [in_n][din][JD] and window^T [in_n][din][Fp]
+// operands of the backward gx / gW contractions
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
-                  int din, int lpad, int rpad, int J, int dout, void* ws, hipStream_t st);
-// one routing pass: partial s over i-chunks into fwd32_slab(p, ws); passes r >= 1
+                  int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
+                  hipStream_t st);
+// one routing pass: partial s over i-chunks into fwd32_slab(p, scratch); passes r >= 1
 // also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr
-int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
-               int J, int dout, int mask_first, const float* vc, float* cst, float* lzst, hipStream_t st);
-// coupling storage of one forward: (iters - 1) blocks of c^r [in_n][JP][Fs] followed by
-// (iters - 1) blocks of logZ^r [in_n][Fs]; JP = JDp / dout, Fs = fwd32_frame_stride(F)
-size_t fwd32_coupling_floats(const Fwd32Plan& p, int F, int in_n, int dout, int iters);
-// one backward routing pass r >= 1 from the stored couplings: partial gVc^r over
-// i-chunks into fwd32_slab(p, ws), the (logZ, sigma) stats and the logit
-// gradients gL^r (glst, laid out as the couplings) of the gu pass
-int bwd32_pass(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad, int J,
-               int dout, const float* cst, const float* lz, const float* gs, float* stats, float* glst,
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T, int N, int din,
+               int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst, float* lzst,
                hipStream_t st);
+// Coupling storage of one training forward (float offsets): c^r [iters-1][in_n][JP][Fs],
+// logZ^r [iters-1][in_n][Fs], the operand planes, WT, xT; JP = JDp / dout,
+// Fs = fwd32_frame_stride(F).
+struct Fwd32Cpl {
+  size_t c, lz, planes, WT, xT, total;
+};
+Fwd32Cpl fwd32_cpl_layout(const Fwd32Plan& p, int F, int in_n, int din, int dout, int J, int iters);
+// one backward routing pass r >= 1 from the stored couplings: partial gVc^r over
+// i-chunks into fwd32_slab(p, scratch), the (logZ, sigma) stats and the logit
+// gradients gL^r (glst, laid out as the couplings) of the gu pass
+int bwd32_pass(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din, int lpad,
+               int rpad, int J, int dout, const float* cst, const float* lz, const float* gs, float* stats,
+               float* glst, hipStream_t st);
 
 }  // namespace srf

@@ -105,13 +105,16 @@ __device__ __forceinline__ void split8(const float* __restrict__ src, bool ok, _
 //   bias [in_n][JD]     -> bs [in_n][JDp][4] = (b1, b2, b3, 0);
 //   bsum[c][row]        =  sum of bias[i][row] over the capsules of i-chunk c (iteration-0 pass);
 //   emb [F][N][din]     -> xs [3][plane], plane = [N][F][din] capsule-major + 16 zeros.
+//   (training forwards also write the fp32 operands of the backward passes:)
+//   W                   -> WT [in_n][din][JD] (A of the gx contraction), 4 per thread;
+//   window(emb)         -> xT [in_n][din][Fp] (A of the gW contraction, zero past F / the utterance).
 struct PrepArgs {
   const float *W, *bias, *emb;
   __bf16 *Ws, *bs, *xs;
-  float* bsum;
-  int in_n, JD, JDp, din, n_chunks, chunk_len, F, N;
+  float *bsum, *WT, *xT;
+  int in_n, JD, JDp, din, n_chunks, chunk_len, F, N, T, lpad, Fp;
   size_t xplane;
-  size_t n_a, n_b, n_c, n_d;   // thread counts of the four ranges
+  size_t n_a, n_b, n_c, n_d, n_e, n_f;   // thread counts of the six ranges
 };
 
 __global__ void prep32_kernel(PrepArgs P) {
@@ -158,6 +161,33 @@ __global__ void prep32_kernel(PrepArgs P) {
     const bool ok = e0 < n_data;
     split8(P.emb + ((size_t)(ok ? f : 0) * P.N + (ok ? n : 0)) * P.din + (ok ? e : 0), ok, P.xs + e0,
            P.xs + P.xplane + e0, P.xs + 2 * P.xplane + e0);
+    return;
+  }
+  idx -= P.n_d;
+  if (idx < P.n_e) {   // WT[i][e][row] = W[i][row][e], 4 rows per thread
+    const size_t o = idx * 4;
+    const int row = o % P.JD;
+    const size_t ie = o / P.JD;
+    const int e = ie % P.din;
+    const size_t i = ie / P.din;
+    const float* w = P.W + (i * P.JD + row) * P.din + e;
+    *reinterpret_cast<f4*>(P.WT + o) = f4{w[0], w[P.din], w[2 * P.din], w[3 * P.din]};
+    return;
+  }
+  idx -= P.n_e;
+  if (idx < P.n_f) {   // xT[i][e][f]: capsule i = w*N + n of frame f is emb[f + w - lpad][n] inside the utterance
+    const int f = idx % P.Fp;
+    const size_t ie = idx / P.Fp;
+    const int e = ie % P.din;
+    const int i = ie / P.din;
+    const int w = i / P.N, n = i - w * P.N;
+    float v = 0.f;
+    if (f < P.F) {
+      const int b = f / P.T, t = f - b * P.T;
+      const int ts = t + w - P.lpad;
+      if (ts >= 0 && ts < P.T) v = P.emb[((size_t)(b * P.T + ts) * P.N + n) * P.din + e];
+    }
+    P.xT[idx] = v;
   }
 }
 
@@ -819,19 +849,21 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   return p;
 }
 
-float* fwd32_slab(const Fwd32Plan& p, void* ws) {
-  return reinterpret_cast<float*>(static_cast<char*>(ws) + p.ws_w + p.ws_b + p.ws_x + p.ws_bsum);
+size_t fwd32_planes_bytes(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x; }
+size_t fwd32_scratch_bytes(const Fwd32Plan& p) { return p.ws_bsum + p.ws_slab; }
+size_t fwd32_workspace(const Fwd32Plan& p) { return fwd32_planes_bytes(p) + fwd32_scratch_bytes(p); }
+float* fwd32_slab(const Fwd32Plan& p, void* scratch) {
+  return reinterpret_cast<float*>(static_cast<char*>(scratch) + p.ws_bsum);
 }
-
-size_t fwd32_workspace(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x + p.ws_bsum + p.ws_slab; }
 
 size_t fwd32_lds(const Fwd32Plan& p) {
   return (size_t)p.NW * kTW * 4 * 64 * 16 + (p.NW > 1 ? (size_t)2 * 32 * p.NW * 8 : 0);
 }
 
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
-                  int din, int lpad, int rpad, int J, int dout, void* ws, hipStream_t st) {
-  char* base = static_cast<char*>(ws);
+                  int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
+                  hipStream_t st) {
+  char* base = static_cast<char*>(planes);
   PrepArgs P;
   P.W = W;
   P.bias = bias;
@@ -839,7 +871,12 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   P.Ws = reinterpret_cast<__bf16*>(base);
   P.bs = reinterpret_cast<__bf16*>(base + p.ws_w);
   P.xs = reinterpret_cast<__bf16*>(base + p.ws_w + p.ws_b);
-  P.bsum = reinterpret_cast<float*>(base + p.ws_w + p.ws_b + p.ws_x);
+  P.bsum = reinterpret_cast<float*>(scratch);
+  P.WT = WT;
+  P.xT = xT;
+  P.T = T;
+  P.lpad = lpad;
+  P.Fp = (B * T + 15) / 16 * 16;
   P.in_n = N * (lpad + rpad + 1);
   P.JD = J * dout;
   P.JDp = p.JDp;
@@ -853,7 +890,9 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   P.n_b = (size_t)P.in_n * p.JDp;
   P.n_c = (size_t)p.n_chunks * P.JD;
   P.n_d = p.xplane / 8;
-  const size_t total = P.n_a + P.n_b + P.n_c + P.n_d;
+  P.n_e = WT ? (size_t)P.in_n * din * P.JD / 4 : 0;
+  P.n_f = xT ? (size_t)P.in_n * din * P.Fp : 0;
+  const size_t total = P.n_a + P.n_b + P.n_c + P.n_d + P.n_e + P.n_f;
   hipLaunchKernelGGL(prep32_kernel, dim3((total + 255) / 256), dim3(256), 0, st, P);
   SRF_LAUNCH_CHECK("prep32");
   return SRF_OK;
@@ -889,10 +928,10 @@ static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipS
   }
 }
 
-static Args32 make_args32(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
-                          int J, int dout, int mask_first) {
+static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din,
+                          int lpad, int rpad, int J, int dout, int mask_first) {
   const int in_n = N * (lpad + rpad + 1);
-  const char* base = static_cast<const char*>(ws);
+  const char* base = static_cast<const char*>(planes);
   Args32 a;
   a.Ws = reinterpret_cast<const __bf16*>(base);
   a.bs = reinterpret_cast<const __bf16*>(base + p.ws_w);
@@ -915,8 +954,8 @@ static Args32 make_args32(const Fwd32Plan& p, const void* ws, int B, int T, int 
   a.mask_first = mask_first;
   a.n_tgroups = p.NW;
   a.vc = nullptr;
-  a.bsum = reinterpret_cast<const float*>(base + p.ws_w + p.ws_b + p.ws_x);
-  a.slab = fwd32_slab(p, const_cast<void*>(ws));
+  a.bsum = reinterpret_cast<const float*>(scratch);
+  a.slab = fwd32_slab(p, scratch);
   a.cst = nullptr;
   a.lzst = nullptr;
   a.JP = p.JDp / dout;
@@ -924,14 +963,28 @@ static Args32 make_args32(const Fwd32Plan& p, const void* ws, int B, int T, int 
   return a;
 }
 
-size_t fwd32_coupling_floats(const Fwd32Plan& p, int F, int in_n, int dout, int iters) {
-  if (iters < 2) return 0;
-  return (size_t)(iters - 1) * fwd32_frame_stride(F) * in_n * (p.JDp / dout + 1);
+Fwd32Cpl fwd32_cpl_layout(const Fwd32Plan& p, int F, int in_n, int din, int dout, int J, int iters) {
+  Fwd32Cpl c{};
+  const size_t blk = (size_t)fwd32_frame_stride(F) * in_n;
+  const int R1 = std::max(iters - 1, 0);
+  c.c = 0;
+  c.lz = (size_t)R1 * blk * (p.JDp / dout);
+  size_t off = c.lz + (size_t)R1 * blk;
+  off = (off + 63) / 64 * 64;   // 256-byte aligned regions
+  c.planes = off;
+  off += (fwd32_planes_bytes(p) + 255) / 256 * 64;
+  c.WT = off;
+  off += ((size_t)in_n * din * J * dout + 63) / 64 * 64;
+  c.xT = off;
+  off += ((size_t)in_n * din * ((F + 15) / 16 * 16) + 63) / 64 * 64;
+  c.total = off;
+  return c;
 }
 
-int fwd32_pass(const Fwd32Plan& p, bool first, const void* ws, int B, int T, int N, int din, int lpad, int rpad,
-               int J, int dout, int mask_first, const float* vc, float* cst, float* lzst, hipStream_t st) {
-  Args32 a = make_args32(p, ws, B, T, N, din, lpad, rpad, J, dout, mask_first);
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T, int N, int din,
+               int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst, float* lzst,
+               hipStream_t st) {
+  Args32 a = make_args32(p, planes, scratch, B, T, N, din, lpad, rpad, J, dout, mask_first);
   a.vc = vc;
   a.cst = first ? nullptr : cst;
   a.lzst = first ? nullptr : lzst;
@@ -970,10 +1023,10 @@ static int launch_bpass_t(const Fwd32Plan& p, const Args32& a, const Bwd32Args& 
   }
 }
 
-int bwd32_pass(const Fwd32Plan& p, const void* ws, int B, int T, int N, int din, int lpad, int rpad, int J,
-               int dout, const float* cst, const float* lz, const float* gs, float* stats, float* glst,
-               hipStream_t st) {
-  Args32 a = make_args32(p, ws, B, T, N, din, lpad, rpad, J, dout, 0);
+int bwd32_pass(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din, int lpad,
+               int rpad, int J, int dout, const float* cst, const float* lz, const float* gs, float* stats,
+               float* glst, hipStream_t st) {
+  Args32 a = make_args32(p, planes, scratch, B, T, N, din, lpad, rpad, J, dout, 0);
   Bwd32Args b{cst, lz, gs, stats, glst};
 #define SRF_B32(DI, DO) \
   if (din == DI && dout == DO) return launch_bpass_t<DI, DO>(p, a, b, st);
