@@ -666,6 +666,163 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
   }
 }
 
+// gu pass from stored couplings (the CPL case of route_gu_kernel) as a software
+// pipeline: the transposed W rows and the per-(i, j, f) scalars c^r, gL^r of
+// capsule k+1 are in flight (buffer loads, SGPR capsule offsets) while capsule k
+// is formed and contracted.  gu is not stored (route_gw2_kernel forms it again).
+template <int DIN, int TW, int R>
+__global__ __launch_bounds__(256, (R >= 4 ? 3 : 4)) void route_gux_kernel(
+    const float* __restrict__ WT, int F, int T, int N, int lpad, int in_n, int J, int mask_first, int n_wgroups,
+    int n_chunks, int n_per, const float* __restrict__ saved, const float* __restrict__ gs, float* __restrict__ g_emb,
+    int nslots_max, const float* __restrict__ cst, const float* __restrict__ glst, int JP) {
+  static_assert(R >= 2, "stored couplings exist for iters >= 2");
+  constexpr int NCT = (DIN + 15) / 16;
+  constexpr int RV = R - 1;
+  extern __shared__ __attribute__((aligned(16))) float gacc[];
+  const int JD = J * DIN;
+  const int NT = (JD + 15) / 16;
+  const size_t FJD = (size_t)F * JD;
+  const int NW = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int fl = lane & 15, g = lane >> 4;
+  const int chunk = blockIdx.x % n_chunks;
+  const int rest = blockIdx.x / n_chunks;
+  const int wgrp = rest % n_wgroups;
+  const int ft = rest / n_wgroups;
+  const int f = ft * 16 + fl;
+  const FrameLoc loc = frame_loc(f, F, T);
+  const int tbase = __builtin_amdgcn_readfirstlane((wgrp * NW + wv) * TW);
+  const int n0 = chunk * n_per, nn = min(N, n0 + n_per) - n0;
+  const int Wn = in_n / N;
+  const int ncap = Wn * nn;
+  const int Jeff = J - (mask_first ? 1 : 0);
+  const int SROW = n_per * DIN + 4;
+  const int nslots = 15 + Wn;
+  float* gw_acc = gacc + (size_t)wv * nslots_max * SROW;
+  for (int k = threadIdx.x; k < NW * nslots_max * SROW; k += blockDim.x) gacc[k] = 0.f;
+  __syncthreads();
+
+  float vcr[RV][TW][4], gsr[R][TW][4];
+  float c0[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int j = tile_j<DIN>(tbase + t, g);
+    c0[t] = (j < J && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r > 0) load_rows(saved + (size_t)(2 * (r - 1) + 1) * FJD, f, loc.valid, JD, tbase + t, g, vcr[r - 1][t]);
+      load_rows(gs + (size_t)r * FJD, f, loc.valid, JD, tbase + t, g, gsr[r][t]);
+    }
+  }
+  // lane byte offsets (capsule-independent) and per-capsule SGPR offsets
+  const int Fs = srf::fwd32_frame_stride(F);
+  const uint32_t cblk_b = (uint32_t)in_n * JP * Fs * 4;
+  const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(WT), 0, (int)((size_t)in_n * DIN * JD * 4),
+                                                       0x00020000);
+  const auto rs_c = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cst), 0, (int)(cblk_b * RV), 0x00020000);
+  const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(glst), 0, (int)(cblk_b * RV), 0x00020000);
+  uint32_t wo[NCT][TW], co[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int tc = min(tbase + t, NT - 1);
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+      wo[ct][t] = (uint32_t)(min(ct * 16 + fl, DIN - 1) * JD + min(tc * 16 + 4 * g, JD - 4)) * 4;
+    co[t] = (uint32_t)(min(tile_j<DIN>(tbase + t, g), J - 1) * Fs + (loc.valid ? f : 0)) * 4;
+  }
+  // three operand sets in a ring: capsule k+2 is fetched while capsule k is formed
+  constexpr int NB = 3;
+  f4 wt_b[NB][NCT][TW];
+  float c_b[NB][RV][TW], g_b[NB][RV][TW];
+  auto fetch = [&](auto slot, int i) {
+    constexpr int sl = decltype(slot)::value;
+    const uint32_t sw = (uint32_t)i * DIN * JD * 4;
+    const uint32_t sc = (uint32_t)i * JP * Fs * 4;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+        wt_b[sl][ct][t] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs_w, wo[ct][t], sw, 0));
+#pragma unroll
+    for (int r = 0; r < RV; ++r)
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        c_b[sl][r][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_c, co[t], sc + r * cblk_b, 0));
+        g_b[sl][r][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, co[t], sc + r * cblk_b, 0));
+      }
+  };
+  // capsule k of the chunk is i = w*N + n0 + nl (visited w-major); (wf, nf) runs two capsules ahead
+  int w = 0, nl = 0, wf = 0, nf = 0;
+  auto advance = [&](int& ww, int& nn_) {
+    if (++nn_ == nn) nn_ = 0, ++ww;
+  };
+  auto compute = [&](auto slot) {
+    constexpr int sl = decltype(slot)::value;
+    const int i = w * N + n0 + nl;
+    float ga[TW][4];
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a = c0[t] * gsr[0][t][q];
+#pragma unroll
+        for (int r = 0; r < RV; ++r) a += c_b[sl][r][t] * gsr[r + 1][t][q] + g_b[sl][r][t] * vcr[r][t][q];
+        ga[t][q] = a;
+      }
+    f4 gx[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) {
+      gx[ct] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gx[ct] = mfma16x16x4(wt_b[sl][ct][t][q], ga[t][q], gx[ct]);
+    }
+    const int ts = loc.t + w - lpad;
+    if (loc.valid && ts >= 0 && ts < T) {
+      const int n = i - w * N;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        if (ct * 16 + 4 * g >= DIN) continue;
+        float* a = gw_acc + (fl + w) * SROW + (n - n0) * DIN + ct * 16 + 4 * g;
+        st4(a, ld4(a) + gx[ct]);
+      }
+    }
+    advance(w, nl);
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  if (ncap > 0) fetch(S0{}, n0);
+  advance(wf, nf);
+  if (ncap > 1) fetch(S1{}, wf * N + n0 + nf);
+  advance(wf, nf);
+  for (int k = 0; k < ncap; k += NB) {
+    // capsule k + u sits in slot u; capsule k + u + 2 goes to slot (u + 2) % 3
+    if (k + 2 < ncap) fetch(S2{}, wf * N + n0 + nf);
+    advance(wf, nf);
+    compute(S0{});
+    if (k + 1 >= ncap) break;
+    if (k + 3 < ncap) fetch(S0{}, wf * N + n0 + nf);
+    advance(wf, nf);
+    compute(S1{});
+    if (k + 2 >= ncap) break;
+    if (k + 4 < ncap) fetch(S1{}, wf * N + n0 + nf);
+    advance(wf, nf);
+    compute(S2{});
+  }
+  __syncthreads();
+  const int f0 = ft * 16 - lpad;
+  const int row = nn * DIN;
+  for (int k = threadIdx.x; k < nslots * row; k += blockDim.x) {
+    const int slot = k / row, rem = k - slot * row;
+    const int fo = f0 + slot;
+    float v = 0.f;
+    for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots_max + slot) * SROW + rem];
+    if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
+  }
+}
+
 // W [in_n][JD][din] -> WT [in_n][din][JD] (A operand of the gx contraction); the
 // same launch zeroes g_emb ([n_zero] floats), which the gu pass accumulates into.
 __global__ void transpose_w_kernel(const float* __restrict__ W, int in_n, int JD, int din, float* __restrict__ WT,
@@ -974,6 +1131,174 @@ __global__ __launch_bounds__(256) void route_gw2_kernel(
   }
 }
 
+// The same contraction, restructured for occupancy and a branch-free load path:
+//   * staging sources are per-thread pointers fixed at kernel start (every staged
+//     part is frame-minor, so tile ft + 1 is 16 floats further on);
+//   * the per-frame vectors come in through buffer loads whose range check
+//     returns 0 for frames past F (no masks);
+//   * tile t + 1's staged registers are written after the barrier of tile t and the
+//     loads of tile t + 2 go out right behind them (one barrier per tile);
+//   * at most 168 registers, so three workgroups share a CU.
+// The stored couplings and logit gradients are 0 for frames past F (the 32x32
+// passes store zeros there) and x^T is 0 past F, so gu is 0 on padded frames.
+template <int D, int R, int CAP>
+__global__ __launch_bounds__(256, 3) void route_gw3_kernel(
+    const float* __restrict__ xT, const float* __restrict__ saved, const float* __restrict__ gs,
+    const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp, int in_n, int J, int mask_first,
+    int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride) {
+  static_assert(R >= 2, "stored couplings exist for iters >= 2");
+  constexpr int NCT = (D + 15) / 16;
+  constexpr int RV = R - 1;
+  constexpr int JW = gw2_jw<D>();
+  constexpr int CG = RV * 2 * JW * 16;   // per capsule: [r][c|gl][jw][16 frames]
+  constexpr int PC = CG + D * 16;        // + x^T [e][16 frames]
+  constexpr int SF = CAP * PC;
+  constexpr int NQ = (SF / 4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float stg[2][SF];
+  const int JD = J * D;
+  const int NT = (JD + 15) / 16;
+  const size_t FJD = (size_t)F * JD;
+  const int Fs = srf::fwd32_frame_stride(F);
+  const size_t cblk = (size_t)in_n * JP * Fs;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l16 = lane & 15, kk = lane >> 4;
+  int b = blockIdx.x;
+  const int s = b % S;
+  b /= S;
+  const int rtg = b % n_rt;
+  const int cc = b / n_rt;
+  const int tg = rtg * 4 + wv;
+  const int row = min(tg * 16 + l16, JD - 1);
+  const bool rvalid = tg < NT && tg * 16 + l16 < JD;
+  const int j = row / D;
+  const int jg0 = (rtg * 64) / D;
+  const int jl = min(j - jg0, JW - 1);
+  const int Jeff = J - (mask_first ? 1 : 0);
+  const float c0 = (rvalid && j < J && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+  const int i0 = cc * CAP, ncap = min(in_n, i0 + CAP) - i0;
+  const int NFT = Fp >> 4;
+  const int ft0 = s * ft_per, ft1 = min(NFT, ft0 + ft_per);
+
+  const float* src[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int idx = min(q * 256 + (int)threadIdx.x, SF / 4 - 1);
+    const int k = idx / (PC / 4), rem = idx - k * (PC / 4);
+    const int i = i0 + min(k, ncap - 1);
+    if (rem < CG / 4) {
+      const int fq = rem & 3, jw = (rem >> 2) % JW, cg = (rem >> 2) / JW;
+      const int jj = min(jg0 + jw, JP - 1);
+      src[q] = ((cg & 1) ? glst : cst) + (size_t)(cg >> 1) * cblk + ((size_t)i * JP + jj) * Fs + 4 * fq;
+    } else {
+      const int x = rem - CG / 4;
+      src[q] = xT + ((size_t)i * D + (x >> 2)) * Fp + 4 * (x & 3);
+    }
+  }
+  f4 sv[NQ];
+  auto stage_load = [&](int ft) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) sv[q] = ld4(src[q] + ft * 16);
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int idx = q * 256 + threadIdx.x;
+      if ((SF / 4) % 256 == 0 || idx < SF / 4) st4(&stg[buf][idx * 4], sv[q]);
+    }
+  };
+  // per-frame vectors: buffer loads, 0 past F (range check)
+  const uint32_t nrec = (uint32_t)(FJD * 4);
+  __amdgpu_buffer_rsrc_t rs_g[R], rs_v[RV];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    rs_g[r] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gs + (size_t)r * FJD), 0, (int)nrec, 0x00020000);
+    if (r > 0)
+      rs_v[r - 1] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(saved + (size_t)(2 * (r - 1) + 1) * FJD), 0,
+                                                      (int)nrec, 0x00020000);
+  }
+  const uint32_t vo0 = (uint32_t)((4 * kk) * JD + row) * 4;
+  float g0[4], gr[RV][4], vr[RV][4];
+  float n0[4], nr[RV][4], nvr[RV][4];
+  auto vec_load = [&](int ft) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const uint32_t o = vo0 + (uint32_t)((ft * 16 + v) * JD) * 4;
+      n0[v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g[0], o, 0, 0));
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        nr[r][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g[r + 1], o, 0, 0));
+        nvr[r][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_v[r], o, 0, 0));
+      }
+    }
+  };
+
+  f4 acc[CAP][NCT];
+  float gb[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    gb[k] = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[k][ct] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (ft0 < ft1) {
+    stage_load(ft0);
+    vec_load(ft0);
+    stage_store(0);
+    if (ft0 + 1 < ft1) stage_load(ft0 + 1);
+  }
+  for (int ft = ft0; ft < ft1; ++ft) {
+    const int buf = (ft - ft0) & 1;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      g0[v] = n0[v];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) gr[r][v] = nr[r][v], vr[r][v] = nvr[r][v];
+    }
+    __syncthreads();   // tile ft staged in buf; buf ^ 1 (tile ft - 1) is free
+    if (ft + 1 < ft1) {
+      stage_store(buf ^ 1);
+      if (ft + 2 < ft1) stage_load(ft + 2);
+      vec_load(ft + 1);
+    }
+    const float* sb = stg[buf];
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) {
+      const float* ck = sb + k * PC;
+      float gu[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) gu[v] = c0 * g0[v];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        const f4 c = ld4(ck + ((r * 2 + 0) * JW + jl) * 16 + 4 * kk);
+        const f4 gl = ld4(ck + ((r * 2 + 1) * JW + jl) * 16 + 4 * kk);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) gu[v] += c[v] * gr[r][v] + gl[v] * vr[r][v];
+      }
+      gb[k] += (gu[0] + gu[1]) + (gu[2] + gu[3]);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const f4 xa = ld4(ck + CG + min(ct * 16 + l16, D - 1) * 16 + 4 * kk);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[k][ct] = mfma16x16x4(xa[v], gu[v], acc[k][ct]);
+      }
+    }
+  }
+  float* gw = gwp + (size_t)s * pstride;
+  float* gbo = gbp + (size_t)s * pstride;
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    if (k >= ncap) continue;
+    const int i = i0 + k;
+    const float t = xor32_sum(xor16_sum(gb[k]));
+    if (rvalid) {
+      if (kk == 0) gbo[(size_t)i * JD + row] = t;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        if (ct * 16 + 4 * kk < D) st4(gw + ((size_t)i * JD + row) * D + ct * 16 + 4 * kk, acc[k][ct]);
+    }
+  }
+}
+
 // gW | gbias = sum of the S partial slabs (float4 per thread).
 __global__ void gw_reduce_kernel(const float* __restrict__ part, int S, size_t n4, size_t stride, float* __restrict__ gW,
                                  size_t nw4, float* __restrict__ gb) {
@@ -1183,6 +1508,18 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
   const int n_chunks = (g.N + n_per - 1) / n_per;
   const int nslots = 15 + gu_window(g);
   const size_t lds = gu_lds_bytes(g, nw, n_per);
+  static const bool gux = [] {
+    const char* e = getenv("SRF_GUX");
+    return !(e && e[0] == '0');
+  }();
+  if constexpr (R >= 2 && D <= 16) {   // couplings are stored by the 32x32 forward (din <= 16)
+    if (lds <= kGuLdsMax && cst != nullptr && gux) {
+      hipLaunchKernelGGL((route_gux_kernel<D, TW, R>), dim3(n_ftiles * n_wgroups * n_chunks), dim3(64 * nw), lds, st,
+                         WT, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved,
+                         gs, g_emb, nslots, cst, glst, JP);
+      return;
+    }
+  }
   if (lds <= kGuLdsMax && cst != nullptr)
     hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, true, true>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
@@ -1222,12 +1559,25 @@ struct Gw2Plan {
 
 inline int gw2_cap_rt(int d) { return d <= 16 ? 8 : (d == 32 ? 4 : 2); }
 
+// route_gw3_kernel (default; SRF_GW3=0 selects route_gw2_kernel) with SRF_GW3_CAP
+// capsules per workgroup (8 or 4).
+inline int gw3_cap(const Geom& g) {
+  static const int v = [] {
+    const char* e = getenv("SRF_GW3");
+    if (e && e[0] == '0') return 0;
+    const char* c = getenv("SRF_GW3_CAP");
+    return (c && atoi(c) == 4) ? 4 : 8;
+  }();
+  return (g.din <= 16 && g.iters <= 3) ? v : 0;   // deeper routing spills at 168 registers
+}
+
 Gw2Plan gw2_plan(const Geom& g) {
   Gw2Plan p{};
   const int NT = g.NT();
   const int NCT = (g.din + 15) / 16;
   p.n_rt = (NT + 3) / 4;
-  p.cap = gw2_cap_rt(g.din);
+  p.cap = gw3_cap(g) ? gw3_cap(g) : gw2_cap_rt(g.din);
+  const int slots = gw3_cap(g) ? 768 : 512;   // workgroups resident at once
   p.n_cc = (g.in_n() + p.cap - 1) / p.cap;
   const int NFT = padded_frames(g) / 16;
   p.pstride = (size_t)g.in_n() * g.JD() * (g.din + 1);
@@ -1239,7 +1589,7 @@ Gw2Plan gw2_plan(const Geom& g) {
     if (forced > 0 && S0 != std::min(forced, NFT)) continue;
     const int ft_per = (NFT + S0 - 1) / S0;
     const int S = (NFT + ft_per - 1) / ft_per;
-    const int rounds = (base * S + 511) / 512;   // 2 workgroups per CU (8 waves at ~180 VGPRs)
+    const int rounds = (base * S + slots - 1) / slots;
     const double work = (double)rounds * ft_per * p.cap * NCT * 200.0 / 2.4e9;
     const double slab = S > 1 ? 2.0 * S * p.pstride * 4 / 4e12 : 0.0;
     if (work + slab < best) {
@@ -1255,6 +1605,25 @@ template <int D>
 int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* saved, const float* gs,
                const float* cst, const float* glst, int JP, float* gwp, float* gbp, hipStream_t st) {
   const int grid = p.n_rt * p.n_cc * p.S;
+  if constexpr (D <= 16) {
+    if (gw3_cap(g)) {
+#define SRF_GW3(R_, C_)                                                                                           \
+  hipLaunchKernelGGL((route_gw3_kernel<D, R_, C_>), dim3(grid), dim3(256), 0, st, xT, saved, gs, cst, glst, g.F(), \
+                     padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride)
+#define SRF_GW3C(R_) \
+  if (p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, 8);
+      switch (g.iters) {
+        case 2: SRF_GW3C(2) break;
+        case 3: SRF_GW3C(3) break;
+        case 4: SRF_GW3C(4) break;
+        default: SRF_GW3C(5) break;
+      }
+#undef SRF_GW3C
+#undef SRF_GW3
+      SRF_LAUNCH_CHECK("route_gw3");
+      return SRF_OK;
+    }
+  }
 #define SRF_GW2(R_)                                                                                              \
   hipLaunchKernelGGL((route_gw2_kernel<D, R_>), dim3(grid), dim3(256), 0, st, xT, saved, gs, cst, glst, g.F(),    \
                      padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.n_cc, p.S, p.ft_per, gwp, gbp,   \

@@ -580,12 +580,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #else
       const float sc = __expf(m - M) / Z;
 #endif
-      if (A.cst != nullptr && fvalid) {
-        // lane half h owns capsules j0 + 2a + h after the logit reduce-scatter
+      if (A.cst != nullptr) {
+        // lane half h owns capsules j0 + 2a + h after the logit reduce-scatter; frames
+        // past F (up to the 32-frame stride) store 0, which the gW pass relies on
         float* dst = A.cst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
 #pragma unroll
-        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = e[a] * sc;
-        if (h == 0 && wv == 0) A.lzst[(size_t)i * A.Fs + f] = M + __logf(Z);
+        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = fvalid ? e[a] * sc : 0.f;
+        if (h == 0 && wv == 0 && fvalid) A.lzst[(size_t)i * A.Fs + f] = M + __logf(Z);
       }
       float c[CP];
 #pragma unroll
@@ -764,10 +765,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       float gown[OWN];
 #pragma unroll
       for (int a = 0; a < OWN; ++a) gown[a] = cc[a] * (Q[a] - S);
-      if (fvalid) {
-        float* dst = Bk.glst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
+      {
+        float* dst = Bk.glst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;   // 0 past F, as the couplings
 #pragma unroll
-        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = gown[a];
+        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = fvalid ? gown[a] : 0.f;
       }
       float g[CP];
 #pragma unroll
