@@ -759,15 +759,20 @@ __global__ __launch_bounds__(256, (R >= 4 ? 3 : 4)) void route_gux_kernel(
   auto compute = [&](auto slot) {
     constexpr int sl = decltype(slot)::value;
     const int i = w * N + n0 + nl;
+    // packed pairs (v_pk_fma_f32): gu rows 2h, 2h+1 of tile t
     float ga[TW][4];
 #pragma unroll
     for (int t = 0; t < TW; ++t)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float a = c0[t] * gsr[0][t][q];
+      for (int h = 0; h < 2; ++h) {
+        f2 a = c0[t] * f2{gsr[0][t][2 * h], gsr[0][t][2 * h + 1]};
 #pragma unroll
-        for (int r = 0; r < RV; ++r) a += c_b[sl][r][t] * gsr[r + 1][t][q] + g_b[sl][r][t] * vcr[r][t][q];
-        ga[t][q] = a;
+        for (int r = 0; r < RV; ++r) {
+          a = c_b[sl][r][t] * f2{gsr[r + 1][t][2 * h], gsr[r + 1][t][2 * h + 1]} + a;
+          a = g_b[sl][r][t] * f2{vcr[r][t][2 * h], vcr[r][t][2 * h + 1]} + a;
+        }
+        ga[t][2 * h] = a.x;
+        ga[t][2 * h + 1] = a.y;
       }
     f4 gx[NCT];
 #pragma unroll
@@ -793,24 +798,34 @@ __global__ __launch_bounds__(256, (R >= 4 ? 3 : 4)) void route_gux_kernel(
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   using S2 = std::integral_constant<int, 2>;
-  if (ncap > 0) fetch(S0{}, n0);
-  advance(wf, nf);
-  if (ncap > 1) fetch(S1{}, wf * N + n0 + nf);
-  advance(wf, nf);
+  // fetches past the chunk's last capsule re-read that capsule: no branch around a
+  // load, so the wait before each compute counts exactly the two fetches in flight
+  const int i_last = (Wn - 1) * N + n0 + nn - 1;
+  auto next_i = [&]() {
+    const int i = min(wf * N + n0 + nf, i_last);
+    advance(wf, nf);
+    return i;
+  };
+  // the fetch stays ahead of the compute it overlaps (no sinking by the scheduler)
+#define SRF_GUX_FETCH(SL) \
+  fetch(SL{}, next_i());  \
+  __builtin_amdgcn_sched_barrier(0);
+  if (ncap > 0) {
+    SRF_GUX_FETCH(S0)
+    SRF_GUX_FETCH(S1)
+  }
   for (int k = 0; k < ncap; k += NB) {
     // capsule k + u sits in slot u; capsule k + u + 2 goes to slot (u + 2) % 3
-    if (k + 2 < ncap) fetch(S2{}, wf * N + n0 + nf);
-    advance(wf, nf);
+    SRF_GUX_FETCH(S2)
     compute(S0{});
     if (k + 1 >= ncap) break;
-    if (k + 3 < ncap) fetch(S0{}, wf * N + n0 + nf);
-    advance(wf, nf);
+    SRF_GUX_FETCH(S0)
     compute(S1{});
     if (k + 2 >= ncap) break;
-    if (k + 4 < ncap) fetch(S1{}, wf * N + n0 + nf);
-    advance(wf, nf);
+    SRF_GUX_FETCH(S1)
     compute(S2{});
   }
+#undef SRF_GUX_FETCH
   __syncthreads();
   const int f0 = ft * 16 - lpad;
   const int row = nn * DIN;
