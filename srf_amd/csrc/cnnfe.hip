@@ -903,6 +903,173 @@ __global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------- dgrad (split-bf16 MFMA)
+// The data gradient on v_mfma_f32_32x32x16_bf16 with 3-term splits, structured as
+// conv2_fwd32_kernel: all four stride-parity classes in one launch (block ranges
+// cls.boff), a workgroup = 4 waves x 32 input pixels of one class, a wave owns its
+// 32 pixels x all 64 cin (two N-tiles).  K = taps of the class x 128 (n) in
+// k-blocks of 16; the A fragments (g_ab rows, split on the VALU) are gathered into
+// registers two k-blocks ahead, the packed pre-split B (wq3[plane][tap][cin][n]) is
+// staged in LDS, double-buffered.
+struct DgCls {
+  int boff[5];   // first block of parity class (qt, qf) = (c >> 1, c & 1); boff[4] = grid
+};
+
+// wq3[plane][tap][cin][n] = split(k_{a|b}[tap][cin][n % C]), one thread per 8 n.
+__global__ void pack_w2t_split_kernel(const float* __restrict__ ka, const float* __restrict__ kb,
+                                      __bf16* __restrict__ wq3) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;   // (tap, cin, n/8)
+  if (idx >= 9 * C * (2 * C / 8)) return;
+  const int n8 = idx % (2 * C / 8), cin = (idx / (2 * C / 8)) % C, tap = idx / (C * (2 * C / 8));
+  const int n = 8 * n8;
+  const float* k = (n < C ? ka : kb) + ((size_t)tap * C + cin) * C + (n % C);
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = k[q];
+  cbf8 p1, p2, p3;
+  split8v(v, p1, p2, p3);
+  const size_t plane = (size_t)9 * C * 2 * C;
+  const size_t o = ((size_t)tap * C + cin) * 2 * C + n;
+  *reinterpret_cast<cbf8*>(wq3 + o) = p1;
+  *reinterpret_cast<cbf8*>(wq3 + plane + o) = p2;
+  *reinterpret_cast<cbf8*>(wq3 + 2 * plane + o) = p3;
+}
+
+constexpr int kD2Waves = 4;
+constexpr int kD2Px = 32 * kD2Waves;
+constexpr int kD2BChunks = 3 * C * 2;   // 16-byte B chunks per k-block (planes x cin x halves)
+
+__global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2))) void conv2_dgrad32_kernel(
+    const float* __restrict__ g_ab, const __bf16* __restrict__ wq3, Dims d, DgCls cls, float* __restrict__ g_x1) {
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][C * kC2BStride];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int bid = blockIdx.x;
+  const int c = (bid >= cls.boff[1]) + (bid >= cls.boff[2]) + (bid >= cls.boff[3]);
+  const int qt = c >> 1, qf = c & 1;
+  const int nkt = (d.T1 - qt + 1) / 2, nkf = (d.F1 - qf + 1) / 2;
+  const int Pc = d.B * nkt * nkf;
+  const int q0 = (bid - cls.boff[c]) * kD2Px;
+  const int dt0 = (qt + d.pt2) & 1, df0 = (qf + d.pf2) & 1;
+  const int ntf = (3 - df0 + 1) / 2, ntt = (3 - dt0 + 1) / 2;
+  const int nkb = ntt * ntf * 8;
+  const size_t plane = (size_t)9 * C * 2 * C;
+
+  // A row of this lane: class pixel q0 + 32 wv + r
+  const int pa = q0 + 32 * wv + r;
+  const bool alive = pa < Pc;
+  const int pcl = min(pa, Pc - 1);
+  const int akf = pcl % nkf, akt = (pcl / nkf) % nkt, ab = pcl / (nkf * nkt);
+  const int at1 = qt + 2 * akt, af1 = qf + 2 * akf;
+  auto tap_of = [&](int k) { return (dt0 + 2 * (k / ntf)) * 3 + df0 + 2 * (k % ntf); };
+
+  constexpr int NBL = (kD2BChunks + 64 * kD2Waves - 1) / (64 * kD2Waves);
+  auto load_b = [&](int kk, cbf8 (&bv)[NBL]) {
+    const int tap = tap_of(kk >> 3), kb = kk & 7;
+#pragma unroll
+    for (int q = 0; q < NBL; ++q) {
+      const int idx = min(q * 64 * kD2Waves + tid, kD2BChunks - 1);
+      const int pl = idx / (2 * C), rem = idx % (2 * C), cin = rem >> 1, half = rem & 1;
+      bv[q] = *reinterpret_cast<const cbf8*>(wq3 + pl * plane + ((size_t)tap * C + cin) * 2 * C + 16 * kb + 8 * half);
+    }
+  };
+  auto store_b = [&](int buf, const cbf8 (&bv)[NBL]) {
+#pragma unroll
+    for (int q = 0; q < NBL; ++q) {
+      const int idx = q * 64 * kD2Waves + tid;
+      if (idx < kD2BChunks) {
+        const int pl = idx / (2 * C), rem = idx % (2 * C), cin = rem >> 1, half = rem & 1;
+        *reinterpret_cast<cbf8*>(&Bs[buf][pl][cin * kC2BStride + 8 * half]) = bv[q];
+      }
+    }
+  };
+  auto load_a = [&](int kk, f4 (&av)[2], bool& ok) {
+    const int tap = tap_of(kk >> 3), kb = kk & 7;
+    const int dt = tap / 3, df = tap - dt * 3;
+    const int t2 = (at1 + d.pt2 - dt) >> 1, f2 = (af1 + d.pf2 - df) >> 1;   // even by the class parity
+    ok = alive && t2 >= 0 && t2 < d.T2 && f2 >= 0 && f2 < d.F2;
+    const int t2c = min(max(t2, 0), d.T2 - 1), f2c = min(max(f2, 0), d.F2 - 1);
+    const float* src = g_ab + (((size_t)ab * d.T2 + t2c) * d.F2 + f2c) * 2 * C + 16 * kb + 8 * h;
+    av[0] = *reinterpret_cast<const f4*>(src);
+    av[1] = *reinterpret_cast<const f4*>(src + 4);
+  };
+
+  cf16 acc[2];
+  acc[0] = cf16{};
+  acc[1] = cf16{};
+  auto compute = [&](int buf, const f4 (&av)[2], bool aok) {
+    cbf8 a1, a2, a3;
+    {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = aok ? (q < 4 ? av[0][q] : av[1][q - 4]) : 0.f;
+      split8v(v, a1, a2, a3);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int nrow = 32 * nt + r;
+      const cbf8 b1 = *reinterpret_cast<const cbf8*>(&Bs[buf][0][nrow * kC2BStride + 8 * h]);
+      const cbf8 b2 = *reinterpret_cast<const cbf8*>(&Bs[buf][1][nrow * kC2BStride + 8 * h]);
+      const cbf8 b3 = *reinterpret_cast<const cbf8*>(&Bs[buf][2][nrow * kC2BStride + 8 * h]);
+      cf16 cc = acc[nt];
+      cc = mfma32bf(a3, b1, cc);
+      cc = mfma32bf(a1, b3, cc);
+      cc = mfma32bf(a2, b2, cc);
+      cc = mfma32bf(a2, b1, cc);
+      cc = mfma32bf(a1, b2, cc);
+      cc = mfma32bf(a1, b1, cc);
+      acc[nt] = cc;
+    }
+  };
+  // two k-blocks ahead, as conv2_fwd32_kernel (nkb is a multiple of 8)
+  cbf8 bvA[NBL], bvB[NBL];
+  f4 avA[2], avB[2];
+  bool okA, okB;
+  load_b(0, bvA);
+  load_a(0, avA, okA);
+  load_b(1, bvB);
+  load_a(1, avB, okB);
+  store_b(0, bvA);
+  __syncthreads();
+  for (int kk = 0; kk < nkb; kk += 2) {
+    {
+      const f4 a0[2] = {avA[0], avA[1]};
+      const bool ok0 = okA;
+      if (kk + 2 < nkb) {
+        load_b(kk + 2, bvA);
+        load_a(kk + 2, avA, okA);
+      }
+      compute(0, a0, ok0);
+      store_b(1, bvB);
+      __syncthreads();
+    }
+    {
+      const f4 a1v[2] = {avB[0], avB[1]};
+      const bool ok1 = okB;
+      if (kk + 3 < nkb) {
+        load_b(kk + 3, bvB);
+        load_a(kk + 3, avB, okB);
+      }
+      compute(1, a1v, ok1);
+      if (kk + 2 < nkb) store_b(0, bvA);
+      __syncthreads();
+    }
+  }
+  // epilogue: lane column r = cin (32 nt + r), rows = pixels 8q + 4h + v of the wave
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int p = q0 + 32 * wv + 8 * q + 4 * h + v;
+      if (p >= Pc) continue;
+      const int kf = p % nkf, kt = (p / nkf) % nkt, b = p / (nkf * nkt);
+      float* dst = g_x1 + (((size_t)b * d.T1 + qt + 2 * kt) * d.F1 + qf + 2 * kf) * C + r;
+      dst[0] = acc[0][4 * q + v];
+      dst[32] = acc[1][4 * q + v];
+    }
+}
+
 // Weight gradient of stage 2 for one tap and one pixel split:
 // part[s][tap][cin][n] = sum_{p in split} xbn1(p, tap)[cin] * g_ab[p][n].
 // K = pixels in chunks of kWgChunk, staged row-major (A [px][cin] with BN1 + mask1
@@ -1353,6 +1520,21 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, nullptr, w.scratch, st, srf::ColSplit{{g_b1a, g_b1b, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
   // stage-2 data gradient (4 stride-parity classes) and weight gradient
+  if (use_conv2_32()) {
+    __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);   // 3 bf16 planes fit the fp32 image
+    hipLaunchKernelGGL(pack_w2t_split_kernel, dim3((9 * C * (2 * C / 8) + 255) / 256), dim3(256), 0, st, k1a, k1b,
+                       wq3);
+    SRF_LAUNCH_CHECK("pack_w2t_split");
+    DgCls cls{};
+    for (int c = 0; c < 4; ++c) {
+      const int qt = c >> 1, qf = c & 1;
+      const int Pc = d.B * ((d.T1 - qt + 1) / 2) * ((d.F1 - qf + 1) / 2);
+      cls.boff[c + 1] = cls.boff[c] + (Pc + kD2Px - 1) / kD2Px;
+    }
+    hipLaunchKernelGGL(conv2_dgrad32_kernel, dim3(cls.boff[4]), dim3(64 * kD2Waves), 0, st, w.g_ab, wq3, d, cls,
+                       w.g_x1);
+    SRF_LAUNCH_CHECK("conv2_dgrad32");
+  } else {
   hipLaunchKernelGGL(pack_w2t_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wq);
   SRF_LAUNCH_CHECK("pack_w2t");
   for (int qt = 0; qt < 2; ++qt) {
@@ -1363,6 +1545,7 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
                          w.g_x1);
       SRF_LAUNCH_CHECK("conv2_dgrad");
     }
+  }
   }
   const int split_len = ((P2 + kWgradSplits - 1) / kWgradSplits + kWgChunk - 1) / kWgChunk * kWgChunk;
   const WgDiv dv{make_fastdiv(d.F2), make_fastdiv(d.T2)};
