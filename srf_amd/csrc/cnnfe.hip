@@ -1183,6 +1183,180 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restric
         dst[(size_t)(mt * 16 + 4 * g + k) * 2 * C + 32 * wv + 16 * nt + l16] = acc[mt][nt][k];
 }
 
+// ---------------------------------------------------------------- wgrad (split-bf16 MFMA)
+// g_ab [P2][n] -> pixel-minor split planes gsT3[plane][n][P2p] (zero past P2), the B
+// operand image of conv2_wgrad32_kernel: 64 pixels per workgroup through LDS.
+constexpr int kTpPx = 64;
+__global__ __launch_bounds__(256) void gab_split_t_kernel(const float* __restrict__ g_ab, int P2, int P2p,
+                                                          __bf16* __restrict__ gsT3) {
+  __shared__ float tile[kTpPx][2 * C + 1];
+  const int tid = threadIdx.x;
+  const int p0 = blockIdx.x * kTpPx;
+  for (int k = tid; k < kTpPx * (2 * C / 4); k += 256) {
+    const int px = k / (2 * C / 4), q = k % (2 * C / 4);
+    const int p = p0 + px;
+    const f4 v = p < P2 ? *reinterpret_cast<const f4*>(g_ab + (size_t)p * 2 * C + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
+    tile[px][4 * q] = v.x;
+    tile[px][4 * q + 1] = v.y;
+    tile[px][4 * q + 2] = v.z;
+    tile[px][4 * q + 3] = v.w;
+  }
+  __syncthreads();
+  const size_t plane = (size_t)2 * C * P2p;
+  for (int task = tid; task < 2 * C * (kTpPx / 8); task += 256) {
+    const int o = task & 7, n = task >> 3;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = tile[8 * o + k][n];
+    cbf8 p1, p2, p3;
+    split8v(v, p1, p2, p3);
+    __bf16* dst = gsT3 + (size_t)n * P2p + p0 + 8 * o;
+    *reinterpret_cast<cbf8*>(dst) = p1;
+    *reinterpret_cast<cbf8*>(dst + plane) = p2;
+    *reinterpret_cast<cbf8*>(dst + 2 * plane) = p3;
+  }
+}
+
+// Weight gradient on v_mfma_f32_32x32x16_bf16 with 3-term splits: per (tap, pixel
+// split) part[s][tap][cin][n] = sum_p x(p, tap)[cin] g_ab[p][n], M = cin (two
+// tiles), N = n (wave w owns n in [32w, 32w+32)), K = pixels in chunks of 32.
+// The A image (BN1 + mask1 applied, split) is staged by the workgroup in LDS as
+// natural [plane][pixel][cin] rows (one pixel x 8 channels per thread: two float4
+// loads, one index decode) and read back transposed into the k = pixel operand with
+// ds_read_b64_tr_b16; double-buffered.  Each wave loads its B fragments (8 pixels of
+// one n, per plane) straight from gsT3, one chunk ahead.
+constexpr int kW2Chunk = 32;
+constexpr int kW2AStride = 96;   // bf16 per pixel row of the A image (64 cin + 32: conflict-free tr reads)
+
+typedef short ws4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ ws4 lds_tr16(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) ws4*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv2_wgrad32_kernel(
+    const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len,
+    const __bf16* __restrict__ gsT3, int P2p, Dims d, WgDiv dv, int nsplit, int split_len, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kW2Chunk * kW2AStride];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  // XCD-aware order (nsplit % 8 == 0): the nine taps of one pixel split run back to
+  // back on one XCD (blocks b, b + 8, ... share an XCD), so its L2 serves the split's
+  // B slab and x rows to all nine
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int tap = loc % 9, sp = xcd + 8 * (loc / 9);
+  const int dt = tap / 3, df = tap - dt * 3;
+  const int P2 = d.B * d.T2 * d.F2;
+  const int pbeg = sp * split_len, pend = min(P2, pbeg + split_len);
+  // staging task: pixel px of the chunk, channels 8 oc .. 8 oc + 7
+  const int px = tid >> 3, oc = tid & 7;
+  float scale[8], shift[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    scale[k] = stats1[2 * C + 8 * oc + k];
+    shift[k] = stats1[3 * C + 8 * oc + k];
+  }
+  f4 xv[2];
+  bool xok = false;
+  auto gather = [&](int pc0) {
+    const int p = pc0 + px;
+    const unsigned pcl = (unsigned)min(p, P2 - 1);
+    const unsigned r1 = fdiv(pcl, dv.f2);
+    const int f2 = (int)(pcl - r1 * d.F2);
+    const unsigned bq = fdiv(r1, dv.t2);
+    const int t2 = (int)(r1 - bq * d.T2), b = (int)bq;
+    const int t1 = 2 * t2 - d.pt2 + dt, f1 = 2 * f2 - d.pf2 + df;
+    xok = p < pend && t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < ceil_div_len(inp_len[b], 2);
+    const int t1c = min(max(t1, 0), d.T1 - 1), f1c = min(max(f1, 0), d.F1 - 1);
+    const float* src = y1 + (((size_t)b * d.T1 + t1c) * d.F1 + f1c) * C + 8 * oc;
+    xv[0] = *reinterpret_cast<const f4*>(src);
+    xv[1] = *reinterpret_cast<const f4*>(src + 4);
+  };
+  auto put = [&](int buf) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = xok ? (k < 4 ? xv[0][k] : xv[1][k - 4]) * scale[k] + shift[k] : 0.f;
+    cbf8 p1, p2, p3;
+    split8v(v, p1, p2, p3);
+    const int o = px * kW2AStride + 8 * oc;
+    *reinterpret_cast<cbf8*>(&As[buf][0][o]) = p1;
+    *reinterpret_cast<cbf8*>(&As[buf][1][o]) = p2;
+    *reinterpret_cast<cbf8*>(&As[buf][2][o]) = p3;
+  };
+  // transposed A read: lane 16 g + 4 q + p reads pixel row 8 (g >> 1) + q (+ 4) of the
+  // k-block, cin 16 (g & 1) + 4 p .. + 3 of the M-tile; it receives cin 16 (g & 1) + (lane & 15)
+  // at pixels 8 (g >> 1) + 0..7 = the 32x32x16 A fragment (row = l & 31, k = 8 (l >> 5) + j)
+  const int gg = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int a_off = (8 * (gg >> 1) + qq) * kW2AStride + 16 * (gg & 1) + 4 * pp;
+  auto read_a = [&](const __bf16* img, int kb, int mt) {
+    const __bf16* base = img + a_off + 16 * kb * kW2AStride + 32 * mt;
+    const ws4 lo = lds_tr16(base), hi = lds_tr16(base + 4 * kW2AStride);
+    return __builtin_bit_cast(cbf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  // B fragments of this wave: n = 32 wv + r, pixels 16 kb + 8 h .. + 7 of the chunk
+  const size_t bplane = (size_t)2 * C * P2p;
+  const __bf16* brow = gsT3 + (size_t)(32 * wv + r) * P2p + 8 * h;
+  cbf8 bc[2][3], bn[2][3];
+  auto load_bf = [&](int pc0, cbf8 (&bf)[2][3]) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bf[kb][pl] = *reinterpret_cast<const cbf8*>(brow + pl * bplane + pc0 + 16 * kb);
+  };
+
+  cf16 acc[2];
+  acc[0] = cf16{};
+  acc[1] = cf16{};
+  const int nch = (pend - pbeg + kW2Chunk - 1) / kW2Chunk;
+  if (nch > 0) {
+    gather(pbeg);
+    load_bf(pbeg, bc);
+    put(0);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const bool more = ch + 1 < nch;
+    const int buf = ch & 1;
+    if (more) {
+      gather(pbeg + (ch + 1) * kW2Chunk);
+      load_bf(pbeg + (ch + 1) * kW2Chunk, bn);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const cbf8 a1 = read_a(As[buf][0], kb, mt);
+        const cbf8 a2 = read_a(As[buf][1], kb, mt);
+        const cbf8 a3 = read_a(As[buf][2], kb, mt);
+        cf16 cc = acc[mt];
+        cc = mfma32bf(a3, bc[kb][0], cc);
+        cc = mfma32bf(a1, bc[kb][2], cc);
+        cc = mfma32bf(a2, bc[kb][1], cc);
+        cc = mfma32bf(a2, bc[kb][0], cc);
+        cc = mfma32bf(a1, bc[kb][1], cc);
+        cc = mfma32bf(a1, bc[kb][0], cc);
+        acc[mt] = cc;
+      }
+    if (more) {
+      put(buf ^ 1);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bc[kb][pl] = bn[kb][pl];
+    }
+    __syncthreads();
+  }
+  // C layout: col = n (32 wv + r), rows = cin 32 mt + 8 q + 4 h + v
+  float* dst = part + ((size_t)sp * 9 + tap) * C * 2 * C + 32 * wv + r;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dst[(size_t)(32 * mt + 8 * q + 4 * h + v) * 2 * C] = acc[mt][4 * q + v];
+}
+
 // Sum the wgrad splits and unpack n -> (conv a|b, cout): gka/gkb [tap][cin][cout].
 __global__ void conv2_wgrad_reduce_kernel(const float* __restrict__ part, int nsplit, float* __restrict__ gka,
                                           float* __restrict__ gkb) {
@@ -1426,11 +1600,23 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
 namespace {
 struct BwdWs2 {
   float *bnpart, *bnsum2, *bnsum1, *g_ab, *biaspart, *g_x1, *wq, *wpart, *c1part, *c1sum, *scratch;
+  __bf16* gsT3;   // split-bf16 g_ab planes, pixel-minor (conv2_wgrad32_kernel)
+  int P2p;
   size_t bytes;
 };
 
 constexpr int kBnBlocks = 1024;
 constexpr int kWgradSplits = 64;
+constexpr int kWgrad32SplitsMax = 128;
+// pixel splits of conv2_wgrad32_kernel (a multiple of 8; SRF_WG32_SPLITS overrides)
+inline int wgrad32_splits() {
+  static const int v = [] {
+    const char* e = getenv("SRF_WG32_SPLITS");
+    const int s = e ? atoi(e) : 56;
+    return std::max(8, std::min(kWgrad32SplitsMax, s / 8 * 8));
+  }();
+  return v;
+}
 
 BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   const size_t P1 = (size_t)d.B * d.T1 * d.F1, P2 = (size_t)d.B * d.T2 * d.F2;
@@ -1442,9 +1628,11 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   };
   const size_t obp = take((size_t)kBnBlocks * 2 * C * 4), os2 = take(2 * C * 4), os1 = take(2 * C * 4),
                oab = take(P2 * 2 * C * 4), obias = take((size_t)kBnBlocks * 2 * C * 4), ogx = take(P1 * C * 4),
-               owq = take((size_t)9 * 2 * C * C * 4), owp = take((size_t)kWgradSplits * 9 * C * 2 * C * 4),
+               owq = take((size_t)9 * 2 * C * C * 4), owp = take((size_t)std::max(kWgradSplits, kWgrad32SplitsMax) * 9 * C * 2 * C * 4),
                oc1 = take((size_t)conv1_blocks(d) * 20 * C * 4), oc1s = take(20 * C * 4),
                oscr = take(srf::colsum_scratch_floats(std::max(conv1_blocks(d), kBnBlocks), 20 * C) * 4);
+  const int P2p = (int)((P2 + kTpPx - 1) / kTpPx * kTpPx);
+  const size_t ogs3 = take((size_t)3 * 2 * C * P2p * 2);
   char* b = static_cast<char*>(base);
   BwdWs2 w;
   w.bnpart = (float*)(b + obp);
@@ -1458,6 +1646,8 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   w.c1part = (float*)(b + oc1);
   w.c1sum = (float*)(b + oc1s);
   w.scratch = (float*)(b + oscr);
+  w.gsT3 = (__bf16*)(b + ogs3);
+  w.P2p = P2p;
   w.bytes = off;
   return w;
 }
@@ -1547,13 +1737,29 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
     }
   }
   }
-  const int split_len = ((P2 + kWgradSplits - 1) / kWgradSplits + kWgChunk - 1) / kWgChunk * kWgChunk;
   const WgDiv dv{make_fastdiv(d.F2), make_fastdiv(d.T2)};
-  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(9 * kWgradSplits), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, w.g_ab,
-                     d, dv, kWgradSplits, split_len, w.wpart);
-  SRF_LAUNCH_CHECK("conv2_wgrad");
+  int nsplit = kWgradSplits;
+  static const bool wg32 = [] {
+    const char* e = getenv("SRF_WGRAD32");
+    return !(e && e[0] == '0');
+  }();
+  if (use_conv2_32() && wg32) {
+    static_assert(kW2Chunk == kWgChunk, "wgrad splits are whole chunks");
+    nsplit = wgrad32_splits();
+    const int split_len = ((P2 + nsplit - 1) / nsplit + kWgChunk - 1) / kWgChunk * kWgChunk;
+    hipLaunchKernelGGL(gab_split_t_kernel, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p, w.gsT3);
+    SRF_LAUNCH_CHECK("gab_split_t");
+    hipLaunchKernelGGL(conv2_wgrad32_kernel, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, w.gsT3,
+                       w.P2p, d, dv, nsplit, split_len, w.wpart);
+    SRF_LAUNCH_CHECK("conv2_wgrad32");
+  } else {
+    const int split_len = ((P2 + nsplit - 1) / nsplit + kWgChunk - 1) / kWgChunk * kWgChunk;
+    hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, w.g_ab, d,
+                       dv, nsplit, split_len, w.wpart);
+    SRF_LAUNCH_CHECK("conv2_wgrad");
+  }
   hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((9 * C * 2 * C + 255) / 256), dim3(256), 0, st, w.wpart,
-                     kWgradSplits, g_k1a, g_k1b);
+                     nsplit, g_k1a, g_k1b);
   SRF_LAUNCH_CHECK("conv2_wgrad_reduce");
   // BN1 backward sums, then stage-1 gradients
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, w.g_x1, sv.y1, sv.stats1, inp_len, d.B,
