@@ -10,9 +10,14 @@
 // utterance (T_b too short for its labels) yields nll = +inf and a zero gradient.
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "srf_common.h"
 #include "../../include/srf.h"
+
+#ifndef SRF_CTC_DBG
+#define SRF_CTC_DBG 0
+#endif
 
 namespace {
 
@@ -20,6 +25,17 @@ __device__ __forceinline__ float lse2(float a, float b) {
   const float m = fmaxf(a, b);
   if (m == -INFINITY) return -INFINITY;
   return m + __logf(__expf(a - m) + __expf(b - m));
+}
+
+// Branch-free log(e^a + e^b) for the serial recursions: with m = max(a, b) taken as
+// 0 when both are -inf, e^(a-m) + e^(b-m) is 0 there and v_log_f32 returns -inf; the
+// sum lies in [1, 2] otherwise, so the raw exp2/log2 instructions need no range fix-up.
+__device__ __forceinline__ float lse2f(float a, float b) {
+  constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  const float m = fmaxf(a, b);
+  const float ms = m == -INFINITY ? 0.f : m;
+  const float z = __builtin_amdgcn_exp2f((a - ms) * kLog2e) + __builtin_amdgcn_exp2f((b - ms) * kLog2e);
+  return ms + __builtin_amdgcn_logf(z) * kLn2;
 }
 
 // Wave-resident recursions (KM > 0, S <= 64*KM): wave 0 holds states
@@ -37,22 +53,28 @@ __device__ __forceinline__ float dpp_wave_shl1(float old, float src) {   // lane
 __device__ __forceinline__ float read_lane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+// The emission row of step t + 1 is read while step t's log-sum-exps run.
 template <int KM>
 __device__ __forceinline__ float alpha_wave(const int* __restrict__ ext, const float* __restrict__ lp, int C, int S,
                                             int Tb, int Smax, int blank, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
-  float a[KM];
+  float a[KM], em[KM];
   int e[KM];
-  bool sk[KM];
+  bool sk[KM], live[KM];
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int s = lane + 64 * k;
-    e[k] = s < S ? ext[s] : blank;
-    sk[k] = s < S && s >= 2 && ext[s] != blank && ext[s] != ext[s - 2];
+    live[k] = s < S;
+    e[k] = live[k] ? ext[s] : blank;
+    sk[k] = live[k] && s >= 2 && ext[s] != blank && ext[s] != ext[s - 2];
     a[k] = -INFINITY;
+    em[k] = Tb > 0 ? lp[e[k]] : 0.f;
   }
   for (int t = 0; t < Tb; ++t) {
-    const float* lpt = lp + (size_t)t * C;
+    float emn[KM];
+    const int tn = min(t + 1, Tb - 1);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) emn[k] = lp[(size_t)tn * C + e[k]];
     float na[KM];
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -65,15 +87,18 @@ __device__ __forceinline__ float alpha_wave(const int* __restrict__ ext, const f
         const float l62 = k > 0 ? read_lane(a[k - 1], 62) : -INFINITY;
         const float p1 = dpp_wave_shr1(l63, a[k]);    // state s - 1
         const float p2 = dpp_wave_shr1(l62, p1);      // state s - 2
-        v = lse2(a[k], p1);
-        if (sk[k]) v = lse2(v, p2);
+        v = lse2f(a[k], p1);
+        v = lse2f(v, sk[k] ? p2 : -INFINITY);
       }
-      v = (s < S && v != -INFINITY) ? v + lpt[e[k]] : -INFINITY;
+      v = live[k] ? v + em[k] : -INFINITY;            // -inf stays -inf
       na[k] = v;
-      if (s < S) out[(size_t)t * Smax + s] = v;
+      if (live[k]) out[(size_t)t * Smax + s] = v;
     }
 #pragma unroll
-    for (int k = 0; k < KM; ++k) a[k] = na[k];
+    for (int k = 0; k < KM; ++k) {
+      a[k] = na[k];
+      em[k] = emn[k];
+    }
   }
   // log-likelihood: the last two states at t = Tb-1
   float loc = -INFINITY;
@@ -94,18 +119,23 @@ template <int KM>
 __device__ __forceinline__ void beta_wave(const int* __restrict__ ext, const float* __restrict__ lp, int C, int S,
                                           int Tb, int Smax, int blank, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
-  float a[KM];
+  float a[KM], em[KM];
   int e[KM];
-  bool sk[KM];
+  bool sk[KM], live[KM];
 #pragma unroll
   for (int k = 0; k < KM; ++k) {
     const int s = lane + 64 * k;
-    e[k] = s < S ? ext[s] : blank;
+    live[k] = s < S;
+    e[k] = live[k] ? ext[s] : blank;
     sk[k] = s + 2 < S && ext[s] != blank && ext[s] != ext[s + 2];
     a[k] = -INFINITY;
+    em[k] = Tb > 0 ? lp[(size_t)(Tb - 1) * C + e[k]] : 0.f;
   }
   for (int t = Tb - 1; t >= 0; --t) {
-    const float* lpt = lp + (size_t)t * C;
+    float emn[KM];
+    const int tn = max(t - 1, 0);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) emn[k] = lp[(size_t)tn * C + e[k]];
     float na[KM];
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -118,30 +148,36 @@ __device__ __forceinline__ void beta_wave(const int* __restrict__ ext, const flo
         const float h1 = k + 1 < KM ? read_lane(a[k + 1], 1) : -INFINITY;
         const float q1 = dpp_wave_shl1(h0, a[k]);     // state s + 1
         const float q2 = dpp_wave_shl1(h1, q1);       // state s + 2
-        v = lse2(a[k], q1);
-        if (sk[k]) v = lse2(v, q2);
+        v = lse2f(a[k], q1);
+        v = lse2f(v, sk[k] ? q2 : -INFINITY);
       }
-      v = (s < S && v != -INFINITY) ? v + lpt[e[k]] : -INFINITY;
+      v = live[k] ? v + em[k] : -INFINITY;
       na[k] = v;
-      if (s < S) out[(size_t)t * Smax + s] = v;
+      if (live[k]) out[(size_t)t * Smax + s] = v;
     }
 #pragma unroll
-    for (int k = 0; k < KM; ++k) a[k] = na[k];
+    for (int k = 0; k < KM; ++k) {
+      a[k] = na[k];
+      em[k] = emn[k];
+    }
   }
 }
 
 // Recursion kernel: grid (B, 2).  Block (b, 0) runs the alpha recursion and
 // writes nll[b]; block (b, 1) runs beta.  Both recompute the log-softmax into
-// LDS (when it fits; else workspace) and stream their rows to workspace.
+// LDS (LPLDS; else workspace) and stream their rows to workspace.
 // Dynamic LDS: ext[Smax] (int) | row[2][Smax] | lp[T*C].
-template <int KM>
+template <int KM, bool LPLDS>
 __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restrict__ logits,
                                                             const int* __restrict__ labels,
                                                             const int* __restrict__ label_len,
                                                             const int* __restrict__ logit_len, int Tmax, int C,
-                                                            int Lmax, int blank, int lp_in_lds, int want_beta,
+                                                            int Lmax, int blank, int want_beta,
                                                             float* __restrict__ nll, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+#if SRF_CTC_DBG
+  const unsigned long long t_beg = __builtin_amdgcn_s_memtime();
+#endif
   const int Smax = 2 * Lmax + 1;
   int* ext = reinterpret_cast<int*>(smem);
   float* row = smem + Smax;
@@ -153,31 +189,27 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
   const int S = 2 * L + 1;
   float* gws = ws + (size_t)b * Tmax * (C + 2 * Smax);
   float* lpg = gws;                                       // [Tmax][C] (global copy, for the gradient)
-  float* lp = lp_in_lds ? (row + 2 * Smax) : lpg;
+  float* lp = LPLDS ? (row + 2 * Smax) : lpg;
   float* out = gws + (size_t)Tmax * C + (is_beta ? (size_t)Tmax * Smax : 0);
   const float* lg = logits + (size_t)b * Tmax * C;
   for (int s = threadIdx.x; s < S; s += blockDim.x) ext[s] = (s & 1) ? labels[(size_t)b * Lmax + (s >> 1)] : blank;
-  if (C <= 64) {
-    // one class per lane; 8 rows per wave in flight, so the row loads overlap
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
-    constexpr int RB = 8;
-    for (int t0 = w * RB; t0 < Tb; t0 += nw * RB) {
-      float v[RB];
-#pragma unroll
-      for (int r = 0; r < RB; ++r) v[r] = (l < C && t0 + r < Tb) ? lg[(size_t)(t0 + r) * C + l] : -INFINITY;
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        float m = v[r];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        const float z = wave_sum(l < C ? __expf(v[r] - m) : 0.f);
-        const float lz = m + __logf(z);
-        if (l < C && t0 + r < Tb) {
-          const size_t o = (size_t)(t0 + r) * C + l;
-          lp[o] = v[r] - lz;
-          if (!is_beta && lp_in_lds) lpg[o] = v[r] - lz;
-        }
-      }
+  if constexpr (LPLDS) {
+    // rows staged into LDS (coalesced), then one thread per row: max, log-sum-exp,
+    // normalise in place; the alpha block copies the rows out for the gradient kernel
+    for (int i = threadIdx.x; i < Tb * C; i += blockDim.x) lp[i] = lg[i];
+    __syncthreads();
+    for (int t = threadIdx.x; t < Tb; t += blockDim.x) {
+      float* r = lp + (size_t)t * C;
+      float m = -INFINITY;
+      for (int c = 0; c < C; ++c) m = fmaxf(m, r[c]);
+      float z = 0.f;
+      for (int c = 0; c < C; ++c) z += __expf(r[c] - m);
+      const float lz = m + __logf(z);
+      for (int c = 0; c < C; ++c) r[c] -= lz;
+    }
+    if (!is_beta) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < Tb * C; i += blockDim.x) lpg[i] = lp[i];
     }
   } else {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
@@ -190,14 +222,13 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
       for (int c = l; c < C; c += 64) z += __expf(lg[(size_t)t * C + c] - m);
       z = wave_sum(z);
       const float lz = m + __logf(z);
-      for (int c = l; c < C; c += 64) {
-        const float v = lg[(size_t)t * C + c] - lz;
-        lp[(size_t)t * C + c] = v;
-        if (!is_beta && lp_in_lds) lpg[(size_t)t * C + c] = v;
-      }
+      for (int c = l; c < C; c += 64) lp[(size_t)t * C + c] = lg[(size_t)t * C + c] - lz;
     }
   }
   __syncthreads();
+#if SRF_CTC_DBG
+  const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
+#endif
   if constexpr (KM > 0) {
     if (threadIdx.x >= 64) return;
     if (!is_beta) {
@@ -206,6 +237,12 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
     } else {
       beta_wave<KM>(ext, lp, C, S, Tb, Smax, blank, out);
     }
+#if SRF_CTC_DBG
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0 && b == 0)
+      printf("ctc blk %d beta %d: prologue %llu recursion %llu (S=%d Tb=%d C=%d)\n", b, (int)is_beta, t_pro - t_beg,
+             t_end - t_pro, S, Tb, C);
+#endif
     return;
   }
   if (!is_beta) {
@@ -330,19 +367,23 @@ int srf_ctc_loss(const float* logits, const int* labels, const int* label_len, c
   const size_t Smax = 2 * (size_t)Lmax + 1;
   size_t shmem = 3 * Smax * sizeof(float);
   const size_t lp_bytes = (size_t)Tmax * C * sizeof(float);
-  const int lp_in_lds = (shmem + lp_bytes) <= 96 * 1024;
+  const bool lp_in_lds = (shmem + lp_bytes) <= 96 * 1024;
   if (lp_in_lds) shmem += lp_bytes;
   hipStream_t st = static_cast<hipStream_t>(stream);
   // wave-resident recursion for up to 512 extended-label states, else the block loop;
   // SRF_CTC_WAVE=0 selects the block loop (A/B, tests)
   const char* ev = getenv("SRF_CTC_WAVE");
   const bool wave = !(ev && ev[0] == '0');
-  auto kern = !wave || Smax > 512 ? ctc_recursion_kernel<0>
-              : Smax <= 128      ? ctc_recursion_kernel<2>
-              : Smax <= 256      ? ctc_recursion_kernel<4>
-                                 : ctc_recursion_kernel<8>;
+  auto pick = [&](auto lds) {
+    constexpr bool LDS = decltype(lds)::value;
+    return !wave || Smax > 512 ? ctc_recursion_kernel<0, LDS>
+           : Smax <= 128      ? ctc_recursion_kernel<2, LDS>
+           : Smax <= 256      ? ctc_recursion_kernel<4, LDS>
+                              : ctc_recursion_kernel<8, LDS>;
+  };
+  auto kern = lp_in_lds ? pick(std::true_type{}) : pick(std::false_type{});
   hipLaunchKernelGGL(kern, dim3(B, 2), dim3(256), shmem, st, logits, labels, label_len, logit_len, Tmax, C, Lmax,
-                     blank, lp_in_lds, grad ? 1 : 0, nll, static_cast<float*>(workspace));
+                     blank, grad ? 1 : 0, nll, static_cast<float*>(workspace));
   SRF_LAUNCH_CHECK("ctc_recursion");
   if (grad) {
     hipLaunchKernelGGL(ctc_grad_kernel, dim3(B, (Tmax + 15) / 16), dim3(256), (size_t)(C + Lmax + 1) * sizeof(int),

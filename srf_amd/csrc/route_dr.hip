@@ -1365,12 +1365,15 @@ __global__ void fwd_finish_kernel(const float* __restrict__ slab, int n_chunks, 
 
 // gs = squash'(s)^T a with a = a_init (the upstream gradient of the last
 // iteration's v) or, for earlier iterations, a = A += sum of gVc slabs.
+// zero4 / nz4: float4s zeroed by the same launch (the g_emb accumulator of the gu pass).
 template <int DOUT>
 __global__ void bwd_finish_kernel(const float* __restrict__ slab, int n_chunks, size_t FJD,
                                   const float* __restrict__ a_init, float* __restrict__ A,
-                                  const float* __restrict__ s, float* __restrict__ gs) {
+                                  const float* __restrict__ s, float* __restrict__ gs, float* __restrict__ zero4,
+                                  size_t nz4) {
   constexpr int Q = DOUT / 4;
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < nz4) st4(zero4 + idx * 4, f4{0.f, 0.f, 0.f, 0.f});
   const bool ok = idx < FJD / 4;
   const size_t off = (ok ? idx : 0) * 4;
   f4 a;
@@ -1473,10 +1476,12 @@ void launch_fwd_finish(const Geom& g, const float* slab, int n_chunks, const flo
 
 template <int D>
 void launch_bwd_finish(const Geom& g, const float* slab, int n_chunks, const float* a_init, float* A,
-                       const float* s, float* gs, hipStream_t st) {
+                       const float* s, float* gs, hipStream_t st, float* zero = nullptr, size_t n_zero = 0) {
   const size_t FJD = (size_t)g.F() * g.JD();
-  hipLaunchKernelGGL((bwd_finish_kernel<D>), dim3((FJD / 4 + 255) / 256), dim3(256), 0, st, slab, n_chunks, FJD,
-                     a_init, A, s, gs);
+  const size_t nz4 = zero ? n_zero / 4 : 0;
+  const size_t n = std::max(FJD / 4, nz4);
+  hipLaunchKernelGGL((bwd_finish_kernel<D>), dim3((n + 255) / 256), dim3(256), 0, st, slab, n_chunks, FJD, a_init,
+                     A, s, gs, zero, nz4);
 }
 
 // row tiles per wave in the gu pass (a wave must hold whole output capsules)
@@ -1819,12 +1824,14 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   const int Fp = padded_frames(g);
   // gs^{R-1} = squash'(s^{R-1}) g_v.  A accumulates sum_{r'>r} gVc^{r'}, the
   // gradient of v^r for r < R-1 (those v reach the loss only through the logits).
-  launch_bwd_finish<D>(g, nullptr, n_chunks, g_v, w.A, saved + (size_t)(2 * (R - 1)) * FJD,
-                       w.gs + (size_t)(R - 1) * FJD, st);
-  SRF_LAUNCH_CHECK("bwd_finish");
   // Iteration 0 needs no backward pass: Vc^0 = 0, so its couplings are uniform
   // and its logits carry no gradient.
   const bool p32 = couplings != nullptr && w.p32 != nullptr && R > 1;
+  const size_t n_emb = (size_t)g.F() * g.N * g.din;
+  // with stored couplings this launch also zeroes g_emb (the gu pass accumulates into it)
+  launch_bwd_finish<D>(g, nullptr, n_chunks, g_v, w.A, saved + (size_t)(2 * (R - 1)) * FJD,
+                       w.gs + (size_t)(R - 1) * FJD, st, p32 ? g_emb : nullptr, n_emb);
+  SRF_LAUNCH_CHECK("bwd_finish");
   srf::Fwd32Plan plan{};
   srf::Fwd32Cpl cl{};
   if (p32) {
@@ -1854,11 +1861,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     }
     SRF_LAUNCH_CHECK("bwd_finish");
   }
-  const size_t n_emb = (size_t)g.F() * g.N * g.din;
-  if (p32) {
-    // W^T is in the coupling storage; g_emb is accumulated by the gu pass through the window adjoint
-    SRF_HIP_TRY(hipMemsetAsync(g_emb, 0, n_emb * sizeof(float), st));
-  } else {
+  if (!p32) {
     // W^T for the gu pass; the same launch zeroes g_emb
     const size_t total = (size_t)g.in_n() * g.JD() * g.din + n_emb;
     hipLaunchKernelGGL(transpose_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, g.in_n(), g.JD(), g.din,
