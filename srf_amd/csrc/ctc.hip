@@ -38,6 +38,18 @@ __device__ __forceinline__ float lse2f(float a, float b) {
   return ms + __builtin_amdgcn_logf(z) * kLn2;
 }
 
+// log(e^a + e^b + e^c) in one step (one max3, three exp, one log; the sum lies in
+// [1, 3], or is 0 when all three are -inf), so a recursion step has one
+// log-sum-exp on its serial chain instead of two nested ones.
+__device__ __forceinline__ float lse3(float a, float b, float c) {
+  constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  const float m = fmaxf(fmaxf(a, b), c);
+  const float ms = m == -INFINITY ? 0.f : m;
+  const float z = __builtin_amdgcn_exp2f((a - ms) * kLog2e) + __builtin_amdgcn_exp2f((b - ms) * kLog2e) +
+                  __builtin_amdgcn_exp2f((c - ms) * kLog2e);
+  return ms + __builtin_amdgcn_logf(z) * kLn2;
+}
+
 // Wave-resident recursions (KM > 0, S <= 64*KM): wave 0 holds states
 // s = lane + 64k in registers; the s-1 / s-2 (alpha) or s+1 / s+2 (beta)
 // neighbours come from DPP whole-wave shifts (wave_shr:1 / wave_shl:1, a VALU
@@ -58,6 +70,7 @@ template <int KM>
 __device__ __forceinline__ float alpha_wave(const int* __restrict__ ext, const float* __restrict__ lp, int C, int S,
                                             int Tb, int Smax, int blank, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
+  const auto ors = __builtin_amdgcn_make_buffer_rsrc(out, 0, Tb * Smax * 4, 0x00020000);
   float a[KM], em[KM];
   int e[KM];
   bool sk[KM], live[KM];
@@ -87,12 +100,13 @@ __device__ __forceinline__ float alpha_wave(const int* __restrict__ ext, const f
         const float l62 = k > 0 ? read_lane(a[k - 1], 62) : -INFINITY;
         const float p1 = dpp_wave_shr1(l63, a[k]);    // state s - 1
         const float p2 = dpp_wave_shr1(l62, p1);      // state s - 2
-        v = lse2f(a[k], p1);
-        v = lse2f(v, sk[k] ? p2 : -INFINITY);
+        v = lse3(a[k], p1, sk[k] ? p2 : -INFINITY);
       }
       v = live[k] ? v + em[k] : -INFINITY;            // -inf stays -inf
       na[k] = v;
-      if (live[k]) out[(size_t)t * Smax + s] = v;
+      // no exec branch on the serial path: dead lanes store out of the buffer's range
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, live[k] ? (uint32_t)(t * Smax + s) * 4 : 0x80000000u,
+                                            0, 0);
     }
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -119,6 +133,7 @@ template <int KM>
 __device__ __forceinline__ void beta_wave(const int* __restrict__ ext, const float* __restrict__ lp, int C, int S,
                                           int Tb, int Smax, int blank, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
+  const auto ors = __builtin_amdgcn_make_buffer_rsrc(out, 0, Tb * Smax * 4, 0x00020000);
   float a[KM], em[KM];
   int e[KM];
   bool sk[KM], live[KM];
@@ -148,12 +163,13 @@ __device__ __forceinline__ void beta_wave(const int* __restrict__ ext, const flo
         const float h1 = k + 1 < KM ? read_lane(a[k + 1], 1) : -INFINITY;
         const float q1 = dpp_wave_shl1(h0, a[k]);     // state s + 1
         const float q2 = dpp_wave_shl1(h1, q1);       // state s + 2
-        v = lse2f(a[k], q1);
-        v = lse2f(v, sk[k] ? q2 : -INFINITY);
+        v = lse3(a[k], q1, sk[k] ? q2 : -INFINITY);
       }
       v = live[k] ? v + em[k] : -INFINITY;
       na[k] = v;
-      if (live[k]) out[(size_t)t * Smax + s] = v;
+      // no exec branch on the serial path: dead lanes store out of the buffer's range
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ors, live[k] ? (uint32_t)(t * Smax + s) * 4 : 0x80000000u,
+                                            0, 0);
     }
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -196,15 +212,26 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
   if constexpr (LPLDS) {
     // rows staged into LDS (coalesced), then one thread per row: max, log-sum-exp,
     // normalise in place; the alpha block copies the rows out for the gradient kernel
-    for (int i = threadIdx.x; i < Tb * C; i += blockDim.x) lp[i] = lg[i];
+    const int n = Tb * C;
+    for (int i0 = threadIdx.x; i0 < n; i0 += 8 * 256) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = lg[min(i0 + u * 256, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u * 256 < n) lp[i0 + u * 256] = v[u];
+    }
     __syncthreads();
     for (int t = threadIdx.x; t < Tb; t += blockDim.x) {
       float* r = lp + (size_t)t * C;
       float m = -INFINITY;
-      for (int c = 0; c < C; ++c) m = fmaxf(m, r[c]);
+#pragma unroll 8
+      for (int c = 0; c < C; ++c) m = r[c] > m ? r[c] : m;
       float z = 0.f;
+#pragma unroll 8
       for (int c = 0; c < C; ++c) z += __expf(r[c] - m);
       const float lz = m + __logf(z);
+#pragma unroll 8
       for (int c = 0; c < C; ++c) r[c] -= lz;
     }
     if (!is_beta) {
@@ -296,49 +323,69 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
 }
 
 // Gradient kernel: grid (B, ceil(Tmax/16)), 256 threads = 16 frames x 16 class
-// lanes.  Per class the label positions are walked through a per-block
-// next-occurrence list (built in LDS), so a frame costs O(L + C), not O(C * L).
+// lanes.  Per class the label positions are walked through a next-occurrence list
+// (built in LDS, one thread per label position), over alpha + beta of the block's
+// 16 frames staged in LDS, so a frame costs O(L + C) LDS reads, not O(C * L) loads.
+// Dynamic LDS: head[C] | next[Lmax] (int) | ab[16][Smax].
 __global__ __launch_bounds__(256) void ctc_grad_kernel(const int* __restrict__ labels,
                                                        const int* __restrict__ label_len,
                                                        const int* __restrict__ logit_len,
                                                        const float* __restrict__ nll, int Tmax, int C, int Lmax,
                                                        int blank, float scale, const float* __restrict__ ws,
                                                        float* __restrict__ grad) {
-  extern __shared__ int lists[];   // head[C] | next[Lmax]
+  extern __shared__ int lists[];
   int* head = lists;
   int* next = lists + C;
+  const int Smax = 2 * Lmax + 1;
+  float* ab = reinterpret_cast<float*>(lists + C + Lmax);
   const int b = blockIdx.x;
   const int L = label_len[b];
   const int Tb = min(logit_len[b], Tmax);
-  const int Smax = 2 * Lmax + 1;
   const float ll = -nll[b];
   const bool feasible = ll > -INFINITY;
-  if (threadIdx.x == 0) {
-    for (int c = 0; c < C; ++c) head[c] = -1;
-    for (int k = L - 1; k >= 0; --k) {
-      const int c = labels[(size_t)b * Lmax + k];
-      next[k] = head[c];
-      head[c] = k;
-    }
-  }
-  __syncthreads();
+  const int* lab = labels + (size_t)b * Lmax;
+  const int t0 = blockIdx.y * 16;
   const float* gws = ws + (size_t)b * Tmax * (C + 2 * Smax);
   const float* lp = gws;
   const float* alpha = gws + (size_t)Tmax * C;
   const float* beta = alpha + (size_t)Tmax * Smax;
-  const int t = blockIdx.y * 16 + (threadIdx.x >> 4);
+  // first occurrence of each class and next occurrence of each label position
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    int h = -1;
+    for (int k = L - 1; k >= 0; --k) h = lab[k] == c ? k : h;
+    head[c] = h;
+  }
+  for (int k = threadIdx.x; k < L; k += blockDim.x) {
+    const int c = lab[k];
+    int nx = -1;
+    for (int k2 = L - 1; k2 > k; --k2) nx = lab[k2] == c ? k2 : nx;
+    next[k] = nx;
+  }
+  const int S = 2 * L + 1;
+  const int nt = min(16, Tb - t0);
+  for (int i = threadIdx.x; i < 16 * S; i += blockDim.x) {
+    const int tt = i / S, sidx = i - tt * S;
+    float v = -INFINITY;
+    if (tt < nt) {
+      const size_t o = (size_t)(t0 + tt) * Smax + sidx;
+      v = alpha[o] + beta[o];
+    }
+    ab[tt * Smax + sidx] = v;
+  }
+  __syncthreads();
+  const int tt = threadIdx.x >> 4;
+  const int t = t0 + tt;
   if (t >= Tmax) return;
   float* gb = grad + ((size_t)b * Tmax + t) * C;
+  const float* abt = ab + tt * Smax;
   for (int c = threadIdx.x & 15; c < C; c += 16) {
     float g = 0.f;
     if (t < Tb && feasible) {
       float acc = -INFINITY;
-      const float* at = alpha + (size_t)t * Smax;
-      const float* bt = beta + (size_t)t * Smax;
       if (c == blank) {
-        for (int s = 0; s <= 2 * L; s += 2) acc = lse2(acc, at[s] + bt[s]);
+        for (int s2 = 0; s2 <= 2 * L; s2 += 2) acc = lse2f(acc, abt[s2]);
       } else {
-        for (int k = head[c]; k >= 0; k = next[k]) acc = lse2(acc, at[2 * k + 1] + bt[2 * k + 1]);
+        for (int k = head[c]; k >= 0; k = next[k]) acc = lse2f(acc, abt[2 * k + 1]);
       }
       const float l = lp[(size_t)t * C + c];
       g = (__expf(l) - (acc == -INFINITY ? 0.f : __expf(acc - l - ll))) * scale;
@@ -386,7 +433,8 @@ int srf_ctc_loss(const float* logits, const int* labels, const int* label_len, c
                      blank, grad ? 1 : 0, nll, static_cast<float*>(workspace));
   SRF_LAUNCH_CHECK("ctc_recursion");
   if (grad) {
-    hipLaunchKernelGGL(ctc_grad_kernel, dim3(B, (Tmax + 15) / 16), dim3(256), (size_t)(C + Lmax + 1) * sizeof(int),
+    hipLaunchKernelGGL(ctc_grad_kernel, dim3(B, (Tmax + 15) / 16), dim3(256),
+                       (size_t)(C + Lmax + 16 * Smax) * sizeof(int),
                        st, labels, label_len, logit_len, nll, Tmax, C, Lmax, blank, grad_scale,
                        static_cast<const float*>(workspace), grad);
   }
