@@ -1397,24 +1397,39 @@ __global__ __launch_bounds__(256) void conv1_bwd_kernel(
   if (t1 < d.T1) {
     const float mask = t1 < ceil_div_len(inp_len[tl.b], 2) ? 1.f : 0.f;
     const int pbase = (tl.b * d.T1 + t1) * d.F1;
-#pragma unroll 2
-    for (int f1 = 0; f1 < d.F1; ++f1) {
-      const int o = (pbase + f1) * C + c;
-      const float gy = bn_bwd_elem(g_x1[o], y1[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
-      const bool sl = sel1[o] != 0;
-      float ga = sl ? gy : 0.f, gb = sl ? 0.f : gy;
-      if (drop_p > 0.f) {
-        ga *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
-        gb *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
-      }
-      float x[9];
-      window9_lds(win, tl, d, w, f1, x);
-      acc[18] += ga;
-      acc[19] += gb;
+    // columns in batches of 8: the batch's loads are all in flight before the first use
+    constexpr int FB = 8;
+    for (int f0 = 0; f0 < d.F1; f0 += FB) {
+      float gxv[FB], yv[FB];
+      unsigned char sv[FB];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        acc[k] += x[k] * ga;
-        acc[9 + k] += x[k] * gb;
+      for (int u = 0; u < FB; ++u) {
+        const int o = (pbase + min(f0 + u, d.F1 - 1)) * C + c;
+        gxv[u] = g_x1[o];
+        yv[u] = y1[o];
+        sv[u] = sel1[o];
+      }
+#pragma unroll
+      for (int u = 0; u < FB; ++u) {
+        const int f1 = f0 + u;
+        if (f1 >= d.F1) break;
+        const int o = (pbase + f1) * C + c;
+        const float gy = bn_bwd_elem(gxv[u], yv[u], mask, mean, rstd, gam, sdy_n, sdyxh_n);
+        const bool sl = sv[u] != 0;
+        float ga = sl ? gy : 0.f, gb = sl ? 0.f : gy;
+        if (drop_p > 0.f) {
+          ga *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
+          gb *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
+        }
+        float x[9];
+        window9_lds(win, tl, d, w, f1, x);
+        acc[18] += ga;
+        acc[19] += gb;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          acc[k] += x[k] * ga;
+          acc[9 + k] += x[k] * gb;
+        }
       }
     }
   }
