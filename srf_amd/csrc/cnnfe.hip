@@ -145,8 +145,10 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
       }
       const int o = (pbase + f1) * C + c;
       if (drop) {
-        a *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
-        bv *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
+        bool ka, kb;
+        srf_keep2(seed, kStreamConv0a, o, drop_p, ka, kb);
+        a *= ka ? keep_scale : 0.f;
+        bv *= kb ? keep_scale : 0.f;
       }
       const bool sl = a >= bv;  // TF Maximum gradient: ties go to the first operand
       const float y = live ? (sl ? a : bv) : 0.f;
@@ -396,8 +398,10 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
       const size_t o = (size_t)p * C + c;
       float a = acc[mt][0][k] + bia, bv = acc[mt][1][k] + bib;
       if (training && drop_p > 0.f) {
-        a *= srf_keep(seed, kStreamConv1a, o, drop_p) ? keep_scale : 0.f;
-        bv *= srf_keep(seed, kStreamConv1b, o, drop_p) ? keep_scale : 0.f;
+        bool ka, kb;
+        srf_keep2(seed, kStreamConv1a, o, drop_p, ka, kb);
+        a *= ka ? keep_scale : 0.f;
+        bv *= kb ? keep_scale : 0.f;
       }
       const bool sel = a >= bv;
       float y = sel ? a : bv;
@@ -619,8 +623,10 @@ __global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2
         const size_t o = (size_t)p * C + c;
         float a = acc[g][4 * q + v] + bia, bvv = acc[2 + g][4 * q + v] + bib;
         if (training && drop_p > 0.f) {
-          a *= srf_keep(seed, kStreamConv1a, o, drop_p) ? keep_scale : 0.f;
-          bvv *= srf_keep(seed, kStreamConv1b, o, drop_p) ? keep_scale : 0.f;
+          bool ka, kb;
+          srf_keep2(seed, kStreamConv1a, o, drop_p, ka, kb);
+          a *= ka ? keep_scale : 0.f;
+          bvv *= kb ? keep_scale : 0.f;
         }
         const bool sel = a >= bvv;
         float y = sel ? a : bvv;
@@ -759,8 +765,10 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     const bool s = sel2[o] != 0;
     float ga = s ? gy : 0.f, gb = s ? 0.f : gy;
     if (drop_p > 0.f) {
-      ga *= srf_keep(seed, kStreamConv1a, o, drop_p) ? keep_scale : 0.f;
-      gb *= srf_keep(seed, kStreamConv1b, o, drop_p) ? keep_scale : 0.f;
+      bool ka, kb;
+      srf_keep2(seed, kStreamConv1a, o, drop_p, ka, kb);
+      ga *= ka ? keep_scale : 0.f;
+      gb *= kb ? keep_scale : 0.f;
     }
     g_ab[(size_t)p * 2 * C + c] = ga;
     g_ab[(size_t)p * 2 * C + C + c] = gb;
@@ -1418,8 +1426,10 @@ __global__ __launch_bounds__(256) void conv1_bwd_kernel(
         const bool sl = sv[u] != 0;
         float ga = sl ? gy : 0.f, gb = sl ? 0.f : gy;
         if (drop_p > 0.f) {
-          ga *= srf_keep(seed, kStreamConv0a, o, drop_p) ? keep_scale : 0.f;
-          gb *= srf_keep(seed, kStreamConv0b, o, drop_p) ? keep_scale : 0.f;
+          bool ka, kb;
+          srf_keep2(seed, kStreamConv0a, o, drop_p, ka, kb);
+          ga *= ka ? keep_scale : 0.f;
+          gb *= kb ? keep_scale : 0.f;
         }
         float x[9];
         window9_lds(win, tl, d, w, f1, x);

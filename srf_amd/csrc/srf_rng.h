@@ -48,3 +48,14 @@ __device__ __forceinline__ float srf_uniform(uint64_t seed, unsigned stream, uin
 __device__ __forceinline__ bool srf_keep(uint64_t seed, unsigned stream, uint64_t idx, float p) {
   return srf_uniform(seed, stream, idx) >= p;
 }
+
+// The maxout convolutions drop both branches (streams a and a + 1) at the same
+// element: one hash keyed by stream a, whose high and low 16 bits are the two
+// uniforms (16-bit resolution: the keep probability is off by < 2^-16).
+__device__ __forceinline__ void srf_keep2(uint64_t seed, unsigned stream_a, uint64_t idx, float p, bool& keep_a,
+                                          bool& keep_b) {
+  const uint32_t k = srf_stream_key(seed, stream_a);
+  const uint32_t h = srf_mix32(srf_mix32((uint32_t)idx + k) ^ k);
+  keep_a = (float)(h >> 16) * (1.0f / 65536.0f) >= p;
+  keep_b = (float)(h & 0xFFFFu) * (1.0f / 65536.0f) >= p;
+}

@@ -1,7 +1,7 @@
 """GPU parity of the HIP CNN front end (srf_cnnfe_fwd/bwd through the C ABI)
 against a float64 torch-autograd restatement of CapsulationLayer
 (sequence_router.py:44-82).  Dropout masks are regenerated on the host from the
-same counter-based RNG (tests/torch_ref.rng_uniform).
+same counter-based RNG (tests/torch_ref.dropout_mult_pair: both maxout branches from one hash).
 
 Tolerances: output |err| <= 2e-4 * (1 + |ref|) (fp32 conv + BN normalisation
 vs fp64); parameter gradients |err| <= 2e-3 * max|ref| (fp32 reductions over
@@ -53,9 +53,9 @@ def test_cnnfe_forward_backward(cuda, case):
     if p > 0:
         drop = {}
         for k, (Tk, Fk) in enumerate(((T1, F1), (T2, F2))):
-            for ab in 'ab':
-                m = tr.dropout_mult(seed, tr.STREAMS[f'conv{k}{ab}'], (B, Tk, Fk, 64), p)
-                drop[f'conv{k}{ab}'] = torch.tensor(m)
+            ma, mb = tr.dropout_mult_pair(seed, tr.STREAMS[f'conv{k}a'], (B, Tk, Fk, 64), p)
+            drop[f'conv{k}a'] = torch.tensor(ma)
+            drop[f'conv{k}b'] = torch.tensor(mb)
     # reference (fp64, CPU)
     Pr = {k: v.clone().requires_grad_() for k, v in P.items()}
     ref = tr.cnnfe(torch.tensor(feats), torch.tensor(inp_len), Pr, drop)

@@ -38,6 +38,18 @@ def dropout_mult(seed, stream, shape, p):
     return (keep.astype(np.float64) / (1.0 - p)).reshape(shape)
 
 
+def dropout_mult_pair(seed, stream_a, shape, p):
+    """srf_keep2 of srf_rng.h: both maxout branches from one hash keyed by stream_a
+    (its high / low 16 bits)."""
+    seed = int(seed)
+    k = int(_mix32((seed & M32) ^ int(_mix32(((seed >> 32) & M32) ^ ((stream_a * 0x9E3779B9 + 0x7F4A7C15) & M32)))))
+    idx = np.arange(int(np.prod(shape)), dtype=np.uint64)
+    h = _mix32(_mix32((idx + np.uint64(k)) & np.uint64(M32)) ^ np.uint64(k))
+    ua = (h >> np.uint64(16)).astype(np.float32) * np.float32(1.0 / 65536.0)
+    ub = (h & np.uint64(0xFFFF)).astype(np.float32) * np.float32(1.0 / 65536.0)
+    return tuple(((u >= np.float32(p)).astype(np.float64) / (1.0 - p)).reshape(shape) for u in (ua, ub))
+
+
 def same_pad(n, k, s):
     out = -(-n // s)
     total = max((out - 1) * s + k - n, 0)
