@@ -6,7 +6,8 @@ mkdir -p $OUT
 for rep in 1 2; do
 for v in base ${VARS}; do
   if [ "$v" = base ]; then e=""; else e="$v"; fi
-  env $e timeout -k 10 200 python bench.py --no-cpu-baseline --steps ${STEPS:-20} --warmup 5 > $OUT/$v.$rep.json 2> $OUT/$v.$rep.err
-  python3 -c "import json,sys; d=json.load(open('$OUT/$v.$rep.json')); print('$v', d['ms_per_step'], d['roofline']['avg_launch_us'] if d.get('roofline') else '')"
+  n=$(echo "$v" | tr '/=' '__')
+  env $e timeout -k 10 200 python bench.py --no-cpu-baseline --steps ${STEPS:-20} --warmup 5 > $OUT/$n.$rep.json 2> $OUT/$n.$rep.err
+  python3 -c "import json,sys; d=json.load(open('$OUT/$n.$rep.json')); print('$v', d['ms_per_step'], d['roofline']['avg_launch_us'] if d.get('roofline') else '')"
 done
 done
