@@ -636,24 +636,6 @@ CapsBwdWs caps_bwd_layout(int F, int K, int PH, int PD, void* base) {
   return w;
 }
 
-__global__ void scatter_encaps_grads(const float* __restrict__ wsum, int E, int PD, float* __restrict__ g_gamma,
-                                     float* __restrict__ g_beta, float* __restrict__ gK1, float* __restrict__ gb1,
-                                     float* __restrict__ gK2, float* __restrict__ gb2) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < E) {
-    g_gamma[i] = wsum[i];
-    g_beta[i] = wsum[E + i];
-  }
-  if (i < 20 * PD) {
-    const int k = i / (10 * PD), tap = (i / PD) % 10, d = i % PD;
-    const float v = wsum[2 * E + i];
-    if (tap < 9)
-      (k == 0 ? gK1 : gK2)[tap * PD + d] = v;
-    else
-      (k == 0 ? gb1 : gb2)[d] = v;
-  }
-}
-
 int check_caps(int B, int T, int PH, int PD) {
   SRF_REQUIRE(B > 0 && T > 0 && PH > 0 && PD > 0, "bad primary capsule shape");
   SRF_REQUIRE((size_t)PH * PD <= kMaxVec, "PH*PD = %d exceeds %d", PH * PD, kMaxVec);
@@ -754,10 +736,10 @@ int srf_primary_caps_bwd_ex(const float* X, const int* inp_len, int B, int T, in
                      gamma, beta, training, p_caps, p_in, seed, srf::seed_source(), w.gv1, w.gv2, w.wpart);
   SRF_LAUNCH_CHECK("encaps_bwd_a");
   const int wcols = 2 * E + 20 * PD;
-  if ((rc = srf::colsum(w.wpart, F, wcols, w.wsum, w.scratch, st))) return rc;
-  hipLaunchKernelGGL(scatter_encaps_grads, dim3((std::max(E, 20 * PD) + 255) / 256), dim3(256), 0, st, w.wsum, E, PD,
-                     g_gamma, g_beta, g_K1, g_b1, g_K2, g_b2);
-  SRF_LAUNCH_CHECK("scatter_encaps_grads");
+  // columns: gamma, beta, then per conv k its 9 taps x PD and its bias -> straight into the gradients
+  if ((rc = srf::colsum(w.wpart, F, wcols, nullptr, w.scratch, st,
+                        srf::ColSplit{{g_gamma, g_beta, g_K1, g_b1, g_K2, g_b2}, {E, E, 9 * PD, PD, 9 * PD, PD}})))
+    return rc;
   hipLaunchKernelGGL(encaps_bwd_b_kernel, dim3(((size_t)F * PH * kEbLanes + 255) / 256), dim3(256), 0, st, w.gv1,
                      w.gv2, cd, K1, K2, w.g_e, proj_scale);
   SRF_LAUNCH_CHECK("encaps_bwd_b");

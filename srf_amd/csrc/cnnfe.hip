@@ -66,6 +66,15 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   n = nn;
 }
 
+// Split-bf16 weight packing of stage 2 (defined with the split kernels below), run
+// by extra blocks of the conv1 forward / conv2_bwd_prep launches.
+constexpr int kPackW2Threads = 9 * 2 * C * (C / 8);    // (tap, n, cin/8)
+constexpr int kPackW2tThreads = 9 * C * (2 * C / 8);   // (tap, cin, n/8)
+__device__ __forceinline__ void pack_w2_split_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
+                                                   __bf16* __restrict__ wp3);
+__device__ __forceinline__ void pack_w2t_split_body(int idx, const float* __restrict__ ka,
+                                                    const float* __restrict__ kb, __bf16* __restrict__ wq3);
+
 // ---------------------------------------------------------------- conv1
 // A workgroup = kRows1 consecutive output rows t1 of one utterance (one wave per
 // row), a lane = one output channel c.  The 2*kRows1+1 input rows the tile reads
@@ -110,7 +119,14 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
     const float* __restrict__ feats, const int* __restrict__ inp_len, Dims d, const float* __restrict__ ka,
     const float* __restrict__ ba, const float* __restrict__ kb, const float* __restrict__ bb, int training,
     float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ y1, unsigned char* __restrict__ sel1,
-    float* __restrict__ part) {
+    float* __restrict__ part, int nconv, const float* __restrict__ pk_a, const float* __restrict__ pk_b,
+    __bf16* __restrict__ wp3) {
+  // blocks past nconv pack the stage-2 split weights (one launch fewer per forward)
+  if ((int)blockIdx.x >= nconv) {
+    const int idx = (blockIdx.x - nconv) * blockDim.x + threadIdx.x;
+    if (idx < kPackW2Threads) pack_w2_split_body(idx, pk_a, pk_b, wp3);
+    return;
+  }
   seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float win[];
   __shared__ float sh[3][kRows1][C];
@@ -457,10 +473,8 @@ __device__ __forceinline__ void split8v(const float (&v)[8], cbf8& p1, cbf8& p2,
 }
 
 // Packed split weights wp3[plane][tap][n][cin] (n = ab*C + cout), one thread per 8 cin.
-__global__ void pack_w2_split_kernel(const float* __restrict__ ka, const float* __restrict__ kb,
-                                     __bf16* __restrict__ wp3) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;   // (tap, n, cin/8)
-  if (idx >= 9 * 2 * C * (C / 8)) return;
+__device__ __forceinline__ void pack_w2_split_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
+                                                   __bf16* __restrict__ wp3) {   // idx = (tap, n, cin/8)
   const int c8 = idx % (C / 8), n = (idx / (C / 8)) % (2 * C), tap = idx / (2 * C * (C / 8));
   const float* k = n < C ? ka : kb;
   float v[8];
@@ -746,7 +760,14 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     const float* __restrict__ g_out, const float* __restrict__ y2, const unsigned char* __restrict__ sel2,
     const float* __restrict__ stats2, const float* __restrict__ gamma2, const float* __restrict__ bnsum2,
     const int* __restrict__ inp_len, Dims d, float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ g_ab,
-    float* __restrict__ part) {
+    float* __restrict__ part, int nprep, const float* __restrict__ pk_a, const float* __restrict__ pk_b,
+    __bf16* __restrict__ wq3) {
+  // blocks past nprep pack the transposed split weights of the data gradient
+  if ((int)blockIdx.x >= nprep) {
+    const int idx = (blockIdx.x - nprep) * blockDim.x + threadIdx.x;
+    if (idx < kPackW2tThreads) pack_w2t_split_body(idx, pk_a, pk_b, wq3);
+    return;
+  }
   seed = srf_step_seed(seed, seed_src);
   __shared__ float sh[2][4][C];
   const int c = threadIdx.x & (C - 1), row = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -756,7 +777,7 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
   const float keep_scale = 1.f / (1.f - drop_p);
   float ga_s = 0.f, gb_s = 0.f;
 #pragma unroll 4
-  for (int p = blockIdx.x * 4 + row; p < P; p += gridDim.x * 4) {
+  for (int p = blockIdx.x * 4 + row; p < P; p += nprep * 4) {
     const int t = (p / d.F2) % d.T2;
     const int b = p / (d.F2 * d.T2);
     const float mask = t < ceil_div_len(inp_len[b], 4) ? 1.f : 0.f;
@@ -924,10 +945,9 @@ struct DgCls {
 };
 
 // wq3[plane][tap][cin][n] = split(k_{a|b}[tap][cin][n % C]), one thread per 8 n.
-__global__ void pack_w2t_split_kernel(const float* __restrict__ ka, const float* __restrict__ kb,
-                                      __bf16* __restrict__ wq3) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;   // (tap, cin, n/8)
-  if (idx >= 9 * C * (2 * C / 8)) return;
+__device__ __forceinline__ void pack_w2t_split_body(int idx, const float* __restrict__ ka,
+                                                    const float* __restrict__ kb, __bf16* __restrict__ wq3) {
+  // idx = (tap, cin, n/8)
   const int n8 = idx % (2 * C / 8), cin = (idx / (2 * C / 8)) % C, tap = idx / (C * (2 * C / 8));
   const int n = 8 * n8;
   const float* k = (n < C ? ka : kb) + ((size_t)tap * C + cin) * C + (n % C);
@@ -1589,16 +1609,16 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   const size_t P2 = (size_t)d.B * d.T2 * d.F2;
   const int nb2 = (int)((P2 + 63) / 64);
   int nparts2 = nb2;
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, k0a, b0a, k0b, b0b,
-                     training, drop_p, seed, srf::seed_source(), sv.y1, sv.sel1, w.part1);
+  const bool c2_32 = use_conv2_32();
+  const int npack = c2_32 ? (kPackW2Threads + 64 * kRows1 - 1) / (64 * kRows1) : 0;
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(conv1_blocks(d) + npack), dim3(64 * kRows1), conv1_lds(d), st, feats,
+                     inp_len, d, k0a, b0a, k0b, b0b, training, drop_p, seed, srf::seed_source(), sv.y1, sv.sel1,
+                     w.part1, conv1_blocks(d), k1a, k1b, w.wp3);
   SRF_LAUNCH_CHECK("conv1_fwd");
   if ((rc = bn_finalize(w.part1, conv1_blocks(d), w.merged, gamma0, beta0, mmean0, mvar0, training, sv.stats1, st)))
     return rc;
   SRF_LAUNCH_CHECK("bn_finalize(1)");
-  if (use_conv2_32()) {
-    hipLaunchKernelGGL(pack_w2_split_kernel, dim3((9 * 2 * C * (C / 8) + 255) / 256), dim3(256), 0, st, k1a, k1b,
-                       w.wp3);
-    SRF_LAUNCH_CHECK("pack_w2_split");
+  if (c2_32) {   // split weights packed by the conv1 launch
     const int nb32 = (int)((P2 + kC2Px - 1) / kC2Px);
     hipLaunchKernelGGL(conv2_fwd32_kernel, dim3(nb32), dim3(64 * kC2Waves), 0, st, sv.y1, sv.stats1, inp_len, d,
                        w.wp3, b1a, b1b, training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2, w.part2);
@@ -1677,23 +1697,6 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   return w;
 }
 
-// Scatter the 20 x C stage-1 sums into the kernel/bias gradients.
-__global__ void conv1_grad_unpack_kernel(const float* __restrict__ sums, float* __restrict__ gka,
-                                         float* __restrict__ gkb, float* __restrict__ gba, float* __restrict__ gbb) {
-  const int idx = threadIdx.x + blockIdx.x * blockDim.x;
-  if (idx >= 20 * C) return;
-  const int j = idx / C, c = idx % C;
-  const float v = sums[idx];
-  if (j < 9)
-    gka[j * C + c] = v;
-  else if (j < 18)
-    gkb[(j - 9) * C + c] = v;
-  else if (j == 18)
-    gba[c] = v;
-  else
-    gbb[c] = v;
-}
-
 }  // namespace
 
 extern "C" {
@@ -1729,17 +1732,17 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   SRF_LAUNCH_CHECK("bn_bwd_reduce(2)");
   if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st, srf::ColSplit{{g_beta1, g_gamma1, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
-  hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.sel2, sv.stats2,
-                     gamma1, w.bnsum2, inp_len, d, drop_p, seed, srf::seed_source(), w.g_ab, w.biaspart);
+  const bool c2_32 = use_conv2_32();
+  __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);   // 3 bf16 planes fit the fp32 image
+  const int npack = c2_32 ? (kPackW2tThreads + 255) / 256 : 0;
+  hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks + npack), dim3(256), 0, st, g_out, sv.y2, sv.sel2,
+                     sv.stats2, gamma1, w.bnsum2, inp_len, d, drop_p, seed, srf::seed_source(), w.g_ab, w.biaspart,
+                     kBnBlocks, k1a, k1b, wq3);
   SRF_LAUNCH_CHECK("conv2_bwd_prep");
   if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, nullptr, w.scratch, st, srf::ColSplit{{g_b1a, g_b1b, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
   // stage-2 data gradient (4 stride-parity classes) and weight gradient
-  if (use_conv2_32()) {
-    __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);   // 3 bf16 planes fit the fp32 image
-    hipLaunchKernelGGL(pack_w2t_split_kernel, dim3((9 * C * (2 * C / 8) + 255) / 256), dim3(256), 0, st, k1a, k1b,
-                       wq3);
-    SRF_LAUNCH_CHECK("pack_w2t_split");
+  if (c2_32) {   // split transposed weights packed by the bwd_prep launch
     DgCls cls{};
     for (int c = 0; c < 4; ++c) {
       const int qt = c >> 1, qf = c & 1;
@@ -1795,10 +1798,10 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   hipLaunchKernelGGL(conv1_bwd_kernel, dim3(conv1_blocks(d)), dim3(64 * kRows1), conv1_lds(d), st, feats, inp_len, d, w.g_x1, sv.y1,
                      sv.sel1, sv.stats1, gamma0, w.bnsum1, drop_p, seed, srf::seed_source(), w.c1part);
   SRF_LAUNCH_CHECK("conv1_bwd");
-  if ((rc = srf::colsum(w.c1part, conv1_blocks(d), 20 * C, w.c1sum, w.scratch, st))) return rc;
-  hipLaunchKernelGGL(conv1_grad_unpack_kernel, dim3((20 * C + 255) / 256), dim3(256), 0, st, w.c1sum, g_k0a, g_k0b,
-                     g_b0a, g_b0b);
-  SRF_LAUNCH_CHECK("conv1_grad_unpack");
+  // columns j*C + c: conv a taps, conv b taps, bias a, bias b -> straight into the gradients
+  if ((rc = srf::colsum(w.c1part, conv1_blocks(d), 20 * C, nullptr, w.scratch, st,
+                        srf::ColSplit{{g_k0a, g_k0b, g_b0a, g_b0b, nullptr, nullptr}, {9 * C, 9 * C, C, C, 0, 0}})))
+    return rc;
   return SRF_OK;
 }
 

@@ -38,7 +38,7 @@ __global__ void colsum_stage2(const float* __restrict__ part, int slices, int co
   if (out) out[c] = s;
   int start = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 6; ++k) {
     if (split.dst[k] && c >= start && c < start + split.width[k]) split.dst[k][c - start] = s;
     start += split.width[k];
   }

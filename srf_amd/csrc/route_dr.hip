@@ -1632,11 +1632,9 @@ int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* sa
                      padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride)
 #define SRF_GW3C(R_) \
   if (p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, 8);
-      switch (g.iters) {
+      switch (g.iters) {   // gw3_cap() is 0 past 3 iterations
         case 2: SRF_GW3C(2) break;
-        case 3: SRF_GW3C(3) break;
-        case 4: SRF_GW3C(4) break;
-        default: SRF_GW3C(5) break;
+        default: SRF_GW3C(3) break;
       }
 #undef SRF_GW3C
 #undef SRF_GW3

@@ -12,8 +12,8 @@ size_t colsum_scratch_floats(int rows, int cols);
 // dst[k][0 .. width_k) (start_k = sum of the earlier widths), e.g. a packed
 // (d_beta | d_gamma) partial straight into two parameter gradients.
 struct ColSplit {
-  float* dst[4] = {nullptr, nullptr, nullptr, nullptr};
-  int width[4] = {0, 0, 0, 0};
+  float* dst[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int width[6] = {0, 0, 0, 0, 0, 0};
 };
 // out (may be null when split is given) receives all cols sums.
 int colsum(const float* in, int rows, int cols, float* out, float* scratch, hipStream_t st,
