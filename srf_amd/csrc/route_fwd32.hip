@@ -823,7 +823,11 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   const int n_ftiles = (F + 31) / 32;
   // one workgroup per CU when NW > 1 (the Vc slabs fill most of the LDS);
   // single-wave workgroups: up to 4 per CU.
-  const int slots = p.NW > 1 ? 256 : 1024;
+  static const int slots1 = [] {
+    const char* e = getenv("SRF_FWD32_SLOTS1");
+    return e ? atoi(e) : 1024;
+  }();
+  const int slots = p.NW > 1 ? 256 : slots1;
   int best = 1;
   double best_cost = 1e30;
   const char* env = getenv("SRF_FWD32_CHUNKS");
