@@ -52,6 +52,9 @@
 #define SRF_FWD32_PRIO 1
 #endif
 // 1: softmax normaliser by the fast reciprocal instead of an IEEE division
+#ifndef SRF_BWD32_CPREFETCH
+#define SRF_BWD32_CPREFETCH 0   // 1: couplings of capsule i+1 loaded during capsule i (4 more live registers)
+#endif
 #ifndef SRF_FWD32_FASTDIV
 #define SRF_FWD32_FASTDIV 0
 #endif
@@ -696,19 +699,27 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   int par = 0;
   if (i0 < i1) {
     Frags32<DIN, TW> fr;
+#if SRF_BWD32_CPREFETCH
     float cn[OWN];
+    load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cn);
+#endif
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                            A.wplane_b, A.xplane_b, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8, fr);
-    load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cn);
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
 #pragma unroll
       for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
+#if SRF_BWD32_CPREFETCH
       float cc[OWN];
 #pragma unroll
       for (int a = 0; a < OWN; ++a) cc[a] = cn[a];
-      // the next capsule's couplings: a whole capsule of work hides their latency
       if (i + 1 < i1) load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
+#else
+      // this capsule's couplings: the pose MFMAs in flight hide their latency (no
+      // registers held across capsules)
+      float cc[OWN];
+      load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
+#endif
       // partial dots <u_ij, gs_j> over this lane's rows
       f2 P2[CP];
 #pragma unroll
