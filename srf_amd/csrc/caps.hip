@@ -136,7 +136,9 @@ __global__ __launch_bounds__(256) void proj_fwd_vec_kernel(const float* __restri
     }
 }
 
-// g_X[f][k..k+3] = sum_p g_e[f][p] Wp[k..k+3][p], one float4 of g_X per thread.
+// g_X[f][k..k+3] = sum_p g_e[f][p] Wp[k..k+3][p]: a thread writes one float4 of g_X for
+// kProjXF consecutive frames, so the Wp rows it loads serve them all.
+constexpr int kProjXF = 4;
 template <int PH>
 __global__ __launch_bounds__(256) void proj_bwd_x_vec_kernel(const float* __restrict__ g_e,
                                                              const float* __restrict__ Wp, int F, int K,
@@ -144,24 +146,33 @@ __global__ __launch_bounds__(256) void proj_bwd_x_vec_kernel(const float* __rest
   constexpr int PQ = PH / 4;
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int K4 = K / 4;
-  if (idx >= (size_t)F * K4) return;
-  const int f = (int)(idx / K4);
-  const int k0 = (int)(idx - (size_t)f * K4) * 4;
-  f4 ge[PQ];
+  const int FG = (F + kProjXF - 1) / kProjXF;
+  if (idx >= (size_t)FG * K4) return;
+  const int fg = (int)(idx / K4);
+  const int k0 = (int)(idx - (size_t)fg * K4) * 4;
+  f4 w[4][PQ];
 #pragma unroll
-  for (int q = 0; q < PQ; ++q) ge[q] = *reinterpret_cast<const f4*>(g_e + (size_t)f * PH + 4 * q);
-  f4 out;
+  for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    float sacc = 0.f;
+    for (int q = 0; q < PQ; ++q) w[kk][q] = *reinterpret_cast<const f4*>(Wp + (size_t)(k0 + kk) * PH + 4 * q);
 #pragma unroll
-    for (int q = 0; q < PQ; ++q) {
-      const f4 w = *reinterpret_cast<const f4*>(Wp + (size_t)(k0 + kk) * PH + 4 * q);
-      sacc += (w.x * ge[q].x + w.y * ge[q].y) + (w.z * ge[q].z + w.w * ge[q].w);
+  for (int u = 0; u < kProjXF; ++u) {
+    const int f = fg * kProjXF + u;
+    if (f >= F) break;
+    f4 ge[PQ];
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) ge[q] = *reinterpret_cast<const f4*>(g_e + (size_t)f * PH + 4 * q);
+    f4 out;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int q = 0; q < PQ; ++q)
+        sacc += (w[kk][q].x * ge[q].x + w[kk][q].y * ge[q].y) + (w[kk][q].z * ge[q].z + w[kk][q].w * ge[q].w);
+      out[kk] = sacc;
     }
-    out[kk] = sacc;
+    *reinterpret_cast<f4*>(g_X + (size_t)f * K + k0) = out;
   }
-  *reinterpret_cast<f4*>(g_X + (size_t)f * K + k0) = out;
 }
 
 // g_X[f][k] = sum_p g_e[f][p] Wp[k][p]
@@ -188,11 +199,18 @@ __global__ void proj_bwd_w_kernel(const float* __restrict__ X, const float* __re
       float acc[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-      for (int f = f0; f < f1; ++f) {
-        const float xv = X[(size_t)f * K + k];
+      // frames in batches of 8: the batch's X loads are in flight together
+      for (int fb = f0; fb < f1; fb += 8) {
+        float xv[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (p0 + q < PH) acc[q] += xv * g_e[(size_t)f * PH + p0 + q];
+        for (int u = 0; u < 8; ++u) xv[u] = X[(size_t)min(fb + u, f1 - 1) * K + k];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (fb + u >= f1) break;
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (p0 + q < PH) acc[q] += xv[u] * g_e[(size_t)(fb + u) * PH + p0 + q];
+        }
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q)
@@ -743,7 +761,7 @@ int srf_primary_caps_bwd_ex(const float* X, const int* inp_len, int B, int T, in
   hipLaunchKernelGGL(encaps_bwd_b_kernel, dim3(((size_t)F * PH * kEbLanes + 255) / 256), dim3(256), 0, st, w.gv1,
                      w.gv2, cd, K1, K2, w.g_e, proj_scale);
   SRF_LAUNCH_CHECK("encaps_bwd_b");
-  const dim3 gx4(((size_t)F * (K / 4) + 255) / 256);
+  const dim3 gx4(((size_t)((F + kProjXF - 1) / kProjXF) * (K / 4) + 255) / 256);
   if (K % 4 == 0 && PH == 4)
     hipLaunchKernelGGL(proj_bwd_x_vec_kernel<4>, gx4, dim3(256), 0, st, w.g_e, Wp, F, K, g_X);
   else if (K % 4 == 0 && PH == 8)
