@@ -136,6 +136,60 @@ __global__ __launch_bounds__(256) void proj_fwd_vec_kernel(const float* __restri
     }
 }
 
+// e[f][p] = proj(X[f] . Wp[:, p] + bp[p]) on v_mfma_f32_16x16x4_f32 (exact fp32): a
+// workgroup = one 16-frame tile, its 16 waves split K (kProjKq each, in steps of 16:
+// lane (m = l & 15, g = l >> 4) feeds X[f0 + m][k + 4g + j] and Wp[k + 4g + j][n] to
+// MFMA j), then the 16 partial tiles are summed through LDS in a fixed order.
+constexpr int kProjWaves = 16;
+template <int PH>
+__global__ __launch_bounds__(64 * kProjWaves) void proj_fwd_mfma_kernel(const float* __restrict__ X, int F, int K,
+                                                                       const float* __restrict__ Wp,
+                                                                       const float* __restrict__ bp,
+                                                                       float* __restrict__ e, int T, float scale,
+                                                                       int pe, int Kq) {
+  static_assert(PH <= 16, "one 16-column output tile");
+  __shared__ float part[kProjWaves][16][17];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int m = lane & 15, g = lane >> 4;
+  const int f0 = blockIdx.x * 16;
+  const int fm = min(f0 + m, F - 1);
+  const bool fok = f0 + m < F;
+  const int kb = wv * Kq, ke = min(K, kb + Kq);
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;   // k-steps of 16 in flight
+  for (int k0 = kb; k0 < ke; k0 += 16 * U) {
+    f4 xa[U];
+    float wb[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 16 * u + 4 * g;
+      const bool kok = k < ke;   // K % 4 == 0: whole float4s
+      const f4 x = *reinterpret_cast<const f4*>(X + (size_t)fm * K + (kok ? k : kb));
+      xa[u] = (fok && kok) ? x : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float w = Wp[(size_t)(kok ? k + j : kb) * PH + min(m, PH - 1)];
+        wb[u][j] = (kok && m < PH) ? w : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma16x16x4(xa[u][j], wb[u][j], acc);
+  }
+  // C: lane column n = m (output p), rows 4g + v (frames)
+#pragma unroll
+  for (int v = 0; v < 4; ++v) part[wv][4 * g + v][m] = acc[v];
+  __syncthreads();
+  if (threadIdx.x < 16 * PH) {
+    const int r = threadIdx.x / PH, pp = threadIdx.x % PH;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < kProjWaves; ++w) sum += part[w][r][pp];
+    if (f0 + r < F) e[(size_t)(f0 + r) * PH + pp] = proj_epilogue(sum + bp[pp], f0 + r, T, pp, PH, scale, pe);
+  }
+}
+
 // g_X[f][k..k+3] = sum_p g_e[f][p] Wp[k..k+3][p]: a thread writes one float4 of g_X for
 // kProjXF consecutive frames, so the Wp rows it loads serve them all.
 constexpr int kProjXF = 4;
@@ -698,7 +752,21 @@ int srf_primary_caps_fwd_ex(const float* X, const int* inp_len, int B, int T, in
   hipStream_t st = static_cast<hipStream_t>(stream);
   constexpr int FW = 2;
   const dim3 gvec((F + 4 * FW - 1) / (4 * FW));
-  if (K % 4 == 0 && PH == 4)
+  static const bool proj_mfma = [] {
+    const char* e = getenv("SRF_PROJ_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  const int Kq = ((K + kProjWaves - 1) / kProjWaves + 15) / 16 * 16;
+  if (proj_mfma && K % 4 == 0 && (PH == 4 || PH == 8 || PH == 16)) {
+    const dim3 gm((F + 15) / 16), bm(64 * kProjWaves);
+    if (PH == 4)
+      hipLaunchKernelGGL((proj_fwd_mfma_kernel<4>), gm, bm, 0, st, X, F, K, Wp, bp, sv.e, T, proj_scale, pos_enc, Kq);
+    else if (PH == 8)
+      hipLaunchKernelGGL((proj_fwd_mfma_kernel<8>), gm, bm, 0, st, X, F, K, Wp, bp, sv.e, T, proj_scale, pos_enc, Kq);
+    else
+      hipLaunchKernelGGL((proj_fwd_mfma_kernel<16>), gm, bm, 0, st, X, F, K, Wp, bp, sv.e, T, proj_scale, pos_enc,
+                         Kq);
+  } else if (K % 4 == 0 && PH == 4)
     hipLaunchKernelGGL((proj_fwd_vec_kernel<4, FW>), gvec, dim3(256), 0, st, X, F, K, Wp, bp, sv.e, T,
                        proj_scale, pos_enc);
   else if (K % 4 == 0 && PH == 8)
