@@ -717,7 +717,9 @@ __global__ __launch_bounds__(256, (R >= 4 ? 3 : 4)) void route_gux_kernel(
   // lane byte offsets (capsule-independent) and per-capsule SGPR offsets
   const int Fs = srf::fwd32_frame_stride(F);
   const uint32_t cblk_b = (uint32_t)in_n * JP * Fs * 4;
-  const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(WT), 0, (int)((size_t)in_n * DIN * JD * 4),
+  // W^T in fragment order [i][tile][row quad g][e][4 rows] (prep32_kernel): a wave's
+  // float4 loads of one tile are 1 KiB contiguous
+  const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(WT), 0, (int)((size_t)in_n * NT * 16 * DIN * 4),
                                                        0x00020000);
   const auto rs_c = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cst), 0, (int)(cblk_b * RV), 0x00020000);
   const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(glst), 0, (int)(cblk_b * RV), 0x00020000);
@@ -727,7 +729,7 @@ __global__ __launch_bounds__(256, (R >= 4 ? 3 : 4)) void route_gux_kernel(
     const int tc = min(tbase + t, NT - 1);
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct)
-      wo[ct][t] = (uint32_t)(min(ct * 16 + fl, DIN - 1) * JD + min(tc * 16 + 4 * g, JD - 4)) * 4;
+      wo[ct][t] = (uint32_t)(((tc * 4 + g) * DIN + min(ct * 16 + fl, DIN - 1)) * 4) * 4;
     co[t] = (uint32_t)(min(tile_j<DIN>(tbase + t, g), J - 1) * Fs + (loc.valid ? f : 0)) * 4;
   }
   // three operand sets in a ring: capsule k+2 is fetched while capsule k is formed
@@ -736,7 +738,7 @@ __global__ __launch_bounds__(256, (R >= 4 ? 3 : 4)) void route_gux_kernel(
   float c_b[NB][RV][TW], g_b[NB][RV][TW];
   auto fetch = [&](auto slot, int i) {
     constexpr int sl = decltype(slot)::value;
-    const uint32_t sw = (uint32_t)i * DIN * JD * 4;
+    const uint32_t sw = (uint32_t)i * NT * 16 * DIN * 4;
     const uint32_t sc = (uint32_t)i * JP * Fs * 4;
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct)
@@ -1528,24 +1530,15 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
   const int n_chunks = (g.N + n_per - 1) / n_per;
   const int nslots = 15 + gu_window(g);
   const size_t lds = gu_lds_bytes(g, nw, n_per);
-  static const bool gux = [] {
-    const char* e = getenv("SRF_GUX");
-    return !(e && e[0] == '0');
-  }();
   if constexpr (R >= 2 && D <= 16) {   // couplings are stored by the 32x32 forward (din <= 16)
-    if (lds <= kGuLdsMax && cst != nullptr && gux) {
+    if (lds <= kGuLdsMax && cst != nullptr) {
       hipLaunchKernelGGL((route_gux_kernel<D, TW, R>), dim3(n_ftiles * n_wgroups * n_chunks), dim3(64 * nw), lds, st,
                          WT, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved,
                          gs, g_emb, nslots, cst, glst, JP);
       return;
     }
   }
-  if (lds <= kGuLdsMax && cst != nullptr)
-    hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, true, true>), dim3(n_ftiles * n_wgroups * n_chunks),
-                       dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
-                       g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots,
-                       cst, glst, JP);
-  else if (lds <= kGuLdsMax)
+  if (lds <= kGuLdsMax)
     hipLaunchKernelGGL((route_gu_kernel<D, D, TW, R, true>), dim3(n_ftiles * n_wgroups * n_chunks),
                        dim3(64 * nw), lds, st, emb, W, WT, bias, g.F(), padded_frames(g), g.T, g.N, g.lpad, g.rpad,
                        g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, stats, gu_t, g_emb, nslots,
@@ -1664,6 +1657,17 @@ inline bool use_fwd32(const Geom& g) {
   if (e && e[0] == '0') return false;
   return srf::fwd32_supported(g.din, g.dout, g.J);
 }
+
+// Coupling storage is used when the split-bf16 forward runs and the gu pass from
+// stored couplings (route_gux_kernel) fits its window accumulator in LDS; otherwise
+// the forward keeps nothing and the backward recomputes (round-1 kernels).
+inline bool couplings_ok(const Geom& g) {
+  if (!use_fwd32(g) || g.iters < 2 || g.din > 16) return false;
+  const int TW = gu_tw(g.dout);
+  const int nw = std::min(kGuNW, (g.NT() + TW - 1) / TW);
+  return gu_lds_bytes(g, nw, 1) <= kGuLdsMax;
+}
+
 
 template <int D>
 int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, const float* bias, float* v_out,
@@ -1916,7 +1920,7 @@ size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rp
 
 size_t srf_route_dr_coupling_floats(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int iters) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, iters, 0};
-  if (!use_fwd32(g) || iters < 2) return 0;
+  if (!couplings_ok(g)) return 0;
   return srf::fwd32_cpl_layout(srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout), B * T, g.in_n(), din, dout, J, iters)
       .total;
 }
@@ -1943,7 +1947,7 @@ int srf_route_dr_fwd_ex(const float* emb, const float* W, const float* bias, int
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* slab = static_cast<float*>(workspace);
-  if (couplings != nullptr && (!use_fwd32(g) || iters < 2)) couplings = nullptr;   // nothing to store
+  if (couplings != nullptr && !couplings_ok(g)) couplings = nullptr;   // nothing to store
   switch (din) {
     case 8: return fwd_impl<8>(g, n_chunks, emb, W, bias, v_out, saved, couplings, slab, st);
     case 16: return fwd_impl<16>(g, n_chunks, emb, W, bias, v_out, saved, couplings, slab, st);
@@ -1968,7 +1972,7 @@ int route_dr_bwd_entry(const float* emb, const float* W, const float* bias, int 
     return SRF_EWORKSPACE;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (couplings != nullptr && (!use_fwd32(g) || iters < 2)) couplings = nullptr;
+  if (couplings != nullptr && !couplings_ok(g)) couplings = nullptr;
   switch (din) {
     case 8:
       return bwd_impl<8>(g, n_chunks, emb, W, bias, saved, couplings, g_v, g_emb, g_W, g_bias, w, st, with_weights);
@@ -2038,7 +2042,7 @@ int srf_route_dr_bwd_weights_ex(const float* emb, int B, int T, int N, int din, 
     return SRF_EWORKSPACE;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (couplings != nullptr && (!use_fwd32(g) || iters < 2 || saved == nullptr)) couplings = nullptr;
+  if (couplings != nullptr && (!couplings_ok(g) || saved == nullptr)) couplings = nullptr;
   switch (din) {
     case 8: return bwd_weights_impl<8>(g, emb, g_W, g_bias, w, st, saved, couplings);
     case 16: return bwd_weights_impl<16>(g, emb, g_W, g_bias, w, st, saved, couplings);

@@ -109,7 +109,8 @@ __device__ __forceinline__ void split8(const float* __restrict__ src, bool ok, _
 //   bsum[c][row]        =  sum of bias[i][row] over the capsules of i-chunk c (iteration-0 pass);
 //   emb [F][N][din]     -> xs [3][plane], plane = [N][F][din] capsule-major + 16 zeros.
 //   (training forwards also write the fp32 operands of the backward passes:)
-//   W                   -> WT [in_n][din][JD] (A of the gx contraction), 4 per thread;
+//   W                   -> WT [in_n][JD/16][4][din][4] (A of the gx contraction in fragment order:
+//                          row quad g of 16-row tile t, input element e, rows 16t+4g..+3), 4 per thread;
 //   window(emb)         -> xT [in_n][din][Fp] (A of the gW contraction, zero past F / the utterance).
 struct PrepArgs {
   const float *W, *bias, *emb;
@@ -167,14 +168,20 @@ __global__ void prep32_kernel(PrepArgs P) {
     return;
   }
   idx -= P.n_d;
-  if (idx < P.n_e) {   // WT[i][e][row] = W[i][row][e], 4 rows per thread
-    const size_t o = idx * 4;
-    const int row = o % P.JD;
-    const size_t ie = o / P.JD;
-    const int e = ie % P.din;
-    const size_t i = ie / P.din;
-    const float* w = P.W + (i * P.JD + row) * P.din + e;
-    *reinterpret_cast<f4*>(P.WT + o) = f4{w[0], w[P.din], w[2 * P.din], w[3 * P.din]};
+  if (idx < P.n_e) {   // WT[i][t][g][e][0..3] = W[i][16t + 4g + 0..3][e] (0 past JD)
+    const int e = idx % P.din;
+    const size_t r1 = idx / P.din;
+    const int g = r1 % 4;
+    const size_t r2 = r1 / 4;
+    const int nt16 = (P.JD + 15) / 16;
+    const int t = r2 % nt16;
+    const size_t i = r2 / nt16;
+    const int row = t * 16 + 4 * g;
+    const float* w = P.W + (i * P.JD + min(row, P.JD - 1)) * P.din + e;
+    f4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = row + q < P.JD ? w[(size_t)q * P.din] : 0.f;
+    *reinterpret_cast<f4*>(P.WT + idx * 4) = v;
     return;
   }
   idx -= P.n_e;
@@ -906,7 +913,7 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   P.n_b = (size_t)P.in_n * p.JDp;
   P.n_c = (size_t)p.n_chunks * P.JD;
   P.n_d = p.xplane / 8;
-  P.n_e = WT ? (size_t)P.in_n * din * P.JD / 4 : 0;
+  P.n_e = WT ? (size_t)P.in_n * ((P.JD + 15) / 16) * 4 * din : 0;
   P.n_f = xT ? (size_t)P.in_n * din * P.Fp : 0;
   const size_t total = P.n_a + P.n_b + P.n_c + P.n_d + P.n_e + P.n_f;
   hipLaunchKernelGGL(prep32_kernel, dim3((total + 255) / 256), dim3(256), 0, st, P);
@@ -990,7 +997,7 @@ Fwd32Cpl fwd32_cpl_layout(const Fwd32Plan& p, int F, int in_n, int din, int dout
   c.planes = off;
   off += (fwd32_planes_bytes(p) + 255) / 256 * 64;
   c.WT = off;
-  off += ((size_t)in_n * din * J * dout + 63) / 64 * 64;
+  off += ((size_t)in_n * din * ((J * dout + 15) / 16 * 16) + 63) / 64 * 64;
   c.xT = off;
   off += ((size_t)in_n * din * ((F + 15) / 16 * 16) + 63) / 64 * 64;
   c.total = off;
