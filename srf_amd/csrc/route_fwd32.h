@@ -1,4 +1,4 @@
-// Host interface of the 32x32-tile split-bf16 DR forward pass (route_fwd32.hip),
+// Host interface of the 32x32-tile split-fp16 DR forward pass (route_fwd32.hip),
 // used by route_dr.hip's srf_route_dr_fwd for the shapes it supports.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -19,12 +19,13 @@ struct Fwd32Plan {
   int JDp;             // J*dout padded to NW*4*32 rows
   int n_chunks, chunk_len, n_ftiles;
   size_t xplane;       // elements per x plane (data + zero row)
-  size_t ws_w, ws_b, ws_x, ws_bsum, ws_slab;   // workspace regions (bytes)
+  size_t ws_w, ws_b, ws_x, ws_h, ws_bsum, ws_slab;   // workspace regions (bytes)
 };
 
 bool fwd32_supported(int din, int dout, int J);
 Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout);
-// Operand planes (split W, bias, x: written by fwd32_prepare, read by every pass)
+// Operand planes (split W, bias, x and their scale header: written by fwd32_prepare,
+// read by every pass)
 // and per-pass scratch (i-chunk bias sums + partial slabs) may live apart: a
 // training forward keeps its planes for the backward (coupling storage).
 size_t fwd32_planes_bytes(const Fwd32Plan& p);
@@ -32,7 +33,8 @@ size_t fwd32_scratch_bytes(const Fwd32Plan& p);
 size_t fwd32_workspace(const Fwd32Plan& p);   // planes + scratch
 size_t fwd32_lds(const Fwd32Plan& p);
 float* fwd32_slab(const Fwd32Plan& p, void* scratch);
-// split W / bias / emb into bf16 planes and the i-chunk bias sums (once per forward);
+// split W / emb into scaled fp16 planes, bias into bf16 planes, and the i-chunk bias
+// sums (two launches per forward: absmax, prep);
 // WT / xT (nullable): also the fp32 W^T [in_n][din][JD] and window^T [in_n][din][Fp]
 // operands of the backward gx / gW contractions
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,

@@ -1,4 +1,4 @@
-// DR routing forward pass on 32x32 tiles with fp32-accurate split-bf16 MFMA, gfx950.
+// DR routing forward pass on 32x32 tiles with fp32-accurate split-fp16 MFMA, gfx950.
 //
 // Replaces, like route_dr.hip's route_pass_kernel, the forward routing iteration of
 // sequence_router_naive.py:171-185 / _loop_body :199-206 (pose :154-159 recomputed
@@ -6,14 +6,18 @@
 // and dout in {8, 16, 32} with J*dout <= 1024 (BASELINE C1 and C2); other shapes
 // keep route_pass_kernel.
 //
-// Pose product.  u = W x + b is formed on v_mfma_f32_32x32x16_bf16 from 3-term
-// bf16 splits a = a1 + a2 + a3 (a1 = bf16(a), a2 = bf16(a - a1), a3 = bf16(a - a1 - a2)),
-// keeping the six products whose size is >= 2^-18 |a b|:
-//     W x ~ W1x1 + W1x2 + W2x1 + W2x2 + W1x3 + W3x1      (dropped terms <= 2^-26 |W x|)
-// and the bias through one more MFMA against a ones column (b1 + b2 + b3 exact to
-// 2^-27).  bf16 x bf16 products are exact in the fp32 accumulator, so the pose is
-// as accurate as an fp32 FMA chain (tests/test_route_dr_gpu.py holds it to the
-// same tolerances) at 6/16 of the fp32 MFMA time.
+// Pose product.  u = W x + b is formed on v_mfma_f32_32x32x16_f16 from 2-term fp16
+// splits of power-of-two scaled operands: W' = 2^aw W and x' = 2^bx x with
+// max|W'|, max|x'| < 2^14 (absmax_kernel + prep32_kernel, one global exponent per
+// operand and forward), a' = a1 + a2 (a1 = f16(a'), a2 = f16(a' - a1)), keeping
+//     W'x' ~ W1x1 + W1x2 + W2x1                          (dropped W2x2 <= 2^-22 |W'x'|)
+// and the bias 2^(aw+bx) b through one bf16 MFMA (3-term bf16 split, exact to 2^-24)
+// against a ones column, all in one fp32 accumulator.  f16 x f16 products are exact
+// in fp32, so u' = 2^(aw+bx) u carries ~2^-22 relative error per product, the level
+// of an fp32 FMA chain over din terms (tests/test_route_dr_gpu.py holds it to the same
+// tolerances); consumers multiply by the exact inverse scale 2^-(aw+bx) (logits,
+// final partial sums).  Four MFMAs per tile and 4 bytes of W per element (the
+// split-bf16 3-term form of round 2 needed seven and 6 bytes).
 //
 // Tiles.  A workgroup owns 32 frames x all J*dout rows (32-row tiles, TW per wave)
 // and an i-chunk of input capsules.  Lane l holds frame (l & 31) and, per tile,
@@ -63,15 +67,30 @@ namespace {
 
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ f16v mfma32(const bf8& a, const bf8& b, const f16v& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// 2^e as a float (|e| <= 126)
+__device__ __forceinline__ float exp2i(int e) { return __int_as_float((127 + e) << 23); }
+// Exponent that scales an operand of max magnitude m below 2^14 (m = mant * 2^e,
+// mant in [0.5, 1): m * 2^(14 - e) < 2^14), clamped so that 2^-(aw + bx) stays normal.
+__device__ __forceinline__ int split_exp(float m) {
+  if (!(m > 0.f) || !(m < INFINITY)) return 0;
+  int e;
+  (void)frexpf(m, &e);
+  return max(-60, min(60, 14 - e));
+}
 
 
 // ------------------------------------------------------------------ splits
-// a -> (a1, a2, a3), each round-to-nearest bf16.
+// a -> (a1, a2, a3), each round-to-nearest bf16 (the bias operand).
 __device__ __forceinline__ void split3(float a, __bf16& a1, __bf16& a2, __bf16& a3) {
   a1 = (__bf16)a;
   const float r = a - (float)a1;
@@ -79,49 +98,100 @@ __device__ __forceinline__ void split3(float a, __bf16& a1, __bf16& a2, __bf16& 
   a3 = (__bf16)(r - (float)a2);
 }
 
-typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+// a' -> (a1, a2) = (f16(a'), f16(a' - a1)), |a'| < 2^14
+__device__ __forceinline__ void split2h(float a, _Float16& a1, _Float16& a2) {
+  a1 = (_Float16)a;
+  a2 = (_Float16)(a - (float)a1);
+}
 
-// 8 consecutive floats -> their three bf16 planes (16 bytes each)
-__device__ __forceinline__ void split8(const float* __restrict__ src, bool ok, __bf16* d1, __bf16* d2, __bf16* d3) {
+// 8 consecutive floats, scaled by s -> their two fp16 planes (16 bytes each)
+__device__ __forceinline__ void split8h(const float* __restrict__ src, bool ok, float s, _Float16* d1,
+                                        _Float16* d2) {
   f4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
   if (ok) {
     lo = *reinterpret_cast<const f4*>(src);
     hi = *reinterpret_cast<const f4*>(src + 4);
   }
   const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  bf8v p1, p2, p3;
+  h8 p1, p2;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    __bf16 a1, a2, a3;
-    split3(v[k], a1, a2, a3);
+    _Float16 a1, a2;
+    split2h(v[k] * s, a1, a2);
     p1[k] = a1;
     p2[k] = a2;
-    p3[k] = a3;
   }
-  *reinterpret_cast<bf8v*>(d1) = p1;
-  *reinterpret_cast<bf8v*>(d2) = p2;
-  *reinterpret_cast<bf8v*>(d3) = p3;
+  *reinterpret_cast<h8*>(d1) = p1;
+  *reinterpret_cast<h8*>(d2) = p2;
+}
+
+// Block maxima of |W| (blockIdx.y = 0) and |emb| (blockIdx.y = 1) -> part[y][blockIdx.x]
+// (kAbsBlocks per operand); prep32_kernel reduces them to the split exponents.
+constexpr int kAbsBlocks = 128;
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ a, size_t na,
+                                                     const float* __restrict__ b, size_t nb, float* part) {
+  const float* p = blockIdx.y ? b : a;
+  const size_t n = blockIdx.y ? nb : na;
+  float m = 0.f;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    const size_t n4 = n / 4;
+    for (; i < n4; i += stride) {
+      const f4 v = reinterpret_cast<const f4*>(p)[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  }
+  for (; i < n; i += stride) m = fmaxf(m, fabsf(p[i]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.y * kAbsBlocks + blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
 }
 
 // One launch prepares every operand of a forward (thread ranges in this order):
-//   W [in_n][JD][din]   -> Ws [3][in_n][JDp][din] bf16 planes (rows past JD = 0), 8 per thread;
-//   bias [in_n][JD]     -> bs [in_n][JDp][4] = (b1, b2, b3, 0);
+//   W [in_n][JD][din]   -> Ws [2][in_n][JDp][din] fp16 planes of 2^aw W (rows past JD = 0), 8 per thread;
+//   bias [in_n][JD]     -> bs [in_n][JDp][4] = bf16 (b1, b2, b3, 0) of 2^(aw+bx) bias;
 //   bsum[c][row]        =  sum of bias[i][row] over the capsules of i-chunk c (iteration-0 pass);
-//   emb [F][N][din]     -> xs [3][plane], plane = [N][F][din] capsule-major + 16 zeros.
+//   emb [F][N][din]     -> xs [2][plane] fp16 of 2^bx x, plane = [N][F][din] capsule-major + 16 zeros;
+//   block 0 also writes the header hdr = {2^-(aw+bx), aw, bx} read by every pass.
 //   (training forwards also write the fp32 operands of the backward passes:)
 //   W                   -> WT [in_n][JD/16][4][din][4] (A of the gx contraction in fragment order:
 //                          row quad g of 16-row tile t, input element e, rows 16t+4g..+3), 4 per thread;
 //   window(emb)         -> xT [in_n][din][Fp] (A of the gW contraction, zero past F / the utterance).
 struct PrepArgs {
   const float *W, *bias, *emb;
-  __bf16 *Ws, *bs, *xs;
+  _Float16 *Ws, *xs;
+  __bf16* bs;
   float *bsum, *WT, *xT;
+  const float* part;   // absmax_kernel block maxima
+  float* hdr;
   int in_n, JD, JDp, din, n_chunks, chunk_len, F, N, T, lpad, Fp;
   size_t xplane;
   size_t n_a, n_b, n_c, n_d, n_e, n_f;   // thread counts of the six ranges
 };
 
-__global__ void prep32_kernel(PrepArgs P) {
+__global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
+  // split exponents from the block maxima (every block reduces the same 2 x kAbsBlocks values)
+  __shared__ int sexp[2];
+  if (threadIdx.x < 128) {
+    const int y = threadIdx.x >> 6, l = threadIdx.x & 63;
+    float m = 0.f;
+    for (int k = l; k < kAbsBlocks; k += 64) m = fmaxf(m, P.part[y * kAbsBlocks + k]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (l == 0) sexp[y] = split_exp(m);
+  }
+  __syncthreads();
+  const int aw = sexp[0], bx = sexp[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    P.hdr[0] = exp2i(-(aw + bx));
+    P.hdr[1] = (float)aw;
+    P.hdr[2] = (float)bx;
+  }
   size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < P.n_a) {
     const size_t e0 = idx * 8;
@@ -130,15 +200,14 @@ __global__ void prep32_kernel(PrepArgs P) {
     const int row = rr % P.JDp;
     const size_t i = rr / P.JDp;
     const size_t nw = (size_t)P.in_n * P.JDp * P.din;
-    split8(P.W + (i * P.JD + min(row, P.JD - 1)) * P.din + e, row < P.JD, P.Ws + e0, P.Ws + nw + e0,
-           P.Ws + 2 * nw + e0);
+    split8h(P.W + (i * P.JD + min(row, P.JD - 1)) * P.din + e, row < P.JD, exp2i(aw), P.Ws + e0, P.Ws + nw + e0);
     return;
   }
   idx -= P.n_a;
   if (idx < P.n_b) {
     const int row = idx % P.JDp;
     const size_t i = idx / P.JDp;
-    const float b = row < P.JD ? P.bias[i * P.JD + row] : 0.f;
+    const float b = row < P.JD ? P.bias[i * P.JD + row] * exp2i(aw + bx) : 0.f;
     __bf16 b1, b2, b3;
     split3(b, b1, b2, b3);
     bf4 v = {b1, b2, b3, (__bf16)0.f};
@@ -163,8 +232,8 @@ __global__ void prep32_kernel(PrepArgs P) {
     const int f = rr % P.F;
     const int n = rr / P.F;
     const bool ok = e0 < n_data;
-    split8(P.emb + ((size_t)(ok ? f : 0) * P.N + (ok ? n : 0)) * P.din + (ok ? e : 0), ok, P.xs + e0,
-           P.xs + P.xplane + e0, P.xs + 2 * P.xplane + e0);
+    split8h(P.emb + ((size_t)(ok ? f : 0) * P.N + (ok ? n : 0)) * P.din + (ok ? e : 0), ok, exp2i(bx), P.xs + e0,
+            P.xs + P.xplane + e0);
     return;
   }
   idx -= P.n_d;
@@ -204,12 +273,12 @@ __global__ void prep32_kernel(PrepArgs P) {
 // ------------------------------------------------------------------ fragments
 // Per input capsule: A fragments (W splits) per tile, the bias fragment per tile,
 // B fragments (x splits) shared by the tiles.
-//   DIN 16: one MFMA covers din; A_p = W plane p (k = 8h + j), B_q = x plane q.
-//   DIN  8: K = 16 packs two planes: A1 = [W1 | W2], A2 = [W1 | W3],
-//           B1 = [x1 | x1], B2 = [x2 | x2], B3 = [x3 | x1] (lane half h holds k = 8h..8h+7):
-//           A1 B1 = W1x1 + W2x1, A1 B2 = W1x2 + W2x2, A2 B3 = W1x3 + W3x1.
-// Bias: A = (b1, b2, b3, 0, 0, 0, 0, 0) of the row, B = ones at k = 0..2 of lane
-// half 0 and zero elsewhere, so only (b1 + b2 + b3) reaches the accumulator.
+//   DIN 16: one MFMA covers din; A_p = W plane p (k = 8h + j), B_q = x plane q:
+//           W2x1, W1x2, W1x1.
+//   DIN  8: K = 16 packs two planes: A = [W1 | W2], B1 = [x1 | x1], B2 = [x2 | 0]
+//           (lane half h holds k = 8h..8h+7): A B2 = W1x2, A B1 = W1x1 + W2x1.
+// Bias: A = bf16 (b1, b2, b3, 0, 0, 0, 0, 0) of the row, B = ones at k = 0..2 of
+// lane half 0 and zero elsewhere, so only (b1 + b2 + b3) reaches the accumulator.
 // All operands come through buffer loads: one descriptor per array, the per-lane
 // byte offset in voffset (fixed per tile), the per-capsule / per-plane offset in
 // soffset.  Invalid window frames read the zero row at the end of each x plane.
@@ -223,22 +292,22 @@ constexpr int kWavesPerEU = 8 / kTW;
 
 template <int DIN>
 struct SplitFrags {
-  static constexpr int NA = DIN == 16 ? 3 : 2;
+  static constexpr int NA = DIN == 16 ? 2 : 1;
 };
 
 template <int DIN, int TW>
 struct Frags32 {
-  bf8 a[TW][SplitFrags<DIN>::NA];
+  h8 a[TW][SplitFrags<DIN>::NA];
   bf8 bias[TW];
-  bf8 b[3];
+  h8 b[2];
 };
 
 struct Rsrc3 {
   __amdgpu_buffer_rsrc_t w, b, x;
 };
 
-__device__ __forceinline__ bf8 bload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(bf8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+__device__ __forceinline__ h8 hload(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, size_t bytes) {
@@ -258,30 +327,39 @@ __device__ __forceinline__ uint32_t x_voff(int i, int N, int lpad, int T, int F,
   return ok ? o : zero_off;
 }
 
+// the two x fragments of one capsule (DIN 8: [x1 | x1] and [x2 | 0])
+template <int DIN>
+__device__ __forceinline__ void fetch_x(const Rsrc3& rs, uint32_t xvo, int h, uint32_t xplane_b, uint32_t zero_off,
+                                        h8 (&b)[2]) {
+  if constexpr (DIN == 16) {
+    b[0] = hload(rs.x, xvo, 0);
+    b[1] = hload(rs.x, xvo, xplane_b);
+  } else {
+    b[0] = hload(rs.x, xvo, 0);
+    b[1] = hload(rs.x, h ? zero_off : xvo, h ? 0u : xplane_b);
+  }
+}
+
+template <int DIN>
+__device__ __forceinline__ void fetch_w(const Rsrc3& rs, uint32_t vo, int h, uint32_t wplane_b, uint32_t wcap_b,
+                                        h8 (&a)[SplitFrags<DIN>::NA]) {
+  if constexpr (DIN == 16) {
+    a[0] = hload(rs.w, vo, wcap_b);
+    a[1] = hload(rs.w, vo, wcap_b + wplane_b);
+  } else {
+    a[0] = hload(rs.w, vo + (h ? wplane_b : 0), wcap_b);   // [W1 | W2]: lane half 1 reads plane 2
+  }
+}
+
 template <int DIN, int TW, bool BIAS>
 __device__ __forceinline__ void fetch32(const Rsrc3& rs, uint32_t wvo, uint32_t bvo, uint32_t xvo, int h,
-                                        uint32_t wplane_b, uint32_t xplane_b, uint32_t wcap_b, uint32_t bcap_b,
-                                        Frags32<DIN, TW>& fr) {
+                                        uint32_t wplane_b, uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
+                                        uint32_t bcap_b, Frags32<DIN, TW>& fr) {
   constexpr uint32_t TSTEP = 32 * DIN * 2;   // bytes between row tiles
-  if constexpr (DIN == 16) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p) fr.b[p] = bload(rs.x, xvo, p * xplane_b);
-  } else {
-    fr.b[0] = bload(rs.x, xvo, 0);
-    fr.b[1] = bload(rs.x, xvo, xplane_b);
-    fr.b[2] = bload(rs.x, xvo + (h == 0 ? 2 * xplane_b : 0), 0);   // [x3 | x1]: lane-dependent plane
-  }
+  fetch_x<DIN>(rs, xvo, h, xplane_b, zero_off, fr.b);
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
-    const uint32_t vo = wvo + t * TSTEP;
-    if constexpr (DIN == 16) {
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fr.a[t][p] = bload(rs.w, vo, wcap_b + p * wplane_b);
-    } else {
-      // lane half 1 reads plane 2 / plane 3 through a voffset shift
-      fr.a[t][0] = bload(rs.w, vo + (h ? wplane_b : 0), wcap_b);
-      fr.a[t][1] = bload(rs.w, vo + (h ? 2 * wplane_b : 0), wcap_b);
-    }
+    fetch_w<DIN>(rs, wvo + t * TSTEP, h, wplane_b, wcap_b, fr.a[t]);
     if constexpr (BIAS) {
       // (b1, b2, b3, 0) of the row; the upper half of the fragment stays zero
       const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap_b, 0);
@@ -291,18 +369,14 @@ __device__ __forceinline__ void fetch32(const Rsrc3& rs, uint32_t wvo, uint32_t 
 }
 
 template <int DIN>
-__device__ __forceinline__ f16v pose_chain(const bf8 (&a)[SplitFrags<DIN>::NA], const bf8 (&b)[3], f16v acc) {
+__device__ __forceinline__ f16v pose_chain(const h8 (&a)[SplitFrags<DIN>::NA], const h8 (&b)[2], f16v acc) {
   if constexpr (DIN == 16) {   // small terms first
-    acc = mfma32(a[2], b[0], acc);   // W3 x1
-    acc = mfma32(a[0], b[2], acc);   // W1 x3
-    acc = mfma32(a[1], b[1], acc);   // W2 x2
-    acc = mfma32(a[1], b[0], acc);   // W2 x1
-    acc = mfma32(a[0], b[1], acc);   // W1 x2
-    acc = mfma32(a[0], b[0], acc);   // W1 x1
+    acc = mfma32h(a[1], b[0], acc);   // W2 x1
+    acc = mfma32h(a[0], b[1], acc);   // W1 x2
+    acc = mfma32h(a[0], b[0], acc);   // W1 x1
   } else {
-    acc = mfma32(a[1], b[2], acc);   // W1 x3 + W3 x1
-    acc = mfma32(a[0], b[1], acc);   // W1 x2 + W2 x2
-    acc = mfma32(a[0], b[0], acc);   // W1 x1 + W2 x1
+    acc = mfma32h(a[0], b[1], acc);   // W1 x2
+    acc = mfma32h(a[0], b[0], acc);   // W1 x1 + W2 x1
   }
   return acc;
 }
@@ -321,7 +395,8 @@ __device__ __forceinline__ constexpr int kpart(int t, int v) {
 }
 
 struct Args32 {
-  const __bf16 *Ws, *bs, *xs;
+  const void *Ws, *bs, *xs;
+  const float* hdr;   // {2^-(aw+bx), aw, bx} of the operand planes (prep32_kernel)
   size_t ws_bytes, bs_bytes, xs_bytes;
   uint32_t wplane_b, xplane_b, zero_off;
   int F, T, N, lpad, in_n, J, JDp, n_chunks, chunk_len, mask_first, n_tgroups;
@@ -349,33 +424,18 @@ constexpr int kFTW = 2;
 
 template <int DIN>
 struct FirstFrags {
-  bf8 a[kFTW][SplitFrags<DIN>::NA];
-  bf8 b[3];
+  h8 a[kFTW][SplitFrags<DIN>::NA];
+  h8 b[2];
 };
 
 template <int DIN>
 __device__ __forceinline__ void fetch_first(const Rsrc3& rs, uint32_t wvo, uint32_t xvo, int h, uint32_t wplane_b,
-                                            uint32_t xplane_b, uint32_t wcap_b, FirstFrags<DIN>& fr) {
+                                            uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
+                                            FirstFrags<DIN>& fr) {
   constexpr uint32_t TSTEP = 32 * DIN * 2;
-  if constexpr (DIN == 16) {
+  fetch_x<DIN>(rs, xvo, h, xplane_b, zero_off, fr.b);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) fr.b[p] = bload(rs.x, xvo, p * xplane_b);
-  } else {
-    fr.b[0] = bload(rs.x, xvo, 0);
-    fr.b[1] = bload(rs.x, xvo, xplane_b);
-    fr.b[2] = bload(rs.x, xvo + (h == 0 ? 2 * xplane_b : 0), 0);
-  }
-#pragma unroll
-  for (int t = 0; t < kFTW; ++t) {
-    const uint32_t vo = wvo + t * TSTEP;
-    if constexpr (DIN == 16) {
-#pragma unroll
-      for (int p = 0; p < 3; ++p) fr.a[t][p] = bload(rs.w, vo, wcap_b + p * wplane_b);
-    } else {
-      fr.a[t][0] = bload(rs.w, vo + (h ? wplane_b : 0), wcap_b);
-      fr.a[t][1] = bload(rs.w, vo + (h ? 2 * wplane_b : 0), wcap_b);
-    }
-  }
+  for (int t = 0; t < kFTW; ++t) fetch_w<DIN>(rs, wvo + t * TSTEP, h, wplane_b, wcap_b, fr.a[t]);
 }
 
 template <int DIN, int DOUT>
@@ -401,7 +461,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   for (int t = 0; t < kFTW; ++t) acc[t] = f16v{};
   auto fetch = [&](int i, FirstFrags<DIN>& fr) {
     fetch_first<DIN>(rs, wvo, x_voff<DIN>(i, A.N, A.lpad, A.T, A.F, f, ftt, fv, h, A.zero_off), h, A.wplane_b,
-                     A.xplane_b, (uint32_t)i * capb, fr);
+                     A.xplane_b, A.zero_off, (uint32_t)i * capb, fr);
   };
   auto mfmas = [&](const FirstFrags<DIN>& fr) {
 #pragma unroll
@@ -420,6 +480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     if (i < i1) mfmas(f0);
   }
   const int Jeff = A.J - (A.mask_first ? 1 : 0);
+  const float inv = A.hdr[0];
 #pragma unroll
   for (int t = 0; t < kFTW; ++t)
 #pragma unroll
@@ -430,7 +491,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
       if (fv && row < JD) {
         const f4 bsv = *reinterpret_cast<const f4*>(A.bsum + (size_t)chunk * JD + row);
         f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = (v + bsv) * c0;
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = (v * inv + bsv) * c0;
       }
     }
 }
@@ -482,6 +543,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     mk[a] = (j < A.J && !(A.mask_first && j == 0)) ? 0.f : -INFINITY;
   }
   const bf8 ones = ones_frag(h);
+  const float inv = A.hdr[0];   // 2^-(aw+bx): the pose tiles hold 2^(aw+bx) u
   f16v acc[TW];
 #pragma unroll
   for (int t = 0; t < TW; ++t) acc[t] = f16v{};
@@ -489,7 +551,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   if (i0 < i1) {
     Frags32<DIN, TW> fr;
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                           A.wplane_b, A.xplane_b, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8, fr);
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
+                           fr);
 #if SRF_FWD32_DBG == 4
     unsigned long long tph[5] = {0, 0, 0, 0, 0};
     unsigned long long tlast = __builtin_amdgcn_s_memtime();
@@ -504,7 +567,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       SRF_TMARK(0)
       if (SRF_FWD32_FETCH_EARLY && i + 1 < i1)
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                               A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
+                               A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
       if (SRF_FWD32_FETCH_EARLY) __builtin_amdgcn_sched_barrier(0);
       // partial agreement dots <u_ij, Vc_j> over this lane's rows (packed FMA pairs)
@@ -527,7 +590,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       for (int a = 0; a < OWN; ++a) {
         const float pa = P2[2 * a].x + P2[2 * a].y, pb = P2[2 * a + 1].x + P2[2 * a + 1].y;
         const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa), __float_as_uint(pb), false, false);
-        L[a] = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + mk[a];
+        L[a] = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) * inv + mk[a];
         m = fmaxf(m, L[a]);
       }
       float z = 0.f;
@@ -580,7 +643,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       __builtin_amdgcn_sched_barrier(0);
       if (!SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                               A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
+                               A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
       __builtin_amdgcn_sched_barrier(0);
       SRF_TMARK(1)
@@ -631,7 +694,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       const int row = (tbase + t) * 32 + 8 * q + 4 * h;
       if (fvalid && row < JD) {
         f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v;
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v * inv;
       }
     }
 }
@@ -698,6 +761,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       gsl[(t * 4 + q) * 64 + lane] = v;
     }
   const bf8 ones = ones_frag(h);
+  const float inv = A.hdr[0];   // 2^-(aw+bx): the pose tiles hold 2^(aw+bx) u
   f16v acc[TW];
 #pragma unroll
   for (int t = 0; t < TW; ++t) acc[t] = f16v{};
@@ -711,7 +775,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cn);
 #endif
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                           A.wplane_b, A.xplane_b, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8, fr);
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
+                           fr);
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
 #pragma unroll
@@ -746,7 +811,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       for (int a = 0; a < OWN; ++a) {
         const float pa = P2[2 * a].x + P2[2 * a].y, pb = P2[2 * a + 1].x + P2[2 * a + 1].y;
         const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa), __float_as_uint(pb), false, false);
-        Q[a] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        Q[a] = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) * inv;
         sp += cc[a] * Q[a];
       }
       float S;
@@ -771,7 +836,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       __builtin_amdgcn_sched_barrier(0);
       if (i + 1 < i1) {
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
-                               h, A.wplane_b, A.xplane_b, (uint32_t)(i + 1) * A.JDp * DIN * 2,
+                               h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -815,7 +880,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       const int row = (tbase + t) * 32 + 8 * q + 4 * h;
       if (fvalid && row < JD) {
         f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v;
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v * inv;
       }
     }
 }
@@ -864,15 +929,16 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   p.chunk_len = (in_n + best - 1) / best;
   p.n_ftiles = n_ftiles;
   p.xplane = (size_t)F * N * din + 16;
-  p.ws_w = srf::align_up((size_t)3 * in_n * p.JDp * din * 2, 256);
+  p.ws_w = srf::align_up((size_t)2 * in_n * p.JDp * din * 2, 256);
   p.ws_b = srf::align_up((size_t)in_n * p.JDp * 4 * 2, 256);
-  p.ws_x = srf::align_up((size_t)3 * p.xplane * 2, 256);
+  p.ws_x = srf::align_up((size_t)2 * p.xplane * 2, 256);
+  p.ws_h = (size_t)(2 * kAbsBlocks + 64) * 4;   // header + absmax block maxima
   p.ws_bsum = srf::align_up((size_t)best * JD * 4, 256);
   p.ws_slab = srf::align_up((size_t)best * F * JD * 4, 256);
   return p;
 }
 
-size_t fwd32_planes_bytes(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x; }
+size_t fwd32_planes_bytes(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x + p.ws_h; }
 size_t fwd32_scratch_bytes(const Fwd32Plan& p) { return p.ws_bsum + p.ws_slab; }
 size_t fwd32_workspace(const Fwd32Plan& p) { return fwd32_planes_bytes(p) + fwd32_scratch_bytes(p); }
 float* fwd32_slab(const Fwd32Plan& p, void* scratch) {
@@ -887,13 +953,20 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
                   int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
                   hipStream_t st) {
   char* base = static_cast<char*>(planes);
+  float* hdr = reinterpret_cast<float*>(base + p.ws_w + p.ws_b + p.ws_x);
+  const int in_n = N * (lpad + rpad + 1);
+  hipLaunchKernelGGL(absmax_kernel, dim3(kAbsBlocks, 2), dim3(256), 0, st, W, (size_t)in_n * J * dout * din, emb,
+                     (size_t)B * T * N * din, hdr + 64);
+  SRF_LAUNCH_CHECK("absmax");
   PrepArgs P;
   P.W = W;
   P.bias = bias;
   P.emb = emb;
-  P.Ws = reinterpret_cast<__bf16*>(base);
+  P.Ws = reinterpret_cast<_Float16*>(base);
   P.bs = reinterpret_cast<__bf16*>(base + p.ws_w);
-  P.xs = reinterpret_cast<__bf16*>(base + p.ws_w + p.ws_b);
+  P.xs = reinterpret_cast<_Float16*>(base + p.ws_w + p.ws_b);
+  P.part = hdr + 64;
+  P.hdr = hdr;
   P.bsum = reinterpret_cast<float*>(scratch);
   P.WT = WT;
   P.xT = xT;
@@ -956,12 +1029,13 @@ static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch,
   const int in_n = N * (lpad + rpad + 1);
   const char* base = static_cast<const char*>(planes);
   Args32 a;
-  a.Ws = reinterpret_cast<const __bf16*>(base);
-  a.bs = reinterpret_cast<const __bf16*>(base + p.ws_w);
-  a.xs = reinterpret_cast<const __bf16*>(base + p.ws_w + p.ws_b);
+  a.Ws = base;
+  a.bs = base + p.ws_w;
+  a.xs = base + p.ws_w + p.ws_b;
+  a.hdr = reinterpret_cast<const float*>(base + p.ws_w + p.ws_b + p.ws_x);
   a.ws_bytes = p.ws_w;
   a.bs_bytes = (size_t)in_n * p.JDp * 8;
-  a.xs_bytes = 3 * p.xplane * 2;
+  a.xs_bytes = 2 * p.xplane * 2;
   a.wplane_b = (uint32_t)((size_t)in_n * p.JDp * din * 2);
   a.xplane_b = (uint32_t)(p.xplane * 2);
   a.zero_off = (uint32_t)((p.xplane - 16) * 2);
@@ -1011,7 +1085,7 @@ int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch
   a.vc = vc;
   a.cst = first ? nullptr : cst;
   a.lzst = first ? nullptr : lzst;
-  SRF_REQUIRE(3 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
+  SRF_REQUIRE(2 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
 #define SRF_P32(DI, DO) \
   if (din == DI && dout == DO) return launch_pass32_t<DI, DO>(p, first, a, st);
   SRF_P32(8, 8)
