@@ -1716,15 +1716,17 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
         cst = couplings + cl.c + (size_t)(r - 1) * blk * (plan.JDp / g.dout);
         lzst = couplings + cl.lz + (size_t)(r - 1) * blk;
       }
-      const int rc = srf::fwd32_pass(plan, r == 0, planes, scratch, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J,
-                                     g.dout, g.mask_first, vc, cst, lzst, st);
+      const int rc = srf::fwd32_pass(plan, r == 0, planes, scratch,
+                                     static_cast<char*>(scratch) + srf::fwd32_scratch_bytes(plan), g.B, g.T, g.N,
+                                     g.din, g.lpad, g.rpad, g.J, g.dout, g.mask_first, vc, cst, lzst, st);
       if (rc) return rc;
     } else {
       dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, r == 0 ? bsum : nullptr, slab, nullptr, 1, st);
     }
     SRF_LAUNCH_CHECK("route_pass(fwd)");
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev1[r], st));
-    launch_fwd_finish<D>(g, p32 ? srf::fwd32_slab(plan, scratch) : slab, p32 ? plan.n_chunks : n_chunks, vc,
+    launch_fwd_finish<D>(g, p32 ? srf::fwd32_slab(plan, scratch) : slab,
+                         p32 ? srf::fwd32_pass_chunks(plan, r == 0) : n_chunks, vc,
                          saved + (size_t)(2 * r) * FJD, saved + (size_t)(2 * r + 1) * FJD,
                          r == g.iters - 1 ? v_out : nullptr, st);
     SRF_LAUNCH_CHECK("fwd_finish");

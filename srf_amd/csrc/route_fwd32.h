@@ -20,6 +20,11 @@ struct Fwd32Plan {
   int n_chunks, chunk_len, n_ftiles;
   size_t xplane;       // elements per x plane (data + zero row)
   size_t ws_w, ws_b, ws_x, ws_h, ws_bsum, ws_slab;   // workspace regions (bytes)
+  // split passes r >= 1 (route_logit / route_lse / route_acc): NWS waves per workgroup,
+  // n_rb row blocks of 64*NWS rows, n_fb 64-frame blocks, logit i-chunks nchL x clenL
+  bool split;
+  int NWS, n_rb, n_fb, nchL, clenL, nchA, clenA;   // route_acc i-chunks nchA x clenA (its slabs)
+  size_t ws_lg, ws_part, ws_lz;   // logits, row-block partials, logZ (bytes)
 };
 
 bool fwd32_supported(int din, int dout, int J);
@@ -30,7 +35,8 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
 // training forward keeps its planes for the backward (coupling storage).
 size_t fwd32_planes_bytes(const Fwd32Plan& p);
 size_t fwd32_scratch_bytes(const Fwd32Plan& p);
-size_t fwd32_workspace(const Fwd32Plan& p);   // planes + scratch
+size_t fwd32_split_bytes(const Fwd32Plan& p);   // logits / partials / logZ of the split passes
+size_t fwd32_workspace(const Fwd32Plan& p);   // planes + scratch + split
 size_t fwd32_lds(const Fwd32Plan& p);
 float* fwd32_slab(const Fwd32Plan& p, void* scratch);
 // split W / emb into scaled fp16 planes, bias into bf16 planes, and the i-chunk bias
@@ -41,10 +47,13 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
                   int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
                   hipStream_t st);
 // one routing pass: partial s over i-chunks into fwd32_slab(p, scratch); passes r >= 1
-// also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr
-int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T, int N, int din,
-               int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst, float* lzst,
-               hipStream_t st);
+// also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr.  With
+// p.split and split_ws (fwd32_split_bytes) a pass r >= 1 runs as the three split kernels.
+// i-chunk slabs a pass leaves for fwd_finish
+inline int fwd32_pass_chunks(const Fwd32Plan& p, bool first) { return !first && p.split ? p.nchA : p.n_chunks; }
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, void* split_ws, int B, int T,
+               int N, int din, int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst,
+               float* lzst, hipStream_t st);
 // Coupling storage of one training forward (float offsets): c^r [iters-1][in_n][JP][Fs],
 // logZ^r [iters-1][in_n][Fs], the operand planes, WT, xT; JP = JDp / dout,
 // Fs = fwd32_frame_stride(F).

@@ -64,6 +64,9 @@
 #ifndef SRF_BWD32_CPREFETCH
 #define SRF_BWD32_CPREFETCH 0   // 1: couplings of capsule i+1 loaded during capsule i (4 more live registers)
 #endif
+#ifndef SRF_SPLIT_DBG
+#define SRF_SPLIT_DBG 0
+#endif
 #ifndef SRF_FWD32_FASTDIV
 #define SRF_FWD32_FASTDIV 0
 #endif
@@ -319,6 +322,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, size_
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
 
+// raw buffer store of one float; a voffset past the buffer drops it (no branch, so the
+// compiler's vmcnt bookkeeping stays exact)
+constexpr uint32_t kNoStore = 0x80000000u;
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t rs, float v, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, voff, soff, 0);
+}
+
 // Window source of capsule i = w*N + n for this lane (naive:150-151): frame
 // t + w - lpad of the same utterance, i.e. row f + w - lpad of capsule n's plane,
 // or the zero row when it falls outside [0, T).
@@ -389,7 +399,7 @@ __device__ __forceinline__ f16v pose_chain(const h8 (&a)[SplitFrags<DIN>::NA], c
 // The pose tiles of one capsule (as pose_chain, bias first) with the next capsule's
 // operands loaded into each register group right after its last reader is issued.
 template <int DIN, int TW>
-__device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones, f16v (&u)[TW], bool next,
+__device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones, f16v (&u)[TW],
                                           const Rsrc3& rs, uint32_t wvo, uint32_t bvo, uint32_t xvo, int h,
                                           uint32_t wplane_b, uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
                                           uint32_t bcap_b) {
@@ -397,7 +407,7 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
 #pragma unroll
   for (int t = 0; t < TW; ++t) u[t] = mfma32(fr.bias[t], ones, f16v{});
   __builtin_amdgcn_sched_barrier(0);
-  if (next) {
+  {
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
       const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap_b, 0);
@@ -409,7 +419,7 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
 #pragma unroll
     for (int t = 0; t < TW; ++t) u[t] = mfma32h(fr.a[t][1], fr.b[0], u[t]);   // W2 x1
     __builtin_amdgcn_sched_barrier(0);
-    if (next) {
+    {
 #pragma unroll
       for (int t = 0; t < TW; ++t) fr.a[t][1] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b);
     }
@@ -417,19 +427,19 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
 #pragma unroll
     for (int t = 0; t < TW; ++t) u[t] = mfma32h(fr.a[t][0], fr.b[1], u[t]);   // W1 x2
     __builtin_amdgcn_sched_barrier(0);
-    if (next) fr.b[1] = hload(rs.x, xvo, xplane_b);
+    fr.b[1] = hload(rs.x, xvo, xplane_b);
     __builtin_amdgcn_sched_barrier(0);
   } else {
 #pragma unroll
     for (int t = 0; t < TW; ++t) u[t] = mfma32h(fr.a[t][0], fr.b[1], u[t]);   // W1 x2
     __builtin_amdgcn_sched_barrier(0);
-    if (next) fr.b[1] = hload(rs.x, h ? zero_off : xvo, h ? 0u : xplane_b);
+    fr.b[1] = hload(rs.x, h ? zero_off : xvo, h ? 0u : xplane_b);
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int t = 0; t < TW; ++t) u[t] = mfma32h(fr.a[t][0], fr.b[0], u[t]);   // W1 x1 (+ W2 x1 for DIN 8)
   __builtin_amdgcn_sched_barrier(0);
-  if (next) {
+  {
 #pragma unroll
     for (int t = 0; t < TW; ++t) fr.a[t][0] = hload(rs.w, wvo + t * TSTEP + (DIN == 8 && h ? wplane_b : 0), wcap_b);
     fr.b[0] = hload(rs.x, xvo, 0);
@@ -465,6 +475,11 @@ struct Args32 {
   float* cst;
   float* lzst;
   int JP, Fs;
+  // split passes (route_logit_kernel / route_lse_kernel / route_acc_kernel)
+  float* lg;       // logits L^r [in_n][JP][Fs] (the couplings overwrite them in place when cst == lg)
+  float2* part;    // per-row-block (max, sum exp) [in_n][n_rb][Fs]
+  float* lz;       // logZ^r [in_n][Fs]
+  int n_rb, n_fb, nchL, clenL;
 };
 
 
@@ -472,56 +487,62 @@ struct Args32 {
 // ------------------------------------------------------------------ kernels
 // Iteration-0 pass (naive:172-181: logits 0 + mask, so c is uniform):
 // s = c0 (sum_i W_i x_i + sum_i b_i).  A pure GEMM: each wave owns
-// (32 frames, kFTW row tiles, i-chunk) and accumulates the pose sum in its MFMA
+// (kFFB x 32 frames, kFTW row tiles, i-chunk) and accumulates the pose sum in its MFMA
 // accumulators; the chunk's bias sum is added at the end.  Operands are double
 // buffered: capsule k+1's loads are issued before capsule k's MFMAs, into the
 // registers capsule k-1 used, so no load waits on a queued MFMA's operand read.
-constexpr int kFTW = 2;
+constexpr int kSplitMaxCl = 32;   // capsules per route_logit_kernel workgroup (LDS partials)
+constexpr int kFTW = 2;   // row tiles per wave
+constexpr int kFFB = 2;   // frame tiles per wave
 
 template <int DIN>
 struct FirstFrags {
   h8 a[kFTW][SplitFrags<DIN>::NA];
-  h8 b[2];
+  h8 b[kFFB][2];
 };
 
-template <int DIN>
-__device__ __forceinline__ void fetch_first(const Rsrc3& rs, uint32_t wvo, uint32_t xvo, int h, uint32_t wplane_b,
-                                            uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
-                                            FirstFrags<DIN>& fr) {
-  constexpr uint32_t TSTEP = 32 * DIN * 2;
-  fetch_x<DIN>(rs, xvo, h, xplane_b, zero_off, fr.b);
-#pragma unroll
-  for (int t = 0; t < kFTW; ++t) fetch_w<DIN>(rs, wvo + t * TSTEP, h, wplane_b, wcap_b, fr.a[t]);
-}
-
 template <int DIN, int DOUT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void route_fwd32_first_kernel(Args32 A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void route_fwd32_first_kernel(Args32 A) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int chunk = task % A.n_chunks;
   const int rest = task / A.n_chunks;
-  const int tg = rest % A.n_tgroups, ft = rest / A.n_tgroups;
-  if (ft * 32 >= A.F) return;
+  const int tg = rest % A.n_tgroups, fp = rest / A.n_tgroups;
+  if (fp * 32 * kFFB >= A.F) return;
   const int tbase = tg * kFTW;
   const int JD = A.J * DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
-  const int f = ft * 32 + r;
-  const int fc = min(f, A.F - 1);
-  const int fb = fc / A.T, ftt = fc - fb * A.T;
-  const bool fv = f < A.F;
+  int f[kFFB], ftt[kFFB];
+  bool fv[kFFB];
+#pragma unroll
+  for (int b = 0; b < kFFB; ++b) {
+    f[b] = (fp * kFFB + b) * 32 + r;
+    const int fc = min(f[b], A.F - 1);
+    ftt[b] = fc - (fc / A.T) * A.T;
+    fv[b] = f[b] < A.F;
+  }
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
   const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
   const uint32_t capb = (uint32_t)A.JDp * DIN * 2;
-  f16v acc[kFTW];
+  constexpr uint32_t TSTEP = 32 * DIN * 2;
+  f16v acc[kFTW][kFFB];
 #pragma unroll
-  for (int t = 0; t < kFTW; ++t) acc[t] = f16v{};
+  for (int t = 0; t < kFTW; ++t)
+#pragma unroll
+    for (int b = 0; b < kFFB; ++b) acc[t][b] = f16v{};
   auto fetch = [&](int i, FirstFrags<DIN>& fr) {
-    fetch_first<DIN>(rs, wvo, x_voff<DIN>(i, A.N, A.lpad, A.T, A.F, f, ftt, fv, h, A.zero_off), h, A.wplane_b,
-                     A.xplane_b, A.zero_off, (uint32_t)i * capb, fr);
+#pragma unroll
+    for (int b = 0; b < kFFB; ++b)
+      fetch_x<DIN>(rs, x_voff<DIN>(i, A.N, A.lpad, A.T, A.F, f[b], ftt[b], fv[b], h, A.zero_off), h, A.xplane_b,
+                   A.zero_off, fr.b[b]);
+#pragma unroll
+    for (int t = 0; t < kFTW; ++t) fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, (uint32_t)i * capb, fr.a[t]);
   };
   auto mfmas = [&](const FirstFrags<DIN>& fr) {
 #pragma unroll
-    for (int t = 0; t < kFTW; ++t) acc[t] = pose_chain<DIN>(fr.a[t], fr.b, acc[t]);
+    for (int t = 0; t < kFTW; ++t)
+#pragma unroll
+      for (int b = 0; b < kFFB; ++b) acc[t][b] = pose_chain<DIN>(fr.a[t], fr.b[b], acc[t][b]);
   };
   if (i0 < i1) {
     FirstFrags<DIN> f0, f1;
@@ -544,10 +565,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
       const int row = (tbase + t) * 32 + 8 * q + 4 * h;
       const int j = row / DOUT;
       const float c0 = (j < A.J && !(A.mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
-      if (fv && row < JD) {
+      if (row < JD) {
         const f4 bsv = *reinterpret_cast<const f4*>(A.bsum + (size_t)chunk * JD + row);
-        f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
-        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = (v * inv + bsv) * c0;
+#pragma unroll
+        for (int b = 0; b < kFFB; ++b) {
+          if (!fv[b]) continue;
+          f4 v = {acc[t][b][4 * q], acc[t][b][4 * q + 1], acc[t][b][4 * q + 2], acc[t][b][4 * q + 3]};
+          *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f[b]) * JD + row) = (v * inv + bsv) * c0;
+        }
       }
     }
 }
@@ -578,6 +603,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #endif
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
+  const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
+  const __amdgpu_buffer_rsrc_t lzs = make_rsrc(A.lzst, A.cst ? (size_t)A.in_n * A.Fs * 4 : 0);
 
   f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
@@ -619,9 +646,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
 #if SRF_FWD32_PROG
-      pose_prog<DIN, TW>(fr, ones, u, i + 1 < i1, rs, wvo, bvo,
-                         x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                         A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2, (uint32_t)(i + 1) * A.JDp * 8);
+      const int in = min(i + 1, i1 - 1);
+      pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
+                         x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                         A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
 #else
 #pragma unroll
       for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
@@ -715,13 +743,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #else
       const float sc = __expf(m - M) / Z;
 #endif
-      if (A.cst != nullptr) {
+      {
         // lane half h owns capsules j0 + 2a + h after the logit reduce-scatter; frames
-        // past F (up to the 32-frame stride) store 0, which the gW pass relies on
-        float* dst = A.cst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
+        // past F (up to the 32-frame stride) store 0, which the gW pass relies on.
+        // Branch-free buffer stores (no storage: zero-record descriptors drop them).
 #pragma unroll
-        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = fvalid ? e[a] * sc : 0.f;
-        if (h == 0 && wv == 0 && fvalid) A.lzst[(size_t)i * A.Fs + f] = M + __logf(Z);
+        for (int a = 0; a < OWN; ++a)
+          bstore(crs, fvalid ? e[a] * sc : 0.f, (uint32_t)((j0 + h + 2 * a) * A.Fs + f) * 4u,
+                 (uint32_t)i * A.JP * A.Fs * 4u);
+        bstore(lzs, M + __logf(Z), (h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore,
+               (uint32_t)i * A.Fs * 4u);
       }
       float c[CP];
 #pragma unroll
@@ -828,6 +859,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #pragma unroll
   for (int t = 0; t < TW; ++t) acc[t] = f16v{};
   const float* crow = Bk.cst + (size_t)(j0 + h) * A.Fs + fc;
+  const __amdgpu_buffer_rsrc_t sts = make_rsrc(Bk.stats, (size_t)A.F * A.in_n * 8);
   const size_t cstep = (size_t)A.JP * A.Fs;   // next capsule i
   int par = 0;
   if (i0 < i1) {
@@ -842,9 +874,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
 #if SRF_FWD32_PROG
-      pose_prog<DIN, TW>(fr, ones, u, i + 1 < i1, rs, wvo, bvo,
-                         x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                         A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2, (uint32_t)(i + 1) * A.JDp * 8);
+      const int in = min(i + 1, i1 - 1);
+      pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
+                         x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                         A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
 #else
 #pragma unroll
       for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
@@ -908,9 +941,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (wv == 0 && h == 0 && fvalid) {
-        const size_t fi = (size_t)f * A.in_n + i;
-        *reinterpret_cast<f2*>(Bk.stats + fi * 2) = f2{Bk.lz[(size_t)i * A.Fs + f], S};
+      {
+        // (logZ, sigma) of frame f, capsule i: branch-free (wave 0, half 0, valid frames)
+        const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
+        __builtin_amdgcn_raw_buffer_store_b64(
+            (unsigned __attribute__((ext_vector_type(2)))){__float_as_uint(lzv), __float_as_uint(S)}, sts,
+            (wv == 0 && h == 0 && fvalid) ? (uint32_t)(f * A.in_n) * 8u : kNoStore, (uint32_t)i * 8u, 0);
       }
       // gL of the owned capsules (stored for the gu pass), then all-gather over the lane halves
       float gown[OWN];
@@ -951,6 +987,402 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v * inv;
       }
     }
+}
+
+
+// ------------------------------------------------------------------ split passes
+// A routing pass r >= 1 as three launches instead of one (route_fwd32_kernel keeps
+// all J*dout rows of 32 frames on one CU, which ties its waves together at one
+// softmax barrier per input capsule and re-streams all of W for every 32 frames):
+//   route_logit_kernel: L_ij = <u_ij, Vc_j> for a block of rows x 64 frames and an
+//       i-chunk (pose on the split-fp16 tiles; no softmax, no accumulator), plus the
+//       block's (max, sum exp) over its j;
+//   route_lse_kernel:   logZ_i = log sum_j exp L_ij from the row-block partials;
+//   route_acc_kernel:   c_ij = exp(L_ij - logZ_i) (stored over L as the coupling
+//       storage when training) and s_j += c_ij u_ij over an i-chunk (pose recomputed).
+// A wave owns 2 row tiles x 2 frame tiles (64 rows x 64 frames), so each W fragment
+// serves two frame tiles and each x fragment two row tiles.  Supported: dout 16, 32.
+template <int DIN>
+struct Frags22 {
+  h8 a[2][SplitFrags<DIN>::NA];
+  bf8 bias[2];
+  h8 x[2][2];
+};
+
+// Loads in the order the pose consumes them (bias, then the operands of each product
+// step), so a wait for the first step leaves the rest in flight.
+template <int DIN>
+__device__ __forceinline__ void fetch22(const Rsrc3& rs, uint32_t wvo, uint32_t bvo, const uint32_t (&xvo)[2], int h,
+                                        uint32_t wplane_b, uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
+                                        uint32_t bcap_b, Frags22<DIN>& fr) {
+  constexpr uint32_t TSTEP = 32 * DIN * 2;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap_b, 0);
+    fr.bias[t] = __builtin_bit_cast(bf8, (unsigned __attribute__((ext_vector_type(4)))){v2[0], v2[1], 0u, 0u});
+  }
+  if constexpr (DIN == 16) {
+    // W2 x1, W1 x2, W1 x1
+#pragma unroll
+    for (int b = 0; b < 2; ++b) fr.x[b][0] = hload(rs.x, xvo[b], 0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) fr.a[t][1] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) fr.x[b][1] = hload(rs.x, xvo[b], xplane_b);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) fr.a[t][0] = hload(rs.w, wvo + t * TSTEP, wcap_b);
+  } else {
+    // W1 x2, W1 x1 (+ W2 x1)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) fr.a[t][0] = hload(rs.w, wvo + t * TSTEP + (h ? wplane_b : 0), wcap_b);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) fr.x[b][1] = hload(rs.x, h ? zero_off : xvo[b], h ? 0u : xplane_b);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) fr.x[b][0] = hload(rs.x, xvo[b], 0);
+  }
+}
+
+// u[b] = pose tiles (row tile t, frame tiles b = 0, 1) of one capsule, bias first
+template <int DIN>
+__device__ __forceinline__ void pose22t(const Frags22<DIN>& fr, int t, const bf8& ones, f16v (&u)[2]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b) u[b] = pose_chain<DIN>(fr.a[t], fr.x[b], mfma32(fr.bias[t], ones, f16v{}));
+}
+
+// all four tiles, the four chains interleaved step by step (same products and order
+// as pose_chain, so the tiles are bit-identical to pose22t's)
+template <int DIN>
+__device__ __forceinline__ void pose22(const Frags22<DIN>& fr, const bf8& ones, f16v (&u)[2][2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) u[t][b] = mfma32(fr.bias[t], ones, f16v{});
+  if constexpr (DIN == 16) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][1], fr.x[b][0], u[t][b]);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][0], fr.x[b][1], u[t][b]);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][0], fr.x[b][1], u[t][b]);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][0], fr.x[b][0], u[t][b]);
+}
+
+// shared setup of the split kernels: one wave = row tiles 2*(rb*NWv + w) + {0,1},
+// frame tiles 2*fbk + {0,1}
+struct Tile22 {
+  int tg, f[2], ftt[2];
+  bool fv[2];
+  uint32_t wvo, bvo;
+};
+template <int DIN>
+__device__ __forceinline__ Tile22 tile22(const Args32& A, int rb, int NWv, int w, int fbk, int r, int h) {
+  Tile22 T;
+  T.tg = 2 * (rb * NWv + w);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    T.f[b] = (2 * fbk + b) * 32 + r;
+    const int fc = min(T.f[b], A.F - 1);
+    T.ftt[b] = fc - (fc / A.T) * A.T;
+    T.fv[b] = T.f[b] < A.F;
+  }
+  T.wvo = (uint32_t)(((T.tg * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  T.bvo = (uint32_t)((T.tg * 32 + r) * 8);
+  return T;
+}
+
+template <int DIN>
+__device__ __forceinline__ void xvo22(const Args32& A, const Tile22& T, int i, int h, uint32_t (&xvo)[2]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b) xvo[b] = x_voff<DIN>(i, A.N, A.lpad, A.T, A.F, T.f[b], T.ftt[b], T.fv[b], h, A.zero_off);
+}
+
+// grid: n_fb * n_rb * nchL (chunk fastest); block: NWL waves; LDS: the Vc tile
+// (64 x (64 NWL + 4) floats), then clenL * NWL * 64 float2 partials
+template <int DIN, int DOUT, int NWL>
+__global__ __launch_bounds__(64 * NWL) __attribute__((amdgpu_waves_per_eu(2))) void route_logit_kernel(Args32 A) {
+  static_assert(DOUT == 16 || DOUT == 32, "split passes: dout 16 or 32");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float2* pst = reinterpret_cast<float2*>(lds);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int chunk = blockIdx.x % A.nchL;
+  const int rest = blockIdx.x / A.nchL;
+  const int rb = rest % A.n_rb, fbk = rest / A.n_rb;
+  const int JD = A.J * DOUT;
+  const Tile22 T = tile22<DIN>(A, rb, NWL, w, fbk, r, h);
+  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+  const int i0 = chunk * A.clenL, i1 = min(A.in_n, i0 + A.clenL);
+  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(A.lg, (size_t)A.in_n * A.JP * A.Fs * 4);
+  // Vc of the workgroup's 64 frames x 64*NWL rows, staged through LDS with coalesced
+  // row loads ([frame][row], row stride padded by 4 floats), then the wave's four tiles
+  // into registers (rows past JD and frames past F: 0)
+  constexpr int RW = 64 * NWL, RS = RW + 4;
+  {
+    const int row0 = rb * RW;
+    for (int k = threadIdx.x; k < 64 * RW / 4; k += 64 * NWL) {
+      const int fr = k / (RW / 4), c4 = (k - fr * (RW / 4)) * 4;
+      const int f = fbk * 64 + fr, row = row0 + c4;
+      const f4 v = (f < A.F && row < JD) ? *reinterpret_cast<const f4*>(A.vc + (size_t)f * JD + row)
+                                         : f4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f4*>(lds + fr * RS + c4) = v;
+    }
+  }
+  __syncthreads();
+  f4 vcr[2][2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        vcr[t][b][q] = *reinterpret_cast<const f4*>(lds + (b * 32 + r) * RS + (2 * w + t) * 32 + 8 * q + 4 * h);
+  __syncthreads();   // the LDS is reused for the partials
+  // owned capsules (DOUT 16: lane half h owns j = 2(tg+t) + h; DOUT 32: j = tg + t) and their masks
+  float mk[2];
+  int jo[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    jo[t] = DOUT == 16 ? 2 * (T.tg + t) + h : T.tg + t;
+    mk[t] = (jo[t] < A.J && !(A.mask_first && jo[t] == 0)) ? 0.f : -INFINITY;
+  }
+  const bf8 ones = ones_frag(h);
+  const float inv = A.hdr[0];
+  const uint32_t capw = (uint32_t)A.JDp * DIN * 2, capb = (uint32_t)A.JDp * 8;
+  const uint32_t capl = (uint32_t)A.JP * A.Fs * 4;   // bytes per capsule of L / c
+  auto fetch = [&](int i, Frags22<DIN>& fr) {
+    uint32_t xvo[2];
+    xvo22<DIN>(A, T, i, h, xvo);
+    fetch22<DIN>(rs, T.wvo, T.bvo, xvo, h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i * capw,
+                 (uint32_t)i * capb, fr);
+  };
+  auto body = [&](int i, const Frags22<DIN>& fr) {
+    float Lg[2][2];   // [t][b]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f16v u[2];
+      pose22t<DIN>(fr, t, ones, u);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f2 p0 = {0.f, 0.f}, p1 = {0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 vv = vcr[t][b][q];
+          f2& pp = (DOUT == 16 && q >= 2) ? p1 : p0;
+          pp += f2{u[b][4 * q], u[b][4 * q + 1]} * f2{vv.x, vv.y};
+          pp += f2{u[b][4 * q + 2], u[b][4 * q + 3]} * f2{vv.z, vv.w};
+        }
+        float l;
+        if constexpr (DOUT == 16) {
+          // reduce-scatter over the lane halves: half h gets the logit of j = 2(tg+t) + h
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0.x + p0.y),
+                                                           __float_as_uint(p1.x + p1.y), false, false);
+          l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+        } else {
+          l = xor32_sum(p0.x + p0.y);
+        }
+        Lg[t][b] = l * inv + mk[t];
+      }
+    }
+    // store L (frame-minor) and the wave's (max, sum exp) over its capsules per frame
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const bool st = T.f[b] < A.Fs && (DOUT == 16 || h == 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        bstore(lrs, Lg[t][b], st ? (uint32_t)(jo[t] * A.Fs + T.f[b]) * 4u : kNoStore, (uint32_t)i * capl);
+      float m = fmaxf(Lg[0][b], Lg[1][b]);
+      float z = m == -INFINITY ? 0.f : __expf(Lg[0][b] - m) + __expf(Lg[1][b] - m);
+      if constexpr (DOUT == 16) {
+        float m0, m1, z0, z1;
+        xpair32(m, m0, m1);
+        xpair32(z, z0, z1);
+        m = fmaxf(m0, m1);
+        z = m == -INFINITY ? 0.f : z0 * __expf(m0 - m) + z1 * __expf(m1 - m);
+      }
+      pst[((i - i0) * NWL + w) * 64 + b * 32 + r] = make_float2(m, z);   // both halves hold the same pair
+    }
+  };
+  // operands double buffered: capsule k+1's loads go out before capsule k's work; the
+  // loads are unconditional (a clamped capsule past the end) so vmcnt waits stay exact
+  if (i0 < i1) {
+    Frags22<DIN> f0, f1;
+    fetch(i0, f0);
+    for (int i = i0; i < i1; i += 2) {
+      fetch(min(i + 1, i1 - 1), f1);
+      body(i, f0);
+      fetch(min(i + 2, i1 - 1), f0);
+      if (i + 1 < i1) body(i + 1, f1);
+    }
+  }
+  __syncthreads();
+  // combine the waves' partials: one (max, sum exp) per capsule, row block and frame
+  const int n = (i1 - i0) * 64;
+  for (int k = threadIdx.x; k < n; k += 64 * NWL) {
+    const int ci = k >> 6, fr = k & 63;
+    const int f = fbk * 64 + fr;
+    float m = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < NWL; ++v) m = fmaxf(m, pst[(ci * NWL + v) * 64 + fr].x);
+    float z = 0.f;
+    if (m != -INFINITY) {
+#pragma unroll
+      for (int v = 0; v < NWL; ++v) {
+        const float2 pv = pst[(ci * NWL + v) * 64 + fr];
+        z += pv.y * __expf(pv.x - m);
+      }
+    }
+    if (f < A.Fs) A.part[((size_t)(i0 + ci) * A.n_rb + rb) * A.Fs + f] = make_float2(m, z);
+  }
+}
+
+// logZ_i(f) from the row-block partials; grid over in_n * Fs
+__global__ __launch_bounds__(256) void route_lse_kernel(const float2* __restrict__ part, int n_rb, int Fs,
+                                                        size_t n, float* __restrict__ lz) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const size_t i = k / Fs, f = k - i * Fs;
+  const float2* p = part + i * n_rb * Fs + f;
+  float m = -INFINITY;
+  for (int v = 0; v < n_rb; ++v) m = fmaxf(m, p[(size_t)v * Fs].x);
+  float z = 0.f;
+  for (int v = 0; v < n_rb; ++v) {
+    const float2 pv = p[(size_t)v * Fs];
+    z += pv.y * __expf(pv.x - m);
+  }
+  lz[k] = m + __logf(z);
+}
+
+// grid: n_fb * n_rb * n_chunks (chunk fastest); block: NWA waves
+template <int DIN, int DOUT, int NWA>
+__global__ __launch_bounds__(64 * NWA) __attribute__((amdgpu_waves_per_eu(2))) void route_acc_kernel(Args32 A) {
+  static_assert(DOUT == 16 || DOUT == 32, "split passes: dout 16 or 32");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int chunk = blockIdx.x % A.n_chunks;
+  const int rest = blockIdx.x / A.n_chunks;
+  const int rb = rest % A.n_rb, fbk = rest / A.n_rb;
+  const int JD = A.J * DOUT;
+  const Tile22 T = tile22<DIN>(A, rb, NWA, w, fbk, r, h);
+  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+  const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
+  const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
+  const bf8 ones = ones_frag(h);
+  const float inv = A.hdr[0];
+  const uint32_t capw = (uint32_t)A.JDp * DIN * 2, capb = (uint32_t)A.JDp * 8;
+  const uint32_t capl = (uint32_t)A.JP * A.Fs * 4;   // bytes per capsule of L / c
+  // the capsules j of each tile: DOUT 16 rows q = 0,1 -> j = 2(tg+t), q = 2,3 -> j + 1; DOUT 32: j = tg + t
+  int fcl[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) fcl[b] = min(T.f[b], A.Fs - 1);
+  f16v acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[t][b] = f16v{};
+  constexpr int NJ = DOUT == 16 ? 2 : 1;   // capsules per row tile
+  auto load_l = [&](int i, float (&lv)[2][2][NJ], float (&zv)[2]) {
+    const float* lrow = A.lg + (size_t)i * A.JP * A.Fs;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      zv[b] = A.lz[(size_t)i * A.Fs + fcl[b]];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) lv[t][b][k] = lrow[(size_t)(NJ * (T.tg + t) + k) * A.Fs + fcl[b]];
+    }
+  };
+  auto fetch = [&](int i, Frags22<DIN>& fr) {
+    uint32_t xvo[2];
+    xvo22<DIN>(A, T, i, h, xvo);
+    fetch22<DIN>(rs, T.wvo, T.bvo, xvo, h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i * capw,
+                 (uint32_t)i * capb, fr);
+  };
+  float lv[2][2][NJ], zv[2];
+  auto body = [&](int i, const Frags22<DIN>& fr) {
+    // couplings of this capsule (their loads were issued a capsule ahead)
+    float cv[2][2][NJ];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) cv[t][b][k] = T.fv[b] ? __expf(lv[t][b][k] - zv[b]) : 0.f;
+    load_l(min(i + 1, i1 - 1), lv, zv);
+    // coupling storage (over the logits when training): lane half h stores capsule
+    // NJ(tg+t) + h (DOUT 16) / half 0 stores tg + t (DOUT 32); frames F..Fs-1 get 0.
+    // Without storage the descriptor has no records and every store is dropped.
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const bool st = T.f[b] < A.Fs && (DOUT == 16 || h == 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        bstore(crs, DOUT == 16 ? (h ? cv[t][b][NJ - 1] : cv[t][b][0]) : cv[t][b][0],
+               st ? (uint32_t)((NJ * (T.tg + t) + (DOUT == 16 ? h : 0)) * A.Fs + T.f[b]) * 4u : kNoStore,
+               (uint32_t)i * capl);
+    }
+    // one row tile at a time (32 registers of pose tiles; the partner wave on the SIMD
+    // keeps the matrix pipe busy during the accumulation)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f16v u[2];
+#if SRF_SPLIT_DBG == 2   // timing experiment: no pose MFMAs
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) u[b][v] = (float)fr.a[t][0][v & 7] + (float)fr.x[b][0][v & 7] + (float)fr.bias[t][0];
+#else
+      pose22t<DIN>(fr, t, ones, u);
+#endif
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const float c = cv[t][b][(DOUT == 16 && v >= 8) ? NJ - 1 : 0];
+          f2 a2 = {acc[t][b][v], acc[t][b][v + 1]};
+          a2 += f2{c, c} * f2{u[b][v], u[b][v + 1]};
+          acc[t][b][v] = a2.x;
+          acc[t][b][v + 1] = a2.y;
+        }
+    }
+  };
+  if (i0 < i1) {
+    Frags22<DIN> f0, f1;
+    load_l(i0, lv, zv);
+    fetch(i0, f0);
+    for (int i = i0; i < i1; i += 2) {
+#if SRF_SPLIT_DBG == 1   // timing experiment: every fetch re-reads the first capsule (cache-hot operands)
+      fetch(i0, f1);
+      body(i, f0);
+      fetch(i0, f0);
+#else
+      fetch(min(i + 1, i1 - 1), f1);
+      body(i, f0);
+      fetch(min(i + 2, i1 - 1), f0);
+#endif
+      if (i + 1 < i1) body(i + 1, f1);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = (T.tg + t) * 32 + 8 * q + 4 * h;
+        if (T.fv[b] && row < JD) {
+          f4 v = {acc[t][b][4 * q], acc[t][b][4 * q + 1], acc[t][b][4 * q + 2], acc[t][b][4 * q + 3]};
+          *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + T.f[b]) * JD + row) = v * inv;
+        }
+      }
 }
 
 }  // namespace
@@ -1003,12 +1435,38 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   p.ws_h = (size_t)(2 * kAbsBlocks + 64) * 4;   // header + absmax block maxima
   p.ws_bsum = srf::align_up((size_t)best * JD * 4, 256);
   p.ws_slab = srf::align_up((size_t)best * F * JD * 4, 256);
+  // split passes (route_logit / route_lse / route_acc)
+  // opt-in (SRF_FWD32_SPLIT=1, read per plan so tests can switch it): at C2 the split
+  // passes measured slower than route_fwd32_kernel (layer 3: 29 + 5 + 27 us against 37 us)
+  const char* se = getenv("SRF_FWD32_SPLIT");
+  p.split = se != nullptr && se[0] == '1' && (dout == 16 || dout == 32);
+  p.NWS = std::min(4, p.JDp / 64);
+  p.n_rb = p.JDp / (64 * p.NWS);
+  p.n_fb = (F + 63) / 64;
+  const int Fs = fwd32_frame_stride(F);
+  // one round of workgroups: 2 waves per SIMD (both kernels' register budgets), so
+  // 2048 / (64 NWS) workgroups per 256 CUs
+  const int base_wg = p.n_fb * p.n_rb;
+  const int sslots = 256 * 8 / p.NWS;
+  p.nchL = std::min(in_n, std::max((in_n + kSplitMaxCl - 1) / kSplitMaxCl, std::max(1, sslots / base_wg)));
+  p.clenL = (in_n + p.nchL - 1) / p.nchL;
+  p.nchL = (in_n + p.clenL - 1) / p.clenL;
+  p.nchA = std::min(std::min(in_n, 24), std::max(1, sslots / base_wg));
+  p.clenA = (in_n + p.nchA - 1) / p.nchA;
+  p.nchA = (in_n + p.clenA - 1) / p.clenA;
+  if (p.split && p.nchA > best) p.ws_slab = srf::align_up((size_t)p.nchA * F * JD * 4, 256);
+  p.ws_lg = srf::align_up((size_t)in_n * (p.JDp / dout) * Fs * 4, 256);
+  p.ws_part = srf::align_up((size_t)in_n * p.n_rb * Fs * 8, 256);
+  p.ws_lz = srf::align_up((size_t)in_n * Fs * 4, 256);
   return p;
 }
 
 size_t fwd32_planes_bytes(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x + p.ws_h; }
 size_t fwd32_scratch_bytes(const Fwd32Plan& p) { return p.ws_bsum + p.ws_slab; }
-size_t fwd32_workspace(const Fwd32Plan& p) { return fwd32_planes_bytes(p) + fwd32_scratch_bytes(p); }
+size_t fwd32_split_bytes(const Fwd32Plan& p) { return p.split ? p.ws_lg + p.ws_part + p.ws_lz : 0; }
+size_t fwd32_workspace(const Fwd32Plan& p) {
+  return fwd32_planes_bytes(p) + fwd32_scratch_bytes(p) + fwd32_split_bytes(p);
+}
 float* fwd32_slab(const Fwd32Plan& p, void* scratch) {
   return reinterpret_cast<float*>(static_cast<char*>(scratch) + p.ws_bsum);
 }
@@ -1078,7 +1536,7 @@ static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipS
   if (first) {
     Args32 b = a;
     b.n_tgroups = p.JDp / (32 * kFTW);
-    const int tasks = p.n_ftiles * b.n_tgroups * p.n_chunks;
+    const int tasks = (p.n_ftiles + kFFB - 1) / kFFB * b.n_tgroups * p.n_chunks;
     hipLaunchKernelGGL((route_fwd32_first_kernel<DIN, DOUT>), dim3((tasks + 3) / 4), dim3(256), 0, st, b);
     SRF_LAUNCH_CHECK("route_fwd32_first");
     return SRF_OK;
@@ -1090,6 +1548,31 @@ static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipS
     case 8: return launch_rpass<DIN, DOUT, 8>(p, a, st);
     default: return launch_rpass<DIN, DOUT, kMaxNW>(p, a, st);
   }
+}
+
+template <int DIN, int DOUT, int NWS>
+static int launch_split(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
+  const size_t lds = std::max((size_t)p.clenL * NWS * 64 * sizeof(float2), (size_t)64 * (64 * NWS + 4) * sizeof(float));
+  auto lk = route_logit_kernel<DIN, DOUT, NWS>;
+  if (lds > 64 * 1024)
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(lk, dim3(p.n_fb * p.n_rb * p.nchL), dim3(64 * NWS), lds, st, a);
+  SRF_LAUNCH_CHECK("route_logit");
+  const size_t n = (size_t)a.in_n * a.Fs;
+  hipLaunchKernelGGL(route_lse_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a.part, p.n_rb, a.Fs, n, a.lz);
+  SRF_LAUNCH_CHECK("route_lse");
+  Args32 b = a;
+  b.n_chunks = p.nchA;
+  b.chunk_len = p.clenA;
+  hipLaunchKernelGGL((route_acc_kernel<DIN, DOUT, NWS>), dim3(p.n_fb * p.n_rb * p.nchA), dim3(64 * NWS), 0, st, b);
+  SRF_LAUNCH_CHECK("route_acc");
+  return SRF_OK;
+}
+
+template <int DIN, int DOUT>
+static int launch_split_t(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
+  if (p.NWS == 2) return launch_split<DIN, DOUT, 2>(p, a, st);
+  return launch_split<DIN, DOUT, 4>(p, a, st);
 }
 
 static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din,
@@ -1125,6 +1608,10 @@ static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch,
   a.lzst = nullptr;
   a.JP = p.JDp / dout;
   a.Fs = fwd32_frame_stride(B * T);
+  a.lg = nullptr;
+  a.part = nullptr;
+  a.lz = nullptr;
+  a.n_rb = a.n_fb = a.nchL = a.clenL = 0;
   return a;
 }
 
@@ -1146,13 +1633,30 @@ Fwd32Cpl fwd32_cpl_layout(const Fwd32Plan& p, int F, int in_n, int din, int dout
   return c;
 }
 
-int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T, int N, int din,
-               int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst, float* lzst,
-               hipStream_t st) {
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, void* split_ws, int B, int T,
+               int N, int din, int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst,
+               float* lzst, hipStream_t st) {
   Args32 a = make_args32(p, planes, scratch, B, T, N, din, lpad, rpad, J, dout, mask_first);
   a.vc = vc;
   a.cst = first ? nullptr : cst;
   a.lzst = first ? nullptr : lzst;
+  if (!first && p.split && split_ws != nullptr) {
+    char* sb = static_cast<char*>(split_ws);
+    a.lg = cst != nullptr ? cst : reinterpret_cast<float*>(sb);
+    a.part = reinterpret_cast<float2*>(sb + p.ws_lg);
+    a.lz = lzst != nullptr ? lzst : reinterpret_cast<float*>(sb + p.ws_lg + p.ws_part);
+    a.n_rb = p.n_rb;
+    a.n_fb = p.n_fb;
+    a.nchL = p.nchL;
+    a.clenL = p.clenL;
+#define SRF_S32(DI, DO) \
+  if (din == DI && dout == DO) return launch_split_t<DI, DO>(p, a, st);
+    SRF_S32(8, 16)
+    SRF_S32(8, 32)
+    SRF_S32(16, 16)
+    SRF_S32(16, 32)
+#undef SRF_S32
+  }
   SRF_REQUIRE(2 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
 #define SRF_P32(DI, DO) \
   if (din == DI && dout == DO) return launch_pass32_t<DI, DO>(p, first, a, st);
