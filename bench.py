@@ -40,7 +40,7 @@ WORKLOADS = {
     'wsj_c5': (dict(enc=8, iters=5, lpad=20, rpad=20, ph=16, pd=64, ch=16, cd=64, vd=64, context=True), 32, 28, 800),
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / f16 MFMA peak
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py` (timit_c2), averaged per
 # dispatch by scripts/pmcsum.py (KiB per dispatch)
@@ -296,7 +296,8 @@ def main():
                    'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
                    'parallelism': f'dp{world}', 'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
         'roofline': {'kernel': (f'route_fwd32_first_kernel + route_fwd32_kernel<{Din},{D}> (layer {last + 1} DR forward '
-                                f'passes, R={R}; pose on v_mfma_f32_32x32x16_bf16 as 3-term bf16 splits = fp32-accurate)'
+                                f'passes, R={R}; pose on v_mfma_f32_32x32x16_f16 as 2-term fp16 splits of power-of-two '
+                                f'scaled operands + one bf16 bias MFMA = fp32-accurate)'
                                 if fwd32 else f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)'),
                      'bound': 'mfma', 'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
@@ -305,11 +306,12 @@ def main():
                                         '2*FETCH_SIZE+WRITE_SIZE)') if traffic else None,
                      'avg_launch_us': round(kern_avg_ms * 1e3, 2),
                      'flops_per_launch': flops_launch,
-                     # what the matrix cores execute: the full pose every pass, as 6 bf16 products
-                     # (+1 bias product) per fp32 product on the split path
-                     'executed_mfma': ({'dtype': 'bf16', 'peak_tflops': BF16_MFMA_PEAK_TFLOPS,
-                                        'frac': round(frames_prime * 2.0 * in_n * (J * D + 31) // 32 * 32 * Din
-                                                      * (7 if Din == 16 else 4) / (kern_avg_ms * 1e-3) / 1e12
+                     # what the matrix cores execute: the full pose every pass, per 32-row tile and
+                     # capsule 3 f16 K=16 products + 1 bf16 bias product (din 16) or 2 + 1 (din 8,
+                     # two planes packed in K), on the 32x32-padded rows
+                     'executed_mfma': ({'dtype': 'f16/bf16', 'peak_tflops': BF16_MFMA_PEAK_TFLOPS,
+                                        'frac': round(frames_prime * 2.0 * in_n * ((J * D + 31) // 32 * 32) * 16
+                                                      * (4 if Din == 16 else 3) / (kern_avg_ms * 1e-3) / 1e12
                                                       / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
                     if dr else None,
     }
