@@ -68,10 +68,10 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
 
 // Split-bf16 weight packing of stage 2 (defined with the split kernels below), run
 // by extra blocks of the conv1 forward / conv2_bwd_prep launches.
-constexpr int kPackW2Threads = 9 * 2 * C * (C / 8);    // (tap, n, cin/8)
+constexpr int kPackW2Threads = 2 * C * 64;             // one wave per stage-2 output column n
 constexpr int kPackW2tThreads = 9 * C * (2 * C / 8);   // (tap, cin, n/8)
-__device__ __forceinline__ void pack_w2_split_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
-                                                   __bf16* __restrict__ wp3);
+__device__ __forceinline__ void pack_w2_f16_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
+                                                 _Float16* __restrict__ wp2, float* __restrict__ wsc);
 __device__ __forceinline__ void pack_w2t_split_body(int idx, const float* __restrict__ ka,
                                                     const float* __restrict__ kb, __bf16* __restrict__ wq3);
 
@@ -120,11 +120,11 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
     const float* __restrict__ ba, const float* __restrict__ kb, const float* __restrict__ bb, int training,
     float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ y1, unsigned char* __restrict__ sel1,
     float* __restrict__ part, int nconv, const float* __restrict__ pk_a, const float* __restrict__ pk_b,
-    __bf16* __restrict__ wp3) {
+    _Float16* __restrict__ wp2, float* __restrict__ wsc, float* __restrict__ ymax) {
   // blocks past nconv pack the stage-2 split weights (one launch fewer per forward)
   if ((int)blockIdx.x >= nconv) {
     const int idx = (blockIdx.x - nconv) * blockDim.x + threadIdx.x;
-    if (idx < kPackW2Threads) pack_w2_split_body(idx, pk_a, pk_b, wp3);
+    if (idx < kPackW2Threads) pack_w2_f16_body(idx, pk_a, pk_b, wp2, wsc);
     return;
   }
   seed = srf_step_seed(seed, seed_src);
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
   const Tile1 tl = stage_rows1(feats, d, win);
   const int t1 = tl.t1_0 + w;
   // statistics as sums shifted by the channel biases (no per-element division)
-  float n = 0.f, s1 = 0.f, s2 = 0.f;
+  float n = 0.f, s1 = 0.f, s2 = 0.f, ym = 0.f;
   const float K = 0.5f * (bia + bib);
   if (t1 < d.T1) {
     const bool live = t1 < ceil_div_len(inp_len[tl.b], 2);
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
       const float y = live ? (sl ? a : bv) : 0.f;
       y1[o] = y;
       sel1[o] = sl ? 1 : 0;
+      ym = fmaxf(ym, fabsf(y));
       n += 1.f;
       s1 += y - K;
       s2 += (y - K) * (y - K);
@@ -178,8 +179,18 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(
   float mean = n > 0.f ? K + s1 / n : 0.f;
   float m2 = n > 0.f ? fmaxf(s2 - s1 * s1 / n, 0.f) : 0.f;
   sh[0][w][c] = n; sh[1][w][c] = mean; sh[2][w][c] = m2;
+  // max |y1| of the block (the stage-2 split exponent, bn_finalize_kernel)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ym = fmaxf(ym, __shfl_xor(ym, o, 64));
+  __shared__ float smax[kRows1];
+  if (c == 0) smax[w] = ym;
   __syncthreads();
   if (w == 0) {
+    if (c == 0) {
+      float m = smax[0];
+      for (int r = 1; r < kRows1; ++r) m = fmaxf(m, smax[r]);
+      ymax[blockIdx.x] = m;
+    }
     for (int r = 1; r < kRows1; ++r) chan_merge(n, mean, m2, sh[0][r][c], sh[1][r][c], sh[2][r][c]);
     part[((size_t)blockIdx.x * 3 + 0) * C + c] = n;
     part[((size_t)blockIdx.x * 3 + 1) * C + c] = mean;
@@ -209,14 +220,26 @@ __global__ __launch_bounds__(256) void bn_merge_kernel(const float* __restrict__
 
 // ---------------------------------------------------------------- BN finalize
 // stats[0][c] = mean, stats[1][c] = rstd, stats[2][c] = scale, stats[3][c] = shift.
+// With ymax (the conv1 block maxima of |y|): stats[4][0] = 2^b, stats[4][1] = 2^-b, the
+// split-fp16 exponent of the BN output, from the bound |scale_c y + shift_c| <=
+// max|scale| max|y| + max|shift| (conv2_fwd32_kernel).
 // 1024 threads = 16 partial streams x 64 channels, Chan-merged through LDS.
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ part, int nparts,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta,
                                                            float* __restrict__ mmean, float* __restrict__ mvar,
-                                                           int training, float* __restrict__ stats) {
+                                                           int training, float* __restrict__ stats,
+                                                           const float* __restrict__ ymax, int nymax) {
   __shared__ float sh[3][16][C];
+  __shared__ float ysh[16], ab[2][C];
   const int c = threadIdx.x & (C - 1), r = threadIdx.x >> 6;
+  if (ymax != nullptr) {
+    float m = 0.f;
+    for (int k = threadIdx.x; k < nymax; k += 1024) m = fmaxf(m, ymax[k]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (c == 0) ysh[r] = m;
+  }
   float n = 0.f, mu = 0.f, m2 = 0.f;
   if (training)
 #pragma unroll 8
@@ -225,7 +248,10 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
                  part[((size_t)k * 3 + 2) * C + c]);
   sh[0][r][c] = n; sh[1][r][c] = mu; sh[2][r][c] = m2;
   __syncthreads();
-  if (r != 0) return;
+  if (r != 0) {
+    if (ymax != nullptr) __syncthreads();
+    return;
+  }
   float mean, var;
   if (training) {
     for (int q = 1; q < 16; ++q) chan_merge(n, mu, m2, sh[0][q][c], sh[1][q][c], sh[2][q][c]);
@@ -240,10 +266,27 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
   }
   const float rstd = 1.f / sqrtf(var + kBnEps);
   const float scale = gamma[c] * rstd;
+  const float shift = beta[c] - mean * scale;
   stats[0 * C + c] = mean;
   stats[1 * C + c] = rstd;
   stats[2 * C + c] = scale;
-  stats[3 * C + c] = beta[c] - mean * scale;
+  stats[3 * C + c] = shift;
+  if (ymax != nullptr) {
+    ab[0][c] = fabsf(scale);
+    ab[1][c] = fabsf(shift);
+    __syncthreads();
+    if (c == 0) {
+      float y = ysh[0], sa = 0.f, sb = 0.f;
+      for (int q = 1; q < 16; ++q) y = fmaxf(y, ysh[q]);
+      for (int q = 0; q < C; ++q) {
+        sa = fmaxf(sa, ab[0][q]);
+        sb = fmaxf(sb, ab[1][q]);
+      }
+      const int e = srf_split_exp(sa * y + sb);
+      stats[4 * C + 0] = srf_exp2i(e);
+      stats[4 * C + 1] = srf_exp2i(-e);
+    }
+  }
 }
 
 // Pack both stage-2 kernels [3][3][C][C] (kh, kw, cin, cout) into the MFMA B
@@ -443,10 +486,12 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
 }
 
 
-// ---------------------------------------------------------------- conv2 (split-bf16 MFMA)
-// The same implicit GEMM on v_mfma_f32_32x32x16_bf16 with fp32-accurate 3-term
-// bf16 splits (a = a1 + a2 + a3; the six products >= 2^-18 |ab|, as the routing
-// pose, route_fwd32.hip): 16/6 of the fp32-MFMA rate.  Workgroup = 2 waves = 64
+// ---------------------------------------------------------------- conv2 (split-fp16 MFMA)
+// The same implicit GEMM on v_mfma_f32_32x32x16_f16 with fp32-accurate 2-term fp16
+// splits of power-of-two scaled operands (as the routing pose, route_fwd32.hip:
+// a1 b1 + a1 b2 + a2 b1, dropped a2 b2 <= 2^-22 |ab|): A = 2^b BN1(y1) (one exponent
+// from bn_finalize_kernel's bound), B = 2^a_n k (one exponent per output column),
+// undone per column in the epilogue; 16/3 of the fp32-MFMA rate.  Workgroup = 2 waves = 64
 // output pixels x 128 outputs; a wave owns 32 pixels x all 128 outputs (conv a
 // channels 0-31 / 32-63, conv b channels 0-31 / 32-63: the maxout pairs share a
 // lane).  Per k-block (one tap, 16 input channels) the A fragments are gathered
@@ -458,6 +503,10 @@ typedef float cf16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ cf16 mfma32bf(const cbf8& a, const cbf8& b, const cf16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+typedef _Float16 ch8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ cf16 mfma32h(const ch8& a, const ch8& b, const cf16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ void split8v(const float (&v)[8], cbf8& p1, cbf8& p2, cbf8& p3) {
@@ -472,35 +521,49 @@ __device__ __forceinline__ void split8v(const float (&v)[8], cbf8& p1, cbf8& p2,
   }
 }
 
-// Packed split weights wp3[plane][tap][n][cin] (n = ab*C + cout), one thread per 8 cin.
-__device__ __forceinline__ void pack_w2_split_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
-                                                   __bf16* __restrict__ wp3) {   // idx = (tap, n, cin/8)
-  const int c8 = idx % (C / 8), n = (idx / (C / 8)) % (2 * C), tap = idx / (2 * C * (C / 8));
+// Packed split-fp16 weights wp2[plane][tap][n][cin] (n = ab*C + cout) of 2^a_n k (one
+// exponent per output column n, uniform over the GEMM's K = taps x cin), and
+// wsc[n] = 2^-a_n for the epilogue.  One wave per n, a lane per cin (9 taps each).
+__device__ __forceinline__ void pack_w2_f16_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
+                                                 _Float16* __restrict__ wp2, float* __restrict__ wsc) {
+  const int n = idx >> 6, cin = idx & 63;
   const float* k = n < C ? ka : kb;
-  float v[8];
+  const int co = n % C;
+  float v[9], m = 0.f;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] = k[((size_t)tap * C + 8 * c8 + q) * C + (n % C)];
-  cbf8 p1, p2, p3;
-  split8v(v, p1, p2, p3);
+  for (int tap = 0; tap < 9; ++tap) {
+    v[tap] = k[((size_t)tap * C + cin) * C + co];
+    m = fmaxf(m, fabsf(v[tap]));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const int e = srf_split_exp(m);
+  const float sc = srf_exp2i(e);
   const size_t plane = (size_t)9 * 2 * C * C;
-  const size_t o = ((size_t)tap * 2 * C + n) * C + 8 * c8;
-  *reinterpret_cast<cbf8*>(wp3 + o) = p1;
-  *reinterpret_cast<cbf8*>(wp3 + plane + o) = p2;
-  *reinterpret_cast<cbf8*>(wp3 + 2 * plane + o) = p3;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    _Float16 h1, h2;
+    srf_split2h(v[tap] * sc, h1, h2);
+    const size_t o = ((size_t)tap * 2 * C + n) * C + cin;
+    wp2[o] = h1;
+    wp2[plane + o] = h2;
+  }
+  if (cin == 0) wsc[n] = srf_exp2i(-e);
 }
 
 constexpr int kC2BStride = 24;   // bf16 per output row of an LDS B k-block (16 + 8: conflict-free b128 reads)
 constexpr int kC2Waves = 4;      // 32 pixels each: 128 pixels per workgroup
 constexpr int kC2Px = 32 * kC2Waves;
-constexpr int kC2BLoads = 3 * 2 * C * 2 / (64 * kC2Waves);   // 16-byte B loads per thread per k-block
+constexpr int kC2BLoads = 2 * 2 * C * 2 / (64 * kC2Waves);   // 16-byte B loads per thread per k-block (2 planes)
 
 __global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2))) void conv2_fwd32_kernel(
     const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len, Dims d,
-    const __bf16* __restrict__ wp3, const float* __restrict__ ba, const float* __restrict__ bb, int training,
-    float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ y2,
-    unsigned char* __restrict__ sel2, float* __restrict__ part) {
+    const _Float16* __restrict__ wp2, const float* __restrict__ wsc, const float* __restrict__ ba,
+    const float* __restrict__ bb, int training, float drop_p, unsigned long long seed,
+    const unsigned long long* __restrict__ seed_src, float* __restrict__ y2, unsigned char* __restrict__ sel2,
+    float* __restrict__ part) {
   seed = srf_step_seed(seed, seed_src);
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][2 * C * kC2BStride];
+  __shared__ __attribute__((aligned(16))) _Float16 Bs[2][2][2 * C * kC2BStride];
   __shared__ __attribute__((aligned(16))) float ss[2][C];
   __shared__ float red[3][kC2Waves][2 * 32];
   const int tid = threadIdx.x;
@@ -509,7 +572,8 @@ __global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2
   const int P2 = d.B * d.T2 * d.F2;
   const int p0 = blockIdx.x * kC2Px;
   const size_t plane = (size_t)9 * 2 * C * C;
-  if (tid < 2 * C) ss[tid >> 6][tid & 63] = stats1[(2 + (tid >> 6)) * C + (tid & 63)];
+  // BN1 scale / shift times the split exponent 2^b (exact): the A operand is 2^b BN1(y1)
+  if (tid < 2 * C) ss[tid >> 6][tid & 63] = stats1[(2 + (tid >> 6)) * C + (tid & 63)] * stats1[4 * C];
 
   // A row of this lane: pixel p0 + 32 wv + r
   const int pa = p0 + 32 * wv + r;
@@ -519,21 +583,21 @@ __global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2
   const int alen1 = ceil_div_len(inp_len[ab], 2);
 
   // k-block kk = tap * 4 + kb: input channels [16 kb, 16 kb + 16)
-  auto load_b = [&](int kk, cbf8 (&bv)[kC2BLoads]) {
+  auto load_b = [&](int kk, ch8 (&bv)[kC2BLoads]) {
     const int tap = kk >> 2, kb = kk & 3;
 #pragma unroll
     for (int q = 0; q < kC2BLoads; ++q) {
       const int idx = q * 64 * kC2Waves + tid;
       const int pl = idx >> 8, rem = idx & 255, n = rem >> 1, half = rem & 1;
-      bv[q] = *reinterpret_cast<const cbf8*>(wp3 + pl * plane + ((size_t)tap * 2 * C + n) * C + 16 * kb + 8 * half);
+      bv[q] = *reinterpret_cast<const ch8*>(wp2 + pl * plane + ((size_t)tap * 2 * C + n) * C + 16 * kb + 8 * half);
     }
   };
-  auto store_b = [&](int buf, const cbf8 (&bv)[kC2BLoads]) {
+  auto store_b = [&](int buf, const ch8 (&bv)[kC2BLoads]) {
 #pragma unroll
     for (int q = 0; q < kC2BLoads; ++q) {
       const int idx = q * 64 * kC2Waves + tid;
       const int pl = idx >> 8, rem = idx & 255, n = rem >> 1, half = rem & 1;
-      *reinterpret_cast<cbf8*>(&Bs[buf][pl][n * kC2BStride + 8 * half]) = bv[q];
+      *reinterpret_cast<ch8*>(&Bs[buf][pl][n * kC2BStride + 8 * half]) = bv[q];
     }
   };
   auto load_a = [&](int kk, f4 (&av)[2], bool& ok) {
@@ -550,38 +614,35 @@ __global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2
   cf16 acc[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) acc[nt] = cf16{};
-  // one k-block: A split from registers, B from LDS buffer buf, 24 MFMAs
+  // one k-block: A split from registers, B from LDS buffer buf, 12 MFMAs
   auto compute = [&](int kk, int buf, const f4 (&av)[2], bool aok) {
-    cbf8 a1, a2, a3;
+    ch8 a1, a2;
     {
       const int c0 = 16 * (kk & 3) + 8 * h;
-      float v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float x = q < 4 ? av[0][q] : av[1][q - 4];
-        v[q] = aok ? x * ss[0][c0 + q] + ss[1][c0 + q] : 0.f;
+        _Float16 h1, h2;
+        srf_split2h(aok ? x * ss[0][c0 + q] + ss[1][c0 + q] : 0.f, h1, h2);
+        a1[q] = h1;
+        a2[q] = h2;
       }
-      split8v(v, a1, a2, a3);
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int nrow = (nt >> 1) * C + 32 * (nt & 1) + r;   // nt: 0/1 conv a, 2/3 conv b
-      const cbf8 b1 = *reinterpret_cast<const cbf8*>(&Bs[buf][0][nrow * kC2BStride + 8 * h]);
-      const cbf8 b2 = *reinterpret_cast<const cbf8*>(&Bs[buf][1][nrow * kC2BStride + 8 * h]);
-      const cbf8 b3 = *reinterpret_cast<const cbf8*>(&Bs[buf][2][nrow * kC2BStride + 8 * h]);
+      const ch8 b1 = *reinterpret_cast<const ch8*>(&Bs[buf][0][nrow * kC2BStride + 8 * h]);
+      const ch8 b2 = *reinterpret_cast<const ch8*>(&Bs[buf][1][nrow * kC2BStride + 8 * h]);
       cf16 c = acc[nt];
-      c = mfma32bf(a3, b1, c);
-      c = mfma32bf(a1, b3, c);
-      c = mfma32bf(a2, b2, c);
-      c = mfma32bf(a2, b1, c);
-      c = mfma32bf(a1, b2, c);
-      c = mfma32bf(a1, b1, c);
+      c = mfma32h(a2, b1, c);
+      c = mfma32h(a1, b2, c);
+      c = mfma32h(a1, b1, c);
       acc[nt] = c;
     }
   };
   // software pipeline, two k-blocks ahead: at k-block kk the registers hold the
   // operands of kk + 1 (stored to LDS at the end of kk) and receive those of kk + 2
-  cbf8 bvA[kC2BLoads], bvB[kC2BLoads];
+  ch8 bvA[kC2BLoads], bvB[kC2BLoads];
   f4 avA[2], avB[2], avC[2];
   bool okA, okB, okC;
   load_b(0, bvA);
@@ -622,10 +683,12 @@ __global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2
 
   // epilogue: lane column r = channel (32 g + r), rows = pixels 8q + 4h + v of the wave
   const float keep_scale = 1.f / (1.f - drop_p);
+  const float inv_b = stats1[4 * C + 1];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const int c = 32 * g + r;
     const float bia = ba[c], bib = bb[c];
+    const float sca = wsc[c] * inv_b, scb = wsc[C + c] * inv_b;   // 2^-(a_n + b), exact
     float n = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -635,7 +698,7 @@ __global__ __launch_bounds__(64 * kC2Waves) __attribute__((amdgpu_waves_per_eu(2
         if (p >= P2) continue;
         const int t2 = (p / d.F2) % d.T2, b = p / (d.F2 * d.T2);
         const size_t o = (size_t)p * C + c;
-        float a = acc[g][4 * q + v] + bia, bvv = acc[2 + g][4 * q + v] + bib;
+        float a = acc[g][4 * q + v] * sca + bia, bvv = acc[2 + g][4 * q + v] * scb + bib;
         if (training && drop_p > 0.f) {
           bool ka, kb;
           srf_keep2(seed, kStreamConv1a, o, drop_p, ka, kb);
@@ -1493,7 +1556,7 @@ FwdSaved saved_layout(const Dims& d, void* base) {
     off += srf::align_up(bytes, 256);
     return o;
   };
-  const size_t oy1 = take(P1 * C * 4), oy2 = take(P2 * C * 4), os1 = take(4 * C * 4), os2 = take(4 * C * 4),
+  const size_t oy1 = take(P1 * C * 4), oy2 = take(P2 * C * 4), os1 = take(5 * C * 4), os2 = take(5 * C * 4),
                osel1 = take(P1 * C), osel2 = take(P2 * C);
   char* b = static_cast<char*>(base);
   FwdSaved s;
@@ -1511,19 +1574,22 @@ constexpr int kBnMerge = 32;   // first-stage groups of the BN finalize
 
 // Two-stage finalize: kBnMerge groups of partials, then one block over the groups.
 int bn_finalize(const float* part, int nparts, float* merged, const float* gamma, const float* beta, float* mmean,
-                float* mvar, int training, float* stats, hipStream_t st) {
+                float* mvar, int training, float* stats, hipStream_t st, const float* ymax = nullptr,
+                int nymax = 0) {
   const int per = (nparts + kBnMerge - 1) / kBnMerge;
   hipLaunchKernelGGL(bn_merge_kernel, dim3(kBnMerge), dim3(256), 0, st, part, nparts, per, merged);
   SRF_LAUNCH_CHECK("bn_merge");
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(1), dim3(1024), 0, st, merged, kBnMerge, gamma, beta, mmean, mvar,
-                     training, stats);
+                     training, stats, ymax, nymax);
   SRF_LAUNCH_CHECK("bn_finalize");
   return SRF_OK;
 }
 
 struct FwdWs {
   float *part1, *part2, *wp, *merged;
-  __bf16* wp3;   // split-bf16 packed stage-2 weights [3][tap][n][cin]
+  _Float16* wp2;   // split-fp16 packed stage-2 weights [2][tap][n][cin]
+  float* wsc;      // their per-column exponents 2^-a_n [2C]
+  float* ymax;     // conv1 block maxima of |y1|
   size_t bytes;
 };
 
@@ -1538,10 +1604,13 @@ FwdWs fwd_ws_layout(const Dims& d, void* base) {
   };
   const size_t op1 = take((size_t)conv1_blocks(d) * 3 * C * 4), op2 = take(nb2 * 3 * C * 4),
                owp = take((size_t)9 * 2 * C * C * 4), omg = take((size_t)kBnMerge * 3 * C * 4),
-               owp3 = take((size_t)3 * 9 * 2 * C * C * 2);
+               owp2 = take((size_t)2 * 9 * 2 * C * C * 2), owsc = take((size_t)2 * C * 4),
+               oym = take((size_t)conv1_blocks(d) * 4);
   char* b = static_cast<char*>(base);
   FwdWs w;
-  w.wp3 = (__bf16*)(b + owp3);
+  w.wp2 = (_Float16*)(b + owp2);
+  w.wsc = (float*)(b + owsc);
+  w.ymax = (float*)(b + oym);
   w.merged = (float*)(b + omg);
   w.part1 = (float*)(b + op1);
   w.part2 = (float*)(b + op2);
@@ -1613,15 +1682,17 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   const int npack = c2_32 ? (kPackW2Threads + 64 * kRows1 - 1) / (64 * kRows1) : 0;
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3(conv1_blocks(d) + npack), dim3(64 * kRows1), conv1_lds(d), st, feats,
                      inp_len, d, k0a, b0a, k0b, b0b, training, drop_p, seed, srf::seed_source(), sv.y1, sv.sel1,
-                     w.part1, conv1_blocks(d), k1a, k1b, w.wp3);
+                     w.part1, conv1_blocks(d), k1a, k1b, w.wp2, w.wsc, w.ymax);
   SRF_LAUNCH_CHECK("conv1_fwd");
-  if ((rc = bn_finalize(w.part1, conv1_blocks(d), w.merged, gamma0, beta0, mmean0, mvar0, training, sv.stats1, st)))
+  if ((rc = bn_finalize(w.part1, conv1_blocks(d), w.merged, gamma0, beta0, mmean0, mvar0, training, sv.stats1, st,
+                        w.ymax, conv1_blocks(d))))
     return rc;
   SRF_LAUNCH_CHECK("bn_finalize(1)");
   if (c2_32) {   // split weights packed by the conv1 launch
     const int nb32 = (int)((P2 + kC2Px - 1) / kC2Px);
     hipLaunchKernelGGL(conv2_fwd32_kernel, dim3(nb32), dim3(64 * kC2Waves), 0, st, sv.y1, sv.stats1, inp_len, d,
-                       w.wp3, b1a, b1b, training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2, w.part2);
+                       w.wp2, w.wsc, b1a, b1b, training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2,
+                       w.part2);
     SRF_LAUNCH_CHECK("conv2_fwd32");
     nparts2 = nb32;
   } else {

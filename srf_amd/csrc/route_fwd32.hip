@@ -85,17 +85,8 @@ __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c)
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// 2^e as a float (|e| <= 126)
-__device__ __forceinline__ float exp2i(int e) { return __int_as_float((127 + e) << 23); }
-// Exponent that scales an operand of max magnitude m below 2^14 (m = mant * 2^e,
-// mant in [0.5, 1): m * 2^(14 - e) < 2^14), clamped so that 2^-(aw + bx) stays normal.
-__device__ __forceinline__ int split_exp(float m) {
-  if (!(m > 0.f) || !(m < INFINITY)) return 0;
-  int e;
-  (void)frexpf(m, &e);
-  return max(-60, min(60, 14 - e));
-}
-
+__device__ __forceinline__ float exp2i(int e) { return srf_exp2i(e); }
+__device__ __forceinline__ int split_exp(float m) { return srf_split_exp(m); }
 
 // ------------------------------------------------------------------ splits
 // a -> (a1, a2, a3), each round-to-nearest bf16 (the bias operand).
@@ -106,11 +97,7 @@ __device__ __forceinline__ void split3(float a, __bf16& a1, __bf16& a2, __bf16& 
   a3 = (__bf16)(r - (float)a2);
 }
 
-// a' -> (a1, a2) = (f16(a'), f16(a' - a1)), |a'| < 2^14
-__device__ __forceinline__ void split2h(float a, _Float16& a1, _Float16& a2) {
-  a1 = (_Float16)a;
-  a2 = (_Float16)(a - (float)a1);
-}
+__device__ __forceinline__ void split2h(float a, _Float16& a1, _Float16& a2) { srf_split2h(a, a1, a2); }
 
 // 8 consecutive floats, scaled by s -> their two fp16 planes (16 bytes each)
 __device__ __forceinline__ void split8h(const float* __restrict__ src, bool ok, float s, _Float16* d1,

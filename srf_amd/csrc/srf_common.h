@@ -98,6 +98,23 @@ __device__ __forceinline__ float xor32_sum(float v) {
   return a + b;
 }
 
+// Split-fp16 operands (route_fwd32.hip, cnnfe.hip): an operand scaled by 2^e with
+// max|a 2^e| < 2^14 is split as a1 = f16(a'), a2 = f16(a' - a1); the MFMA products
+// a1 b1 + a1 b2 + a2 b1 are exact in fp32 and miss only a2 b2 <= 2^-22 |ab|.
+// 2^e as a float (|e| <= 126)
+__device__ __forceinline__ float srf_exp2i(int e) { return __int_as_float((127 + e) << 23); }
+// exponent that scales an operand of max magnitude m below 2^14, clamped to [-60, 60]
+__device__ __forceinline__ int srf_split_exp(float m) {
+  if (!(m > 0.f) || !(m < __builtin_inff())) return 0;
+  int e;
+  (void)frexpf(m, &e);
+  return max(-60, min(60, 14 - e));
+}
+__device__ __forceinline__ void srf_split2h(float a, _Float16& a1, _Float16& a2) {
+  a1 = (_Float16)a;
+  a2 = (_Float16)(a - (float)a1);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
