@@ -98,7 +98,7 @@ def test_route_dr_chunking_invariant(cuda):
 @pytest.mark.parametrize('case', [(3, 37, 8, 16, 4, 4, 63, 3, True), (2, 19, 8, 16, 4, 4, 8, 3, False),
                                   (1, 33, 4, 8, 0, 0, 63, 1, True)])
 def test_route_dr_fwd32_matches_fp32_mfma_path(cuda, case, monkeypatch):
-    """The split-bf16 32x32 forward (route_fwd32.hip) against the exact-fp32
+    """The split-fp16 32x32 forward (route_fwd32.hip) against the exact-fp32
     16x16x4 MFMA forward (route_pass_kernel): same routing to fp32 accuracy."""
     emb, W, bias = _mk(case, 5)
     _, _, _, v32 = _run_gpu(case, emb, W, bias, cuda)
@@ -126,3 +126,24 @@ def test_route_dr_backward_from_stored_couplings(cuda, case, monkeypatch):
         grads.append([t.grad.detach().cpu().double().numpy() for t in (te, tW, tb)])
     for a, b, name in zip(grads[0], grads[1], ('g_emb', 'g_W', 'g_bias')):
         assert np.abs(a - b).max() <= 2e-5 * max(1.0, np.abs(b).max()), (name, np.abs(a - b).max())
+
+
+@pytest.mark.parametrize('case', [(3, 37, 8, 16, 4, 4, 63, 3, True), (2, 19, 8, 16, 4, 4, 8, 3, False),
+                                  (1, 5, 3, 16, 1, 2, 5, 2, True)])
+def test_split_passes_match(cuda, case, monkeypatch):
+    """The opt-in split routing passes (SRF_FWD32_SPLIT=1: route_logit_kernel,
+    route_lse_kernel, route_acc_kernel) against route_fwd32_kernel: same routing to
+    fp32 accuracy, and the backward from the couplings they store agrees too."""
+    emb, W, bias = _mk(case, 8)
+    gv = torch.tensor(np.random.default_rng(9).standard_normal(case[:2] + (case[6], case[3])), dtype=torch.float32,
+                      device=cuda)
+    outs = []
+    for flag in ('1', '0'):
+        monkeypatch.setenv('SRF_FWD32_SPLIT', flag)
+        te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
+        v.backward(gv)
+        outs.append([v.detach().cpu().double().numpy()] + [t.grad.detach().cpu().double().numpy() for t in (te, tW, tb)])
+    a, b = outs[0][0], outs[1][0]
+    assert np.all(np.abs(a - b) <= 1e-5 * (1 + np.abs(b))), np.abs(a - b).max()
+    for x, y, name in zip(outs[0][1:], outs[1][1:], ('g_emb', 'g_W', 'g_bias')):
+        assert np.abs(x - y).max() <= 2e-5 * max(1.0, np.abs(y).max()), (name, np.abs(x - y).max())
