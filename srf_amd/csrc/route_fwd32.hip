@@ -170,9 +170,13 @@ struct PrepArgs {
 };
 
 __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
-  // split exponents from the block maxima (every block reduces the same 2 x kAbsBlocks values)
+  // split exponents from the block maxima (every block with split work reduces the
+  // same 2 x kAbsBlocks values; the block-uniform test keeps the barrier uniform)
   __shared__ int sexp[2];
-  if (threadIdx.x < 128) {
+  const size_t b0 = (size_t)blockIdx.x * blockDim.x, b1 = b0 + blockDim.x;
+  const size_t ec = P.n_a + P.n_b, sd = ec + P.n_c, ed = sd + P.n_d;
+  const bool split_work = b0 < ec || (b1 > sd && b0 < ed);
+  if (split_work && threadIdx.x < 128) {
     const int y = threadIdx.x >> 6, l = threadIdx.x & 63;
     float m = 0.f;
     for (int k = l; k < kAbsBlocks; k += 64) m = fmaxf(m, P.part[y * kAbsBlocks + k]);
@@ -180,8 +184,8 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
     for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
     if (l == 0) sexp[y] = split_exp(m);
   }
-  __syncthreads();
-  const int aw = sexp[0], bx = sexp[1];
+  if (split_work) __syncthreads();
+  const int aw = split_work ? sexp[0] : 0, bx = split_work ? sexp[1] : 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     P.hdr[0] = exp2i(-(aw + bx));
     P.hdr[1] = (float)aw;
@@ -249,19 +253,25 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
     return;
   }
   idx -= P.n_e;
-  if (idx < P.n_f) {   // xT[i][e][f]: capsule i = w*N + n of frame f is emb[f + w - lpad][n] inside the utterance
-    const int f = idx % P.Fp;
-    const size_t ie = idx / P.Fp;
+  if (idx < P.n_f) {   // xT[i][e][f..f+3]: capsule i = w*N + n of frame f is emb[f + w - lpad][n] inside the utterance
+    const int Fq = P.Fp / 4;
+    const int f0 = (int)(idx % Fq) * 4;
+    const size_t ie = idx / Fq;
     const int e = ie % P.din;
     const int i = ie / P.din;
     const int w = i / P.N, n = i - w * P.N;
-    float v = 0.f;
-    if (f < P.F) {
-      const int b = f / P.T, t = f - b * P.T;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    int b = f0 / P.T, t = f0 - b * P.T;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
       const int ts = t + w - P.lpad;
-      if (ts >= 0 && ts < P.T) v = P.emb[((size_t)(b * P.T + ts) * P.N + n) * P.din + e];
+      if (f0 + q < P.F && ts >= 0 && ts < P.T) v[q] = P.emb[((size_t)(b * P.T + ts) * P.N + n) * P.din + e];
+      if (++t == P.T) {
+        t = 0;
+        ++b;
+      }
     }
-    P.xT[idx] = v;
+    *reinterpret_cast<f4*>(P.xT + idx * 4) = v;
   }
 }
 
@@ -593,6 +603,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
   const __amdgpu_buffer_rsrc_t lzs = make_rsrc(A.lzst, A.cst ? (size_t)A.in_n * A.Fs * 4 : 0);
 
+#if SRF_FWD32_DBG == 4
+  const unsigned long long t_body0 = __builtin_amdgcn_s_memtime();
+#endif
   f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
   // Vc rows of this wave's tiles -> private LDS in fragment order
@@ -626,6 +639,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #if SRF_FWD32_DBG == 4
     unsigned long long tph[5] = {0, 0, 0, 0, 0};
     unsigned long long tlast = __builtin_amdgcn_s_memtime();
+    const unsigned long long t_loop0 = tlast;
 #define SRF_TMARK(k) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); tph[k] += tn - tlast; tlast = tn; }
 #else
 #define SRF_TMARK(k)
@@ -763,8 +777,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     }
 #if SRF_FWD32_DBG == 4
     if (lane == 0 && (blockIdx.x == 100 || blockIdx.x == 7) && (wv == 0 || wv == NW - 1))
-      printf("fwd32 blk %d wv %d caps %d: mfma-issue %llu loads-issue %llu softmax1 %llu barrier %llu softmax2+acc %llu\n",
-             blockIdx.x, wv, i1 - i0, tph[0], tph[1], tph[2], tph[3], tph[4]);
+      printf("fwd32 NW %d blk %d wv %d caps %d: prologue %llu mfma-issue %llu loads-issue %llu softmax1 %llu barrier %llu "
+             "softmax2+acc %llu\n",
+             NW, blockIdx.x, wv, i1 - i0, t_loop0 - t_body0, tph[0], tph[1], tph[2], tph[3], tph[4]);
 #endif
   }
 #pragma unroll
@@ -1500,7 +1515,7 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   P.n_c = (size_t)p.n_chunks * P.JD;
   P.n_d = p.xplane / 8;
   P.n_e = WT ? (size_t)P.in_n * ((P.JD + 15) / 16) * 4 * din : 0;
-  P.n_f = xT ? (size_t)P.in_n * din * P.Fp : 0;
+  P.n_f = xT ? (size_t)P.in_n * din * (P.Fp / 4) : 0;   // 4 frames per thread (Fp % 16 == 0)
   const size_t total = P.n_a + P.n_b + P.n_c + P.n_d + P.n_e + P.n_f;
   hipLaunchKernelGGL(prep32_kernel, dim3((total + 255) / 256), dim3(256), 0, st, P);
   SRF_LAUNCH_CHECK("prep32");
