@@ -1,5 +1,6 @@
 // Deterministic column sums shared by the backward passes:
 // out[c] = sum_r in[r][c] over a [rows][cols] slab of per-block partials.
+// Up to 4096 rows (or >= 128 column blocks): colsum_one, one launch.
 // Stage 1: blocks of 4 row-lanes x 64 columns stream a slice of rows (coalesced
 // along columns) into part[slice][cols]; stage 2: one thread per column adds the
 // slices in order.  Fixed order => bitwise reproducible.
@@ -44,6 +45,33 @@ __global__ void colsum_stage2(const float* __restrict__ part, int slices, int co
   }
 }
 
+// One launch for moderate row counts: a 1024-thread block per 64 columns, 16 row lanes
+// each summing rows r = lane16 (mod 16) in order, then the 16 lane sums in order.
+__global__ __launch_bounds__(1024) void colsum_one(const float* __restrict__ in, int rows, int cols,
+                                                   float* __restrict__ out, ColSplit split) {
+  __shared__ float sh[16][64];
+  const int l = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l;
+  float s = 0.f;
+  if (c < cols) {
+#pragma unroll 8
+    for (int r = rg; r < rows; r += 16) s += in[(size_t)r * cols + c];
+  }
+  sh[rg][l] = s;
+  __syncthreads();
+  if (rg != 0 || c >= cols) return;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += sh[k][l];
+  if (out) out[c] = t;
+  int start = 0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    if (split.dst[k] && c >= start && c < start + split.width[k]) split.dst[k][c - start] = t;
+    start += split.width[k];
+  }
+}
+
 }  // namespace
 
 namespace srf {
@@ -57,6 +85,13 @@ int colsum(const float* in, int rows, int cols, float* out, float* scratch, hipS
     return SRF_OK;
   }
   const int cblocks = (cols + 63) / 64;
+  if ((size_t)rows * 64 <= 256 * 1024 || cblocks >= 128) {
+    // up to 16K rows per 16 lanes (<= 1K adds per thread) or enough column blocks to fill the
+    // chip: one launch instead of two
+    hipLaunchKernelGGL(colsum_one, dim3(cblocks), dim3(1024), 0, st, in, rows, cols, out, split);
+    SRF_LAUNCH_CHECK("colsum_one");
+    return SRF_OK;
+  }
   int slices = std::max(1, std::min(kColsumMaxSlices, (1024 + cblocks - 1) / cblocks));
   slices = std::min(slices, std::max(1, rows / 16));
   const int rps = (rows + slices - 1) / slices;
