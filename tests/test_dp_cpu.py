@@ -44,7 +44,9 @@ def _worker(rank, world, port, q):
     loss.backward()
     model.flat_grad.copy_(w.grad)
     trainer_sr.allreduce_grads(model)
-    q.put((rank, model.flat_grad.clone(), X, B))
+    # plain numpy copies: a queued tensor travels as a shared-memory fd that the
+    # parent must fetch from this process, which may already have exited
+    q.put((rank, model.flat_grad.numpy().copy(), X.numpy().copy(), B))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -61,11 +63,11 @@ def test_gloo_allreduce_gives_global_gradient():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    g0, g1 = res[0][1], res[1][1]
+    g0, g1 = torch.from_numpy(res[0][1]), torch.from_numpy(res[1][1])
     assert torch.allclose(g0, g1)
     # reference: each rank scales by its own B (the reference's semantics), summed
     w = FlatModel(5).flat_params.clone().requires_grad_()
-    total = sum(((X @ w) ** 2).sum() / float(B * world) for _, _, X, B in res)
+    total = sum(((torch.from_numpy(X) @ w) ** 2).sum() / float(B * world) for _, _, X, B in res)
     total.backward()
     assert torch.allclose(g0, w.grad, atol=1e-6)
 
