@@ -268,7 +268,7 @@ def main():
     kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
     kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
     in_n, J, D, Din = model.layer_shapes[last]
-    fwd32 = Din in (8, 16) and D in (8, 16, 32) and J * D <= 1024 and os.environ.get('SRF_ROUTE_FWD32', '1') != '0'
+    fwd32 = Din in (8, 16, 32) and D in (8, 16, 32) and Din <= D and J * D <= 1024 and os.environ.get('SRF_ROUTE_FWD32', '1') != '0'
     frames_prime = B * Tp
     # algorithmic FLOPs per launch: the layer's pose contraction (once per
     # forward, spread over its R pass launches) + one routing iteration
@@ -307,11 +307,12 @@ def main():
                      'avg_launch_us': round(kern_avg_ms * 1e3, 2),
                      'flops_per_launch': flops_launch,
                      # what the matrix cores execute: the full pose every pass, per 32-row tile and
-                     # capsule 3 f16 K=16 products + 1 bf16 bias product (din 16) or 2 + 1 (din 8,
-                     # two planes packed in K), on the 32x32-padded rows
+                     # capsule 3 f16 K=16 products + 1 bf16 bias product (din 16), 2 + 1 (din 8,
+                     # two planes packed in K) or 6 + 1 (din 32, two K=16 halves), on the
+                     # 32x32-padded rows
                      'executed_mfma': ({'dtype': 'f16/bf16', 'peak_tflops': BF16_MFMA_PEAK_TFLOPS,
                                         'frac': round(frames_prime * 2.0 * in_n * ((J * D + 31) // 32 * 32) * 16
-                                                      * (4 if Din == 16 else 3) / (kern_avg_ms * 1e-3) / 1e12
+                                                      * {8: 3, 16: 4, 32: 7}[Din] / (kern_avg_ms * 1e-3) / 1e12
                                                       / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
                     if dr else None,
     }

@@ -671,7 +671,7 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
 // capsule k+1 are in flight (buffer loads, SGPR capsule offsets) while capsule k
 // is formed and contracted.  gu is not stored (route_gw2_kernel forms it again).
 template <int DIN, int TW, int R>
-__global__ __launch_bounds__(256, (R >= 4 ? 3 : 4)) void route_gux_kernel(
+__global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4)) void route_gux_kernel(
     const float* __restrict__ WT, int F, int T, int N, int lpad, int in_n, int J, int mask_first, int n_wgroups,
     int n_chunks, int n_per, const float* __restrict__ saved, const float* __restrict__ gs, float* __restrict__ g_emb,
     int nslots_max, const float* __restrict__ cst, const float* __restrict__ glst, int JP) {
@@ -1530,7 +1530,7 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
   const int n_chunks = (g.N + n_per - 1) / n_per;
   const int nslots = 15 + gu_window(g);
   const size_t lds = gu_lds_bytes(g, nw, n_per);
-  if constexpr (R >= 2 && D <= 16) {   // couplings are stored by the 32x32 forward (din <= 16)
+  if constexpr (R >= 2 && D <= 32) {   // couplings are stored by the 32x32 forward (din <= 32)
     if (lds <= kGuLdsMax && cst != nullptr) {
       hipLaunchKernelGGL((route_gux_kernel<D, TW, R>), dim3(n_ftiles * n_wgroups * n_chunks), dim3(64 * nw), lds, st,
                          WT, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved,
@@ -1581,7 +1581,8 @@ inline int gw3_cap(const Geom& g) {
     const char* c = getenv("SRF_GW3_CAP");
     return (c && atoi(c) == 4) ? 4 : 8;
   }();
-  return (g.din <= 16 && g.iters <= 3) ? v : 0;   // deeper routing spills at 168 registers
+  if (g.iters > 3 || v == 0) return 0;   // deeper routing spills at 168 registers
+  return g.din <= 16 ? v : (g.din == 32 ? 4 : 0);   // din 32: two 16-column accumulators per capsule
 }
 
 Gw2Plan gw2_plan(const Geom& g) {
@@ -1618,13 +1619,13 @@ template <int D>
 int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* saved, const float* gs,
                const float* cst, const float* glst, int JP, float* gwp, float* gbp, hipStream_t st) {
   const int grid = p.n_rt * p.n_cc * p.S;
-  if constexpr (D <= 16) {
+  if constexpr (D <= 32) {
     if (gw3_cap(g)) {
 #define SRF_GW3(R_, C_)                                                                                           \
   hipLaunchKernelGGL((route_gw3_kernel<D, R_, C_>), dim3(grid), dim3(256), 0, st, xT, saved, gs, cst, glst, g.F(), \
                      padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride)
 #define SRF_GW3C(R_) \
-  if (p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, 8);
+  if (D == 32 || p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, (D == 32 ? 4 : 8));
       switch (g.iters) {   // gw3_cap() is 0 past 3 iterations
         case 2: SRF_GW3C(2) break;
         default: SRF_GW3C(3) break;
@@ -1662,7 +1663,7 @@ inline bool use_fwd32(const Geom& g) {
 // stored couplings (route_gux_kernel) fits its window accumulator in LDS; otherwise
 // the forward keeps nothing and the backward recomputes (round-1 kernels).
 inline bool couplings_ok(const Geom& g) {
-  if (!use_fwd32(g) || g.iters < 2 || g.din > 16) return false;
+  if (!use_fwd32(g) || g.iters < 2 || g.din > 32) return false;
   const int TW = gu_tw(g.dout);
   const int nw = std::min(kGuNW, (g.NT() + TW - 1) / TW);
   return gu_lds_bytes(g, nw, 1) <= kGuLdsMax;

@@ -6,7 +6,7 @@
 
 namespace srf {
 
-// Row tiles (of 32 rows) per wave of route_fwd32 / route_bwd32.
+// Row tiles (of 32 rows) per wave of route_fwd32 / route_bwd32 for din 8, 16.
 #ifndef SRF_FWD32_TW
 #define SRF_FWD32_TW 4
 #endif
@@ -15,8 +15,10 @@ constexpr int kFwd32TW = SRF_FWD32_TW;
 __host__ __device__ inline int fwd32_frame_stride(int F) { return (F + 31) / 32 * 32; }
 
 struct Fwd32Plan {
-  int NW;              // waves per workgroup (TW = 4 row tiles of 32 each)
-  int JDp;             // J*dout padded to NW*4*32 rows
+  int NW;              // waves per workgroup
+  int TW;              // 32-row tiles per wave (kFwd32TW; 2 for din 32 with J*dout <= 512)
+  int JDp;             // J*dout padded to NW*TW*32 rows
+  int xpad;            // zero halves after each x plane (the invalid-frame row)
   int n_chunks, chunk_len, n_ftiles;
   size_t xplane;       // elements per x plane (data + zero row)
   size_t ws_w, ws_b, ws_x, ws_h, ws_bsum, ws_slab;   // workspace regions (bytes)

@@ -2,9 +2,9 @@
 //
 // Replaces, like route_dr.hip's route_pass_kernel, the forward routing iteration of
 // sequence_router_naive.py:171-185 / _loop_body :199-206 (pose :154-159 recomputed
-// per pass, window :150-151).  This variant is the forward pass for din in {8, 16}
-// and dout in {8, 16, 32} with J*dout <= 1024 (BASELINE C1 and C2); other shapes
-// keep route_pass_kernel.
+// per pass, window :150-151).  This variant is the forward pass for din in {8, 16, 32}
+// and dout in {8, 16, 32} (din <= dout) with J*dout <= 1024 (BASELINE C1, C2 and the
+// C3/C4 DR layers); other shapes keep route_pass_kernel.
 //
 // Pose product.  u = W x + b is formed on v_mfma_f32_32x32x16_f16 from 2-term fp16
 // splits of power-of-two scaled operands: W' = 2^aw W and x' = 2^bx x with
@@ -290,21 +290,22 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
 #ifndef SRF_FWD32_TW
 #define SRF_FWD32_TW 4
 #endif
-constexpr int kTW = SRF_FWD32_TW;        // 32-row tiles per wave
-static_assert(kTW == srf::kFwd32TW, "stored-coupling layout (route_fwd32.h) assumes kFwd32TW row tiles per wave");
+constexpr int kTW = SRF_FWD32_TW;        // 32-row tiles per wave (din 8, 16; din 32: Fwd32Plan::TW)
+static_assert(kTW == srf::kFwd32TW, "route_fwd32.h and route_fwd32.hip disagree on the row tiles per wave");
 constexpr int kMaxNW = 32 / kTW;         // J*dout <= 1024
 constexpr int kWavesPerEU = 8 / kTW;
 
 template <int DIN>
 struct SplitFrags {
-  static constexpr int NA = DIN == 16 ? 2 : 1;
+  static constexpr int NA = DIN / 8;              // A fragments per tile (W planes x k-halves)
+  static constexpr int NB = DIN == 32 ? 4 : 2;    // B fragments per frame tile
 };
 
 template <int DIN, int TW>
 struct Frags32 {
   h8 a[TW][SplitFrags<DIN>::NA];
   bf8 bias[TW];
-  h8 b[2];
+  h8 b[SplitFrags<DIN>::NB];
 };
 
 struct Rsrc3 {
@@ -335,15 +336,21 @@ __device__ __forceinline__ uint32_t x_voff(int i, int N, int lpad, int T, int F,
   const int w = i / N, n = i - w * N;
   const int ts = ft + w - lpad;
   const bool ok = fvalid && ts >= 0 && ts < T;
-  const uint32_t o = (uint32_t)(((n * F + f + w - lpad) * DIN) * 2 + (DIN == 16 ? 16 * h : 0));
+  const uint32_t o = (uint32_t)(((n * F + f + w - lpad) * DIN) * 2 + (DIN >= 16 ? 16 * h : 0));
   return ok ? o : zero_off;
 }
 
-// the two x fragments of one capsule (DIN 8: [x1 | x1] and [x2 | 0])
+// the x fragments of one capsule (DIN 8: [x1 | x1] and [x2 | 0]; DIN 32: x1, x2 of
+// k-half 0, then of k-half 1 at +32 bytes; the zero row is 32 halves long for DIN 32)
 template <int DIN>
 __device__ __forceinline__ void fetch_x(const Rsrc3& rs, uint32_t xvo, int h, uint32_t xplane_b, uint32_t zero_off,
-                                        h8 (&b)[2]) {
-  if constexpr (DIN == 16) {
+                                        h8 (&b)[SplitFrags<DIN>::NB]) {
+  if constexpr (DIN == 32) {
+    b[0] = hload(rs.x, xvo, 0);
+    b[1] = hload(rs.x, xvo, xplane_b);
+    b[2] = hload(rs.x, xvo, 32);
+    b[3] = hload(rs.x, xvo, xplane_b + 32);
+  } else if constexpr (DIN == 16) {
     b[0] = hload(rs.x, xvo, 0);
     b[1] = hload(rs.x, xvo, xplane_b);
   } else {
@@ -355,7 +362,12 @@ __device__ __forceinline__ void fetch_x(const Rsrc3& rs, uint32_t xvo, int h, ui
 template <int DIN>
 __device__ __forceinline__ void fetch_w(const Rsrc3& rs, uint32_t vo, int h, uint32_t wplane_b, uint32_t wcap_b,
                                         h8 (&a)[SplitFrags<DIN>::NA]) {
-  if constexpr (DIN == 16) {
+  if constexpr (DIN == 32) {   // (W1, W2) of k-half 0, then of k-half 1 (+32 bytes)
+    a[0] = hload(rs.w, vo, wcap_b);
+    a[1] = hload(rs.w, vo, wcap_b + wplane_b);
+    a[2] = hload(rs.w, vo, wcap_b + 32);
+    a[3] = hload(rs.w, vo, wcap_b + wplane_b + 32);
+  } else if constexpr (DIN == 16) {
     a[0] = hload(rs.w, vo, wcap_b);
     a[1] = hload(rs.w, vo, wcap_b + wplane_b);
   } else {
@@ -381,8 +393,16 @@ __device__ __forceinline__ void fetch32(const Rsrc3& rs, uint32_t wvo, uint32_t 
 }
 
 template <int DIN>
-__device__ __forceinline__ f16v pose_chain(const h8 (&a)[SplitFrags<DIN>::NA], const h8 (&b)[2], f16v acc) {
-  if constexpr (DIN == 16) {   // small terms first
+__device__ __forceinline__ f16v pose_chain(const h8 (&a)[SplitFrags<DIN>::NA], const h8 (&b)[SplitFrags<DIN>::NB],
+                                           f16v acc) {
+  if constexpr (DIN == 32) {   // small terms first, both k-halves
+    acc = mfma32h(a[1], b[0], acc);   // W2 x1
+    acc = mfma32h(a[3], b[2], acc);
+    acc = mfma32h(a[0], b[1], acc);   // W1 x2
+    acc = mfma32h(a[2], b[3], acc);
+    acc = mfma32h(a[0], b[0], acc);   // W1 x1
+    acc = mfma32h(a[2], b[2], acc);
+  } else if constexpr (DIN == 16) {   // small terms first
     acc = mfma32h(a[1], b[0], acc);   // W2 x1
     acc = mfma32h(a[0], b[1], acc);   // W1 x2
     acc = mfma32h(a[0], b[0], acc);   // W1 x1
@@ -412,7 +432,44 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (DIN == 16) {
+  if constexpr (DIN == 32) {
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {   // W2 x1, both k-halves
+      u[t] = mfma32h(fr.a[t][1], fr.b[0], u[t]);
+      u[t] = mfma32h(fr.a[t][3], fr.b[2], u[t]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      fr.a[t][1] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b);
+      fr.a[t][3] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b + 32);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {   // W1 x2
+      u[t] = mfma32h(fr.a[t][0], fr.b[1], u[t]);
+      u[t] = mfma32h(fr.a[t][2], fr.b[3], u[t]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    fr.b[1] = hload(rs.x, xvo, xplane_b);
+    fr.b[3] = hload(rs.x, xvo, xplane_b + 32);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {   // W1 x1
+      u[t] = mfma32h(fr.a[t][0], fr.b[0], u[t]);
+      u[t] = mfma32h(fr.a[t][2], fr.b[2], u[t]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      fr.a[t][0] = hload(rs.w, wvo + t * TSTEP, wcap_b);
+      fr.a[t][2] = hload(rs.w, wvo + t * TSTEP, wcap_b + 32);
+    }
+    fr.b[0] = hload(rs.x, xvo, 0);
+    fr.b[2] = hload(rs.x, xvo, 32);
+    __builtin_amdgcn_sched_barrier(0);
+    return;
+  } else if constexpr (DIN == 16) {
 #pragma unroll
     for (int t = 0; t < TW; ++t) u[t] = mfma32h(fr.a[t][1], fr.b[0], u[t]);   // W2 x1
     __builtin_amdgcn_sched_barrier(0);
@@ -495,7 +552,7 @@ constexpr int kFFB = 2;   // frame tiles per wave
 template <int DIN>
 struct FirstFrags {
   h8 a[kFTW][SplitFrags<DIN>::NA];
-  h8 b[kFFB][2];
+  h8 b[kFFB][SplitFrags<DIN>::NB];
 };
 
 template <int DIN, int DOUT>
@@ -518,7 +575,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
     ftt[b] = fc - (fc / A.T) * A.T;
     fv[b] = f[b] < A.F;
   }
-  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
   const uint32_t capb = (uint32_t)A.JDp * DIN * 2;
   constexpr uint32_t TSTEP = 32 * DIN * 2;
@@ -577,9 +634,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
 // Routing pass r >= 1.  grid: n_ftiles * n_chunks (chunk = blockIdx % n_chunks);
 // block: NW waves of kTW row tiles.  LDS: NW * kTW * 4 KiB of Vc fragments, then
 // 2 x NW x 32 float2 of per-wave softmax stats.
-template <int DIN, int DOUT, int NW>
+template <int DIN, int DOUT, int NW, int TW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesPerEU))) void route_fwd32_kernel(Args32 A) {
-  constexpr int TW = kTW;
   constexpr int CP = TW * 32 / DOUT;   // capsule partials per lane
   constexpr int OWN = CP / 2;          // capsules whose logit this lane owns
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -598,7 +654,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #if SRF_FWD32_PRIO
   if (NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
   const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
   const __amdgpu_buffer_rsrc_t lzs = make_rsrc(A.lzst, A.cst ? (size_t)A.in_n * A.Fs * 4 : 0);
@@ -819,10 +875,9 @@ __device__ __forceinline__ void load_c(const float* __restrict__ p, size_t fs, f
   for (int a = 0; a < OWN; ++a) c[a] = p[2 * a * fs];
 }
 
-template <int DIN, int DOUT, int NW>
+template <int DIN, int DOUT, int NW, int TW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesPerEU))) void route_bwd32_kernel(
     Args32 A, Bwd32Args Bk) {
-  constexpr int TW = kTW;
   constexpr int CP = TW * 32 / DOUT;
   constexpr int OWN = CP / 2;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -841,7 +896,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #if SRF_FWD32_PRIO
   if (NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
 
   f4* gsl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
@@ -1098,7 +1153,7 @@ __device__ __forceinline__ Tile22 tile22(const Args32& A, int rb, int NWv, int w
     T.ftt[b] = fc - (fc / A.T) * A.T;
     T.fv[b] = T.f[b] < A.F;
   }
-  T.wvo = (uint32_t)(((T.tg * 32 + r) * DIN + (DIN == 16 ? 8 * h : 0)) * 2);
+  T.wvo = (uint32_t)(((T.tg * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   T.bvo = (uint32_t)((T.tg * 32 + r) * 8);
   return T;
 }
@@ -1392,8 +1447,16 @@ __global__ __launch_bounds__(64 * NWA) __attribute__((amdgpu_waves_per_eu(2))) v
 namespace srf {
 
 bool fwd32_supported(int din, int dout, int J) {
-  return (din == 8 || din == 16) && (dout == 8 || dout == 16 || dout == 32) && din <= dout &&
+  return (din == 8 || din == 16 || din == 32) && (dout == 8 || dout == 16 || dout == 32) && din <= dout &&
          J * dout <= 32 * kTW * kMaxNW && (J * dout) % 8 == 0;
+}
+
+// Row tiles per wave: kTW, except din 32 with J*dout <= 512, where the six-MFMA pose
+// keeps 2 tiles per wave (SRF_FWD32_TW32=4 forces 4 for A/B runs)
+static int plan_tw(int din, int JD) {
+  if (din != 32 || JD > 32 * 2 * kMaxNW) return kTW;
+  const char* e = getenv("SRF_FWD32_TW32");   // read per plan: tests switch it
+  return (e && atoi(e) == 4) ? 4 : 2;
 }
 
 Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout) {
@@ -1401,18 +1464,21 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   const int in_n = N * (lpad + rpad + 1);
   const int JD = J * dout;
   const int NT = (JD + 31) / 32;
+  p.TW = plan_tw(din, JD);
   p.NW = 1;
-  while (p.NW * kTW < NT) p.NW *= 2;
-  p.JDp = p.NW * kTW * 32;
+  while (p.NW * p.TW < NT) p.NW *= 2;
+  p.JDp = p.NW * p.TW * 32;
+  p.xpad = din == 32 ? 32 : 16;
   const int F = B * T;
   const int n_ftiles = (F + 31) / 32;
-  // one workgroup per CU when NW > 1 (the Vc slabs fill most of the LDS);
-  // single-wave workgroups: up to 4 per CU.
+  // NW > 1: as many workgroups per CU as the waves (2 per SIMD) and the LDS (Vc
+  // slabs) allow; single-wave workgroups: up to 4 per CU.
   static const int slots1 = [] {
     const char* e = getenv("SRF_FWD32_SLOTS1");
     return e ? atoi(e) : 1024;
   }();
-  const int slots = p.NW > 1 ? 256 : slots1;
+  const int per_cu = std::max(1, std::min(8 / p.NW, (int)(160 * 1024 / fwd32_lds(p))));
+  const int slots = p.NW > 1 ? 256 * per_cu : slots1;
   int best = 1;
   double best_cost = 1e30;
   const char* env = getenv("SRF_FWD32_CHUNKS");
@@ -1430,7 +1496,7 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   p.n_chunks = best;
   p.chunk_len = (in_n + best - 1) / best;
   p.n_ftiles = n_ftiles;
-  p.xplane = (size_t)F * N * din + 16;
+  p.xplane = (size_t)F * N * din + p.xpad;
   p.ws_w = srf::align_up((size_t)2 * in_n * p.JDp * din * 2, 256);
   p.ws_b = srf::align_up((size_t)in_n * p.JDp * 4 * 2, 256);
   p.ws_x = srf::align_up((size_t)2 * p.xplane * 2, 256);
@@ -1441,7 +1507,7 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   // opt-in (SRF_FWD32_SPLIT=1, read per plan so tests can switch it): at C2 the split
   // passes measured slower than route_fwd32_kernel (layer 3: 29 + 5 + 27 us against 37 us)
   const char* se = getenv("SRF_FWD32_SPLIT");
-  p.split = se != nullptr && se[0] == '1' && (dout == 16 || dout == 32);
+  p.split = se != nullptr && se[0] == '1' && (dout == 16 || dout == 32) && din <= 16;
   p.NWS = std::min(4, p.JDp / 64);
   p.n_rb = p.JDp / (64 * p.NWS);
   p.n_fb = (F + 63) / 64;
@@ -1474,7 +1540,7 @@ float* fwd32_slab(const Fwd32Plan& p, void* scratch) {
 }
 
 size_t fwd32_lds(const Fwd32Plan& p) {
-  return (size_t)p.NW * kTW * 4 * 64 * 16 + (p.NW > 1 ? (size_t)2 * 32 * p.NW * 8 : 0);
+  return (size_t)p.NW * p.TW * 4 * 64 * 16 + (p.NW > 1 ? (size_t)2 * 32 * p.NW * 8 : 0);
 }
 
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
@@ -1522,10 +1588,10 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   return SRF_OK;
 }
 
-template <int DIN, int DOUT, int NW>
+template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_rpass(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
-  auto kern = route_fwd32_kernel<DIN, DOUT, NW>;
+  auto kern = route_fwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a);
@@ -1542,6 +1608,16 @@ static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipS
     hipLaunchKernelGGL((route_fwd32_first_kernel<DIN, DOUT>), dim3((tasks + 3) / 4), dim3(256), 0, st, b);
     SRF_LAUNCH_CHECK("route_fwd32_first");
     return SRF_OK;
+  }
+  if constexpr (DIN == 32) {
+    if (p.TW == 2) {
+      switch (p.NW) {
+        case 1: return launch_rpass<DIN, DOUT, 1, 2>(p, a, st);
+        case 2: return launch_rpass<DIN, DOUT, 2, 2>(p, a, st);
+        case 4: return launch_rpass<DIN, DOUT, 4, 2>(p, a, st);
+        default: return launch_rpass<DIN, DOUT, 8, 2>(p, a, st);
+      }
+    }
   }
   switch (p.NW) {
     case 1: return launch_rpass<DIN, DOUT, 1>(p, a, st);
@@ -1591,7 +1667,7 @@ static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch,
   a.xs_bytes = 2 * p.xplane * 2;
   a.wplane_b = (uint32_t)((size_t)in_n * p.JDp * din * 2);
   a.xplane_b = (uint32_t)(p.xplane * 2);
-  a.zero_off = (uint32_t)((p.xplane - 16) * 2);
+  a.zero_off = (uint32_t)((p.xplane - p.xpad) * 2);
   a.F = B * T;
   a.T = T;
   a.N = N;
@@ -1667,15 +1743,16 @@ int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch
   SRF_P32(8, 32)
   SRF_P32(16, 16)
   SRF_P32(16, 32)
+  SRF_P32(32, 32)
 #undef SRF_P32
   srf::set_error("fwd32: unsupported din %d dout %d", din, dout);
   return SRF_EUNSUPPORTED;
 }
 
-template <int DIN, int DOUT, int NW>
+template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
-  auto kern = route_bwd32_kernel<DIN, DOUT, NW>;
+  auto kern = route_bwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a, b);
@@ -1685,6 +1762,16 @@ static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b,
 
 template <int DIN, int DOUT>
 static int launch_bpass_t(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b, hipStream_t st) {
+  if constexpr (DIN == 32) {
+    if (p.TW == 2) {
+      switch (p.NW) {
+        case 1: return launch_bpass<DIN, DOUT, 1, 2>(p, a, b, st);
+        case 2: return launch_bpass<DIN, DOUT, 2, 2>(p, a, b, st);
+        case 4: return launch_bpass<DIN, DOUT, 4, 2>(p, a, b, st);
+        default: return launch_bpass<DIN, DOUT, 8, 2>(p, a, b, st);
+      }
+    }
+  }
   switch (p.NW) {
     case 1: return launch_bpass<DIN, DOUT, 1>(p, a, b, st);
     case 2: return launch_bpass<DIN, DOUT, 2>(p, a, b, st);
@@ -1706,6 +1793,7 @@ int bwd32_pass(const Fwd32Plan& p, const void* planes, void* scratch, int B, int
   SRF_B32(8, 32)
   SRF_B32(16, 16)
   SRF_B32(16, 32)
+  SRF_B32(32, 32)
 #undef SRF_B32
   srf::set_error("bwd32: unsupported din %d dout %d", din, dout);
   return SRF_EUNSUPPORTED;

@@ -96,7 +96,8 @@ def test_route_dr_chunking_invariant(cuda):
 
 
 @pytest.mark.parametrize('case', [(3, 37, 8, 16, 4, 4, 63, 3, True), (2, 19, 8, 16, 4, 4, 8, 3, False),
-                                  (1, 33, 4, 8, 0, 0, 63, 1, True)])
+                                  (1, 33, 4, 8, 0, 0, 63, 1, True), (2, 40, 16, 32, 2, 2, 16, 3, False),
+                                  (2, 23, 16, 32, 2, 2, 32, 3, True)])
 def test_route_dr_fwd32_matches_fp32_mfma_path(cuda, case, monkeypatch):
     """The split-fp16 32x32 forward (route_fwd32.hip) against the exact-fp32
     16x16x4 MFMA forward (route_pass_kernel): same routing to fp32 accuracy."""
@@ -110,7 +111,9 @@ def test_route_dr_fwd32_matches_fp32_mfma_path(cuda, case, monkeypatch):
 
 
 @pytest.mark.parametrize('case', [(3, 37, 8, 16, 4, 4, 63, 3, True), (2, 19, 8, 16, 4, 4, 8, 3, False),
-                                  (2, 21, 4, 8, 2, 1, 12, 3, False), (2, 7, 4, 8, 1, 1, 6, 5, False)])
+                                  (2, 21, 4, 8, 2, 1, 12, 3, False), (2, 7, 4, 8, 1, 1, 6, 5, False),
+                                  (2, 40, 16, 32, 2, 2, 16, 3, False), (2, 23, 16, 32, 2, 2, 32, 3, True),
+                                  (1, 9, 4, 32, 1, 1, 8, 5, False)])
 def test_route_dr_backward_from_stored_couplings(cuda, case, monkeypatch):
     """The backward routing passes that read the forward's stored couplings
     (route_bwd32_kernel) against the ones that recompute the logits
@@ -140,6 +143,25 @@ def test_split_passes_match(cuda, case, monkeypatch):
     outs = []
     for flag in ('1', '0'):
         monkeypatch.setenv('SRF_FWD32_SPLIT', flag)
+        te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
+        v.backward(gv)
+        outs.append([v.detach().cpu().double().numpy()] + [t.grad.detach().cpu().double().numpy() for t in (te, tW, tb)])
+    a, b = outs[0][0], outs[1][0]
+    assert np.all(np.abs(a - b) <= 1e-5 * (1 + np.abs(b))), np.abs(a - b).max()
+    for x, y, name in zip(outs[0][1:], outs[1][1:], ('g_emb', 'g_W', 'g_bias')):
+        assert np.abs(x - y).max() <= 2e-5 * max(1.0, np.abs(y).max()), (name, np.abs(x - y).max())
+
+
+@pytest.mark.parametrize('case', [(2, 40, 16, 32, 2, 2, 16, 3, False), (1, 35, 8, 32, 1, 2, 8, 2, True)])
+def test_din32_row_tiles_per_wave_match(cuda, case, monkeypatch):
+    """din 32 runs 2 row tiles per wave (J*dout <= 512); SRF_FWD32_TW32=4 forces 4.
+    Both plans (and their coupling layouts) give the same routing and gradients."""
+    emb, W, bias = _mk(case, 10)
+    gv = torch.tensor(np.random.default_rng(11).standard_normal(case[:2] + (case[6], case[3])), dtype=torch.float32,
+                      device=cuda)
+    outs = []
+    for tw in ('2', '4'):
+        monkeypatch.setenv('SRF_FWD32_TW32', tw)
         te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
         v.backward(gv)
         outs.append([v.detach().cpu().double().numpy()] + [t.grad.detach().cpu().double().numpy() for t in (te, tW, tb)])
