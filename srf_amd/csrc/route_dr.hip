@@ -1159,7 +1159,7 @@ __global__ __launch_bounds__(256) void route_gw2_kernel(
 // The stored couplings and logit gradients are 0 for frames past F (the 32x32
 // passes store zeros there) and x^T is 0 past F, so gu is 0 on padded frames.
 template <int D, int R, int CAP>
-__global__ __launch_bounds__(256, 3) void route_gw3_kernel(
+__global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_kernel(
     const float* __restrict__ xT, const float* __restrict__ saved, const float* __restrict__ gs,
     const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp, int in_n, int J, int mask_first,
     int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride) {
@@ -1582,7 +1582,13 @@ inline int gw3_cap(const Geom& g) {
     return (c && atoi(c) == 4) ? 4 : 8;
   }();
   if (g.iters > 3 || v == 0) return 0;   // deeper routing spills at 168 registers
-  return g.din <= 16 ? v : (g.din == 32 ? 4 : 0);   // din 32: two 16-column accumulators per capsule
+  if (g.din <= 16) return v;
+  if (g.din != 32) return 0;
+  static const int v32 = [] {   // din 32: two 16-column accumulators per capsule (SRF_GW3_CAP32=8 for A/B)
+    const char* c = getenv("SRF_GW3_CAP32");
+    return (c && atoi(c) == 8) ? 8 : 4;
+  }();
+  return v32;
 }
 
 Gw2Plan gw2_plan(const Geom& g) {
@@ -1625,7 +1631,7 @@ int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* sa
   hipLaunchKernelGGL((route_gw3_kernel<D, R_, C_>), dim3(grid), dim3(256), 0, st, xT, saved, gs, cst, glst, g.F(), \
                      padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride)
 #define SRF_GW3C(R_) \
-  if (D == 32 || p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, (D == 32 ? 4 : 8));
+  if (p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, 8);
       switch (g.iters) {   // gw3_cap() is 0 past 3 iterations
         case 2: SRF_GW3C(2) break;
         default: SRF_GW3C(3) break;

@@ -60,6 +60,12 @@
 #ifndef SRF_FWD32_PRIO
 #define SRF_FWD32_PRIO 1
 #endif
+// 1: tile-major pose in the r >= 1 forward pass: tile t's MFMA chain, then its operand
+// reloads, then the agreement dots of tile t - 1 (whose Vc fragments were read from
+// LDS before tile t's MFMAs), so the dots overlap the matrix pipe
+#ifndef SRF_FWD32_TM
+#define SRF_FWD32_TM 1
+#endif
 // 1: softmax normaliser by the fast reciprocal instead of an IEEE division
 #ifndef SRF_BWD32_CPREFETCH
 #define SRF_BWD32_CPREFETCH 0   // 1: couplings of capsule i+1 loaded during capsule i (4 more live registers)
@@ -166,10 +172,41 @@ struct PrepArgs {
   float* hdr;
   int in_n, JD, JDp, din, n_chunks, chunk_len, F, N, T, lpad, Fp;
   size_t xplane;
-  size_t n_a, n_b, n_c, n_d, n_e, n_f;   // thread counts of the six ranges
+  size_t n_a, n_b, n_c, n_d, n_e;   // thread counts of the first five ranges
+  size_t n_f, xt_block0;             // xT: 64-frame tiles, one block each from block xt_block0 on
 };
 
+constexpr int kXtTile = 64;   // frames per xT tile of prep32_kernel
+
 __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
+  if (P.n_f && blockIdx.x >= P.xt_block0) {
+    // xT[i][e][f] (capsule i = w*N + n of frame f is emb[f + w - lpad][n] inside the
+    // utterance, 0 past F): the tile's 64 window rows are read along e (coalesced),
+    // transposed through LDS and written as din runs of 64 consecutive frames
+    __shared__ float tile[kXtTile][32 + 1];
+    const int ntile = (P.Fp + kXtTile - 1) / kXtTile;
+    const int blk = blockIdx.x - (int)P.xt_block0;
+    const int i = blk / ntile, f0 = (blk - i * ntile) * kXtTile;
+    const int w = i / P.N, n = i - w * P.N;
+    for (int k = threadIdx.x; k < kXtTile * P.din; k += blockDim.x) {
+      const int fl = k / P.din, e = k - fl * P.din;
+      const int f = f0 + fl;
+      float v = 0.f;
+      if (f < P.F) {
+        const int b = f / P.T, t = f - b * P.T;
+        const int ts = t + w - P.lpad;
+        if (ts >= 0 && ts < P.T) v = P.emb[((size_t)(b * P.T + ts) * P.N + n) * P.din + e];
+      }
+      tile[fl][e] = v;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kXtTile * P.din; k += blockDim.x) {
+      const int e = k / kXtTile, fl = k - e * kXtTile;
+      const int f = f0 + fl;
+      if (f < P.Fp) P.xT[((size_t)i * P.din + e) * P.Fp + f] = tile[fl][e];
+    }
+    return;
+  }
   // split exponents from the block maxima (every block with split work reduces the
   // same 2 x kAbsBlocks values; the block-uniform test keeps the barrier uniform)
   __shared__ int sexp[2];
@@ -218,7 +255,14 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
     const int c = idx / P.JD, row = idx - (size_t)c * P.JD;
     const int i0 = c * P.chunk_len, i1 = min(P.in_n, i0 + P.chunk_len);
     float acc = 0.f;
-    for (int i = i0; i < i1; ++i) acc += P.bias[(size_t)i * P.JD + row];
+    // loads in batches of 8 (one round trip each), summed in capsule order
+    for (int i = i0; i < i1; i += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = i + k < i1 ? P.bias[(size_t)(i + k) * P.JD + row] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += v[k];
+    }
     P.bsum[idx] = acc;
     return;
   }
@@ -252,27 +296,7 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
     *reinterpret_cast<f4*>(P.WT + idx * 4) = v;
     return;
   }
-  idx -= P.n_e;
-  if (idx < P.n_f) {   // xT[i][e][f..f+3]: capsule i = w*N + n of frame f is emb[f + w - lpad][n] inside the utterance
-    const int Fq = P.Fp / 4;
-    const int f0 = (int)(idx % Fq) * 4;
-    const size_t ie = idx / Fq;
-    const int e = ie % P.din;
-    const int i = ie / P.din;
-    const int w = i / P.N, n = i - w * P.N;
-    f4 v = {0.f, 0.f, 0.f, 0.f};
-    int b = f0 / P.T, t = f0 - b * P.T;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ts = t + w - P.lpad;
-      if (f0 + q < P.F && ts >= 0 && ts < P.T) v[q] = P.emb[((size_t)(b * P.T + ts) * P.N + n) * P.din + e];
-      if (++t == P.T) {
-        t = 0;
-        ++b;
-      }
-    }
-    *reinterpret_cast<f4*>(P.xT + idx * 4) = v;
-  }
+
 }
 
 // ------------------------------------------------------------------ fragments
@@ -702,6 +726,50 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #endif
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
+      // partial agreement dots <u_ij, Vc_j> over this lane's rows (packed FMA pairs)
+      f2 P2[CP];
+#pragma unroll
+      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
+#if SRF_FWD32_TM
+      {
+        constexpr uint32_t TSTEP = 32 * DIN * 2;
+        const int in = min(i + 1, i1 - 1);
+        const uint32_t wcap = (uint32_t)in * A.JDp * DIN * 2, bcap = (uint32_t)in * A.JDp * 8;
+        const uint32_t xvn = x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off);
+        f4 vv[4];
+        auto dots = [&](int t) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int k = kpart<DOUT>(t, 4 * q);
+            P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv[q].x, vv[q].y};
+            P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv[q].z, vv[q].w};
+          }
+        };
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          if (t > 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vv[q] = vcl[((t - 1) * 4 + q) * 64 + lane];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
+          __builtin_amdgcn_sched_barrier(0);
+          fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, wcap, fr.a[t]);
+          {
+            const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap, 0);
+            fr.bias[t] = __builtin_bit_cast(bf8, (unsigned __attribute__((ext_vector_type(4)))){v2[0], v2[1], 0u, 0u});
+          }
+          if (t == TW - 1) fetch_x<DIN>(rs, xvn, h, A.xplane_b, A.zero_off, fr.b);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t > 0) dots(t - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vv[q] = vcl[((TW - 1) * 4 + q) * 64 + lane];
+        dots(TW - 1);
+      }
+      SRF_TMARK(0)
+#else
 #if SRF_FWD32_PROG
       const int in = min(i + 1, i1 - 1);
       pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
@@ -717,10 +785,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
                                A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
       if (SRF_FWD32_FETCH_EARLY) __builtin_amdgcn_sched_barrier(0);
-      // partial agreement dots <u_ij, Vc_j> over this lane's rows (packed FMA pairs)
-      f2 P2[CP];
-#pragma unroll
-      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -730,6 +794,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
           P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv.x, vv.y};
           P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv.z, vv.w};
         }
+#endif
       // reduce-scatter over lane halves: half h owns capsule partial 2a + h
       float L[OWN], e[OWN];
       float m = -1e30f;
@@ -788,7 +853,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       // next capsule's operands: issued once every MFMA result has been consumed
       // (the dots), so no load waits on a queued MFMA's operand read
       __builtin_amdgcn_sched_barrier(0);
-      if (!SRF_FWD32_PROG && !SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
+      if (!SRF_FWD32_TM && !SRF_FWD32_PROG && !SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                                A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
@@ -1581,9 +1646,10 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   P.n_c = (size_t)p.n_chunks * P.JD;
   P.n_d = p.xplane / 8;
   P.n_e = WT ? (size_t)P.in_n * ((P.JD + 15) / 16) * 4 * din : 0;
-  P.n_f = xT ? (size_t)P.in_n * din * (P.Fp / 4) : 0;   // 4 frames per thread (Fp % 16 == 0)
-  const size_t total = P.n_a + P.n_b + P.n_c + P.n_d + P.n_e + P.n_f;
-  hipLaunchKernelGGL(prep32_kernel, dim3((total + 255) / 256), dim3(256), 0, st, P);
+  SRF_REQUIRE(din <= 32, "prep32: xT tile holds din <= 32, got %d", din);
+  P.n_f = xT ? (size_t)P.in_n * ((P.Fp + kXtTile - 1) / kXtTile) : 0;   // xT tiles (one block each)
+  P.xt_block0 = (P.n_a + P.n_b + P.n_c + P.n_d + P.n_e + 255) / 256;
+  hipLaunchKernelGGL(prep32_kernel, dim3(P.xt_block0 + P.n_f), dim3(256), 0, st, P);
   SRF_LAUNCH_CHECK("prep32");
   return SRF_OK;
 }
