@@ -60,6 +60,10 @@ MODEL_CASES = {
                                class_n=63, context=False, caps_type='lowmemory'), 2, [37, 29], [5, 3], 15),
     'c3_mini_sdr_lowmemory': (dict(feat_dim=123, enc_num=2, iters=3, lpad=2, rpad=2, ph=4, pd=8, ch=4, cd=8, vd=8,
                                    class_n=32, context=True, caps_type='lowmemory'), 2, [26, 19], [4, 2], 16),
+    # C4-shaped DR (DIM 32, WSJ classes): the din-32 split-fp16 routing path, with two
+    # row tiles per wave in the inner layer (J*dout = 128) and four in the last (1024)
+    'c4_mini': (dict(feat_dim=123, enc_num=2, iters=3, lpad=2, rpad=2, ph=4, pd=32, ch=4, cd=32, vd=32,
+                     class_n=32, context=False), 2, [34, 27], [4, 3], 17),
 }
 
 

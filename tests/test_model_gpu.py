@@ -16,6 +16,7 @@ from tests.helpers import config_from_shape, load_model_fixture
 pytestmark = pytest.mark.gpu
 
 DR_FIXTURES = ['c1_mini', 'c2_mini', 'c3_mini_sdr',   # c3: SDR routing
+               'c4_mini',                                # DR at DIM 32 (C3/C4 capsule width)
                # the einsum / lowmemory variants (trainer_sr.py:188-199)
                'c2_mini_einsum', 'c2_mini_lowmemory', 'c3_mini_sdr_lowmemory']
 
