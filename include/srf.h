@@ -44,7 +44,7 @@ size_t srf_route_dr_bwd_workspace(int B, int T, int N, int din, int lpad, int rp
 int srf_route_dr_fwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int iters, int mask_first, int n_chunks, float* v_out,
                      float* saved, void* workspace, size_t workspace_bytes, void* stream);
-/* Coupling storage (the 32x32 split-bf16 path: din in {8, 16}, dout in {8, 16, 32},
+/* Coupling storage (the 32x32 split-fp16 path: din in {8, 16, 32} <= dout in {8, 16, 32},
  * J*dout <= 1024; 0 for other shapes or iters < 2): the couplings c^r and logZ^r
  * of the routing iterations r >= 1, written by srf_route_dr_fwd_ex when
  * couplings != NULL and read by srf_route_dr_bwd_ex / _bwd_data_ex, whose

@@ -1516,9 +1516,16 @@ bool fwd32_supported(int din, int dout, int J) {
          J * dout <= 32 * kTW * kMaxNW && (J * dout) % 8 == 0;
 }
 
-// Row tiles per wave: kTW, except din 32 with J*dout <= 512, where the six-MFMA pose
-// keeps 2 tiles per wave (SRF_FWD32_TW32=4 forces 4 for A/B runs)
+// Row tiles per wave: kTW, except (a) din 32 with J*dout <= 512, where the six-MFMA
+// pose keeps 2 tiles per wave (SRF_FWD32_TW32=4 forces 4 for A/B runs), and (b) small
+// din <= 16 layers (J*dout <= 128, C2 layers 1-2), which run 2 tiles on each of two
+// waves instead of 4 on one: twice the waves on the one-wave-per-SIMD grid, the
+// softmax across the pair through LDS (C2 step -0.5 to -1 %; SRF_FWD32_TW16=4 restores)
 static int plan_tw(int din, int JD) {
+  if (din <= 16) {   // small layers (J*dout <= 128): two-wave workgroups (SRF_FWD32_TW16=4: one wave)
+    const char* e = getenv("SRF_FWD32_TW16");
+    return (JD <= 128 && !(e && atoi(e) == 4)) ? 2 : kTW;
+  }
   if (din != 32 || JD > 32 * 2 * kMaxNW) return kTW;
   const char* e = getenv("SRF_FWD32_TW32");   // read per plan: tests switch it
   return (e && atoi(e) == 4) ? 4 : 2;
@@ -1675,6 +1682,9 @@ static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipS
     SRF_LAUNCH_CHECK("route_fwd32_first");
     return SRF_OK;
   }
+  if constexpr (DIN <= 16) {
+    if (p.TW == 2) return p.NW == 1 ? launch_rpass<DIN, DOUT, 1, 2>(p, a, st) : launch_rpass<DIN, DOUT, 2, 2>(p, a, st);
+  }
   if constexpr (DIN == 32) {
     if (p.TW == 2) {
       switch (p.NW) {
@@ -1828,6 +1838,10 @@ static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b,
 
 template <int DIN, int DOUT>
 static int launch_bpass_t(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b, hipStream_t st) {
+  if constexpr (DIN <= 16) {
+    if (p.TW == 2)
+      return p.NW == 1 ? launch_bpass<DIN, DOUT, 1, 2>(p, a, b, st) : launch_bpass<DIN, DOUT, 2, 2>(p, a, b, st);
+  }
   if constexpr (DIN == 32) {
     if (p.TW == 2) {
       switch (p.NW) {

@@ -381,19 +381,27 @@ __global__ __launch_bounds__(256) void sdr_gw_kernel(const float* __restrict__ g
   f4 acc[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) acc[ct] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int f0 = 0; f0 < F; f0 += 4) {
-    const int f = f0 + g;
-    const int fc = min(f, F - 1);
-    const float a = f < F ? gu[((size_t)fc * in_n + i) * JD + row] : 0.f;
-    const int b = fc / T, t = fc - b * T;
-    const int ts = t + w - lpad;
-    const bool ok = f < F && ts >= 0 && ts < T;
-    const float* xp = emb + ((size_t)(b * T + min(max(ts, 0), T - 1)) * N + n) * DIN;
+  // 8 groups of 4 frames per iteration: every load of the batch is issued before the
+  // first MFMA (one round trip per 32 frames); the accumulation order is unchanged
+  constexpr int U = 8;
+  for (int f0 = 0; f0 < F; f0 += 4 * U) {
+    float a[U], xv[U][NCT];
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
-      const float xv = ok ? xp[min(ct * 16 + l16, DIN - 1)] : 0.f;
-      acc[ct] = mfma16x16x4(a, xv, acc[ct]);
+    for (int q = 0; q < U; ++q) {
+      const int f = f0 + 4 * q + g;
+      const int fc = min(f, F - 1);
+      a[q] = f < F ? gu[((size_t)fc * in_n + i) * JD + row] : 0.f;
+      const int b = fc / T, t = fc - b * T;
+      const int ts = t + w - lpad;
+      const bool ok = f < F && ts >= 0 && ts < T;
+      const float* xp = emb + ((size_t)(b * T + min(max(ts, 0), T - 1)) * N + n) * DIN;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) xv[q][ct] = ok ? xp[min(ct * 16 + l16, DIN - 1)] : 0.f;
     }
+#pragma unroll
+    for (int q = 0; q < U; ++q)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) acc[ct] = mfma16x16x4(a[q], xv[q][ct], acc[ct]);
   }
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {

@@ -152,16 +152,20 @@ def test_split_passes_match(cuda, case, monkeypatch):
         assert np.abs(x - y).max() <= 2e-5 * max(1.0, np.abs(y).max()), (name, np.abs(x - y).max())
 
 
-@pytest.mark.parametrize('case', [(2, 40, 16, 32, 2, 2, 16, 3, False), (1, 35, 8, 32, 1, 2, 8, 2, True)])
-def test_din32_row_tiles_per_wave_match(cuda, case, monkeypatch):
-    """din 32 runs 2 row tiles per wave (J*dout <= 512); SRF_FWD32_TW32=4 forces 4.
-    Both plans (and their coupling layouts) give the same routing and gradients."""
+@pytest.mark.parametrize('case,var', [((2, 40, 16, 32, 2, 2, 16, 3, False), 'SRF_FWD32_TW32'),
+                                      ((1, 35, 8, 32, 1, 2, 8, 2, True), 'SRF_FWD32_TW32'),
+                                      ((2, 45, 8, 16, 4, 4, 8, 3, False), 'SRF_FWD32_TW16'),
+                                      ((2, 21, 4, 8, 2, 1, 12, 3, False), 'SRF_FWD32_TW16')])
+def test_row_tiles_per_wave_plans_match(cuda, case, var, monkeypatch):
+    """Row tiles per wave are a plan choice: din 32 runs 2 (J*dout <= 512) unless
+    SRF_FWD32_TW32=4; small din <= 16 layers run 4 unless SRF_FWD32_TW16=2.  Both
+    plans (and their coupling layouts) give the same routing and gradients."""
     emb, W, bias = _mk(case, 10)
     gv = torch.tensor(np.random.default_rng(11).standard_normal(case[:2] + (case[6], case[3])), dtype=torch.float32,
                       device=cuda)
     outs = []
     for tw in ('2', '4'):
-        monkeypatch.setenv('SRF_FWD32_TW32', tw)
+        monkeypatch.setenv(var, tw)
         te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
         v.backward(gv)
         outs.append([v.detach().cpu().double().numpy()] + [t.grad.detach().cpu().double().numpy() for t in (te, tW, tb)])
