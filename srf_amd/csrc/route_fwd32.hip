@@ -730,7 +730,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       f2 P2[CP];
 #pragma unroll
       for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
-#if SRF_FWD32_TM
+      if constexpr (SRF_FWD32_TM && DIN <= 16) {   // din 32: pose_prog measured faster (C4 A/B)
       {
         constexpr uint32_t TSTEP = 32 * DIN * 2;
         const int in = min(i + 1, i1 - 1);
@@ -768,8 +768,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         for (int q = 0; q < 4; ++q) vv[q] = vcl[((TW - 1) * 4 + q) * 64 + lane];
         dots(TW - 1);
       }
-      SRF_TMARK(0)
-#else
+      } else {
 #if SRF_FWD32_PROG
       const int in = min(i + 1, i1 - 1);
       pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
@@ -794,7 +793,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
           P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv.x, vv.y};
           P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv.z, vv.w};
         }
-#endif
+      }
       // reduce-scatter over lane halves: half h owns capsule partial 2a + h
       float L[OWN], e[OWN];
       float m = -1e30f;
@@ -853,7 +852,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       // next capsule's operands: issued once every MFMA result has been consumed
       // (the dots), so no load waits on a queued MFMA's operand read
       __builtin_amdgcn_sched_barrier(0);
-      if (!SRF_FWD32_TM && !SRF_FWD32_PROG && !SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
+      if (!(SRF_FWD32_TM && DIN <= 16) && !SRF_FWD32_PROG && !SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                                A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
@@ -995,6 +994,53 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
                            fr);
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
+      // partial dots <u_ij, gs_j> over this lane's rows
+      f2 P2[CP];
+#pragma unroll
+      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
+      float cc[OWN];
+      if constexpr (SRF_FWD32_TM && DIN <= 16) {   // din 32: pose_prog measured faster (C4 A/B)
+      // this capsule's couplings, then the tile-major pose with the dots of tile t - 1
+      // behind tile t's MFMAs (as route_fwd32_kernel)
+      load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
+      {
+        constexpr uint32_t TSTEP = 32 * DIN * 2;
+        const int in = min(i + 1, i1 - 1);
+        const uint32_t wcap = (uint32_t)in * A.JDp * DIN * 2, bcap = (uint32_t)in * A.JDp * 8;
+        const uint32_t xvn = x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off);
+        f4 gq[4];
+        auto dots = [&](int t) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int k = kpart<DOUT>(t, 4 * q);
+            P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{gq[q].x, gq[q].y};
+            P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{gq[q].z, gq[q].w};
+          }
+        };
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          if (t > 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gq[q] = gsl[((t - 1) * 4 + q) * 64 + lane];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
+          __builtin_amdgcn_sched_barrier(0);
+          fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, wcap, fr.a[t]);
+          {
+            const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap, 0);
+            fr.bias[t] = __builtin_bit_cast(bf8, (unsigned __attribute__((ext_vector_type(4)))){v2[0], v2[1], 0u, 0u});
+          }
+          if (t == TW - 1) fetch_x<DIN>(rs, xvn, h, A.xplane_b, A.zero_off, fr.b);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t > 0) dots(t - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gq[q] = gsl[((TW - 1) * 4 + q) * 64 + lane];
+        dots(TW - 1);
+      }
+      } else {
 #if SRF_FWD32_PROG
       const int in = min(i + 1, i1 - 1);
       pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
@@ -1005,20 +1051,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
 #endif
 #if SRF_BWD32_CPREFETCH
-      float cc[OWN];
 #pragma unroll
       for (int a = 0; a < OWN; ++a) cc[a] = cn[a];
       if (i + 1 < i1) load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
 #else
       // this capsule's couplings: the pose MFMAs in flight hide their latency (no
       // registers held across capsules)
-      float cc[OWN];
       load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
 #endif
-      // partial dots <u_ij, gs_j> over this lane's rows
-      f2 P2[CP];
-#pragma unroll
-      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1028,6 +1068,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
           P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{gv.x, gv.y};
           P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{gv.z, gv.w};
         }
+      }
       float Q[OWN];
       float sp = 0.f;
 #pragma unroll
@@ -1057,7 +1098,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         par ^= 1;
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (!SRF_FWD32_PROG && i + 1 < i1) {
+      if (!(SRF_FWD32_TM && DIN <= 16) && !SRF_FWD32_PROG && i + 1 < i1) {
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
                                h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
