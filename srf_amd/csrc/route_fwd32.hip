@@ -66,6 +66,10 @@
 #ifndef SRF_FWD32_TM
 #define SRF_FWD32_TM 1
 #endif
+// 0: the compiler may move the operand reloads among the tile's MFMAs (A/B knob)
+#ifndef SRF_FWD32_TMSB
+#define SRF_FWD32_TMSB 1
+#endif
 // 1: softmax normaliser by the fast reciprocal instead of an IEEE division
 #ifndef SRF_BWD32_CPREFETCH
 #define SRF_BWD32_CPREFETCH 0   // 1: couplings of capsule i+1 loaded during capsule i (4 more live registers)
@@ -751,9 +755,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #pragma unroll
             for (int q = 0; q < 4; ++q) vv[q] = vcl[((t - 1) * 4 + q) * 64 + lane];
           }
-          __builtin_amdgcn_sched_barrier(0);
+          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
           u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
-          __builtin_amdgcn_sched_barrier(0);
+          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
           fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, wcap, fr.a[t]);
           {
             const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap, 0);
@@ -1023,9 +1027,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #pragma unroll
             for (int q = 0; q < 4; ++q) gq[q] = gsl[((t - 1) * 4 + q) * 64 + lane];
           }
-          __builtin_amdgcn_sched_barrier(0);
+          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
           u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
-          __builtin_amdgcn_sched_barrier(0);
+          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
           fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, wcap, fr.a[t]);
           {
             const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap, 0);
