@@ -45,24 +45,28 @@ __global__ void colsum_stage2(const float* __restrict__ part, int slices, int co
   }
 }
 
-// One launch for moderate row counts: a 1024-thread block per 64 columns, 16 row lanes
-// each summing rows r = lane16 (mod 16) in order, then the 16 lane sums in order.
+// One launch for moderate row counts: a 1024-thread block per CW columns, 1024/CW row
+// lanes each summing rows r = lane (mod 1024/CW) in order, then the lane sums in
+// order.  CW = 64 when there are enough column blocks; CW = 16 for narrow slabs (four
+// times the row lanes, so a few blocks still keep many loads in flight).
+template <int CW>
 __global__ __launch_bounds__(1024) void colsum_one(const float* __restrict__ in, int rows, int cols,
                                                    float* __restrict__ out, ColSplit split) {
-  __shared__ float sh[16][64];
-  const int l = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + l;
+  constexpr int RG = 1024 / CW;
+  __shared__ float sh[RG][CW];
+  const int l = threadIdx.x % CW, rg = threadIdx.x / CW;
+  const int c = blockIdx.x * CW + l;
   float s = 0.f;
   if (c < cols) {
 #pragma unroll 8
-    for (int r = rg; r < rows; r += 16) s += in[(size_t)r * cols + c];
+    for (int r = rg; r < rows; r += RG) s += in[(size_t)r * cols + c];
   }
   sh[rg][l] = s;
   __syncthreads();
   if (rg != 0 || c >= cols) return;
   float t = 0.f;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) t += sh[k][l];
+#pragma unroll 16
+  for (int k = 0; k < RG; ++k) t += sh[k][l];
   if (out) out[c] = t;
   int start = 0;
 #pragma unroll
@@ -88,7 +92,10 @@ int colsum(const float* in, int rows, int cols, float* out, float* scratch, hipS
   if ((size_t)rows * 64 <= 256 * 1024 || cblocks >= 128) {
     // up to 16K rows per 16 lanes (<= 1K adds per thread) or enough column blocks to fill the
     // chip: one launch instead of two
-    hipLaunchKernelGGL(colsum_one, dim3(cblocks), dim3(1024), 0, st, in, rows, cols, out, split);
+    if (cblocks < 64)
+      hipLaunchKernelGGL(colsum_one<16>, dim3((cols + 15) / 16), dim3(1024), 0, st, in, rows, cols, out, split);
+    else
+      hipLaunchKernelGGL(colsum_one<64>, dim3(cblocks), dim3(1024), 0, st, in, rows, cols, out, split);
     SRF_LAUNCH_CHECK("colsum_one");
     return SRF_OK;
   }
