@@ -17,6 +17,7 @@
 //                partials;
 //   bn_apply     writes the CapsulationLayer output mask2(BN2(y2)).
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdlib>
 
@@ -74,6 +75,9 @@ __device__ __forceinline__ void pack_w2_f16_body(int idx, const float* __restric
                                                  _Float16* __restrict__ wp2, float* __restrict__ wsc);
 __device__ __forceinline__ void pack_w2t_split_body(int idx, const float* __restrict__ ka,
                                                     const float* __restrict__ kb, __bf16* __restrict__ wq3);
+__device__ __forceinline__ void pack_w2t_f16_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
+                                                  _Float16* __restrict__ wq2h, float* __restrict__ wdsc);
+constexpr int kPackW2tF16Threads = C * 64;   // one wave per data-gradient output column cin
 
 // ---------------------------------------------------------------- conv1
 // A workgroup = kRows1 consecutive output rows t1 of one utterance (one wave per
@@ -824,11 +828,16 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     const float* __restrict__ stats2, const float* __restrict__ gamma2, const float* __restrict__ bnsum2,
     const int* __restrict__ inp_len, Dims d, float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ g_ab,
     float* __restrict__ part, int nprep, const float* __restrict__ pk_a, const float* __restrict__ pk_b,
-    __bf16* __restrict__ wq3) {
+    __bf16* __restrict__ wq3, _Float16* __restrict__ wq2h, float* __restrict__ wdsc, float* __restrict__ gmax) {
   // blocks past nprep pack the transposed split weights of the data gradient
+  // (split-fp16 planes + per-cin exponents when wq2h != nullptr, else split-bf16)
   if ((int)blockIdx.x >= nprep) {
     const int idx = (blockIdx.x - nprep) * blockDim.x + threadIdx.x;
-    if (idx < kPackW2tThreads) pack_w2t_split_body(idx, pk_a, pk_b, wq3);
+    if (wq2h != nullptr) {
+      if (idx < kPackW2tF16Threads) pack_w2t_f16_body(idx, pk_a, pk_b, wq2h, wdsc);
+    } else if (idx < kPackW2tThreads) {
+      pack_w2t_split_body(idx, pk_a, pk_b, wq3);
+    }
     return;
   }
   seed = srf_step_seed(seed, seed_src);
@@ -838,7 +847,7 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
   const float mean = stats2[c], rstd = stats2[C + c], gam = gamma2[c];
   const float sdy_n = bnsum2[c] / (float)P, sdyxh_n = bnsum2[C + c] / (float)P;
   const float keep_scale = 1.f / (1.f - drop_p);
-  float ga_s = 0.f, gb_s = 0.f;
+  float ga_s = 0.f, gb_s = 0.f, gm = 0.f;
 #pragma unroll 4
   for (int p = blockIdx.x * 4 + row; p < P; p += nprep * 4) {
     const int t = (p / d.F2) % d.T2;
@@ -858,13 +867,20 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     g_ab[(size_t)p * 2 * C + C + c] = gb;
     ga_s += ga;
     gb_s += gb;
+    gm = fmaxf(gm, fmaxf(fabsf(ga), fabsf(gb)));
   }
   sh[0][row][c] = ga_s; sh[1][row][c] = gb_s;
+  // block max |g_ab| (the data gradient's split exponent, conv2_dgrad32_kernel)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) gm = fmaxf(gm, __shfl_xor(gm, o, 64));
+  __shared__ float smax[4];
+  if (c == 0) smax[row] = gm;
   __syncthreads();
   if (row == 0) {
     for (int r = 1; r < 4; ++r) { ga_s += sh[0][r][c]; gb_s += sh[1][r][c]; }
     part[(size_t)blockIdx.x * 2 * C + c] = ga_s;
     part[(size_t)blockIdx.x * 2 * C + C + c] = gb_s;
+    if (c == 0 && gmax != nullptr) gmax[blockIdx.x] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
   }
 }
 
@@ -1026,13 +1042,58 @@ __device__ __forceinline__ void pack_w2t_split_body(int idx, const float* __rest
   *reinterpret_cast<cbf8*>(wq3 + 2 * plane + o) = p3;
 }
 
+// wq2h[plane][tap][cin][n] = 2-term fp16 split of 2^e_cin k_{a|b}[tap][cin][n % C] (one
+// exponent per data-gradient output column cin, uniform over K = taps x n), and
+// wdsc[cin] = 2^-e_cin.  One wave per cin; lane l holds n = 2l, 2l+1 over the 9 taps.
+__device__ __forceinline__ void pack_w2t_f16_body(int idx, const float* __restrict__ ka, const float* __restrict__ kb,
+                                                  _Float16* __restrict__ wq2h, float* __restrict__ wdsc) {
+  const int cin = idx >> 6, l = idx & 63;
+  float v[9][2], m = 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int n = 2 * l + u;
+      v[tap][u] = (n < C ? ka : kb)[((size_t)tap * C + cin) * C + (n % C)];
+      m = fmaxf(m, fabsf(v[tap][u]));
+    }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const int e = srf_split_exp(m);
+  const float sc = srf_exp2i(e);
+  const size_t plane = (size_t)9 * C * 2 * C;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    _Float16 h1[2], h2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) srf_split2h(v[tap][u] * sc, h1[u], h2[u]);
+    const size_t o = ((size_t)tap * C + cin) * 2 * C + 2 * l;
+    wq2h[o] = h1[0];
+    wq2h[o + 1] = h1[1];
+    wq2h[plane + o] = h2[0];
+    wq2h[plane + o + 1] = h2[1];
+  }
+  if (l == 0) wdsc[cin] = srf_exp2i(-e);
+}
+
 constexpr int kD2Waves = 4;
 constexpr int kD2Px = 32 * kD2Waves;
 constexpr int kD2BChunks = 3 * C * 2;   // 16-byte B chunks per k-block (planes x cin x halves)
 
+// H = true: 2-term fp16 splits of power-of-two scaled operands (A = 2^ea g_ab with ea
+// from conv2_bwd_prep's block maxima, reduced by every workgroup; B = 2^e_cin k from
+// pack_w2t_f16_body), three f16 MFMAs per k-block tile instead of six bf16 ones;
+// the epilogue multiplies column cin by 2^-ea wdsc[cin].
+template <bool H>
 __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2))) void conv2_dgrad32_kernel(
-    const float* __restrict__ g_ab, const __bf16* __restrict__ wq3, Dims d, DgCls cls, float* __restrict__ g_x1) {
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][3][C * kC2BStride];
+    const float* __restrict__ g_ab, const void* __restrict__ wqv, Dims d, DgCls cls, float* __restrict__ g_x1,
+    const float* __restrict__ gmax, int ngmax, const float* __restrict__ wdsc) {
+  using BT = std::conditional_t<H, _Float16, __bf16>;
+  using V8 = std::conditional_t<H, ch8, cbf8>;
+  constexpr int NPL = H ? 2 : 3;
+  constexpr int BCH = NPL * C * 2;   // 16-byte B chunks per k-block (planes x cin x halves)
+  const BT* __restrict__ wq3 = static_cast<const BT*>(wqv);
+  __shared__ __attribute__((aligned(16))) BT Bs[2][NPL][C * kC2BStride];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -1046,6 +1107,21 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
   const int ntf = (3 - df0 + 1) / 2, ntt = (3 - dt0 + 1) / 2;
   const int nkb = ntt * ntf * 8;
   const size_t plane = (size_t)9 * C * 2 * C;
+  float sa = 1.f, inv_sa = 1.f;
+  if constexpr (H) {   // split exponent of g_ab: max over conv2_bwd_prep's block maxima
+    __shared__ float wmx[kD2Waves];
+    float m = 0.f;
+    for (int k = tid; k < ngmax; k += 64 * kD2Waves) m = fmaxf(m, gmax[k]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) wmx[wv] = m;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kD2Waves; ++k) m = fmaxf(m, wmx[k]);
+    const int ea = srf_split_exp(m);
+    sa = srf_exp2i(ea);
+    inv_sa = srf_exp2i(-ea);
+  }
 
   // A row of this lane: class pixel q0 + 32 wv + r
   const int pa = q0 + 32 * wv + r;
@@ -1055,23 +1131,23 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
   const int at1 = qt + 2 * akt, af1 = qf + 2 * akf;
   auto tap_of = [&](int k) { return (dt0 + 2 * (k / ntf)) * 3 + df0 + 2 * (k % ntf); };
 
-  constexpr int NBL = (kD2BChunks + 64 * kD2Waves - 1) / (64 * kD2Waves);
-  auto load_b = [&](int kk, cbf8 (&bv)[NBL]) {
+  constexpr int NBL = (BCH + 64 * kD2Waves - 1) / (64 * kD2Waves);
+  auto load_b = [&](int kk, V8 (&bv)[NBL]) {
     const int tap = tap_of(kk >> 3), kb = kk & 7;
 #pragma unroll
     for (int q = 0; q < NBL; ++q) {
-      const int idx = min(q * 64 * kD2Waves + tid, kD2BChunks - 1);
+      const int idx = min(q * 64 * kD2Waves + tid, BCH - 1);
       const int pl = idx / (2 * C), rem = idx % (2 * C), cin = rem >> 1, half = rem & 1;
-      bv[q] = *reinterpret_cast<const cbf8*>(wq3 + pl * plane + ((size_t)tap * C + cin) * 2 * C + 16 * kb + 8 * half);
+      bv[q] = *reinterpret_cast<const V8*>(wq3 + pl * plane + ((size_t)tap * C + cin) * 2 * C + 16 * kb + 8 * half);
     }
   };
-  auto store_b = [&](int buf, const cbf8 (&bv)[NBL]) {
+  auto store_b = [&](int buf, const V8 (&bv)[NBL]) {
 #pragma unroll
     for (int q = 0; q < NBL; ++q) {
       const int idx = q * 64 * kD2Waves + tid;
-      if (idx < kD2BChunks) {
+      if (idx < BCH) {
         const int pl = idx / (2 * C), rem = idx % (2 * C), cin = rem >> 1, half = rem & 1;
-        *reinterpret_cast<cbf8*>(&Bs[buf][pl][cin * kC2BStride + 8 * half]) = bv[q];
+        *reinterpret_cast<V8*>(&Bs[buf][pl][cin * kC2BStride + 8 * half]) = bv[q];
       }
     }
   };
@@ -1090,6 +1166,29 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
   acc[0] = cf16{};
   acc[1] = cf16{};
   auto compute = [&](int buf, const f4 (&av)[2], bool aok) {
+    if constexpr (H) {
+      ch8 a1, a2;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = aok ? (q < 4 ? av[0][q] : av[1][q - 4]) : 0.f;
+        _Float16 h1, h2;
+        srf_split2h(v * sa, h1, h2);
+        a1[q] = h1;
+        a2[q] = h2;
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int nrow = 32 * nt + r;
+        const ch8 b1 = *reinterpret_cast<const ch8*>(&Bs[buf][0][nrow * kC2BStride + 8 * h]);
+        const ch8 b2 = *reinterpret_cast<const ch8*>(&Bs[buf][1][nrow * kC2BStride + 8 * h]);
+        cf16 cc = acc[nt];
+        cc = mfma32h(a2, b1, cc);   // small terms first
+        cc = mfma32h(a1, b2, cc);
+        cc = mfma32h(a1, b1, cc);
+        acc[nt] = cc;
+      }
+      return;
+    } else {
     cbf8 a1, a2, a3;
     {
       float v[8];
@@ -1112,9 +1211,10 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
       cc = mfma32bf(a1, b1, cc);
       acc[nt] = cc;
     }
+    }
   };
   // two k-blocks ahead, as conv2_fwd32_kernel (nkb is a multiple of 8)
-  cbf8 bvA[NBL], bvB[NBL];
+  V8 bvA[NBL], bvB[NBL];
   f4 avA[2], avB[2];
   bool okA, okB;
   load_b(0, bvA);
@@ -1148,6 +1248,11 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
     }
   }
   // epilogue: lane column r = cin (32 nt + r), rows = pixels 8q + 4h + v of the wave
+  float osc[2] = {1.f, 1.f};
+  if constexpr (H) {
+    osc[0] = inv_sa * wdsc[r];
+    osc[1] = inv_sa * wdsc[32 + r];
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1156,8 +1261,8 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
       if (p >= Pc) continue;
       const int kf = p % nkf, kt = (p / nkf) % nkt, b = p / (nkf * nkt);
       float* dst = g_x1 + (((size_t)b * d.T1 + qt + 2 * kt) * d.F1 + qf + 2 * kf) * C + r;
-      dst[0] = acc[0][4 * q + v];
-      dst[32] = acc[1][4 * q + v];
+      dst[0] = H ? acc[0][4 * q + v] * osc[0] : acc[0][4 * q + v];
+      dst[32] = H ? acc[1][4 * q + v] * osc[1] : acc[1][4 * q + v];
     }
 }
 
@@ -1717,6 +1822,8 @@ namespace {
 struct BwdWs2 {
   float *bnpart, *bnsum2, *bnsum1, *g_ab, *biaspart, *g_x1, *wq, *wpart, *c1part, *c1sum, *scratch;
   __bf16* gsT3;   // split-bf16 g_ab planes, pixel-minor (conv2_wgrad32_kernel)
+  float* gmax;    // block maxima of |g_ab| (conv2_bwd_prep_kernel)
+  float* wdsc;    // 2^-e_cin of the split-fp16 transposed weights
   int P2p;
   size_t bytes;
 };
@@ -1749,6 +1856,7 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
                oscr = take(srf::colsum_scratch_floats(std::max(conv1_blocks(d), kBnBlocks), 20 * C) * 4);
   const int P2p = (int)((P2 + kTpPx - 1) / kTpPx * kTpPx);
   const size_t ogs3 = take((size_t)3 * 2 * C * P2p * 2);
+  const size_t ogm = take((size_t)kBnBlocks * 4), ods = take((size_t)C * 4);
   char* b = static_cast<char*>(base);
   BwdWs2 w;
   w.bnpart = (float*)(b + obp);
@@ -1763,6 +1871,8 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   w.c1sum = (float*)(b + oc1s);
   w.scratch = (float*)(b + oscr);
   w.gsT3 = (__bf16*)(b + ogs3);
+  w.gmax = (float*)(b + ogm);
+  w.wdsc = (float*)(b + ods);
   w.P2p = P2p;
   w.bytes = off;
   return w;
@@ -1804,11 +1914,14 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st, srf::ColSplit{{g_beta1, g_gamma1, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
   const bool c2_32 = use_conv2_32();
+  // split-fp16 data gradient (SRF_DGRAD_F16=0: the split-bf16 one)
+  const bool dg16 = c2_32 && !(getenv("SRF_DGRAD_F16") && getenv("SRF_DGRAD_F16")[0] == '0');
   __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);   // 3 bf16 planes fit the fp32 image
-  const int npack = c2_32 ? (kPackW2tThreads + 255) / 256 : 0;
+  _Float16* wq2h = reinterpret_cast<_Float16*>(w.wq);
+  const int npack = c2_32 ? ((dg16 ? kPackW2tF16Threads : kPackW2tThreads) + 255) / 256 : 0;
   hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks + npack), dim3(256), 0, st, g_out, sv.y2, sv.sel2,
                      sv.stats2, gamma1, w.bnsum2, inp_len, d, drop_p, seed, srf::seed_source(), w.g_ab, w.biaspart,
-                     kBnBlocks, k1a, k1b, wq3);
+                     kBnBlocks, k1a, k1b, wq3, dg16 ? wq2h : nullptr, w.wdsc, w.gmax);
   SRF_LAUNCH_CHECK("conv2_bwd_prep");
   if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, nullptr, w.scratch, st, srf::ColSplit{{g_b1a, g_b1b, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
@@ -1820,8 +1933,12 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
       const int Pc = d.B * ((d.T1 - qt + 1) / 2) * ((d.F1 - qf + 1) / 2);
       cls.boff[c + 1] = cls.boff[c] + (Pc + kD2Px - 1) / kD2Px;
     }
-    hipLaunchKernelGGL(conv2_dgrad32_kernel, dim3(cls.boff[4]), dim3(64 * kD2Waves), 0, st, w.g_ab, wq3, d, cls,
-                       w.g_x1);
+    if (dg16)
+      hipLaunchKernelGGL(conv2_dgrad32_kernel<true>, dim3(cls.boff[4]), dim3(64 * kD2Waves), 0, st, w.g_ab,
+                         (const void*)wq2h, d, cls, w.g_x1, (const float*)w.gmax, kBnBlocks, (const float*)w.wdsc);
+    else
+      hipLaunchKernelGGL(conv2_dgrad32_kernel<false>, dim3(cls.boff[4]), dim3(64 * kD2Waves), 0, st, w.g_ab,
+                         (const void*)wq3, d, cls, w.g_x1, (const float*)nullptr, 0, (const float*)nullptr);
     SRF_LAUNCH_CHECK("conv2_dgrad32");
   } else {
   hipLaunchKernelGGL(pack_w2t_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wq);
