@@ -1084,6 +1084,21 @@ constexpr int kD2BChunks = 3 * C * 2;   // 16-byte B chunks per k-block (planes 
 // from conv2_bwd_prep's block maxima, reduced by every workgroup; B = 2^e_cin k from
 // pack_w2t_f16_body), three f16 MFMAs per k-block tile instead of six bf16 ones;
 // the epilogue multiplies column cin by 2^-ea wdsc[cin].
+// split exponent of g_ab (max|g_ab| < 2^14 after scaling) from conv2_bwd_prep's block
+// maxima; every thread of the block calls it (one barrier)
+__device__ __forceinline__ int gab_exp(const float* __restrict__ gmax, int n) {
+  __shared__ float wmx[16];
+  const int tid = threadIdx.x, nw = (blockDim.x + 63) >> 6;
+  float m = 0.f;
+  for (int k = tid; k < n; k += blockDim.x) m = fmaxf(m, gmax[k]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((tid & 63) == 0) wmx[tid >> 6] = m;
+  __syncthreads();
+  for (int k = 0; k < nw; ++k) m = fmaxf(m, wmx[k]);
+  return srf_split_exp(m);
+}
+
 template <bool H>
 __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2))) void conv2_dgrad32_kernel(
     const float* __restrict__ g_ab, const void* __restrict__ wqv, Dims d, DgCls cls, float* __restrict__ g_x1,
@@ -1109,16 +1124,7 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
   const size_t plane = (size_t)9 * C * 2 * C;
   float sa = 1.f, inv_sa = 1.f;
   if constexpr (H) {   // split exponent of g_ab: max over conv2_bwd_prep's block maxima
-    __shared__ float wmx[kD2Waves];
-    float m = 0.f;
-    for (int k = tid; k < ngmax; k += 64 * kD2Waves) m = fmaxf(m, gmax[k]);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if (lane == 0) wmx[wv] = m;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kD2Waves; ++k) m = fmaxf(m, wmx[k]);
-    const int ea = srf_split_exp(m);
+    const int ea = gab_exp(gmax, ngmax);
     sa = srf_exp2i(ea);
     inv_sa = srf_exp2i(-ea);
   }
@@ -1383,11 +1389,16 @@ __global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restric
 // g_ab [P2][n] -> pixel-minor split planes gsT3[plane][n][P2p] (zero past P2), the B
 // operand image of conv2_wgrad32_kernel: 64 pixels per workgroup through LDS.
 constexpr int kTpPx = 64;
+// H: two fp16 planes of 2^ea g_ab (ea as conv2_dgrad32_kernel) instead of three bf16
+template <bool H>
 __global__ __launch_bounds__(256) void gab_split_t_kernel(const float* __restrict__ g_ab, int P2, int P2p,
-                                                          __bf16* __restrict__ gsT3) {
+                                                          void* __restrict__ gsTv, const float* __restrict__ gmax,
+                                                          int ngmax) {
   __shared__ float tile[kTpPx][2 * C + 1];
   const int tid = threadIdx.x;
   const int p0 = blockIdx.x * kTpPx;
+  float sa = 1.f;
+  if constexpr (H) sa = srf_exp2i(gab_exp(gmax, ngmax));
   for (int k = tid; k < kTpPx * (2 * C / 4); k += 256) {
     const int px = k / (2 * C / 4), q = k % (2 * C / 4);
     const int p = p0 + px;
@@ -1404,12 +1415,26 @@ __global__ __launch_bounds__(256) void gab_split_t_kernel(const float* __restric
     float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = tile[8 * o + k][n];
-    cbf8 p1, p2, p3;
-    split8v(v, p1, p2, p3);
-    __bf16* dst = gsT3 + (size_t)n * P2p + p0 + 8 * o;
-    *reinterpret_cast<cbf8*>(dst) = p1;
-    *reinterpret_cast<cbf8*>(dst + plane) = p2;
-    *reinterpret_cast<cbf8*>(dst + 2 * plane) = p3;
+    if constexpr (H) {
+      ch8 p1, p2;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        _Float16 h1, h2;
+        srf_split2h(v[k] * sa, h1, h2);
+        p1[k] = h1;
+        p2[k] = h2;
+      }
+      _Float16* dst = static_cast<_Float16*>(gsTv) + (size_t)n * P2p + p0 + 8 * o;
+      *reinterpret_cast<ch8*>(dst) = p1;
+      *reinterpret_cast<ch8*>(dst + plane) = p2;
+    } else {
+      cbf8 p1, p2, p3;
+      split8v(v, p1, p2, p3);
+      __bf16* dst = static_cast<__bf16*>(gsTv) + (size_t)n * P2p + p0 + 8 * o;
+      *reinterpret_cast<cbf8*>(dst) = p1;
+      *reinterpret_cast<cbf8*>(dst + plane) = p2;
+      *reinterpret_cast<cbf8*>(dst + 2 * plane) = p3;
+    }
   }
 }
 
@@ -1426,15 +1451,27 @@ constexpr int kW2AStride = 96;   // bf16 per pixel row of the A image (64 cin + 
 
 typedef short ws4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ ws4 lds_tr16(const __bf16* p) {
+template <typename BT>
+__device__ __forceinline__ ws4 lds_tr16(const BT* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) ws4*)(reinterpret_cast<uintptr_t>(p)));
 }
 
+// H = true: split-fp16 operands (A = 2^b BN1(y1) with bn_finalize's exponent, B = the
+// 2^ea g_ab planes of gab_split_t_kernel<true>), three f16 MFMAs per tile instead of
+// six bf16; the partial sums leave unscaled by 2^-(b + ea).
+template <bool H>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv2_wgrad32_kernel(
     const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len,
-    const __bf16* __restrict__ gsT3, int P2p, Dims d, WgDiv dv, int nsplit, int split_len, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][3][kW2Chunk * kW2AStride];
+    const void* __restrict__ gsTv, int P2p, Dims d, WgDiv dv, int nsplit, int split_len, float* __restrict__ part,
+    const float* __restrict__ gmax, int ngmax) {
+  using BT = std::conditional_t<H, _Float16, __bf16>;
+  using V8 = std::conditional_t<H, ch8, cbf8>;
+  constexpr int NPL = H ? 2 : 3;
+  const BT* __restrict__ gsT3 = static_cast<const BT*>(gsTv);
+  __shared__ __attribute__((aligned(16))) BT As[2][NPL][kW2Chunk * kW2AStride];
+  float out_sc = 1.f;
+  if constexpr (H) out_sc = stats1[4 * C + 1] * srf_exp2i(-gab_exp(gmax, ngmax));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   // XCD-aware order (nsplit % 8 == 0): the nine taps of one pixel split run back to
@@ -1448,10 +1485,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   // staging task: pixel px of the chunk, channels 8 oc .. 8 oc + 7
   const int px = tid >> 3, oc = tid & 7;
   float scale[8], shift[8];
+  const float bsc = H ? stats1[4 * C] : 1.f;   // 2^b (exact): the H operand is 2^b BN1(y1)
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    scale[k] = stats1[2 * C + 8 * oc + k];
-    shift[k] = stats1[3 * C + 8 * oc + k];
+    scale[k] = stats1[2 * C + 8 * oc + k] * bsc;
+    shift[k] = stats1[3 * C + 8 * oc + k] * bsc;
   }
   f4 xv[2];
   bool xok = false;
@@ -1473,32 +1511,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     float v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = xok ? (k < 4 ? xv[0][k] : xv[1][k - 4]) * scale[k] + shift[k] : 0.f;
-    cbf8 p1, p2, p3;
-    split8v(v, p1, p2, p3);
     const int o = px * kW2AStride + 8 * oc;
-    *reinterpret_cast<cbf8*>(&As[buf][0][o]) = p1;
-    *reinterpret_cast<cbf8*>(&As[buf][1][o]) = p2;
-    *reinterpret_cast<cbf8*>(&As[buf][2][o]) = p3;
+    if constexpr (H) {
+      ch8 p1, p2;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        _Float16 h1, h2;
+        srf_split2h(v[k], h1, h2);
+        p1[k] = h1;
+        p2[k] = h2;
+      }
+      *reinterpret_cast<ch8*>(&As[buf][0][o]) = p1;
+      *reinterpret_cast<ch8*>(&As[buf][1][o]) = p2;
+    } else {
+      cbf8 p1, p2, p3;
+      split8v(v, p1, p2, p3);
+      *reinterpret_cast<cbf8*>(&As[buf][0][o]) = p1;
+      *reinterpret_cast<cbf8*>(&As[buf][1][o]) = p2;
+      *reinterpret_cast<cbf8*>(&As[buf][2][o]) = p3;
+    }
   };
   // transposed A read: lane 16 g + 4 q + p reads pixel row 8 (g >> 1) + q (+ 4) of the
   // k-block, cin 16 (g & 1) + 4 p .. + 3 of the M-tile; it receives cin 16 (g & 1) + (lane & 15)
   // at pixels 8 (g >> 1) + 0..7 = the 32x32x16 A fragment (row = l & 31, k = 8 (l >> 5) + j)
   const int gg = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
   const int a_off = (8 * (gg >> 1) + qq) * kW2AStride + 16 * (gg & 1) + 4 * pp;
-  auto read_a = [&](const __bf16* img, int kb, int mt) {
-    const __bf16* base = img + a_off + 16 * kb * kW2AStride + 32 * mt;
+  auto read_a = [&](const BT* img, int kb, int mt) {
+    const BT* base = img + a_off + 16 * kb * kW2AStride + 32 * mt;
     const ws4 lo = lds_tr16(base), hi = lds_tr16(base + 4 * kW2AStride);
-    return __builtin_bit_cast(cbf8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    return __builtin_bit_cast(V8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   // B fragments of this wave: n = 32 wv + r, pixels 16 kb + 8 h .. + 7 of the chunk
   const size_t bplane = (size_t)2 * C * P2p;
-  const __bf16* brow = gsT3 + (size_t)(32 * wv + r) * P2p + 8 * h;
-  cbf8 bc[2][3], bn[2][3];
-  auto load_bf = [&](int pc0, cbf8 (&bf)[2][3]) {
+  const BT* brow = gsT3 + (size_t)(32 * wv + r) * P2p + 8 * h;
+  V8 bc[2][NPL], bn[2][NPL];
+  auto load_bf = [&](int pc0, V8 (&bf)[2][NPL]) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) bf[kb][pl] = *reinterpret_cast<const cbf8*>(brow + pl * bplane + pc0 + 16 * kb);
+      for (int pl = 0; pl < NPL; ++pl) bf[kb][pl] = *reinterpret_cast<const V8*>(brow + pl * bplane + pc0 + 16 * kb);
   };
 
   cf16 acc[2];
@@ -1522,24 +1573,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const cbf8 a1 = read_a(As[buf][0], kb, mt);
-        const cbf8 a2 = read_a(As[buf][1], kb, mt);
-        const cbf8 a3 = read_a(As[buf][2], kb, mt);
-        cf16 cc = acc[mt];
-        cc = mfma32bf(a3, bc[kb][0], cc);
-        cc = mfma32bf(a1, bc[kb][2], cc);
-        cc = mfma32bf(a2, bc[kb][1], cc);
-        cc = mfma32bf(a2, bc[kb][0], cc);
-        cc = mfma32bf(a1, bc[kb][1], cc);
-        cc = mfma32bf(a1, bc[kb][0], cc);
-        acc[mt] = cc;
+        if constexpr (H) {
+          const ch8 a1 = read_a(As[buf][0], kb, mt);
+          const ch8 a2 = read_a(As[buf][1], kb, mt);
+          cf16 cc = acc[mt];
+          cc = mfma32h(a2, bc[kb][0], cc);   // small terms first
+          cc = mfma32h(a1, bc[kb][1], cc);
+          cc = mfma32h(a1, bc[kb][0], cc);
+          acc[mt] = cc;
+        } else {
+          const cbf8 a1 = read_a(As[buf][0], kb, mt);
+          const cbf8 a2 = read_a(As[buf][1], kb, mt);
+          const cbf8 a3 = read_a(As[buf][2], kb, mt);
+          cf16 cc = acc[mt];
+          cc = mfma32bf(a3, bc[kb][0], cc);
+          cc = mfma32bf(a1, bc[kb][2], cc);
+          cc = mfma32bf(a2, bc[kb][1], cc);
+          cc = mfma32bf(a2, bc[kb][0], cc);
+          cc = mfma32bf(a1, bc[kb][1], cc);
+          cc = mfma32bf(a1, bc[kb][0], cc);
+          acc[mt] = cc;
+        }
       }
     if (more) {
       put(buf ^ 1);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bc[kb][pl] = bn[kb][pl];
+        for (int pl = 0; pl < NPL; ++pl) bc[kb][pl] = bn[kb][pl];
     }
     __syncthreads();
   }
@@ -1550,7 +1611,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) dst[(size_t)(32 * mt + 8 * q + 4 * h + v) * 2 * C] = acc[mt][4 * q + v];
+      for (int v = 0; v < 4; ++v) dst[(size_t)(32 * mt + 8 * q + 4 * h + v) * 2 * C] = acc[mt][4 * q + v] * out_sc;
 }
 
 // Sum the wgrad splits and unpack n -> (conv a|b, cout): gka/gkb [tap][cin][cout].
@@ -1963,10 +2024,21 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
     static_assert(kW2Chunk == kWgChunk, "wgrad splits are whole chunks");
     nsplit = wgrad32_splits();
     const int split_len = ((P2 + nsplit - 1) / nsplit + kWgChunk - 1) / kWgChunk * kWgChunk;
-    hipLaunchKernelGGL(gab_split_t_kernel, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p, w.gsT3);
-    SRF_LAUNCH_CHECK("gab_split_t");
-    hipLaunchKernelGGL(conv2_wgrad32_kernel, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, w.gsT3,
-                       w.P2p, d, dv, nsplit, split_len, w.wpart);
+    // split-fp16 weight gradient with the split-fp16 data gradient (SRF_DGRAD_F16=0: split-bf16)
+    if (dg16) {
+      hipLaunchKernelGGL(gab_split_t_kernel<true>, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p,
+                         (void*)w.gsT3, (const float*)w.gmax, kBnBlocks);
+      SRF_LAUNCH_CHECK("gab_split_t");
+      hipLaunchKernelGGL(conv2_wgrad32_kernel<true>, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len,
+                         (const void*)w.gsT3, w.P2p, d, dv, nsplit, split_len, w.wpart, (const float*)w.gmax,
+                         kBnBlocks);
+    } else {
+      hipLaunchKernelGGL(gab_split_t_kernel<false>, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p,
+                         (void*)w.gsT3, (const float*)nullptr, 0);
+      SRF_LAUNCH_CHECK("gab_split_t");
+      hipLaunchKernelGGL(conv2_wgrad32_kernel<false>, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len,
+                         (const void*)w.gsT3, w.P2p, d, dv, nsplit, split_len, w.wpart, (const float*)nullptr, 0);
+    }
     SRF_LAUNCH_CHECK("conv2_wgrad32");
   } else {
     const int split_len = ((P2 + nsplit - 1) / nsplit + kWgChunk - 1) / kWgChunk * kWgChunk;

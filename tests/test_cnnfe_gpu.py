@@ -130,11 +130,11 @@ def test_conv2_split_bf16_matches_fp32_mfma(cuda, monkeypatch):
     assert err <= 2e-5 * max(1.0, np.abs(outs[1]).max()), err
 
 
-def test_conv2_dgrad_split_fp16_matches_split_bf16(cuda, monkeypatch):
-    """The split-fp16 stage-2 data gradient (conv2_dgrad32_kernel<true>: scaled 2-term
-    fp16 operands, three f16 MFMAs per tile) against the split-bf16 one
-    (SRF_DGRAD_F16=0, six bf16 MFMAs): the same stage-1 parameter gradients to fp32
-    accuracy, dropout included."""
+def test_conv2_bwd_split_fp16_matches_split_bf16(cuda, monkeypatch):
+    """The split-fp16 stage-2 data and weight gradients (conv2_dgrad32_kernel<true>,
+    conv2_wgrad32_kernel<true>: scaled 2-term fp16 operands, three f16 MFMAs per tile)
+    against the split-bf16 ones (SRF_DGRAD_F16=0, six bf16 MFMAs): the same gradients
+    of every CNN-FE parameter to fp32 accuracy, dropout included."""
     from srf_amd import ops
     torch.manual_seed(5)
     B, T, Fd = 3, 45, 123
@@ -158,7 +158,8 @@ def test_conv2_dgrad_split_fp16_matches_split_bf16(cuda, monkeypatch):
         if gout is None:
             gout = torch.randn_like(out)
         out.backward(gout)
-        # stage-1 parameters (conv1 kernels/biases, BN1) see the stage-2 data gradient
-        grads.append([p.grad.cpu().double().numpy() for p in params[:6]])
+        # stage-1 parameters (conv1 kernels/biases, BN1) see the stage-2 data gradient,
+        # the stage-2 kernels the weight gradient
+        grads.append([p.grad.cpu().double().numpy() for p in params])
     for a, b in zip(grads[0], grads[1]):
         assert np.abs(a - b).max() <= 2e-5 * max(1.0, np.abs(b).max()), np.abs(a - b).max()
