@@ -102,7 +102,7 @@ def test_train_step_runs_and_updates(cuda):
     assert samples.result() == 4
 
 
-@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c3_mini_sdr_lowmemory'])
+@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c3_mini_sdr_lowmemory', 'c4_mini'])
 def test_backward_overwrites_every_gradient(cuda, name):
     """The train step never zeroes grads: every parameter's gradient must be
     written (not accumulated) by the backward kernels.  Poison the flat gradient
@@ -155,7 +155,7 @@ def test_fused_loss_head_matches_autograd(cuda):
     assert (model.flat_grad - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c2_mini_einsum'])
+@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c2_mini_einsum', 'c4_mini'])
 def test_graphed_train_step_matches_eager(cuda, name):
     """GraphedTrainStep (forward + CTC + backward in one hipGraph) computes the same
     loss and gradient as the eager process_train_step, and draws fresh dropout masks
