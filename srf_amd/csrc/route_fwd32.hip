@@ -1599,7 +1599,8 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   int best = 1;
   double best_cost = 1e30;
   const char* env = getenv("SRF_FWD32_CHUNKS");
-  const int forced = env ? atoi(env) : 0;
+  const char* envb = getenv("SRF_FWD32_CHUNKS_BIG");   // A/B: forces only multi-wave (NW > 1, JD > 128) plans
+  const int forced = env ? atoi(env) : (envb && p.NW > 1 && JD > 128 ? atoi(envb) : 0);
   for (int c = 1; c <= std::min(in_n, 96); ++c) {
     const int rounds = (n_ftiles * c + slots - 1) / slots;
     const int len = (in_n + c - 1) / c;
