@@ -680,7 +680,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int j0 = tbase * 32 / DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
 #if SRF_FWD32_PRIO
-  if (NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (DIN <= 16 && NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);   // din 32: measured faster without
 #endif
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
@@ -962,7 +962,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int j0 = tbase * 32 / DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
 #if SRF_FWD32_PRIO
-  if (NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (DIN <= 16 && NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);   // din 32: measured faster without
 #endif
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
