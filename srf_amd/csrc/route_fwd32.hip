@@ -66,6 +66,10 @@
 #ifndef SRF_FWD32_TM
 #define SRF_FWD32_TM 1
 #endif
+// 1: the tile-major schedule for din 32 as well (A/B knob; pose_prog measured faster)
+#ifndef SRF_FWD32_TM32
+#define SRF_FWD32_TM32 0
+#endif
 // 0: the compiler may move the operand reloads among the tile's MFMAs (A/B knob)
 #ifndef SRF_FWD32_TMSB
 #define SRF_FWD32_TMSB 1
@@ -734,7 +738,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       f2 P2[CP];
 #pragma unroll
       for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
-      if constexpr (SRF_FWD32_TM && DIN <= 16) {   // din 32: pose_prog measured faster (C4 A/B)
+      if constexpr (SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) {   // din 32: pose_prog measured faster (C4 A/B)
       {
         constexpr uint32_t TSTEP = 32 * DIN * 2;
         const int in = min(i + 1, i1 - 1);
@@ -856,7 +860,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       // next capsule's operands: issued once every MFMA result has been consumed
       // (the dots), so no load waits on a queued MFMA's operand read
       __builtin_amdgcn_sched_barrier(0);
-      if (!(SRF_FWD32_TM && DIN <= 16) && !SRF_FWD32_PROG && !SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
+      if (!(SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) && !SRF_FWD32_PROG && !SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                                A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
@@ -1003,7 +1007,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #pragma unroll
       for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
       float cc[OWN];
-      if constexpr (SRF_FWD32_TM && DIN <= 16) {   // din 32: pose_prog measured faster (C4 A/B)
+      if constexpr (SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) {   // din 32: pose_prog measured faster (C4 A/B)
       // this capsule's couplings, then the tile-major pose with the dots of tile t - 1
       // behind tile t's MFMAs (as route_fwd32_kernel)
       load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
@@ -1102,7 +1106,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         par ^= 1;
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (!(SRF_FWD32_TM && DIN <= 16) && !SRF_FWD32_PROG && i + 1 < i1) {
+      if (!(SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) && !SRF_FWD32_PROG && i + 1 < i1) {
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
                                h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
                                (uint32_t)(i + 1) * A.JDp * 8, fr);
