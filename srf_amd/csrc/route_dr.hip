@@ -1597,7 +1597,10 @@ Gw2Plan gw2_plan(const Geom& g) {
   const int NCT = (g.din + 15) / 16;
   p.n_rt = (NT + 3) / 4;
   p.cap = gw3_cap(g) ? gw3_cap(g) : gw2_cap_rt(g.din);
-  const int slots = gw3_cap(g) ? 768 : 512;   // workgroups resident at once
+  // workgroups resident at once; route_gw3_kernel (latency-bound) is planned for two
+  // resident rounds: at C4 S = 8 frame splits (1280 workgroups) beat S = 4 (640, one
+  // round) by 2 %, at C2 the slab term keeps S = 5
+  const int slots = gw3_cap(g) ? 2 * 768 : 512;
   p.n_cc = (g.in_n() + p.cap - 1) / p.cap;
   const int NFT = padded_frames(g) / 16;
   p.pstride = (size_t)g.in_n() * g.JD() * (g.din + 1);
