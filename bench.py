@@ -44,7 +44,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / f16 MFMA peak
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py` (timit_c2), averaged per
 # dispatch by scripts/pmcsum.py (KiB per dispatch)
-PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4g.json')
+PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4h.json')
 
 
 def make_config(kw):
