@@ -5,17 +5,21 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1] = C2): TIMIT SRF L=3, PH=CH=8, DIM=16,
-LPAD=RPAD=4, DR iter 3, fp32, class_n 63; per GPU B=17 utterances of T=320
-frames (the reference's bucket rule for 7000 frames/batch, SURVEY.md 8d);
-synthetic N(0,1) 123-d fbank, labels uniform in [1, 61], L = T'/2.
+Headline workload (the metric's "3-iter DR at 1/2/4/8 MI355X" = BASELINE.json
+configs[3], C4, whose per-GPU batch fits one GPU): WSJ SRF L=6, PH=CH=16, DIM=32,
+LPAD=RPAD=2, DR iter 3, fp32, class_n 32; per GPU B=28 utterances of T=800 frames
+(the reference's bucket rule for 24000 frames/batch).  The TIMIT C2
+model (configs[1]: L=3, PH=CH=8, DIM=16, LPAD=RPAD=4, B=17, T=320) is measured
+after it and reported under "extra".  Synthetic N(0,1) 123-d fbank, labels
+uniform in [1, C-2], L = T'/2.
 One step = process_train_step: crop, forward, CTC, backward, RCCL gradient
 all-reduce (N > 1), fused Adam.  value = sum(inp_len) over all ranks / step time
 (the reference's frame counter, trainer_sr.py:74), weak scaling.
 
 Prints ONE JSON line on rank 0 (roofline of the dominant kernel from HIP events
 inside the timed region; CPU baseline = torch-CPU op-for-op mirror of
-sequence_router_naive.py on a bounded sample, rank 0 at N=1 only).
+sequence_router_naive.py on a bounded sample, rank 0 at N=1 only, on all host
+threads and on one core).
 """
 import argparse
 import ctypes
@@ -42,9 +46,9 @@ WORKLOADS = {
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / f16 MFMA peak
 HBM_PEAK_GBS = 8000.0
-# rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py` (timit_c2), averaged per
-# dispatch by scripts/pmcsum.py (KiB per dispatch)
-PMC_TRAFFIC = os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4h.json')
+# rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`, averaged per dispatch by
+# scripts/pmcsum.py (KiB per dispatch), per workload
+PMC_TRAFFIC = {'timit_c2': os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4h.json')}
 
 
 def make_config(kw):
@@ -103,7 +107,18 @@ class HipEvents:
         return ms.value
 
 
-def cpu_baseline(model_gpu, cfg, class_n, T, seconds):
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for ln in fh:
+                if ln.startswith('model name'):
+                    return ln.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def cpu_baseline(model_gpu, cfg, class_n, T, seconds, threads=None, max_steps=50):
     """torch-CPU op-for-op mirror of naive (oracle/naive_mirror.py), fp32,
     one T-frame utterance per step, timed for >= `seconds` (>= 1 step)."""
     from oracle import naive_mirror as nm
@@ -113,7 +128,9 @@ def cpu_baseline(model_gpu, cfg, class_n, T, seconds):
               pd=cfg.model_caps_primary_dim, ch=cfg.model_caps_convolution_num, cd=cfg.model_caps_convolution_dim,
               vd=cfg.model_caps_class_dim, class_n=class_n, context=bool(cfg.model_caps_context))
     shape = so.SrfShape(**kw)
-    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16') or 16))
+    if threads is None:
+        threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16') or 16))
+    prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     params = model_gpu.export_params()
     mirror = nm.NaiveMirror(shape, params, dtype=torch.float32)
@@ -126,9 +143,11 @@ def cpu_baseline(model_gpu, cfg, class_n, T, seconds):
         frames += int(inp_len.sum())
         steps += 1
         el = time.perf_counter() - t0
-        if el >= seconds or steps >= 50:
+        if el >= seconds or steps >= max_steps:
             break
-    return {'value': frames / el, 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+    torch.set_num_threads(prev)
+    return {'value': round(frames / el, 1), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+            'cpu_model': _cpu_model(),
             'sample': f'{steps} train steps x 1 utterance x {T} frames (torch-CPU mirror of '
                       f'sequence_router_naive.py, fp32, {el:.1f}s)'}
 
@@ -153,12 +172,154 @@ def pmc_traffic(path, kernels, weights):
     return total / sum(weights)
 
 
+def _timed(step, steps, world, dev):
+    """Barrier + synchronize on both sides of `steps` calls; max over ranks."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def measure(workload, args, world, rank, dev):
+    """One workload: W eager + W graphed warmup steps, K timed training steps (the
+    hipGraph replay of forward + CTC + backward, then the all-reduce and Adam), K
+    eager steps with HIP events around the last layer's forward routing passes,
+    and K forward-only passes."""
+    from srf_amd import train_helper, trainer_sr
+    from srf_amd.sequence_router import SequenceRouter
+
+    kw, class_n, B, T = WORKLOADS[workload]
+    cfg = make_config(kw)
+    model = SequenceRouter(cfg, None, class_n, device=dev, seed=1234)   # same init on every rank
+    opt = train_helper.get_optimizer(cfg)
+    batch = synthetic_batch(B, T, class_n, rank, dev)
+    loss_state, frame_state, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
+
+    def eager_step():
+        trainer_sr.process_train_step(4, batch, model, opt, loss_state, frame_state, world, class_n - 1, samples)
+
+    for _ in range(args.warmup):
+        eager_step()
+    torch.cuda.synchronize()
+    graphed = None
+    if args.eager:
+        step = eager_step
+    else:
+        # forward + CTC + backward as one hipGraph; all-reduce and Adam eager per step
+        graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
+        for _ in range(args.warmup):
+            graphed(loss_state, frame_state, samples)
+        torch.cuda.synchronize()
+
+        def step():
+            graphed(loss_state, frame_state, samples)
+
+    # HIP events around the dominant kernel (forward routing passes of the last
+    # layer), recorded on the launch stream
+    ev = HipEvents()
+    Tp = (T + 3) // 4
+    last = model.enc_num - 1
+    geom = model._geom(last, B, Tp)
+    R = model.iter
+    dr = not model.is_context    # the event hook times DR passes; SDR runs no such pass
+    ev_pairs = [(ev.create(R), ev.create(R)) for _ in range(args.steps)] if dr else []
+    if dr and args.eager:
+        geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
+
+    elapsed = _timed(step, args.steps, world, dev)
+    geom.timing = None
+    if dr and not args.eager:
+        # graph replays carry no per-kernel events: time the same kernels in as many
+        # eager steps right after the timed region (same shapes, same stream)
+        geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
+        for _ in range(args.steps):
+            eager_step()
+        torch.cuda.synchronize()
+        geom.timing = None
+    if graphed is not None:
+        graphed.close()
+
+    # forward-only frames/s (SURVEY section 8d): model(feats, training=False) as in
+    # process_valid_step (BN moving statistics, no dropout), eager launches, outside
+    # the training-step timed region, same barrier + max-over-ranks timing
+    feats_b, il_b = batch[0], batch[2]
+    with torch.no_grad():
+        for _ in range(max(1, args.warmup)):
+            model(feats_b, input_lengths=il_b, training=False)
+        fwd_elapsed = _timed(lambda: model(feats_b, input_lengths=il_b, training=False), args.steps, world, dev)
+
+    kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
+    kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
+    in_n, J, D, Din = model.layer_shapes[last]
+    fwd32 = Din in (8, 16, 32) and D in (8, 16, 32) and Din <= D and J * D <= 1024 and \
+        os.environ.get('SRF_ROUTE_FWD32', '1') != '0'
+    frames_prime = B * Tp
+    # algorithmic FLOPs per launch: the layer's pose contraction (once per
+    # forward, spread over its R pass launches) + one routing iteration
+    pose = 2.0 * in_n * J * D * Din
+    route = 4.0 * in_n * J * D
+    flops_launch = frames_prime * (pose / R + route)
+    achieved_tflops = flops_launch / (kern_avg_ms * 1e-3) / 1e12
+
+    traffic, traffic_src = None, PMC_TRAFFIC.get(workload)
+    if fwd32 and traffic_src:
+        traffic = pmc_traffic(traffic_src, [f'void route_fwd32_first_kernel<{Din}, {D}>',
+                                            f'void route_fwd32_kernel<{Din}, {D}, '], [1.0, R - 1.0])
+    res = {
+        'value': round(B * T * world * args.steps / elapsed, 1), 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+        'config': {'workload': f'{workload}: SRF L={cfg.model_encoder_num} PH=CH={cfg.model_caps_primary_num} '
+                               f'DIM={cfg.model_caps_primary_dim} LPAD=RPAD={cfg.model_caps_window_lpad} '
+                               f'{"SDR" if model.is_context else "DR"} iter={cfg.model_caps_iter}, '
+                               f'train step (fwd+bwd+allreduce+Adam)',
+                   'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
+                   'parallelism': f'dp{world}', 'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
+        'roofline': {'kernel': (f'route_fwd32_first_kernel + route_fwd32_kernel<{Din},{D}> (layer {last + 1} DR forward '
+                                f'passes, R={R}; pose on v_mfma_f32_32x32x16_f16 as 2-term fp16 splits of power-of-two '
+                                f'scaled operands + one bf16 bias MFMA = fp32-accurate)'
+                                if fwd32 else f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)'),
+                     'bound': 'mfma', 'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
+                     'traffic': round(traffic) if traffic else None,
+                     'traffic_source': (os.path.relpath(traffic_src, HERE) + ' (HBM bytes per launch, '
+                                        '2*FETCH_SIZE+WRITE_SIZE)') if traffic else None,
+                     'avg_launch_us': round(kern_avg_ms * 1e3, 2),
+                     'flops_per_launch': flops_launch,
+                     # what the matrix cores execute: the full pose every pass, per 32-row tile and
+                     # capsule 3 f16 K=16 products + 1 bf16 bias product (din 16), 2 + 1 (din 8,
+                     # two planes packed in K) or 6 + 1 (din 32, two K=16 halves), on the
+                     # 32x32-padded rows
+                     'executed_mfma': ({'dtype': 'f16/bf16', 'peak_tflops': BF16_MFMA_PEAK_TFLOPS,
+                                        'frac': round(frames_prime * 2.0 * in_n * ((J * D + 31) // 32 * 32) * 16
+                                                      * {8: 3, 16: 4, 32: 7}[Din] / (kern_avg_ms * 1e-3) / 1e12
+                                                      / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
+                    if dr else None,
+        'forward_only': {'value': round(B * T * world * args.steps / fwd_elapsed, 1), 'unit': 'frames/s',
+                         'ms_per_step': round(fwd_elapsed / args.steps * 1e3, 4),
+                         'mode': 'model(feats, training=False), eager launches'},
+    }
+    return res, model, cfg, class_n, T
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--workload', default='timit_c2', choices=sorted(WORKLOADS))
+    ap.add_argument('--workload', default='wsj_c4', choices=sorted(WORKLOADS),
+                    help='the headline line (BASELINE metric: 3-iter DR on the WSJ C4 model)')
+    ap.add_argument('--extra', default='timit_c2',
+                    help='comma-separated workloads also measured, reported under "extra" (empty: none)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--eager', action='store_true', help='launch every kernel from Python each step (no hipGraph)')
@@ -179,148 +340,29 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from srf_amd import train_helper, trainer_sr
-    from srf_amd.sequence_router import SequenceRouter
-
-    kw, class_n, B, T = WORKLOADS[args.workload]
-    cfg = make_config(kw)
-    model = SequenceRouter(cfg, None, class_n, device=dev, seed=1234)   # same init on every rank
-    opt = train_helper.get_optimizer(cfg)
-    batch = synthetic_batch(B, T, class_n, rank, dev)
-    loss_state, frame_state, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
-
-    def eager_step():
-        trainer_sr.process_train_step(4, batch, model, opt, loss_state, frame_state, world, class_n - 1, samples)
-
-    for _ in range(args.warmup):
-        eager_step()
-    torch.cuda.synchronize()
-    if args.eager:
-        step = eager_step
-    else:
-        # forward + CTC + backward as one hipGraph; all-reduce and Adam eager per step
-        graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
-        for _ in range(args.warmup):
-            graphed(loss_state, frame_state, samples)
-        torch.cuda.synchronize()
-
-        def step():
-            graphed(loss_state, frame_state, samples)
-
-    # HIP events around the dominant kernel (forward routing pass of the last
-    # layer) for every timed step, recorded on the launch stream.
-    ev = HipEvents()
-    Tp = (T + 3) // 4
-    last = model.enc_num - 1
-    geom = model._geom(last, B, Tp)
-    R = model.iter
-    dr = not model.is_context    # the event hook times DR passes; SDR runs no such pass
-    ev_pairs = [(ev.create(R), ev.create(R)) for _ in range(args.steps)] if dr else []
-    if dr and args.eager:
-        geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    geom.timing = None
-    if dr and not args.eager:
-        # graph replays carry no per-kernel events: time the same kernels in as many
-        # eager steps right after the timed region (same shapes, same stream)
-        geom.timing = [(ctypes.cast(a, ctypes.c_void_p), ctypes.cast(b, ctypes.c_void_p), R) for a, b in ev_pairs]
-        for _ in range(args.steps):
-            eager_step()
-        torch.cuda.synchronize()
-        geom.timing = None
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # forward-only frames/s: model(feats, training=False) as in
-    # process_valid_step (BN moving statistics, no dropout), eager launches, outside
-    # the training-step timed region, same barrier + max-over-ranks timing
-    feats_b, il_b = batch[0], batch[2]
-    with torch.no_grad():
-        for _ in range(max(1, args.warmup)):
-            model(feats_b, input_lengths=il_b, training=False)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        tf0 = time.perf_counter()
-        for _ in range(args.steps):
-            model(feats_b, input_lengths=il_b, training=False)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        fwd_elapsed = time.perf_counter() - tf0
-    if world > 1:
-        t = torch.tensor([fwd_elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        fwd_elapsed = float(t.item())
-
-    kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
-    kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
-    in_n, J, D, Din = model.layer_shapes[last]
-    fwd32 = Din in (8, 16, 32) and D in (8, 16, 32) and Din <= D and J * D <= 1024 and os.environ.get('SRF_ROUTE_FWD32', '1') != '0'
-    frames_prime = B * Tp
-    # algorithmic FLOPs per launch: the layer's pose contraction (once per
-    # forward, spread over its R pass launches) + one routing iteration
-    pose = 2.0 * in_n * J * D * Din
-    route = 4.0 * in_n * J * D
-    flops_launch = frames_prime * (pose / R + route)
-    achieved_tflops = flops_launch / (kern_avg_ms * 1e-3) / 1e12
-
-    traffic = None
-    if fwd32 and args.workload == 'timit_c2':
-        traffic = pmc_traffic(PMC_TRAFFIC, [f'void route_fwd32_first_kernel<{Din}, {D}>',
-                                            f'void route_fwd32_kernel<{Din}, {D}, '], [1.0, R - 1.0])
-
-    frames_per_step = B * T * world
-    value = frames_per_step * args.steps / elapsed
+    res, model, cfg, class_n, T = measure(args.workload, args, world, rank, dev)
     line = {
         'metric': 'acoustic frames/sec through SRF (123-d fbank, 3-iter DR) at 1/2/4/8 MI355X',
-        'value': round(value, 1), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
-        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
+        'value': res['value'], 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': res['ms_per_step'], 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic (N(0,1) 123-d fbank, random init)',
-        'config': {'workload': f'{args.workload}: SRF L={cfg.model_encoder_num} PH=CH={cfg.model_caps_primary_num} '
-                               f'DIM={cfg.model_caps_primary_dim} LPAD=RPAD={cfg.model_caps_window_lpad} '
-                               f'{"SDR" if model.is_context else "DR"} iter={cfg.model_caps_iter}, '
-                               f'train step (fwd+bwd+allreduce+Adam)',
-                   'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
-                   'parallelism': f'dp{world}', 'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
-        'roofline': {'kernel': (f'route_fwd32_first_kernel + route_fwd32_kernel<{Din},{D}> (layer {last + 1} DR forward '
-                                f'passes, R={R}; pose on v_mfma_f32_32x32x16_f16 as 2-term fp16 splits of power-of-two '
-                                f'scaled operands + one bf16 bias MFMA = fp32-accurate)'
-                                if fwd32 else f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)'),
-                     'bound': 'mfma', 'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS,
-                     'unit': 'TFLOP/s', 'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4),
-                     'traffic': round(traffic) if traffic else None,
-                     'traffic_source': (os.path.relpath(PMC_TRAFFIC, HERE) + ' (HBM bytes per launch, '
-                                        '2*FETCH_SIZE+WRITE_SIZE)') if traffic else None,
-                     'avg_launch_us': round(kern_avg_ms * 1e3, 2),
-                     'flops_per_launch': flops_launch,
-                     # what the matrix cores execute: the full pose every pass, per 32-row tile and
-                     # capsule 3 f16 K=16 products + 1 bf16 bias product (din 16), 2 + 1 (din 8,
-                     # two planes packed in K) or 6 + 1 (din 32, two K=16 halves), on the
-                     # 32x32-padded rows
-                     'executed_mfma': ({'dtype': 'f16/bf16', 'peak_tflops': BF16_MFMA_PEAK_TFLOPS,
-                                        'frac': round(frames_prime * 2.0 * in_n * ((J * D + 31) // 32 * 32) * 16
-                                                      * {8: 3, 16: 4, 32: 7}[Din] / (kern_avg_ms * 1e-3) / 1e12
-                                                      / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
-                    if dr else None,
+        'config': res['config'], 'roofline': res['roofline'], 'forward_only': res['forward_only'],
     }
-    line['forward_only'] = {'value': round(B * T * world * args.steps / fwd_elapsed, 1), 'unit': 'frames/s',
-                            'ms_per_step': round(fwd_elapsed / args.steps * 1e3, 4),
-                            'mode': 'model(feats, training=False), eager launches'}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)
+        # the full host (16 threads on the box) on one utterance of the workload's
+        # length, and one core on a quarter-length utterance (frames/s is per frame)
+        cb = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)
+        one = cpu_baseline(model, cfg, class_n, max(40, T // 4), args.cpu_seconds / 2, threads=1)
+        cb['one_core'] = {k: one[k] for k in ('value', 'cores', 'sample')}
+        line['cpu_baseline'] = cb
+    del model
+    extra = [w for w in args.extra.split(',') if w and w != args.workload]
+    if extra:
+        line['extra'] = {}
+        for w in extra:
+            r, m, _, _, _ = measure(w, args, world, rank, dev)
+            del m
+            line['extra'][w] = r
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,9 +1,11 @@
 /* srf.h -- C ABI of the MI355X-native Sequential Routing Framework hot path.
  *
  * Every entry point takes caller-owned device pointers (fp32 unless stated),
- * plain int shapes and a hipStream_t passed as void*.  Nothing allocates, nothing
- * synchronises, no global mutable state: calls are stream-ordered and may be
- * captured into a hipGraph.  Return value: 0 on success, < 0 on error
+ * plain int shapes and a hipStream_t passed as void*.  Nothing allocates and
+ * nothing synchronises: calls are stream-ordered and may be captured into a
+ * hipGraph.  One piece of process-wide state exists, set only by the caller: the
+ * dropout step counter of srf_set_seed_source (below); every other call depends
+ * on its arguments alone.  Return value: 0 on success, < 0 on error
  * (SRF_EINVAL -1 bad argument, SRF_EHIP -2 HIP error, SRF_EUNSUPPORTED -3,
  * SRF_EWORKSPACE -4); srf_last_error() then holds a thread-local message.
  *
@@ -68,19 +70,15 @@ int srf_route_dr_bwd_data_ex(const float* emb, const float* W, const float* bias
                              int lpad, int rpad, int J, int dout, int iters, int mask_first, int n_chunks,
                              const float* saved, const float* couplings, const float* g_v, float* g_emb,
                              void* workspace, size_t workspace_bytes, void* stream);
-/* Dropout step counter (process-wide): a device uint64 that every dropout kernel
- * launched afterwards, from any thread, mixes into its seed (NULL restores the
- * per-call seeds alone).  It lets a training step captured into a hipGraph draw
- * fresh masks on every replay: the step advances the counter on the device.
- * Forward and backward of one step must see the same counter value (the autograd
- * backward runs on torch's device worker thread, hence process-wide, not per
- * thread; one process drives one GPU). */
+/* Dropout step counter -- PROCESS-GLOBAL state: a device uint64 that every dropout
+ * kernel launched afterwards, from any thread and for any model, mixes into its
+ * seed (NULL restores the per-call seeds alone).  It lets a training step captured
+ * into a hipGraph draw fresh masks on every replay: the step advances the counter
+ * on the device.  Forward and backward of one step must see the same counter value
+ * (the autograd backward runs on torch's device worker thread, hence process-wide,
+ * not per thread).  One process drives one GPU, so the host keeps one counter per
+ * process and never detaches it (srf_amd.trainer_sr.seed_counter). */
 int srf_set_seed_source(const void* step_counter);
-
-/* Profiling hook (opt-in, this thread only): the next srf_route_dr_fwd call
- * records starts[r] / stops[r] (hipEvent_t) on its stream around the routing-pass
- * kernel of iteration r < n, then forgets the arrays. */
-int srf_route_dr_set_timing_events(void* const* starts, void* const* stops, int n);
 /* Gradients are written (not accumulated): g_emb [B*T][N][din], g_W like W,
  * g_bias like bias. */
 int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,

@@ -116,9 +116,13 @@ def sequential_routing(u, iters, mask_first):
 class NaiveMirror(torch.nn.Module):
     """Parameters are held in a dict of tensors keyed like ``srf_oracle.init_params``."""
 
-    def __init__(self, shape, params, dtype=torch.float64):
+    def __init__(self, shape, params, dtype=torch.float64, tile=True):
+        """tile=False contracts the pose with an einsum instead of the reference's
+        tf.tile-materialised W (same products, float64; for full-size fixtures,
+        whose tiled W would not fit in memory)."""
         super().__init__()
         self.shape = shape
+        self.tile = tile
         self.p = torch.nn.ParameterDict()
         self.buffers_ = {}
         for k, v in params.items():
@@ -169,8 +173,10 @@ class NaiveMirror(torch.nn.Module):
             if sh.caps_type == 'lowmemory' and not sh.context:
                 J = self.P(f'W{l}').shape[1]
                 u = xw.unsqueeze(3).repeat(1, 1, 1, J, 1)              # lowmemory:162, no W / bias
-            else:
+            elif self.tile:
                 u = pose_tiled(xw, self.P(f'W{l}'), self.P(f'b{l}'))
+            else:
+                u = torch.einsum('ijde,btie->btijd', self.P(f'W{l}'), xw) + self.P(f'b{l}')
             if sh.context:
                 v = sequential_routing(u, sh.route_iters, l == L - 1)
             else:

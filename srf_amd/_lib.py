@@ -16,7 +16,6 @@ _c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
 _SIGNATURES = {
     'srf_version': (_c_int, []),
     'srf_last_error': (ctypes.c_char_p, []),
-    'srf_route_dr_set_timing_events': (_c_int, [_vp, _vp, _c_int]),
     'srf_set_seed_source': (_c_int, [_vp]),
     'srf_route_dr_auto_chunks': (_c_int, [_c_int] * 8),
     'srf_route_dr_saved_floats': (_c_size, [_c_int] * 5),
@@ -76,6 +75,11 @@ _SIGNATURES = {
                                ctypes.c_float, _vp]),
 }
 
+# include/srf_prof.h: diagnostics (bench.py's kernel timing), not the product ABI.
+_PROF_SIGNATURES = {
+    'srf_route_dr_set_timing_events': (_c_int, [_vp, _vp, _c_int]),
+}
+
 
 class SrfError(RuntimeError):
     pass
@@ -95,7 +99,7 @@ def lib():
         # /opt/rocm's) is the one this library binds to.
         import torch  # noqa: F401
         h = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in _SIGNATURES.items():
+        for name, (res, args) in list(_SIGNATURES.items()) + list(_PROF_SIGNATURES.items()):
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
@@ -105,6 +109,10 @@ def lib():
 
 def exported_symbols():
     return list(_SIGNATURES)
+
+
+def prof_symbols():
+    return list(_PROF_SIGNATURES)
 
 
 def check(rc, what):

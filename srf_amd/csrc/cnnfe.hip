@@ -252,44 +252,43 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
                  part[((size_t)k * 3 + 2) * C + c]);
   sh[0][r][c] = n; sh[1][r][c] = mu; sh[2][r][c] = m2;
   __syncthreads();
-  if (r != 0) {
-    if (ymax != nullptr) __syncthreads();
-    return;
-  }
-  float mean, var;
-  if (training) {
-    for (int q = 1; q < 16; ++q) chan_merge(n, mu, m2, sh[0][q][c], sh[1][q][c], sh[2][q][c]);
-    mean = mu;
-    var = m2 / n;
-    // moving averages; the fused NHWC kernel feeds the Bessel-corrected variance
-    mmean[c] = mmean[c] * kBnMomentum + mean * (1.f - kBnMomentum);
-    mvar[c] = mvar[c] * kBnMomentum + (n > 1.f ? var * n / (n - 1.f) : var) * (1.f - kBnMomentum);
-  } else {
-    mean = mmean[c];
-    var = mvar[c];
-  }
-  const float rstd = 1.f / sqrtf(var + kBnEps);
-  const float scale = gamma[c] * rstd;
-  const float shift = beta[c] - mean * scale;
-  stats[0 * C + c] = mean;
-  stats[1 * C + c] = rstd;
-  stats[2 * C + c] = scale;
-  stats[3 * C + c] = shift;
-  if (ymax != nullptr) {
+  // wave 0 (r == 0) finalises the 64 channels; every wave then meets the one
+  // barrier below (taken by all or none: ymax is a kernel argument)
+  if (r == 0) {
+    float mean, var;
+    if (training) {
+      for (int q = 1; q < 16; ++q) chan_merge(n, mu, m2, sh[0][q][c], sh[1][q][c], sh[2][q][c]);
+      mean = mu;
+      var = m2 / n;
+      // moving averages; the fused NHWC kernel feeds the Bessel-corrected variance
+      mmean[c] = mmean[c] * kBnMomentum + mean * (1.f - kBnMomentum);
+      mvar[c] = mvar[c] * kBnMomentum + (n > 1.f ? var * n / (n - 1.f) : var) * (1.f - kBnMomentum);
+    } else {
+      mean = mmean[c];
+      var = mvar[c];
+    }
+    const float rstd = 1.f / sqrtf(var + kBnEps);
+    const float scale = gamma[c] * rstd;
+    const float shift = beta[c] - mean * scale;
+    stats[0 * C + c] = mean;
+    stats[1 * C + c] = rstd;
+    stats[2 * C + c] = scale;
+    stats[3 * C + c] = shift;
     ab[0][c] = fabsf(scale);
     ab[1][c] = fabsf(shift);
-    __syncthreads();
-    if (c == 0) {
-      float y = ysh[0], sa = 0.f, sb = 0.f;
-      for (int q = 1; q < 16; ++q) y = fmaxf(y, ysh[q]);
-      for (int q = 0; q < C; ++q) {
-        sa = fmaxf(sa, ab[0][q]);
-        sb = fmaxf(sb, ab[1][q]);
-      }
-      const int e = srf_split_exp(sa * y + sb);
-      stats[4 * C + 0] = srf_exp2i(e);
-      stats[4 * C + 1] = srf_exp2i(-e);
+  }
+  if (ymax == nullptr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float y = ysh[0], sa = 0.f, sb = 0.f;
+    for (int q = 1; q < 16; ++q) y = fmaxf(y, ysh[q]);
+    for (int q = 0; q < C; ++q) {
+      sa = fmaxf(sa, ab[0][q]);
+      sb = fmaxf(sb, ab[1][q]);
     }
+    const int e = srf_split_exp(sa * y + sb);
+    stats[4 * C + 0] = srf_exp2i(e);
+    stats[4 * C + 1] = srf_exp2i(-e);
   }
 }
 

@@ -322,16 +322,22 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
   }
 }
 
-// Gradient kernel: grid (B, ceil(Tmax/16)), 256 threads = 16 frames x 16 class
+// Gradient kernel: grid (B, ceil(Tmax/FR)), 256 threads = FR frames x 256/FR class
 // lanes.  Per class the label positions are walked through a next-occurrence list
 // (built in LDS, one thread per label position), over alpha + beta of the block's
-// 16 frames staged in LDS, so a frame costs O(L + C) LDS reads, not O(C * L) loads.
-// Dynamic LDS: head[C] | next[Lmax] (int) | ab[16][Smax].
+// FR frames staged in LDS (STAGE), so a frame costs O(L + C) LDS reads, not
+// O(C * L) loads.  FR (16 down to 1) is the largest whose staging fits
+// kCtcGradLds; past that (very long label sequences) alpha + beta are read from
+// the workspace directly (STAGE = false).
+// Dynamic LDS: head[C] | next[Lmax] (int) | ab[FR][Smax] (STAGE only).
+constexpr size_t kCtcGradLds = 64 * 1024;
+
+template <bool STAGE>
 __global__ __launch_bounds__(256) void ctc_grad_kernel(const int* __restrict__ labels,
                                                        const int* __restrict__ label_len,
                                                        const int* __restrict__ logit_len,
                                                        const float* __restrict__ nll, int Tmax, int C, int Lmax,
-                                                       int blank, float scale, const float* __restrict__ ws,
+                                                       int blank, float scale, int FR, const float* __restrict__ ws,
                                                        float* __restrict__ grad) {
   extern __shared__ int lists[];
   int* head = lists;
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const int* __restrict__ l
   const float ll = -nll[b];
   const bool feasible = ll > -INFINITY;
   const int* lab = labels + (size_t)b * Lmax;
-  const int t0 = blockIdx.y * 16;
+  const int t0 = blockIdx.y * FR;
   const float* gws = ws + (size_t)b * Tmax * (C + 2 * Smax);
   const float* lp = gws;
   const float* alpha = gws + (size_t)Tmax * C;
@@ -362,30 +368,36 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const int* __restrict__ l
     next[k] = nx;
   }
   const int S = 2 * L + 1;
-  const int nt = min(16, Tb - t0);
-  for (int i = threadIdx.x; i < 16 * S; i += blockDim.x) {
-    const int tt = i / S, sidx = i - tt * S;
-    float v = -INFINITY;
-    if (tt < nt) {
-      const size_t o = (size_t)(t0 + tt) * Smax + sidx;
-      v = alpha[o] + beta[o];
+  const int nt = min(FR, Tb - t0);
+  if constexpr (STAGE) {
+    for (int i = threadIdx.x; i < FR * S; i += blockDim.x) {
+      const int tt = i / S, sidx = i - tt * S;
+      float v = -INFINITY;
+      if (tt < nt) {
+        const size_t o = (size_t)(t0 + tt) * Smax + sidx;
+        v = alpha[o] + beta[o];
+      }
+      ab[tt * Smax + sidx] = v;
     }
-    ab[tt * Smax + sidx] = v;
   }
   __syncthreads();
-  const int tt = threadIdx.x >> 4;
+  const int lanes = blockDim.x / FR;
+  const int tt = threadIdx.x / lanes;
   const int t = t0 + tt;
   if (t >= Tmax) return;
   float* gb = grad + ((size_t)b * Tmax + t) * C;
   const float* abt = ab + tt * Smax;
-  for (int c = threadIdx.x & 15; c < C; c += 16) {
+  const float* at = alpha + (size_t)t * Smax;
+  const float* bt = beta + (size_t)t * Smax;
+  auto abv = [&](int sidx) { return STAGE ? abt[sidx] : at[sidx] + bt[sidx]; };
+  for (int c = threadIdx.x % lanes; c < C; c += lanes) {
     float g = 0.f;
     if (t < Tb && feasible) {
       float acc = -INFINITY;
       if (c == blank) {
-        for (int s2 = 0; s2 <= 2 * L; s2 += 2) acc = lse2f(acc, abt[s2]);
+        for (int s2 = 0; s2 <= 2 * L; s2 += 2) acc = lse2f(acc, abv(s2));
       } else {
-        for (int k = head[c]; k >= 0; k = next[k]) acc = lse2f(acc, abt[2 * k + 1]);
+        for (int k = head[c]; k >= 0; k = next[k]) acc = lse2f(acc, abv(2 * k + 1));
       }
       const float l = lp[(size_t)t * C + c];
       g = (__expf(l) - (acc == -INFINITY ? 0.f : __expf(acc - l - ll))) * scale;
@@ -433,10 +445,16 @@ int srf_ctc_loss(const float* logits, const int* labels, const int* label_len, c
                      blank, grad ? 1 : 0, nll, static_cast<float*>(workspace));
   SRF_LAUNCH_CHECK("ctc_recursion");
   if (grad) {
-    hipLaunchKernelGGL(ctc_grad_kernel, dim3(B, (Tmax + 15) / 16), dim3(256),
-                       (size_t)(C + Lmax + 16 * Smax) * sizeof(int),
-                       st, labels, label_len, logit_len, nll, Tmax, C, Lmax, blank, grad_scale,
-                       static_cast<const float*>(workspace), grad);
+    const size_t lists = (size_t)(C + Lmax) * sizeof(int);
+    SRF_REQUIRE(lists <= kCtcGradLds, "CTC: labels too long for the gradient kernel's LDS lists");
+    int fr = 16;
+    while (fr > 1 && lists + (size_t)fr * Smax * sizeof(float) > kCtcGradLds) fr >>= 1;
+    const bool stage = lists + (size_t)fr * Smax * sizeof(float) <= kCtcGradLds;
+    if (!stage) fr = 16;
+    hipLaunchKernelGGL(stage ? ctc_grad_kernel<true> : ctc_grad_kernel<false>, dim3(B, (Tmax + fr - 1) / fr),
+                       dim3(256), lists + (stage ? (size_t)fr * Smax * sizeof(float) : 0), st, labels, label_len,
+                       logit_len, nll, Tmax, C, Lmax, blank, grad_scale, fr, static_cast<const float*>(workspace),
+                       grad);
   }
   SRF_LAUNCH_CHECK("ctc");
   return SRF_OK;

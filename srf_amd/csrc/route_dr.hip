@@ -22,6 +22,7 @@
 #include "srf_common.h"
 #include "route_fwd32.h"
 #include "../../include/srf.h"
+#include "../../include/srf_prof.h"
 
 namespace {
 
@@ -1671,11 +1672,23 @@ inline bool use_fwd32(const Geom& g) {
 // Coupling storage is used when the split-bf16 forward runs and the gu pass from
 // stored couplings (route_gux_kernel) fits its window accumulator in LDS; otherwise
 // the forward keeps nothing and the backward recomputes (round-1 kernels).
+// The coupling readers address their blocks through buffer descriptors with 32-bit
+// byte ranges and 32-bit offsets (route_gux_kernel's c / gL blocks over all
+// iterations, route_gw3_kernel's per-iteration s and gs slices, the forward's
+// c / logZ stores): past 2^31 bytes the forward stores nothing and the backward
+// recomputes the logits instead of reading wrapped offsets.
+inline bool coupling_sizes_fit(const Geom& g) {
+  constexpr size_t kLim = size_t(1) << 31;
+  const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+  const size_t total = srf::fwd32_cpl_layout(plan, g.F(), g.in_n(), g.din, g.dout, g.J, g.iters).total;
+  return total * 4 < kLim && (size_t)g.F() * g.JD() * 4 * g.iters < kLim;
+}
+
 inline bool couplings_ok(const Geom& g) {
   if (!use_fwd32(g) || g.iters < 2 || g.din > 32) return false;
   const int TW = gu_tw(g.dout);
   const int nw = std::min(kGuNW, (g.NT() + TW - 1) / TW);
-  return gu_lds_bytes(g, nw, 1) <= kGuLdsMax;
+  return gu_lds_bytes(g, nw, 1) <= kGuLdsMax && coupling_sizes_fit(g);
 }
 
 

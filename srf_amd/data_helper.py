@@ -38,10 +38,77 @@ def create_ds_for_evaluation(config, logger):
     return test_ds.map(load_speech_data.map_data_for_transformer_utt_id_fn, config.feat_dim)
 
 
-def create_ds_for_training(config, logger, num_gpus, manual_bucket_batch_sizes=None, seed=None):
+def replica_slice(batch_size, rank, world):
+    """[lo, hi) of replica ``rank``'s share of a global batch: batch_size // world
+    utterances each, the first batch_size % world replicas one more, in order --
+    how tf.distribute rebatches a global batch over the replicas of
+    MirroredStrategy.experimental_distribute_dataset (trainer_sr.py:147-153,168)."""
+    if not 0 <= rank < world:
+        raise ValueError(f'rank {rank} outside world {world}')
+    q, r = divmod(batch_size, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def split_global_batch(batch, rank, world):
+    """Replica ``rank``'s sub-batch of one global batch (a tuple of arrays whose
+    first axis is the utterance).  Padding is left as the global batch had it:
+    process_train_step crops each replica to its own longest utterance
+    (trainer_sr.py:59-60), as the reference's replicas do."""
+    lo, hi = replica_slice(len(batch[0]), rank, world)
+    return tuple(c[lo:hi] for c in batch)
+
+
+def distribute_dataset(dataset, rank, world):
+    """strategy.experimental_distribute_dataset (trainer_sr.py:168) for one process
+    per GPU: every rank iterates the same global batches (same files, same shuffle
+    seed) and keeps its own slice.  The reference forces every bucket batch size
+    above num_gpus (train_helper.py:289-296,301-309), so no replica is empty."""
+    if world <= 1:
+        return dataset
+    return load_speech_data.Dataset(lambda: (split_global_batch(b, rank, world) for b in dataset))
+
+
+def _shared_seed(seed, world):
+    """All ranks must shuffle identically: an explicit seed, or rank 0's draw
+    broadcast over the process group."""
+    if seed is not None or world <= 1:
+        return seed
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        raise ValueError('create_ds_for_training with world > 1 needs a seed or an initialised process group')
+    t = torch.tensor([int(np.random.default_rng().integers(0, 2 ** 31 - 1))], dtype=torch.int64)
+    if dist.get_backend() == 'nccl':
+        t = t.cuda()
+    dist.broadcast(t, src=0)
+    return int(t.item())
+
+
+def _dist_rank():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def create_ds_for_training(config, logger, num_gpus, manual_bucket_batch_sizes=None, seed=None, rank=None,
+                           world=None):
     """data_helper.py:71-125: length-bucketed batches of ~train_batch_frame
     frames (buckets from get_bucket_info(frames, num_gpus, 241, 10000, 150)) or
-    fixed-size batches."""
+    fixed-size batches.
+
+    ``rank`` / ``world`` (defaults: the process-group rank, or 0, and one replica
+    per GPU, world = num_gpus) give the per-process view of MirroredStrategy's
+    distributed dataset: each yielded batch is this replica's slice of a global
+    batch (distribute_dataset)."""
+    world = num_gpus if world is None else world
+    rank = _dist_rank() if rank is None else rank
+    seed = _shared_seed(seed, world)
+    train_ds, valid_ds = _create_global(config, logger, num_gpus, manual_bucket_batch_sizes, seed)
+    return distribute_dataset(train_ds, rank, world), distribute_dataset(valid_ds, rank, world)
+
+
+def _create_global(config, logger, num_gpus, manual_bucket_batch_sizes, seed):
     train_file_ptrn = os.path.join(config.path_base, config.path_train_ptrn)
     valid_file_ptrn = os.path.join(config.path_base, config.path_valid_ptrn)
     if config.train_batch_dynamic:

@@ -31,6 +31,11 @@ BN_MOMENTUM = 0.99
 CNN_DROPOUT = 0.2   # hard-coded, sequence_router.py:62 and naive:82
 
 
+def _replica_id():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
 class SequenceRouter(torch.nn.Module):
     """SRF acoustic model.  ``config.model_caps_type`` picks the reference variant
     (trainer_sr.py:188-199); all three run on the same HIP kernels:
@@ -48,7 +53,7 @@ class SequenceRouter(torch.nn.Module):
 
     iter = -1  # class-level like the reference (naive:40,56): shared by every instance
 
-    def __init__(self, config, logger, class_n, device=None, seed=None):
+    def __init__(self, config, logger, class_n, device=None, seed=None, replica_id=None):
         super().__init__()
         dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
         self.stride = 2
@@ -83,7 +88,14 @@ class SequenceRouter(torch.nn.Module):
         self.length_eps = LENGTH_EPS_EINSUM if self.caps_type == 'einsum' else LENGTH_EPS
         self.dropout_enabled = True     # test hook: parity runs use BN batch stats without dropout
         self.n_chunks_override = {}     # layer -> n_chunks (tuning hook)
+        # Dropout seed base.  Parameters are initialised from `seed` identically on every
+        # replica (MirroredStrategy mirrors one set of variables), but each replica draws
+        # its own dropout masks, so the replica id is mixed in (rank 0 keeps the plain
+        # seed's stream).
         self._seed_base = int(np.random.default_rng(seed).integers(1, 2 ** 62))
+        self.replica_id = _replica_id() if replica_id is None else int(replica_id)
+        if self.replica_id:
+            self._seed_base = int(np.random.default_rng([self._seed_base, self.replica_id]).integers(1, 2 ** 62))
         self._calls = 0
 
         w = self.window

@@ -8,6 +8,8 @@ explicit RCCL all-reduce (SUM) of the model's flat gradient buffer -- with the
 loss scaled by 1/(B_local * n_gpus) as in trainer_sr.py:58,67-68 the sum is the
 global-batch mean.
 """
+from collections import OrderedDict
+
 import torch
 import torch.distributed as dist
 
@@ -117,40 +119,68 @@ def process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_s
     return pe_loss
 
 
+_SEED_COUNTERS = {}
+
+
+def seed_counter(dev):
+    """The process's device-resident dropout step counter on ``dev`` (one per
+    process, created once and never released: srf_set_seed_source is process-wide).
+    Every captured training step advances it, so graph replays draw fresh masks;
+    eager steps leave it alone and differ through their per-call seeds."""
+    dev = torch.device(dev)
+    c = _SEED_COUNTERS.get(dev)
+    if c is None:
+        from . import _lib
+        if _SEED_COUNTERS:
+            raise RuntimeError('one process drives one GPU: the dropout step counter already lives on '
+                               f'{next(iter(_SEED_COUNTERS))}')
+        c = torch.zeros(1, dtype=torch.int64, device=dev)
+        _lib.check(_lib.lib().srf_set_seed_source(c.data_ptr()), 'srf_set_seed_source')
+        _SEED_COUNTERS[dev] = c
+    return c
+
+
+def _label_capacity(L):
+    return max(8, -(-int(L) // 8) * 8)
+
+
 class GraphedTrainStep:
     """process_train_step with its forward, CTC loss head and backward captured
-    into one hipGraph (torch.cuda.CUDAGraph) for a fixed batch shape; the gradient
-    all-reduce, the Adam update and the metrics run eagerly after each replay.
+    into one hipGraph (torch.cuda.CUDAGraph) for one batch shape (B utterances
+    cropped to T frames); the gradient all-reduce, the Adam update and the
+    metrics run eagerly after each replay.
 
     The ~110 kernel launches of a step then cost one graph launch on the host, so
     the step is bound by the GPU, not by Python/ctypes launch overhead (which
     grows when several ranks share a host).  Dropout stays random per step: the
-    captured step first advances a device-resident step counter that every dropout
-    kernel mixes into its seed (srf_set_seed_source).
+    captured step first advances the process's device step counter
+    (seed_counter), which every dropout kernel mixes into its seed.
 
-    The graph reads the static tensors ``self.feats`` (cropped to max(inp_len),
-    which may be a private copy of the caller's feats), ``self.labels``,
-    ``self.inp_len`` (device copy) and ``self.tar_len``, not the caller's
-    ``inputs``.  Feed a new batch of the same shape and lengths with
-    ``refill(...)``, which copies into those tensors and refuses any other shape
-    or lengths.
+    Every per-batch quantity the kernels read is device-resident: ``self.feats``
+    [B, T, F], ``self.labels`` [B, label_capacity] (zero-padded past tar_len),
+    ``self.inp_len`` / ``self.tar_len`` [B] int32; the logit lengths
+    ceil(inp_len / 4) are computed inside the graph.  ``refill(...)`` copies any
+    batch of the same B and T (max(inp_len) == T, trainer_sr.py:59-60) with at most
+    label_capacity labels into them; utterance lengths and label lengths may differ
+    from the captured batch.
     """
 
-    def __init__(self, in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=2):
-        from . import _lib
+    def __init__(self, in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=2, label_capacity=None):
         self.model, self.optimizer = model, optimizer
         self.in_len_div, self.n_gpus, self.blank_idx = in_len_div, n_gpus, blank_idx
         feats, labels, inp_len, tar_len = inputs
         dev = feats.device
         self.batch = feats.shape[0]
-        self.host_len = inp_len
-        self.feats = _crop(feats, inp_len)
-        self.labels, self.tar_len = labels, tar_len
-        self.inp_len = inp_len.to(dev)
-        self.logit_len = ceil_div(self.inp_len, in_len_div)
-        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
-        rc = _lib.lib().srf_set_seed_source(self.counter.data_ptr())
-        _lib.check(rc, 'srf_set_seed_source')
+        host_len = torch.as_tensor(inp_len)
+        self.T = int(host_len.max())
+        self.host_len = host_len.cpu()
+        self.label_capacity = _label_capacity(labels.shape[1] if label_capacity is None else label_capacity)
+        self.feats = torch.zeros((self.batch, self.T, feats.shape[2]), dtype=torch.float32, device=dev)
+        self.labels = torch.zeros((self.batch, self.label_capacity), dtype=torch.int32, device=dev)
+        self.inp_len = torch.zeros(self.batch, dtype=torch.int32, device=dev)
+        self.tar_len = torch.zeros(self.batch, dtype=torch.int32, device=dev)
+        self.refill(feats, labels, inp_len, tar_len)
+        self.counter = seed_counter(dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
@@ -161,38 +191,43 @@ class GraphedTrainStep:
         with torch.cuda.graph(self.graph):
             self.nll = self._fwd_bwd()
 
+    def accepts(self, feats, labels, inp_len):
+        return (feats.shape[0] == self.batch and int(torch.as_tensor(inp_len).max()) == self.T
+                and labels.shape[1] <= self.label_capacity)
+
     def refill(self, feats, labels, inp_len, tar_len):
         """Copy a new batch into the tensors the captured graph reads."""
-        if not torch.equal(torch.as_tensor(inp_len).cpu().to(torch.int64),
-                           torch.as_tensor(self.host_len).cpu().to(torch.int64)):
-            raise ValueError('GraphedTrainStep.refill: input lengths differ from the captured batch')
-        feats = feats[:, :self.feats.shape[1], :]
-        for dst, src, what in ((self.feats, feats, 'feats'), (self.labels, labels, 'labels'),
-                               (self.tar_len, tar_len, 'tar_len')):
-            if tuple(src.shape) != tuple(dst.shape):
-                raise ValueError(f'GraphedTrainStep.refill: {what} shape {tuple(src.shape)} != {tuple(dst.shape)}')
-            dst.copy_(src, non_blocking=True)
+        host_len = torch.as_tensor(inp_len)
+        if feats.shape[0] != self.batch or int(host_len.max()) != self.T:
+            raise ValueError(f'GraphedTrainStep.refill: batch of {feats.shape[0]} utterances cropped to '
+                             f'{int(host_len.max())} frames, the graph runs {self.batch} x {self.T}')
+        if labels.shape[1] > self.label_capacity:
+            raise ValueError(f'GraphedTrainStep.refill: {labels.shape[1]} labels exceed the capacity '
+                             f'{self.label_capacity}')
+        self.host_len = host_len.cpu()
+        self.feats.copy_(torch.as_tensor(feats)[:, :self.T, :], non_blocking=True)
+        self.labels[:, labels.shape[1]:].zero_()
+        self.labels[:, :labels.shape[1]].copy_(torch.as_tensor(labels), non_blocking=True)
+        self.inp_len.copy_(host_len, non_blocking=True)
+        self.tar_len.copy_(torch.as_tensor(tar_len), non_blocking=True)
 
     def _fwd_bwd(self):
         self.counter.add_(1)
         y_pred = self.model(self.feats, input_lengths=self.inp_len, training=True)
-        pe_loss, g_logits = ctc.ctc_loss_and_grad(self.labels, y_pred, self.tar_len, self.logit_len, self.blank_idx,
+        logit_len = ceil_div(self.inp_len, self.in_len_div)
+        pe_loss, g_logits = ctc.ctc_loss_and_grad(self.labels, y_pred, self.tar_len, logit_len, self.blank_idx,
                                                   1.0 / float(self.batch * self.n_gpus))
         y_pred.backward(g_logits)
         return pe_loss
 
-    def close(self):
-        """Detach the dropout kernels from this step's counter (before it is freed)."""
-        from . import _lib
-        if getattr(self, 'counter', None) is not None:
-            _lib.lib().srf_set_seed_source(None)
-            self.counter = None
+    @property
+    def logit_len(self):
+        return ceil_div(self.inp_len, self.in_len_div)
 
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+    def close(self):
+        """Release the graph (its private memory pool goes with it).  The process's
+        step counter stays attached: other graphs and models keep using it."""
+        self.graph = None
 
     def __call__(self, loss_state=None, frame_state=None, samples=None):
         self.graph.replay()
@@ -205,6 +240,79 @@ class GraphedTrainStep:
         if samples is not None:
             samples.update_state(self.batch)
         return self.nll
+
+
+class GraphCache:
+    """One GraphedTrainStep per batch shape (B, T), least recently used evicted
+    past ``max_graphs``.  Bucketed batches (load_speech_data.create_ds_bucket) come
+    in a bounded set of shapes; a new label length beyond a cached graph's capacity
+    re-captures that shape with a larger one."""
+
+    def __init__(self, in_len_div, model, optimizer, n_gpus, blank_idx, max_graphs=32, warmup=1):
+        self.args = (in_len_div, model, optimizer, n_gpus, blank_idx)
+        self.max_graphs, self.warmup = max_graphs, warmup
+        self.graphs = OrderedDict()
+        self.captures = 0
+
+    def step(self, inputs, loss_state=None, frame_state=None, samples=None):
+        feats, labels, inp_len, tar_len = inputs
+        key = (feats.shape[0], int(torch.as_tensor(inp_len).max()))
+        g = self.graphs.get(key)
+        if g is not None and not g.accepts(feats, labels, inp_len):
+            g.close()
+            del self.graphs[key]
+            g = None
+        if g is None:
+            in_len_div, model, optimizer, n_gpus, blank_idx = self.args
+            g = GraphedTrainStep(in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=self.warmup)
+            self.captures += 1
+            self.graphs[key] = g
+            while len(self.graphs) > self.max_graphs:
+                _, old = self.graphs.popitem(last=False)
+                old.close()
+        else:
+            g.refill(feats, labels, inp_len, tar_len)
+            self.graphs.move_to_end(key)
+        return g(loss_state, frame_state, samples)
+
+
+def batch_to_device(batch, dev):
+    """A dataset batch (numpy: feats [B,T,F] f32, labels [B,L], inp_len [B],
+    tar_len [B]) as process_train_step takes it: feats / labels / tar_len on the
+    device, inp_len host-resident (the crop needs no device sync)."""
+    feats, labels, inp_len, tar_len = batch[:4]
+    pin = torch.device(dev).type == 'cuda'
+
+    def dev_t(a, dtype):
+        t = torch.as_tensor(a).to(dtype)
+        return (t.pin_memory() if pin else t).to(dev, non_blocking=True)
+    return (dev_t(feats, torch.float32), dev_t(labels, torch.int32), torch.as_tensor(inp_len).to(torch.int32),
+            dev_t(tar_len, torch.int32))
+
+
+def distributed_train_step(dataset, in_len_div, model, optimizer, loss_state, frame_state, n_gpus, blank_idx,
+                           samples, train_num=None, graphs=None, log=print):
+    """trainer_sr.py:205-222 (the hot loop): every batch of this replica's
+    dataset (data_helper.create_ds_for_training(..., rank, world)) through one
+    training step, with the reference's progress line every 50 steps.  ``graphs``
+    (a GraphCache) replays a captured step per batch shape; None runs
+    process_train_step eagerly."""
+    dev = model.flat_params.device
+    index = 0
+    if log is not None:
+        log('Step, Progress%, Average Loss, lr')
+    for example in dataset:
+        inputs = batch_to_device(example, dev)
+        if graphs is None:
+            process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_state, n_gpus, blank_idx,
+                               samples)
+        else:
+            graphs.step(inputs, loss_state, frame_state, samples)
+        if index % 50 == 0 and index > 0 and log is not None:
+            prog = samples.result() / train_num * 100 if train_num else float('nan')
+            log('STEP', optimizer.iterations, prog, loss_state.result(), optimizer.current_lr())
+        index += 1
+    return index
 
 
 @torch.no_grad()

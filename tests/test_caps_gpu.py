@@ -124,10 +124,14 @@ def test_ctc_infeasible_is_inf_with_zero_grad(cuda):
 
 
 @pytest.mark.parametrize('B,T,C,L,wave', [(3, 150, 12, 70, '0'), (2, 420, 32, 200, '0'), (3, 150, 12, 70, '1'),
-                                          (2, 420, 32, 200, '1'), (2, 90, 63, 40, '1')])
+                                          (2, 420, 32, 200, '1'), (2, 90, 63, 40, '1'),
+                                          (1, 2100, 32, 1000, '1'),    # gradient stages 4 frames per block
+                                          (1, 11300, 8, 5600, '0')])   # gradient reads alpha/beta from HBM
 def test_ctc_long_labels_cross_state_groups(cuda, B, T, C, L, wave, monkeypatch):
     """Extended-label lengths past 64 states exercise the group boundaries of the
-    wave-resident recursion (KM = 4, 8); SRF_CTC_WAVE=0 runs the block loop."""
+    wave-resident recursion (KM = 4, 8); SRF_CTC_WAVE=0 runs the block loop.  The
+    longest cases exceed the gradient kernel's 16-frame LDS staging (fewer frames
+    per block, then no staging)."""
     from srf_amd import ops
     monkeypatch.setenv('SRF_CTC_WAVE', wave)
     rng = np.random.default_rng(B * 1000 + T)
@@ -147,6 +151,13 @@ def test_ctc_long_labels_cross_state_groups(cuda, B, T, C, L, wave, monkeypatch)
     got = nll.detach().cpu().double().numpy()
     assert np.all(np.abs(got - ref.detach().numpy()) <= 1e-4 * np.maximum(1, np.abs(ref.detach().numpy()))), got
     nll.sum().backward()
-    # fp32 log-space recursions over T frames: gradient entries agree to 2e-6 * T absolute
+    # fp32 log-space recursions over T frames: gradient entries agree to 2e-6 * T
+    # absolute, or to twice the error of torch's own fp32 CTC (whose rounding grows
+    # with the log-likelihood's magnitude over very long utterances)
+    lr32 = torch.tensor(logits, dtype=torch.float32, requires_grad=True)
+    torch.nn.functional.ctc_loss(torch.log_softmax(lr32, -1).transpose(0, 1), torch.tensor(labels).long(),
+                                 torch.tensor(logit_len).long(), torch.tensor(lab_len).long(), blank=C - 1,
+                                 reduction='none').sum().backward()
+    e32 = (lr32.grad.double() - lr.grad).abs().max().item()
     e = (lg.grad.cpu().double() - lr.grad).abs().max().item()
-    assert e < 2e-6 * T, e
+    assert e < max(2e-6 * T, 2 * e32), (e, e32)

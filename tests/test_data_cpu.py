@@ -276,3 +276,42 @@ def test_data_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert declared == set(lsd.exported_symbols())
+
+
+def test_replica_slices_cover_the_global_batch_in_order():
+    """tf.distribute rebatching (trainer_sr.py:147-153,168): B // world each, the
+    first B % world replicas one more, contiguous and in order."""
+    for B in range(1, 40):
+        for world in (1, 2, 3, 4, 8):
+            sl = [data_helper.replica_slice(B, r, world) for r in range(world)]
+            assert sl[0][0] == 0 and sl[-1][1] == B
+            assert all(a[1] == b[0] for a, b in zip(sl, sl[1:]))
+            sizes = [hi - lo for lo, hi in sl]
+            assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+    assert [hi - lo for lo, hi in (data_helper.replica_slice(17, r, 8) for r in range(8))] == [3] + [2] * 7
+
+
+def test_training_datasets_split_per_replica(tmp_path):
+    """create_ds_for_training(..., rank, world): every rank sees the same global
+    batch sequence (shared shuffle seed) and keeps its own slice; the slices of all
+    ranks rebuild each global batch, padded like it (each replica crops later)."""
+    from srf_amd.common_helper import build_parser
+    _write_corpus(tmp_path, 60, 3, shards=2, seed=6)
+    cfg = build_parser().parse_args([])
+    cfg.path_base = str(tmp_path)
+    cfg.path_train_ptrn = cfg.path_valid_ptrn = 'tfr/*'
+    cfg.feat_dim = 3
+    cfg.train_batch_dynamic = True
+    cfg.train_batch_frame = 1400
+    world = 2
+    glob_train, _ = data_helper.create_ds_for_training(cfg, None, world, seed=3, rank=0, world=1)
+    parts = [data_helper.create_ds_for_training(cfg, None, world, seed=3, rank=r)[0] for r in range(world)]
+    glob = list(glob_train)
+    per_rank = [list(p) for p in parts]
+    assert len(glob) > 0 and all(len(p) == len(glob) for p in per_rank)
+    for k, g in enumerate(glob):
+        assert g[0].shape[0] > world     # bucket sizes are forced above num_gpus
+        for comp in range(4):
+            np.testing.assert_array_equal(np.concatenate([p[k][comp] for p in per_rank]), g[comp])
+    with pytest.raises(ValueError):
+        data_helper.create_ds_for_training(cfg, None, world, seed=None, rank=0)

@@ -11,14 +11,18 @@ import numpy as np
 import pytest
 import torch
 
-from tests.helpers import config_from_shape, load_model_fixture
+from tests.helpers import config_from_shape, gradient_mismatches, load_model_fixture
 
 pytestmark = pytest.mark.gpu
 
 DR_FIXTURES = ['c1_mini', 'c2_mini', 'c3_mini_sdr',   # c3: SDR routing
                'c4_mini',                                # DR at DIM 32 (C3/C4 capsule width)
                # the einsum / lowmemory variants (trainer_sr.py:188-199)
-               'c2_mini_einsum', 'c2_mini_lowmemory', 'c3_mini_sdr_lowmemory']
+               'c2_mini_einsum', 'c2_mini_lowmemory', 'c3_mini_sdr_lowmemory',
+               # BASELINE's real configurations (oracle/gen_golden.py BIG_CASES): C2 as the
+               # bench runs it (B=17, T=320, ragged), C4 / C3 at L=6 PH=CH=16 DIM=32,
+               # C5 at L=8 DIM=64 LPAD=RPAD=20 with 5 SDR iterations
+               'c2_full', 'c4_real', 'c3_real', 'c5_real']
 
 
 def _build(name, dev):
@@ -61,16 +65,7 @@ def test_gradients(cuda, name):
     nll = ctc.ctc_loss(torch.tensor(z['labels'], device=cuda), logits, torch.tensor(z['tar_len'], device=cuda),
                        (inp_len + 3) // 4, blank_index=sh.class_n - 1)
     (nll.sum() / feats.shape[0]).backward()
-    bad = []
-    for key in z:
-        if not key.startswith('grad.'):
-            continue
-        pname = key[5:].replace('.', '_')
-        ref = z[key].astype(np.float64)
-        got = model.P(pname).grad.detach().cpu().double().numpy()
-        err = np.abs(got - ref).max()
-        if err > 2e-3 * np.abs(ref).max() + 1e-5:
-            bad.append((pname, err, np.abs(ref).max()))
+    bad = gradient_mismatches(z, lambda p: model.P(p).grad.detach().cpu().double().numpy())
     assert not bad, bad
 
 

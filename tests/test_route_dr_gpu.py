@@ -173,3 +173,34 @@ def test_row_tiles_per_wave_plans_match(cuda, case, var, monkeypatch):
     assert np.all(np.abs(a - b) <= 1e-5 * (1 + np.abs(b))), np.abs(a - b).max()
     for x, y, name in zip(outs[0][1:], outs[1][1:], ('g_emb', 'g_W', 'g_bias')):
         assert np.abs(x - y).max() <= 2e-5 * max(1.0, np.abs(y).max()), (name, np.abs(x - y).max())
+
+
+@pytest.mark.parametrize('case', [(2, 37, 8, 16, 4, 4, 63, 3, True), (2, 23, 16, 32, 2, 2, 16, 3, False),
+                                  (2, 21, 4, 8, 2, 1, 12, 3, False)])
+def test_route_dr_skewed_operand_magnitudes(cuda, case):
+    """The split-fp16 pose scales each operand tensor by one power of two
+    (route_fwd32.hip prep32_kernel), so rows far below the tensor's maximum land in
+    fp16's subnormal range.  W rows (per input capsule i, output capsule j) and
+    emb frames spanning 2^-20 .. 2^4, with all-zero padded frames, against the
+    fp64 oracle: forward and gradients at the layer tests' tolerances."""
+    B, T, N, D, lp, rp, J, it, mf = case
+    emb, W, bias = _mk(case, 12)
+    rng = np.random.default_rng(13)
+    W = W * np.exp2(rng.uniform(-20, 4, size=W.shape[:2]))[:, :, None, None]
+    emb = emb * np.exp2(rng.uniform(-20, 4, size=(B, T)))[:, :, None, None]
+    emb[:, T - 3:] = 0.0                               # padded frames
+    emb[0, 1] *= 0.0
+    te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
+    ref = so.dynamic_routing(so.pose(so.window(emb, lp, rp), W, bias), it, mf)
+    got = v.detach().cpu().double().numpy()
+    assert np.all(np.abs(got - ref) <= 2e-5 * (1 + np.abs(ref))), np.abs(got - ref).max()
+    gv = rng.standard_normal(v.shape)
+    v.backward(torch.tensor(gv, dtype=torch.float32, device=cuda))
+    ce, cW, cb = (torch.tensor(a, requires_grad=True) for a in (emb, W, bias))
+    ep = torch.nn.functional.pad(ce, (0, 0, 0, 0, lp, rp))
+    xw = torch.cat([ep[:, w:w + T] for w in range(lp + rp + 1)], dim=2)
+    nm.dynamic_routing(nm.pose_tiled(xw, cW, cb), it, mf).backward(torch.tensor(gv))
+    for name, g, r in (('g_emb', te.grad, ce.grad), ('g_W', tW.grad, cW.grad), ('g_bias', tb.grad, cb.grad)):
+        g, r = g.cpu().double().numpy(), r.numpy()
+        err = np.abs(g - r).max()
+        assert err <= 1e-4 * max(1.0, np.abs(r).max()), (name, err, np.abs(r).max())
