@@ -12,8 +12,10 @@ Every tensor is stored under the key TF2's object-based checkpoint would give
 it (``model/<attribute path>/.ATTRIBUTES/VARIABLE_VALUE``, optimizer slots as
 ``.../.OPTIMIZER_SLOT/optimizer/{m,v}/...``), following the attribute names of
 sequence_router_naive.py:68-118 and sequence_router.py:44-63, so a checkpoint
-converts to or from a TF bundle by renaming nothing.  Files are safetensors
-(``ckpt-N.srf.safetensors``); tf_bundle.py reads TF's own bundles.
+converts to or from a TF bundle by renaming nothing.  Files are TF TensorBundles
+by default -- ``ckpt-N.index`` + ``ckpt-N.data-00000-of-00001``, the layout
+tf.train.CheckpointManager writes, through tf_bundle.py -- or safetensors
+(``ckpt-N.srf.safetensors``, ``fmt='safetensors'``); readers take either.
 
 Parity note: TensorFlow is not installed here, so the key scheme restates TF2's
 documented object-path convention; no TF-written checkpoint ships in the
@@ -153,10 +155,14 @@ class CheckpointManager:
     exists therefore writes ckpt-4 next, as TF does."""
 
     SUFFIX = '.srf.safetensors'
+    FORMATS = ('tf', 'safetensors')
 
-    def __init__(self, model, optimizer, directory, max_to_keep=5):
+    def __init__(self, model, optimizer, directory, max_to_keep=5, fmt='tf'):
+        if fmt not in self.FORMATS:
+            raise ValueError(f'checkpoint format must be one of {self.FORMATS}')
         self.model, self.optimizer, self.directory = model, optimizer, directory
         self.max_to_keep = max_to_keep
+        self.fmt = fmt
         self.save_counter = 0
         os.makedirs(directory, exist_ok=True)
         self._ckpts = self._read_state()
@@ -174,7 +180,7 @@ class CheckpointManager:
         if not os.path.exists(path):
             return []
         names = re.findall(r'all_model_checkpoint_paths:\s*"([^"]+)"', open(path).read())
-        return [n for n in names if os.path.exists(os.path.join(self.directory, n) + self.SUFFIX)]
+        return [n for n in names if checkpoint_files(os.path.join(self.directory, n))]
 
     def _write_state(self):
         lines = []
@@ -194,17 +200,39 @@ class CheckpointManager:
         if self.optimizer is not None:
             state.update(optimizer_state(self.model, self.optimizer))
         state[SAVE_COUNTER] = np.array(self.save_counter, np.int64)
-        save_file(state, os.path.join(self.directory, name) + self.SUFFIX)
+        prefix = os.path.join(self.directory, name)
+        for f in checkpoint_files(prefix):   # re-saving a number replaces it in either format
+            os.remove(f)
+        if self.fmt == 'tf':
+            from . import tf_bundle
+            tf_bundle.save_checkpoint(prefix, state)
+        else:
+            save_file(state, prefix + self.SUFFIX)
         self._ckpts = [c for c in self._ckpts if c != name] + [name]
         if self.max_to_keep is not None and self.max_to_keep > 0:
             while len(self._ckpts) > self.max_to_keep:
                 old = self._ckpts.pop(0)
-                os.remove(os.path.join(self.directory, old) + self.SUFFIX)
+                for f in checkpoint_files(os.path.join(self.directory, old)):
+                    os.remove(f)
         self._write_state()
-        return os.path.join(self.directory, name)
+        return prefix
+
+
+def checkpoint_files(prefix):
+    """The files of checkpoint ``prefix`` on disk (TF bundle or safetensors), [] if none."""
+    import glob
+    if os.path.exists(prefix + '.index'):
+        return [prefix + '.index'] + sorted(glob.glob(glob.escape(prefix) + '.data-*-of-*'))
+    if os.path.exists(prefix + CheckpointManager.SUFFIX):
+        return [prefix + CheckpointManager.SUFFIX]
+    return []
 
 
 def read_checkpoint(prefix):
+    """{TF key: array} of checkpoint ``prefix``, from a TF bundle (``.index``) or safetensors."""
+    if os.path.exists(prefix + '.index'):
+        from . import tf_bundle
+        return tf_bundle.load_checkpoint(prefix)
     return load_file(prefix + CheckpointManager.SUFFIX)
 
 

@@ -6,6 +6,7 @@ import argparse
 import os
 
 import numpy as np
+import pytest
 import torch
 
 from srf_amd import checkpoint as ck
@@ -53,18 +54,26 @@ def test_tf_shapes_per_variant():
         assert torch.equal(m2.params['b1'], m.params['b1'])
 
 
-def test_manager_save_restore_rotation(tmp_path):
+@pytest.mark.parametrize('fmt', ['tf', 'safetensors'])
+def test_manager_save_restore_rotation(tmp_path, fmt):
     m, opt = _model(1), SrfAdam(CustomSchedule(0.5, 1, 1200))
     opt._m = torch.randn(m.n_flat)
     opt._v = torch.rand(m.n_flat)
     opt.iterations = 17
-    mgr = ck.CheckpointManager(m, opt, str(tmp_path), max_to_keep=2)
+    mgr = ck.CheckpointManager(m, opt, str(tmp_path), max_to_keep=2, fmt=fmt)
     for _ in range(3):
         with torch.no_grad():
             m.flat_params.add_(1.0)
         path = mgr.save()
     assert path.endswith('ckpt-3') and mgr.latest_checkpoint == path
-    assert sorted(os.listdir(tmp_path)) == ['checkpoint', 'ckpt-2.srf.safetensors', 'ckpt-3.srf.safetensors']
+    if fmt == 'tf':   # tf.train.CheckpointManager's file layout (the default)
+        assert sorted(os.listdir(tmp_path)) == ['checkpoint', 'ckpt-2.data-00000-of-00001', 'ckpt-2.index',
+                                                'ckpt-3.data-00000-of-00001', 'ckpt-3.index']
+        from srf_amd import tf_bundle
+        names = {n for n, _, _ in tf_bundle.list_variables(str(tmp_path / 'ckpt-3'))}
+        assert 'model/wgt/0/' + ck.VALUE in names and ck.SAVE_COUNTER in names
+    else:
+        assert sorted(os.listdir(tmp_path)) == ['checkpoint', 'ckpt-2.srf.safetensors', 'ckpt-3.srf.safetensors']
     state_file = open(tmp_path / 'checkpoint').read()
     assert 'model_checkpoint_path: "ckpt-3"' in state_file and 'all_model_checkpoint_paths: "ckpt-2"' in state_file
     m2, opt2 = _model(2), SrfAdam(CustomSchedule(0.5, 1, 1200))
