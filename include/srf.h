@@ -118,6 +118,39 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
                       float* g_emb, float* g_W, float* g_bias, void* workspace, size_t workspace_bytes,
                       void* stream);
 
+/* ---- The SDR layer in frame ranges (the layer-pipelined SDR stack) ----------
+ * srf_route_sdr_fwd/bwd split into calls over frames [t0, t1) of every utterance,
+ * so a host can run an SDR stack as a wavefront over (layer, frame range): layer
+ * l's range k needs only layer l-1's output up to frame t1 - 1 + rpad (the window,
+ * naive:150-151), and, going backward, layer l+1's gx down to frame t0 - rpad.
+ * Same arithmetic as the whole-layer calls (naive:162-170, 212-245 and autodiff).
+ *   u / gu buffers hold frames [v0, v0 + vn) / [g0, g0 + gn) of each utterance,
+ *   laid out [B][vn][in_n][J*dout] (v0 = 0, vn = T: the whole layer);
+ *   v_out, v_saved, g_v are whole [B][T][J*dout];
+ *   recur_fwd starts from v_out[t0 - 1] (0 at t0 = 0): earlier ranges first;
+ *   recur_bwd walks t1-1 .. t0, carry [B][J*dout] holds dL/dv_{t1-1} on entry
+ *   (zero it before the last range) and dL/dv_{t0-1} on return: later ranges first;
+ *   gx adds W^T gu of the range's frames into g_emb through the window adjoint
+ *   (zero g_emb first); gw writes (accumulate = 0) or adds the range's
+ *   gW = sum_f gu x^T and g_bias = sum_f gu.
+ * recur_workspace: state slices for shapes beyond the register / LDS budget (0 else). */
+int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                       int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream);
+size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters);
+int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
+                            int mask_first, int t0, int t1, float* v_out, void* workspace, size_t workspace_bytes,
+                            void* stream);
+int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved, const float* g_v, int B, int T,
+                            int in_n, int J, int dout, int iters, int mask_first, int t0, int t1, float* carry,
+                            float* gu, int g0, int gn, void* workspace, size_t workspace_bytes, void* stream);
+/* W [in_n][J*dout][din] -> WT [in_n][din][J*dout] (the gx operand). */
+int srf_route_sdr_transpose_w(const float* W, int in_n, int J, int dout, int din, float* WT, void* stream);
+int srf_route_sdr_gx(const float* gu, int g0, int gn, const float* WT, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int t0, int t1, float* g_emb, void* stream);
+int srf_route_sdr_gw(const float* gu, int g0, int gn, const float* emb, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int t0, int t1, int accumulate, float* g_W, float* g_bias,
+                     void* stream);
+
 /* ---- CNN front end (CapsulationLayer, tfsr/model/sequence_router.py:44-82) ---
  * feats [B][T][feat_dim] fp32 (already cropped to max(inp_len), trainer_sr.py:59-60),
  * inp_len [B] int32 (device).  Kernels [3][3][Cin][64] (kh, kw, cin, cout), as the
@@ -189,6 +222,19 @@ int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const flo
 int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
                      unsigned long long seed, int layer, const float* stat, const float* g_y, float* g_x,
                      float* g_gamma, float* g_beta, void* workspace, size_t workspace_bytes, void* stream);
+/* capsnorm over the rows (b, t), t in [t0, t1), of every utterance of a [B][T] batch
+ * (same masks and arithmetic as the whole call).  The backward writes g_x rows and
+ * gpart rows [B*T][2n] (per-row gamma / beta gradient terms); once every range is
+ * done, srf_capsnorm_bwd_params sums gpart into g_gamma / g_beta. */
+int srf_capsnorm_fwd_range(const float* x, int B, int T, int t0, int t1, int n, const float* gamma, const float* beta,
+                           int training, float p, unsigned long long seed, int layer, float* y, float* stat,
+                           void* stream);
+int srf_capsnorm_bwd_range(const float* x, int B, int T, int t0, int t1, int n, const float* gamma, const float* beta,
+                           int training, float p, unsigned long long seed, int layer, const float* stat,
+                           const float* g_y, float* g_x, float* gpart, void* stream);
+size_t srf_capsnorm_params_workspace(int F, int n);
+int srf_capsnorm_bwd_params(const float* gpart, int F, int n, float* g_gamma, float* g_beta, void* workspace,
+                            size_t workspace_bytes, void* stream);
 int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
                       const float* gamma_out, const float* beta_out, int training, float p, unsigned long long seed,
                       int layer, float* logits, float* stat, float* lens, void* stream);

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-check}
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/ -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} \
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} ${PYTEST_K:+-k "$PYTEST_K"} \
   > $OUT/pytest.log 2>&1
 rc=$?
 tail -30 $OUT/pytest.log

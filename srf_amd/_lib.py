@@ -35,6 +35,14 @@ _SIGNATURES = {
     'srf_route_sdr_bwd_workspace': (_c_size, [_c_int] * 9),
     'srf_route_sdr_fwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _vp, _vp, _c_size, _vp]),
     'srf_route_sdr_bwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
+    'srf_route_sdr_pose': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _c_int, _c_int, _vp]),
+    'srf_route_sdr_recur_workspace': (_c_size, [_c_int] * 5),
+    'srf_route_sdr_recur_fwd': (_c_int, [_vp] + [_c_int] * 11 + [_vp, _vp, _c_size, _vp]),
+    'srf_route_sdr_recur_bwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp] + [_c_int] * 9 + [_vp, _vp, _c_int, _c_int,
+                                                                                         _vp, _c_size, _vp]),
+    'srf_route_sdr_transpose_w': (_c_int, [_vp] + [_c_int] * 4 + [_vp, _vp]),
+    'srf_route_sdr_gx': (_c_int, [_vp, _c_int, _c_int, _vp] + [_c_int] * 10 + [_vp, _vp]),
+    'srf_route_sdr_gw': (_c_int, [_vp, _c_int, _c_int, _vp] + [_c_int] * 11 + [_vp, _vp, _vp]),
     'srf_cnnfe_out_dims': (_c_int, [_c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
     'srf_cnnfe_saved_bytes': (_c_size, [_c_int] * 4),
     'srf_cnnfe_fwd_workspace': (_c_size, [_c_int] * 4),
@@ -61,6 +69,12 @@ _SIGNATURES = {
                                   _vp, _vp, _vp]),
     'srf_capsnorm_bwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong, _c_int]
                          + [_vp] * 6 + [_c_size, _vp]),
+    'srf_capsnorm_fwd_range': (_c_int, [_vp] + [_c_int] * 5 + [_vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong,
+                                                             _c_int, _vp, _vp, _vp]),
+    'srf_capsnorm_bwd_range': (_c_int, [_vp] + [_c_int] * 5 + [_vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong,
+                                                             _c_int, _vp, _vp, _vp, _vp, _vp]),
+    'srf_capsnorm_params_workspace': (_c_size, [_c_int] * 2),
+    'srf_capsnorm_bwd_params': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _vp, _c_size, _vp]),
     'srf_caps_head_fwd': (_c_int, [_vp, _c_int, _c_int, _c_int] + [_vp] * 4 + [_c_int, ctypes.c_float,
                                                                               ctypes.c_ulonglong, _c_int]
                           + [_vp] * 4),

@@ -511,6 +511,17 @@ __global__ __launch_bounds__(256) void encaps_bwd_b_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------- LN + dropout
+// Frames of a row map: workgroup q handles row f = b*T + t0 + (q - b*nt), b = q / nt
+// (frames [t0, t0 + nt) of every utterance; {T, 0, T} is every row, f = q).
+struct RowMap {
+  int T, t0, nt;
+  __device__ __forceinline__ int row(int q) const {
+    const int b = q / nt;
+    return b * T + t0 + (q - b * nt);
+  }
+  static RowMap all(int F) { return RowMap{F, 0, F}; }
+};
+
 // y = drop(LN(x)) over vectors of length n (one frame per workgroup); also the
 // output head: logits = LN_out(length_D(drop(LN_mid(v)))) when head != 0.
 __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restrict__ x, int n,
@@ -521,12 +532,12 @@ __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restri
                                                            int J, int D, const float* __restrict__ gamma_o,
                                                            const float* __restrict__ beta_o,
                                                            float* __restrict__ logits, float* __restrict__ lens,
-                                                           float len_eps) {
+                                                           float len_eps, RowMap rmap) {
   seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* v = sm;           // n
   float* red = v + n;      // 8
-  const int f = blockIdx.x;
+  const int f = rmap.row(blockIdx.x);
   float s1 = 0.f, dummy = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const float a = x[(size_t)f * n + i];
@@ -590,13 +601,13 @@ __global__ __launch_bounds__(256) void capsnorm_bwd_kernel(
     const float* __restrict__ x, int n, const float* __restrict__ gamma, const float* __restrict__ beta,
     int training, float p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream, const float* __restrict__ stat,
     const float* __restrict__ g_in, int head, int J, int D, const float* __restrict__ gamma_o,
-    const float* __restrict__ lens, float* __restrict__ g_x, float* __restrict__ gpart) {
+    const float* __restrict__ lens, float* __restrict__ g_x, float* __restrict__ gpart, RowMap rmap) {
   seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* gy = sm;          // n
   float* red = gy + n;     // 8
   float* gl = red + 8;     // J
-  const int f = blockIdx.x;
+  const int f = rmap.row(blockIdx.x);
   const float mean = stat[4 * f], rstd = stat[4 * f + 1];
   const size_t stride = head ? (size_t)2 * n + 2 * J : (size_t)2 * n;
   if (head) {
@@ -862,9 +873,53 @@ int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const flo
   SRF_REQUIRE(x && gamma && beta && y && stat && F > 0 && n > 0 && n <= kMaxVec, "bad capsnorm arguments");
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, static_cast<hipStream_t>(stream),
                      x, n, gamma, beta, training, p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0,
-                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr, kLengthEps);
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr, kLengthEps,
+                     RowMap::all(F));
   SRF_LAUNCH_CHECK("capsnorm_fwd");
   return SRF_OK;
+}
+
+int srf_capsnorm_fwd_range(const float* x, int B, int T, int t0, int t1, int n, const float* gamma, const float* beta,
+                           int training, float p, unsigned long long seed, int layer, float* y, float* stat,
+                           void* stream) {
+  SRF_REQUIRE(x && gamma && beta && y && stat && B > 0 && T > 0 && 0 <= t0 && t0 <= t1 && t1 <= T && n > 0 &&
+                  n <= kMaxVec,
+              "bad capsnorm range arguments");
+  if (t0 == t1) return SRF_OK;
+  hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(B * (t1 - t0)), dim3(256), (size_t)(n + 8) * 4,
+                     static_cast<hipStream_t>(stream), x, n, gamma, beta, training, p, seed, srf::seed_source(),
+                     (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0, (const float*)nullptr, (const float*)nullptr,
+                     (float*)nullptr, (float*)nullptr, kLengthEps, RowMap{T, t0, t1 - t0});
+  SRF_LAUNCH_CHECK("capsnorm_fwd_range");
+  return SRF_OK;
+}
+
+int srf_capsnorm_bwd_range(const float* x, int B, int T, int t0, int t1, int n, const float* gamma, const float* beta,
+                           int training, float p, unsigned long long seed, int layer, const float* stat,
+                           const float* g_y, float* g_x, float* gpart, void* stream) {
+  SRF_REQUIRE(x && gamma && beta && stat && g_y && g_x && gpart && B > 0 && T > 0 && 0 <= t0 && t0 <= t1 && t1 <= T &&
+                  n > 0 && n <= kMaxVec,
+              "bad capsnorm range arguments");
+  if (t0 == t1) return SRF_OK;
+  hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(B * (t1 - t0)), dim3(256), (size_t)(n + 8) * 4,
+                     static_cast<hipStream_t>(stream), x, n, gamma, beta, training, p, seed, srf::seed_source(),
+                     (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr, (const float*)nullptr,
+                     g_x, gpart, RowMap{T, t0, t1 - t0});
+  SRF_LAUNCH_CHECK("capsnorm_bwd_range");
+  return SRF_OK;
+}
+
+size_t srf_capsnorm_params_workspace(int F, int n) { return srf::colsum_scratch_floats(F, 2 * n) * 4; }
+
+int srf_capsnorm_bwd_params(const float* gpart, int F, int n, float* g_gamma, float* g_beta, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+  SRF_REQUIRE(gpart && g_gamma && g_beta && workspace && F > 0 && n > 0, "bad capsnorm params arguments");
+  if (workspace_bytes < srf_capsnorm_params_workspace(F, n)) {
+    srf::set_error("capsnorm params workspace too small");
+    return SRF_EWORKSPACE;
+  }
+  return srf::colsum(gpart, F, 2 * n, nullptr, static_cast<float*>(workspace), static_cast<hipStream_t>(stream),
+                     srf::ColSplit{{g_gamma, g_beta, nullptr, nullptr}, {n, n, 0, 0}});
 }
 
 int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
@@ -883,7 +938,7 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
   float* scratch = sum + srf::align_up((size_t)2 * n * 4, 256) / 4;
   hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, st, x, n, gamma, beta, training, p,
                      seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr,
-                     (const float*)nullptr, g_x, part);
+                     (const float*)nullptr, g_x, part, RowMap::all(F));
   SRF_LAUNCH_CHECK("capsnorm_bwd");
   (void)sum;
   return srf::colsum(part, F, 2 * n, nullptr, scratch, st, srf::ColSplit{{g_gamma, g_beta, nullptr, nullptr}, {n, n, 0, 0}});
@@ -906,7 +961,7 @@ int srf_caps_head_fwd_ex(const float* v, int F, int J, int D, const float* gamma
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4,
                      static_cast<hipStream_t>(stream), v, n, gamma_mid, beta_mid, training, p, seed, srf::seed_source(),
                      (unsigned)(kStreamMid0 + layer), (float*)nullptr, stat, 1, J, D, gamma_out, beta_out, logits,
-                     lens, length_eps);
+                     lens, length_eps, RowMap::all(F));
   SRF_LAUNCH_CHECK("caps_head_fwd");
   return SRF_OK;
 }
@@ -931,7 +986,7 @@ int srf_caps_head_bwd(const float* v, int F, int J, int D, const float* gamma_mi
   float* scratch = sum + srf::align_up((size_t)cols * 4, 256) / 4;
   hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4, st, v, n, gamma_mid, beta_mid,
                      training, p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), stat, g_logits, 1, J, D, gamma_out, lens,
-                     g_v, part);
+                     g_v, part, RowMap::all(F));
   SRF_LAUNCH_CHECK("caps_head_bwd");
   (void)sum;
   return srf::colsum(part, F, cols, nullptr, scratch, st,

@@ -48,23 +48,37 @@ struct SGeom {
   int NT() const { return (J * dout + 15) / 16; }
 };
 
+// ------------------------------------------------------------------ frame ranges
+// Frames t in [t0, t0 + nt) of every utterance, enumerated q = b * nt + (t - t0) in
+// [0, B * nt); a u / gu buffer holds frames [v0, v0 + vn) of each utterance
+// ([B][vn][in_n][JD]).  The whole layer is {T, 0, T, 0, T}.
+struct FrameMap {
+  int T, t0, nt, v0, vn;
+  __device__ __forceinline__ void frame(int q, int& b, int& t) const {
+    b = q / nt;
+    t = t0 + (q - b * nt);
+  }
+  __device__ __forceinline__ size_t view(int b, int t) const { return (size_t)b * vn + (t - v0); }
+};
+
 // ------------------------------------------------------------------ pose
 // Workgroup = 4 waves over one frame tile (16 frames) and one capsule i; wave w
 // takes row tiles w, w+4, ...  Operands as in the DR pass (k-permuted MFMA).
 template <int DIN>
 __global__ __launch_bounds__(256) void sdr_pose_kernel(const float* __restrict__ emb, const float* __restrict__ W,
-                                                       const float* __restrict__ bias, int F, int T, int N, int lpad,
-                                                       int in_n, int JD, float* __restrict__ u) {
+                                                       const float* __restrict__ bias, int Q, FrameMap fm, int N,
+                                                       int lpad, int in_n, int JD, float* __restrict__ u) {
   constexpr int KS = DIN / 4;
+  const int T = fm.T;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fl = lane & 15, g = lane >> 4;
   const int i = blockIdx.y;
-  const int f = blockIdx.x * 16 + fl;
-  const int fc = min(f, F - 1);
-  const int b = fc / T, t = fc - b * T;
+  const int q = blockIdx.x * 16 + fl;
+  int b, t;
+  fm.frame(min(q, Q - 1), b, t);
   const int w = i / N, n = i - w * N;
   const int ts = t + w - lpad;
-  const bool ok = f < F && ts >= 0 && ts < T;
+  const bool ok = q < Q && ts >= 0 && ts < T;
   float x[KS];
   const float* xp = emb + ((size_t)(b * T + min(max(ts, 0), T - 1)) * N + n) * DIN + g * KS;
 #pragma unroll
@@ -78,7 +92,7 @@ __global__ __launch_bounds__(256) void sdr_pose_kernel(const float* __restrict__
 #pragma unroll
     for (int k = 0; k < KS; ++k) acc = mfma16x16x4(wp[k], x[k], acc);
     const int row = tile * 16 + 4 * g;
-    if (f < F && row < JD) *reinterpret_cast<f4*>(u + ((size_t)f * in_n + i) * JD + row) = acc;
+    if (q < Q && row < JD) *reinterpret_cast<f4*>(u + (fm.view(b, t) * in_n + i) * JD + row) = acc;
   }
 }
 
@@ -150,17 +164,18 @@ template <int NT, bool GS>
 __global__ __launch_bounds__(NT) void sdr_fwd_kernel(const float* __restrict__ u, int T, int in_n, int J,
                                                               int D, int iters, int mask_first,
                                                               float* __restrict__ v_out, float* __restrict__ gstate,
-                                                              size_t gstride) {
+                                                              size_t gstride, srf::SeqRange rg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* smem = GS ? gstate + blockIdx.x * gstride : lds;
   const int JD = J * D, P = in_n * J;
   SeqSmem sm{smem, smem + JD, smem + JD + P, smem + JD + 2 * P, smem + 2 * JD + 2 * P};
   const int b = blockIdx.x;
-  for (int e = threadIdx.x; e < JD; e += NT) sm.v[e] = 0.f;   // v_{-1} = 0
+  for (int e = threadIdx.x; e < JD; e += NT)   // v_{t0-1} (v_{-1} = 0)
+    sm.v[e] = rg.t0 > 0 ? v_out[((size_t)b * T + rg.t0 - 1) * JD + e] : 0.f;
   __syncthreads();
-  for (int t = 0; t < T; ++t) {
+  for (int t = rg.t0; t < rg.t1; ++t) {
     const size_t f = (size_t)b * T + t;
-    const float* ut = u + f * in_n * JD;
+    const float* ut = u + ((size_t)b * rg.tu_n + (t - rg.tu0)) * in_n * JD;
     for (int p = threadIdx.x; p < P; p += NT) sm.bl[p] = 0.f;
     __syncthreads();
     for (int r = 0; r < iters; ++r) sdr_iteration<NT>(ut, sm, in_n, J, D, mask_first, nullptr, nullptr);
@@ -193,7 +208,7 @@ __global__ __launch_bounds__(NT) void sdr_bwd_kernel(const float* __restrict__ u
                                                               const float* __restrict__ g_v, int T, int in_n, int J,
                                                               int D, int iters, int mask_first,
                                                               float* __restrict__ gu, float* __restrict__ gstate,
-                                                              size_t gstride) {
+                                                              size_t gstride, srf::SeqRange rg) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* smem = GS ? gstate + blockIdx.x * gstride : lds;
   const int JD = J * D, P = in_n * J, R = iters;
@@ -215,11 +230,12 @@ __global__ __launch_bounds__(NT) void sdr_bwd_kernel(const float* __restrict__ u
   bs.gv = q; q += JD;
   const SeqSmem sm{bs.v, bs.bl, bs.c, bs.s, bs.red};
   const int b = blockIdx.x;
-  for (int e = tid; e < JD; e += NT) bs.carry[e] = 0.f;
+  float* carry_io = rg.carry ? rg.carry + (size_t)b * JD : nullptr;
+  for (int e = tid; e < JD; e += NT) bs.carry[e] = carry_io ? carry_io[e] : 0.f;
   __syncthreads();
-  for (int t = T - 1; t >= 0; --t) {
+  for (int t = rg.t1 - 1; t >= rg.t0; --t) {
     const size_t f = (size_t)b * T + t;
-    const float* ut = u + f * in_n * JD;
+    const float* ut = u + ((size_t)b * rg.tu_n + (t - rg.tu0)) * in_n * JD;
     // ---- recompute the frame's iterations from v_{t-1}
     for (int e = tid; e < JD; e += NT) {
       const float vp = t > 0 ? v_saved[(f - 1) * JD + e] : 0.f;
@@ -294,10 +310,12 @@ __global__ __launch_bounds__(NT) void sdr_bwd_kernel(const float* __restrict__ u
       for (int r = 0; r < R; ++r)
         g += bs.ck[(size_t)r * P + i * J + j] * bs.gsk[(size_t)r * JD + e] +
              bs.gl[(size_t)r * P + i * J + j] * bs.vck[(size_t)r * JD + e];
-      gu[f * in_n * JD + idx] = g;
+      gu[((size_t)b * rg.tg_n + (t - rg.tg0)) * in_n * JD + idx] = g;
     }
     __syncthreads();
   }
+  if (carry_io)
+    for (int e = tid; e < JD; e += NT) carry_io[e] = bs.carry[e];
 }
 
 size_t sdr_bwd_smem(int in_n, int J, int D, int R) {
@@ -308,19 +326,22 @@ size_t sdr_bwd_smem(int in_n, int J, int D, int R) {
 // ------------------------------------------------------------------ gx, gW
 // gx^T[e][f] = sum_row W^T[i][e][row] gu[f][i][row] for one frame tile and capsule
 // (K = rows, float4 operands), scattered into g_emb through the window adjoint.
+// Frames of the map fm, gu through its view.
 template <int DIN>
 __global__ __launch_bounds__(64) void sdr_gx_kernel(const float* __restrict__ gu, const float* __restrict__ WT,
-                                                    int F, int T, int N, int lpad, int in_n, int JD,
+                                                    int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
                                                     float* __restrict__ g_emb) {
   constexpr int NCT = (DIN + 15) / 16;
+  const int T = fm.T;
   const int lane = threadIdx.x, fl = lane & 15, g = lane >> 4;
   const int i = blockIdx.y;
-  const int f = blockIdx.x * 16 + fl;
-  const int fc = min(f, F - 1);
+  const int q = blockIdx.x * 16 + fl;
+  int b, t;
+  fm.frame(min(q, Q - 1), b, t);
   f4 acc[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) acc[ct] = f4{0.f, 0.f, 0.f, 0.f};
-  const float* bp = gu + ((size_t)fc * in_n + i) * JD + 4 * g;
+  const float* bp = gu + (fm.view(b, t) * in_n + i) * JD + 4 * g;
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
   for (int k0 = 0; k0 < JD; k0 += 16) {
     const bool kin = k0 + 4 * g < JD;   // JD % 4 == 0: a float4 is wholly in or out
@@ -334,10 +355,9 @@ __global__ __launch_bounds__(64) void sdr_gx_kernel(const float* __restrict__ gu
     }
   }
   // C layout: col = frame (fl), rows e = ct*16 + 4g + k
-  const int b = fc / T, t = fc - b * T;
   const int w = i / N, n = i - w * N;
   const int ts = t + w - lpad;
-  if (f >= F || ts < 0 || ts >= T) return;
+  if (q >= Q || ts < 0 || ts >= T) return;
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
@@ -363,13 +383,17 @@ __global__ void sdr_transpose_w_kernel(const float* __restrict__ W, int in_n, in
   WT[idx] = W[(i * JD + row) * din + e];
 }
 
-// gW[i][row][e] = sum_f gu[f][i][row] x_i(f)[e]: one wave per (i, row tile); K =
-// frames in steps of 4 (lane group g = frame), x read through the window.
+// gW[i][row][e] = sum_f gu[f][i][row] x_i(f)[e] and gbias[i][row] = sum_f gu[f][i][row]:
+// one wave per (i, row tile); K = frames in steps of 4 (lane group g = frame), x read
+// through the window.  Frames of the map fm (gu through its view); accumulate != 0
+// adds to gW / gbias (a layer's frame ranges in turn, one writer per element).
 template <int DIN>
 __global__ __launch_bounds__(256) void sdr_gw_kernel(const float* __restrict__ gu, const float* __restrict__ emb,
-                                                     int F, int T, int N, int lpad, int in_n, int JD,
-                                                     float* __restrict__ gW) {
+                                                     int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
+                                                     float* __restrict__ gW, float* __restrict__ gbias,
+                                                     int accumulate) {
   constexpr int NCT = (DIN + 15) / 16;
+  const int T = fm.T;
   const int NT = (JD + 15) / 16;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l16 = lane & 15, g = lane >> 4;
@@ -381,27 +405,36 @@ __global__ __launch_bounds__(256) void sdr_gw_kernel(const float* __restrict__ g
   f4 acc[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) acc[ct] = f4{0.f, 0.f, 0.f, 0.f};
+  float sb = 0.f;
   // 8 groups of 4 frames per iteration: every load of the batch is issued before the
   // first MFMA (one round trip per 32 frames); the accumulation order is unchanged
   constexpr int U = 8;
-  for (int f0 = 0; f0 < F; f0 += 4 * U) {
+  for (int q0 = 0; q0 < Q; q0 += 4 * U) {
     float a[U], xv[U][NCT];
 #pragma unroll
-    for (int q = 0; q < U; ++q) {
-      const int f = f0 + 4 * q + g;
-      const int fc = min(f, F - 1);
-      a[q] = f < F ? gu[((size_t)fc * in_n + i) * JD + row] : 0.f;
-      const int b = fc / T, t = fc - b * T;
+    for (int k = 0; k < U; ++k) {
+      const int q = q0 + 4 * k + g;
+      int b, t;
+      fm.frame(min(q, Q - 1), b, t);
+      a[k] = q < Q ? gu[(fm.view(b, t) * in_n + i) * JD + row] : 0.f;
       const int ts = t + w - lpad;
-      const bool ok = f < F && ts >= 0 && ts < T;
+      const bool ok = q < Q && ts >= 0 && ts < T;
       const float* xp = emb + ((size_t)(b * T + min(max(ts, 0), T - 1)) * N + n) * DIN;
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) xv[q][ct] = ok ? xp[min(ct * 16 + l16, DIN - 1)] : 0.f;
+      for (int ct = 0; ct < NCT; ++ct) xv[k][ct] = ok ? xp[min(ct * 16 + l16, DIN - 1)] : 0.f;
     }
 #pragma unroll
-    for (int q = 0; q < U; ++q)
+    for (int k = 0; k < U; ++k) {
+      sb += a[k];
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) acc[ct] = mfma16x16x4(a[q], xv[q][ct], acc[ct]);
+      for (int ct = 0; ct < NCT; ++ct) acc[ct] = mfma16x16x4(a[k], xv[k][ct], acc[ct]);
+    }
+  }
+  sb += __shfl_xor(sb, 16, 64);
+  sb += __shfl_xor(sb, 32, 64);
+  if (g == 0 && tg * 16 + l16 < JD) {
+    float* gb = gbias + (size_t)i * JD + tg * 16 + l16;
+    *gb = accumulate ? *gb + sb : sb;
   }
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) {
@@ -410,7 +443,10 @@ __global__ __launch_bounds__(256) void sdr_gw_kernel(const float* __restrict__ g
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int r = tg * 16 + 4 * g + k;
-      if (r < JD) gW[((size_t)i * JD + r) * DIN + e] = acc[ct][k];
+      if (r < JD) {
+        float* dst = gW + ((size_t)i * JD + r) * DIN + e;
+        *dst = accumulate ? *dst + acc[ct][k] : acc[ct][k];
+      }
     }
   }
 }
@@ -440,57 +476,140 @@ size_t gstate_bytes(const SGeom& g, size_t state_bytes) {
   return sdr_gstate(state_bytes) ? (size_t)g.B * gstate_stride(state_bytes) * sizeof(float) : 0;
 }
 
-template <int D>
-void launch_pose(const SGeom& g, const float* emb, const float* W, const float* bias, float* u, hipStream_t st) {
-  hipLaunchKernelGGL(sdr_pose_kernel<D>, dim3((g.F() + 15) / 16, g.in_n()), dim3(256), 0, st, emb, W, bias, g.F(),
-                     g.T, g.N, g.lpad, g.in_n(), g.JD(), u);
-}
+FrameMap frame_map(int T, int t0, int t1, int v0, int vn) { return FrameMap{T, t0, t1 - t0, v0, vn}; }
 
-int pose_dispatch(const SGeom& g, const float* emb, const float* W, const float* bias, float* u, hipStream_t st) {
+int pose_range(const SGeom& g, const float* emb, const float* W, const float* bias, const FrameMap& fm, float* u,
+               hipStream_t st) {
+  const int Q = g.B * fm.nt;
+  if (Q == 0) return SRF_OK;
+  const dim3 grid((Q + 15) / 16, g.in_n());
+#define SRF_POSE(DIN) \
+  hipLaunchKernelGGL(sdr_pose_kernel<DIN>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(), g.JD(), u)
   switch (g.din) {
-    case 8: launch_pose<8>(g, emb, W, bias, u, st); break;
-    case 16: launch_pose<16>(g, emb, W, bias, u, st); break;
-    case 32: launch_pose<32>(g, emb, W, bias, u, st); break;
-    default: launch_pose<64>(g, emb, W, bias, u, st); break;
+    case 8: SRF_POSE(8); break;
+    case 16: SRF_POSE(16); break;
+    case 32: SRF_POSE(32); break;
+    default: SRF_POSE(64); break;
   }
+#undef SRF_POSE
   SRF_LAUNCH_CHECK("sdr_pose");
   return SRF_OK;
 }
 
+// recurrence over one frame range: the register-resident kernels when the shape fits,
+// else the LDS / global-state ones (gstate: B slices of the state, when it exceeds LDS)
+int recur_fwd(const SGeom& g, const float* u, float* v_out, const srf::SeqRange& rg, float* gstate, hipStream_t st) {
+  if (rg.t0 >= rg.t1) return SRF_OK;
+  if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
+    return srf::sdr_seq_fwd(u, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, v_out, rg, st);
+  const size_t sm = sdr_fwd_smem(g.in_n(), g.J, g.dout);
+  if (sdr_gstate(sm))
+    hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, g.T, g.in_n(), g.J,
+                       g.dout, g.iters, g.mask_first, v_out, gstate, gstate_stride(sm), rg);
+  else
+    hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, false>), dim3(g.B), dim3(kGsThreads), sm, st, u, g.T, g.in_n(), g.J,
+                       g.dout, g.iters, g.mask_first, v_out, (float*)nullptr, (size_t)0, rg);
+  SRF_LAUNCH_CHECK("sdr_fwd");
+  return SRF_OK;
+}
+
+int recur_bwd(const SGeom& g, const float* u, const float* v_saved, const float* g_v, float* gu,
+              const srf::SeqRange& rg, float* gstate, hipStream_t st) {
+  if (rg.t0 >= rg.t1) return SRF_OK;
+  if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
+    return srf::sdr_seq_bwd(u, v_saved, g_v, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, rg, st);
+  const size_t sm = sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters);
+  if (sdr_gstate(sm))
+    hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, v_saved, g_v, g.T,
+                       g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, gstate, gstate_stride(sm), rg);
+  else
+    hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, false>), dim3(g.B), dim3(kGsThreads), sm, st, u, v_saved, g_v, g.T,
+                       g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, (float*)nullptr, (size_t)0, rg);
+  SRF_LAUNCH_CHECK("sdr_bwd");
+  return SRF_OK;
+}
+
+size_t recur_workspace(const SGeom& g) {
+  if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters)) return 0;
+  return std::max(gstate_bytes(g, sdr_fwd_smem(g.in_n(), g.J, g.dout)),
+                  gstate_bytes(g, sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters)));
+}
+
+int gx_range(const SGeom& g, const float* gu, const float* WT, const FrameMap& fm, float* g_emb, hipStream_t st) {
+  const int Q = g.B * fm.nt;
+  if (Q == 0) return SRF_OK;
+  const dim3 grid((Q + 15) / 16, g.in_n());
+#define SRF_GX(DIN) \
+  hipLaunchKernelGGL(sdr_gx_kernel<DIN>, grid, dim3(64), 0, st, gu, WT, Q, fm, g.N, g.lpad, g.in_n(), g.JD(), g_emb)
+  switch (g.din) {
+    case 8: SRF_GX(8); break;
+    case 16: SRF_GX(16); break;
+    case 32: SRF_GX(32); break;
+    default: SRF_GX(64); break;
+  }
+#undef SRF_GX
+  SRF_LAUNCH_CHECK("sdr_gx");
+  return SRF_OK;
+}
+
+int gw_range(const SGeom& g, const float* gu, const float* emb, const FrameMap& fm, int accumulate, float* g_W,
+             float* g_bias, hipStream_t st) {
+  const int Q = g.B * fm.nt;
+  if (Q == 0 && accumulate) return SRF_OK;
+  const int tasks = g.in_n() * g.NT();
+  const dim3 grid((tasks + 3) / 4);
+#define SRF_GW(DIN)                                                                                             \
+  hipLaunchKernelGGL(sdr_gw_kernel<DIN>, grid, dim3(256), 0, st, gu, emb, Q, fm, g.N, g.lpad, g.in_n(), g.JD(), \
+                     g_W, g_bias, accumulate)
+  switch (g.din) {
+    case 8: SRF_GW(8); break;
+    case 16: SRF_GW(16); break;
+    case 32: SRF_GW(32); break;
+    default: SRF_GW(64); break;
+  }
+#undef SRF_GW
+  SRF_LAUNCH_CHECK("sdr_gw");
+  return SRF_OK;
+}
+
+int transpose_w(const SGeom& g, const float* W, float* WT, float* zero, size_t n_zero, hipStream_t st) {
+  const size_t total = (size_t)g.in_n() * g.JD() * g.din + n_zero;
+  hipLaunchKernelGGL(sdr_transpose_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, g.in_n(), g.JD(), g.din,
+                     WT, zero, n_zero);
+  SRF_LAUNCH_CHECK("sdr_transpose_w");
+  return SRF_OK;
+}
+
 struct SdrBwdWs {
-  float *u, *gu, *WT, *scratch, *gstate;
+  float *u, *gu, *WT, *gstate;
   size_t bytes;
 };
 
 SdrBwdWs sdr_bwd_layout(const SGeom& g, void* base) {
   const size_t FU = (size_t)g.F() * g.in_n() * g.JD();
   size_t off = 0;
-  auto take = [&](size_t nfloat) {
+  auto take = [&](size_t nbytes) {
     size_t o = off;
-    off += srf::align_up(nfloat * sizeof(float), 256);
+    off += srf::align_up(nbytes, 256);
     return o;
   };
-  const size_t ou = take(FU), ogu = take(FU), owt = take((size_t)g.in_n() * g.JD() * g.din),
-               osc = take(srf::colsum_scratch_floats(g.F(), g.in_n() * g.JD())),
-               ogs = take(gstate_bytes(g, sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters)) / sizeof(float));
+  const size_t ou = take(FU * 4), ogu = take(FU * 4), owt = take((size_t)g.in_n() * g.JD() * g.din * 4),
+               ogs = take(recur_workspace(g));
   char* b = static_cast<char*>(base);
   SdrBwdWs w;
   w.u = (float*)(b + ou);
   w.gu = (float*)(b + ogu);
   w.WT = (float*)(b + owt);
-  w.scratch = (float*)(b + osc);
   w.gstate = (float*)(b + ogs);
   w.bytes = off;
   return w;
 }
 
-template <int D>
-void launch_gx_gw(const SGeom& g, const float* emb, const SdrBwdWs& w, float* g_emb, float* g_W, hipStream_t st) {
-  hipLaunchKernelGGL(sdr_gx_kernel<D>, dim3((g.F() + 15) / 16, g.in_n()), dim3(64), 0, st, w.gu, w.WT, g.F(), g.T,
-                     g.N, g.lpad, g.in_n(), g.JD(), g_emb);
-  const int tasks = g.in_n() * g.NT();
-  hipLaunchKernelGGL(sdr_gw_kernel<D>, dim3((tasks + 3) / 4), dim3(256), 0, st, w.gu, emb, g.F(), g.T, g.N, g.lpad,
-                     g.in_n(), g.JD(), g_W);
+int range_ok(const SGeom& g, int t0, int t1, int v0, int vn) {
+  SRF_REQUIRE(0 <= t0 && t0 <= t1 && t1 <= g.T, "frame range [%d, %d) outside [0, %d)", t0, t1, g.T);
+  SRF_REQUIRE(t0 == t1 || (v0 <= t0 && t1 <= v0 + vn), "frame range [%d, %d) outside the buffer view [%d, %d)", t0,
+              t1, v0, v0 + vn);
+  return SRF_OK;
 }
 
 }  // namespace
@@ -521,23 +640,11 @@ int srf_route_sdr_fwd(const float* emb, const float* W, const float* bias, int B
     srf::set_error("SDR forward workspace too small");
     return SRF_EWORKSPACE;
   }
-  const bool seq = srf::sdr_seq_supported(g.in_n(), J, dout, iters);
-  const size_t sm = sdr_fwd_smem(g.in_n(), J, dout);
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* u = static_cast<float*>(workspace);
   float* gstate = u + srf::align_up((size_t)g.F() * g.in_n() * g.JD() * sizeof(float), 256) / sizeof(float);
-  if ((rc = pose_dispatch(g, emb, W, bias, u, st))) return rc;
-  if (seq) {
-    if ((rc = srf::sdr_seq_fwd(u, B, T, g.in_n(), J, dout, iters, g.mask_first, v_out, st))) return rc;
-  } else {
-    if (sdr_gstate(sm))
-      hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, true>), dim3(B), dim3(kGsThreads), 0, st, u, T, g.in_n(), J, dout, iters,
-                         g.mask_first, v_out, gstate, gstate_stride(sm));
-    else
-      hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, false>), dim3(B), dim3(kGsThreads), sm, st, u, T, g.in_n(), J, dout, iters,
-                         g.mask_first, v_out, (float*)nullptr, (size_t)0);
-    SRF_LAUNCH_CHECK("sdr_fwd");
-  }
+  if ((rc = pose_range(g, emb, W, bias, frame_map(T, 0, T, 0, T), u, st))) return rc;
+  if ((rc = recur_fwd(g, u, v_out, srf::SeqRange::whole(T), gstate, st))) return rc;
   SRF_HIP_TRY(hipMemcpyAsync(saved, v_out, (size_t)g.F() * g.JD() * sizeof(float), hipMemcpyDeviceToDevice, st));
   return SRF_OK;
 }
@@ -555,36 +662,80 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
     srf::set_error("SDR backward workspace too small");
     return SRF_EWORKSPACE;
   }
-  const bool seq = srf::sdr_seq_supported(g.in_n(), J, dout, iters);
-  const size_t sm = sdr_bwd_smem(g.in_n(), J, dout, iters);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if ((rc = pose_dispatch(g, emb, W, bias, w.u, st))) return rc;
-  if (seq) {
-    if ((rc = srf::sdr_seq_bwd(w.u, saved, g_v, B, T, g.in_n(), J, dout, iters, g.mask_first, w.gu, st))) return rc;
-  } else {
-    if (sdr_gstate(sm))
-      hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, true>), dim3(B), dim3(kGsThreads), 0, st, w.u, saved, g_v, T, g.in_n(), J,
-                         dout, iters, g.mask_first, w.gu, w.gstate, gstate_stride(sm));
-    else
-      hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, false>), dim3(B), dim3(kGsThreads), sm, st, w.u, saved, g_v, T, g.in_n(), J,
-                         dout, iters, g.mask_first, w.gu, (float*)nullptr, (size_t)0);
-    SRF_LAUNCH_CHECK("sdr_bwd");
-  }
-  {
-    const size_t n_emb = (size_t)g.F() * N * din;
-    const size_t total = (size_t)g.in_n() * g.JD() * din + n_emb;
-    hipLaunchKernelGGL(sdr_transpose_w_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, g.in_n(), g.JD(), din,
-                       w.WT, g_emb, n_emb);
-    SRF_LAUNCH_CHECK("sdr_transpose_w");
-  }
-  switch (din) {
-    case 8: launch_gx_gw<8>(g, emb, w, g_emb, g_W, st); break;
-    case 16: launch_gx_gw<16>(g, emb, w, g_emb, g_W, st); break;
-    case 32: launch_gx_gw<32>(g, emb, w, g_emb, g_W, st); break;
-    default: launch_gx_gw<64>(g, emb, w, g_emb, g_W, st); break;
-  }
-  SRF_LAUNCH_CHECK("sdr_gx_gw");
-  return srf::colsum(w.gu, g.F(), g.in_n() * g.JD(), g_bias, w.scratch, st);
+  const FrameMap all = frame_map(T, 0, T, 0, T);
+  if ((rc = pose_range(g, emb, W, bias, all, w.u, st))) return rc;
+  if ((rc = recur_bwd(g, w.u, saved, g_v, w.gu, srf::SeqRange::whole(T), w.gstate, st))) return rc;
+  if ((rc = transpose_w(g, W, w.WT, g_emb, (size_t)g.F() * N * din, st))) return rc;
+  if ((rc = gx_range(g, w.gu, w.WT, all, g_emb, st))) return rc;
+  return gw_range(g, w.gu, emb, all, 0, g_W, g_bias, st);
+}
+
+// ---- the same layer in frame ranges (the layer-pipelined SDR stack)
+int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                       int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = range_ok(g, t0, t1, v0, vn))) return rc;
+  SRF_REQUIRE(emb && W && bias && u, "null pointer argument");
+  return pose_range(g, emb, W, bias, frame_map(T, t0, t1, v0, vn), u, static_cast<hipStream_t>(stream));
+}
+
+size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters) {
+  SGeom g{B, 1, in_n, 8, 0, 0, J, dout, iters, 0};
+  return recur_workspace(g);
+}
+
+int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
+                            int mask_first, int t0, int t1, float* v_out, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+  SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};   // N = in_n, window 1: in_n() = in_n
+  int rc = check_sgeom(g);
+  if (rc || (rc = range_ok(g, t0, t1, v0, vn))) return rc;
+  SRF_REQUIRE(u && v_out, "null pointer argument");
+  SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
+              "SDR recurrence workspace too small");
+  return recur_fwd(g, u, v_out, srf::SeqRange{t0, t1, v0, vn, 0, T, nullptr}, static_cast<float*>(workspace),
+                   static_cast<hipStream_t>(stream));
+}
+
+int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved, const float* g_v, int B, int T,
+                            int in_n, int J, int dout, int iters, int mask_first, int t0, int t1, float* carry,
+                            float* gu, int g0, int gn, void* workspace, size_t workspace_bytes, void* stream) {
+  SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = range_ok(g, t0, t1, v0, vn)) || (rc = range_ok(g, t0, t1, g0, gn))) return rc;
+  SRF_REQUIRE(u && v_saved && g_v && carry && gu, "null pointer argument");
+  SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
+              "SDR recurrence workspace too small");
+  return recur_bwd(g, u, v_saved, g_v, gu, srf::SeqRange{t0, t1, v0, vn, g0, gn, carry},
+                   static_cast<float*>(workspace), static_cast<hipStream_t>(stream));
+}
+
+int srf_route_sdr_transpose_w(const float* W, int in_n, int J, int dout, int din, float* WT, void* stream) {
+  SRF_REQUIRE(W && WT && in_n > 0 && J > 0 && dout > 0 && din > 0, "bad transpose arguments");
+  SGeom g{1, 1, in_n, din, 0, 0, J, dout, 1, 0};
+  return transpose_w(g, W, WT, nullptr, 0, static_cast<hipStream_t>(stream));
+}
+
+int srf_route_sdr_gx(const float* gu, int g0, int gn, const float* WT, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int t0, int t1, float* g_emb, void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = range_ok(g, t0, t1, g0, gn))) return rc;
+  SRF_REQUIRE(gu && WT && g_emb, "null pointer argument");
+  return gx_range(g, gu, WT, frame_map(T, t0, t1, g0, gn), g_emb, static_cast<hipStream_t>(stream));
+}
+
+int srf_route_sdr_gw(const float* gu, int g0, int gn, const float* emb, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int t0, int t1, int accumulate, float* g_W, float* g_bias,
+                     void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = range_ok(g, t0, t1, g0, gn))) return rc;
+  SRF_REQUIRE(gu && emb && g_W && g_bias, "null pointer argument");
+  return gw_range(g, gu, emb, frame_map(T, t0, t1, g0, gn), accumulate, g_W, g_bias,
+                  static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -7,6 +7,21 @@
 
 namespace srf {
 
+// A range of frames of every utterance and the buffer views the recurrence kernels
+// address (the chunked, layer-pipelined SDR stack runs a layer as several ranges):
+//   frames t in [t0, t1) of each utterance are routed (backward: from t1-1 down);
+//   u holds frames [tu0, tu0 + tu_n) of each utterance, laid out [B][tu_n][in_n][JD];
+//   gu likewise holds frames [tg0, tg0 + tg_n);
+//   v_out / v_saved / g_v are always whole [B][T][JD];
+//   carry [B][JD] (backward): dL/dv_{t1-1} carried in from the later frames, and
+//   dL/dv_{t0-1} carried out -- nullptr: start from 0 and drop it (whole-T calls).
+// The forward starts from v_out[t0 - 1] (0 at t0 = 0).
+struct SeqRange {
+  int t0, t1, tu0, tu_n, tg0, tg_n;
+  float* carry;
+  static SeqRange whole(int T) { return SeqRange{0, T, 0, T, 0, T, nullptr}; }
+};
+
 // True when sdr_seq_fwd/bwd handle (in_n, J, dout, iters): dout in {8,16,32},
 // J <= 64 (padded to a power of two JP, dout*JP <= 1024), in_n within the
 // per-lane register budget.  Disabled by SRF_SDR_SEQ=0 (A/B runs, legacy tests).
@@ -14,12 +29,12 @@ bool sdr_seq_supported(int in_n, int J, int dout, int iters);
 
 // u [B*T][in_n][J*dout] (pose output) -> v_out [B*T][J*dout]; one workgroup per utterance.
 int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                hipStream_t st);
+                const SeqRange& rg, hipStream_t st);
 
 // Reverse-time pass: recomputes each frame's iterations from v_saved (the
 // forward's v_out), writes gu [B*T][in_n][J*dout] = dL/du.
 int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                int iters, int mask_first, float* gu, hipStream_t st);
+                int iters, int mask_first, float* gu, const SeqRange& rg, hipStream_t st);
 
 // Template choice for a shape: per-lane input-capsule count NIM in {2, 5, 10} and
 // the iteration bound RM of the backward in {3, 5}.  False when unsupported.

@@ -38,7 +38,8 @@ using namespace srf_seq;
 // part [16][JD].
 template <int D, int JP, int NIM>
 __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __restrict__ u, int T, int in_n, int J,
-                                                               int iters, int mask_first, float* __restrict__ v_out) {
+                                                               int iters, int mask_first, float* __restrict__ v_out,
+                                                               srf::SeqRange rg) {
   using C = Cfg<D, JP, NIM>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = J * D;
@@ -47,15 +48,16 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
   const int tid = threadIdx.x;
   const Lane L = lane_map<C>(in_n, J, mask_first);
   const size_t ff = (size_t)in_n * JD;
-  const float* ub = u + (size_t)blockIdx.x * T * ff;
+  const float* ub = u + (size_t)blockIdx.x * rg.tu_n * ff;   // frame t at ub + (t - tu0) * ff
   float* vo = v_out + (size_t)blockIdx.x * T * JD;
   const bool owner_wave = (tid >> 6) * 64 < JD;   // waves holding elements e = tid < JD
   const bool ev = tid < JD;
-  if (ev) wl[tid] = 0.f;   // v_{-1} = 0
+  if (rg.t0 >= rg.t1) return;
+  if (ev) wl[tid] = rg.t0 > 0 ? vo[(size_t)(rg.t0 - 1) * JD + tid] : 0.f;   // v_{t0-1} (v_{-1} = 0)
   float ur[C::NIM][C::KD];
-  load_frame<C>(ub, JD, L, ur);
+  load_frame<C>(ub + (size_t)(rg.t0 - rg.tu0) * ff, JD, L, ur);
   __syncthreads();
-  for (int t = 0; t < T; ++t) {
+  for (int t = rg.t0; t < rg.t1; ++t) {
     float b[C::NIM], c[C::NIM];
 #pragma unroll
     for (int k = 0; k < C::NIM; ++k) b[k] = 0.f;
@@ -65,9 +67,9 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
       logits_softmax<C>(ur, w, L, b, c);
       row_partial<C>(c, ur, L, JD, part);
 #if SRF_SEQ_DBG == 1   // timing experiment: re-load the current (cache-hot) frame
-      if (r == iters - 1 && t + 1 < T) load_frame<C>(ub + (size_t)t * ff, JD, L, ur);
+      if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(t - rg.tu0) * ff, JD, L, ur);
 #else
-      if (r == iters - 1 && t + 1 < T) load_frame<C>(ub + (size_t)(t + 1) * ff, JD, L, ur);   // u_t is dead
+      if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(t + 1 - rg.tu0) * ff, JD, L, ur);   // u_t is dead
 #endif
       __syncthreads();
       if (owner_wave) {
@@ -88,22 +90,22 @@ size_t fwd_lds(int J, int D) {
 
 template <int D, int JP, int NIM>
 int launch_fwd(const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
-               hipStream_t st) {
+               const srf::SeqRange& rg, hipStream_t st) {
   const size_t lds = fwd_lds(J, D);
   auto k = sdr_seq_fwd_kernel<D, JP, NIM>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, T, in_n, J, iters, mask_first, v_out);
+  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, T, in_n, J, iters, mask_first, v_out, rg);
   SRF_LAUNCH_CHECK("sdr_seq_fwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
 int fwd_nim(int nim, const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
-            hipStream_t st) {
-  if (nim == 2) return launch_fwd<D, JP, 2>(u, B, T, in_n, J, iters, mask_first, v_out, st);
-  if (nim == 5) return launch_fwd<D, JP, 5>(u, B, T, in_n, J, iters, mask_first, v_out, st);
-  if constexpr (seq_kd(D, JP) <= 8) return launch_fwd<D, JP, 10>(u, B, T, in_n, J, iters, mask_first, v_out, st);
+            const srf::SeqRange& rg, hipStream_t st) {
+  if (nim == 2) return launch_fwd<D, JP, 2>(u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
+  if (nim == 5) return launch_fwd<D, JP, 5>(u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
+  if constexpr (seq_kd(D, JP) <= 8) return launch_fwd<D, JP, 10>(u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
   srf::set_error("sdr_seq: no forward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -136,7 +138,7 @@ bool sdr_seq_supported(int in_n, int J, int dout, int iters) {
 }
 
 int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                hipStream_t st) {
+                const SeqRange& rg, hipStream_t st) {
   int nim = 0, rm = 0;
   if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
@@ -144,7 +146,7 @@ int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int ite
   }
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_F(DD, PP) \
-  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, u, B, T, in_n, J, iters, mask_first, v_out, st);
+  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
   SRF_SEQ_CASES(SRF_SEQ_F)
 #undef SRF_SEQ_F
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

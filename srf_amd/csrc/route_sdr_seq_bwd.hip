@@ -33,7 +33,8 @@ template <int D, int JP, int NIM, int RM, bool CL>
 __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __restrict__ u,
                                                                const float* __restrict__ v_saved,
                                                                const float* __restrict__ g_v, int T, int in_n, int J,
-                                                               int iters, int mask_first, float* __restrict__ gu) {
+                                                               int iters, int mask_first, float* __restrict__ gu,
+                                                               srf::SeqRange rg) {
   using C = Cfg<D, JP, NIM>;
   constexpr int RR = CL ? 1 : RM;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -50,16 +51,21 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
   const Lane L = lane_map<C>(in_n, J, mask_first);
   const size_t ff = (size_t)in_n * JD;
   const size_t f0 = (size_t)blockIdx.x * T;
+  const float* ub = u + (size_t)blockIdx.x * rg.tu_n * ff;    // frame t at ub + (t - tu0) * ff
+  float* gub = gu + (size_t)blockIdx.x * rg.tg_n * ff;        // frame t at gub + (t - tg0) * ff
   const bool owner_wave = (tid >> 6) * 64 < JD;
   const bool ev = tid < JD;
-  float carry = 0.f;   // dL/dv_t carried back from frame t+1 (owner threads)
+  if (rg.t0 >= rg.t1) return;
+  float* carry_io = rg.carry ? rg.carry + (size_t)blockIdx.x * JD : nullptr;
+  // dL/dv_t carried back from frame t+1 (owner threads), from the later range
+  float carry = (carry_io && ev) ? carry_io[tid] : 0.f;
   float ur[C::NIM][C::KD];
   float cr[RR][C::NIM], gl[RR][C::NIM];
   float sr[RM];        // s^r of the owned element
 #pragma unroll
   for (int r = 0; r < RM; ++r) sr[r] = 0.f;
-  load_frame<C>(u + (f0 + T - 1) * ff, JD, L, ur);
-  for (int t = T - 1; t >= 0; --t) {
+  load_frame<C>(ub + (size_t)(rg.t1 - 1 - rg.tu0) * ff, JD, L, ur);
+  for (int t = rg.t1 - 1; t >= rg.t0; --t) {
     const size_t f = f0 + t;
     float a = 0.f;
     if (ev) {
@@ -183,15 +189,16 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
           }
         }
         if (L.jv) {
-          float* dst = gu + f * ff + (size_t)(L.g + k * C::G) * JD + L.eoff;
+          float* dst = gub + (size_t)(t - rg.tg0) * ff + (size_t)(L.g + k * C::G) * JD + L.eoff;
 #pragma unroll
           for (int c = 0; c < C::KD; c += 4) *reinterpret_cast<f4*>(dst + c) = f4{acc[c], acc[c + 1], acc[c + 2], acc[c + 3]};
         }
       }
     }
-    if (t > 0) load_frame<C>(u + (f - 1) * ff, JD, L, ur);
+    if (t > rg.t0) load_frame<C>(ub + (size_t)(t - 1 - rg.tu0) * ff, JD, L, ur);
     __syncthreads();   // the next frame overwrites w, Vc^0 and the c / gL slabs
   }
+  if (carry_io && ev) carry_io[tid] = carry;   // dL/dv_{t0-1} for the earlier range
 }
 
 size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
@@ -203,26 +210,26 @@ size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
 
 template <int D, int JP, int NIM, int RM>
 int launch_bwd(const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J, int iters,
-               int mask_first, float* gu, hipStream_t st) {
+               int mask_first, float* gu, const srf::SeqRange& rg, hipStream_t st) {
   constexpr bool want = cl_wanted(NIM, seq_kd(D, JP));
   const bool cl = want && bwd_lds(J, D, RM, in_n, true) <= 160 * 1024;
   const size_t lds = bwd_lds(J, D, RM, in_n, cl);
   auto k = cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want> : sdr_seq_bwd_kernel<D, JP, NIM, RM, false>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, vs, gv, T, in_n, J, iters, mask_first, gu);
+  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, vs, gv, T, in_n, J, iters, mask_first, gu, rg);
   SRF_LAUNCH_CHECK("sdr_seq_bwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
 int bwd_nim(int nim, int rm, const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J,
-            int iters, int mask_first, float* gu, hipStream_t st) {
-  if (rm == 5) return launch_bwd<D, JP, 2, 5>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
-  if (nim == 2) return launch_bwd<D, JP, 2, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
-  if (nim == 5) return launch_bwd<D, JP, 5, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
+            int iters, int mask_first, float* gu, const srf::SeqRange& rg, hipStream_t st) {
+  if (rm == 5) return launch_bwd<D, JP, 2, 5>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
+  if (nim == 2) return launch_bwd<D, JP, 2, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
+  if (nim == 5) return launch_bwd<D, JP, 5, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
   if constexpr (seq_kd(D, JP) <= 8)
-    return launch_bwd<D, JP, 10, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, st);
+    return launch_bwd<D, JP, 10, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
   srf::set_error("sdr_seq: no backward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -232,7 +239,7 @@ int bwd_nim(int nim, int rm, const float* u, const float* vs, const float* gv, i
 namespace srf {
 
 int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                int iters, int mask_first, float* gu, hipStream_t st) {
+                int iters, int mask_first, float* gu, const SeqRange& rg, hipStream_t st) {
   int nim = 0, rm = 0;
   if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
@@ -241,7 +248,7 @@ int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, i
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_B(DD, PP)     \
   if (dout == DD && JP == PP) \
-    return bwd_nim<DD, PP>(nim, rm, u, v_saved, g_v, B, T, in_n, J, iters, mask_first, gu, st);
+    return bwd_nim<DD, PP>(nim, rm, u, v_saved, g_v, B, T, in_n, J, iters, mask_first, gu, rg, st);
   SRF_SEQ_CASES(SRF_SEQ_B)
 #undef SRF_SEQ_B
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

@@ -449,3 +449,229 @@ def ctc_loss_and_grad(logits, labels, label_len, logit_len, blank, grad_scale):
 
 def ctc_loss(logits, labels, label_len, logit_len, blank):
     return CtcLoss.apply(logits, _i32(labels), _i32(label_len), _i32(logit_len), blank)
+
+
+# ---------------------------------------------------------------------------
+# SDR stack: every SDR layer and the LN + dropout between them, as a wavefront
+class SdrStackPlan:
+    """Static plan of an SDR stack (sequence_router_naive.py:145-191 with
+    --model-caps-context, the per-layer LN / dropout of :187-191 between layers).
+
+    The frames of each utterance are cut into K ranges.  Layer l's recurrence over
+    range k (frames are routed in order, naive:162-170) needs only layer l-1's
+    output up to frame t1 - 1 + rpad (the window, naive:150-151), so with the range
+    bounds of layer l shifted down by l * rpad, range (l, k) depends on (l - 1, k)
+    and (l, k - 1) only: the L layers run as a wavefront, one HIP stream per layer,
+    L per-utterance recurrences in flight instead of one.  The backward walks the
+    ranges in reverse with bounds shifted up by (L - 1 - l) * rpad: (l, k) needs
+    layer l+1's gx (the window adjoint) down to frame t0 - rpad, i.e. (l + 1, k).
+    layers: [(N, din, J, dout, mask_first)] per layer."""
+
+    def __init__(self, B, T, layers, lpad, rpad, iters, n_chunks=0):
+        self.B, self.T, self.lpad, self.rpad, self.iters = B, T, lpad, rpad, iters
+        self.layers = layers
+        self.L = len(layers)
+        self.win = lpad + rpad + 1
+        if n_chunks <= 0:
+            n_chunks = int(os.environ.get('SRF_SDR_CHUNKS', '0') or 0) or max(1, min(16, -(-T // 20)))
+        K = max(1, min(n_chunks, T))
+        self.K = K
+        c = [round(k * T / K) for k in range(K + 1)]
+
+        def bounds(shift):
+            b = [0] + [min(max(c[k] + shift, 0), T) for k in range(1, K)] + [T]
+            for k in range(1, K + 1):        # monotone after clipping
+                b[k] = max(b[k], b[k - 1])
+            return b
+        self.fwd = [bounds(-rpad * l) for l in range(self.L)]
+        self.bwd = [bounds(rpad * (self.L - 1 - l)) for l in range(self.L)]
+        self.nmax = max(max(b[k + 1] - b[k] for k in range(K)) for b in self.fwd + self.bwd)
+        L_ = _lib.lib()
+        self.rws = [L_.srf_route_sdr_recur_workspace(B, N * self.win, J, D, iters) for (N, din, J, D, mf) in layers]
+
+    def in_n(self, l):
+        return self.layers[l][0] * self.win
+
+    def events(self, which):
+        """[L][K] events of the forward or backward wavefront, created once and kept
+        with the plan: a captured step (hipGraph) must not see its events destroyed
+        before the capture ends."""
+        ev = getattr(self, '_ev_' + which, None)
+        if ev is None:
+            ev = [[torch.cuda.Event() for _ in range(self.K)] for _ in range(self.L)]
+            setattr(self, '_ev_' + which, ev)
+        return ev
+
+    def u_floats(self, l, frames):
+        N, din, J, D, mf = self.layers[l]
+        return self.B * frames * N * self.win * J * D
+
+
+_stack_streams = {}
+
+
+def _layer_streams(dev, n, role):
+    """One stream per layer for the forward or the backward wavefront.  The two roles
+    use disjoint streams: a captured step (hipGraph) that forks the same side streams
+    in the forward (caller's thread) and again in the backward (torch's autograd device
+    thread) crashes at capture end on this ROCm, while forking them twice from one
+    thread, or disjoint streams per role, capture fine (scripts/dbg/capture_probe*.py)."""
+    if os.environ.get('SRF_SDR_STREAMS', '') == '1':   # A/B and debugging: the wavefront on one stream
+        return [torch.cuda.current_stream(dev)] * n
+    ss = _stack_streams.setdefault((dev, role), [])
+    while len(ss) < n:
+        ss.append(torch.cuda.Stream(device=dev))
+    return ss[:n]
+
+
+def _store_u(plan):
+    budget = float(os.environ.get('SRF_SDR_STORE_U_GB', '24')) * 2 ** 30
+    return sum(plan.u_floats(l, plan.T) for l in range(plan.L)) * 4 <= budget
+
+
+class SdrStack(torch.autograd.Function):
+    """emb0 [B,T,N0,din0] -> v of the last layer [B,T,J,D]; in between, layer l's v
+    goes through drop(LN_mid{l+1}(v)) (the CapsNorm of naive:187-191) into layer
+    l+1.  params: W_l, b_l for every layer, then gamma_l, beta_l for l < L-1."""
+
+    @staticmethod
+    def forward(ctx, emb0, plan, training, p_mid, seed, *params):
+        L_ = _lib.lib()
+        P, B, T, L = plan, plan.B, plan.T, plan.L
+        dev = emb0.device
+        Ws, bs = params[0:2 * L:2], params[1:2 * L:2]
+        gammas, betas = params[2 * L::2], params[2 * L + 1::2]
+        _check_dev('emb0', emb0, (B, T, P.layers[0][0], P.layers[0][1]))
+        need_bwd = P.need_bwd
+        store = need_bwd and _store_u(P)
+        tr = int(bool(training))
+        embs, vs, stats, us, rws = [emb0], [], [], [], []
+        for l, (N, din, J, D, mf) in enumerate(P.layers):
+            vs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
+            if l < L - 1:
+                embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
+                stats.append(torch.empty((B * T, 4), device=dev, dtype=torch.float32))
+            us.append(torch.empty(P.u_floats(l, T if store else P.nmax), device=dev, dtype=torch.float32))
+            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
+        main = torch.cuda.current_stream(dev)
+        streams = _layer_streams(dev, L, 'fwd')
+        done = P.events('fwd')
+        for s in streams:
+            s.wait_stream(main)
+        # issue along anti-diagonals d = k + l: the streams share a few hardware queues
+        # (in-order), so items are queued in the order they become ready
+        for k, l in ((d - l, l) for d in range(P.K + L - 1) for l in range(L) if 0 <= d - l < P.K):
+            N, din, J, D, mf = P.layers[l]
+            s = streams[l]
+            t0, t1 = P.fwd[l][k], P.fwd[l][k + 1]
+            if l > 0:
+                s.wait_event(done[l - 1][k])
+            if t1 > t0:
+                sp = ctypes_void(s.cuda_stream)
+                v0, vn = (0, T) if store else (t0, P.nmax)
+                _lib.check(L_.srf_route_sdr_pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din, P.lpad,
+                                                 P.rpad, J, D, t0, t1, _ptr(us[l]), v0, vn, sp), 'sdr_pose')
+                _lib.check(L_.srf_route_sdr_recur_fwd(_ptr(us[l]), v0, vn, B, T, P.in_n(l), J, D, P.iters, mf, t0,
+                                                      t1, _ptr(vs[l]), _ptr(rws[l]), rws[l].numel(), sp),
+                           'sdr_recur_fwd')
+                if l < L - 1:
+                    _lib.check(L_.srf_capsnorm_fwd_range(_ptr(vs[l]), B, T, t0, t1, J * D, _ptr(gammas[l]),
+                                                         _ptr(betas[l]), tr, float(p_mid), int(seed), l,
+                                                         _ptr(embs[l + 1]), _ptr(stats[l]), sp), 'capsnorm_range')
+            done[l][k].record(s)
+        for s in streams:
+            main.wait_stream(s)
+        ctx.plan, ctx.meta = P, (tr, float(p_mid), int(seed), store)
+        ctx.params = params
+        ctx.save_for_backward(*embs, *vs, *stats, *(us if store else []), *params)
+        return vs[-1]
+
+    @staticmethod
+    def backward(ctx, g_v_last):
+        L_ = _lib.lib()
+        P = ctx.plan
+        B, T, L = P.B, P.T, P.L
+        tr, p_mid, seed, store = ctx.meta
+        saved = list(ctx.saved_tensors)
+        embs, saved = saved[:L], saved[L:]
+        vs, saved = saved[:L], saved[L:]
+        stats, saved = saved[:L - 1], saved[L - 1:]
+        if store:
+            us, saved = saved[:L], saved[L:]
+        params = saved
+        Ws, bs = params[0:2 * L:2], params[1:2 * L:2]
+        gammas, betas = params[2 * L::2], params[2 * L + 1::2]
+        dev = g_v_last.device
+        g_v_last = g_v_last.contiguous()
+        targets = [_grad_target(p) for p in ctx.params]
+        gWs, gbs = [targets[2 * l][0] for l in range(L)], [targets[2 * l + 1][0] for l in range(L)]
+        ggs = [targets[2 * L + 2 * l][0] for l in range(L - 1)]
+        gbts = [targets[2 * L + 2 * l + 1][0] for l in range(L - 1)]
+        g_embs = [torch.zeros_like(e) for e in embs]           # gx scatter targets
+        g_vs, gparts, carries, WTs, gus, urs, rws, pws = [], [], [], [], [], [], [], []
+        for l, (N, din, J, D, mf) in enumerate(P.layers):
+            n = J * D
+            g_vs.append(torch.empty((B, T, J, D), device=dev) if l < L - 1 else g_v_last)
+            gparts.append(torch.empty((B * T, 2 * n), device=dev) if l < L - 1 else None)
+            carries.append(torch.zeros((B, n), device=dev))
+            WTs.append(torch.empty(Ws[l].numel(), device=dev))
+            gus.append(torch.empty(P.u_floats(l, P.nmax), device=dev))
+            urs.append(us[l] if store else torch.empty(P.u_floats(l, P.nmax), device=dev))
+            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
+            pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
+                                   dtype=torch.uint8) if l < L - 1 else None)
+        main = torch.cuda.current_stream(dev)
+        streams = _layer_streams(dev, L, 'bwd')
+        done = P.events('bwd')
+        for s in streams:
+            s.wait_stream(main)
+        for l, (N, din, J, D, mf) in enumerate(P.layers):
+            _lib.check(L_.srf_route_sdr_transpose_w(_ptr(Ws[l]), P.in_n(l), J, D, din, _ptr(WTs[l]),
+                                                    ctypes_void(streams[l].cuda_stream)), 'sdr_transpose_w')
+        # anti-diagonals of (range position from the end, layer position from the top)
+        for k, l in ((P.K - 1 - (d - (L - 1 - l)), l) for d in range(P.K + L - 1) for l in reversed(range(L))
+                     if 0 <= d - (L - 1 - l) < P.K):
+            N, din, J, D, mf = P.layers[l]
+            s = streams[l]
+            sp = ctypes_void(s.cuda_stream)
+            t0, t1 = P.bwd[l][k], P.bwd[l][k + 1]
+            if l < L - 1:
+                s.wait_event(done[l + 1][k])
+            if t1 > t0:
+                if l < L - 1:
+                    _lib.check(L_.srf_capsnorm_bwd_range(_ptr(vs[l]), B, T, t0, t1, J * D, _ptr(gammas[l]),
+                                                         _ptr(betas[l]), tr, p_mid, seed, l, _ptr(stats[l]),
+                                                         _ptr(g_embs[l + 1]), _ptr(g_vs[l]), _ptr(gparts[l]), sp),
+                               'capsnorm_bwd_range')
+                v0, vn = (0, T) if store else (t0, P.nmax)
+                if not store:
+                    _lib.check(L_.srf_route_sdr_pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din,
+                                                     P.lpad, P.rpad, J, D, t0, t1, _ptr(urs[l]), v0, vn, sp),
+                               'sdr_pose')
+                _lib.check(L_.srf_route_sdr_recur_bwd(_ptr(urs[l]), v0, vn, _ptr(vs[l]), _ptr(g_vs[l]), B, T,
+                                                      P.in_n(l), J, D, P.iters, mf, t0, t1, _ptr(carries[l]),
+                                                      _ptr(gus[l]), t0, P.nmax, _ptr(rws[l]), rws[l].numel(),
+                                                      sp), 'sdr_recur_bwd')
+                _lib.check(L_.srf_route_sdr_gx(_ptr(gus[l]), t0, P.nmax, _ptr(WTs[l]), B, T, N, din, P.lpad,
+                                               P.rpad, J, D, t0, t1, _ptr(g_embs[l]), sp), 'sdr_gx')
+                _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), t0, P.nmax, _ptr(embs[l]), B, T, N, din, P.lpad,
+                                               P.rpad, J, D, t0, t1, int(k != P.K - 1), _ptr(gWs[l]),
+                                               _ptr(gbs[l]), sp), 'sdr_gw')
+            elif k == P.K - 1:   # empty first range: the accumulation still starts from zero
+                _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), 0, P.nmax, _ptr(embs[l]), B, T, N, din, P.lpad,
+                                               P.rpad, J, D, 0, 0, 0, _ptr(gWs[l]), _ptr(gbs[l]), sp), 'sdr_gw')
+            done[l][k].record(s)
+            if k == 0 and l < L - 1:
+                _lib.check(L_.srf_capsnorm_bwd_params(_ptr(gparts[l]), B * T, J * D, _ptr(ggs[l]),
+                                                      _ptr(gbts[l]), _ptr(pws[l]), pws[l].numel(), sp),
+                           'capsnorm_bwd_params')
+        for s in streams:
+            main.wait_stream(s)
+        return (g_embs[0], None, None, None, None, *_returned(targets))
+
+
+def sdr_stack(emb0, plan, training, p_mid, seed, params):
+    """SdrStack.apply; the forward keeps the pose outputs for the backward only when
+    one will run (grad mode on and something requires a gradient)."""
+    plan.need_bwd = torch.is_grad_enabled() and (emb0.requires_grad or any(p.requires_grad for p in params))
+    return SdrStack.apply(emb0, plan, training, p_mid, seed, *params)

@@ -231,6 +231,17 @@ class SequenceRouter(torch.nn.Module):
             self._geoms[key] = g
         return g
 
+    def _stack_plan(self, B, T):
+        key = ('sdr_stack', B, T)
+        p = self._geoms.get(key)
+        if p is None:
+            layers = []
+            for l, (in_n, out_n, out_d, in_d) in enumerate(self.layer_shapes):
+                layers.append((in_n // self.window, in_d, out_n, out_d, int(l == self.enc_num - 1)))
+            p = ops.SdrStackPlan(B, T, layers, self.lpad, self.rpad, self.route_iters)
+            self._geoms[key] = p
+        return p
+
     def _next_seed(self):
         self._calls += 1
         return (self._seed_base * 0x9E3779B1 + self._calls) % (1 << 63)
@@ -254,6 +265,16 @@ class SequenceRouter(torch.nn.Module):
                                self.proj_scale, self.caps_type == 'einsum')
         B, T2 = emb.shape[:2]
         p_mid = self.inn_dropout if drop else 0.0
+        if self.is_context and self.enc_num > 1 and os.environ.get('SRF_SDR_STACK', '1') != '0':
+            # every SDR layer (and the LN + dropout between them) as one layer-pipelined
+            # wavefront (ops.SdrStack); the head as below
+            last = self.enc_num - 1
+            params = [self.P(f'{w}{l}') for l in range(self.enc_num) for w in ('W', 'b')]
+            params += [self.P(f'ln_mid{l + 1}_{t}') for l in range(last) for t in ('gamma', 'beta')]
+            v = ops.sdr_stack(emb, self._stack_plan(B, T2), training, p_mid, seed, params)
+            return ops.CapsHead.apply(v, self.P(f'ln_mid{last + 1}_gamma'), self.P(f'ln_mid{last + 1}_beta'),
+                                      self.P('ln_output_gamma'), self.P('ln_output_beta'), training, p_mid, seed,
+                                      last, self.length_eps)
         for l in range(self.enc_num):
             route = ops.sequential_routing if self.is_context else ops.dynamic_routing
             W, bias = self._identity.get(l, (self.P(f'W{l}'), self.P(f'b{l}')))

@@ -150,7 +150,7 @@ def test_fused_loss_head_matches_autograd(cuda):
     assert (model.flat_grad - ref).abs().max().item() <= 1e-4 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c2_mini_einsum', 'c4_mini'])
+@pytest.mark.parametrize('name', ['c2_mini', 'c2_mini_lowmemory', 'c2_mini_einsum', 'c4_mini', 'c3_mini_sdr'])
 def test_graphed_train_step_matches_eager(cuda, name):
     """GraphedTrainStep (forward + CTC + backward in one hipGraph) computes the same
     loss and gradient as the eager process_train_step, and draws fresh dropout masks
@@ -237,3 +237,30 @@ def test_graphed_dropout_gradient_matches_finite_difference(cuda):
             assert abs(fd - an) <= 0.02 * abs(float(grad.norm())), (fd, an, float(grad.norm()))
     finally:
         g.close()
+
+
+@pytest.mark.parametrize('name,chunks', [('c3_mini_sdr', 1), ('c3_mini_sdr', 3), ('c3_mini_sdr', 64),
+                                         ('c3_real', 4), ('c5_real', 3), ('c3_mini_sdr_lowmemory', 2)])
+def test_sdr_stack_matches_layer_by_layer(cuda, name, chunks, monkeypatch):
+    """The layer-pipelined SDR stack (ops.SdrStack: frame ranges of every layer as a
+    wavefront over one HIP stream per layer) against the layer-by-layer path
+    (SRF_SDR_STACK=0): the same logits and gradients to fp32 reassociation, for one
+    range, several, and one frame per range (64 > T')."""
+    from srf_amd import ctc
+    outs = []
+    for stack in ('1', '0'):
+        monkeypatch.setenv('SRF_SDR_STACK', stack)
+        monkeypatch.setenv('SRF_SDR_CHUNKS', str(chunks))
+        model, sh, z = _build(name, cuda)
+        feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
+        inp_len = torch.tensor(z['inp_len'], device=cuda)
+        model.zero_grad()
+        logits = model(feats, input_lengths=inp_len, training=True)
+        nll = ctc.ctc_loss(torch.tensor(z['labels'], device=cuda), logits, torch.tensor(z['tar_len'], device=cuda),
+                           (inp_len + 3) // 4, blank_index=sh.class_n - 1)
+        (nll.sum() / feats.shape[0]).backward()
+        torch.cuda.synchronize()
+        outs.append((logits.detach().clone(), model.flat_grad.clone()))
+    (la, ga), (lb, gb) = outs
+    assert (la - lb).abs().max().item() <= 1e-5 * (1 + lb.abs().max().item())
+    assert (ga - gb).abs().max().item() <= 1e-4 * gb.abs().max().item()
