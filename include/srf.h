@@ -137,12 +137,18 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
 int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                        int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream);
 size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters);
+/* Coupling storage per frame (0 when the shape runs on the LDS / global-state
+ * kernels): with couplings != NULL ([B][T][this many floats]) recur_fwd stores each
+ * frame's couplings c^r and pre-squash s^r, and recur_bwd reads them instead of
+ * recomputing the frame's iterations (NULL: recompute). */
+size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters);
 int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
-                            int mask_first, int t0, int t1, float* v_out, void* workspace, size_t workspace_bytes,
-                            void* stream);
-int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved, const float* g_v, int B, int T,
-                            int in_n, int J, int dout, int iters, int mask_first, int t0, int t1, float* carry,
-                            float* gu, int g0, int gn, void* workspace, size_t workspace_bytes, void* stream);
+                            int mask_first, int t0, int t1, float* v_out, float* couplings, void* workspace,
+                            size_t workspace_bytes, void* stream);
+int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved, const float* couplings,
+                            const float* g_v, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                            int t0, int t1, float* carry, float* gu, int g0, int gn, void* workspace,
+                            size_t workspace_bytes, void* stream);
 /* W [in_n][J*dout][din] -> WT [in_n][din][J*dout] (the gx operand). */
 int srf_route_sdr_transpose_w(const float* W, int in_n, int J, int dout, int din, float* WT, void* stream);
 int srf_route_sdr_gx(const float* gu, int g0, int gn, const float* WT, int B, int T, int N, int din, int lpad,

@@ -498,10 +498,11 @@ int pose_range(const SGeom& g, const float* emb, const float* W, const float* bi
 
 // recurrence over one frame range: the register-resident kernels when the shape fits,
 // else the LDS / global-state ones (gstate: B slices of the state, when it exceeds LDS)
-int recur_fwd(const SGeom& g, const float* u, float* v_out, const srf::SeqRange& rg, float* gstate, hipStream_t st) {
+int recur_fwd(const SGeom& g, const float* u, float* v_out, const srf::SeqRange& rg, float* gstate, float* cs,
+              hipStream_t st) {
   if (rg.t0 >= rg.t1) return SRF_OK;
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
-    return srf::sdr_seq_fwd(u, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, v_out, rg, st);
+    return srf::sdr_seq_fwd(u, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, v_out, rg, cs, st);
   const size_t sm = sdr_fwd_smem(g.in_n(), g.J, g.dout);
   if (sdr_gstate(sm))
     hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, g.T, g.in_n(), g.J,
@@ -514,10 +515,11 @@ int recur_fwd(const SGeom& g, const float* u, float* v_out, const srf::SeqRange&
 }
 
 int recur_bwd(const SGeom& g, const float* u, const float* v_saved, const float* g_v, float* gu,
-              const srf::SeqRange& rg, float* gstate, hipStream_t st) {
+              const srf::SeqRange& rg, float* gstate, const float* cs, hipStream_t st) {
   if (rg.t0 >= rg.t1) return SRF_OK;
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
-    return srf::sdr_seq_bwd(u, v_saved, g_v, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, rg, st);
+    return srf::sdr_seq_bwd(u, v_saved, g_v, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, rg, cs,
+                            st);
   const size_t sm = sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters);
   if (sdr_gstate(sm))
     hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, v_saved, g_v, g.T,
@@ -644,7 +646,7 @@ int srf_route_sdr_fwd(const float* emb, const float* W, const float* bias, int B
   float* u = static_cast<float*>(workspace);
   float* gstate = u + srf::align_up((size_t)g.F() * g.in_n() * g.JD() * sizeof(float), 256) / sizeof(float);
   if ((rc = pose_range(g, emb, W, bias, frame_map(T, 0, T, 0, T), u, st))) return rc;
-  if ((rc = recur_fwd(g, u, v_out, srf::SeqRange::whole(T), gstate, st))) return rc;
+  if ((rc = recur_fwd(g, u, v_out, srf::SeqRange::whole(T), gstate, nullptr, st))) return rc;
   SRF_HIP_TRY(hipMemcpyAsync(saved, v_out, (size_t)g.F() * g.JD() * sizeof(float), hipMemcpyDeviceToDevice, st));
   return SRF_OK;
 }
@@ -665,7 +667,7 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
   hipStream_t st = static_cast<hipStream_t>(stream);
   const FrameMap all = frame_map(T, 0, T, 0, T);
   if ((rc = pose_range(g, emb, W, bias, all, w.u, st))) return rc;
-  if ((rc = recur_bwd(g, w.u, saved, g_v, w.gu, srf::SeqRange::whole(T), w.gstate, st))) return rc;
+  if ((rc = recur_bwd(g, w.u, saved, g_v, w.gu, srf::SeqRange::whole(T), w.gstate, nullptr, st))) return rc;
   if ((rc = transpose_w(g, W, w.WT, g_emb, (size_t)g.F() * N * din, st))) return rc;
   if ((rc = gx_range(g, w.gu, w.WT, all, g_emb, st))) return rc;
   return gw_range(g, w.gu, emb, all, 0, g_W, g_bias, st);
@@ -686,30 +688,37 @@ size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters
   return recur_workspace(g);
 }
 
+size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters) {
+  return srf::sdr_seq_cs_floats(in_n, J, dout, iters);
+}
+
 int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
-                            int mask_first, int t0, int t1, float* v_out, void* workspace, size_t workspace_bytes,
-                            void* stream) {
+                            int mask_first, int t0, int t1, float* v_out, float* couplings, void* workspace,
+                            size_t workspace_bytes, void* stream) {
   SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};   // N = in_n, window 1: in_n() = in_n
   int rc = check_sgeom(g);
   if (rc || (rc = range_ok(g, t0, t1, v0, vn))) return rc;
   SRF_REQUIRE(u && v_out, "null pointer argument");
   SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
               "SDR recurrence workspace too small");
+  if (!srf::sdr_seq_cs_floats(in_n, J, dout, iters)) couplings = nullptr;
   return recur_fwd(g, u, v_out, srf::SeqRange{t0, t1, v0, vn, 0, T, nullptr}, static_cast<float*>(workspace),
-                   static_cast<hipStream_t>(stream));
+                   couplings, static_cast<hipStream_t>(stream));
 }
 
-int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved, const float* g_v, int B, int T,
-                            int in_n, int J, int dout, int iters, int mask_first, int t0, int t1, float* carry,
-                            float* gu, int g0, int gn, void* workspace, size_t workspace_bytes, void* stream) {
+int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved, const float* couplings,
+                            const float* g_v, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                            int t0, int t1, float* carry, float* gu, int g0, int gn, void* workspace,
+                            size_t workspace_bytes, void* stream) {
   SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};
   int rc = check_sgeom(g);
   if (rc || (rc = range_ok(g, t0, t1, v0, vn)) || (rc = range_ok(g, t0, t1, g0, gn))) return rc;
   SRF_REQUIRE(u && v_saved && g_v && carry && gu, "null pointer argument");
   SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
               "SDR recurrence workspace too small");
+  if (!srf::sdr_seq_cs_floats(in_n, J, dout, iters)) couplings = nullptr;
   return recur_bwd(g, u, v_saved, g_v, gu, srf::SeqRange{t0, t1, v0, vn, g0, gn, carry},
-                   static_cast<float*>(workspace), static_cast<hipStream_t>(stream));
+                   static_cast<float*>(workspace), couplings, static_cast<hipStream_t>(stream));
 }
 
 int srf_route_sdr_transpose_w(const float* W, int in_n, int J, int dout, int din, float* WT, void* stream) {

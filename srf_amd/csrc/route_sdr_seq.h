@@ -28,13 +28,17 @@ struct SeqRange {
 bool sdr_seq_supported(int in_n, int J, int dout, int iters);
 
 // u [B*T][in_n][J*dout] (pose output) -> v_out [B*T][J*dout]; one workgroup per utterance.
+// cs (optional, [B*T][sdr_seq_cs_floats]): the forward stores each frame's couplings
+// c^r [iters][in_n][JP] and pre-squash s^r [iters][J*dout]; a backward given them
+// skips recomputing the iterations.
+size_t sdr_seq_cs_floats(int in_n, int J, int dout, int iters);
 int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                const SeqRange& rg, hipStream_t st);
+                const SeqRange& rg, float* cs, hipStream_t st);
 
 // Reverse-time pass: recomputes each frame's iterations from v_saved (the
 // forward's v_out), writes gu [B*T][in_n][J*dout] = dL/du.
 int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                int iters, int mask_first, float* gu, const SeqRange& rg, hipStream_t st);
+                int iters, int mask_first, float* gu, const SeqRange& rg, const float* cs, hipStream_t st);
 
 // Template choice for a shape: per-lane input-capsule count NIM in {2, 5, 10} and
 // the iteration bound RM of the backward in {3, 5}.  False when unsupported.

@@ -39,7 +39,7 @@ using namespace srf_seq;
 template <int D, int JP, int NIM>
 __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __restrict__ u, int T, int in_n, int J,
                                                                int iters, int mask_first, float* __restrict__ v_out,
-                                                               srf::SeqRange rg) {
+                                                               srf::SeqRange rg, float* __restrict__ cs) {
   using C = Cfg<D, JP, NIM>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = J * D;
@@ -52,6 +52,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
   float* vo = v_out + (size_t)blockIdx.x * T * JD;
   const bool owner_wave = (tid >> 6) * 64 < JD;   // waves holding elements e = tid < JD
   const bool ev = tid < JD;
+  const size_t csr = (size_t)iters * (in_n * JP + JD);   // coupling record per frame (cs != nullptr)
   if (rg.t0 >= rg.t1) return;
   if (ev) wl[tid] = rg.t0 > 0 ? vo[(size_t)(rg.t0 - 1) * JD + tid] : 0.f;   // v_{t0-1} (v_{-1} = 0)
   float ur[C::NIM][C::KD];
@@ -66,6 +67,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
       lds_slice<C::KD>(wl + L.eoff, L.jv, w);
       logits_softmax<C>(ur, w, L, b, c);
       row_partial<C>(c, ur, L, JD, part);
+      if (cs) store_ij<C>(c, L, cs + ((size_t)blockIdx.x * T + t) * csr + (size_t)r * in_n * JP);
 #if SRF_SEQ_DBG == 1   // timing experiment: re-load the current (cache-hot) frame
       if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(t - rg.tu0) * ff, JD, L, ur);
 #else
@@ -73,10 +75,12 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
 #endif
       __syncthreads();
       if (owner_wave) {
-        const float v = squash_elem<D>(ev ? sum_parts(part, JD, tid) : 0.f);
+        const float s = ev ? sum_parts(part, JD, tid) : 0.f;
+        const float v = squash_elem<D>(s);
         if (ev) {
           wl[tid] = v;
           if (r == iters - 1) vo[(size_t)t * JD + tid] = v;
+          if (cs) cs[((size_t)blockIdx.x * T + t) * csr + (size_t)iters * in_n * JP + r * JD + tid] = s;
         }
       }
       __syncthreads();
@@ -90,22 +94,23 @@ size_t fwd_lds(int J, int D) {
 
 template <int D, int JP, int NIM>
 int launch_fwd(const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
-               const srf::SeqRange& rg, hipStream_t st) {
+               const srf::SeqRange& rg, float* cs, hipStream_t st) {
   const size_t lds = fwd_lds(J, D);
   auto k = sdr_seq_fwd_kernel<D, JP, NIM>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, T, in_n, J, iters, mask_first, v_out, rg);
+  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, T, in_n, J, iters, mask_first, v_out, rg, cs);
   SRF_LAUNCH_CHECK("sdr_seq_fwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
 int fwd_nim(int nim, const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
-            const srf::SeqRange& rg, hipStream_t st) {
-  if (nim == 2) return launch_fwd<D, JP, 2>(u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
-  if (nim == 5) return launch_fwd<D, JP, 5>(u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
-  if constexpr (seq_kd(D, JP) <= 8) return launch_fwd<D, JP, 10>(u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
+            const srf::SeqRange& rg, float* cs, hipStream_t st) {
+  if (nim == 2) return launch_fwd<D, JP, 2>(u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
+  if (nim == 5) return launch_fwd<D, JP, 5>(u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
+  if constexpr (seq_kd(D, JP) <= 8)
+    return launch_fwd<D, JP, 10>(u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
   srf::set_error("sdr_seq: no forward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -137,8 +142,13 @@ bool sdr_seq_supported(int in_n, int J, int dout, int iters) {
   return sdr_seq_plan(in_n, J, dout, iters, nullptr, nullptr);
 }
 
+size_t sdr_seq_cs_floats(int in_n, int J, int dout, int iters) {
+  if (!sdr_seq_supported(in_n, J, dout, iters)) return 0;
+  return (size_t)iters * ((size_t)in_n * srf_seq::pow2_at_least(J) + (size_t)J * dout);
+}
+
 int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                const SeqRange& rg, hipStream_t st) {
+                const SeqRange& rg, float* cs, hipStream_t st) {
   int nim = 0, rm = 0;
   if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
@@ -146,7 +156,7 @@ int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int ite
   }
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_F(DD, PP) \
-  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, u, B, T, in_n, J, iters, mask_first, v_out, rg, st);
+  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
   SRF_SEQ_CASES(SRF_SEQ_F)
 #undef SRF_SEQ_F
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

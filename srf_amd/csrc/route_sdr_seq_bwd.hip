@@ -29,12 +29,19 @@ using namespace srf_seq;
 constexpr bool cl_wanted(int nim, int kd) { return nim * kd >= 40; }
 
 // LDS: w [JDa], Vc [RM][JDa], gs [RM][JDa], part [16][JD] (+ c, gL [RM][in_n][JP]).
-template <int D, int JP, int NIM, int RM, bool CL>
+// CS: the forward stored each frame's couplings c^r and s^r (srf::sdr_seq_cs_floats
+// per frame): the backward reads them instead of recomputing the R iterations, so
+// only the adjoint runs per frame (and the logits no longer hold registers).
+// With CS the lane keeps only its first KR rows of u in registers and re-reads the
+// others from L2 where the adjoint uses them (once per iteration), and the gu pass
+// accumulates GR rows at a time per LDS read of gs^r / Vc^r: the J = 32 last layer
+// otherwise needs more than the 128 registers a 1024-thread workgroup allows.
+template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, int GR = NIM>
 __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __restrict__ u,
                                                                const float* __restrict__ v_saved,
                                                                const float* __restrict__ g_v, int T, int in_n, int J,
                                                                int iters, int mask_first, float* __restrict__ gu,
-                                                               srf::SeqRange rg) {
+                                                               srf::SeqRange rg, const float* __restrict__ cs) {
   using C = Cfg<D, JP, NIM>;
   constexpr int RR = CL ? 1 : RM;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -59,12 +66,13 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
   float* carry_io = rg.carry ? rg.carry + (size_t)blockIdx.x * JD : nullptr;
   // dL/dv_t carried back from frame t+1 (owner threads), from the later range
   float carry = (carry_io && ev) ? carry_io[tid] : 0.f;
-  float ur[C::NIM][C::KD];
+  constexpr int KRES = CS ? KR : C::NIM;   // rows of u held in registers
+  float ur[KRES][C::KD];
   float cr[RR][C::NIM], gl[RR][C::NIM];
   float sr[RM];        // s^r of the owned element
 #pragma unroll
   for (int r = 0; r < RM; ++r) sr[r] = 0.f;
-  load_frame<C>(ub + (size_t)(rg.t1 - 1 - rg.tu0) * ff, JD, L, ur);
+  load_rows<C, KRES>(ub + (size_t)(rg.t1 - 1 - rg.tu0) * ff, JD, L, ur);
   for (int t = rg.t1 - 1; t >= rg.t0; --t) {
     const size_t f = f0 + t;
     float a = 0.f;
@@ -75,6 +83,36 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
       a = g_v[f * JD + tid] + carry;       // dL/dv^{R-1}
       carry = 0.f;
     }
+    if constexpr (CS) {
+      // ---- the forward's c^r, s^r of this frame; Vc^{r+1} = Vc^r + squash(s^r)
+      const int P = in_n * JP;
+      const float* rec = cs + f * (size_t)R * (P + JD);
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        if (r < R) {
+          if constexpr (CL) {
+            for (int idx = tid; idx < P; idx += kThreads) cl[r * P + idx] = rec[r * P + idx];
+          } else {
+            load_ij<C>(rec + r * P, L, cr[r]);
+          }
+        }
+      }
+      __syncthreads();   // Vc^0 (above) before the owner threads extend it
+      if (owner_wave) {
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          if (r < R) {
+            const float s = ev ? rec[(size_t)R * P + r * JD + tid] : 0.f;
+            sr[r] = s;
+            if (r + 1 < R) {
+              const float v = squash_elem<D>(s);
+              if (ev) vcl[(r + 1) * JDa + tid] = vcl[r * JDa + tid] + v;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    } else {
     __syncthreads();
     // ---- recompute the frame's iterations: c^r, s^r, Vc^r
     float b[C::NIM];
@@ -106,6 +144,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
         __syncthreads();
       }
     }
+    }   // recompute
     // ---- adjoint, r = R-1 .. 0 (a = dL/dv^r)
     float grun = 0.f;
 #pragma unroll
@@ -130,6 +169,46 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
 #pragma unroll
           for (int k = 0; k < C::NIM; ++k) cc[k] = cr[r][k];
         }
+        if constexpr (CS) {
+          // rows in registers (k < KR): q, sigma, gL first; then the rows re-read from L2
+          // one at a time (q, sigma, gL and their gVc share); then the resident rows' share
+          auto adjoint = [&](int k, const float (&urow)[C::KD]) {
+            float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+            for (int d = 0; d < C::KD; d += 2) {
+              p0 += urow[d] * gsv[d];
+              p1 += urow[d + 1] * gsv[d + 1];
+            }
+            const float q = group_sum<1, C::Q>(p0 + p1);
+            const float sig = group_sum<C::Q, C::ROWL>(cc[k] * q);
+            gg[k] = cc[k] * (q - sig);
+          };
+#pragma unroll
+          for (int k = 0; k < C::NIM; ++k) {
+            gg[k] = 0.f;
+            if (k < KR && k < L.NI) adjoint(k, ur[k < KR ? k : 0]);
+          }
+          float sp[C::KD];
+#pragma unroll
+          for (int d = 0; d < C::KD; ++d) sp[d] = 0.f;
+          const float* uf = ub + (size_t)(t - rg.tu0) * ff;
+#pragma unroll
+          for (int k = KR; k < C::NIM; ++k) {
+            __builtin_amdgcn_sched_barrier(0);   // one re-read row in flight at a time
+            if (k < L.NI) {
+              float urow[C::KD];
+              lds_slice<C::KD>(uf + (size_t)(L.g + k * C::G) * JD + L.eoff, L.jv, urow);
+              adjoint(k, urow);
+#pragma unroll
+              for (int d = 0; d < C::KD; ++d) sp[d] += gg[k] * urow[d];
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < KR; ++k)
+#pragma unroll
+            for (int d = 0; d < C::KD; ++d) sp[d] += gg[k] * ur[k][d];
+          partial_out<C>(sp, L, JD, part);
+        } else {
 #pragma unroll
         for (int k = 0; k < C::NIM; ++k) {
           gg[k] = 0.f;
@@ -146,6 +225,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
           }
         }
         row_partial<C>(gg, ur, L, JD, part);
+        }   // CS
         if constexpr (CL) {
           store_ij<C>(gg, L, gll + r * in_n * JP);
         } else {
@@ -162,7 +242,53 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
       }
     }
     // ---- gu, one input capsule of the lane at a time (u is dead: its registers
-    // take the next frame's loads, issued right after)
+    // take the next frame's loads, issued right after); with CS, GR capsules per
+    // read of gs^r / Vc^r
+    if constexpr (CS) {
+#pragma unroll
+      for (int k0 = 0; k0 < C::NIM; k0 += GR) {
+        float acc[GR][C::KD];
+#pragma unroll
+        for (int kk = 0; kk < GR; ++kk)
+#pragma unroll
+          for (int d = 0; d < C::KD; ++d) acc[kk][d] = 0.f;
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          if (r < R) {
+            float gsv[C::KD], vcv[C::KD];
+            lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
+            lds_slice<C::KD>(vcl + r * JDa + L.eoff, L.jv, vcv);
+#pragma unroll
+            for (int kk = 0; kk < GR; ++kk) {
+              const int k = k0 + kk;
+              if (k < C::NIM && k < L.NI) {
+                float ck, gk;
+                if constexpr (CL) {
+                  const int idx = (L.g + k * C::G) * JP + L.j;
+                  ck = cl[r * in_n * JP + idx];
+                  gk = gll[r * in_n * JP + idx];
+                } else {
+                  ck = cr[r][k < C::NIM ? k : 0];
+                  gk = gl[r][k < C::NIM ? k : 0];
+                }
+#pragma unroll
+                for (int d = 0; d < C::KD; ++d) acc[kk][d] += ck * gsv[d] + gk * vcv[d];
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < GR; ++kk) {
+          const int k = k0 + kk;
+          if (k < C::NIM && k < L.NI && L.jv) {
+            float* dst = gub + (size_t)(t - rg.tg0) * ff + (size_t)(L.g + k * C::G) * JD + L.eoff;
+#pragma unroll
+            for (int c = 0; c < C::KD; c += 4)
+              *reinterpret_cast<f4*>(dst + c) = f4{acc[kk][c], acc[kk][c + 1], acc[kk][c + 2], acc[kk][c + 3]};
+          }
+        }
+      }
+    } else {
 #pragma unroll
     for (int k = 0; k < C::NIM; ++k) {
       if (k < L.NI) {
@@ -195,7 +321,8 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
         }
       }
     }
-    if (t > rg.t0) load_frame<C>(ub + (size_t)(t - 1 - rg.tu0) * ff, JD, L, ur);
+    }   // CS gu
+    if (t > rg.t0) load_rows<C, KRES>(ub + (size_t)(t - 1 - rg.tu0) * ff, JD, L, ur);
     __syncthreads();   // the next frame overwrites w, Vc^0 and the c / gL slabs
   }
   if (carry_io && ev) carry_io[tid] = carry;   // dL/dv_{t0-1} for the earlier range
@@ -210,26 +337,34 @@ size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
 
 template <int D, int JP, int NIM, int RM>
 int launch_bwd(const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J, int iters,
-               int mask_first, float* gu, const srf::SeqRange& rg, hipStream_t st) {
+               int mask_first, float* gu, const srf::SeqRange& rg, const float* cs, hipStream_t st) {
   constexpr bool want = cl_wanted(NIM, seq_kd(D, JP));
   const bool cl = want && bwd_lds(J, D, RM, in_n, true) <= 160 * 1024;
   const size_t lds = bwd_lds(J, D, RM, in_n, cl);
-  auto k = cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want> : sdr_seq_bwd_kernel<D, JP, NIM, RM, false>;
+  // with stored couplings: rows past KR re-read from L2 when u would take more than 48
+  // of the 128 registers (the J = 32, dout = 32 last layer: 5 rows of 16 values)
+  constexpr int KD = seq_kd(D, JP);
+  constexpr int KR = NIM * KD > 48 ? 32 / KD : NIM;
+  constexpr int GR = 1;
+  auto k = cs ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, GR>
+                    : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, GR>)
+              : (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, false>
+                    : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, false>);
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, vs, gv, T, in_n, J, iters, mask_first, gu, rg);
+  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, vs, gv, T, in_n, J, iters, mask_first, gu, rg, cs);
   SRF_LAUNCH_CHECK("sdr_seq_bwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
 int bwd_nim(int nim, int rm, const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J,
-            int iters, int mask_first, float* gu, const srf::SeqRange& rg, hipStream_t st) {
-  if (rm == 5) return launch_bwd<D, JP, 2, 5>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
-  if (nim == 2) return launch_bwd<D, JP, 2, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
-  if (nim == 5) return launch_bwd<D, JP, 5, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
+            int iters, int mask_first, float* gu, const srf::SeqRange& rg, const float* cs, hipStream_t st) {
+  if (rm == 5) return launch_bwd<D, JP, 2, 5>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
+  if (nim == 2) return launch_bwd<D, JP, 2, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
+  if (nim == 5) return launch_bwd<D, JP, 5, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
   if constexpr (seq_kd(D, JP) <= 8)
-    return launch_bwd<D, JP, 10, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, st);
+    return launch_bwd<D, JP, 10, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
   srf::set_error("sdr_seq: no backward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -239,7 +374,7 @@ int bwd_nim(int nim, int rm, const float* u, const float* vs, const float* gv, i
 namespace srf {
 
 int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                int iters, int mask_first, float* gu, const SeqRange& rg, hipStream_t st) {
+                int iters, int mask_first, float* gu, const SeqRange& rg, const float* cs, hipStream_t st) {
   int nim = 0, rm = 0;
   if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
@@ -248,7 +383,7 @@ int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, i
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_B(DD, PP)     \
   if (dout == DD && JP == PP) \
-    return bwd_nim<DD, PP>(nim, rm, u, v_saved, g_v, B, T, in_n, J, iters, mask_first, gu, rg, st);
+    return bwd_nim<DD, PP>(nim, rm, u, v_saved, g_v, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
   SRF_SEQ_CASES(SRF_SEQ_B)
 #undef SRF_SEQ_B
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

@@ -170,6 +170,38 @@ __device__ __forceinline__ void load_frame(const float* __restrict__ ut, int JD,
   }
 }
 
+// the lane's first KR rows of u_t -> registers (load_frame for KR = NIM)
+template <class C, int KR>
+__device__ __forceinline__ void load_rows(const float* __restrict__ ut, int JD, const Lane& L,
+                                          float (&ur)[KR][C::KD]) {
+#pragma unroll
+  for (int k = 0; k < KR; ++k) {
+    const bool ok = L.jv && k < L.NI;
+    const float* p = ut + (size_t)(L.g + k * C::G) * JD + L.eoff;
+#pragma unroll
+    for (int c = 0; c < C::KD; c += 4) {
+      f4 x = {0.f, 0.f, 0.f, 0.f};
+      if (ok) x = *reinterpret_cast<const f4*>(p + c);
+      ur[k][c] = x.x;
+      ur[k][c + 1] = x.y;
+      ur[k][c + 2] = x.z;
+      ur[k][c + 3] = x.w;
+    }
+  }
+}
+
+// sp summed over the wave's rows; the first row's lanes write it to part[wave][eoff ..]
+template <class C>
+__device__ __forceinline__ void partial_out(float (&sp)[C::KD], const Lane& L, int JD, float* __restrict__ part) {
+#pragma unroll
+  for (int d = 0; d < C::KD; ++d) sp[d] = group_sum<C::ROWL, 64>(sp[d]);
+  if (L.jv && (threadIdx.x & 63) < C::ROWL) {
+    float* dst = part + (threadIdx.x >> 6) * JD + L.eoff;
+#pragma unroll
+    for (int c = 0; c < C::KD; c += 4) *reinterpret_cast<f4*>(dst + c) = f4{sp[c], sp[c + 1], sp[c + 2], sp[c + 3]};
+  }
+}
+
 template <int KD>
 __device__ __forceinline__ void lds_slice(const float* __restrict__ src, bool ok, float (&w)[KD]) {
 #pragma unroll

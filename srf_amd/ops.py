@@ -545,9 +545,13 @@ class SdrStack(torch.autograd.Function):
         need_bwd = P.need_bwd
         store = need_bwd and _store_u(P)
         tr = int(bool(training))
-        embs, vs, stats, us, rws = [emb0], [], [], [], []
+        embs, vs, stats, us, rws, css = [emb0], [], [], [], [], []
         for l, (N, din, J, D, mf) in enumerate(P.layers):
             vs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
+            # each frame's couplings and s^r, for a backward without the recompute
+            ncs = L_.srf_route_sdr_coupling_floats(P.in_n(l), J, D, P.iters) \
+                if need_bwd and os.environ.get('SRF_SDR_CS', '1') != '0' else 0
+            css.append(torch.empty(B * T * ncs, device=dev, dtype=torch.float32) if ncs else None)
             if l < L - 1:
                 embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
                 stats.append(torch.empty((B * T, 4), device=dev, dtype=torch.float32))
@@ -572,8 +576,8 @@ class SdrStack(torch.autograd.Function):
                 _lib.check(L_.srf_route_sdr_pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din, P.lpad,
                                                  P.rpad, J, D, t0, t1, _ptr(us[l]), v0, vn, sp), 'sdr_pose')
                 _lib.check(L_.srf_route_sdr_recur_fwd(_ptr(us[l]), v0, vn, B, T, P.in_n(l), J, D, P.iters, mf, t0,
-                                                      t1, _ptr(vs[l]), _ptr(rws[l]), rws[l].numel(), sp),
-                           'sdr_recur_fwd')
+                                                      t1, _ptr(vs[l]), _ptr(css[l]) if css[l] is not None else None,
+                                                      _ptr(rws[l]), rws[l].numel(), sp), 'sdr_recur_fwd')
                 if l < L - 1:
                     _lib.check(L_.srf_capsnorm_fwd_range(_ptr(vs[l]), B, T, t0, t1, J * D, _ptr(gammas[l]),
                                                          _ptr(betas[l]), tr, float(p_mid), int(seed), l,
@@ -583,6 +587,7 @@ class SdrStack(torch.autograd.Function):
             main.wait_stream(s)
         ctx.plan, ctx.meta = P, (tr, float(p_mid), int(seed), store)
         ctx.params = params
+        ctx.css = css
         ctx.save_for_backward(*embs, *vs, *stats, *(us if store else []), *params)
         return vs[-1]
 
@@ -648,7 +653,9 @@ class SdrStack(torch.autograd.Function):
                     _lib.check(L_.srf_route_sdr_pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din,
                                                      P.lpad, P.rpad, J, D, t0, t1, _ptr(urs[l]), v0, vn, sp),
                                'sdr_pose')
-                _lib.check(L_.srf_route_sdr_recur_bwd(_ptr(urs[l]), v0, vn, _ptr(vs[l]), _ptr(g_vs[l]), B, T,
+                cs = ctx.css[l]
+                _lib.check(L_.srf_route_sdr_recur_bwd(_ptr(urs[l]), v0, vn, _ptr(vs[l]),
+                                                      _ptr(cs) if cs is not None else None, _ptr(g_vs[l]), B, T,
                                                       P.in_n(l), J, D, P.iters, mf, t0, t1, _ptr(carries[l]),
                                                       _ptr(gus[l]), t0, P.nmax, _ptr(rws[l]), rws[l].numel(),
                                                       sp), 'sdr_recur_bwd')
@@ -667,6 +674,7 @@ class SdrStack(torch.autograd.Function):
                            'capsnorm_bwd_params')
         for s in streams:
             main.wait_stream(s)
+        ctx.css = None
         return (g_embs[0], None, None, None, None, *_returned(targets))
 
 

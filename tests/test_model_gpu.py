@@ -239,14 +239,17 @@ def test_graphed_dropout_gradient_matches_finite_difference(cuda):
         g.close()
 
 
-@pytest.mark.parametrize('name,chunks', [('c3_mini_sdr', 1), ('c3_mini_sdr', 3), ('c3_mini_sdr', 64),
-                                         ('c3_real', 4), ('c5_real', 3), ('c3_mini_sdr_lowmemory', 2)])
-def test_sdr_stack_matches_layer_by_layer(cuda, name, chunks, monkeypatch):
+@pytest.mark.parametrize('name,chunks,cs', [('c3_mini_sdr', 1, '1'), ('c3_mini_sdr', 3, '1'), ('c3_mini_sdr', 64, '1'),
+                                            ('c3_real', 4, '1'), ('c3_real', 4, '0'), ('c5_real', 3, '1'),
+                                            ('c3_mini_sdr_lowmemory', 2, '1')])
+def test_sdr_stack_matches_layer_by_layer(cuda, name, chunks, cs, monkeypatch):
     """The layer-pipelined SDR stack (ops.SdrStack: frame ranges of every layer as a
     wavefront over one HIP stream per layer) against the layer-by-layer path
     (SRF_SDR_STACK=0): the same logits and gradients to fp32 reassociation, for one
-    range, several, and one frame per range (64 > T')."""
+    range, several, and one frame per range (64 > T'); its backward from the
+    forward's stored couplings (SRF_SDR_CS=1) and recomputing them (0)."""
     from srf_amd import ctc
+    monkeypatch.setenv('SRF_SDR_CS', cs)
     outs = []
     for stack in ('1', '0'):
         monkeypatch.setenv('SRF_SDR_STACK', stack)
