@@ -48,7 +48,8 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / f16 MFMA peak
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`, averaged per dispatch by
 # scripts/pmcsum.py (KiB per dispatch), per workload
-PMC_TRAFFIC = {'timit_c2': os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4h.json')}
+PMC_TRAFFIC = {'timit_c2': os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4h.json'),
+               'wsj_c4': os.path.join(HERE, 'profiles', 'r03_pmc_traffic_c4.json')}
 
 
 def make_config(kw):
@@ -274,8 +275,9 @@ def measure(workload, args, world, rank, dev):
 
     traffic, traffic_src = None, PMC_TRAFFIC.get(workload)
     if fwd32 and traffic_src:
+        tw = 4 if (Din < 32 or J * D > 512) else 2     # row tiles per wave (route_fwd32.hip Fwd32Plan::TW)
         traffic = pmc_traffic(traffic_src, [f'void route_fwd32_first_kernel<{Din}, {D}>',
-                                            f'void route_fwd32_kernel<{Din}, {D}, '], [1.0, R - 1.0])
+                                            f'void route_fwd32_kernel<{Din}, {D}, 8, {tw}>'], [1.0, R - 1.0])
     res = {
         'value': round(B * T * world * args.steps / elapsed, 1), 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
         'config': {'workload': f'{workload}: SRF L={cfg.model_encoder_num} PH=CH={cfg.model_caps_primary_num} '

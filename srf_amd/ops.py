@@ -529,6 +529,15 @@ def _store_u(plan):
     return sum(plan.u_floats(l, plan.T) for l in range(plan.L)) * 4 <= budget
 
 
+def _whole_gu(plan):
+    """Keep each layer's whole gu (instead of one frame range at a time) so its weight
+    gradient runs once per layer, off the wavefront, on a stream of its own.  Off by
+    default (SRF_SDR_WHOLE_GU_GB=0): at C3 the concurrent gW passes slow the
+    latency-bound recurrences more than they save (32.2 vs 30.6 ms per step)."""
+    budget = float(os.environ.get('SRF_SDR_WHOLE_GU_GB', '0')) * 2 ** 30
+    return sum(plan.u_floats(l, plan.T) for l in range(plan.L)) * 4 <= budget
+
+
 class SdrStack(torch.autograd.Function):
     """emb0 [B,T,N0,din0] -> v of the last layer [B,T,J,D]; in between, layer l's v
     goes through drop(LN_mid{l+1}(v)) (the CapsNorm of naive:187-191) into layer
@@ -608,6 +617,7 @@ class SdrStack(torch.autograd.Function):
         gammas, betas = params[2 * L::2], params[2 * L + 1::2]
         dev = g_v_last.device
         g_v_last = g_v_last.contiguous()
+        whole_gu = _whole_gu(P)
         targets = [_grad_target(p) for p in ctx.params]
         gWs, gbs = [targets[2 * l][0] for l in range(L)], [targets[2 * l + 1][0] for l in range(L)]
         ggs = [targets[2 * L + 2 * l][0] for l in range(L - 1)]
@@ -620,13 +630,15 @@ class SdrStack(torch.autograd.Function):
             gparts.append(torch.empty((B * T, 2 * n), device=dev) if l < L - 1 else None)
             carries.append(torch.zeros((B, n), device=dev))
             WTs.append(torch.empty(Ws[l].numel(), device=dev))
-            gus.append(torch.empty(P.u_floats(l, P.nmax), device=dev))
+            gus.append(torch.empty(P.u_floats(l, T if whole_gu else P.nmax), device=dev))
             urs.append(us[l] if store else torch.empty(P.u_floats(l, P.nmax), device=dev))
             rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
             pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
                                    dtype=torch.uint8) if l < L - 1 else None)
         main = torch.cuda.current_stream(dev)
         streams = _layer_streams(dev, L, 'bwd')
+        ws = _layer_streams(dev, 1, 'weights')[0]
+        ws.wait_stream(main)
         done = P.events('bwd')
         for s in streams:
             s.wait_stream(main)
@@ -654,25 +666,34 @@ class SdrStack(torch.autograd.Function):
                                                      P.lpad, P.rpad, J, D, t0, t1, _ptr(urs[l]), v0, vn, sp),
                                'sdr_pose')
                 cs = ctx.css[l]
+                g0, gn = (0, T) if whole_gu else (t0, P.nmax)
                 _lib.check(L_.srf_route_sdr_recur_bwd(_ptr(urs[l]), v0, vn, _ptr(vs[l]),
                                                       _ptr(cs) if cs is not None else None, _ptr(g_vs[l]), B, T,
                                                       P.in_n(l), J, D, P.iters, mf, t0, t1, _ptr(carries[l]),
-                                                      _ptr(gus[l]), t0, P.nmax, _ptr(rws[l]), rws[l].numel(),
+                                                      _ptr(gus[l]), g0, gn, _ptr(rws[l]), rws[l].numel(),
                                                       sp), 'sdr_recur_bwd')
-                _lib.check(L_.srf_route_sdr_gx(_ptr(gus[l]), t0, P.nmax, _ptr(WTs[l]), B, T, N, din, P.lpad,
+                _lib.check(L_.srf_route_sdr_gx(_ptr(gus[l]), g0, gn, _ptr(WTs[l]), B, T, N, din, P.lpad,
                                                P.rpad, J, D, t0, t1, _ptr(g_embs[l]), sp), 'sdr_gx')
-                _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), t0, P.nmax, _ptr(embs[l]), B, T, N, din, P.lpad,
-                                               P.rpad, J, D, t0, t1, int(k != P.K - 1), _ptr(gWs[l]),
-                                               _ptr(gbs[l]), sp), 'sdr_gw')
-            elif k == P.K - 1:   # empty first range: the accumulation still starts from zero
+                if not whole_gu:
+                    _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), t0, P.nmax, _ptr(embs[l]), B, T, N, din, P.lpad,
+                                                   P.rpad, J, D, t0, t1, int(k != P.K - 1), _ptr(gWs[l]),
+                                                   _ptr(gbs[l]), sp), 'sdr_gw')
+            elif k == P.K - 1 and not whole_gu:   # empty first range: the accumulation still starts from zero
                 _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), 0, P.nmax, _ptr(embs[l]), B, T, N, din, P.lpad,
                                                P.rpad, J, D, 0, 0, 0, _ptr(gWs[l]), _ptr(gbs[l]), sp), 'sdr_gw')
             done[l][k].record(s)
+            if k == 0 and whole_gu:
+                # the layer's whole gu is written: its gW / gbias on the weights stream,
+                # overlapping the recurrences of the layers below
+                ws.wait_event(done[l][0])
+                _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), 0, T, _ptr(embs[l]), B, T, N, din, P.lpad, P.rpad,
+                                               J, D, 0, T, 0, _ptr(gWs[l]), _ptr(gbs[l]),
+                                               ctypes_void(ws.cuda_stream)), 'sdr_gw')
             if k == 0 and l < L - 1:
                 _lib.check(L_.srf_capsnorm_bwd_params(_ptr(gparts[l]), B * T, J * D, _ptr(ggs[l]),
                                                       _ptr(gbts[l]), _ptr(pws[l]), pws[l].numel(), sp),
                            'capsnorm_bwd_params')
-        for s in streams:
+        for s in streams + [ws]:
             main.wait_stream(s)
         ctx.css = None
         return (g_embs[0], None, None, None, None, *_returned(targets))
