@@ -61,10 +61,31 @@ struct FrameMap {
   __device__ __forceinline__ size_t view(int b, int t) const { return (size_t)b * vn + (t - v0); }
 };
 
+// KS consecutive floats (float4 loads when KS is a multiple of 4), zeros when !ok
+template <int KS>
+__device__ __forceinline__ void load_ks(const float* __restrict__ p, bool ok, float (&v)[KS]) {
+  if constexpr (KS % 4 == 0) {
+#pragma unroll
+    for (int k = 0; k < KS; k += 4) {
+      f4 q = {0.f, 0.f, 0.f, 0.f};
+      if (ok) q = *reinterpret_cast<const f4*>(p + k);
+      v[k] = q.x;
+      v[k + 1] = q.y;
+      v[k + 2] = q.z;
+      v[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) v[k] = ok ? p[k] : 0.f;
+  }
+}
+
 // ------------------------------------------------------------------ pose
-// Workgroup = 4 waves over one frame tile (16 frames) and one capsule i; wave w
-// takes row tiles w, w+4, ...  Operands as in the DR pass (k-permuted MFMA).
-template <int DIN>
+// Workgroup = 4 waves over FT frame tiles (16 frames each) and one capsule i; wave w
+// takes row tiles w, w+4, ..., each W fragment (loaded as float4s) feeding the FT
+// frame tiles.  Operands as in the DR pass (k-permuted MFMA: lane group g holds K
+// elements g*KS .. g*KS + KS-1 of both operands).
+template <int DIN, int FT>
 __global__ __launch_bounds__(256) void sdr_pose_kernel(const float* __restrict__ emb, const float* __restrict__ W,
                                                        const float* __restrict__ bias, int Q, FrameMap fm, int N,
                                                        int lpad, int in_n, int JD, float* __restrict__ u) {
@@ -73,26 +94,38 @@ __global__ __launch_bounds__(256) void sdr_pose_kernel(const float* __restrict__
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fl = lane & 15, g = lane >> 4;
   const int i = blockIdx.y;
-  const int q = blockIdx.x * 16 + fl;
-  int b, t;
-  fm.frame(min(q, Q - 1), b, t);
   const int w = i / N, n = i - w * N;
-  const int ts = t + w - lpad;
-  const bool ok = q < Q && ts >= 0 && ts < T;
-  float x[KS];
-  const float* xp = emb + ((size_t)(b * T + min(max(ts, 0), T - 1)) * N + n) * DIN + g * KS;
+  float x[FT][KS];
+  int qq[FT], bb[FT], tt[FT];
 #pragma unroll
-  for (int k = 0; k < KS; ++k) x[k] = ok ? xp[k] : 0.f;
+  for (int ft = 0; ft < FT; ++ft) {
+    qq[ft] = (blockIdx.x * FT + ft) * 16 + fl;
+    fm.frame(min(qq[ft], Q - 1), bb[ft], tt[ft]);
+    const int ts = tt[ft] + w - lpad;
+    const bool ok = qq[ft] < Q && ts >= 0 && ts < T;
+    const float* xp = emb + ((size_t)(bb[ft] * T + min(max(ts, 0), T - 1)) * N + n) * DIN + g * KS;
+    load_ks<KS>(xp, ok, x[ft]);
+  }
   const int NT = (JD + 15) / 16;
   for (int tile = wv; tile < NT; tile += 4) {
     const int arow = min(tile * 16 + fl, JD - 1);
     const float* wp = W + ((size_t)i * JD + arow) * DIN + g * KS;
+    float a[KS];
+    load_ks<KS>(wp, true, a);
     const int crow = min(tile * 16 + 4 * g, JD - 4);
-    f4 acc = *reinterpret_cast<const f4*>(bias + (size_t)i * JD + crow);
+    const f4 b4 = *reinterpret_cast<const f4*>(bias + (size_t)i * JD + crow);
+    f4 acc[FT];
 #pragma unroll
-    for (int k = 0; k < KS; ++k) acc = mfma16x16x4(wp[k], x[k], acc);
+    for (int ft = 0; ft < FT; ++ft) acc[ft] = b4;
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+      for (int ft = 0; ft < FT; ++ft) acc[ft] = mfma16x16x4(a[k], x[ft][k], acc[ft]);
     const int row = tile * 16 + 4 * g;
-    if (q < Q && row < JD) *reinterpret_cast<f4*>(u + (fm.view(b, t) * in_n + i) * JD + row) = acc;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft)
+      if (qq[ft] < Q && row < JD)
+        *reinterpret_cast<f4*>(u + (fm.view(bb[ft], tt[ft]) * in_n + i) * JD + row) = acc[ft];
   }
 }
 
@@ -482,9 +515,11 @@ int pose_range(const SGeom& g, const float* emb, const float* W, const float* bi
                hipStream_t st) {
   const int Q = g.B * fm.nt;
   if (Q == 0) return SRF_OK;
-  const dim3 grid((Q + 15) / 16, g.in_n());
-#define SRF_POSE(DIN) \
-  hipLaunchKernelGGL(sdr_pose_kernel<DIN>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(), g.JD(), u)
+  constexpr int FT = 2;   // frame tiles per workgroup: each W fragment feeds two MFMA chains
+  const dim3 grid((Q + 16 * FT - 1) / (16 * FT), g.in_n());
+#define SRF_POSE(DIN)                                                                                            \
+  hipLaunchKernelGGL((sdr_pose_kernel<DIN, FT>), grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(), \
+                     g.JD(), u)
   switch (g.din) {
     case 8: SRF_POSE(8); break;
     case 16: SRF_POSE(16); break;
