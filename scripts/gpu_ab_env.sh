@@ -10,5 +10,5 @@ for v in "${VS[@]}"; do
   i=$((i+1))
   env $v timeout -k 10 300 python -u bench.py --workload ${WL:-wsj_c3} --extra= --no-cpu-baseline --steps ${STEPS:-5} \
     --warmup 2 > $OUT/v$i.json 2> $OUT/v$i.err || { echo "variant [$v] failed"; tail -5 $OUT/v$i.err; exit 1; }
-  python -c "import json,sys; d=json.load(open('$OUT/v$i.json')); print('[$v]', d['ms_per_step'], 'ms', d['forward_only']['ms_per_step'], 'fwd ms')"
+  python -c "import json,sys; d=json.load(open('$OUT/v$i.json')); r=d['roofline'] or {}; print('[$v]', d['ms_per_step'], 'ms', d['forward_only']['ms_per_step'], 'fwd ms', r.get('avg_launch_us'), 'us', r.get('frac'))"
 done

@@ -465,6 +465,25 @@ __global__ void bias_chunk_sum_kernel(const float* __restrict__ bias, int in_n, 
 // CPL: the couplings c^r and logit gradients gL^r of the 32x32 passes are given
 // (cst, glst: [r-1][in_n][JP][Fs], frame-minor), so gu needs
 // neither the pose nor any logit: gu_ij = c^0 gs^0_j + sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j.
+//
+// gx accumulator layout: a frame slot (row) holds n_per*din floats; lane 16*g + fl
+// updates row w + fl at float4 column chunk g of a 16-float block with one
+// ds_read_b128 + ds_write_b128.  A ds_read_b128 is serviced per lane group
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) over 64 banks, a ds_write_b128 per
+// 8 contiguous lanes over 32 banks.  With a plain stride no value serves both (4
+// mod 64: 2-way reads; 8 mod 16: 2-way writes), so for din % 16 == 0 the row
+// stride is 16 (mod 32) and chunk g of row s sits at g ^ ((s >> 1) & 3): every
+// group of either instruction then covers distinct banks for any window offset w.
+__host__ __device__ constexpr int gu_row_stride(int n_per, int din) {
+  return din % 16 ? n_per * din + 4 : n_per * din + ((n_per * din) % 32 == 16 ? 0 : 16);
+}
+// float offset inside row `slot` of the row element `col`
+template <int DIN>
+__device__ __forceinline__ int gu_acc_col(int slot, int col) {
+  if constexpr (DIN % 16 == 0) return col ^ (((slot >> 1) & 3) << 2);
+  return col;
+}
+
 template <int DIN, int DOUT, int TW, int R, bool LDSACC, bool CPL = false>
 __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
     const float* __restrict__ emb, const float* __restrict__ W, const float* __restrict__ WT,
@@ -498,7 +517,7 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
   const int Jeff = J - (mask_first ? 1 : 0);
   // Per-wave gx accumulators (no LDS atomics): frame slot s <-> emb frame
   // ft*16 - lpad + s, row (n - n0, e); the stride keeps float4 rows bank-conflict free.
-  const int SROW = n_per * DIN + 4;
+  const int SROW = gu_row_stride(n_per, DIN);
   const int nslots = 15 + Wn;
   float* gw_acc = gacc + (size_t)wv * nslots_max * SROW;
 
@@ -642,7 +661,7 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
         for (int ct = 0; ct < NCT; ++ct) {
           if (ct * 16 + 4 * g >= DIN) continue;
           if constexpr (LDSACC) {
-            float* a = gw_acc + (fl + w) * SROW + (n - n0) * DIN + ct * 16 + 4 * g;
+            float* a = gw_acc + (fl + w) * SROW + gu_acc_col<DIN>(fl + w, (n - n0) * DIN + ct * 16 + 4 * g);
             st4(a, ld4(a) + gx[ct]);
           } else {
 #pragma unroll
@@ -661,7 +680,8 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
       const int slot = k / row, rem = k - slot * row;
       const int fo = f0 + slot;
       float v = 0.f;
-      for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots_max + slot) * SROW + rem];
+      const int pos = gu_acc_col<DIN>(slot, rem);
+      for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots_max + slot) * SROW + pos];
       if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
     }
   }
@@ -697,7 +717,7 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
   const int Wn = in_n / N;
   const int ncap = Wn * nn;
   const int Jeff = J - (mask_first ? 1 : 0);
-  const int SROW = n_per * DIN + 4;
+  const int SROW = gu_row_stride(n_per, DIN);
   const int nslots = 15 + Wn;
   float* gw_acc = gacc + (size_t)wv * nslots_max * SROW;
   for (int k = threadIdx.x; k < NW * nslots_max * SROW; k += blockDim.x) gacc[k] = 0.f;
@@ -792,7 +812,7 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
         if (ct * 16 + 4 * g >= DIN) continue;
-        float* a = gw_acc + (fl + w) * SROW + (n - n0) * DIN + ct * 16 + 4 * g;
+        float* a = gw_acc + (fl + w) * SROW + gu_acc_col<DIN>(fl + w, (n - n0) * DIN + ct * 16 + 4 * g);
         st4(a, ld4(a) + gx[ct]);
       }
     }
@@ -836,7 +856,8 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
     const int slot = k / row, rem = k - slot * row;
     const int fo = f0 + slot;
     float v = 0.f;
-    for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots_max + slot) * SROW + rem];
+    const int pos = gu_acc_col<DIN>(slot, rem);
+    for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots_max + slot) * SROW + pos];
     if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
   }
 }
@@ -1169,10 +1190,18 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
   constexpr int RV = R - 1;
   constexpr int JW = gw2_jw<D>();
   constexpr int CG = RV * 2 * JW * 16;   // per capsule: [r][c|gl][jw][16 frames]
-  constexpr int PC = CG + D * 16;        // + x^T [e][16 frames]
+  constexpr int PC = CG + D * 16;        // + x^T [e][16 frames] (in global memory order)
+  // x^T rows in LDS: 16 frames, frame chunk c (4 floats) of row e at c ^ ((e >> 1) & 3).
+  // A ds_read_b128 is serviced per lane group {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...
+  // over 64 banks and lane kk*16+l16 reads row l16, chunk kk: unswizzled, two lanes of
+  // a group share banks (padding the row to 24 floats fixes the reads but puts the two
+  // rows of each 8-lane ds_write_b128 group on the same banks).  The swizzle keeps
+  // both conflict-free without padding.
+  constexpr int PCL = PC;                // per capsule in LDS
   constexpr int SF = CAP * PC;
+  constexpr int SFL = CAP * PCL;
   constexpr int NQ = (SF / 4 + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float stg[2][SF];
+  __shared__ __attribute__((aligned(16))) float stg[2][SFL];
   const int JD = J * D;
   const int NT = (JD + 15) / 16;
   const size_t FJD = (size_t)F * JD;
@@ -1198,6 +1227,7 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
   const int ft0 = s * ft_per, ft1 = min(NFT, ft0 + ft_per);
 
   const float* src[NQ];
+  int dst[NQ];   // LDS float offset of each staged float4
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int idx = min(q * 256 + (int)threadIdx.x, SF / 4 - 1);
@@ -1207,9 +1237,12 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
       const int fq = rem & 3, jw = (rem >> 2) % JW, cg = (rem >> 2) / JW;
       const int jj = min(jg0 + jw, JP - 1);
       src[q] = ((cg & 1) ? glst : cst) + (size_t)(cg >> 1) * cblk + ((size_t)i * JP + jj) * Fs + 4 * fq;
+      dst[q] = k * PCL + rem * 4;
     } else {
       const int x = rem - CG / 4;
       src[q] = xT + ((size_t)i * D + (x >> 2)) * Fp + 4 * (x & 3);
+      const int e = x >> 2;
+      dst[q] = k * PCL + CG + e * 16 + 4 * ((x & 3) ^ ((e >> 1) & 3));
     }
   }
   f4 sv[NQ];
@@ -1221,7 +1254,7 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int idx = q * 256 + threadIdx.x;
-      if ((SF / 4) % 256 == 0 || idx < SF / 4) st4(&stg[buf][idx * 4], sv[q]);
+      if ((SF / 4) % 256 == 0 || idx < SF / 4) st4(&stg[buf][dst[q]], sv[q]);
     }
   };
   // per-frame vectors: buffer loads, 0 past F (range check)
@@ -1281,7 +1314,7 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
     const float* sb = stg[buf];
 #pragma unroll
     for (int k = 0; k < CAP; ++k) {
-      const float* ck = sb + k * PC;
+      const float* ck = sb + k * PCL;
       float gu[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v) gu[v] = c0 * g0[v];
@@ -1295,7 +1328,8 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
       gb[k] += (gu[0] + gu[1]) + (gu[2] + gu[3]);
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
-        const f4 xa = ld4(ck + CG + min(ct * 16 + l16, D - 1) * 16 + 4 * kk);
+        const int e = min(ct * 16 + l16, D - 1);
+        const f4 xa = ld4(ck + CG + e * 16 + 4 * (kk ^ ((e >> 1) & 3)));
 #pragma unroll
         for (int v = 0; v < 4; ++v) acc[k][ct] = mfma16x16x4(xa[v], gu[v], acc[k][ct]);
       }
@@ -1495,7 +1529,7 @@ inline int gu_wgroups(const Geom& g) { return (g.NT() + kGuNW * gu_tw(g.dout) - 
 inline int padded_frames(const Geom& g) { return (g.F() + 15) / 16 * 16; }
 inline int gu_window(const Geom& g) { return g.lpad + g.rpad + 1; }
 inline size_t gu_lds_bytes(const Geom& g, int nw, int n_per) {
-  return (size_t)nw * (15 + gu_window(g)) * (n_per * g.din + 4) * sizeof(float);
+  return (size_t)nw * (15 + gu_window(g)) * gu_row_stride(n_per, g.din) * sizeof(float);
 }
 constexpr size_t kGuLdsMax = 64 * 1024;
 
