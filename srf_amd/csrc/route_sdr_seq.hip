@@ -34,6 +34,12 @@ namespace {
 
 using namespace srf_seq;
 
+#if SRF_SEQ_STAMP
+__device__ unsigned long long* g_stamps;   // diagnostic builds: phase cycle sums
+#else
+constexpr unsigned long long* g_stamps = nullptr;
+#endif
+
 // LDS: w [JD] (agreement input of the iteration: v_{t-1} at r = 0, then v^{r-1}),
 // part [16][JD].
 template <int D, int JP, int NIM>
@@ -58,6 +64,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
   float ur[C::NIM][C::KD];
   load_frame<C>(ub + (size_t)(rg.t0 - rg.tu0) * ff, JD, L, ur);
   __syncthreads();
+  SEQ_STAMP_DECL
   for (int t = rg.t0; t < rg.t1; ++t) {
     float b[C::NIM], c[C::NIM];
 #pragma unroll
@@ -73,7 +80,9 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
 #else
       if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(t + 1 - rg.tu0) * ff, JD, L, ur);   // u_t is dead
 #endif
+      SEQ_MARK(0);   // logits, softmax, row partials (+ next frame's loads issued)
       __syncthreads();
+      SEQ_MARK(1);
       if (owner_wave) {
         const float s = ev ? sum_parts(part, JD, tid) : 0.f;
         const float v = squash_elem<D>(s);
@@ -83,9 +92,12 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __re
           if (cs) cs[((size_t)blockIdx.x * T + t) * csr + (size_t)iters * in_n * JP + r * JD + tid] = s;
         }
       }
+      SEQ_MARK(2);   // wave sums + squash (owner waves)
       __syncthreads();
+      SEQ_MARK(3);
     }
   }
+  SEQ_FLUSH(g_stamps);
 }
 
 size_t fwd_lds(int J, int D) {
@@ -116,6 +128,12 @@ int fwd_nim(int nim, const float* u, int B, int T, int in_n, int J, int iters, i
 }
 
 }  // namespace
+
+#if SRF_SEQ_STAMP
+extern "C" int srf_seq_fwd_stamp_buffer(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 namespace srf {
 

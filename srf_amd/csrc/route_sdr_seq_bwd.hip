@@ -23,6 +23,12 @@ namespace {
 
 using namespace srf_seq;
 
+#if SRF_SEQ_STAMP
+__device__ unsigned long long* g_stamps;   // diagnostic builds: phase cycle sums
+#else
+constexpr unsigned long long* g_stamps = nullptr;
+#endif
+
 // c^r and gL^r of the lane's rows live in registers or, with CL (chosen when u
 // already takes most of the lane's register budget and the slabs fit), in LDS
 // [RM][in_n][JP] (written by the first lane of each capsule, read by all Q lanes).
@@ -73,6 +79,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
 #pragma unroll
   for (int r = 0; r < RM; ++r) sr[r] = 0.f;
   load_rows<C, KRES>(ub + (size_t)(rg.t1 - 1 - rg.tu0) * ff, JD, L, ur);
+  SEQ_STAMP_DECL
   for (int t = rg.t1 - 1; t >= rg.t0; --t) {
     const size_t f = f0 + t;
     float a = 0.f;
@@ -98,6 +105,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
         }
       }
       __syncthreads();   // Vc^0 (above) before the owner threads extend it
+      SEQ_MARK(0);       // v_{t-1}, g_v, c^r loads (+ the previous frame's barrier)
       if (owner_wave) {
 #pragma unroll
         for (int r = 0; r < RM; ++r) {
@@ -112,6 +120,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
         }
       }
       __syncthreads();
+      SEQ_MARK(1);       // s^r loads, Vc^r
     } else {
     __syncthreads();
     // ---- recompute the frame's iterations: c^r, s^r, Vc^r
@@ -161,6 +170,8 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
           if (ev) gsl[r * JDa + tid] = gfac * a + dg2 * s;
         }
         __syncthreads();
+        SEQ_MARK(2);     // squash adjoint
+
         float gsv[C::KD], cc[C::NIM], gg[C::NIM];
         lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
         if constexpr (CL) {
@@ -232,13 +243,16 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
 #pragma unroll
           for (int k = 0; k < C::NIM; ++k) gl[r][k] = gg[k];
         }
+        SEQ_MARK(3);     // q, sigma, gL, gVc partials (+ re-read rows)
         __syncthreads();
+        SEQ_MARK(4);
         if (ev) {
           const float g = sum_parts(part, JD, tid);   // gVc^r_e
           carry += g;
           grun = (r == R - 1) ? g : grun + g;
           a = grun;
         }
+        SEQ_MARK(5);
       }
     }
     // ---- gu, one input capsule of the lane at a time (u is dead: its registers
@@ -322,9 +336,12 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __re
       }
     }
     }   // CS gu
+    SEQ_MARK(6);       // gu
     if (t > rg.t0) load_rows<C, KRES>(ub + (size_t)(t - 1 - rg.tu0) * ff, JD, L, ur);
     __syncthreads();   // the next frame overwrites w, Vc^0 and the c / gL slabs
+    SEQ_MARK(7);
   }
+  SEQ_FLUSH(g_stamps);
   if (carry_io && ev) carry_io[tid] = carry;   // dL/dv_{t0-1} for the earlier range
 }
 
@@ -370,6 +387,12 @@ int bwd_nim(int nim, int rm, const float* u, const float* vs, const float* gv, i
 }
 
 }  // namespace
+
+#if SRF_SEQ_STAMP
+extern "C" int srf_seq_bwd_stamp_buffer(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 namespace srf {
 

@@ -272,6 +272,50 @@ __device__ __forceinline__ float sum_parts(const float* __restrict__ part, int J
   return s;
 }
 
+// ------------------------------------------------------------------ stamps
+// Diagnostic builds only (-DSRF_SEQ_STAMP=1, scripts/seq_stamps.py): per-phase
+// cycle sums of waves 0 and 15 of every workgroup, stored once at the end into a
+// buffer of their own (never read by the kernel, never an output).  The shipped
+// build compiles every mark to nothing.
+#ifndef SRF_SEQ_STAMP
+#define SRF_SEQ_STAMP 0
+#endif
+constexpr int kStampPh = 8;
+#if SRF_SEQ_STAMP
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+struct Stamps {
+  unsigned long long last, sum[kStampPh];
+  __device__ void start() {
+    for (int p = 0; p < kStampPh; ++p) sum[p] = 0;
+    last = stamp_now();
+  }
+  __device__ void mark(int p) {
+    const unsigned long long t = stamp_now();
+    sum[p] += t - last;
+    last = t;
+  }
+  __device__ void flush(unsigned long long* out) {
+    const int wv = threadIdx.x >> 6;
+    if (out == nullptr || (threadIdx.x & 63) != 0 || (wv != 0 && wv != kWaves - 1)) return;
+    unsigned long long* o = out + ((size_t)blockIdx.x * 2 + (wv ? 1 : 0)) * kStampPh;
+    for (int p = 0; p < kStampPh; ++p) o[p] = sum[p];
+  }
+};
+#define SEQ_STAMP_DECL Stamps st_; st_.start();
+#define SEQ_MARK(p) st_.mark(p)
+#define SEQ_FLUSH(buf) st_.flush(buf)
+#else
+#define SEQ_STAMP_DECL
+#define SEQ_MARK(p) ((void)0)
+#define SEQ_FLUSH(buf) ((void)(buf))
+#endif
+
 // squash over the D consecutive owner lanes of a capsule (naive:247-252); the
 // recurrence is VALU-issue bound, so 1-ulp v_rcp / v_rsq replace IEEE div / sqrt
 template <int D>
