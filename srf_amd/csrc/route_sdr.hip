@@ -538,6 +538,8 @@ int recur_fwd(const SGeom& g, const float* u, float* v_out, const srf::SeqRange&
   if (rg.t0 >= rg.t1) return SRF_OK;
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_seq_fwd(u, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, v_out, rg, cs, st);
+  if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
+    return srf::sdr_stream_fwd(u, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, v_out, rg, cs, st);
   const size_t sm = sdr_fwd_smem(g.in_n(), g.J, g.dout);
   if (sdr_gstate(sm))
     hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, g.T, g.in_n(), g.J,
@@ -555,6 +557,8 @@ int recur_bwd(const SGeom& g, const float* u, const float* v_saved, const float*
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_seq_bwd(u, v_saved, g_v, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, rg, cs,
                             st);
+  if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
+    return srf::sdr_stream_bwd(u, v_saved, g_v, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, gu, rg, cs, gstate, st);
   const size_t sm = sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters);
   if (sdr_gstate(sm))
     hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, v_saved, g_v, g.T,
@@ -568,6 +572,8 @@ int recur_bwd(const SGeom& g, const float* u, const float* v_saved, const float*
 
 size_t recur_workspace(const SGeom& g) {
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters)) return 0;
+  if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
+    return srf::sdr_stream_workspace_floats(g.B, g.in_n(), g.J, g.dout, g.iters) * sizeof(float);
   return std::max(gstate_bytes(g, sdr_fwd_smem(g.in_n(), g.J, g.dout)),
                   gstate_bytes(g, sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters)));
 }
@@ -617,10 +623,18 @@ int transpose_w(const SGeom& g, const float* W, float* WT, float* zero, size_t n
   return SRF_OK;
 }
 
+// The stream recurrence (srf::sdr_stream_*) needs the forward's couplings: the
+// whole-layer backward reruns its forward into cs (and a scratch v) first.
 struct SdrBwdWs {
-  float *u, *gu, *WT, *gstate;
+  float *u, *gu, *WT, *gstate, *cs, *v;
   size_t bytes;
 };
+
+size_t stream_cs_floats(const SGeom& g) {
+  return srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters)
+             ? 0
+             : srf::sdr_stream_cs_floats(g.in_n(), g.J, g.dout, g.iters);
+}
 
 SdrBwdWs sdr_bwd_layout(const SGeom& g, void* base) {
   const size_t FU = (size_t)g.F() * g.in_n() * g.JD();
@@ -630,14 +644,18 @@ SdrBwdWs sdr_bwd_layout(const SGeom& g, void* base) {
     off += srf::align_up(nbytes, 256);
     return o;
   };
+  const size_t ncs = stream_cs_floats(g);
   const size_t ou = take(FU * 4), ogu = take(FU * 4), owt = take((size_t)g.in_n() * g.JD() * g.din * 4),
-               ogs = take(recur_workspace(g));
+               ogs = take(recur_workspace(g)), ocs = take((size_t)g.F() * ncs * 4),
+               ov = take(ncs ? (size_t)g.F() * g.JD() * 4 : 0);
   char* b = static_cast<char*>(base);
   SdrBwdWs w;
   w.u = (float*)(b + ou);
   w.gu = (float*)(b + ogu);
   w.WT = (float*)(b + owt);
   w.gstate = (float*)(b + ogs);
+  w.cs = ncs ? (float*)(b + ocs) : nullptr;
+  w.v = ncs ? (float*)(b + ov) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -702,7 +720,8 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
   hipStream_t st = static_cast<hipStream_t>(stream);
   const FrameMap all = frame_map(T, 0, T, 0, T);
   if ((rc = pose_range(g, emb, W, bias, all, w.u, st))) return rc;
-  if ((rc = recur_bwd(g, w.u, saved, g_v, w.gu, srf::SeqRange::whole(T), w.gstate, nullptr, st))) return rc;
+  if (w.cs && (rc = recur_fwd(g, w.u, w.v, srf::SeqRange::whole(T), w.gstate, w.cs, st))) return rc;
+  if ((rc = recur_bwd(g, w.u, saved, g_v, w.gu, srf::SeqRange::whole(T), w.gstate, w.cs, st))) return rc;
   if ((rc = transpose_w(g, W, w.WT, g_emb, (size_t)g.F() * N * din, st))) return rc;
   if ((rc = gx_range(g, w.gu, w.WT, all, g_emb, st))) return rc;
   return gw_range(g, w.gu, emb, all, 0, g_W, g_bias, st);
@@ -724,7 +743,8 @@ size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters
 }
 
 size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters) {
-  return srf::sdr_seq_cs_floats(in_n, J, dout, iters);
+  const size_t n = srf::sdr_seq_cs_floats(in_n, J, dout, iters);
+  return n ? n : srf::sdr_stream_cs_floats(in_n, J, dout, iters);
 }
 
 int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
@@ -736,7 +756,7 @@ int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in
   SRF_REQUIRE(u && v_out, "null pointer argument");
   SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
               "SDR recurrence workspace too small");
-  if (!srf::sdr_seq_cs_floats(in_n, J, dout, iters)) couplings = nullptr;
+  if (!srf_route_sdr_coupling_floats(in_n, J, dout, iters)) couplings = nullptr;
   return recur_fwd(g, u, v_out, srf::SeqRange{t0, t1, v0, vn, 0, T, nullptr}, static_cast<float*>(workspace),
                    couplings, static_cast<hipStream_t>(stream));
 }
@@ -751,7 +771,7 @@ int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved
   SRF_REQUIRE(u && v_saved && g_v && carry && gu, "null pointer argument");
   SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
               "SDR recurrence workspace too small");
-  if (!srf::sdr_seq_cs_floats(in_n, J, dout, iters)) couplings = nullptr;
+  if (!srf_route_sdr_coupling_floats(in_n, J, dout, iters)) couplings = nullptr;
   return recur_bwd(g, u, v_saved, g_v, gu, srf::SeqRange{t0, t1, v0, vn, g0, gn, carry},
                    static_cast<float*>(workspace), couplings, static_cast<hipStream_t>(stream));
 }

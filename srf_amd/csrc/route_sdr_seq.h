@@ -44,4 +44,18 @@ int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, i
 // the iteration bound RM of the backward in {3, 5}.  False when unsupported.
 bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm);
 
+// Streaming recurrence (route_sdr_stream.hip) for frames beyond the register budget
+// (BASELINE C5): dout in {32, 64} with J*dout in {512, 1024, 2048} (dout 32: 512,
+// 1024), in_n >= 8.  u_t is re-read from HBM once per iteration.  The forward
+// stores per frame c^r [iters][in_n][J] and s^r [iters][J*dout]
+// (sdr_stream_cs_floats, 256-B padded); the backward requires them and a scratch of
+// sdr_stream_workspace_floats (gL^r of every utterance).  Disabled by SRF_SDR_STREAM=0.
+bool sdr_stream_supported(int in_n, int J, int dout, int iters);
+size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters);
+size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters);
+int sdr_stream_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
+                   const SeqRange& rg, float* cs, hipStream_t st);
+int sdr_stream_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
+                   int iters, float* gu, const SeqRange& rg, const float* cs, float* gls, hipStream_t st);
+
 }  // namespace srf

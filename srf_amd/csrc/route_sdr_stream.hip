@@ -1,0 +1,471 @@
+// Streaming SDR recurrence for layers whose frame exceeds a workgroup's registers,
+// gfx950: BASELINE C5 (in_n = 16*41 = 656 input capsules, J = 16 | 32 output
+// capsules of D = 64, five iterations; u_t = 2.7 | 5.4 MB per frame).
+//
+// Same recurrence as route_sdr_seq*.hip (sequence_router_naive.py:162-170 with
+// body_context :231-245 / pad_body_context :212-229, and its autodiff), one
+// 512-thread workgroup per utterance walking its frames in order (forward) or in
+// reverse (backward), but u_t is streamed from HBM once per routing iteration
+// instead of held in registers:
+//   lane map: an input capsule's u_ij (J*D floats) is one wave-wide slice, lane l
+//   holds the KD = J*D/64 consecutive floats [l*KD, l*KD + KD), i.e. output capsule
+//   j = l / RQ, dims q*KD .. q*KD + KD - 1 (RQ = D/KD lanes per capsule);
+//   wave w takes input capsules i = w, w + 8, ... (NMp per pass, a multiple of PD,
+//   the tail predicated off), PD capsules in flight per wave in a register ring that
+//   runs ahead across iterations and frames;
+//   per capsule: logit = KD FMAs + a butterfly over the RQ lanes, softmax over j =
+//   butterflies over the J capsule groups (DPP / permlane, VALU only), then
+//   s_j += c_ij u_ij in the lane's KD accumulators;
+//   per iteration: the 8 wave partials through LDS, thread e owns s_e, the squash is
+//   a butterfly over the D owner lanes, Vc (v_{t-1} + sum_{k<r} v^k, b^r = <u, Vc^r>
+//   by linearity of b += <u, v>) goes back through LDS.  Two barriers per iteration.
+// The forward stores each frame's couplings c^r [R][in_n][J] and pre-squash s^r
+// [R][J*D] (sdr_stream_cs_floats per frame); the backward reads them and runs only
+// the adjoint (same algebra as route_sdr_seq_bwd.hip):
+//   gs^r = squash'(s^r)^T a^r,  q_ij = <u_ij, gs^r_j>,  sigma_i = sum_j c_ij q_ij,
+//   gL_ij = c_ij (q_ij - sigma_i) (kept in a per-utterance L2 scratch),
+//   gVc^r = sum_i gL_ij u_ij  (one streamed pass of u_t per iteration),
+//   gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j  (a pass without u: the lane's
+//   gs^r / Vc^r slices in registers, the 2R scalars of (i, j) per capsule).
+// HBM per frame: forward R reads of u_t; backward R reads of u_t + one write of gu_t.
+#include <cstdlib>
+
+#include "route_sdr_seq.h"
+#include "route_sdr_seq_dev.h"
+
+namespace {
+
+using srf_seq::group_max;
+using srf_seq::group_sum;
+
+constexpr int kNT = 512;          // threads per workgroup (two waves per SIMD, 256 VGPRs each)
+constexpr int kNW = kNT / 64;
+constexpr int kRM = 5;            // iteration bound (check_sgeom)
+constexpr float kEps = 1e-7f;     // naive:248
+
+template <int D_, int KD_>
+struct SC {
+  static constexpr int D = D_;
+  static constexpr int KD = KD_;              // floats of a capsule per lane
+  static constexpr int JD = 64 * KD;          // floats of one input capsule's u
+  static constexpr int J = JD / D;
+  static constexpr int RQ = D / KD;           // lanes per output capsule
+  static constexpr int NE = JD / kNT;         // elements per thread in the element phases
+  static constexpr int PD = KD <= 16 ? 4 : 2; // capsules in flight per wave
+  static constexpr int HD = 8;                 // gu outputs per lane per sub-pass (registers: 2R*HD)
+  static_assert(D % KD == 0 && NE >= 1 && KD % 4 == 0 && KD % HD == 0, "unsupported stream shape");
+};
+
+// floats per frame of the coupling record: c^r [R][in_n][J], s^r [R][JD], padded to 256 B
+__host__ __device__ inline size_t cs_rec(int in_n, int J, int D, int R) {
+  return ((size_t)R * ((size_t)in_n * J + (size_t)J * D) + 63) / 64 * 64;
+}
+
+// position in a wave's capsule stream: frame t, pass p of the frame, capsule slot m
+struct Cur {
+  int t, p, m;
+  __device__ __forceinline__ void adv(int NMp, int NP, int dt) {
+    if (++m == NMp) {
+      m = 0;
+      if (++p == NP) {
+        p = 0;
+        t += dt;
+      }
+    }
+  }
+};
+
+template <int KD>
+__device__ __forceinline__ void load_slice(const float* __restrict__ p, float (&x)[KD]) {
+#pragma unroll
+  for (int c = 0; c < KD; c += 4) {
+    const f4 q = *reinterpret_cast<const f4*>(p + c);
+    x[c] = q.x;
+    x[c + 1] = q.y;
+    x[c + 2] = q.z;
+    x[c + 3] = q.w;
+  }
+}
+
+template <int KD>
+__device__ __forceinline__ float dot_slice(const float (&x)[KD], const float (&w)[KD]) {
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int d = 0; d < KD; d += 2) {
+    p0 += x[d] * w[d];
+    p1 += x[d + 1] * w[d + 1];
+  }
+  return p0 + p1;
+}
+
+__device__ __forceinline__ float squash_fac(float n2) {
+  return n2 * __builtin_amdgcn_rcpf(1.f + n2) * __builtin_amdgcn_rsqf(n2 + kEps);
+}
+
+// gs = squash'(s)^T a over the D owner lanes of a capsule (sdr_bwd_kernel's algebra)
+template <int D>
+__device__ __forceinline__ float dsquash(float s, float a) {
+  const float n2 = group_sum<1, D>(s * s);
+  const float sa = group_sum<1, D>(s * a);
+  const float rs = 1.f / sqrtf(n2 + kEps);
+  const float ip = 1.f / (1.f + n2);
+  const float gfac = n2 * ip * rs;
+  const float dg2 = 2.f * rs * ip * (ip - 0.5f * n2 / (n2 + kEps)) * sa;
+  return gfac * a + dg2 * s;
+}
+
+// ------------------------------------------------------------------ forward
+// LDS: wl [JD] (Vc of the iteration), part [kNW][JD].
+template <int D, int KD>
+__global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(const float* __restrict__ u, int T, int in_n,
+                                                             int iters, int mask_first, float* __restrict__ v_out,
+                                                             srf::SeqRange rg, float* __restrict__ cs, int NMp) {
+  using C = SC<D, KD>;
+  constexpr int JD = C::JD, J = C::J, PD = C::PD, NE = C::NE;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* wl = lds;
+  float* part = lds + JD;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (rg.t0 >= rg.t1) return;
+  const int b = blockIdx.x;
+  const int j = lane / C::RQ;
+  const bool q0 = (lane % C::RQ) == 0;
+  const bool jm = !(mask_first && j == 0);
+  const size_t ff = (size_t)in_n * JD;
+  const float* ub = u + (size_t)b * rg.tu_n * ff + lane * KD;
+  float* vo = v_out + (size_t)b * T * JD;
+  const size_t csr = cs_rec(in_n, J, D, iters);
+
+  float vc[NE];   // Vc of the thread's elements e = tid + n * kNT
+#pragma unroll
+  for (int n = 0; n < NE; ++n) {
+    const int e = tid + n * kNT;
+    vc[n] = rg.t0 > 0 ? vo[(size_t)(rg.t0 - 1) * JD + e] : 0.f;
+    wl[e] = vc[n];
+  }
+  float xr[PD][KD];
+  Cur lc{rg.t0, 0, 0};
+  auto issue = [&](float(&x)[KD]) {
+    const int tc = min(lc.t, rg.t1 - 1);
+    const int i = min(wv + kNW * lc.m, in_n - 1);
+    load_slice<KD>(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD, x);
+    lc.adv(NMp, iters, 1);
+  };
+#pragma unroll
+  for (int p = 0; p < PD; ++p) issue(xr[p]);
+  __syncthreads();
+
+  for (int t = rg.t0; t < rg.t1; ++t) {
+    float* csf = cs ? cs + ((size_t)b * T + t) * csr : nullptr;
+    for (int r = 0; r < iters; ++r) {
+      float w[KD], acc[KD];
+      load_slice<KD>(wl + lane * KD, w);
+#pragma unroll
+      for (int d = 0; d < KD; ++d) acc[d] = 0.f;
+      for (int m0 = 0; m0 < NMp; m0 += PD) {
+#pragma unroll
+        for (int p = 0; p < PD; ++p) {
+          const int i = wv + kNW * (m0 + p);
+          const bool iv = i < in_n;
+          const float lg = group_sum<1, C::RQ>(dot_slice<KD>(xr[p], w));
+          const float x = jm ? lg : -INFINITY;
+          const float mx = group_max<C::RQ, 64>(x);
+          const float ex = __expf(x - mx);
+          const float c = iv ? ex * __builtin_amdgcn_rcpf(group_sum<C::RQ, 64>(ex)) : 0.f;
+#pragma unroll
+          for (int d = 0; d < KD; ++d) acc[d] += c * xr[p][d];
+          if (csf && q0 && iv) csf[(size_t)r * in_n * J + (size_t)i * J + j] = c;
+          issue(xr[p]);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < KD; d += 4)
+        *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{acc[d], acc[d + 1], acc[d + 2], acc[d + 3]};
+      __syncthreads();
+#pragma unroll
+      for (int n = 0; n < NE; ++n) {
+        const int e = tid + n * kNT;
+        float s = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < kNW; ++w2) s += part[w2 * JD + e];
+        const float v = s * squash_fac(group_sum<1, D>(s * s));
+        if (csf) csf[(size_t)iters * in_n * J + (size_t)r * JD + e] = s;
+        if (r == iters - 1) {
+          vo[(size_t)t * JD + e] = v;
+          vc[n] = v;   // v_t: Vc^0 of frame t + 1
+        } else {
+          vc[n] += v;
+        }
+        wl[e] = vc[n];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// LDS: part [kNW][JD], gsl [kRM][JD] (gs^r), vcl [kRM][JD] (Vc^r).
+// gls: per-utterance scratch gL^r [R][in_n][J].
+template <int D, int KD>
+__global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(const float* __restrict__ u,
+                                                             const float* __restrict__ v_saved,
+                                                             const float* __restrict__ g_v, int T, int in_n,
+                                                             int iters, float* __restrict__ gu, srf::SeqRange rg,
+                                                             const float* __restrict__ cs, float* __restrict__ gls,
+                                                             int NMp) {
+  using C = SC<D, KD>;
+  constexpr int JD = C::JD, J = C::J, PD = C::PD, NE = C::NE, HD = C::HD;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* part = lds;
+  float* gsl = part + kNW * JD;
+  float* vcl = gsl + kRM * JD;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (rg.t0 >= rg.t1) return;
+  const int b = blockIdx.x;
+  const int R = iters;
+  const int j = lane / C::RQ;
+  const bool q0 = (lane % C::RQ) == 0;
+  const size_t ff = (size_t)in_n * JD;
+  const size_t PJ = (size_t)in_n * J;
+  const float* ub = u + (size_t)b * rg.tu_n * ff + lane * KD;
+  float* gub = gu + (size_t)b * rg.tg_n * ff + lane * KD;
+  const size_t csr = cs_rec(in_n, J, D, iters);
+  const float* csb = cs + (size_t)b * T * csr;
+  float* gl = gls + (size_t)b * R * PJ;
+  float* carry_io = rg.carry ? rg.carry + (size_t)b * JD : nullptr;
+
+  float carry[NE];
+#pragma unroll
+  for (int n = 0; n < NE; ++n) carry[n] = carry_io ? carry_io[tid + n * kNT] : 0.f;
+
+  // ring of the adjoint passes: u_t slice and c^r_ij of capsule i, pass p <-> r = R-1-p
+  float xr[PD][KD], cr[PD];
+  Cur lc{rg.t1 - 1, 0, 0};
+  auto issue = [&](float(&x)[KD], float& c) {
+    const int tc = max(lc.t, rg.t0);
+    const int i = min(wv + kNW * lc.m, in_n - 1);
+    load_slice<KD>(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD, x);
+    c = csb[(size_t)tc * csr + (size_t)(R - 1 - lc.p) * PJ + (size_t)i * J + j];
+    lc.adv(NMp, R, -1);
+  };
+
+  for (int t = rg.t1 - 1; t >= rg.t0; --t) {
+    const float* csf = csb + (size_t)t * csr;
+#pragma unroll
+    for (int p = 0; p < PD; ++p) issue(xr[p], cr[p]);
+    // ---- element phase: Vc^r from s^r, the top adjoint
+    float gv[NE];
+#pragma unroll
+    for (int n = 0; n < NE; ++n) {
+      const int e = tid + n * kNT;
+      const float a = g_v[((size_t)b * T + t) * JD + e] + carry[n];
+      float vcv = t > 0 ? v_saved[((size_t)b * T + t - 1) * JD + e] : 0.f;
+      for (int r = 0; r < R; ++r) {
+        const float sv = csf[(size_t)R * PJ + (size_t)r * JD + e];
+        vcl[r * JD + e] = vcv;
+        vcv += sv * squash_fac(group_sum<1, D>(sv * sv));
+        if (r == R - 1) gsl[r * JD + e] = dsquash<D>(sv, a);
+      }
+      carry[n] = 0.f;
+      gv[n] = 0.f;
+    }
+    __syncthreads();
+    // ---- adjoint passes r = R-1 .. 0 over u_t
+    for (int p = 0; p < R; ++p) {
+      const int r = R - 1 - p;
+      float g[KD], gacc[KD], sn[NE];
+      load_slice<KD>(gsl + r * JD + lane * KD, g);
+#pragma unroll
+      for (int n = 0; n < NE; ++n)   // s^{r-1}, for gs^{r-1} at the end of the pass
+        sn[n] = r > 0 ? csf[(size_t)R * PJ + (size_t)(r - 1) * JD + tid + n * kNT] : 0.f;
+#pragma unroll
+      for (int d = 0; d < KD; ++d) gacc[d] = 0.f;
+      for (int m0 = 0; m0 < NMp; m0 += PD) {
+#pragma unroll
+        for (int pp = 0; pp < PD; ++pp) {
+          const int i = wv + kNW * (m0 + pp);
+          const bool iv = i < in_n;
+          const float qd = group_sum<1, C::RQ>(dot_slice<KD>(xr[pp], g));
+          const float c = iv ? cr[pp] : 0.f;
+          const float sig = group_sum<C::RQ, 64>(c * qd);
+          const float gL = c * (qd - sig);
+#pragma unroll
+          for (int d = 0; d < KD; ++d) gacc[d] += gL * xr[pp][d];
+          if (q0 && iv) gl[(size_t)r * PJ + (size_t)i * J + j] = gL;
+          // the ring stops at the frame's last pass: the gu pass below needs its registers
+          if (!(p == R - 1 && m0 + pp + PD >= NMp)) issue(xr[pp], cr[pp]);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < KD; d += 4)
+        *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{gacc[d], gacc[d + 1], gacc[d + 2], gacc[d + 3]};
+      __syncthreads();
+#pragma unroll
+      for (int n = 0; n < NE; ++n) {
+        const int e = tid + n * kNT;
+        float gvc = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < kNW; ++w2) gvc += part[w2 * JD + e];
+        carry[n] += gvc;      // dL/dv_{t-1} = sum_r gVc^r
+        gv[n] += gvc;         // dL/dv^{r-1} = sum_{r' >= r} gVc^{r'}
+        if (r > 0) gsl[(r - 1) * JD + e] = dsquash<D>(sn[n], gv[n]);
+      }
+      __syncthreads();
+    }
+    // skip the issue-slot bookkeeping of the stopped ring: restart at frame t-1
+    lc = Cur{t - 1, 0, 0};
+    // ---- gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j, HD outputs per lane per sub-pass
+    float* gut = gub + (size_t)(t - rg.tg0) * ff;
+#pragma unroll
+    for (int h = 0; h < KD; h += HD) {
+      float gs[kRM][HD], vv[kRM][HD];
+#pragma unroll
+      for (int r = 0; r < kRM; ++r) {
+        if (r < R) {
+          load_slice<HD>(gsl + r * JD + lane * KD + h, gs[r]);
+          load_slice<HD>(vcl + r * JD + lane * KD + h, vv[r]);
+        } else {
+#pragma unroll
+          for (int d = 0; d < HD; ++d) gs[r][d] = vv[r][d] = 0.f;
+        }
+      }
+      // scalars of capsule i for the lane's j, one capsule ahead
+      float sc[2][2 * kRM];
+      auto fetch = [&](int m, float(&s)[2 * kRM]) {
+        const int i = min(wv + kNW * m, in_n - 1);
+#pragma unroll
+        for (int r = 0; r < kRM; ++r) {
+          const int rr = min(r, R - 1);
+          s[r] = csf[(size_t)rr * PJ + (size_t)i * J + j];
+          s[kRM + r] = gl[(size_t)rr * PJ + (size_t)i * J + j];
+        }
+      };
+      fetch(0, sc[0]);
+      for (int m0 = 0; m0 < NMp; m0 += 2) {
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const int m = m0 + pp;
+          fetch(m + 1, sc[pp ^ 1]);
+          const int i = wv + kNW * m;
+          float o[HD];
+#pragma unroll
+          for (int d = 0; d < HD; ++d) o[d] = 0.f;
+#pragma unroll
+          for (int r = 0; r < kRM; ++r) {
+            if (r < R) {
+#pragma unroll
+              for (int d = 0; d < HD; ++d) o[d] += sc[pp][r] * gs[r][d] + sc[pp][kRM + r] * vv[r][d];
+            }
+          }
+          if (i < in_n) {
+#pragma unroll
+            for (int d = 0; d < HD; d += 4)
+              *reinterpret_cast<f4*>(gut + (size_t)i * JD + h + d) = f4{o[d], o[d + 1], o[d + 2], o[d + 3]};
+          }
+        }
+      }
+    }
+    __syncthreads();   // gsl / vcl / the gL scratch are rewritten by frame t - 1
+  }
+  if (carry_io)
+#pragma unroll
+    for (int n = 0; n < NE; ++n) carry_io[tid + n * kNT] = carry[n];
+}
+
+// ------------------------------------------------------------------ host
+// capsule slots per wave and pass: a multiple of the ring depth PD (the ring's slots
+// are static registers) and of 2 (the gu pass walks slots in pairs)
+int nm_padded(int in_n, int pd) {
+  const int step = pd % 2 ? 2 * pd : pd;
+  const int nm = (in_n + kNW - 1) / kNW;
+  return (nm + step - 1) / step * step;
+}
+
+size_t fwd_lds(int JD) { return (size_t)(1 + kNW) * JD * sizeof(float); }
+size_t bwd_lds(int JD) { return (size_t)(kNW + 2 * kRM) * JD * sizeof(float); }
+
+template <int D, int KD>
+int launch_fwd(const float* u, int B, int T, int in_n, int iters, int mask_first, float* v_out,
+               const srf::SeqRange& rg, float* cs, hipStream_t st) {
+  using C = SC<D, KD>;
+  const size_t lds = fwd_lds(C::JD);
+  auto k = sdr_stream_fwd_kernel<D, KD>;
+  if (lds > 64 * 1024)
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k, dim3(B), dim3(kNT), lds, st, u, T, in_n, iters, mask_first, v_out, rg, cs,
+                     nm_padded(in_n, C::PD));
+  SRF_LAUNCH_CHECK("sdr_stream_fwd");
+  return SRF_OK;
+}
+
+template <int D, int KD>
+int launch_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int iters, float* gu,
+               const srf::SeqRange& rg, const float* cs, float* gls, hipStream_t st) {
+  using C = SC<D, KD>;
+  const size_t lds = bwd_lds(C::JD);
+  auto k = sdr_stream_bwd_kernel<D, KD>;
+  if (lds > 64 * 1024)
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k, dim3(B), dim3(kNT), lds, st, u, v_saved, g_v, T, in_n, iters, gu, rg, cs, gls,
+                     nm_padded(in_n, C::PD));
+  SRF_LAUNCH_CHECK("sdr_stream_bwd");
+  return SRF_OK;
+}
+
+// (dout, KD = J*dout/64) instances
+#define SRF_STREAM_CASES(X) X(64, 8) X(64, 16) X(64, 32) X(32, 8) X(32, 16)
+
+}  // namespace
+
+namespace srf {
+
+bool sdr_stream_supported(int in_n, int J, int dout, int iters) {
+  const char* e = getenv("SRF_SDR_STREAM");
+  if (e && e[0] == '0') return false;
+  if (iters < 1 || iters > kRM || in_n < kNW) return false;
+  const int JD = J * dout;
+  if (JD % 64) return false;
+  const int KD = JD / 64;
+#define SRF_STREAM_OK(DD, KK) \
+  if (dout == DD && KD == KK) return true;
+  SRF_STREAM_CASES(SRF_STREAM_OK)
+#undef SRF_STREAM_OK
+  return false;
+}
+
+size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters) {
+  return sdr_stream_supported(in_n, J, dout, iters) ? cs_rec(in_n, J, dout, iters) : 0;
+}
+
+size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters) {
+  return sdr_stream_supported(in_n, J, dout, iters) ? (size_t)B * iters * in_n * J : 0;
+}
+
+int sdr_stream_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
+                   const SeqRange& rg, float* cs, hipStream_t st) {
+  const int KD = J * dout / 64;
+#define SRF_STREAM_F(DD, KK) \
+  if (dout == DD && KD == KK) return launch_fwd<DD, KK>(u, B, T, in_n, iters, mask_first, v_out, rg, cs, st);
+  SRF_STREAM_CASES(SRF_STREAM_F)
+#undef SRF_STREAM_F
+  srf::set_error("sdr_stream: unsupported shape J=%d dout=%d", J, dout);
+  return SRF_EUNSUPPORTED;
+}
+
+int sdr_stream_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
+                   int iters, float* gu, const SeqRange& rg, const float* cs, float* gls, hipStream_t st) {
+  if (!cs || !gls) {
+    srf::set_error("sdr_stream backward needs the forward's stored couplings and its scratch workspace");
+    return SRF_EINVAL;
+  }
+  const int KD = J * dout / 64;
+#define SRF_STREAM_B(DD, KK)                                                                                 \
+  if (dout == DD && KD == KK) return launch_bwd<DD, KK>(u, v_saved, g_v, B, T, in_n, iters, gu, rg, cs, gls, \
+                                                        st);
+  SRF_STREAM_CASES(SRF_STREAM_B)
+#undef SRF_STREAM_B
+  srf::set_error("sdr_stream: unsupported shape J=%d dout=%d", J, dout);
+  return SRF_EUNSUPPORTED;
+}
+
+}  // namespace srf

@@ -32,6 +32,17 @@ CASES = [
 ]
 # shapes run again through the first (LDS-state, one workgroup per utterance) recurrence kernels
 LEGACY = [CASES[0], CASES[2], CASES[3], CASES[5]]
+# shapes of the streaming recurrence (route_sdr_stream.hip: dout 32 | 64, J*dout in
+# {512, 1024, 2048}), run with SRF_SDR_SEQ=0 so that shapes the register path also
+# takes come here too
+STREAM = [
+    (1, 3, 16, 64, 20, 20, 16, 5, False),  # C5 inner layer: in_n = 656, J*D = 1024, five iterations
+    (2, 6, 4, 64, 2, 2, 16, 3, True),      # in_n = 20, last-layer mask
+    (2, 5, 8, 32, 12, 12, 16, 3, False),   # D = 32, in_n = 200 (beyond the register path)
+    (1, 4, 4, 64, 1, 1, 8, 2, True),       # J*D = 512
+    (1, 3, 4, 32, 2, 2, 32, 4, False),     # D = 32, J = 32
+    (2, 4, 3, 64, 1, 2, 32, 1, True),      # one iteration, J*D = 2048, in_n = 12 (ragged wave tail)
+]
 
 
 def _mk(case, seed):
@@ -73,6 +84,16 @@ def test_route_sdr_legacy_kernels(cuda, case, monkeypatch):
     """SRF_SDR_SEQ=0 selects the LDS-state recurrence kernels (the path for
     shapes beyond the register-resident kernels' budget)."""
     monkeypatch.setenv('SRF_SDR_SEQ', '0')
+    monkeypatch.setenv('SRF_SDR_STREAM', '0')
+    _check_forward(case, cuda)
+    _check_backward(case, cuda)
+
+
+@pytest.mark.parametrize('case', STREAM)
+def test_route_sdr_stream_kernels(cuda, case, monkeypatch):
+    """The streaming recurrence (u_t re-read per iteration, stored couplings for the
+    backward): forward and backward against the oracle."""
+    monkeypatch.setenv('SRF_SDR_SEQ', '0')
     _check_forward(case, cuda)
     _check_backward(case, cuda)
 
@@ -107,6 +128,7 @@ def test_route_sdr_global_state_kernels(cuda, case, monkeypatch):
     """SRF_SDR_GSTATE=1 moves the legacy kernels' frame state from LDS to the
     global-memory workspace (the path of shapes whose state exceeds one CU's LDS)."""
     monkeypatch.setenv('SRF_SDR_SEQ', '0')
+    monkeypatch.setenv('SRF_SDR_STREAM', '0')
     monkeypatch.setenv('SRF_SDR_GSTATE', '1')
     _check_forward(case, cuda)
     _check_backward(case, cuda)
@@ -114,9 +136,8 @@ def test_route_sdr_global_state_kernels(cuda, case, monkeypatch):
 
 def test_route_sdr_c5_last_layer_shape(cuda):
     """BASELINE C5's last layer (in_n = 16*41 = 656, J = 32, D = 64, 5 iterations,
-    lpad = rpad = 20): the frame state (198 KB forward, 2.3 MB backward) exceeds
-    one CU's LDS, so it runs on the global-state kernels.  Two frames, forward and
-    backward against the oracle."""
+    lpad = rpad = 20): u_t (5.4 MB) exceeds a workgroup's registers, so it runs on
+    the streaming recurrence.  Two frames, forward and backward against the oracle."""
     case = (1, 2, 16, 64, 20, 20, 32, 5, True)
     _check_forward(case, cuda)
     _check_backward(case, cuda)
