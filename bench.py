@@ -39,9 +39,11 @@ WORKLOADS = {
     'timit_c2': (dict(enc=3, iters=3, lpad=4, rpad=4, ph=8, pd=16, ch=8, cd=16, vd=16, context=False), 63, 17, 320),
     'wsj_c4': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=False), 32, 28, 800),
     'wsj_c3': (dict(enc=6, iters=3, lpad=2, rpad=2, ph=16, pd=32, ch=16, cd=32, vd=32, context=True), 32, 28, 800),
-    # BASELINE C5 (HBM-bound stress): PH=CH=16 assumed as in C3; fp32 here --
-    # the fp8 pose MFMA the config names is not built
+    # BASELINE C5 (HBM-bound stress): PH=CH=16 assumed as in C3; fp32 pose
+    # (the parity path) and, as BASELINE names it, the opt-in fp8 (e4m3) pose MFMA
     'wsj_c5': (dict(enc=8, iters=5, lpad=20, rpad=20, ph=16, pd=64, ch=16, cd=64, vd=64, context=True), 32, 28, 800),
+    'wsj_c5_fp8': (dict(enc=8, iters=5, lpad=20, rpad=20, ph=16, pd=64, ch=16, cd=64, vd=64, context=True,
+                        pose_fp8=True), 32, 28, 800),
 }
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / f16 MFMA peak
@@ -64,6 +66,7 @@ def make_config(kw):
     ns.model_caps_class_dim = kw['vd']
     ns.model_caps_context = kw['context']
     ns.model_caps_type = 'naive'
+    ns.model_pose_fp8 = kw.get('pose_fp8', False)
     ns.model_initializer = 'fan_avg'
     ns.train_lr_param_k, ns.train_warmup_n = 0.5, 1200      # train_srf_timit.sh:49-51
     return ns
@@ -283,6 +286,7 @@ def measure(workload, args, world, rank, dev):
         'config': {'workload': f'{workload}: SRF L={cfg.model_encoder_num} PH=CH={cfg.model_caps_primary_num} '
                                f'DIM={cfg.model_caps_primary_dim} LPAD=RPAD={cfg.model_caps_window_lpad} '
                                f'{"SDR" if model.is_context else "DR"} iter={cfg.model_caps_iter}, '
+                               f'{"fp8 (e4m3) pose MFMA, " if model.pose_fp8 else ""}'
                                f'train step (fwd+bwd+allreduce+Adam)',
                    'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
                    'parallelism': f'dp{world}', 'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
@@ -306,6 +310,7 @@ def measure(workload, args, world, rank, dev):
                                                       * {8: 3, 16: 4, 32: 7}[Din] / (kern_avg_ms * 1e-3) / 1e12
                                                       / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
                     if dr else None,
+        'dtype': 'fp8 pose (e4m3, fp32 accumulate) / fp32' if model.pose_fp8 else 'fp32',
         'forward_only': {'value': round(B * T * world * args.steps / fwd_elapsed, 1), 'unit': 'frames/s',
                          'ms_per_step': round(fwd_elapsed / args.steps * 1e3, 4),
                          'mode': 'model(feats, training=False), eager launches'},
@@ -347,7 +352,8 @@ def main():
         'metric': 'acoustic frames/sec through SRF (123-d fbank, 3-iter DR) at 1/2/4/8 MI355X',
         'value': res['value'], 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': res['ms_per_step'], 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic (N(0,1) 123-d fbank, random init)',
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': res['dtype'],
+        'data': 'synthetic (N(0,1) 123-d fbank, random init)',
         'config': res['config'], 'roofline': res['roofline'], 'forward_only': res['forward_only'],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -136,12 +136,21 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
  * recur_workspace: state slices for shapes beyond the register / LDS budget (0 else). */
 int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                        int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream);
+/* The same on fp8 (OCP e4m3) MFMA, opt-in (BASELINE C5 "fp8 pose-transform MFMA"): x
+ * per frame and W per row scaled by powers of two into e4m3 range, fp32 accumulation,
+ * fp32 bias.  Bound per element: |u - u_exact| <= 0.13 * sum_k |W_rk| |x_k| (+ fp32
+ * rounding).  in_d 32 or 64. */
+int srf_route_sdr_pose_fp8(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                           int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream);
 size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters);
 /* Coupling storage per frame (0 when the shape runs on the LDS / global-state
  * kernels): with couplings != NULL ([B][T][this many floats]) recur_fwd stores each
  * frame's couplings c^r and pre-squash s^r, and recur_bwd reads them instead of
- * recomputing the frame's iterations (NULL: recompute). */
+ * recomputing the frame's iterations (NULL: recompute).  Shapes on the streaming
+ * kernels (frames beyond the register budget, e.g. BASELINE C5) have no recompute
+ * path: srf_route_sdr_couplings_required is 1 and recur_bwd needs them. */
 size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters);
+int srf_route_sdr_couplings_required(int in_n, int J, int dout, int iters);
 int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
                             int mask_first, int t0, int t1, float* v_out, float* couplings, void* workspace,
                             size_t workspace_bytes, void* stream);

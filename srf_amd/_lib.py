@@ -36,8 +36,10 @@ _SIGNATURES = {
     'srf_route_sdr_fwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _vp, _vp, _c_size, _vp]),
     'srf_route_sdr_bwd': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _vp, _vp, _vp, _vp, _vp, _c_size, _vp]),
     'srf_route_sdr_pose': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _c_int, _c_int, _vp]),
+    'srf_route_sdr_pose_fp8': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _c_int, _c_int, _vp]),
     'srf_route_sdr_recur_workspace': (_c_size, [_c_int] * 5),
     'srf_route_sdr_coupling_floats': (_c_size, [_c_int] * 4),
+    'srf_route_sdr_couplings_required': (_c_int, [_c_int] * 4),
     'srf_route_sdr_recur_fwd': (_c_int, [_vp] + [_c_int] * 11 + [_vp, _vp, _vp, _c_size, _vp]),
     'srf_route_sdr_recur_bwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _vp] + [_c_int] * 9
                                 + [_vp, _vp, _c_int, _c_int, _vp, _c_size, _vp]),

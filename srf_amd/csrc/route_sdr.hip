@@ -484,6 +484,349 @@ __global__ __launch_bounds__(256) void sdr_gw_kernel(const float* __restrict__ g
   }
 }
 
+// ------------------------------------------------------------------ pose / gx / gW on 32x32 tiles
+// din 32 and 64 (C3/C4/C5): the three frame-parallel contractions of the layer on
+// v_mfma_f32_32x32x2_f32, 32x32 output tiles, each lane feeding one float per operand
+// per MFMA.  K runs in float4 chunks: lane half h supplies k = 8c + 4h + m for
+// MFMA 4c + m (the same permutation on both operands), so every operand load is a
+// float4 along k.  Output lane map: col = lane % 32, row = 8 (reg / 4) + 4 h + reg % 4.
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v mfma32x32x2(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int mfma32_row(int reg, int h) { return 8 * (reg >> 2) + 4 * h + (reg & 3); }
+
+// x_i(frame q) of the window (zeros outside the utterance / past Q), chunk c of lane half h
+template <int KC>
+__device__ __forceinline__ void load_window_x(const float* __restrict__ emb, const FrameMap& fm, int q, int Q, int N,
+                                              int DIN, int w, int n, int lpad, int h, f4 (&x)[KC]) {
+  int b, t;
+  fm.frame(min(q, Q - 1), b, t);
+  const int ts = t + w - lpad;
+  const bool ok = q < Q && ts >= 0 && ts < fm.T;
+  const float* xp = emb + ((size_t)(b * fm.T + min(max(ts, 0), fm.T - 1)) * N + n) * DIN + 4 * h;
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    x[c] = f4{0.f, 0.f, 0.f, 0.f};
+    if (ok) x[c] = *reinterpret_cast<const f4*>(xp + 8 * c);
+  }
+}
+
+// u[f][i][row] = W_i x_i(f) + b_i.  Workgroup = one capsule i, 128 frames x 128 rows;
+// wave (wf, wr) = 64 frames x 64 rows = 2 x 2 tiles (A = x: M = frames, B = W^T: N =
+// rows, so a store writes 32 consecutive rows of one frame).  K = din at once.
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void sdr_pose32_kernel(const float* __restrict__ emb, const float* __restrict__ W,
+                                                            const float* __restrict__ bias, int Q, FrameMap fm, int N,
+                                                            int lpad, int in_n, int JD, int nrb,
+                                                            float* __restrict__ u) {
+  constexpr int KC = DIN / 8;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int i = blockIdx.y;
+  const int rb = blockIdx.x % nrb, fb = blockIdx.x / nrb;
+  const int w = i / N, n = i - w * N;
+  const int f0 = fb * 128 + (wv & 1) * 64, r0 = rb * 128 + (wv >> 1) * 64;
+  f4 a[2][KC], bw[2][KC];
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft) load_window_x<KC>(emb, fm, f0 + ft * 32 + l32, Q, N, DIN, w, n, lpad, h, a[ft]);
+  f16v acc[2][2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int row = min(r0 + rt * 32 + l32, JD - 1);
+    const float* wp = W + ((size_t)i * JD + row) * DIN + 4 * h;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) bw[rt][c] = *reinterpret_cast<const f4*>(wp + 8 * c);
+    const float bv = bias[(size_t)i * JD + row];
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ft][rt][r] = bv;
+  }
+#pragma unroll
+  for (int c = 0; c < KC; ++c)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[ft][rt] = mfma32x32x2(a[ft][c][m], bw[rt][c][m], acc[ft][rt]);
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = f0 + ft * 32 + mfma32_row(r, h);
+      if (q >= Q) continue;
+      int b, t;
+      fm.frame(q, b, t);
+      float* up = u + (fm.view(b, t) * in_n + i) * JD;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int row = r0 + rt * 32 + l32;
+        if (row < JD) up[row] = acc[ft][rt][r];
+      }
+    }
+}
+
+// gx_i(f)[e] = sum_row gu[f][i][row] W_i[row][e], added into g_emb through the window
+// adjoint.  Workgroup = one capsule, 128 frames; wave = 32 frames x din (din/32 tiles);
+// K = JD in chunks of 64 (A = gu rows along k, B = W^T [i][e][row] along k), the next
+// chunk's operands loaded while the current one's MFMAs run.
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void sdr_gx32_kernel(const float* __restrict__ gu, const float* __restrict__ WT,
+                                                          int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
+                                                          float* __restrict__ g_emb) {
+  constexpr int NE = DIN / 32;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int i = blockIdx.y;
+  const int f0 = blockIdx.x * 128 + wv * 32;
+  const int qa = min(f0 + l32, Q - 1);
+  int ba, ta;
+  fm.frame(qa, ba, ta);
+  const float* ap = gu + (fm.view(ba, ta) * in_n + i) * JD + 4 * h;
+  const float* bp[NE];
+#pragma unroll
+  for (int et = 0; et < NE; ++et) bp[et] = WT + ((size_t)i * DIN + et * 32 + l32) * JD + 4 * h;
+  f16v acc[NE];
+#pragma unroll
+  for (int et = 0; et < NE; ++et)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[et][r] = 0.f;
+  f4 a[2][8], bv[2][NE][8];
+  auto fetch = [&](int k0, f4(&ax)[8], f4(&bx)[NE][8]) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bool kin = k0 + 8 * c < JD;   // JD % 8 == 0 (check_sgeom)
+      ax[c] = kin ? *reinterpret_cast<const f4*>(ap + k0 + 8 * c) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int et = 0; et < NE; ++et)
+        bx[et][c] = kin ? *reinterpret_cast<const f4*>(bp[et] + k0 + 8 * c) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  fetch(0, a[0], bv[0]);
+  for (int k0 = 0; k0 < JD; k0 += 128) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (k0 + 64 * s >= JD) break;
+      fetch(k0 + 64 * (s + 1), a[s ^ 1], bv[s ^ 1]);
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int et = 0; et < NE; ++et) acc[et] = mfma32x32x2(a[s][c][m], bv[s][et][c][m], acc[et]);
+    }
+  }
+  const int w = i / N, n = i - w * N;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int q = f0 + mfma32_row(r, h);
+    if (q >= Q) continue;
+    int b, t;
+    fm.frame(q, b, t);
+    const int ts = t + w - lpad;
+    if (ts < 0 || ts >= fm.T) continue;
+    float* gp = g_emb + ((size_t)(b * fm.T + ts) * N + n) * DIN + l32;
+#pragma unroll
+    for (int et = 0; et < NE; ++et) atomicAdd(gp + et * 32, acc[et][r]);
+  }
+}
+
+// gW_i[row][e] (+)= sum_f gu[f][i][row] x_i(f)[e], gbias_i[row] (+)= sum_f gu[f][i][row].
+// Workgroup = one capsule, 128 rows; wave = 32 rows x din; K = frames, two per MFMA
+// (lane half h takes frame 2s + h), 16 frames of loads issued before their MFMAs.
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void sdr_gw32_kernel(const float* __restrict__ gu, const float* __restrict__ emb,
+                                                          int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
+                                                          float* __restrict__ gW, float* __restrict__ gbias,
+                                                          int accumulate) {
+  constexpr int NE = DIN / 32, U = 8;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int i = blockIdx.y;
+  const int r0 = blockIdx.x * 128 + wv * 32;
+  if (r0 >= JD) return;
+  const int row = min(r0 + l32, JD - 1);
+  const int w = i / N, n = i - w * N;
+  f16v acc[NE];
+#pragma unroll
+  for (int et = 0; et < NE; ++et)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[et][r] = 0.f;
+  float sb = 0.f;
+  for (int q0 = 0; q0 < Q; q0 += 2 * U) {
+    float a[U], xv[U][NE];
+#pragma unroll
+    for (int s = 0; s < U; ++s) {
+      const int q = q0 + 2 * s + h;
+      int b, t;
+      fm.frame(min(q, Q - 1), b, t);
+      a[s] = q < Q ? gu[(fm.view(b, t) * in_n + i) * JD + row] : 0.f;
+      const int ts = t + w - lpad;
+      const bool ok = q < Q && ts >= 0 && ts < fm.T;
+      const float* xp = emb + ((size_t)(b * fm.T + min(max(ts, 0), fm.T - 1)) * N + n) * DIN + l32;
+#pragma unroll
+      for (int et = 0; et < NE; ++et) xv[s][et] = ok ? xp[et * 32] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < U; ++s) {
+      sb += a[s];
+#pragma unroll
+      for (int et = 0; et < NE; ++et) acc[et] = mfma32x32x2(a[s], xv[s][et], acc[et]);
+    }
+  }
+  sb += __shfl_xor(sb, 32, 64);
+  if (h == 0 && r0 + l32 < JD) {
+    float* gb = gbias + (size_t)i * JD + r0 + l32;
+    *gb = accumulate ? *gb + sb : sb;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rr = r0 + mfma32_row(r, h);
+    if (rr >= JD) continue;
+#pragma unroll
+    for (int et = 0; et < NE; ++et) {
+      float* dst = gW + ((size_t)i * JD + rr) * DIN + et * 32 + l32;
+      *dst = accumulate ? *dst + acc[et][r] : acc[et][r];
+    }
+  }
+}
+
+// ---- fp8 pose (opt-in, BASELINE C5 "fp8 pose-transform MFMA"): OCP e4m3 operands on
+// v_mfma_f32_32x32x16_fp8_fp8, fp32 accumulation.  Every frame's x_i(f) and every row
+// of W_i gets its own power-of-two scale 2^e with max|a 2^e| in (224, 448] (e4m3's
+// largest finite value is 448), applied exactly, so each product carries at most the
+// two operands' e4m3 rounding (2^-4 relative each): |u - u_exact| <= 0.13 sum_k |W||x|
+// plus fp32 accumulation.  The bias is added in fp32.  Same tiles as sdr_pose32_kernel;
+// lane half h holds k = 16 s + 8 h .. + 7 of k-step s (8 bytes), the same on both operands.
+typedef long fp8x8;
+
+__device__ __forceinline__ int e4m3_exp(float amax) {
+  if (!(amax > 0.f) || !(amax < __builtin_inff())) return 0;
+  int e;
+  (void)frexpf(448.f / amax, &e);   // 2^(e-1) <= 448 / amax < 2^e
+  return max(-100, min(100, e - 1));
+}
+__device__ __forceinline__ fp8x8 pack_e4m3(const f4& a, const f4& b, float s) {
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a.x * s, a.y * s, 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(a.z * s, a.w * s, lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(b.x * s, b.y * s, 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(b.z * s, b.w * s, hi, true);
+  return (fp8x8)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float amax8(const f4& a, const f4& b) {
+  return fmaxf(fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))),
+               fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w))));
+}
+
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(const float* __restrict__ emb, const float* __restrict__ W,
+                                                           const float* __restrict__ bias, int Q, FrameMap fm, int N,
+                                                           int lpad, int in_n, int JD, int nrb,
+                                                           float* __restrict__ u) {
+  constexpr int KS = DIN / 16;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int i = blockIdx.y;
+  const int rb = blockIdx.x % nrb, fb = blockIdx.x / nrb;
+  const int w = i / N, n = i - w * N;
+  const int f0 = fb * 128 + (wv & 1) * 64, r0 = rb * 128 + (wv >> 1) * 64;
+  fp8x8 aq[2][KS], bq[2][KS];
+  int ex[2], ew[2];
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft) {
+    const int q = f0 + ft * 32 + l32;
+    int b, t;
+    fm.frame(min(q, Q - 1), b, t);
+    const int ts = t + w - lpad;
+    const bool ok = q < Q && ts >= 0 && ts < fm.T;
+    const float* xp = emb + ((size_t)(b * fm.T + min(max(ts, 0), fm.T - 1)) * N + n) * DIN + 8 * h;
+    f4 x[KS][2];
+    float mx = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) x[s][c] = ok ? *reinterpret_cast<const f4*>(xp + 16 * s + 4 * c) : f4{0.f, 0.f, 0.f, 0.f};
+      mx = fmaxf(mx, amax8(x[s][0], x[s][1]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));   // the frame's other half of din
+    ex[ft] = e4m3_exp(mx);
+    const float sc = srf_exp2i(ex[ft]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) aq[ft][s] = pack_e4m3(x[s][0], x[s][1], sc);
+  }
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int row = min(r0 + rt * 32 + l32, JD - 1);
+    const float* wp = W + ((size_t)i * JD + row) * DIN + 8 * h;
+    f4 x[KS][2];
+    float mx = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) x[s][c] = *reinterpret_cast<const f4*>(wp + 16 * s + 4 * c);
+      mx = fmaxf(mx, amax8(x[s][0], x[s][1]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    ew[rt] = e4m3_exp(mx);
+    const float sc = srf_exp2i(ew[rt]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bq[rt][s] = pack_e4m3(x[s][0], x[s][1], sc);
+  }
+  f16v acc[2][2];
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ft][rt][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+        acc[ft][rt] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(aq[ft][s], bq[rt][s], acc[ft][rt], 0, 0, 0);
+  float bv[2], sw[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int row = min(r0 + rt * 32 + l32, JD - 1);
+    bv[rt] = bias[(size_t)i * JD + row];
+    sw[rt] = srf_exp2i(-ew[rt]);
+  }
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int fr = mfma32_row(r, h);
+      const float sx = srf_exp2i(-__shfl(ex[ft], fr, 64));   // the frame's scale, from the lane that loaded it
+      const int q = f0 + ft * 32 + fr;
+      if (q >= Q) continue;
+      int b, t;
+      fm.frame(q, b, t);
+      float* up = u + (fm.view(b, t) * in_n + i) * JD;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int row = r0 + rt * 32 + l32;
+        if (row < JD) up[row] = acc[ft][rt][r] * sx * sw[rt] + bv[rt];
+      }
+    }
+}
+
+// Which contraction runs on the 32x32-tile kernels, by din (scripts/bench_sdr_gemm.py,
+// one frame range alone on the GPU, us 32x32 vs 16x16): C5 din 64 pose 850 vs 973, gx
+// 1228 vs 1174, gW 937 vs 1073; C3 din 32 pose 46 vs 33, gx 47 vs 53, gW 91 vs 65.
+// SRF_SDR_MFMA32=0 / 1 forces one family for all three (A/B).
+enum class SdrGemm { kPose, kGx, kGw };
+bool use_mfma32(int din, int JD, SdrGemm k) {
+  if ((din != 32 && din != 64) || JD % 8) return false;
+  const char* e = getenv("SRF_SDR_MFMA32");
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  return din == 64 ? k != SdrGemm::kGx : k == SdrGemm::kGx;
+}
+
 // ------------------------------------------------------------------ host
 int check_sgeom(const SGeom& g) {
   SRF_REQUIRE(g.B > 0 && g.T > 0 && g.N > 0 && g.J > 1, "bad shape B=%d T=%d N=%d J=%d", g.B, g.T, g.N, g.J);
@@ -512,9 +855,37 @@ size_t gstate_bytes(const SGeom& g, size_t state_bytes) {
 FrameMap frame_map(int T, int t0, int t1, int v0, int vn) { return FrameMap{T, t0, t1 - t0, v0, vn}; }
 
 int pose_range(const SGeom& g, const float* emb, const float* W, const float* bias, const FrameMap& fm, float* u,
-               hipStream_t st) {
+               hipStream_t st, bool fp8 = false) {
   const int Q = g.B * fm.nt;
   if (Q == 0) return SRF_OK;
+  if (fp8) {
+    if ((g.din != 32 && g.din != 64) || g.JD() % 8) {
+      srf::set_error("fp8 pose: in_d must be 32 or 64 (got %d) and J*out_d a multiple of 8", g.din);
+      return SRF_EUNSUPPORTED;
+    }
+    const int nrb = (g.JD() + 127) / 128;
+    const dim3 grid(nrb * ((Q + 127) / 128), g.in_n());
+    if (g.din == 32)
+      hipLaunchKernelGGL(sdr_pose8_kernel<32>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
+                         g.JD(), nrb, u);
+    else
+      hipLaunchKernelGGL(sdr_pose8_kernel<64>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
+                         g.JD(), nrb, u);
+    SRF_LAUNCH_CHECK("sdr_pose8");
+    return SRF_OK;
+  }
+  if (use_mfma32(g.din, g.JD(), SdrGemm::kPose)) {
+    const int nrb = (g.JD() + 127) / 128;
+    const dim3 grid(nrb * ((Q + 127) / 128), g.in_n());
+    if (g.din == 32)
+      hipLaunchKernelGGL(sdr_pose32_kernel<32>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
+                         g.JD(), nrb, u);
+    else
+      hipLaunchKernelGGL(sdr_pose32_kernel<64>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
+                         g.JD(), nrb, u);
+    SRF_LAUNCH_CHECK("sdr_pose32");
+    return SRF_OK;
+  }
   constexpr int FT = 2;   // frame tiles per workgroup: each W fragment feeds two MFMA chains
   const dim3 grid((Q + 16 * FT - 1) / (16 * FT), g.in_n());
 #define SRF_POSE(DIN)                                                                                            \
@@ -581,6 +952,17 @@ size_t recur_workspace(const SGeom& g) {
 int gx_range(const SGeom& g, const float* gu, const float* WT, const FrameMap& fm, float* g_emb, hipStream_t st) {
   const int Q = g.B * fm.nt;
   if (Q == 0) return SRF_OK;
+  if (use_mfma32(g.din, g.JD(), SdrGemm::kGx)) {
+    const dim3 grid((Q + 127) / 128, g.in_n());
+    if (g.din == 32)
+      hipLaunchKernelGGL(sdr_gx32_kernel<32>, grid, dim3(256), 0, st, gu, WT, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
+                         g_emb);
+    else
+      hipLaunchKernelGGL(sdr_gx32_kernel<64>, grid, dim3(256), 0, st, gu, WT, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
+                         g_emb);
+    SRF_LAUNCH_CHECK("sdr_gx32");
+    return SRF_OK;
+  }
   const dim3 grid((Q + 15) / 16, g.in_n());
 #define SRF_GX(DIN) \
   hipLaunchKernelGGL(sdr_gx_kernel<DIN>, grid, dim3(64), 0, st, gu, WT, Q, fm, g.N, g.lpad, g.in_n(), g.JD(), g_emb)
@@ -599,6 +981,17 @@ int gw_range(const SGeom& g, const float* gu, const float* emb, const FrameMap& 
              float* g_bias, hipStream_t st) {
   const int Q = g.B * fm.nt;
   if (Q == 0 && accumulate) return SRF_OK;
+  if (use_mfma32(g.din, g.JD(), SdrGemm::kGw)) {
+    const dim3 grid((g.JD() + 127) / 128, g.in_n());
+    if (g.din == 32)
+      hipLaunchKernelGGL(sdr_gw32_kernel<32>, grid, dim3(256), 0, st, gu, emb, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
+                         g_W, g_bias, accumulate);
+    else
+      hipLaunchKernelGGL(sdr_gw32_kernel<64>, grid, dim3(256), 0, st, gu, emb, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
+                         g_W, g_bias, accumulate);
+    SRF_LAUNCH_CHECK("sdr_gw32");
+    return SRF_OK;
+  }
   const int tasks = g.in_n() * g.NT();
   const dim3 grid((tasks + 3) / 4);
 #define SRF_GW(DIN)                                                                                             \
@@ -737,6 +1130,15 @@ int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int 
   return pose_range(g, emb, W, bias, frame_map(T, t0, t1, v0, vn), u, static_cast<hipStream_t>(stream));
 }
 
+int srf_route_sdr_pose_fp8(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                           int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = range_ok(g, t0, t1, v0, vn))) return rc;
+  SRF_REQUIRE(emb && W && bias && u, "null pointer argument");
+  return pose_range(g, emb, W, bias, frame_map(T, t0, t1, v0, vn), u, static_cast<hipStream_t>(stream), true);
+}
+
 size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters) {
   SGeom g{B, 1, in_n, 8, 0, 0, J, dout, iters, 0};
   return recur_workspace(g);
@@ -745,6 +1147,10 @@ size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters
 size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters) {
   const size_t n = srf::sdr_seq_cs_floats(in_n, J, dout, iters);
   return n ? n : srf::sdr_stream_cs_floats(in_n, J, dout, iters);
+}
+
+int srf_route_sdr_couplings_required(int in_n, int J, int dout, int iters) {
+  return !srf::sdr_seq_supported(in_n, J, dout, iters) && srf::sdr_stream_supported(in_n, J, dout, iters);
 }
 
 int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,

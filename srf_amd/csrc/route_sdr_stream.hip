@@ -51,7 +51,9 @@ struct SC {
   static constexpr int J = JD / D;
   static constexpr int RQ = D / KD;           // lanes per output capsule
   static constexpr int NE = JD / kNT;         // elements per thread in the element phases
-  static constexpr int PD = KD <= 16 ? 4 : 2; // capsules in flight per wave
+  // capsules in flight per wave in the forward / backward register ring
+  static constexpr int PDF = KD <= 8 ? 8 : KD <= 16 ? 6 : 3;
+  static constexpr int PDB = KD <= 16 ? 4 : 2;
   static constexpr int HD = 8;                 // gu outputs per lane per sub-pass (registers: 2R*HD)
   static_assert(D % KD == 0 && NE >= 1 && KD % 4 == 0 && KD % HD == 0, "unsupported stream shape");
 };
@@ -62,18 +64,27 @@ __host__ __device__ inline size_t cs_rec(int in_n, int J, int D, int R) {
 }
 
 // position in a wave's capsule stream: frame t, pass p of the frame, capsule slot m
+// (branch-free: selects, so that the compiler's vmcnt waits on the ring stay exact)
 struct Cur {
   int t, p, m;
   __device__ __forceinline__ void adv(int NMp, int NP, int dt) {
-    if (++m == NMp) {
-      m = 0;
-      if (++p == NP) {
-        p = 0;
-        t += dt;
-      }
-    }
+    const bool wm = m + 1 == NMp;
+    m = wm ? 0 : m + 1;
+    const bool wp = wm && p + 1 == NP;
+    p = wp ? 0 : p + (wm ? 1 : 0);
+    t += wp ? dt : 0;
   }
 };
+
+// buffer resource over n floats (n = 0: every access dropped); an offset of
+// kDrop bytes is out of range, so a store predicated off is a dropped store, not a branch
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t float_rsrc(const float* p, size_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, p ? (int)(n * 4) : 0, 0x00020000);
+}
+constexpr uint32_t kDrop = 0x80000000u;
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t rs, float v, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, off, 0, 0);
+}
 
 template <int KD>
 __device__ __forceinline__ void load_slice(const float* __restrict__ p, float (&x)[KD]) {
@@ -121,11 +132,12 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(const float* __rest
                                                              int iters, int mask_first, float* __restrict__ v_out,
                                                              srf::SeqRange rg, float* __restrict__ cs, int NMp) {
   using C = SC<D, KD>;
-  constexpr int JD = C::JD, J = C::J, PD = C::PD, NE = C::NE;
+  constexpr int JD = C::JD, J = C::J, PD = C::PDF, NE = C::NE;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* wl = lds;
   float* part = lds + JD;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: capsule indices in SGPRs
   if (rg.t0 >= rg.t1) return;
   const int b = blockIdx.x;
   const int j = lane / C::RQ;
@@ -156,7 +168,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(const float* __rest
   __syncthreads();
 
   for (int t = rg.t0; t < rg.t1; ++t) {
-    float* csf = cs ? cs + ((size_t)b * T + t) * csr : nullptr;
+    const __amdgpu_buffer_rsrc_t csf = float_rsrc(cs ? cs + ((size_t)b * T + t) * csr : nullptr, csr);
     for (int r = 0; r < iters; ++r) {
       float w[KD], acc[KD];
       load_slice<KD>(wl + lane * KD, w);
@@ -174,8 +186,9 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(const float* __rest
           const float c = iv ? ex * __builtin_amdgcn_rcpf(group_sum<C::RQ, 64>(ex)) : 0.f;
 #pragma unroll
           for (int d = 0; d < KD; ++d) acc[d] += c * xr[p][d];
-          if (csf && q0 && iv) csf[(size_t)r * in_n * J + (size_t)i * J + j] = c;
+          bstore(csf, c, q0 && iv ? (uint32_t)((r * in_n + i) * J + j) * 4 : kDrop);
           issue(xr[p]);
+          __builtin_amdgcn_sched_barrier(0);   // keep the ring order: no hoisting across capsules
         }
       }
 #pragma unroll
@@ -189,7 +202,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(const float* __rest
 #pragma unroll
         for (int w2 = 0; w2 < kNW; ++w2) s += part[w2 * JD + e];
         const float v = s * squash_fac(group_sum<1, D>(s * s));
-        if (csf) csf[(size_t)iters * in_n * J + (size_t)r * JD + e] = s;
+        bstore(csf, s, (uint32_t)(iters * in_n * J + r * JD + e) * 4);
         if (r == iters - 1) {
           vo[(size_t)t * JD + e] = v;
           vc[n] = v;   // v_t: Vc^0 of frame t + 1
@@ -214,12 +227,13 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(const float* __rest
                                                              const float* __restrict__ cs, float* __restrict__ gls,
                                                              int NMp) {
   using C = SC<D, KD>;
-  constexpr int JD = C::JD, J = C::J, PD = C::PD, NE = C::NE, HD = C::HD;
+  constexpr int JD = C::JD, J = C::J, PD = C::PDB, NE = C::NE, HD = C::HD;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* part = lds;
   float* gsl = part + kNW * JD;
   float* vcl = gsl + kRM * JD;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: capsule indices in SGPRs
   if (rg.t0 >= rg.t1) return;
   const int b = blockIdx.x;
   const int R = iters;
@@ -232,6 +246,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(const float* __rest
   const size_t csr = cs_rec(in_n, J, D, iters);
   const float* csb = cs + (size_t)b * T * csr;
   float* gl = gls + (size_t)b * R * PJ;
+  const __amdgpu_buffer_rsrc_t glr = float_rsrc(gl, (size_t)R * PJ);
   float* carry_io = rg.carry ? rg.carry + (size_t)b * JD : nullptr;
 
   float carry[NE];
@@ -249,10 +264,10 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(const float* __rest
     lc.adv(NMp, R, -1);
   };
 
+#pragma unroll
+  for (int p = 0; p < PD; ++p) issue(xr[p], cr[p]);
   for (int t = rg.t1 - 1; t >= rg.t0; --t) {
     const float* csf = csb + (size_t)t * csr;
-#pragma unroll
-    for (int p = 0; p < PD; ++p) issue(xr[p], cr[p]);
     // ---- element phase: Vc^r from s^r, the top adjoint
     float gv[NE];
 #pragma unroll
@@ -291,9 +306,9 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(const float* __rest
           const float gL = c * (qd - sig);
 #pragma unroll
           for (int d = 0; d < KD; ++d) gacc[d] += gL * xr[pp][d];
-          if (q0 && iv) gl[(size_t)r * PJ + (size_t)i * J + j] = gL;
-          // the ring stops at the frame's last pass: the gu pass below needs its registers
-          if (!(p == R - 1 && m0 + pp + PD >= NMp)) issue(xr[pp], cr[pp]);
+          bstore(glr, gL, q0 && iv ? (uint32_t)((r * in_n + i) * J + j) * 4 : kDrop);
+          issue(xr[pp], cr[pp]);   // runs on into frame t - 1 (the gu pass leaves the ring alone)
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
 #pragma unroll
@@ -312,8 +327,6 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(const float* __rest
       }
       __syncthreads();
     }
-    // skip the issue-slot bookkeeping of the stopped ring: restart at frame t-1
-    lc = Cur{t - 1, 0, 0};
     // ---- gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j, HD outputs per lane per sub-pass
     float* gut = gub + (size_t)(t - rg.tg0) * ff;
 #pragma unroll
@@ -393,7 +406,7 @@ int launch_fwd(const float* u, int B, int T, int in_n, int iters, int mask_first
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k, dim3(B), dim3(kNT), lds, st, u, T, in_n, iters, mask_first, v_out, rg, cs,
-                     nm_padded(in_n, C::PD));
+                     nm_padded(in_n, C::PDF));
   SRF_LAUNCH_CHECK("sdr_stream_fwd");
   return SRF_OK;
 }
@@ -407,7 +420,7 @@ int launch_bwd(const float* u, const float* v_saved, const float* g_v, int B, in
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k, dim3(B), dim3(kNT), lds, st, u, v_saved, g_v, T, in_n, iters, gu, rg, cs, gls,
-                     nm_padded(in_n, C::PD));
+                     nm_padded(in_n, C::PDB));
   SRF_LAUNCH_CHECK("sdr_stream_bwd");
   return SRF_OK;
 }

@@ -463,29 +463,34 @@ class SdrStackPlan:
     bounds of layer l shifted down by l * rpad, range (l, k) depends on (l - 1, k)
     and (l, k - 1) only: the L layers run as a wavefront, one HIP stream per layer,
     L per-utterance recurrences in flight instead of one.  The backward walks the
-    ranges in reverse with bounds shifted up by (L - 1 - l) * rpad: (l, k) needs
-    layer l+1's gx (the window adjoint) down to frame t0 - rpad, i.e. (l + 1, k).
+    same ranges in reverse: (l, k) needs layer l+1's gx (the window adjoint) down to
+    frame t0 - rpad, i.e. (l + 1, k), and the carry of (l, k + 1).
     layers: [(N, din, J, dout, mask_first)] per layer."""
 
-    def __init__(self, B, T, layers, lpad, rpad, iters, n_chunks=0):
+    def __init__(self, B, T, layers, lpad, rpad, iters, n_chunks=0, pose_fp8=False):
         self.B, self.T, self.lpad, self.rpad, self.iters = B, T, lpad, rpad, iters
+        self.pose_fp8 = bool(pose_fp8)
         self.layers = layers
         self.L = len(layers)
         self.win = lpad + rpad + 1
         if n_chunks <= 0:
             n_chunks = int(os.environ.get('SRF_SDR_CHUNKS', '0') or 0) or max(1, min(16, -(-T // 20)))
-        K = max(1, min(n_chunks, T))
-        self.K = K
-        c = [round(k * T / K) for k in range(K + 1)]
+        # ranges of S frames on one grid, layer l's shifted down by l * rpad; the grid
+        # runs M >= K ranges so that no layer's shifted range is clipped into a long
+        # one (C5: rpad = 20 frames per layer would otherwise leave the last layer one
+        # 160-frame range at the end of the forward and the first layer one at the end
+        # of the backward).  Ranges outside [0, T) are empty.  The backward uses the
+        # same bounds: (l, k) needs (l + 1, k) for the window adjoint and (l, k + 1) for
+        # the carry.
+        S = -(-T // max(1, min(n_chunks, T)))
+        K = -(-(T + rpad * (self.L - 1)) // S)
+        self.K, self.S = K, S
 
         def bounds(shift):
-            b = [0] + [min(max(c[k] + shift, 0), T) for k in range(1, K)] + [T]
-            for k in range(1, K + 1):        # monotone after clipping
-                b[k] = max(b[k], b[k - 1])
-            return b
+            return [min(max(k * S + shift, 0), T) for k in range(K)] + [T]
         self.fwd = [bounds(-rpad * l) for l in range(self.L)]
-        self.bwd = [bounds(rpad * (self.L - 1 - l)) for l in range(self.L)]
-        self.nmax = max(max(b[k + 1] - b[k] for k in range(K)) for b in self.fwd + self.bwd)
+        self.bwd = self.fwd
+        self.nmax = max(max(b[k + 1] - b[k] for k in range(K)) for b in self.fwd)
         L_ = _lib.lib()
         self.rws = [L_.srf_route_sdr_recur_workspace(B, N * self.win, J, D, iters) for (N, din, J, D, mf) in layers]
 
@@ -524,8 +529,12 @@ def _layer_streams(dev, n, role):
     return ss[:n]
 
 
-def _store_u(plan):
-    budget = float(os.environ.get('SRF_SDR_STORE_U_GB', '24')) * 2 ** 30
+def _store_u(plan, dev):
+    """Keep every layer's pose output u from the forward for the backward (instead of
+    recomputing it per range) when it fits SRF_SDR_STORE_U_GB, by default 55 % of the
+    device's memory: C5 keeps 135 GB of u on a 288 GB MI355X, C3 5.5 GB."""
+    gb = os.environ.get('SRF_SDR_STORE_U_GB', '')
+    budget = float(gb) * 2 ** 30 if gb else 0.55 * torch.cuda.get_device_properties(dev).total_memory
     return sum(plan.u_floats(l, plan.T) for l in range(plan.L)) * 4 <= budget
 
 
@@ -552,14 +561,16 @@ class SdrStack(torch.autograd.Function):
         gammas, betas = params[2 * L::2], params[2 * L + 1::2]
         _check_dev('emb0', emb0, (B, T, P.layers[0][0], P.layers[0][1]))
         need_bwd = P.need_bwd
-        store = need_bwd and _store_u(P)
+        store = need_bwd and _store_u(P, emb0.device)
         tr = int(bool(training))
         embs, vs, stats, us, rws, css = [emb0], [], [], [], [], []
         for l, (N, din, J, D, mf) in enumerate(P.layers):
             vs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
             # each frame's couplings and s^r, for a backward without the recompute
+            # (SRF_SDR_CS=0: recompute them, where the shape's kernels can)
             ncs = L_.srf_route_sdr_coupling_floats(P.in_n(l), J, D, P.iters) \
-                if need_bwd and os.environ.get('SRF_SDR_CS', '1') != '0' else 0
+                if need_bwd and (os.environ.get('SRF_SDR_CS', '1') != '0'
+                                 or L_.srf_route_sdr_couplings_required(P.in_n(l), J, D, P.iters)) else 0
             css.append(torch.empty(B * T * ncs, device=dev, dtype=torch.float32) if ncs else None)
             if l < L - 1:
                 embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
@@ -582,8 +593,9 @@ class SdrStack(torch.autograd.Function):
             if t1 > t0:
                 sp = ctypes_void(s.cuda_stream)
                 v0, vn = (0, T) if store else (t0, P.nmax)
-                _lib.check(L_.srf_route_sdr_pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din, P.lpad,
-                                                 P.rpad, J, D, t0, t1, _ptr(us[l]), v0, vn, sp), 'sdr_pose')
+                pose = L_.srf_route_sdr_pose_fp8 if P.pose_fp8 else L_.srf_route_sdr_pose
+                _lib.check(pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din, P.lpad,
+                                P.rpad, J, D, t0, t1, _ptr(us[l]), v0, vn, sp), 'sdr_pose')
                 _lib.check(L_.srf_route_sdr_recur_fwd(_ptr(us[l]), v0, vn, B, T, P.in_n(l), J, D, P.iters, mf, t0,
                                                       t1, _ptr(vs[l]), _ptr(css[l]) if css[l] is not None else None,
                                                       _ptr(rws[l]), rws[l].numel(), sp), 'sdr_recur_fwd')
@@ -662,9 +674,9 @@ class SdrStack(torch.autograd.Function):
                                'capsnorm_bwd_range')
                 v0, vn = (0, T) if store else (t0, P.nmax)
                 if not store:
-                    _lib.check(L_.srf_route_sdr_pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din,
-                                                     P.lpad, P.rpad, J, D, t0, t1, _ptr(urs[l]), v0, vn, sp),
-                               'sdr_pose')
+                    pose = L_.srf_route_sdr_pose_fp8 if P.pose_fp8 else L_.srf_route_sdr_pose
+                    _lib.check(pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din,
+                                    P.lpad, P.rpad, J, D, t0, t1, _ptr(urs[l]), v0, vn, sp), 'sdr_pose')
                 cs = ctx.css[l]
                 g0, gn = (0, T) if whole_gu else (t0, P.nmax)
                 _lib.check(L_.srf_route_sdr_recur_bwd(_ptr(urs[l]), v0, vn, _ptr(vs[l]),

@@ -86,6 +86,10 @@ class SequenceRouter(torch.nn.Module):
         self.route_iters = 1 if self.caps_type == 'lowmemory' else self.iter
         self.proj_scale = math.sqrt(self.caps_inp_n) if self.caps_type == 'einsum' else 1.0
         self.length_eps = LENGTH_EPS_EINSUM if self.caps_type == 'einsum' else LENGTH_EPS
+        # Opt-in fp8 (e4m3) pose transform for SDR stacks (BASELINE C5 "fp8 pose-transform
+        # MFMA"; not a reference flag: the reference is fp32 throughout).  Its bound is
+        # stated in include/srf.h (srf_route_sdr_pose_fp8); gradients stay fp32.
+        self.pose_fp8 = bool(getattr(config, 'model_pose_fp8', False)) or os.environ.get('SRF_POSE_FP8', '') == '1'
         self.dropout_enabled = True     # test hook: parity runs use BN batch stats without dropout
         self.n_chunks_override = {}     # layer -> n_chunks (tuning hook)
         # Dropout seed base.  Parameters are initialised from `seed` identically on every
@@ -238,7 +242,7 @@ class SequenceRouter(torch.nn.Module):
             layers = []
             for l, (in_n, out_n, out_d, in_d) in enumerate(self.layer_shapes):
                 layers.append((in_n // self.window, in_d, out_n, out_d, int(l == self.enc_num - 1)))
-            p = ops.SdrStackPlan(B, T, layers, self.lpad, self.rpad, self.route_iters)
+            p = ops.SdrStackPlan(B, T, layers, self.lpad, self.rpad, self.route_iters, pose_fp8=self.pose_fp8)
             self._geoms[key] = p
         return p
 

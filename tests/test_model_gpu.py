@@ -239,17 +239,21 @@ def test_graphed_dropout_gradient_matches_finite_difference(cuda):
         g.close()
 
 
-@pytest.mark.parametrize('name,chunks,cs', [('c3_mini_sdr', 1, '1'), ('c3_mini_sdr', 3, '1'), ('c3_mini_sdr', 64, '1'),
-                                            ('c3_real', 4, '1'), ('c3_real', 4, '0'), ('c5_real', 3, '1'),
-                                            ('c3_mini_sdr_lowmemory', 2, '1')])
-def test_sdr_stack_matches_layer_by_layer(cuda, name, chunks, cs, monkeypatch):
+@pytest.mark.parametrize('name,chunks,cs,store', [('c3_mini_sdr', 1, '1', ''), ('c3_mini_sdr', 3, '1', ''),
+                                                  ('c3_mini_sdr', 64, '1', ''), ('c3_real', 4, '1', ''),
+                                                  ('c3_real', 4, '0', ''), ('c3_real', 4, '1', '0'),
+                                                  ('c5_real', 3, '1', ''), ('c5_real', 3, '1', '0'),
+                                                  ('c3_mini_sdr_lowmemory', 2, '1', '')])
+def test_sdr_stack_matches_layer_by_layer(cuda, name, chunks, cs, store, monkeypatch):
     """The layer-pipelined SDR stack (ops.SdrStack: frame ranges of every layer as a
     wavefront over one HIP stream per layer) against the layer-by-layer path
     (SRF_SDR_STACK=0): the same logits and gradients to fp32 reassociation, for one
     range, several, and one frame per range (64 > T'); its backward from the
-    forward's stored couplings (SRF_SDR_CS=1) and recomputing them (0)."""
+    forward's stored couplings (SRF_SDR_CS=1) and recomputing them (0); u kept from
+    the forward (default) and recomputed per range (SRF_SDR_STORE_U_GB=0)."""
     from srf_amd import ctc
     monkeypatch.setenv('SRF_SDR_CS', cs)
+    monkeypatch.setenv('SRF_SDR_STORE_U_GB', store)
     outs = []
     for stack in ('1', '0'):
         monkeypatch.setenv('SRF_SDR_STACK', stack)

@@ -141,3 +141,56 @@ def test_route_sdr_c5_last_layer_shape(cuda):
     case = (1, 2, 16, 64, 20, 20, 32, 5, True)
     _check_forward(case, cuda)
     _check_backward(case, cuda)
+
+
+@pytest.mark.parametrize('din,J,D', [(64, 16, 64), (64, 32, 64), (32, 16, 32)])
+def test_sdr_pose_fp8_bound(cuda, din, J, D):
+    """srf_route_sdr_pose_fp8 (opt-in e4m3 pose, BASELINE C5) against the float64 pose
+    (sequence_router_naive.py:154-159): per element |u - ref| <= 0.13 sum_k |W||x|
+    (each operand rounded to e4m3, 2^-4 relative, after a per-row / per-frame
+    power-of-two scale) + fp32 rounding, on operands whose rows and frames span
+    2^-20 .. 2^4 with zero (padded) frames.  The median error must stay at e4m3
+    level (not merely inside the bound)."""
+    import ctypes
+    from srf_amd import _lib
+    B, T, N, lp, rp = 2, 9, 3, 2, 1
+    t0, t1 = 2, 8
+    in_n, JD = N * (lp + rp + 1), J * D
+    rng = np.random.default_rng(21)
+    emb = rng.standard_normal((B, T, N, din)) * 2.0 ** rng.uniform(-20, 4, (B, T, N, 1))
+    emb[1, 4] = 0.0
+    W = rng.standard_normal((in_n, JD, din)) * 0.1 * 2.0 ** rng.uniform(-20, 4, (in_n, JD, 1))
+    bias = rng.standard_normal((in_n, JD)) * 0.1
+    L = _lib.lib()
+    te = torch.tensor(emb, dtype=torch.float32, device=cuda)
+    tW = torch.tensor(W, dtype=torch.float32, device=cuda)
+    tb = torch.tensor(bias, dtype=torch.float32, device=cuda)
+    nt = t1 - t0
+    u = torch.full((B, nt, in_n, JD), float('nan'), device=cuda)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    _lib.check(L.srf_route_sdr_pose_fp8(p(te), p(tW), p(tb), B, T, N, din, lp, rp, J, D, t0, t1, p(u), t0, nt, st),
+               'pose_fp8')
+    torch.cuda.synchronize()
+    e32 = te.double().cpu().numpy()   # the fp32 operands the kernel saw
+    W32 = tW.double().cpu().numpy()
+    b32 = tb.double().cpu().numpy()
+    x = so.window(e32, lp, rp)[:, t0:t1]                      # [B, nt, in_n, din]
+    ref = np.einsum('irk,btik->btir', W32, x) + b32[None, None]
+    mag = np.einsum('irk,btik->btir', np.abs(W32), np.abs(x))
+    got = u.cpu().double().numpy()
+    err = np.abs(got - ref)
+    assert np.all(err <= 0.13 * mag + 1e-6 * (np.abs(ref) + 1e-30)), (err - 0.13 * mag).max()
+    rel = err[mag > 0] / mag[mag > 0]
+    assert np.median(rel) < 0.02, np.median(rel)
+
+
+@pytest.mark.parametrize('mf', ['0', '1'])
+@pytest.mark.parametrize('case', [CASES[2], CASES[3], STREAM[1]])
+def test_route_sdr_gemm_families(cuda, case, mf, monkeypatch):
+    """Both kernel families of the frame-parallel contractions (pose, gx, gW; 16x16
+    f32 MFMA tiles and 32x32 ones, chosen per contraction and din by default) forced
+    for all three, din 32 and 64, against the oracle."""
+    monkeypatch.setenv('SRF_SDR_MFMA32', mf)
+    _check_forward(case, cuda)
+    _check_backward(case, cuda)
