@@ -118,6 +118,46 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
                       float* g_emb, float* g_W, float* g_bias, void* workspace, size_t workspace_bytes,
                       void* stream);
 
+/* ---- Batched frame ranges (the layer-pipelined SDR stack, ops.SdrStack): one launch
+ * runs up to SRF_SDR_MAX_ITEMS frame ranges [t0, t1) of layers with the same shape
+ * (one anti-diagonal of the stack's wavefront), instead of one HIP stream per layer.
+ * Each entry point reads only its fields; the single-range functions below are the
+ * n = 1 case.  Ranges with t0 == t1 are skipped (gW: one with accumulate == 0 still
+ * zeroes its layer's gradient).  Replaces the per-layer loop of
+ * sequence_router_naive.py:145-191 over the frames of :162-170. */
+#define SRF_SDR_MAX_ITEMS 8
+typedef struct {
+  int t0, t1;                  /* frame range of every utterance */
+  const float* emb;            /* layer input [B][T][N][din] (pose, gW) */
+  const float* W;              /* pose: [in_n][J*dout][din] */
+  const float* bias;           /* pose: [in_n][J*dout] */
+  const float* WT;             /* gx: W^T [in_n][din][J*dout] */
+  float* u;                    /* pose output / recurrence input, frames [v0, v0 + vn) */
+  int v0, vn;
+  float* v;                    /* recur_fwd: v_out; recur_bwd: the forward's v [B][T][J*dout] */
+  float* couplings;            /* [B][T][srf_route_sdr_coupling_floats] or NULL */
+  void* workspace;             /* srf_route_sdr_recur_workspace bytes, per range */
+  size_t workspace_bytes;
+  const float* g_v;            /* recur_bwd: dL/dv [B][T][J*dout] */
+  float* carry;                /* recur_bwd: [B][J*dout] in / out */
+  float* gu;                   /* recur_bwd output, gx / gW input: frames [g0, g0 + gn) */
+  int g0, gn;
+  float* g_emb;                /* gx: added into [B][T][N][din] */
+  float* g_W;                  /* gW: [in_n][J*dout][din] */
+  float* g_bias;               /* gW: [in_n][J*dout] */
+  int accumulate;              /* gW: add to g_W / g_bias (else overwrite) */
+} srf_sdr_range;
+int srf_route_sdr_pose_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                         int dout, int fp8, void* stream);
+int srf_route_sdr_recur_fwd_n(const srf_sdr_range* ranges, int n, int B, int T, int in_n, int J, int dout, int iters,
+                              int mask_first, void* stream);
+int srf_route_sdr_recur_bwd_n(const srf_sdr_range* ranges, int n, int B, int T, int in_n, int J, int dout, int iters,
+                              int mask_first, void* stream);
+int srf_route_sdr_gx_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                       int dout, void* stream);
+int srf_route_sdr_gw_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                       int dout, void* stream);
+
 /* ---- The SDR layer in frame ranges (the layer-pipelined SDR stack) ----------
  * srf_route_sdr_fwd/bwd split into calls over frames [t0, t1) of every utterance,
  * so a host can run an SDR stack as a wavefront over (layer, frame range): layer

@@ -12,6 +12,20 @@ LIB_PATH = os.environ.get('SRF_LIB_PATH') or os.path.join(_HERE, 'libsrf.so')   
 
 _c_int, _c_size, _vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
 
+SDR_MAX_ITEMS = 8   # SRF_SDR_MAX_ITEMS
+
+
+class SdrRange(ctypes.Structure):
+    """srf_sdr_range: one frame range of one SDR layer for the batched entry points."""
+    _fields_ = [('t0', _c_int), ('t1', _c_int), ('emb', _vp), ('W', _vp), ('bias', _vp), ('WT', _vp),
+                ('u', _vp), ('v0', _c_int), ('vn', _c_int), ('v', _vp), ('couplings', _vp),
+                ('workspace', _vp), ('workspace_bytes', _c_size), ('g_v', _vp), ('carry', _vp),
+                ('gu', _vp), ('g0', _c_int), ('gn', _c_int), ('g_emb', _vp), ('g_W', _vp), ('g_bias', _vp),
+                ('accumulate', _c_int)]
+
+
+_ranges = ctypes.POINTER(SdrRange)
+
 # name -> (restype, argtypes); mirrors include/srf.h one to one.
 _SIGNATURES = {
     'srf_version': (_c_int, []),
@@ -46,6 +60,11 @@ _SIGNATURES = {
     'srf_route_sdr_transpose_w': (_c_int, [_vp] + [_c_int] * 4 + [_vp, _vp]),
     'srf_route_sdr_gx': (_c_int, [_vp, _c_int, _c_int, _vp] + [_c_int] * 10 + [_vp, _vp]),
     'srf_route_sdr_gw': (_c_int, [_vp, _c_int, _c_int, _vp] + [_c_int] * 11 + [_vp, _vp, _vp]),
+    'srf_route_sdr_pose_n': (_c_int, [_ranges] + [_c_int] * 10 + [_vp]),
+    'srf_route_sdr_recur_fwd_n': (_c_int, [_ranges] + [_c_int] * 8 + [_vp]),
+    'srf_route_sdr_recur_bwd_n': (_c_int, [_ranges] + [_c_int] * 8 + [_vp]),
+    'srf_route_sdr_gx_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
+    'srf_route_sdr_gw_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
     'srf_cnnfe_out_dims': (_c_int, [_c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
     'srf_cnnfe_saved_bytes': (_c_size, [_c_int] * 4),
     'srf_cnnfe_fwd_workspace': (_c_size, [_c_int] * 4),

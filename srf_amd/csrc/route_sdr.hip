@@ -61,6 +61,23 @@ struct FrameMap {
   __device__ __forceinline__ size_t view(int b, int t) const { return (size_t)b * vn + (t - v0); }
 };
 
+// One launch of the frame-parallel contractions runs up to srf::kMaxItems frame ranges
+// of same-shaped layers (grid.z = item).  pose: x = emb, w = W, b = bias, o = u;
+// gx: x = gu, w = W^T, o = g_emb; gW: x = gu, b = emb, o = gW, o2 = gbias, acc.
+struct GemmItem {
+  const float* x;
+  const float* w;
+  const float* b;
+  float* o;
+  float* o2;
+  int acc, Q;
+  FrameMap fm;
+};
+struct GemmItems {
+  GemmItem it[srf::kMaxItems];
+  int n;
+};
+
 // KS consecutive floats (float4 loads when KS is a multiple of 4), zeros when !ok
 template <int KS>
 __device__ __forceinline__ void load_ks(const float* __restrict__ p, bool ok, float (&v)[KS]) {
@@ -86,9 +103,15 @@ __device__ __forceinline__ void load_ks(const float* __restrict__ p, bool ok, fl
 // frame tiles.  Operands as in the DR pass (k-permuted MFMA: lane group g holds K
 // elements g*KS .. g*KS + KS-1 of both operands).
 template <int DIN, int FT>
-__global__ __launch_bounds__(256) void sdr_pose_kernel(const float* __restrict__ emb, const float* __restrict__ W,
-                                                       const float* __restrict__ bias, int Q, FrameMap fm, int N,
-                                                       int lpad, int in_n, int JD, float* __restrict__ u) {
+__global__ __launch_bounds__(256) void sdr_pose_kernel(GemmItems items, int N, int lpad, int in_n, int JD) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ emb = G.x;
+  const float* __restrict__ W = G.w;
+  const float* __restrict__ bias = G.b;
+  float* __restrict__ u = G.o;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  if (blockIdx.x * FT * 16 >= Q) return;
   constexpr int KS = DIN / 4;
   const int T = fm.T;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -361,9 +384,14 @@ size_t sdr_bwd_smem(int in_n, int J, int D, int R) {
 // (K = rows, float4 operands), scattered into g_emb through the window adjoint.
 // Frames of the map fm, gu through its view.
 template <int DIN>
-__global__ __launch_bounds__(64) void sdr_gx_kernel(const float* __restrict__ gu, const float* __restrict__ WT,
-                                                    int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
-                                                    float* __restrict__ g_emb) {
+__global__ __launch_bounds__(64) void sdr_gx_kernel(GemmItems items, int N, int lpad, int in_n, int JD) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ gu = G.x;
+  const float* __restrict__ WT = G.w;
+  float* __restrict__ g_emb = G.o;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  if (blockIdx.x * 16 >= Q) return;
   constexpr int NCT = (DIN + 15) / 16;
   const int T = fm.T;
   const int lane = threadIdx.x, fl = lane & 15, g = lane >> 4;
@@ -421,10 +449,15 @@ __global__ void sdr_transpose_w_kernel(const float* __restrict__ W, int in_n, in
 // through the window.  Frames of the map fm (gu through its view); accumulate != 0
 // adds to gW / gbias (a layer's frame ranges in turn, one writer per element).
 template <int DIN>
-__global__ __launch_bounds__(256) void sdr_gw_kernel(const float* __restrict__ gu, const float* __restrict__ emb,
-                                                     int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
-                                                     float* __restrict__ gW, float* __restrict__ gbias,
-                                                     int accumulate) {
+__global__ __launch_bounds__(256) void sdr_gw_kernel(GemmItems items, int N, int lpad, int in_n, int JD) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ gu = G.x;
+  const float* __restrict__ emb = G.b;
+  float* __restrict__ gW = G.o;
+  float* __restrict__ gbias = G.o2;
+  const int accumulate = G.acc;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
   constexpr int NCT = (DIN + 15) / 16;
   const int T = fm.T;
   const int NT = (JD + 15) / 16;
@@ -517,10 +550,15 @@ __device__ __forceinline__ void load_window_x(const float* __restrict__ emb, con
 // wave (wf, wr) = 64 frames x 64 rows = 2 x 2 tiles (A = x: M = frames, B = W^T: N =
 // rows, so a store writes 32 consecutive rows of one frame).  K = din at once.
 template <int DIN>
-__global__ __launch_bounds__(256, 2) void sdr_pose32_kernel(const float* __restrict__ emb, const float* __restrict__ W,
-                                                            const float* __restrict__ bias, int Q, FrameMap fm, int N,
-                                                            int lpad, int in_n, int JD, int nrb,
-                                                            float* __restrict__ u) {
+__global__ __launch_bounds__(256, 2) void sdr_pose32_kernel(GemmItems items, int N, int lpad, int in_n, int JD, int nrb) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ emb = G.x;
+  const float* __restrict__ W = G.w;
+  const float* __restrict__ bias = G.b;
+  float* __restrict__ u = G.o;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  if ((int)(blockIdx.x / nrb) * 128 >= Q) return;
   constexpr int KC = DIN / 8;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -574,9 +612,14 @@ __global__ __launch_bounds__(256, 2) void sdr_pose32_kernel(const float* __restr
 // K = JD in chunks of 64 (A = gu rows along k, B = W^T [i][e][row] along k), the next
 // chunk's operands loaded while the current one's MFMAs run.
 template <int DIN>
-__global__ __launch_bounds__(256, 2) void sdr_gx32_kernel(const float* __restrict__ gu, const float* __restrict__ WT,
-                                                          int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
-                                                          float* __restrict__ g_emb) {
+__global__ __launch_bounds__(256, 2) void sdr_gx32_kernel(GemmItems items, int N, int lpad, int in_n, int JD) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ gu = G.x;
+  const float* __restrict__ WT = G.w;
+  float* __restrict__ g_emb = G.o;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  if (blockIdx.x * 128 >= Q) return;
   constexpr int NE = DIN / 32;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -638,10 +681,15 @@ __global__ __launch_bounds__(256, 2) void sdr_gx32_kernel(const float* __restric
 // Workgroup = one capsule, 128 rows; wave = 32 rows x din; K = frames, two per MFMA
 // (lane half h takes frame 2s + h), 16 frames of loads issued before their MFMAs.
 template <int DIN>
-__global__ __launch_bounds__(256, 2) void sdr_gw32_kernel(const float* __restrict__ gu, const float* __restrict__ emb,
-                                                          int Q, FrameMap fm, int N, int lpad, int in_n, int JD,
-                                                          float* __restrict__ gW, float* __restrict__ gbias,
-                                                          int accumulate) {
+__global__ __launch_bounds__(256, 2) void sdr_gw32_kernel(GemmItems items, int N, int lpad, int in_n, int JD) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ gu = G.x;
+  const float* __restrict__ emb = G.b;
+  float* __restrict__ gW = G.o;
+  float* __restrict__ gbias = G.o2;
+  const int accumulate = G.acc;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
   constexpr int NE = DIN / 32, U = 8;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -722,10 +770,15 @@ __device__ __forceinline__ float amax8(const f4& a, const f4& b) {
 }
 
 template <int DIN>
-__global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(const float* __restrict__ emb, const float* __restrict__ W,
-                                                           const float* __restrict__ bias, int Q, FrameMap fm, int N,
-                                                           int lpad, int in_n, int JD, int nrb,
-                                                           float* __restrict__ u) {
+__global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int N, int lpad, int in_n, int JD, int nrb) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ emb = G.x;
+  const float* __restrict__ W = G.w;
+  const float* __restrict__ bias = G.b;
+  float* __restrict__ u = G.o;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  if ((int)(blockIdx.x / nrb) * 128 >= Q) return;
   constexpr int KS = DIN / 16;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
@@ -854,43 +907,43 @@ size_t gstate_bytes(const SGeom& g, size_t state_bytes) {
 
 FrameMap frame_map(int T, int t0, int t1, int v0, int vn) { return FrameMap{T, t0, t1 - t0, v0, vn}; }
 
-int pose_range(const SGeom& g, const float* emb, const float* W, const float* bias, const FrameMap& fm, float* u,
-               hipStream_t st, bool fp8 = false) {
-  const int Q = g.B * fm.nt;
-  if (Q == 0) return SRF_OK;
+// Launches of the frame-parallel contractions over it.n items (grid.z), each a frame
+// range of a same-shaped layer; items with no frames are dropped by the caller.
+int max_q(const GemmItems& it) {
+  int q = 0;
+  for (int k = 0; k < it.n; ++k) q = std::max(q, it.it[k].Q);
+  return q;
+}
+
+int pose_n(const SGeom& g, const GemmItems& it, hipStream_t st, bool fp8 = false) {
+  const int Q = max_q(it);
+  if (it.n == 0 || Q == 0) return SRF_OK;
+  const int nrb = (g.JD() + 127) / 128;
+  const dim3 grid32(nrb * ((Q + 127) / 128), g.in_n(), it.n);
   if (fp8) {
     if ((g.din != 32 && g.din != 64) || g.JD() % 8) {
       srf::set_error("fp8 pose: in_d must be 32 or 64 (got %d) and J*out_d a multiple of 8", g.din);
       return SRF_EUNSUPPORTED;
     }
-    const int nrb = (g.JD() + 127) / 128;
-    const dim3 grid(nrb * ((Q + 127) / 128), g.in_n());
     if (g.din == 32)
-      hipLaunchKernelGGL(sdr_pose8_kernel<32>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
-                         g.JD(), nrb, u);
+      hipLaunchKernelGGL(sdr_pose8_kernel<32>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
     else
-      hipLaunchKernelGGL(sdr_pose8_kernel<64>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
-                         g.JD(), nrb, u);
+      hipLaunchKernelGGL(sdr_pose8_kernel<64>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
     SRF_LAUNCH_CHECK("sdr_pose8");
     return SRF_OK;
   }
   if (use_mfma32(g.din, g.JD(), SdrGemm::kPose)) {
-    const int nrb = (g.JD() + 127) / 128;
-    const dim3 grid(nrb * ((Q + 127) / 128), g.in_n());
     if (g.din == 32)
-      hipLaunchKernelGGL(sdr_pose32_kernel<32>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
-                         g.JD(), nrb, u);
+      hipLaunchKernelGGL(sdr_pose32_kernel<32>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
     else
-      hipLaunchKernelGGL(sdr_pose32_kernel<64>, grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(),
-                         g.JD(), nrb, u);
+      hipLaunchKernelGGL(sdr_pose32_kernel<64>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
     SRF_LAUNCH_CHECK("sdr_pose32");
     return SRF_OK;
   }
   constexpr int FT = 2;   // frame tiles per workgroup: each W fragment feeds two MFMA chains
-  const dim3 grid((Q + 16 * FT - 1) / (16 * FT), g.in_n());
-#define SRF_POSE(DIN)                                                                                            \
-  hipLaunchKernelGGL((sdr_pose_kernel<DIN, FT>), grid, dim3(256), 0, st, emb, W, bias, Q, fm, g.N, g.lpad, g.in_n(), \
-                     g.JD(), u)
+  const dim3 grid((Q + 16 * FT - 1) / (16 * FT), g.in_n(), it.n);
+#define SRF_POSE(DIN) \
+  hipLaunchKernelGGL((sdr_pose_kernel<DIN, FT>), grid, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD())
   switch (g.din) {
     case 8: SRF_POSE(8); break;
     case 16: SRF_POSE(16); break;
@@ -902,43 +955,62 @@ int pose_range(const SGeom& g, const float* emb, const float* W, const float* bi
   return SRF_OK;
 }
 
-// recurrence over one frame range: the register-resident kernels when the shape fits,
-// else the LDS / global-state ones (gstate: B slices of the state, when it exceeds LDS)
-int recur_fwd(const SGeom& g, const float* u, float* v_out, const srf::SeqRange& rg, float* gstate, float* cs,
-              hipStream_t st) {
-  if (rg.t0 >= rg.t1) return SRF_OK;
+int pose_range(const SGeom& g, const float* emb, const float* W, const float* bias, const FrameMap& fm, float* u,
+               hipStream_t st) {
+  GemmItems it{};
+  it.it[0] = GemmItem{emb, W, bias, u, nullptr, 0, g.B * fm.nt, fm};
+  it.n = 1;
+  return pose_n(g, it, st);
+}
+
+// The recurrence over it.n frame ranges (grid.y): the register-resident kernels when the
+// shape fits, else the streaming ones, else the LDS / global-state ones (one launch per
+// item; gstate: the item's workspace, B slices of the state, when it exceeds LDS).
+int recur_fwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
+  if (it.n == 0) return SRF_OK;
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
-    return srf::sdr_seq_fwd(u, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, v_out, rg, cs, st);
+    return srf::sdr_seq_fwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, st);
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
-    return srf::sdr_stream_fwd(u, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, v_out, rg, cs, st);
+    return srf::sdr_stream_fwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, st);
   const size_t sm = sdr_fwd_smem(g.in_n(), g.J, g.dout);
-  if (sdr_gstate(sm))
-    hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, g.T, g.in_n(), g.J,
-                       g.dout, g.iters, g.mask_first, v_out, gstate, gstate_stride(sm), rg);
-  else
-    hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, false>), dim3(g.B), dim3(kGsThreads), sm, st, u, g.T, g.in_n(), g.J,
-                       g.dout, g.iters, g.mask_first, v_out, (float*)nullptr, (size_t)0, rg);
-  SRF_LAUNCH_CHECK("sdr_fwd");
+  for (int k = 0; k < it.n; ++k) {
+    const srf::SeqItem& I = it.it[k];
+    if (sdr_gstate(sm))
+      hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, I.u, g.T, g.in_n(),
+                         g.J, g.dout, g.iters, g.mask_first, I.v, I.ws, gstate_stride(sm), I.rg);
+    else
+      hipLaunchKernelGGL((sdr_fwd_kernel<kGsThreads, false>), dim3(g.B), dim3(kGsThreads), sm, st, I.u, g.T, g.in_n(),
+                         g.J, g.dout, g.iters, g.mask_first, I.v, (float*)nullptr, (size_t)0, I.rg);
+    SRF_LAUNCH_CHECK("sdr_fwd");
+  }
   return SRF_OK;
 }
 
-int recur_bwd(const SGeom& g, const float* u, const float* v_saved, const float* g_v, float* gu,
-              const srf::SeqRange& rg, float* gstate, const float* cs, hipStream_t st) {
-  if (rg.t0 >= rg.t1) return SRF_OK;
+int recur_bwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
+  if (it.n == 0) return SRF_OK;
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
-    return srf::sdr_seq_bwd(u, v_saved, g_v, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, rg, cs,
-                            st);
+    return srf::sdr_seq_bwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, st);
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
-    return srf::sdr_stream_bwd(u, v_saved, g_v, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, gu, rg, cs, gstate, st);
+    return srf::sdr_stream_bwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, st);
   const size_t sm = sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters);
-  if (sdr_gstate(sm))
-    hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, u, v_saved, g_v, g.T,
-                       g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, gstate, gstate_stride(sm), rg);
-  else
-    hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, false>), dim3(g.B), dim3(kGsThreads), sm, st, u, v_saved, g_v, g.T,
-                       g.in_n(), g.J, g.dout, g.iters, g.mask_first, gu, (float*)nullptr, (size_t)0, rg);
-  SRF_LAUNCH_CHECK("sdr_bwd");
+  for (int k = 0; k < it.n; ++k) {
+    const srf::SeqItem& I = it.it[k];
+    if (sdr_gstate(sm))
+      hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, true>), dim3(g.B), dim3(kGsThreads), 0, st, I.u, I.v, I.g_v, g.T,
+                         g.in_n(), g.J, g.dout, g.iters, g.mask_first, I.gu, I.ws, gstate_stride(sm), I.rg);
+    else
+      hipLaunchKernelGGL((sdr_bwd_kernel<kGsThreads, false>), dim3(g.B), dim3(kGsThreads), sm, st, I.u, I.v, I.g_v,
+                         g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, I.gu, (float*)nullptr, (size_t)0, I.rg);
+    SRF_LAUNCH_CHECK("sdr_bwd");
+  }
   return SRF_OK;
+}
+
+srf::SeqItems one_seq_item(const srf::SeqItem& I) {
+  srf::SeqItems it{};
+  it.it[0] = I;
+  it.n = I.rg.t0 < I.rg.t1 ? 1 : 0;
+  return it;
 }
 
 size_t recur_workspace(const SGeom& g) {
@@ -949,23 +1021,20 @@ size_t recur_workspace(const SGeom& g) {
                   gstate_bytes(g, sdr_bwd_smem(g.in_n(), g.J, g.dout, g.iters)));
 }
 
-int gx_range(const SGeom& g, const float* gu, const float* WT, const FrameMap& fm, float* g_emb, hipStream_t st) {
-  const int Q = g.B * fm.nt;
-  if (Q == 0) return SRF_OK;
+int gx_n(const SGeom& g, const GemmItems& it, hipStream_t st) {
+  const int Q = max_q(it);
+  if (it.n == 0 || Q == 0) return SRF_OK;
   if (use_mfma32(g.din, g.JD(), SdrGemm::kGx)) {
-    const dim3 grid((Q + 127) / 128, g.in_n());
+    const dim3 grid((Q + 127) / 128, g.in_n(), it.n);
     if (g.din == 32)
-      hipLaunchKernelGGL(sdr_gx32_kernel<32>, grid, dim3(256), 0, st, gu, WT, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
-                         g_emb);
+      hipLaunchKernelGGL(sdr_gx32_kernel<32>, grid, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD());
     else
-      hipLaunchKernelGGL(sdr_gx32_kernel<64>, grid, dim3(256), 0, st, gu, WT, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
-                         g_emb);
+      hipLaunchKernelGGL(sdr_gx32_kernel<64>, grid, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD());
     SRF_LAUNCH_CHECK("sdr_gx32");
     return SRF_OK;
   }
-  const dim3 grid((Q + 15) / 16, g.in_n());
-#define SRF_GX(DIN) \
-  hipLaunchKernelGGL(sdr_gx_kernel<DIN>, grid, dim3(64), 0, st, gu, WT, Q, fm, g.N, g.lpad, g.in_n(), g.JD(), g_emb)
+  const dim3 grid((Q + 15) / 16, g.in_n(), it.n);
+#define SRF_GX(DIN) hipLaunchKernelGGL(sdr_gx_kernel<DIN>, grid, dim3(64), 0, st, it, g.N, g.lpad, g.in_n(), g.JD())
   switch (g.din) {
     case 8: SRF_GX(8); break;
     case 16: SRF_GX(16); break;
@@ -977,26 +1046,28 @@ int gx_range(const SGeom& g, const float* gu, const float* WT, const FrameMap& f
   return SRF_OK;
 }
 
-int gw_range(const SGeom& g, const float* gu, const float* emb, const FrameMap& fm, int accumulate, float* g_W,
-             float* g_bias, hipStream_t st) {
-  const int Q = g.B * fm.nt;
-  if (Q == 0 && accumulate) return SRF_OK;
+int gx_range(const SGeom& g, const float* gu, const float* WT, const FrameMap& fm, float* g_emb, hipStream_t st) {
+  GemmItems it{};
+  it.it[0] = GemmItem{gu, WT, nullptr, g_emb, nullptr, 0, g.B * fm.nt, fm};
+  it.n = 1;
+  return gx_n(g, it, st);
+}
+
+// items with Q == 0 still run when they start the accumulation (acc == 0: zeros)
+int gw_n(const SGeom& g, const GemmItems& it, hipStream_t st) {
+  if (it.n == 0) return SRF_OK;
   if (use_mfma32(g.din, g.JD(), SdrGemm::kGw)) {
-    const dim3 grid((g.JD() + 127) / 128, g.in_n());
+    const dim3 grid((g.JD() + 127) / 128, g.in_n(), it.n);
     if (g.din == 32)
-      hipLaunchKernelGGL(sdr_gw32_kernel<32>, grid, dim3(256), 0, st, gu, emb, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
-                         g_W, g_bias, accumulate);
+      hipLaunchKernelGGL(sdr_gw32_kernel<32>, grid, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD());
     else
-      hipLaunchKernelGGL(sdr_gw32_kernel<64>, grid, dim3(256), 0, st, gu, emb, Q, fm, g.N, g.lpad, g.in_n(), g.JD(),
-                         g_W, g_bias, accumulate);
+      hipLaunchKernelGGL(sdr_gw32_kernel<64>, grid, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD());
     SRF_LAUNCH_CHECK("sdr_gw32");
     return SRF_OK;
   }
   const int tasks = g.in_n() * g.NT();
-  const dim3 grid((tasks + 3) / 4);
-#define SRF_GW(DIN)                                                                                             \
-  hipLaunchKernelGGL(sdr_gw_kernel<DIN>, grid, dim3(256), 0, st, gu, emb, Q, fm, g.N, g.lpad, g.in_n(), g.JD(), \
-                     g_W, g_bias, accumulate)
+  const dim3 grid((tasks + 3) / 4, 1, it.n);
+#define SRF_GW(DIN) hipLaunchKernelGGL(sdr_gw_kernel<DIN>, grid, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD())
   switch (g.din) {
     case 8: SRF_GW(8); break;
     case 16: SRF_GW(16); break;
@@ -1006,6 +1077,14 @@ int gw_range(const SGeom& g, const float* gu, const float* emb, const FrameMap& 
 #undef SRF_GW
   SRF_LAUNCH_CHECK("sdr_gw");
   return SRF_OK;
+}
+
+int gw_range(const SGeom& g, const float* gu, const float* emb, const FrameMap& fm, int accumulate, float* g_W,
+             float* g_bias, hipStream_t st) {
+  GemmItems it{};
+  it.it[0] = GemmItem{gu, nullptr, emb, g_W, g_bias, accumulate, g.B * fm.nt, fm};
+  it.n = (fm.nt > 0 || !accumulate) ? 1 : 0;
+  return gw_n(g, it, st);
 }
 
 int transpose_w(const SGeom& g, const float* W, float* WT, float* zero, size_t n_zero, hipStream_t st) {
@@ -1092,7 +1171,9 @@ int srf_route_sdr_fwd(const float* emb, const float* W, const float* bias, int B
   float* u = static_cast<float*>(workspace);
   float* gstate = u + srf::align_up((size_t)g.F() * g.in_n() * g.JD() * sizeof(float), 256) / sizeof(float);
   if ((rc = pose_range(g, emb, W, bias, frame_map(T, 0, T, 0, T), u, st))) return rc;
-  if ((rc = recur_fwd(g, u, v_out, srf::SeqRange::whole(T), gstate, nullptr, st))) return rc;
+  if ((rc = recur_fwd_n(g, one_seq_item(srf::SeqItem{u, v_out, nullptr, nullptr, nullptr, gstate,
+                                                     srf::SeqRange::whole(T)}), st)))
+    return rc;
   SRF_HIP_TRY(hipMemcpyAsync(saved, v_out, (size_t)g.F() * g.JD() * sizeof(float), hipMemcpyDeviceToDevice, st));
   return SRF_OK;
 }
@@ -1113,30 +1194,82 @@ int srf_route_sdr_bwd(const float* emb, const float* W, const float* bias, int B
   hipStream_t st = static_cast<hipStream_t>(stream);
   const FrameMap all = frame_map(T, 0, T, 0, T);
   if ((rc = pose_range(g, emb, W, bias, all, w.u, st))) return rc;
-  if (w.cs && (rc = recur_fwd(g, w.u, w.v, srf::SeqRange::whole(T), w.gstate, w.cs, st))) return rc;
-  if ((rc = recur_bwd(g, w.u, saved, g_v, w.gu, srf::SeqRange::whole(T), w.gstate, w.cs, st))) return rc;
+  if (w.cs && (rc = recur_fwd_n(g, one_seq_item(srf::SeqItem{w.u, w.v, nullptr, nullptr, w.cs, w.gstate,
+                                                               srf::SeqRange::whole(T)}), st)))
+    return rc;
+  if ((rc = recur_bwd_n(g, one_seq_item(srf::SeqItem{w.u, const_cast<float*>(saved), g_v, w.gu, w.cs, w.gstate,
+                                                     srf::SeqRange::whole(T)}), st)))
+    return rc;
   if ((rc = transpose_w(g, W, w.WT, g_emb, (size_t)g.F() * N * din, st))) return rc;
   if ((rc = gx_range(g, w.gu, w.WT, all, g_emb, st))) return rc;
   return gw_range(g, w.gu, emb, all, 0, g_W, g_bias, st);
 }
 
-// ---- the same layer in frame ranges (the layer-pipelined SDR stack)
-int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
-                       int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream) {
+// ---- the same layer in frame ranges (the layer-pipelined SDR stack); the _n forms run
+// up to SRF_SDR_MAX_ITEMS ranges of same-shaped layers in one launch
+}  // extern "C"
+
+namespace {
+
+int items_ok(const SGeom& g, const srf_sdr_range* r, int n, bool use_u, bool use_g) {
+  SRF_REQUIRE(r && n >= 0 && n <= SRF_SDR_MAX_ITEMS, "between 0 and %d ranges per launch, got %d", SRF_SDR_MAX_ITEMS,
+              n);
+  int rc;
+  for (int k = 0; k < n; ++k) {
+    if (use_u && (rc = range_ok(g, r[k].t0, r[k].t1, r[k].v0, r[k].vn))) return rc;
+    if (use_g && (rc = range_ok(g, r[k].t0, r[k].t1, r[k].g0, r[k].gn))) return rc;
+  }
+  return SRF_OK;
+}
+
+srf::SeqItems seq_items(const srf_sdr_range* r, int n, int T, bool bwd, bool keep_cs) {
+  srf::SeqItems it{};
+  for (int k = 0; k < n; ++k) {
+    if (r[k].t0 >= r[k].t1) continue;
+    srf::SeqItem& I = it.it[it.n++];
+    I.u = r[k].u;
+    I.v = r[k].v;
+    I.g_v = r[k].g_v;
+    I.gu = r[k].gu;
+    I.cs = keep_cs ? r[k].couplings : nullptr;
+    I.ws = static_cast<float*>(r[k].workspace);
+    I.rg = bwd ? srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, r[k].g0, r[k].gn, r[k].carry}
+               : srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, 0, T, nullptr};
+  }
+  return it;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srf_route_sdr_pose_n(const srf_sdr_range* r, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                         int dout, int fp8, void* stream) {
   SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
   int rc = check_sgeom(g);
-  if (rc || (rc = range_ok(g, t0, t1, v0, vn))) return rc;
-  SRF_REQUIRE(emb && W && bias && u, "null pointer argument");
-  return pose_range(g, emb, W, bias, frame_map(T, t0, t1, v0, vn), u, static_cast<hipStream_t>(stream));
+  if (rc || (rc = items_ok(g, r, n, true, false))) return rc;
+  GemmItems it{};
+  for (int k = 0; k < n; ++k) {
+    if (r[k].t0 >= r[k].t1) continue;
+    SRF_REQUIRE(r[k].emb && r[k].W && r[k].bias && r[k].u, "null pointer argument");
+    it.it[it.n++] = GemmItem{r[k].emb, r[k].W, r[k].bias, r[k].u, nullptr, 0, B * (r[k].t1 - r[k].t0),
+                             frame_map(T, r[k].t0, r[k].t1, r[k].v0, r[k].vn)};
+  }
+  return pose_n(g, it, static_cast<hipStream_t>(stream), fp8 != 0);
+}
+
+int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
+                       int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream) {
+  srf_sdr_range r{};
+  r.t0 = t0, r.t1 = t1, r.emb = emb, r.W = W, r.bias = bias, r.u = u, r.v0 = v0, r.vn = vn;
+  return srf_route_sdr_pose_n(&r, 1, B, T, N, din, lpad, rpad, J, dout, 0, stream);
 }
 
 int srf_route_sdr_pose_fp8(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                            int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream) {
-  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
-  int rc = check_sgeom(g);
-  if (rc || (rc = range_ok(g, t0, t1, v0, vn))) return rc;
-  SRF_REQUIRE(emb && W && bias && u, "null pointer argument");
-  return pose_range(g, emb, W, bias, frame_map(T, t0, t1, v0, vn), u, static_cast<hipStream_t>(stream), true);
+  srf_sdr_range r{};
+  r.t0 = t0, r.t1 = t1, r.emb = emb, r.W = W, r.bias = bias, r.u = u, r.v0 = v0, r.vn = vn;
+  return srf_route_sdr_pose_n(&r, 1, B, T, N, din, lpad, rpad, J, dout, 1, stream);
 }
 
 size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters) {
@@ -1153,33 +1286,52 @@ int srf_route_sdr_couplings_required(int in_n, int J, int dout, int iters) {
   return !srf::sdr_seq_supported(in_n, J, dout, iters) && srf::sdr_stream_supported(in_n, J, dout, iters);
 }
 
+int srf_route_sdr_recur_fwd_n(const srf_sdr_range* r, int n, int B, int T, int in_n, int J, int dout, int iters,
+                              int mask_first, void* stream) {
+  SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};   // N = in_n, window 1: in_n() = in_n
+  int rc = check_sgeom(g);
+  if (rc || (rc = items_ok(g, r, n, true, false))) return rc;
+  const size_t ws = recur_workspace(g);
+  for (int k = 0; k < n; ++k) {
+    SRF_REQUIRE(r[k].u && r[k].v, "null pointer argument");
+    SRF_REQUIRE(r[k].workspace_bytes >= ws && (r[k].workspace || !ws), "SDR recurrence workspace too small");
+  }
+  return recur_fwd_n(g, seq_items(r, n, T, false, srf_route_sdr_coupling_floats(in_n, J, dout, iters) != 0),
+                     static_cast<hipStream_t>(stream));
+}
+
 int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
                             int mask_first, int t0, int t1, float* v_out, float* couplings, void* workspace,
                             size_t workspace_bytes, void* stream) {
-  SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};   // N = in_n, window 1: in_n() = in_n
+  srf_sdr_range r{};
+  r.t0 = t0, r.t1 = t1, r.u = const_cast<float*>(u), r.v0 = v0, r.vn = vn, r.v = v_out, r.couplings = couplings;
+  r.workspace = workspace, r.workspace_bytes = workspace_bytes;
+  return srf_route_sdr_recur_fwd_n(&r, 1, B, T, in_n, J, dout, iters, mask_first, stream);
+}
+
+int srf_route_sdr_recur_bwd_n(const srf_sdr_range* r, int n, int B, int T, int in_n, int J, int dout, int iters,
+                              int mask_first, void* stream) {
+  SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};
   int rc = check_sgeom(g);
-  if (rc || (rc = range_ok(g, t0, t1, v0, vn))) return rc;
-  SRF_REQUIRE(u && v_out, "null pointer argument");
-  SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
-              "SDR recurrence workspace too small");
-  if (!srf_route_sdr_coupling_floats(in_n, J, dout, iters)) couplings = nullptr;
-  return recur_fwd(g, u, v_out, srf::SeqRange{t0, t1, v0, vn, 0, T, nullptr}, static_cast<float*>(workspace),
-                   couplings, static_cast<hipStream_t>(stream));
+  if (rc || (rc = items_ok(g, r, n, true, true))) return rc;
+  const size_t ws = recur_workspace(g);
+  for (int k = 0; k < n; ++k) {
+    SRF_REQUIRE(r[k].u && r[k].v && r[k].g_v && r[k].carry && r[k].gu, "null pointer argument");
+    SRF_REQUIRE(r[k].workspace_bytes >= ws && (r[k].workspace || !ws), "SDR recurrence workspace too small");
+  }
+  return recur_bwd_n(g, seq_items(r, n, T, true, srf_route_sdr_coupling_floats(in_n, J, dout, iters) != 0),
+                     static_cast<hipStream_t>(stream));
 }
 
 int srf_route_sdr_recur_bwd(const float* u, int v0, int vn, const float* v_saved, const float* couplings,
                             const float* g_v, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
                             int t0, int t1, float* carry, float* gu, int g0, int gn, void* workspace,
                             size_t workspace_bytes, void* stream) {
-  SGeom g{B, T, in_n, 8, 0, 0, J, dout, iters, mask_first ? 1 : 0};
-  int rc = check_sgeom(g);
-  if (rc || (rc = range_ok(g, t0, t1, v0, vn)) || (rc = range_ok(g, t0, t1, g0, gn))) return rc;
-  SRF_REQUIRE(u && v_saved && g_v && carry && gu, "null pointer argument");
-  SRF_REQUIRE(workspace_bytes >= recur_workspace(g) && (workspace || !recur_workspace(g)),
-              "SDR recurrence workspace too small");
-  if (!srf_route_sdr_coupling_floats(in_n, J, dout, iters)) couplings = nullptr;
-  return recur_bwd(g, u, v_saved, g_v, gu, srf::SeqRange{t0, t1, v0, vn, g0, gn, carry},
-                   static_cast<float*>(workspace), couplings, static_cast<hipStream_t>(stream));
+  srf_sdr_range r{};
+  r.t0 = t0, r.t1 = t1, r.u = const_cast<float*>(u), r.v0 = v0, r.vn = vn, r.v = const_cast<float*>(v_saved);
+  r.couplings = const_cast<float*>(couplings), r.g_v = g_v, r.carry = carry, r.gu = gu, r.g0 = g0, r.gn = gn;
+  r.workspace = workspace, r.workspace_bytes = workspace_bytes;
+  return srf_route_sdr_recur_bwd_n(&r, 1, B, T, in_n, J, dout, iters, mask_first, stream);
 }
 
 int srf_route_sdr_transpose_w(const float* W, int in_n, int J, int dout, int din, float* WT, void* stream) {
@@ -1188,24 +1340,50 @@ int srf_route_sdr_transpose_w(const float* W, int in_n, int J, int dout, int din
   return transpose_w(g, W, WT, nullptr, 0, static_cast<hipStream_t>(stream));
 }
 
-int srf_route_sdr_gx(const float* gu, int g0, int gn, const float* WT, int B, int T, int N, int din, int lpad,
-                     int rpad, int J, int dout, int t0, int t1, float* g_emb, void* stream) {
+int srf_route_sdr_gx_n(const srf_sdr_range* r, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                       int dout, void* stream) {
   SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
   int rc = check_sgeom(g);
-  if (rc || (rc = range_ok(g, t0, t1, g0, gn))) return rc;
-  SRF_REQUIRE(gu && WT && g_emb, "null pointer argument");
-  return gx_range(g, gu, WT, frame_map(T, t0, t1, g0, gn), g_emb, static_cast<hipStream_t>(stream));
+  if (rc || (rc = items_ok(g, r, n, false, true))) return rc;
+  GemmItems it{};
+  for (int k = 0; k < n; ++k) {
+    if (r[k].t0 >= r[k].t1) continue;
+    SRF_REQUIRE(r[k].gu && r[k].WT && r[k].g_emb, "null pointer argument");
+    it.it[it.n++] = GemmItem{r[k].gu, r[k].WT, nullptr, r[k].g_emb, nullptr, 0, B * (r[k].t1 - r[k].t0),
+                             frame_map(T, r[k].t0, r[k].t1, r[k].g0, r[k].gn)};
+  }
+  return gx_n(g, it, static_cast<hipStream_t>(stream));
+}
+
+int srf_route_sdr_gx(const float* gu, int g0, int gn, const float* WT, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int t0, int t1, float* g_emb, void* stream) {
+  srf_sdr_range r{};
+  r.t0 = t0, r.t1 = t1, r.gu = const_cast<float*>(gu), r.g0 = g0, r.gn = gn, r.WT = WT, r.g_emb = g_emb;
+  return srf_route_sdr_gx_n(&r, 1, B, T, N, din, lpad, rpad, J, dout, stream);
+}
+
+int srf_route_sdr_gw_n(const srf_sdr_range* r, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                       int dout, void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = items_ok(g, r, n, false, true))) return rc;
+  GemmItems it{};
+  for (int k = 0; k < n; ++k) {
+    if (r[k].t0 >= r[k].t1 && r[k].accumulate) continue;   // an empty range still starts the sum
+    SRF_REQUIRE(r[k].gu && r[k].emb && r[k].g_W && r[k].g_bias, "null pointer argument");
+    it.it[it.n++] = GemmItem{r[k].gu, nullptr, r[k].emb, r[k].g_W, r[k].g_bias, r[k].accumulate,
+                             B * (r[k].t1 - r[k].t0), frame_map(T, r[k].t0, r[k].t1, r[k].g0, r[k].gn)};
+  }
+  return gw_n(g, it, static_cast<hipStream_t>(stream));
 }
 
 int srf_route_sdr_gw(const float* gu, int g0, int gn, const float* emb, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int t0, int t1, int accumulate, float* g_W, float* g_bias,
                      void* stream) {
-  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
-  int rc = check_sgeom(g);
-  if (rc || (rc = range_ok(g, t0, t1, g0, gn))) return rc;
-  SRF_REQUIRE(gu && emb && g_W && g_bias, "null pointer argument");
-  return gw_range(g, gu, emb, frame_map(T, t0, t1, g0, gn), accumulate, g_W, g_bias,
-                  static_cast<hipStream_t>(stream));
+  srf_sdr_range r{};
+  r.t0 = t0, r.t1 = t1, r.gu = const_cast<float*>(gu), r.g0 = g0, r.gn = gn, r.emb = emb, r.g_W = g_W;
+  r.g_bias = g_bias, r.accumulate = accumulate;
+  return srf_route_sdr_gw_n(&r, 1, B, T, N, din, lpad, rpad, J, dout, stream);
 }
 
 }  // extern "C"

@@ -22,6 +22,27 @@ struct SeqRange {
   static SeqRange whole(int T) { return SeqRange{0, T, 0, T, 0, T, nullptr}; }
 };
 
+// One recurrence launch runs up to kMaxItems frame ranges of layers with the same
+// shape at once (grid.y = item): the layer-pipelined stack batches the ranges of one
+// anti-diagonal of its wavefront into one launch instead of one stream per layer.
+//   u: pose output view of the range; v: v_out (forward) / v_saved (backward);
+//   g_v, gu: backward; cs: the range's layer couplings ([B][T][cs floats]);
+//   ws: the stream backward's scratch (sdr_stream_workspace_floats).
+constexpr int kMaxItems = 8;
+struct SeqItem {
+  const float* u;
+  float* v;
+  const float* g_v;
+  float* gu;
+  float* cs;
+  float* ws;
+  SeqRange rg;
+};
+struct SeqItems {
+  SeqItem it[kMaxItems];
+  int n;
+};
+
 // True when sdr_seq_fwd/bwd handle (in_n, J, dout, iters): dout in {8,16,32},
 // J <= 64 (padded to a power of two JP, dout*JP <= 1024), in_n within the
 // per-lane register budget.  Disabled by SRF_SDR_SEQ=0 (A/B runs, legacy tests).
@@ -32,13 +53,13 @@ bool sdr_seq_supported(int in_n, int J, int dout, int iters);
 // c^r [iters][in_n][JP] and pre-squash s^r [iters][J*dout]; a backward given them
 // skips recomputing the iterations.
 size_t sdr_seq_cs_floats(int in_n, int J, int dout, int iters);
-int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                const SeqRange& rg, float* cs, hipStream_t st);
+int sdr_seq_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                hipStream_t st);
 
 // Reverse-time pass: recomputes each frame's iterations from v_saved (the
 // forward's v_out), writes gu [B*T][in_n][J*dout] = dL/du.
-int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                int iters, int mask_first, float* gu, const SeqRange& rg, const float* cs, hipStream_t st);
+int sdr_seq_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                hipStream_t st);
 
 // Template choice for a shape: per-lane input-capsule count NIM in {2, 5, 10} and
 // the iteration bound RM of the backward in {3, 5}.  False when unsupported.
@@ -53,9 +74,8 @@ bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm);
 bool sdr_stream_supported(int in_n, int J, int dout, int iters);
 size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters);
 size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters);
-int sdr_stream_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                   const SeqRange& rg, float* cs, hipStream_t st);
-int sdr_stream_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                   int iters, float* gu, const SeqRange& rg, const float* cs, float* gls, hipStream_t st);
+int sdr_stream_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                   hipStream_t st);
+int sdr_stream_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, hipStream_t st);
 
 }  // namespace srf

@@ -43,10 +43,14 @@ constexpr unsigned long long* g_stamps = nullptr;
 // LDS: w [JD] (agreement input of the iteration: v_{t-1} at r = 0, then v^{r-1}),
 // part [16][JD].
 template <int D, int JP, int NIM>
-__global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(const float* __restrict__ u, int T, int in_n, int J,
-                                                               int iters, int mask_first, float* __restrict__ v_out,
-                                                               srf::SeqRange rg, float* __restrict__ cs) {
+__global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems items, int T, int in_n, int J,
+                                                               int iters, int mask_first) {
   using C = Cfg<D, JP, NIM>;
+  const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
+  const float* __restrict__ u = I.u;
+  float* __restrict__ v_out = I.v;
+  float* __restrict__ cs = I.cs;
+  const srf::SeqRange rg = I.rg;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = J * D;
   float* wl = lds;
@@ -105,24 +109,24 @@ size_t fwd_lds(int J, int D) {
 }
 
 template <int D, int JP, int NIM>
-int launch_fwd(const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
-               const srf::SeqRange& rg, float* cs, hipStream_t st) {
+int launch_fwd(const srf::SeqItems& items, int B, int T, int in_n, int J, int iters, int mask_first,
+               hipStream_t st) {
   const size_t lds = fwd_lds(J, D);
   auto k = sdr_seq_fwd_kernel<D, JP, NIM>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, T, in_n, J, iters, mask_first, v_out, rg, cs);
+  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kThreads), lds, st, items, T, in_n, J, iters, mask_first);
   SRF_LAUNCH_CHECK("sdr_seq_fwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
-int fwd_nim(int nim, const float* u, int B, int T, int in_n, int J, int iters, int mask_first, float* v_out,
-            const srf::SeqRange& rg, float* cs, hipStream_t st) {
-  if (nim == 2) return launch_fwd<D, JP, 2>(u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
-  if (nim == 5) return launch_fwd<D, JP, 5>(u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
+int fwd_nim(int nim, const srf::SeqItems& items, int B, int T, int in_n, int J, int iters, int mask_first,
+            hipStream_t st) {
+  if (nim == 2) return launch_fwd<D, JP, 2>(items, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 5) return launch_fwd<D, JP, 5>(items, B, T, in_n, J, iters, mask_first, st);
   if constexpr (seq_kd(D, JP) <= 8)
-    return launch_fwd<D, JP, 10>(u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
+    return launch_fwd<D, JP, 10>(items, B, T, in_n, J, iters, mask_first, st);
   srf::set_error("sdr_seq: no forward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -140,6 +144,9 @@ namespace srf {
 bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm) {
   const char* e = getenv("SRF_SDR_SEQ");
   if (e && e[0] == '0') return false;
+  // A/B hook: layers with J*dout above this run on the streaming kernels instead
+  const char* mj = getenv("SRF_SDR_SEQ_MAXJD");
+  if (mj && mj[0] && J * dout > atoi(mj)) return false;
   if (J < 2 || J > 64 || iters < 1 || iters > 5 || in_n < 1) return false;
   if (dout != 8 && dout != 16 && dout != 32) return false;
   const int JP = srf_seq::pow2_at_least(J);
@@ -165,8 +172,8 @@ size_t sdr_seq_cs_floats(int in_n, int J, int dout, int iters) {
   return (size_t)iters * ((size_t)in_n * srf_seq::pow2_at_least(J) + (size_t)J * dout);
 }
 
-int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                const SeqRange& rg, float* cs, hipStream_t st) {
+int sdr_seq_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                hipStream_t st) {
   int nim = 0, rm = 0;
   if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
@@ -174,7 +181,7 @@ int sdr_seq_fwd(const float* u, int B, int T, int in_n, int J, int dout, int ite
   }
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_F(DD, PP) \
-  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, u, B, T, in_n, J, iters, mask_first, v_out, rg, cs, st);
+  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, items, B, T, in_n, J, iters, mask_first, st);
   SRF_SEQ_CASES(SRF_SEQ_F)
 #undef SRF_SEQ_F
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

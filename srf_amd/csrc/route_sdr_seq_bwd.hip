@@ -43,12 +43,16 @@ constexpr bool cl_wanted(int nim, int kd) { return nim * kd >= 40; }
 // accumulates GR rows at a time per LDS read of gs^r / Vc^r: the J = 32 last layer
 // otherwise needs more than the 128 registers a 1024-thread workgroup allows.
 template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, int GR = NIM>
-__global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(const float* __restrict__ u,
-                                                               const float* __restrict__ v_saved,
-                                                               const float* __restrict__ g_v, int T, int in_n, int J,
-                                                               int iters, int mask_first, float* __restrict__ gu,
-                                                               srf::SeqRange rg, const float* __restrict__ cs) {
+__global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems items, int T, int in_n, int J,
+                                                               int iters, int mask_first) {
   using C = Cfg<D, JP, NIM>;
+  const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
+  const float* __restrict__ u = I.u;
+  const float* __restrict__ v_saved = I.v;
+  const float* __restrict__ g_v = I.g_v;
+  float* __restrict__ gu = I.gu;
+  const float* __restrict__ cs = I.cs;
+  const srf::SeqRange rg = I.rg;
   constexpr int RR = CL ? 1 : RM;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = J * D;
@@ -353,8 +357,8 @@ size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
 }
 
 template <int D, int JP, int NIM, int RM>
-int launch_bwd(const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J, int iters,
-               int mask_first, float* gu, const srf::SeqRange& rg, const float* cs, hipStream_t st) {
+int launch_bwd(const srf::SeqItems& items, bool cs, int B, int T, int in_n, int J, int iters, int mask_first,
+               hipStream_t st) {
   constexpr bool want = cl_wanted(NIM, seq_kd(D, JP));
   const bool cl = want && bwd_lds(J, D, RM, in_n, true) <= 160 * 1024;
   const size_t lds = bwd_lds(J, D, RM, in_n, cl);
@@ -369,19 +373,19 @@ int launch_bwd(const float* u, const float* vs, const float* gv, int B, int T, i
                     : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, false>);
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kThreads), lds, st, u, vs, gv, T, in_n, J, iters, mask_first, gu, rg, cs);
+  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kThreads), lds, st, items, T, in_n, J, iters, mask_first);
   SRF_LAUNCH_CHECK("sdr_seq_bwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
-int bwd_nim(int nim, int rm, const float* u, const float* vs, const float* gv, int B, int T, int in_n, int J,
-            int iters, int mask_first, float* gu, const srf::SeqRange& rg, const float* cs, hipStream_t st) {
-  if (rm == 5) return launch_bwd<D, JP, 2, 5>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
-  if (nim == 2) return launch_bwd<D, JP, 2, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
-  if (nim == 5) return launch_bwd<D, JP, 5, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
+int bwd_nim(int nim, int rm, const srf::SeqItems& items, bool cs, int B, int T, int in_n, int J, int iters,
+            int mask_first, hipStream_t st) {
+  if (rm == 5) return launch_bwd<D, JP, 2, 5>(items, cs, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 2) return launch_bwd<D, JP, 2, 3>(items, cs, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 5) return launch_bwd<D, JP, 5, 3>(items, cs, B, T, in_n, J, iters, mask_first, st);
   if constexpr (seq_kd(D, JP) <= 8)
-    return launch_bwd<D, JP, 10, 3>(u, vs, gv, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
+    return launch_bwd<D, JP, 10, 3>(items, cs, B, T, in_n, J, iters, mask_first, st);
   srf::set_error("sdr_seq: no backward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -396,8 +400,12 @@ extern "C" int srf_seq_bwd_stamp_buffer(void* p) {
 
 namespace srf {
 
-int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                int iters, int mask_first, float* gu, const SeqRange& rg, const float* cs, hipStream_t st) {
+int sdr_seq_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                hipStream_t st) {
+  // the items of one launch share the kernel: all with stored couplings or none
+  const bool cs = items.n > 0 && items.it[0].cs != nullptr;
+  for (int k = 1; k < items.n; ++k)
+    SRF_REQUIRE((items.it[k].cs != nullptr) == cs, "sdr_seq: launch items mix stored and recomputed couplings");
   int nim = 0, rm = 0;
   if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
@@ -406,7 +414,7 @@ int sdr_seq_bwd(const float* u, const float* v_saved, const float* g_v, int B, i
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_B(DD, PP)     \
   if (dout == DD && JP == PP) \
-    return bwd_nim<DD, PP>(nim, rm, u, v_saved, g_v, B, T, in_n, J, iters, mask_first, gu, rg, cs, st);
+    return bwd_nim<DD, PP>(nim, rm, items, cs, B, T, in_n, J, iters, mask_first, st);
   SRF_SEQ_CASES(SRF_SEQ_B)
 #undef SRF_SEQ_B
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

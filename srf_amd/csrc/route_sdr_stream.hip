@@ -128,10 +128,14 @@ __device__ __forceinline__ float dsquash(float s, float a) {
 // ------------------------------------------------------------------ forward
 // LDS: wl [JD] (Vc of the iteration), part [kNW][JD].
 template <int D, int KD>
-__global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(const float* __restrict__ u, int T, int in_n,
-                                                             int iters, int mask_first, float* __restrict__ v_out,
-                                                             srf::SeqRange rg, float* __restrict__ cs, int NMp) {
+__global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items, int T, int in_n, int iters,
+                                                             int mask_first, int NMp) {
   using C = SC<D, KD>;
+  const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
+  const float* __restrict__ u = I.u;
+  float* __restrict__ v_out = I.v;
+  float* __restrict__ cs = I.cs;
+  const srf::SeqRange rg = I.rg;
   constexpr int JD = C::JD, J = C::J, PD = C::PDF, NE = C::NE;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* wl = lds;
@@ -220,13 +224,17 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(const float* __rest
 // LDS: part [kNW][JD], gsl [kRM][JD] (gs^r), vcl [kRM][JD] (Vc^r).
 // gls: per-utterance scratch gL^r [R][in_n][J].
 template <int D, int KD>
-__global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(const float* __restrict__ u,
-                                                             const float* __restrict__ v_saved,
-                                                             const float* __restrict__ g_v, int T, int in_n,
-                                                             int iters, float* __restrict__ gu, srf::SeqRange rg,
-                                                             const float* __restrict__ cs, float* __restrict__ gls,
+__global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items, int T, int in_n, int iters,
                                                              int NMp) {
   using C = SC<D, KD>;
+  const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
+  const float* __restrict__ u = I.u;
+  const float* __restrict__ v_saved = I.v;
+  const float* __restrict__ g_v = I.g_v;
+  float* __restrict__ gu = I.gu;
+  const float* __restrict__ cs = I.cs;
+  float* __restrict__ gls = I.ws;
+  const srf::SeqRange rg = I.rg;
   constexpr int JD = C::JD, J = C::J, PD = C::PDB, NE = C::NE, HD = C::HD;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* part = lds;
@@ -398,29 +406,26 @@ size_t fwd_lds(int JD) { return (size_t)(1 + kNW) * JD * sizeof(float); }
 size_t bwd_lds(int JD) { return (size_t)(kNW + 2 * kRM) * JD * sizeof(float); }
 
 template <int D, int KD>
-int launch_fwd(const float* u, int B, int T, int in_n, int iters, int mask_first, float* v_out,
-               const srf::SeqRange& rg, float* cs, hipStream_t st) {
+int launch_fwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, int mask_first, hipStream_t st) {
   using C = SC<D, KD>;
   const size_t lds = fwd_lds(C::JD);
   auto k = sdr_stream_fwd_kernel<D, KD>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kNT), lds, st, u, T, in_n, iters, mask_first, v_out, rg, cs,
+  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kNT), lds, st, items, T, in_n, iters, mask_first,
                      nm_padded(in_n, C::PDF));
   SRF_LAUNCH_CHECK("sdr_stream_fwd");
   return SRF_OK;
 }
 
 template <int D, int KD>
-int launch_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int iters, float* gu,
-               const srf::SeqRange& rg, const float* cs, float* gls, hipStream_t st) {
+int launch_bwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, hipStream_t st) {
   using C = SC<D, KD>;
   const size_t lds = bwd_lds(C::JD);
   auto k = sdr_stream_bwd_kernel<D, KD>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(kNT), lds, st, u, v_saved, g_v, T, in_n, iters, gu, rg, cs, gls,
-                     nm_padded(in_n, C::PDB));
+  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kNT), lds, st, items, T, in_n, iters, nm_padded(in_n, C::PDB));
   SRF_LAUNCH_CHECK("sdr_stream_bwd");
   return SRF_OK;
 }
@@ -454,27 +459,26 @@ size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters) 
   return sdr_stream_supported(in_n, J, dout, iters) ? (size_t)B * iters * in_n * J : 0;
 }
 
-int sdr_stream_fwd(const float* u, int B, int T, int in_n, int J, int dout, int iters, int mask_first, float* v_out,
-                   const SeqRange& rg, float* cs, hipStream_t st) {
+int sdr_stream_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
+                   hipStream_t st) {
   const int KD = J * dout / 64;
 #define SRF_STREAM_F(DD, KK) \
-  if (dout == DD && KD == KK) return launch_fwd<DD, KK>(u, B, T, in_n, iters, mask_first, v_out, rg, cs, st);
+  if (dout == DD && KD == KK) return launch_fwd<DD, KK>(items, B, T, in_n, iters, mask_first, st);
   SRF_STREAM_CASES(SRF_STREAM_F)
 #undef SRF_STREAM_F
   srf::set_error("sdr_stream: unsupported shape J=%d dout=%d", J, dout);
   return SRF_EUNSUPPORTED;
 }
 
-int sdr_stream_bwd(const float* u, const float* v_saved, const float* g_v, int B, int T, int in_n, int J, int dout,
-                   int iters, float* gu, const SeqRange& rg, const float* cs, float* gls, hipStream_t st) {
-  if (!cs || !gls) {
-    srf::set_error("sdr_stream backward needs the forward's stored couplings and its scratch workspace");
-    return SRF_EINVAL;
-  }
+int sdr_stream_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, hipStream_t st) {
+  for (int k = 0; k < items.n; ++k)
+    if (!items.it[k].cs || !items.it[k].ws) {
+      srf::set_error("sdr_stream backward needs the forward's stored couplings and its scratch workspace");
+      return SRF_EINVAL;
+    }
   const int KD = J * dout / 64;
-#define SRF_STREAM_B(DD, KK)                                                                                 \
-  if (dout == DD && KD == KK) return launch_bwd<DD, KK>(u, v_saved, g_v, B, T, in_n, iters, gu, rg, cs, gls, \
-                                                        st);
+#define SRF_STREAM_B(DD, KK) \
+  if (dout == DD && KD == KK) return launch_bwd<DD, KK>(items, B, T, in_n, iters, st);
   SRF_STREAM_CASES(SRF_STREAM_B)
 #undef SRF_STREAM_B
   srf::set_error("sdr_stream: unsupported shape J=%d dout=%d", J, dout);

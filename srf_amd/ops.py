@@ -497,13 +497,14 @@ class SdrStackPlan:
     def in_n(self, l):
         return self.layers[l][0] * self.win
 
-    def events(self, which):
-        """[L][K] events of the forward or backward wavefront, created once and kept
-        with the plan: a captured step (hipGraph) must not see its events destroyed
-        before the capture ends."""
+    def events(self, which, n=None):
+        """Events of the forward or backward wavefront ([L][K], or n of them), created
+        once and kept with the plan: a captured step (hipGraph) must not see its
+        events destroyed before the capture ends."""
         ev = getattr(self, '_ev_' + which, None)
         if ev is None:
-            ev = [[torch.cuda.Event() for _ in range(self.K)] for _ in range(self.L)]
+            ev = ([[torch.cuda.Event() for _ in range(self.K)] for _ in range(self.L)] if n is None
+                  else [torch.cuda.Event() for _ in range(n)])
             setattr(self, '_ev_' + which, ev)
         return ev
 
@@ -547,7 +548,229 @@ def _whole_gu(plan):
     return sum(plan.u_floats(l, plan.T) for l in range(plan.L)) * 4 <= budget
 
 
+def _sdr_r(**kw):
+    r = _lib.SdrRange()
+    for k, v in kw.items():
+        setattr(r, k, v)
+    return r
+
+
+def _sdr_call(fn, ranges, *args, what):
+    """fn(ranges, n, *args) for up to SDR_MAX_ITEMS ranges per launch."""
+    for c in range(0, len(ranges), _lib.SDR_MAX_ITEMS):
+        part = ranges[c:c + _lib.SDR_MAX_ITEMS]
+        arr = (_lib.SdrRange * len(part))(*part)
+        _lib.check(fn(arr, len(part), *args), what)
+
+
 class SdrStack(torch.autograd.Function):
+    """emb0 [B,T,N0,din0] -> v of the last layer [B,T,J,D]; in between, layer l's v
+    goes through drop(LN_mid{l+1}(v)) (the CapsNorm of naive:187-191) into layer
+    l+1.  params: W_l, b_l for every layer, then gamma_l, beta_l for l < L-1.
+
+    Schedule (SdrStackPlan's wavefront): the ranges (l, k) of the inner layers
+    l < L-1 on one anti-diagonal d = l + k are independent, so each diagonal is ONE
+    batched launch per kernel (pose, recurrence, gx, gW over srf_sdr_range items, the
+    layers in grid.y / grid.z) on one stream A, in diagonal order; the last layer
+    (J = 32 for C3/C5, its own kernels and the critical chain of the backward) runs
+    range by range on a second stream B, synchronised with A by one event per
+    diagonal / range.  Two streams, so no range ever waits behind another stream's
+    blocked packet in a shared in-order hardware queue."""
+
+    @staticmethod
+    def forward(ctx, emb0, plan, training, p_mid, seed, *params):
+        L_ = _lib.lib()
+        P, B, T, L = plan, plan.B, plan.T, plan.L
+        dev = emb0.device
+        Ws, bs = params[0:2 * L:2], params[1:2 * L:2]
+        gammas, betas = params[2 * L::2], params[2 * L + 1::2]
+        _check_dev('emb0', emb0, (B, T, P.layers[0][0], P.layers[0][1]))
+        need_bwd = P.need_bwd
+        store = need_bwd and _store_u(P, dev)
+        tr = int(bool(training))
+        embs, vs, stats, us, rws, css = [emb0], [], [], [], [], []
+        for l, (N, din, J, D, mf) in enumerate(P.layers):
+            vs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
+            # each frame's couplings and s^r, for a backward without the recompute
+            # (SRF_SDR_CS=0: recompute them, where the shape's kernels can)
+            ncs = L_.srf_route_sdr_coupling_floats(P.in_n(l), J, D, P.iters) \
+                if need_bwd and (os.environ.get('SRF_SDR_CS', '1') != '0'
+                                 or L_.srf_route_sdr_couplings_required(P.in_n(l), J, D, P.iters)) else 0
+            css.append(torch.empty(B * T * ncs, device=dev, dtype=torch.float32) if ncs else None)
+            if l < L - 1:
+                embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
+                stats.append(torch.empty((B * T, 4), device=dev, dtype=torch.float32))
+            us.append(torch.empty(P.u_floats(l, T if store else P.nmax), device=dev, dtype=torch.float32))
+            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
+        main = torch.cuda.current_stream(dev)
+        sa, sb = _layer_streams(dev, 2, 'fwd')
+        ev_a = P.events('fwd_a', P.K + L)
+        for s_ in (sa, sb):
+            s_.wait_stream(main)
+        pa, pb = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream)
+
+        def item(l, k):
+            t0, t1 = P.fwd[l][k], P.fwd[l][k + 1]
+            v0, vn = (0, T) if store else (t0, P.nmax)
+            return _sdr_r(t0=t0, t1=t1, emb=_ptr(embs[l]), W=_ptr(Ws[l]), bias=_ptr(bs[l]), u=_ptr(us[l]), v0=v0,
+                          vn=vn, v=_ptr(vs[l]), couplings=_ptr(css[l]) if css[l] is not None else None,
+                          workspace=_ptr(rws[l]), workspace_bytes=rws[l].numel())
+
+        def run(sp, ls, ks):
+            """pose + recurrence (+ LN/dropout for inner layers) of ranges (ls[i], ks[i])
+            of same-shaped layers, batched."""
+            N, din, J, D, mf = P.layers[ls[0]]
+            rr = [item(l, k) for l, k in zip(ls, ks)]
+            _sdr_call(L_.srf_route_sdr_pose_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, int(P.pose_fp8), sp,
+                      what='sdr_pose_n')
+            _sdr_call(L_.srf_route_sdr_recur_fwd_n, rr, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
+                      what='sdr_recur_fwd_n')
+            for l, r in zip(ls, rr):
+                if l < L - 1:
+                    _lib.check(L_.srf_capsnorm_fwd_range(_ptr(vs[l]), B, T, r.t0, r.t1, J * D, _ptr(gammas[l]),
+                                                         _ptr(betas[l]), tr, float(p_mid), int(seed), l,
+                                                         _ptr(embs[l + 1]), _ptr(stats[l]), sp), 'capsnorm_range')
+
+        for d in range(P.K + L - 1):
+            # inner layers: diagonal d on stream A, grouped by layer shape
+            groups = {}
+            for l in range(L - 1):
+                k = d - l
+                if 0 <= k < P.K and P.fwd[l][k] < P.fwd[l][k + 1]:
+                    groups.setdefault(P.layers[l], []).append((l, k))
+            for g in groups.values():
+                run(pa, [l for l, _ in g], [k for _, k in g])
+            ev_a[d].record(sa)
+            # last layer: range k = d - (L-1) needs (L-2, k), done on diagonal d - 1
+            k = d - (L - 1)
+            if 0 <= k < P.K and P.fwd[L - 1][k] < P.fwd[L - 1][k + 1]:
+                if L > 1:
+                    sb.wait_event(ev_a[d - 1])
+                run(pb, [L - 1], [k])
+        for s_ in (sa, sb):
+            main.wait_stream(s_)
+        ctx.plan, ctx.meta = P, (tr, float(p_mid), int(seed), store)
+        ctx.params = params
+        ctx.css = css
+        ctx.save_for_backward(*embs, *vs, *stats, *(us if store else []), *params)
+        return vs[-1]
+
+    @staticmethod
+    def backward(ctx, g_v_last):
+        L_ = _lib.lib()
+        P = ctx.plan
+        B, T, L = P.B, P.T, P.L
+        tr, p_mid, seed, store = ctx.meta
+        saved = list(ctx.saved_tensors)
+        embs, saved = saved[:L], saved[L:]
+        vs, saved = saved[:L], saved[L:]
+        stats, saved = saved[:L - 1], saved[L - 1:]
+        if store:
+            us, saved = saved[:L], saved[L:]
+        params = saved
+        Ws, bs = params[0:2 * L:2], params[1:2 * L:2]
+        gammas, betas = params[2 * L::2], params[2 * L + 1::2]
+        dev = g_v_last.device
+        g_v_last = g_v_last.contiguous()
+        targets = [_grad_target(p) for p in ctx.params]
+        gWs, gbs = [targets[2 * l][0] for l in range(L)], [targets[2 * l + 1][0] for l in range(L)]
+        ggs = [targets[2 * L + 2 * l][0] for l in range(L - 1)]
+        gbts = [targets[2 * L + 2 * l + 1][0] for l in range(L - 1)]
+        g_embs = [torch.zeros_like(e) for e in embs]           # gx scatter targets
+        g_vs, gparts, carries, WTs, gus, urs, rws, pws = [], [], [], [], [], [], [], []
+        for l, (N, din, J, D, mf) in enumerate(P.layers):
+            n = J * D
+            g_vs.append(torch.empty((B, T, J, D), device=dev) if l < L - 1 else g_v_last)
+            gparts.append(torch.empty((B * T, 2 * n), device=dev) if l < L - 1 else None)
+            carries.append(torch.zeros((B, n), device=dev))
+            WTs.append(torch.empty(Ws[l].numel(), device=dev))
+            gus.append(torch.empty(P.u_floats(l, P.nmax), device=dev))
+            urs.append(us[l] if store else torch.empty(P.u_floats(l, P.nmax), device=dev))
+            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
+            pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
+                                   dtype=torch.uint8) if l < L - 1 else None)
+        main = torch.cuda.current_stream(dev)
+        sa, sb = _layer_streams(dev, 2, 'bwd')
+        ev_b = P.events('bwd_b', P.K)
+        for s_ in (sa, sb):
+            s_.wait_stream(main)
+        pa, pb = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream)
+        for l, (N, din, J, D, mf) in enumerate(P.layers):
+            _lib.check(L_.srf_route_sdr_transpose_w(_ptr(Ws[l]), P.in_n(l), J, D, din, _ptr(WTs[l]),
+                                                    pb if l == L - 1 else pa), 'sdr_transpose_w')
+
+        def item(l, k):
+            t0, t1 = P.bwd[l][k], P.bwd[l][k + 1]
+            v0, vn = (0, T) if store else (t0, P.nmax)
+            cs = ctx.css[l]
+            return _sdr_r(t0=t0, t1=t1, emb=_ptr(embs[l]), W=_ptr(Ws[l]), bias=_ptr(bs[l]), WT=_ptr(WTs[l]),
+                          u=_ptr(urs[l]), v0=v0, vn=vn, v=_ptr(vs[l]),
+                          couplings=_ptr(cs) if cs is not None else None, workspace=_ptr(rws[l]),
+                          workspace_bytes=rws[l].numel(), g_v=_ptr(g_vs[l]), carry=_ptr(carries[l]),
+                          gu=_ptr(gus[l]), g0=t0, gn=P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
+                          g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1))
+
+        def run(sp, ls, ks, ev=None):
+            """backward of ranges (ls[i], ks[i]) of same-shaped layers, batched: LN
+            backward of the range's rows (inner layers), pose (when u was not kept),
+            recurrence, gx (window adjoint into the layer below), gW / gbias."""
+            N, din, J, D, mf = P.layers[ls[0]]
+            rr = [item(l, k) for l, k in zip(ls, ks)]
+            live = [r for r in rr if r.t1 > r.t0]
+            for l, r in zip(ls, rr):
+                if l < L - 1 and r.t1 > r.t0:
+                    _lib.check(L_.srf_capsnorm_bwd_range(_ptr(vs[l]), B, T, r.t0, r.t1, J * D, _ptr(gammas[l]),
+                                                         _ptr(betas[l]), tr, p_mid, seed, l, _ptr(stats[l]),
+                                                         _ptr(g_embs[l + 1]), _ptr(g_vs[l]), _ptr(gparts[l]), sp),
+                               'capsnorm_bwd_range')
+            if live:
+                if not store:
+                    _sdr_call(L_.srf_route_sdr_pose_n, live, B, T, N, din, P.lpad, P.rpad, J, D, int(P.pose_fp8), sp,
+                              what='sdr_pose_n')
+                _sdr_call(L_.srf_route_sdr_recur_bwd_n, live, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
+                          what='sdr_recur_bwd_n')
+                _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')
+            if ev is not None:
+                ev.record(sa if sp is pa else sb)
+            # gW of every range (an empty first range still zeroes the layer's sums)
+            _sdr_call(L_.srf_route_sdr_gw_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gw_n')
+            for l, k in zip(ls, ks):
+                if k == 0 and l < L - 1:
+                    _lib.check(L_.srf_capsnorm_bwd_params(_ptr(gparts[l]), B * T, J * D, _ptr(ggs[l]),
+                                                          _ptr(gbts[l]), _ptr(pws[l]), pws[l].numel(), sp),
+                               'capsnorm_bwd_params')
+
+        # diagonal e of the inner layers holds (l, k) with (K-1-k) + (L-2-l) = e: (l, k)
+        # needs (l+1, k) (diagonal e-1, or the last layer's range k on stream B) and
+        # (l, k+1) (diagonal e-1)
+        for e in range(P.K + L - 1):
+            k = P.K - 1 - e
+            if k >= 0:   # last layer, range k, on stream B
+                run(pb, [L - 1], [k], ev=ev_b[k])
+            groups = {}
+            for l in range(L - 1):
+                kk = P.K - 1 - (e - (L - 2 - l))
+                if 0 <= kk < P.K:
+                    groups.setdefault(P.layers[l], []).append((l, kk))
+            if not groups:
+                continue
+            kl = P.K - 1 - e   # (L-2, kl) is in this diagonal: it needs the last layer's range kl
+            if L > 1 and 0 <= kl < P.K:
+                sa.wait_event(ev_b[kl])
+            for g in groups.values():
+                run(pa, [l for l, _ in g], [kk for _, kk in g])
+        for s_ in (sa, sb):
+            main.wait_stream(s_)
+        ctx.css = None
+        return (g_embs[0], None, None, None, None, *_returned(targets))
+
+
+class SdrStackPerLayer(torch.autograd.Function):
+    """The round-3 first form of the stack (one HIP stream per layer, one launch per
+    range), kept for A/B runs (SRF_SDR_BATCH=0): the layer streams share the process's
+    four in-order hardware queues, so a range waiting on another layer blocks the
+    ranges queued behind it (measured concurrency 1-2 recurrences at C3/C5)."""
+
     """emb0 [B,T,N0,din0] -> v of the last layer [B,T,J,D]; in between, layer l's v
     goes through drop(LN_mid{l+1}(v)) (the CapsNorm of naive:187-191) into layer
     l+1.  params: W_l, b_l for every layer, then gamma_l, beta_l for l < L-1."""
@@ -715,4 +938,6 @@ def sdr_stack(emb0, plan, training, p_mid, seed, params):
     """SdrStack.apply; the forward keeps the pose outputs for the backward only when
     one will run (grad mode on and something requires a gradient)."""
     plan.need_bwd = torch.is_grad_enabled() and (emb0.requires_grad or any(p.requires_grad for p in params))
+    if os.environ.get('SRF_SDR_BATCH', '1') == '0':
+        return SdrStackPerLayer.apply(emb0, plan, training, p_mid, seed, *params)
     return SdrStack.apply(emb0, plan, training, p_mid, seed, *params)
