@@ -474,7 +474,9 @@ class SdrStackPlan:
         self.L = len(layers)
         self.win = lpad + rpad + 1
         if n_chunks <= 0:
-            n_chunks = int(os.environ.get('SRF_SDR_CHUNKS', '0') or 0) or max(1, min(16, -(-T // 20)))
+            # ~10 frames per range (C3 step: 20-frame ranges 25.3 ms, 10-frame 23.95, 8-frame
+            # 23.9, 5-frame 25.3: shorter ranges shorten the wavefront's fill and drain)
+            n_chunks = int(os.environ.get('SRF_SDR_CHUNKS', '0') or 0) or max(1, min(32, -(-T // 10)))
         # ranges of S frames on one grid, layer l's shifted down by l * rpad; the grid
         # runs M >= K ranges so that no layer's shifted range is clipped into a long
         # one (C5: rpad = 20 frames per layer would otherwise leave the last layer one
@@ -603,26 +605,38 @@ class SdrStack(torch.autograd.Function):
             us.append(torch.empty(P.u_floats(l, T if store else P.nmax), device=dev, dtype=torch.float32))
             rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
         main = torch.cuda.current_stream(dev)
-        sa, sb = _layer_streams(dev, 2, 'fwd')
-        ev_a = P.events('fwd_a', P.K + L)
-        for s_ in (sa, sb):
+        sa, sb, sc = _layer_streams(dev, 3, 'fwd')
+        ev_a, ev_p = P.events('fwd_a', P.K + L), P.events('fwd_p', P.K)
+        for s_ in (sa, sb, sc):
             s_.wait_stream(main)
-        pa, pb = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream)
+        pa, pb, pc = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream), ctypes_void(sc.cuda_stream)
+        # the last layer's pose runs ahead of its recurrence on stream C when u is kept
+        # whole (a range buffer would be overwritten by the next pose)
+        pose_ahead = (store or not need_bwd and P.u_floats(L - 1, T) * 4 <= 2 ** 30) and \
+            os.environ.get('SRF_SDR_POSE_AHEAD', '1') != '0'
+        if pose_ahead and not store:
+            us[L - 1] = torch.empty(P.u_floats(L - 1, T), device=dev, dtype=torch.float32)
 
         def item(l, k):
             t0, t1 = P.fwd[l][k], P.fwd[l][k + 1]
-            v0, vn = (0, T) if store else (t0, P.nmax)
+            v0, vn = (0, T) if (store or (pose_ahead and l == L - 1)) else (t0, P.nmax)
             return _sdr_r(t0=t0, t1=t1, emb=_ptr(embs[l]), W=_ptr(Ws[l]), bias=_ptr(bs[l]), u=_ptr(us[l]), v0=v0,
                           vn=vn, v=_ptr(vs[l]), couplings=_ptr(css[l]) if css[l] is not None else None,
                           workspace=_ptr(rws[l]), workspace_bytes=rws[l].numel())
 
-        def run(sp, ls, ks):
-            """pose + recurrence (+ LN/dropout for inner layers) of ranges (ls[i], ks[i])
-            of same-shaped layers, batched."""
+        def pose(sp, ls, ks):
             N, din, J, D, mf = P.layers[ls[0]]
             rr = [item(l, k) for l, k in zip(ls, ks)]
             _sdr_call(L_.srf_route_sdr_pose_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, int(P.pose_fp8), sp,
                       what='sdr_pose_n')
+
+        def run(sp, ls, ks, with_pose=True):
+            """pose + recurrence (+ LN/dropout for inner layers) of ranges (ls[i], ks[i])
+            of same-shaped layers, batched."""
+            N, din, J, D, mf = P.layers[ls[0]]
+            rr = [item(l, k) for l, k in zip(ls, ks)]
+            if with_pose:
+                pose(sp, ls, ks)
             _sdr_call(L_.srf_route_sdr_recur_fwd_n, rr, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
                       what='sdr_recur_fwd_n')
             for l, r in zip(ls, rr):
@@ -644,10 +658,16 @@ class SdrStack(torch.autograd.Function):
             # last layer: range k = d - (L-1) needs (L-2, k), done on diagonal d - 1
             k = d - (L - 1)
             if 0 <= k < P.K and P.fwd[L - 1][k] < P.fwd[L - 1][k + 1]:
-                if L > 1:
+                if pose_ahead:
+                    if L > 1:
+                        sc.wait_event(ev_a[d - 1])
+                    pose(pc, [L - 1], [k])
+                    ev_p[k].record(sc)
+                    sb.wait_event(ev_p[k])
+                elif L > 1:
                     sb.wait_event(ev_a[d - 1])
-                run(pb, [L - 1], [k])
-        for s_ in (sa, sb):
+                run(pb, [L - 1], [k], with_pose=not pose_ahead)
+        for s_ in (sa, sb, sc):
             main.wait_stream(s_)
         ctx.plan, ctx.meta = P, (tr, float(p_mid), int(seed), store)
         ctx.params = params
@@ -691,7 +711,15 @@ class SdrStack(torch.autograd.Function):
                                    dtype=torch.uint8) if l < L - 1 else None)
         main = torch.cuda.current_stream(dev)
         sa, sb = _layer_streams(dev, 2, 'bwd')
-        ev_b = P.events('bwd_b', P.K)
+        # The last layer's gW runs on stream A, off B's critical chain, when its whole gu
+        # fits SRF_SDR_GW_SIDE_GB (default 0, off: at C3 26.8 vs 25.2 ms, stream A is as
+        # critical as B; the last layer's whole gu is 1.8 GB): B then never reuses a gu range
+        # buffer that A still reads, so A waits on B only.  (B waiting on A as well --
+        # two side streams ordered both ways -- crashes this ROCm's capture_end.)
+        gw_side = L > 1 and P.u_floats(L - 1, T) * 4 <= float(os.environ.get('SRF_SDR_GW_SIDE_GB', '0')) * 2 ** 30
+        if gw_side:
+            gus[L - 1] = torch.empty(P.u_floats(L - 1, T), device=dev)
+        ev_b = P.events('bwd_b', P.K)   # the last layer's range k has its gu and gx
         for s_ in (sa, sb):
             s_.wait_stream(main)
         pa, pb = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream)
@@ -707,13 +735,14 @@ class SdrStack(torch.autograd.Function):
                           u=_ptr(urs[l]), v0=v0, vn=vn, v=_ptr(vs[l]),
                           couplings=_ptr(cs) if cs is not None else None, workspace=_ptr(rws[l]),
                           workspace_bytes=rws[l].numel(), g_v=_ptr(g_vs[l]), carry=_ptr(carries[l]),
-                          gu=_ptr(gus[l]), g0=t0, gn=P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
+                          gu=_ptr(gus[l]), g0=0 if (gw_side and l == L - 1) else t0,
+                          gn=T if (gw_side and l == L - 1) else P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
                           g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1))
 
-        def run(sp, ls, ks, ev=None):
+        def run(sp, ls, ks, ev=None, gw=True):
             """backward of ranges (ls[i], ks[i]) of same-shaped layers, batched: LN
             backward of the range's rows (inner layers), pose (when u was not kept),
-            recurrence, gx (window adjoint into the layer below), gW / gbias."""
+            recurrence, gx (window adjoint into the layer below), then (gw) gW / gbias."""
             N, din, J, D, mf = P.layers[ls[0]]
             rr = [item(l, k) for l, k in zip(ls, ks)]
             live = [r for r in rr if r.t1 > r.t0]
@@ -732,13 +761,19 @@ class SdrStack(torch.autograd.Function):
                 _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')
             if ev is not None:
                 ev.record(sa if sp is pa else sb)
-            # gW of every range (an empty first range still zeroes the layer's sums)
-            _sdr_call(L_.srf_route_sdr_gw_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gw_n')
+            if gw:
+                gw_ranges(sp, ls, ks)
             for l, k in zip(ls, ks):
                 if k == 0 and l < L - 1:
                     _lib.check(L_.srf_capsnorm_bwd_params(_ptr(gparts[l]), B * T, J * D, _ptr(ggs[l]),
                                                           _ptr(gbts[l]), _ptr(pws[l]), pws[l].numel(), sp),
                                'capsnorm_bwd_params')
+
+        def gw_ranges(sp, ls, ks):
+            """gW / gbias of the ranges (an empty first range still zeroes the layer's sums)."""
+            N, din, J, D, mf = P.layers[ls[0]]
+            rr = [item(l, k) for l, k in zip(ls, ks)]
+            _sdr_call(L_.srf_route_sdr_gw_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gw_n')
 
         # diagonal e of the inner layers holds (l, k) with (K-1-k) + (L-2-l) = e: (l, k)
         # needs (l+1, k) (diagonal e-1, or the last layer's range k on stream B) and
@@ -746,7 +781,7 @@ class SdrStack(torch.autograd.Function):
         for e in range(P.K + L - 1):
             k = P.K - 1 - e
             if k >= 0:   # last layer, range k, on stream B
-                run(pb, [L - 1], [k], ev=ev_b[k])
+                run(pb, [L - 1], [k], ev=ev_b[k], gw=not gw_side)
             groups = {}
             for l in range(L - 1):
                 kk = P.K - 1 - (e - (L - 2 - l))
@@ -757,6 +792,8 @@ class SdrStack(torch.autograd.Function):
             kl = P.K - 1 - e   # (L-2, kl) is in this diagonal: it needs the last layer's range kl
             if L > 1 and 0 <= kl < P.K:
                 sa.wait_event(ev_b[kl])
+                if gw_side:
+                    gw_ranges(pa, [L - 1], [kl])
             for g in groups.values():
                 run(pa, [l for l, _ in g], [kk for _, kk in g])
         for s_ in (sa, sb):
