@@ -195,6 +195,32 @@ def _timed(step, steps, world, dev):
     return elapsed
 
 
+def sdr_roofline(model, tms):
+    """HBM roofline of the SDR recurrence (the last layer's forward launches, one
+    workgroup per utterance walking its frames; sequence_router_naive.py:162-170).
+    Algorithmic bytes per frame: the frame's u_t read once per routing iteration by
+    the streaming kernel (route_sdr_stream.hip, frames beyond the register budget) or
+    once in all by the register-resident one (route_sdr_seq.hip), plus v_t written."""
+    from srf_amd import _lib
+    in_n, J, D, Din = model.layer_shapes[model.enc_num - 1]
+    R = model.route_iters
+    stream = bool(_lib.lib().srf_route_sdr_couplings_required(in_n, J, D, R))
+    reads = R if stream else 1
+    per_frame = reads * in_n * J * D * 4 + J * D * 4
+    ms = sum(t for t, _ in tms)
+    frames = sum(f for _, f in tms)
+    if not tms or ms <= 0:
+        return None
+    gbs = per_frame * frames / (ms * 1e-3) / 1e9
+    return {'kernel': ('sdr_stream_fwd_kernel<%d,%d>' % (D, J * D // 64) if stream else
+                       'sdr_seq_fwd_kernel<%d,%d,...>' % (D, J)) +
+            ' (layer %d SDR recurrence, forward, one workgroup per utterance)' % model.enc_num,
+            'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+            'avg_launch_us': round(ms / len(tms) * 1e3, 2), 'bytes_per_launch': per_frame * frames / len(tms),
+            'bytes_per_frame': per_frame, 'note': 'u_t read %d time(s) per frame' % reads}
+
+
 def measure(workload, args, world, rank, dev):
     """One workload: W eager + W graphed warmup steps, K timed training steps (the
     hipGraph replay of forward + CTC + backward, then the all-reduce and Adam), K
@@ -263,6 +289,20 @@ def measure(workload, args, world, rank, dev):
             model(feats_b, input_lengths=il_b, training=False)
         fwd_elapsed = _timed(lambda: model(feats_b, input_lengths=il_b, training=False), args.steps, world, dev)
 
+    sdr_roof = None
+    if not dr:
+        # SDR: HIP events (on the launch stream) around the last layer's forward
+        # recurrence launches of eager forward passes, after the timed region
+        plan = model._stack_plan(B, Tp)
+        plan.timing = []
+        with torch.no_grad():
+            for _ in range(max(1, min(args.steps, 3))):
+                model(feats_b, input_lengths=il_b, training=False)
+        torch.cuda.synchronize()
+        tms = [(e0.elapsed_time(e1), fr) for e0, e1, fr in plan.timing]
+        plan.timing = None
+        sdr_roof = sdr_roofline(model, tms)
+
     kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
     kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
     in_n, J, D, Din = model.layer_shapes[last]
@@ -309,7 +349,7 @@ def measure(workload, args, world, rank, dev):
                                         'frac': round(frames_prime * 2.0 * in_n * ((J * D + 31) // 32 * 32) * 16
                                                       * {8: 3, 16: 4, 32: 7}[Din] / (kern_avg_ms * 1e-3) / 1e12
                                                       / BF16_MFMA_PEAK_TFLOPS, 4)} if fwd32 else None)}
-                    if dr else None,
+                    if dr else sdr_roof,
         'dtype': 'fp8 pose (e4m3, fp32 accumulate) / fp32' if model.pose_fp8 else 'fp32',
         'forward_only': {'value': round(B * T * world * args.steps / fwd_elapsed, 1), 'unit': 'frames/s',
                          'ms_per_step': round(fwd_elapsed / args.steps * 1e3, 4),

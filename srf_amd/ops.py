@@ -630,6 +630,8 @@ class SdrStack(torch.autograd.Function):
             _sdr_call(L_.srf_route_sdr_pose_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, int(P.pose_fp8), sp,
                       what='sdr_pose_n')
 
+        timing = getattr(P, 'timing', None)   # bench.py: [(start, end, frames)] of the last layer
+
         def run(sp, ls, ks, with_pose=True):
             """pose + recurrence (+ LN/dropout for inner layers) of ranges (ls[i], ks[i])
             of same-shaped layers, batched."""
@@ -637,8 +639,15 @@ class SdrStack(torch.autograd.Function):
             rr = [item(l, k) for l, k in zip(ls, ks)]
             if with_pose:
                 pose(sp, ls, ks)
+            tm = timing is not None and ls[0] == L - 1
+            if tm:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record(sb)
             _sdr_call(L_.srf_route_sdr_recur_fwd_n, rr, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
                       what='sdr_recur_fwd_n')
+            if tm:
+                ev1.record(sb)
+                timing.append((ev0, ev1, B * sum(r.t1 - r.t0 for r in rr)))
             for l, r in zip(ls, rr):
                 if l < L - 1:
                     _lib.check(L_.srf_capsnorm_fwd_range(_ptr(vs[l]), B, T, r.t0, r.t1, J * D, _ptr(gammas[l]),
