@@ -566,7 +566,21 @@ struct Args32 {
   float2* part;    // per-row-block (max, sum exp) [in_n][n_rb][Fs]
   float* lz;       // logZ^r [in_n][Fs]
   int n_rb, n_fb, nchL, clenL;
+  // XCD-aware block order (routing passes r >= 1, forward and B1): > 0 = the number of
+  // (frame tile, i-chunk) workgroups, the grid padded to a multiple of 8 (kXcds)
+  int xcd_nwg;
 };
+
+// The dispatcher deals consecutive workgroups round-robin to the 8 XCDs (each with its
+// own L2).  Block b runs logical workgroup (b % 8) * (grid / 8) + b / 8, so the
+// i-chunk workgroups of one frame tile (consecutive logical ids) share an XCD and its
+// L2 copy of the tile's Vc rows / gs rows instead of each fetching them from HBM.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_block(int nwg) {
+  if (nwg <= 0) return blockIdx.x;
+  const int per = gridDim.x / kXcds;
+  return (blockIdx.x % kXcds) * per + blockIdx.x / kXcds;
+}
 
 
 
@@ -674,7 +688,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int JD = A.J * DOUT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int ft = blockIdx.x / A.n_chunks, chunk = blockIdx.x - ft * A.n_chunks;
+  const int bid = xcd_block(A.xcd_nwg);
+  if (A.xcd_nwg > 0 && bid >= A.xcd_nwg) return;   // grid padding
+  const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
   const int f = ft * 32 + r;
   const int fc = min(f, A.F - 1);
   const int fb = fc / A.T, ftt = fc - fb * A.T;
@@ -956,7 +972,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int JD = A.J * DOUT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int ft = blockIdx.x / A.n_chunks, chunk = blockIdx.x - ft * A.n_chunks;
+  const int bid = xcd_block(A.xcd_nwg);
+  if (A.xcd_nwg > 0 && bid >= A.xcd_nwg) return;   // grid padding
+  const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
   const int f = ft * 32 + r;
   const int fc = min(f, A.F - 1);
   const int fb = fc / A.T, ftt = fc - fb * A.T;
@@ -1711,13 +1729,24 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   return SRF_OK;
 }
 
+// SRF_XCD_REMAP=0: the plain block order (A/B)
+static bool xcd_remap() {
+  const char* e = getenv("SRF_XCD_REMAP");
+  return !(e && e[0] == '0');
+}
+static int xcd_grid(int nwg) { return xcd_remap() ? (nwg + kXcds - 1) / kXcds * kXcds : nwg; }
+static Args32 xcd_args(Args32 a, const Fwd32Plan& p) {
+  a.xcd_nwg = xcd_remap() ? p.n_ftiles * p.n_chunks : 0;
+  return a;
+}
+
 template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_rpass(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
   auto kern = route_fwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(xcd_grid(p.n_ftiles * p.n_chunks)), dim3(64 * NW), lds, st, xcd_args(a, p));
   SRF_LAUNCH_CHECK("route_fwd32");
   return SRF_OK;
 }
@@ -1783,7 +1812,7 @@ static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch,
                           int lpad, int rpad, int J, int dout, int mask_first) {
   const int in_n = N * (lpad + rpad + 1);
   const char* base = static_cast<const char*>(planes);
-  Args32 a;
+  Args32 a{};
   a.Ws = base;
   a.bs = base + p.ws_w;
   a.xs = base + p.ws_w + p.ws_b;
@@ -1881,7 +1910,7 @@ static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b,
   auto kern = route_bwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a, b);
+  hipLaunchKernelGGL(kern, dim3(xcd_grid(p.n_ftiles * p.n_chunks)), dim3(64 * NW), lds, st, xcd_args(a, p), b);
   SRF_LAUNCH_CHECK("route_bwd32");
   return SRF_OK;
 }
