@@ -206,7 +206,8 @@ def sdr_roofline(model, tms):
     R = model.route_iters
     stream = bool(_lib.lib().srf_route_sdr_couplings_required(in_n, J, D, R))
     reads = R if stream else 1
-    per_frame = reads * in_n * J * D * 4 + J * D * 4
+    elt = 2 if (stream and model.pose_fp8 and os.environ.get('SRF_SDR_U_BF16', '1') != '0') else 4   # bf16 u
+    per_frame = reads * in_n * J * D * elt + J * D * 4
     ms = sum(t for t, _ in tms)
     frames = sum(f for _, f in tms)
     if not tms or ms <= 0:
@@ -218,7 +219,8 @@ def sdr_roofline(model, tms):
             'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
             'avg_launch_us': round(ms / len(tms) * 1e3, 2), 'bytes_per_launch': per_frame * frames / len(tms),
-            'bytes_per_frame': per_frame, 'note': 'u_t read %d time(s) per frame' % reads}
+            'bytes_per_frame': per_frame, 'note': 'u_t (%s) read %d time(s) per frame' % ('bf16' if elt == 2 else 'fp32',
+                                                                                     reads)}
 
 
 def measure(workload, args, world, rank, dev):

@@ -146,7 +146,10 @@ typedef struct {
   float* g_W;                  /* gW: [in_n][J*dout][din] */
   float* g_bias;               /* gW: [in_n][J*dout] */
   int accumulate;              /* gW: add to g_W / g_bias (else overwrite) */
+  int u_bf16;                  /* u holds bf16 (written by pose_n mode 2; read by the streaming
+                                  recurrence kernels only, i.e. srf_route_sdr_couplings_required) */
 } srf_sdr_range;
+/* pose_n fp8: 0 fp32 pose, 1 fp8 pose (fp32 u), 2 fp8 pose storing u in bf16 */
 int srf_route_sdr_pose_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
                          int dout, int fp8, void* stream);
 int srf_route_sdr_recur_fwd_n(const srf_sdr_range* ranges, int n, int B, int T, int in_n, int J, int dout, int iters,

@@ -769,7 +769,16 @@ __device__ __forceinline__ float amax8(const f4& a, const f4& b) {
                fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w))));
 }
 
-template <int DIN>
+__device__ __forceinline__ unsigned short bf16_rne(float v) {
+  unsigned x = __float_as_uint(v);
+  x += 0x7fffu + ((x >> 16) & 1u);
+  return (unsigned short)(x >> 16);
+}
+
+// BF: u stored as bf16 (round to nearest even) for the streaming recurrence of the fp8
+// C5 variant: half the bytes of every u read, error 2^-9 relative -- well inside the
+// e4m3 operands' 2^-4.
+template <int DIN, bool BF = false>
 __global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int N, int lpad, int in_n, int JD, int nrb) {
   const GemmItem& G = items.it[blockIdx.z];
   const float* __restrict__ emb = G.x;
@@ -859,11 +868,15 @@ __global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int 
       if (q >= Q) continue;
       int b, t;
       fm.frame(q, b, t);
-      float* up = u + (fm.view(b, t) * in_n + i) * JD;
+      const size_t uo = (fm.view(b, t) * in_n + i) * JD;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         const int row = r0 + rt * 32 + l32;
-        if (row < JD) up[row] = acc[ft][rt][r] * sx * sw[rt] + bv[rt];
+        const float val = acc[ft][rt][r] * sx * sw[rt] + bv[rt];
+        if (row < JD) {
+          if constexpr (BF) reinterpret_cast<unsigned short*>(u)[uo + row] = bf16_rne(val);
+          else u[uo + row] = val;
+        }
       }
     }
 }
@@ -915,7 +928,9 @@ int max_q(const GemmItems& it) {
   return q;
 }
 
-int pose_n(const SGeom& g, const GemmItems& it, hipStream_t st, bool fp8 = false) {
+// mode: 0 fp32 pose, 1 fp8 pose with fp32 u, 2 fp8 pose with bf16 u
+int pose_n(const SGeom& g, const GemmItems& it, hipStream_t st, int mode = 0) {
+  const bool fp8 = mode != 0;
   const int Q = max_q(it);
   if (it.n == 0 || Q == 0) return SRF_OK;
   const int nrb = (g.JD() + 127) / 128;
@@ -925,10 +940,14 @@ int pose_n(const SGeom& g, const GemmItems& it, hipStream_t st, bool fp8 = false
       srf::set_error("fp8 pose: in_d must be 32 or 64 (got %d) and J*out_d a multiple of 8", g.din);
       return SRF_EUNSUPPORTED;
     }
-    if (g.din == 32)
-      hipLaunchKernelGGL(sdr_pose8_kernel<32>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
-    else
-      hipLaunchKernelGGL(sdr_pose8_kernel<64>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
+#define SRF_POSE8(DIN, BF) \
+  hipLaunchKernelGGL((sdr_pose8_kernel<DIN, BF>), grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb)
+    if (g.din == 32) {
+      if (mode == 2) SRF_POSE8(32, true); else SRF_POSE8(32, false);
+    } else {
+      if (mode == 2) SRF_POSE8(64, true); else SRF_POSE8(64, false);
+    }
+#undef SRF_POSE8
     SRF_LAUNCH_CHECK("sdr_pose8");
     return SRF_OK;
   }
@@ -966,8 +985,22 @@ int pose_range(const SGeom& g, const float* emb, const float* W, const float* bi
 // The recurrence over it.n frame ranges (grid.y): the register-resident kernels when the
 // shape fits, else the streaming ones, else the LDS / global-state ones (one launch per
 // item; gstate: the item's workspace, B slices of the state, when it exceeds LDS).
+// bf16 u (the fp8 C5 variant) is read by the streaming kernels only
+int u_type_ok(const SGeom& g, const srf::SeqItems& it) {
+  bool bf = false;
+  for (int k = 0; k < it.n; ++k) bf = bf || it.it[k].u_bf16;
+  if (bf && (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters) ||
+             !srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))) {
+    srf::set_error("bf16 u: only layers on the streaming recurrence kernels (in_n=%d J=%d dout=%d)", g.in_n(), g.J,
+                   g.dout);
+    return SRF_EUNSUPPORTED;
+  }
+  return SRF_OK;
+}
+
 int recur_fwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
   if (it.n == 0) return SRF_OK;
+  if (int rc = u_type_ok(g, it)) return rc;
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_seq_fwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, st);
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
@@ -988,6 +1021,7 @@ int recur_fwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
 
 int recur_bwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
   if (it.n == 0) return SRF_OK;
+  if (int rc = u_type_ok(g, it)) return rc;
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_seq_bwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, st);
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
@@ -1235,6 +1269,7 @@ srf::SeqItems seq_items(const srf_sdr_range* r, int n, int T, bool bwd, bool kee
     I.ws = static_cast<float*>(r[k].workspace);
     I.rg = bwd ? srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, r[k].g0, r[k].gn, r[k].carry}
                : srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, 0, T, nullptr};
+    I.u_bf16 = r[k].u_bf16;
   }
   return it;
 }
@@ -1255,7 +1290,8 @@ int srf_route_sdr_pose_n(const srf_sdr_range* r, int n, int B, int T, int N, int
     it.it[it.n++] = GemmItem{r[k].emb, r[k].W, r[k].bias, r[k].u, nullptr, 0, B * (r[k].t1 - r[k].t0),
                              frame_map(T, r[k].t0, r[k].t1, r[k].v0, r[k].vn)};
   }
-  return pose_n(g, it, static_cast<hipStream_t>(stream), fp8 != 0);
+  SRF_REQUIRE(fp8 >= 0 && fp8 <= 2, "pose mode %d (0 fp32, 1 fp8, 2 fp8 with bf16 u)", fp8);
+  return pose_n(g, it, static_cast<hipStream_t>(stream), fp8);
 }
 
 int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,

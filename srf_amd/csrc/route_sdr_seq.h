@@ -30,13 +30,14 @@ struct SeqRange {
 //   ws: the stream backward's scratch (sdr_stream_workspace_floats).
 constexpr int kMaxItems = 8;
 struct SeqItem {
-  const float* u;
+  const float* u;   // fp32, or bf16 (u_bf16: the streaming kernels only) behind the same pointer
   float* v;
   const float* g_v;
   float* gu;
   float* cs;
   float* ws;
   SeqRange rg;
+  int u_bf16;
 };
 struct SeqItems {
   SeqItem it[kMaxItems];

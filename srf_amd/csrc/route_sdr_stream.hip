@@ -86,6 +86,21 @@ __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t rs, float v, uint3
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, off, 0, 0);
 }
 
+// KD consecutive bf16 values (u stored in bf16 by the fp8 pose), widened exactly to fp32
+template <int KD>
+__device__ __forceinline__ void load_slice(const unsigned short* __restrict__ p, float (&x)[KD]) {
+  static_assert(KD % 8 == 0, "bf16 slices load 8 values per 16 bytes");
+#pragma unroll
+  for (int c = 0; c < KD; c += 8) {
+    const auto q = *reinterpret_cast<const unsigned __attribute__((ext_vector_type(4)))*>(p + c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[c + 2 * k] = __uint_as_float(q[k] << 16);
+      x[c + 2 * k + 1] = __uint_as_float(q[k] & 0xffff0000u);
+    }
+  }
+}
+
 template <int KD>
 __device__ __forceinline__ void load_slice(const float* __restrict__ p, float (&x)[KD]) {
 #pragma unroll
@@ -127,12 +142,12 @@ __device__ __forceinline__ float dsquash(float s, float a) {
 
 // ------------------------------------------------------------------ forward
 // LDS: wl [JD] (Vc of the iteration), part [kNW][JD].
-template <int D, int KD>
+template <int D, int KD, class TU>
 __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items, int T, int in_n, int iters,
                                                              int mask_first, int NMp) {
   using C = SC<D, KD>;
   const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
-  const float* __restrict__ u = I.u;
+  const TU* __restrict__ u = reinterpret_cast<const TU*>(I.u);
   float* __restrict__ v_out = I.v;
   float* __restrict__ cs = I.cs;
   const srf::SeqRange rg = I.rg;
@@ -148,7 +163,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
   const bool q0 = (lane % C::RQ) == 0;
   const bool jm = !(mask_first && j == 0);
   const size_t ff = (size_t)in_n * JD;
-  const float* ub = u + (size_t)b * rg.tu_n * ff + lane * KD;
+  const TU* ub = u + (size_t)b * rg.tu_n * ff + lane * KD;
   float* vo = v_out + (size_t)b * T * JD;
   const size_t csr = cs_rec(in_n, J, D, iters);
 
@@ -223,12 +238,12 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
 // ------------------------------------------------------------------ backward
 // LDS: part [kNW][JD], gsl [kRM][JD] (gs^r), vcl [kRM][JD] (Vc^r).
 // gls: per-utterance scratch gL^r [R][in_n][J].
-template <int D, int KD>
+template <int D, int KD, class TU>
 __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items, int T, int in_n, int iters,
                                                              int NMp) {
   using C = SC<D, KD>;
   const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
-  const float* __restrict__ u = I.u;
+  const TU* __restrict__ u = reinterpret_cast<const TU*>(I.u);
   const float* __restrict__ v_saved = I.v;
   const float* __restrict__ g_v = I.g_v;
   float* __restrict__ gu = I.gu;
@@ -249,7 +264,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
   const bool q0 = (lane % C::RQ) == 0;
   const size_t ff = (size_t)in_n * JD;
   const size_t PJ = (size_t)in_n * J;
-  const float* ub = u + (size_t)b * rg.tu_n * ff + lane * KD;
+  const TU* ub = u + (size_t)b * rg.tu_n * ff + lane * KD;
   float* gub = gu + (size_t)b * rg.tg_n * ff + lane * KD;
   const size_t csr = cs_rec(in_n, J, D, iters);
   const float* csb = cs + (size_t)b * T * csr;
@@ -409,7 +424,7 @@ template <int D, int KD>
 int launch_fwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, int mask_first, hipStream_t st) {
   using C = SC<D, KD>;
   const size_t lds = fwd_lds(C::JD);
-  auto k = sdr_stream_fwd_kernel<D, KD>;
+  auto k = items.it[0].u_bf16 ? sdr_stream_fwd_kernel<D, KD, unsigned short> : sdr_stream_fwd_kernel<D, KD, float>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kNT), lds, st, items, T, in_n, iters, mask_first,
@@ -422,7 +437,7 @@ template <int D, int KD>
 int launch_bwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, hipStream_t st) {
   using C = SC<D, KD>;
   const size_t lds = bwd_lds(C::JD);
-  auto k = sdr_stream_bwd_kernel<D, KD>;
+  auto k = items.it[0].u_bf16 ? sdr_stream_bwd_kernel<D, KD, unsigned short> : sdr_stream_bwd_kernel<D, KD, float>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kNT), lds, st, items, T, in_n, iters, nm_padded(in_n, C::PDB));
@@ -459,8 +474,16 @@ size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters) 
   return sdr_stream_supported(in_n, J, dout, iters) ? (size_t)B * iters * in_n * J : 0;
 }
 
+// the items of one launch share the u element type
+static int same_u_type(const SeqItems& items) {
+  for (int k = 1; k < items.n; ++k)
+    SRF_REQUIRE(items.it[k].u_bf16 == items.it[0].u_bf16, "sdr_stream: launch items mix fp32 and bf16 u");
+  return SRF_OK;
+}
+
 int sdr_stream_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
                    hipStream_t st) {
+  if (int rc = same_u_type(items)) return rc;
   const int KD = J * dout / 64;
 #define SRF_STREAM_F(DD, KK) \
   if (dout == DD && KD == KK) return launch_fwd<DD, KK>(items, B, T, in_n, iters, mask_first, st);
@@ -471,6 +494,7 @@ int sdr_stream_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dou
 }
 
 int sdr_stream_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, hipStream_t st) {
+  if (int rc = same_u_type(items)) return rc;
   for (int k = 0; k < items.n; ++k)
     if (!items.it[k].cs || !items.it[k].ws) {
       srf::set_error("sdr_stream backward needs the forward's stored couplings and its scratch workspace");

@@ -495,6 +495,23 @@ class SdrStackPlan:
         self.nmax = max(max(b[k + 1] - b[k] for k in range(K)) for b in self.fwd)
         L_ = _lib.lib()
         self.rws = [L_.srf_route_sdr_recur_workspace(B, N * self.win, J, D, iters) for (N, din, J, D, mf) in layers]
+        # fp8 pose: layers on the streaming recurrence keep u in bf16 (half the bytes of
+        # every read; 2^-9 against the e4m3 operands' 2^-4); SRF_SDR_U_BF16=0 keeps fp32
+        self.ubf = [self.pose_fp8 and os.environ.get('SRF_SDR_U_BF16', '1') != '0'
+                    and bool(L_.srf_route_sdr_couplings_required(N * self.win, J, D, iters))
+                    for (N, din, J, D, mf) in layers]
+
+    def pose_mode(self, l):
+        """srf_route_sdr_pose_n mode: 0 fp32, 1 fp8, 2 fp8 with bf16 u."""
+        return 2 if self.ubf[l] else int(self.pose_fp8)
+
+    def u_empty(self, l, frames, dev):
+        """u buffer of `frames` frames per utterance (bf16 for ubf layers)."""
+        return torch.empty(self.u_floats(l, frames), device=dev,
+                           dtype=torch.bfloat16 if self.ubf[l] else torch.float32)
+
+    def u_bytes(self, l, frames):
+        return self.u_floats(l, frames) * (2 if self.ubf[l] else 4)
 
     def in_n(self, l):
         return self.layers[l][0] * self.win
@@ -538,7 +555,7 @@ def _store_u(plan, dev):
     device's memory: C5 keeps 135 GB of u on a 288 GB MI355X, C3 5.5 GB."""
     gb = os.environ.get('SRF_SDR_STORE_U_GB', '')
     budget = float(gb) * 2 ** 30 if gb else 0.55 * torch.cuda.get_device_properties(dev).total_memory
-    return sum(plan.u_floats(l, plan.T) for l in range(plan.L)) * 4 <= budget
+    return sum(plan.u_bytes(l, plan.T) for l in range(plan.L)) <= budget
 
 
 def _whole_gu(plan):
@@ -602,7 +619,7 @@ class SdrStack(torch.autograd.Function):
             if l < L - 1:
                 embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
                 stats.append(torch.empty((B * T, 4), device=dev, dtype=torch.float32))
-            us.append(torch.empty(P.u_floats(l, T if store else P.nmax), device=dev, dtype=torch.float32))
+            us.append(P.u_empty(l, T if store else P.nmax, dev))
             rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
         main = torch.cuda.current_stream(dev)
         sa, sb, sc = _layer_streams(dev, 3, 'fwd')
@@ -612,22 +629,22 @@ class SdrStack(torch.autograd.Function):
         pa, pb, pc = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream), ctypes_void(sc.cuda_stream)
         # the last layer's pose runs ahead of its recurrence on stream C when u is kept
         # whole (a range buffer would be overwritten by the next pose)
-        pose_ahead = (store or not need_bwd and P.u_floats(L - 1, T) * 4 <= 2 ** 30) and \
+        pose_ahead = (store or not need_bwd and P.u_bytes(L - 1, T) <= 2 ** 30) and \
             os.environ.get('SRF_SDR_POSE_AHEAD', '1') != '0'
         if pose_ahead and not store:
-            us[L - 1] = torch.empty(P.u_floats(L - 1, T), device=dev, dtype=torch.float32)
+            us[L - 1] = P.u_empty(L - 1, T, dev)
 
         def item(l, k):
             t0, t1 = P.fwd[l][k], P.fwd[l][k + 1]
             v0, vn = (0, T) if (store or (pose_ahead and l == L - 1)) else (t0, P.nmax)
             return _sdr_r(t0=t0, t1=t1, emb=_ptr(embs[l]), W=_ptr(Ws[l]), bias=_ptr(bs[l]), u=_ptr(us[l]), v0=v0,
                           vn=vn, v=_ptr(vs[l]), couplings=_ptr(css[l]) if css[l] is not None else None,
-                          workspace=_ptr(rws[l]), workspace_bytes=rws[l].numel())
+                          workspace=_ptr(rws[l]), workspace_bytes=rws[l].numel(), u_bf16=int(P.ubf[l]))
 
         def pose(sp, ls, ks):
             N, din, J, D, mf = P.layers[ls[0]]
             rr = [item(l, k) for l, k in zip(ls, ks)]
-            _sdr_call(L_.srf_route_sdr_pose_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, int(P.pose_fp8), sp,
+            _sdr_call(L_.srf_route_sdr_pose_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, P.pose_mode(ls[0]), sp,
                       what='sdr_pose_n')
 
         timing = getattr(P, 'timing', None)   # bench.py: [(start, end, frames)] of the last layer
@@ -714,7 +731,7 @@ class SdrStack(torch.autograd.Function):
             carries.append(torch.zeros((B, n), device=dev))
             WTs.append(torch.empty(Ws[l].numel(), device=dev))
             gus.append(torch.empty(P.u_floats(l, P.nmax), device=dev))
-            urs.append(us[l] if store else torch.empty(P.u_floats(l, P.nmax), device=dev))
+            urs.append(us[l] if store else P.u_empty(l, P.nmax, dev))
             rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
             pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
                                    dtype=torch.uint8) if l < L - 1 else None)
@@ -746,7 +763,7 @@ class SdrStack(torch.autograd.Function):
                           workspace_bytes=rws[l].numel(), g_v=_ptr(g_vs[l]), carry=_ptr(carries[l]),
                           gu=_ptr(gus[l]), g0=0 if (gw_side and l == L - 1) else t0,
                           gn=T if (gw_side and l == L - 1) else P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
-                          g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1))
+                          g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1), u_bf16=int(P.ubf[l]))
 
         def run(sp, ls, ks, ev=None, gw=True):
             """backward of ranges (ls[i], ks[i]) of same-shaped layers, batched: LN
@@ -763,8 +780,8 @@ class SdrStack(torch.autograd.Function):
                                'capsnorm_bwd_range')
             if live:
                 if not store:
-                    _sdr_call(L_.srf_route_sdr_pose_n, live, B, T, N, din, P.lpad, P.rpad, J, D, int(P.pose_fp8), sp,
-                              what='sdr_pose_n')
+                    _sdr_call(L_.srf_route_sdr_pose_n, live, B, T, N, din, P.lpad, P.rpad, J, D, P.pose_mode(ls[0]),
+                              sp, what='sdr_pose_n')
                 _sdr_call(L_.srf_route_sdr_recur_bwd_n, live, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
                           what='sdr_recur_bwd_n')
                 _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')

@@ -194,3 +194,55 @@ def test_route_sdr_gemm_families(cuda, case, mf, monkeypatch):
     monkeypatch.setenv('SRF_SDR_MFMA32', mf)
     _check_forward(case, cuda)
     _check_backward(case, cuda)
+
+
+@pytest.mark.parametrize('J,D,iters,mf', [(16, 64, 5, False), (32, 64, 3, True)])
+def test_sdr_stream_bf16_u_equals_fp32(cuda, J, D, iters, mf):
+    """The streaming recurrence reading u stored in bf16 (the fp8 C5 variant) computes
+    exactly what the fp32 kernels compute from the same, bf16-representable u:
+    forward v, couplings and backward gu / carry to fp32 rounding (the widening is
+    exact).  And the fp8 pose storing bf16 (pose_n mode 2) writes the fp32-output
+    fp8 pose (mode 1) rounded to nearest even."""
+    import ctypes
+    from srf_amd import _lib
+    L = _lib.lib()
+    B, T, N, lp, rp = 2, 5, 8, 4, 4
+    in_n, JD = N * (lp + rp + 1), J * D
+    rng = torch.Generator().manual_seed(5)
+    u32 = (torch.randn(B * T * in_n * JD, generator=rng) * 0.3).to(torch.bfloat16)
+    u16 = u32.to(cuda)
+    u32 = u32.float().to(cuda)
+    ncs = L.srf_route_sdr_coupling_floats(in_n, J, D, iters)
+    ws_n = L.srf_route_sdr_recur_workspace(B, in_n, J, D, iters)
+    assert ncs > 0 and L.srf_route_sdr_couplings_required(in_n, J, D, iters)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    g_v = torch.randn(B, T, JD, generator=rng).to(cuda)
+    outs = []
+    for u, bf in ((u32, 0), (u16, 1)):
+        v = torch.zeros(B, T, JD, device=cuda)
+        cs = torch.zeros(B * T * ncs, device=cuda)
+        ws = torch.zeros(max(ws_n // 4, 4), device=cuda)
+        r = _lib.SdrRange(t0=0, t1=T, u=p(u), v0=0, vn=T, v=p(v), couplings=p(cs), workspace=p(ws),
+                          workspace_bytes=ws.numel() * 4, u_bf16=bf)
+        _lib.check(L.srf_route_sdr_recur_fwd_n((_lib.SdrRange * 1)(r), 1, B, T, in_n, J, D, iters, int(mf), st), 'fwd')
+        gu = torch.zeros(B * T * in_n * JD, device=cuda)
+        carry = torch.zeros(B, JD, device=cuda)
+        r.g_v, r.carry, r.gu, r.g0, r.gn = p(g_v), p(carry), p(gu), 0, T
+        _lib.check(L.srf_route_sdr_recur_bwd_n((_lib.SdrRange * 1)(r), 1, B, T, in_n, J, D, iters, int(mf), st), 'bwd')
+        torch.cuda.synchronize()
+        outs.append((v, cs, gu, carry))
+    for a, b in zip(*outs):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max().item()
+    # pose_n mode 2 == mode 1 rounded to bf16
+    din = 64
+    emb = torch.randn(B, T, N, din, generator=rng).to(cuda)
+    W = (torch.randn(in_n, JD, din, generator=rng) * 0.1).to(cuda)
+    bias = (torch.randn(in_n, JD, generator=rng) * 0.1).to(cuda)
+    uf = torch.zeros(B * T * in_n * JD, device=cuda)
+    ub = torch.zeros(B * T * in_n * JD, device=cuda, dtype=torch.bfloat16)
+    for buf, mode in ((uf, 1), (ub, 2)):
+        r = _lib.SdrRange(t0=0, t1=T, emb=p(emb), W=p(W), bias=p(bias), u=p(buf), v0=0, vn=T, u_bf16=int(mode == 2))
+        _lib.check(L.srf_route_sdr_pose_n((_lib.SdrRange * 1)(r), 1, B, T, N, din, lp, rp, J, D, mode, st), 'pose')
+    torch.cuda.synchronize()
+    assert torch.equal(uf.to(torch.bfloat16), ub)
