@@ -38,6 +38,15 @@ namespace {
 using srf_seq::group_max;
 using srf_seq::group_sum;
 
+// Forward ring depths (A/B builds, scripts/build_ab.sh + gpu_lib_ab_c5.sh, C5 step:
+// (6, 3) 990 ms, (6, 2) 959, (6, 1) 955, (3, 2) 951, (2, 3) 980, (8, 3) 1065, (6, 4)
+// 1131): deeper rings only add register pressure once the eight layers share HBM
+#ifndef SRF_STREAM_PDF16
+#define SRF_STREAM_PDF16 3
+#endif
+#ifndef SRF_STREAM_PDF32
+#define SRF_STREAM_PDF32 2
+#endif
 constexpr int kNT = 512;          // threads per workgroup (two waves per SIMD, 256 VGPRs each)
 constexpr int kNW = kNT / 64;
 constexpr int kRM = 5;            // iteration bound (check_sgeom)
@@ -52,7 +61,7 @@ struct SC {
   static constexpr int RQ = D / KD;           // lanes per output capsule
   static constexpr int NE = JD / kNT;         // elements per thread in the element phases
   // capsules in flight per wave in the forward / backward register ring
-  static constexpr int PDF = KD <= 8 ? 8 : KD <= 16 ? 6 : 3;
+  static constexpr int PDF = KD <= 8 ? 8 : KD <= 16 ? SRF_STREAM_PDF16 : SRF_STREAM_PDF32;
   static constexpr int PDB = KD <= 16 ? 4 : 2;
   static constexpr int HD = 8;                 // gu outputs per lane per sub-pass (registers: 2R*HD)
   static_assert(D % KD == 0 && NE >= 1 && KD % 4 == 0 && KD % HD == 0, "unsupported stream shape");
