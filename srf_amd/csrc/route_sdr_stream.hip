@@ -47,6 +47,12 @@ using srf_seq::group_sum;
 #ifndef SRF_STREAM_PDF32
 #define SRF_STREAM_PDF32 2
 #endif
+#ifndef SRF_STREAM_PDB16   // backward ring depths
+#define SRF_STREAM_PDB16 4
+#endif
+#ifndef SRF_STREAM_PDB32
+#define SRF_STREAM_PDB32 2
+#endif
 constexpr int kNT = 512;          // threads per workgroup (two waves per SIMD, 256 VGPRs each)
 constexpr int kNW = kNT / 64;
 constexpr int kRM = 5;            // iteration bound (check_sgeom)
@@ -62,7 +68,7 @@ struct SC {
   static constexpr int NE = JD / kNT;         // elements per thread in the element phases
   // capsules in flight per wave in the forward / backward register ring
   static constexpr int PDF = KD <= 8 ? 8 : KD <= 16 ? SRF_STREAM_PDF16 : SRF_STREAM_PDF32;
-  static constexpr int PDB = KD <= 16 ? 4 : 2;
+  static constexpr int PDB = KD <= 16 ? SRF_STREAM_PDB16 : SRF_STREAM_PDB32;
   static constexpr int HD = 8;                 // gu outputs per lane per sub-pass (registers: 2R*HD)
   static_assert(D % KD == 0 && NE >= 1 && KD % 4 == 0 && KD % HD == 0, "unsupported stream shape");
 };
