@@ -1729,10 +1729,13 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   return SRF_OK;
 }
 
-// SRF_XCD_REMAP=0: the plain block order (A/B)
+// Opt-in (SRF_XCD_REMAP=1).  Measured: C4 step 10.12 -> 10.10 ms (noise level), but the
+// layer-6 pass fetches 146 instead of 104 MB per launch (PMC): in the plain order
+// the dispatcher already gives each XCD one or two i-chunks of every frame tile,
+// i.e. a quarter of W (2.6 MB, L2-resident), which beats sharing the Vc rows.
 static bool xcd_remap() {
   const char* e = getenv("SRF_XCD_REMAP");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 static int xcd_grid(int nwg) { return xcd_remap() ? (nwg + kXcds - 1) / kXcds * kXcds : nwg; }
 static Args32 xcd_args(Args32 a, const Fwd32Plan& p) {
