@@ -1019,9 +1019,23 @@ int recur_fwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
   return SRF_OK;
 }
 
+// SRF_SDR_BWD_STREAM=1 (A/B): register-path layers whose stored couplings have the
+// streaming layout too (J a power of two, record sizes equal) run the streaming backward
+bool bwd_stream(const SGeom& g) {
+  const char* e = getenv("SRF_SDR_BWD_STREAM");   // 1: every such layer, 2: J*dout >= 1024 only
+  if (!(e && (e[0] == '1' || (e[0] == '2' && g.J * g.dout >= 1024)))) return false;
+  const int in_n = g.in_n();
+  if (!srf::sdr_seq_supported(in_n, g.J, g.dout, g.iters) || !srf::sdr_stream_supported(in_n, g.J, g.dout, g.iters))
+    return false;
+  return (g.J & (g.J - 1)) == 0 &&
+         srf::sdr_seq_cs_floats(in_n, g.J, g.dout, g.iters) == srf::sdr_stream_cs_floats(in_n, g.J, g.dout, g.iters);
+}
+
 int recur_bwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
   if (it.n == 0) return SRF_OK;
   if (int rc = u_type_ok(g, it)) return rc;
+  if (bwd_stream(g) && it.it[0].cs && it.it[0].ws)
+    return srf::sdr_stream_bwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, st);
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_seq_bwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, st);
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
@@ -1048,6 +1062,7 @@ srf::SeqItems one_seq_item(const srf::SeqItem& I) {
 }
 
 size_t recur_workspace(const SGeom& g) {
+  if (bwd_stream(g)) return srf::sdr_stream_workspace_floats(g.B, g.in_n(), g.J, g.dout, g.iters) * sizeof(float);
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters)) return 0;
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_stream_workspace_floats(g.B, g.in_n(), g.J, g.dout, g.iters) * sizeof(float);
