@@ -862,6 +862,216 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
   }
 }
 
+// gu pass from stored couplings on 32x32x16 split-fp16 MFMA (din 32, dout 32: the
+// C3 / C4 DR layers).  gx^T[e][f] = sum_row W^T[e][row] gu[row][f] with
+//   * W' = 2^aw W (the forward's exponent, prep header hdr[1]) and gu' = 2^eg gu, eg
+//     one exponent per (wave, capsule, frame) from the frame's max |gu| over the
+//     wave's 32 rows, so max|W'|, max|gu'| < 2^14;
+//   * a' = a1 + a2 (fp16 each) and the tile W1 gu1 + W1 gu2 + W2 gu1 (the dropped
+//     W2 gu2 <= 2^-22 |W' gu'|), three MFMAs per 16-row K step, products exact in fp32;
+//   * the result scaled back by the exact 2^-(aw+eg) of the lane's frame column.
+// A workgroup = 32 frames x 4 waves x 32 rows (one output capsule j per wave) x an
+// n-chunk; lane l holds frame l & 31 and rows 8(l >> 5) + 0..7 of each K step (the
+// MFMA's B map), and the rows 8q + 4(l >> 5) + 0..3 of e in its C map.  The window
+// adjoint goes through per-wave LDS slabs [31 + window][n_per*32 + 4] (row stride 4
+// mod 32: conflict-free ds_read_b128 / ds_write_b128 for every window offset) and is
+// flushed into g_emb by one atomic add per element, as in route_gux_kernel.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+constexpr int kGux16NW = 4;
+
+__device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int R>
+__global__ __launch_bounds__(256, 2) void route_gux16_kernel(
+    const float* __restrict__ WT, const float* __restrict__ hdr, int F, int T, int N, int lpad, int in_n, int J,
+    int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
+    const float* __restrict__ gs, float* __restrict__ g_emb, const float* __restrict__ cst,
+    const float* __restrict__ glst, int JP) {
+  static_assert(R >= 2, "stored couplings exist for iters >= 2");
+  constexpr int DIN = 32, RV = R - 1, NW = kGux16NW;
+  extern __shared__ __attribute__((aligned(16))) float gacc[];
+  const int JD = J * DIN;
+  const int NT = JD / 16;
+  const size_t FJD = (size_t)F * JD;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int fl = lane & 31, h = lane >> 5;
+  const int chunk = blockIdx.x % n_chunks;
+  const int rest = blockIdx.x / n_chunks;
+  const int wgrp = rest % n_wgroups;
+  const int ft = rest / n_wgroups;
+  const int f = ft * 32 + fl;
+  const FrameLoc loc = frame_loc(f, F, T);
+  const int fv = loc.valid ? f : 0;
+  const bool wave_on = wgrp * NW + wv < J;
+  const int j = __builtin_amdgcn_readfirstlane(min(wgrp * NW + wv, J - 1));
+  const int n0 = chunk * n_per, nn = min(N, n0 + n_per) - n0;
+  const int Wn = in_n / N;
+  const int ncap = Wn * nn;
+  const int Jeff = J - (mask_first ? 1 : 0);
+  const int SROW = n_per * DIN + 4;
+  const int nslots = 31 + Wn;
+  float* slab = gacc + (size_t)wv * nslots * SROW;
+  for (int k = threadIdx.x; k < NW * nslots * SROW; k += blockDim.x) gacc[k] = 0.f;
+  __syncthreads();
+
+  // the lane's 16 rows j*32 + 16 ks + 8 h + 0..7 of gs^r (c^0 folded into gs^0) and Vc^r
+  const float c0 = (wave_on && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+  float gsr[R][16], vcr[RV][16];
+  {
+    const bool ok = loc.valid && wave_on;
+    auto rows = [&](const float* base, float (&o)[16]) {
+      const float* p = base + (size_t)fv * JD + j * DIN + 8 * h;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f4 a = ld4(p + 16 * ks + 4 * q);
+          o[8 * ks + 4 * q] = ok ? a.x : 0.f;
+          o[8 * ks + 4 * q + 1] = ok ? a.y : 0.f;
+          o[8 * ks + 4 * q + 2] = ok ? a.z : 0.f;
+          o[8 * ks + 4 * q + 3] = ok ? a.w : 0.f;
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      rows(gs + (size_t)r * FJD, gsr[r]);
+      if (r > 0) rows(saved + (size_t)(2 * (r - 1) + 1) * FJD, vcr[r - 1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) gsr[0][k] *= c0;
+  }
+  const int aw = (int)hdr[1];
+  const float sw = srf_exp2i(aw);
+  // W^T in fragment order [i][tile][row quad][e][4 rows]: K step ks of the wave is
+  // tile 2j + ks, the lane's rows 8h..8h+7 are quads 2h, 2h+1 at e = fl
+  const int Fs = srf::fwd32_frame_stride(F);
+  const uint32_t cblk_b = (uint32_t)in_n * JP * Fs * 4;
+  const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(WT), 0, (int)((size_t)in_n * NT * 16 * DIN * 4),
+                                                       0x00020000);
+  const auto rs_c = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cst), 0, (int)(cblk_b * RV), 0x00020000);
+  const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(glst), 0, (int)(cblk_b * RV), 0x00020000);
+  uint32_t wo[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) wo[ks][q] = (uint32_t)((((2 * j + ks) * 4 + 2 * h + q) * DIN + fl) * 16);
+  const uint32_t co = (uint32_t)(j * Fs + fv) * 4;
+  constexpr int NB = 3;
+  f4 wt_b[NB][2][2];
+  float c_b[NB][RV], g_b[NB][RV];
+  auto fetch = [&](auto slot, int i) {
+    constexpr int sl = decltype(slot)::value;
+    const uint32_t swo = (uint32_t)i * NT * 16 * DIN * 4;
+    const uint32_t sc = (uint32_t)i * JP * Fs * 4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        wt_b[sl][ks][q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs_w, wo[ks][q], swo, 0));
+#pragma unroll
+    for (int r = 0; r < RV; ++r) {
+      c_b[sl][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_c, co, sc + r * cblk_b, 0));
+      g_b[sl][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, co, sc + r * cblk_b, 0));
+    }
+  };
+  int w = 0, nl = 0, wf = 0, nf = 0;
+  auto advance = [&](int& ww, int& nn_) {
+    if (++nn_ == nn) nn_ = 0, ++ww;
+  };
+  auto compute = [&](auto slot) {
+    constexpr int sl = decltype(slot)::value;
+    float gu[16];
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      float a = gsr[0][k];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        a = fmaf(c_b[sl][r], gsr[r + 1][k], a);
+        a = fmaf(g_b[sl][r], vcr[r][k], a);
+      }
+      gu[k] = a;
+      m = fmaxf(m, fabsf(a));
+    }
+    float ma, mb;
+    xpair32(m, ma, mb);
+    const int eg = srf_split_exp(fmaxf(ma, mb));
+    const float sg = srf_exp2i(eg);
+    h8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        _Float16 a1, a2;
+        srf_split2h(gu[8 * ks + k] * sg, a1, a2);
+        bh[ks][k] = a1;
+        bl[ks][k] = a2;
+        srf_split2h(wt_b[sl][ks][k >> 2][k & 3] * sw, a1, a2);
+        ah[ks][k] = a1;
+        al[ks][k] = a2;
+      }
+    f16v acc = {};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      acc = mfma32h(ah[ks], bh[ks], acc);
+      acc = mfma32h(ah[ks], bl[ks], acc);
+      acc = mfma32h(al[ks], bh[ks], acc);
+    }
+    const float un = srf_exp2i(-(aw + eg));
+    const int ts = loc.t + w - lpad;
+    if (wave_on && loc.valid && ts >= 0 && ts < T) {
+      float* a = slab + (fl + w) * SROW + nl * DIN + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 v = {acc[4 * q] * un, acc[4 * q + 1] * un, acc[4 * q + 2] * un, acc[4 * q + 3] * un};
+        st4(a + 8 * q, ld4(a + 8 * q) + v);
+      }
+    }
+    advance(w, nl);
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  const int i_last = (Wn - 1) * N + n0 + nn - 1;
+  auto next_i = [&]() {
+    const int i = min(wf * N + n0 + nf, i_last);
+    advance(wf, nf);
+    return i;
+  };
+#define SRF_GUX16_FETCH(SL) \
+  fetch(SL{}, next_i());    \
+  __builtin_amdgcn_sched_barrier(0);
+  if (ncap > 0) {
+    SRF_GUX16_FETCH(S0)
+    SRF_GUX16_FETCH(S1)
+  }
+  for (int k = 0; k < ncap; k += NB) {
+    SRF_GUX16_FETCH(S2)
+    compute(S0{});
+    if (k + 1 >= ncap) break;
+    SRF_GUX16_FETCH(S0)
+    compute(S1{});
+    if (k + 2 >= ncap) break;
+    SRF_GUX16_FETCH(S1)
+    compute(S2{});
+  }
+#undef SRF_GUX16_FETCH
+  __syncthreads();
+  const int f0 = ft * 32 - lpad;
+  const int row = nn * DIN;
+  for (int k = threadIdx.x; k < nslots * row; k += blockDim.x) {
+    const int s = k / row, rem = k - s * row;
+    const int fo = f0 + s;
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots + s) * SROW + rem];
+    if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
+  }
+}
+
 // W [in_n][JD][din] -> WT [in_n][din][JD] (A operand of the gx contraction); the
 // same launch zeroes g_emb ([n_zero] floats), which the gu pass accumulates into.
 __global__ void transpose_w_kernel(const float* __restrict__ W, int in_n, int JD, int din, float* __restrict__ WT,
@@ -1351,6 +1561,233 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
   }
 }
 
+// gW pass on 32x32x16 split-fp16 MFMA (din = dout = 32; route_gux16_kernel's
+// scheme with K = frames): gW^T_i[e][row] = sum_f x_i^T[e][f] gu_i[f][row].
+//   * x' = 2^bx x (the forward's exponent, hdr[2]), split once per tile by the
+//     staging threads into fp16 hi / lo planes in LDS;
+//   * gu (formed from the per-frame vectors and the staged c^r / gL^r) scaled per
+//     row and 16-frame K step by 2^eg (the row's max |gu| over those frames), split;
+//   * three MFMAs per capsule and K step into a temporary tile that is added to the
+//     fp32 sum scaled back by 2^-(bx + eg) (the K steps carry different scales).
+// Workgroup = 4 waves x 32 rows (one output capsule j each) x CAP capsules x one of S
+// frame splits; lane l holds row 32j + (l & 31) and frames 8(l >> 5) + 0..7 of each
+// K step (B map), e = 8q + 4(l >> 5) + 0..3 of its C map.  Tile t + 1 is staged while
+// tile t computes (one barrier per tile), the per-frame vectors one tile ahead.
+// LDS x planes: row e = 16 halves = two 8-half chunks, chunk c of row e at
+// c ^ ((e >> 3) & 1): the ds_read_b128 lane groups then cover 64 distinct banks.
+constexpr int kGw16Cap = 4;
+template <int R, int CAP>
+__global__ __launch_bounds__(256, 2) void route_gw16_kernel(
+    const float* __restrict__ xT, const float* __restrict__ hdr, const float* __restrict__ saved,
+    const float* __restrict__ gs, const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp,
+    int in_n, int J, int mask_first, int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp,
+    float* __restrict__ gbp, size_t pstride) {
+  static_assert(R >= 2, "stored couplings exist for iters >= 2");
+  constexpr int D = 32, RV = R - 1;
+  constexpr int CG = RV * 2 * 4 * 16;    // couplings per capsule: [r][c|gl][4 j][16 frames] floats
+  constexpr int PQ = CG / 4 + D * 4;     // float4 staged per capsule (couplings + x^T [e][16])
+  constexpr int PCB = CG * 4 + 2 * D * 16 * 2;   // LDS bytes per capsule: couplings, x hi, x lo
+  constexpr int NQ = (CAP * PQ + 255) / 256;
+  __shared__ __attribute__((aligned(16))) unsigned char stg[2][CAP * PCB];
+  const int JD = J * D;
+  const size_t FJD = (size_t)F * JD;
+  const int Fs = srf::fwd32_frame_stride(F);
+  const size_t cblk = (size_t)in_n * JP * Fs;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = lane & 31, h = lane >> 5;
+  int b = blockIdx.x;
+  const int s = b % S;
+  b /= S;
+  const int rtg = b % n_rt;
+  const int cc = b / n_rt;
+  const int jw = rtg * 4 + wv;
+  const bool wave_on = jw < J;
+  const int j = min(jw, J - 1);
+  const int row = j * D + n;
+  const int Jeff = J - (mask_first ? 1 : 0);
+  const float c0 = (wave_on && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+  const int i0 = cc * CAP, ncap = min(in_n, i0 + CAP) - i0;
+  const int NFT = Fp >> 4;
+  const int ft0 = s * ft_per, ft1 = min(NFT, ft0 + ft_per);
+  const int bx = (int)hdr[2];
+  const float sx = srf_exp2i(bx);
+
+  // staging: float4 q of a tile <-> (capsule k, part): couplings (r, c|gl, jw, frame
+  // quad) or x^T (e, frame quad); per-thread sources fixed, tile t + 1 is 16 floats on
+  const float* src[NQ];
+  int dst[NQ];     // LDS byte offset; x parts: of the hi plane (lo = + D*16*2)
+  bool isx[NQ];
+  // the CAP * CG / 4 coupling float4s first, then the x^T ones: at RV = 2, CAP = 4 each
+  // thread's q = 0 is a coupling and q >= 1 an x^T float4 (no branch in stage_store)
+  constexpr int NCPL = CAP * CG / 4;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int idx = min(q * 256 + (int)threadIdx.x, CAP * PQ - 1);
+    if (idx < NCPL) {
+      const int k = idx / (CG / 4), rem = idx - k * (CG / 4);
+      const int i = i0 + min(k, ncap - 1);
+      const int fq = rem & 3, jq = (rem >> 2) & 3, cg = rem >> 4;   // cg = r * 2 + (0: c, 1: gL)
+      const int jj = min(rtg * 4 + jq, JP - 1);
+      src[q] = ((cg & 1) ? glst : cst) + (size_t)(cg >> 1) * cblk + ((size_t)i * JP + jj) * Fs + 4 * fq;
+      dst[q] = k * PCB + rem * 16;
+      isx[q] = false;
+    } else {
+      const int x = idx - NCPL, k = x / (D * 4), xr = x - k * (D * 4), e = xr >> 2, fq = xr & 3;
+      const int i = i0 + min(k, ncap - 1);
+      src[q] = xT + ((size_t)i * D + e) * Fp + 4 * fq;
+      dst[q] = k * PCB + CG * 4 + (e * 16 + (((fq >> 1) ^ ((e >> 3) & 1)) * 8) + (fq & 1) * 4) * 2;
+      isx[q] = true;
+    }
+  }
+  f4 sv[NQ];
+  auto stage_load = [&](int ft) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) sv[q] = ld4(src[q] + ft * 16);
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int idx = q * 256 + threadIdx.x;
+      if ((CAP * PQ) % 256 != 0 && idx >= CAP * PQ) continue;
+      unsigned char* p = &stg[buf][dst[q]];
+      const bool xq = q * 256 >= NCPL ? true : (q + 1) * 256 <= NCPL ? false : isx[q];
+      if (xq) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 a, c;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          _Float16 a1, a2;
+          srf_split2h(sv[q][v] * sx, a1, a2);
+          a[v] = a1;
+          c[v] = a2;
+        }
+        *reinterpret_cast<h4*>(p) = a;
+        *reinterpret_cast<h4*>(p + D * 16 * 2) = c;
+      } else {
+        *reinterpret_cast<f4*>(p) = sv[q];
+      }
+    }
+  };
+  // per-frame vectors of the lane's row, frames 8h + 0..7 of a tile: buffer loads, 0 past F
+  const uint32_t nrec = (uint32_t)(FJD * 4);
+  __amdgpu_buffer_rsrc_t rs_g[R], rs_v[RV];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    rs_g[r] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gs + (size_t)r * FJD), 0, (int)nrec, 0x00020000);
+    if (r > 0)
+      rs_v[r - 1] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(saved + (size_t)(2 * (r - 1) + 1) * FJD), 0,
+                                                      (int)nrec, 0x00020000);
+  }
+  const uint32_t vo0 = (uint32_t)((8 * h) * JD + row) * 4;
+  float nx[R + RV][8];
+  auto vec_load = [&](int ft) {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const uint32_t so = (uint32_t)((ft * 16 + v) * JD) * 4;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        nx[r][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g[r], vo0, so, 0));
+        if (r > 0) nx[R + r - 1][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_v[r - 1], vo0, so, 0));
+      }
+    }
+  };
+
+  f16v acc[CAP];
+  float gb[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    gb[k] = 0.f;
+    acc[k] = f16v{};
+  }
+  if (ft0 < ft1) {
+    stage_load(ft0);
+    vec_load(ft0);
+    stage_store(0);
+    if (ft0 + 1 < ft1) stage_load(ft0 + 1);
+  }
+  const int xoff = CG * 4 + (n * 16 + ((h ^ ((n >> 3) & 1)) * 8)) * 2;
+  for (int ft = ft0; ft < ft1; ++ft) {
+    const int buf = (ft - ft0) & 1;
+    float fv[R + RV][8];
+#pragma unroll
+    for (int a = 0; a < R + RV; ++a)
+#pragma unroll
+      for (int v = 0; v < 8; ++v) fv[a][v] = nx[a][v];
+    __syncthreads();   // tile ft staged in buf; buf ^ 1 (tile ft - 1) is free
+    if (ft + 1 < ft1) {
+      stage_store(buf ^ 1);
+      if (ft + 2 < ft1) stage_load(ft + 2);
+      vec_load(ft + 1);
+    }
+    const unsigned char* sb = stg[buf];
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) {
+      const unsigned char* ck = sb + k * PCB;
+      const float* ckf = reinterpret_cast<const float*>(ck);
+      float gu[8];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) gu[v] = c0 * fv[0][v];
+#pragma unroll
+      for (int r = 0; r < RV; ++r) {
+        const float* cp = ckf + ((r * 2 + 0) * 4 + wv) * 16 + 8 * h;
+        const float* gp = ckf + ((r * 2 + 1) * 4 + wv) * 16 + 8 * h;
+        const f4 ca = ld4(cp), cb = ld4(cp + 4), ga = ld4(gp), gbv = ld4(gp + 4);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          gu[v] = fmaf(ca[v], fv[r + 1][v], gu[v]);
+          gu[v] = fmaf(ga[v], fv[R + r][v], gu[v]);
+          gu[v + 4] = fmaf(cb[v], fv[r + 1][v + 4], gu[v + 4]);
+          gu[v + 4] = fmaf(gbv[v], fv[R + r][v + 4], gu[v + 4]);
+        }
+      }
+      float m = 0.f, sum = 0.f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        m = fmaxf(m, fabsf(gu[v]));
+        sum += gu[v];
+      }
+      gb[k] += sum;
+      float ma, mb;
+      xpair32(m, ma, mb);
+      const int eg = srf_split_exp(fmaxf(ma, mb));
+      const float sg = srf_exp2i(eg);
+      h8 bh, bl;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        _Float16 a1, a2;
+        srf_split2h(gu[v] * sg, a1, a2);
+        bh[v] = a1;
+        bl[v] = a2;
+      }
+      const h8 xh = *reinterpret_cast<const h8*>(ck + xoff);
+      const h8 xl = *reinterpret_cast<const h8*>(ck + xoff + D * 16 * 2);
+      f16v t = {};
+      t = mfma32h(xh, bh, t);
+      t = mfma32h(xh, bl, t);
+      t = mfma32h(xl, bh, t);
+      const float un = srf_exp2i(-(bx + eg));
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[k][v] = fmaf(t[v], un, acc[k][v]);
+      __builtin_amdgcn_sched_barrier(0);   // one capsule in flight at a time (registers)
+    }
+  }
+  float* gw = gwp + (size_t)s * pstride;
+  float* gbo = gbp + (size_t)s * pstride;
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    const float a = gb[k];
+    float pa, pb;
+    xpair32(a, pa, pb);
+    if (k >= ncap || !wave_on) continue;
+    const int i = i0 + k;
+    if (h == 0) gbo[(size_t)i * JD + row] = pa + pb;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      st4(gw + ((size_t)i * JD + row) * D + 8 * q + 4 * h,
+          f4{acc[k][4 * q], acc[k][4 * q + 1], acc[k][4 * q + 2], acc[k][4 * q + 3]});
+  }
+}
+
 // gW | gbias = sum of the S partial slabs (float4 per thread).
 __global__ void gw_reduce_kernel(const float* __restrict__ part, int S, size_t n4, size_t stride, float* __restrict__ gW,
                                  size_t nw4, float* __restrict__ gb) {
@@ -1553,10 +1990,57 @@ int gu_n_per(const Geom& g, int nw) {
   return best;
 }
 
+// route_gux16_kernel (split-fp16 32x32 tiles) for din = dout = 32 with stored
+// couplings; SRF_GUX16=0 keeps route_gux_kernel (A/B).
+inline bool use_gux16(const Geom& g) {
+  const char* e = getenv("SRF_GUX16");   // read per launch (tests toggle it)
+  return !(e && e[0] == '0') && g.din == 32 && g.dout == 32 && g.iters >= 2 && g.iters <= 4;   // R = 5 spills
+}
+inline size_t gux16_lds_bytes(const Geom& g, int n_per) {
+  return (size_t)kGux16NW * (31 + gu_window(g)) * (n_per * 32 + 4) * sizeof(float);
+}
+constexpr size_t kGux16LdsMax = 76 * 1024;   // two workgroups per CU
+// n-chunk size: fewest rounds of two workgroups per CU, then fewest capsules each
+int gux16_n_per(const Geom& g) {
+  const int base = (g.F() + 31) / 32 * ((g.J + kGux16NW - 1) / kGux16NW);
+  const int slots = 256 * 2;
+  int best = 1;
+  double best_cost = 1e30;
+  for (int n_per = 1; n_per <= g.N; ++n_per) {
+    if (n_per > 1 && gux16_lds_bytes(g, n_per) > kGux16LdsMax) break;
+    const int chunks = (g.N + n_per - 1) / n_per;
+    const int rounds = (base * chunks + slots - 1) / slots;
+    const double cost = (double)rounds * (gu_window(g) * n_per + 4);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = n_per;
+    }
+  }
+  return best;
+}
+
+template <int R>
+void launch_gux16(const Geom& g, const float* WT, const float* hdr, const float* saved, const float* gs,
+                  float* g_emb, const float* cst, const float* glst, int JP, hipStream_t st) {
+  const int n_wgroups = (g.J + kGux16NW - 1) / kGux16NW;
+  const int n_per = gux16_n_per(g);
+  const int n_chunks = (g.N + n_per - 1) / n_per;
+  const int grid = (g.F() + 31) / 32 * n_wgroups * n_chunks;
+  hipLaunchKernelGGL((route_gux16_kernel<R>), dim3(grid), dim3(64 * kGux16NW), gux16_lds_bytes(g, n_per), st, WT,
+                     hdr, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs,
+                     g_emb, cst, glst, JP);
+}
+
 template <int D, int R>
 void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
                const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st,
-               const float* cst, const float* glst, int JP) {
+               const float* cst, const float* glst, int JP, const float* hdr = nullptr) {
+  if constexpr (R >= 2 && D == 32) {
+    if (cst != nullptr && hdr != nullptr && use_gux16(g) && gux16_lds_bytes(g, 1) <= kGux16LdsMax) {
+      launch_gux16<R>(g, WT, hdr, saved, gs, g_emb, cst, glst, JP, st);
+      return;
+    }
+  }
   const int n_ftiles = (g.F() + 15) / 16;
   const int n_wgroups = gu_wgroups(g);
   constexpr int TW = gu_tw(D);
@@ -1588,13 +2072,13 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
 template <int D>
 void launch_gu_r(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
                  const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st,
-                 const float* cst = nullptr, const float* glst = nullptr, int JP = 0) {
+                 const float* cst = nullptr, const float* glst = nullptr, int JP = 0, const float* hdr = nullptr) {
   switch (g.iters) {
     case 1: launch_gu<D, 1>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, nullptr, nullptr, 0); break;
-    case 2: launch_gu<D, 2>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
-    case 3: launch_gu<D, 3>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
-    case 4: launch_gu<D, 4>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
-    default: launch_gu<D, 5>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP); break;
+    case 2: launch_gu<D, 2>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
+    case 3: launch_gu<D, 3>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
+    case 4: launch_gu<D, 4>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
+    default: launch_gu<D, 5>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
   }
 }
 
@@ -1626,16 +2110,24 @@ inline int gw3_cap(const Geom& g) {
   return v32;
 }
 
-Gw2Plan gw2_plan(const Geom& g) {
+// route_gw16_kernel (split-fp16 32x32 tiles) for din = dout = 32, iters 2..3 with
+// stored couplings, opt-in (SRF_GW16=1): at C4 it measured 9.81 against 9.68 ms per
+// step with route_gw3_kernel (276 vs 250 us per launch).
+inline bool use_gw16(const Geom& g) {
+  const char* e = getenv("SRF_GW16");   // read per launch (tests toggle it)
+  return (e && e[0] == '1') && g.din == 32 && g.dout == 32 && g.iters >= 2 && g.iters <= 3;
+}
+
+Gw2Plan gw2_plan_for(const Geom& g, bool g16) {
   Gw2Plan p{};
   const int NT = g.NT();
-  const int NCT = (g.din + 15) / 16;
-  p.n_rt = (NT + 3) / 4;
-  p.cap = gw3_cap(g) ? gw3_cap(g) : gw2_cap_rt(g.din);
+  const int NCT = g16 ? 2 : (g.din + 15) / 16;
+  p.n_rt = g16 ? (g.J + 3) / 4 : (NT + 3) / 4;
+  p.cap = g16 ? kGw16Cap : gw3_cap(g) ? gw3_cap(g) : gw2_cap_rt(g.din);
   // workgroups resident at once; route_gw3_kernel (latency-bound) is planned for two
   // resident rounds: at C4 S = 8 frame splits (1280 workgroups) beat S = 4 (640, one
-  // round) by 2 %, at C2 the slab term keeps S = 5
-  const int slots = gw3_cap(g) ? 2 * 768 : 512;
+  // round) by 2 %, at C2 the slab term keeps S = 5; route_gw16_kernel: two per CU
+  const int slots = g16 ? 2 * 512 : gw3_cap(g) ? 2 * 768 : 512;
   p.n_cc = (g.in_n() + p.cap - 1) / p.cap;
   const int NFT = padded_frames(g) / 16;
   p.pstride = (size_t)g.in_n() * g.JD() * (g.din + 1);
@@ -1658,11 +2150,33 @@ Gw2Plan gw2_plan(const Geom& g) {
   }
   return p;
 }
+Gw2Plan gw2_plan(const Geom& g) { return gw2_plan_for(g, use_gw16(g)); }
+// partial-slab floats for either gW kernel (the workspace must not depend on SRF_GW16)
+size_t gw2_part_floats(const Geom& g) {
+  size_t n = gw2_plan_for(g, false).S;
+  if (g.din == 32 && g.dout == 32) n = std::max(n, (size_t)gw2_plan_for(g, true).S);
+  return n * gw2_plan_for(g, false).pstride;
+}
 
 template <int D>
 int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* saved, const float* gs,
-               const float* cst, const float* glst, int JP, float* gwp, float* gbp, hipStream_t st) {
+               const float* cst, const float* glst, int JP, float* gwp, float* gbp, hipStream_t st,
+               const float* hdr = nullptr) {
   const int grid = p.n_rt * p.n_cc * p.S;
+  if constexpr (D == 32) {
+    if (hdr != nullptr && use_gw16(g) && p.cap == kGw16Cap) {
+      if (g.iters == 2)
+        hipLaunchKernelGGL((route_gw16_kernel<2, kGw16Cap>), dim3(grid), dim3(256), 0, st, xT, hdr, saved, gs, cst,
+                           glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp,
+                           gbp, p.pstride);
+      else
+        hipLaunchKernelGGL((route_gw16_kernel<3, kGw16Cap>), dim3(grid), dim3(256), 0, st, xT, hdr, saved, gs, cst,
+                           glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp,
+                           gbp, p.pstride);
+      SRF_LAUNCH_CHECK("route_gw16");
+      return SRF_OK;
+    }
+  }
   if constexpr (D <= 32) {
     if (gw3_cap(g)) {
 #define SRF_GW3(R_, C_)                                                                                           \
@@ -1815,8 +2329,7 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
     const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
     op32 = take((srf::fwd32_scratch_bytes(plan) + 3) / 4);
     ogl = take((size_t)std::max(g.iters - 1, 1) * srf::fwd32_frame_stride(g.F()) * in_n * (plan.JDp / g.dout));
-    const Gw2Plan gp = gw2_plan(g);
-    ogwp = take(gp.S * gp.pstride);
+    ogwp = take(gw2_part_floats(g));
   }
   char* b = static_cast<char*>(base);
   BwdWs w;
@@ -1851,7 +2364,7 @@ int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias,
     float* gwp = direct ? g_W : w.gwpart;
     float* gbp = direct ? g_bias : w.gwpart + (size_t)g.in_n() * g.JD() * g.din;
     int rc = launch_gw2<D>(g, p, couplings + cl.xT, saved, w.gs, couplings + cl.c, w.gl, plan.JDp / g.dout, gwp, gbp,
-                           st);
+                           st, srf::fwd32_hdr(plan, couplings + cl.planes));
     if (rc || direct) return rc;
     const size_t nw4 = (size_t)g.in_n() * g.JD() * g.din / 4, n4 = p.pstride / 4;
     hipLaunchKernelGGL(gw_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, w.gwpart, p.S, n4, p.pstride, g_W,
@@ -1931,7 +2444,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   }
   if (p32)
     launch_gu_r<D>(g, emb, W, couplings + cl.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st, couplings + cl.c,
-                   w.gl, plan.JDp / g.dout);
+                   w.gl, plan.JDp / g.dout, srf::fwd32_hdr(plan, couplings + cl.planes));
   else
     launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");

@@ -41,6 +41,8 @@ size_t fwd32_split_bytes(const Fwd32Plan& p);   // logits / partials / logZ of t
 size_t fwd32_workspace(const Fwd32Plan& p);   // planes + scratch + split
 size_t fwd32_lds(const Fwd32Plan& p);
 float* fwd32_slab(const Fwd32Plan& p, void* scratch);
+// the planes' scale header {2^-(aw+bx), aw, bx} (written by fwd32_prepare)
+const float* fwd32_hdr(const Fwd32Plan& p, const void* planes);
 // split W / emb into scaled fp16 planes, bias into bf16 planes, and the i-chunk bias
 // sums (two launches per forward: absmax, prep);
 // WT / xT (nullable): also the fp32 W^T [in_n][din][JD] and window^T [in_n][din][Fp]

@@ -1669,6 +1669,9 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   return p;
 }
 
+const float* fwd32_hdr(const Fwd32Plan& p, const void* planes) {
+  return reinterpret_cast<const float*>(static_cast<const char*>(planes) + p.ws_w + p.ws_b + p.ws_x);
+}
 size_t fwd32_planes_bytes(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x + p.ws_h; }
 size_t fwd32_scratch_bytes(const Fwd32Plan& p) { return p.ws_bsum + p.ws_slab; }
 size_t fwd32_split_bytes(const Fwd32Plan& p) { return p.split ? p.ws_lg + p.ws_part + p.ws_lz : 0; }
