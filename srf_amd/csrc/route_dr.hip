@@ -944,33 +944,32 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
     for (int k = 0; k < 16; ++k) gsr[0][k] *= c0;
   }
   const int aw = (int)hdr[1];
-  const float sw = srf_exp2i(aw);
-  // W^T in fragment order [i][tile][row quad][e][4 rows]: K step ks of the wave is
-  // tile 2j + ks, the lane's rows 8h..8h+7 are quads 2h, 2h+1 at e = fl
+  // split W^T planes (prep32_kernel, wt16) [i][tile][h][e][8 rows] hi, then lo: K step
+  // ks of the wave is tile 2j + ks, the lane's 16 bytes sit at (h, e = fl)
   const int Fs = srf::fwd32_frame_stride(F);
   const uint32_t cblk_b = (uint32_t)in_n * JP * Fs * 4;
-  const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(WT), 0, (int)((size_t)in_n * NT * 16 * DIN * 4),
-                                                       0x00020000);
+  const uint32_t wplane = (uint32_t)in_n * NT * 16 * DIN * 2;   // bytes per plane
+  const auto rs_w = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(WT), 0, (int)(2 * wplane), 0x00020000);
   const auto rs_c = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cst), 0, (int)(cblk_b * RV), 0x00020000);
   const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(glst), 0, (int)(cblk_b * RV), 0x00020000);
   uint32_t wo[2][2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) wo[ks][q] = (uint32_t)((((2 * j + ks) * 4 + 2 * h + q) * DIN + fl) * 16);
+    for (int p = 0; p < 2; ++p) wo[ks][p] = (uint32_t)((((2 * j + ks) * 2 + h) * DIN + fl) * 16) + p * wplane;
   const uint32_t co = (uint32_t)(j * Fs + fv) * 4;
   constexpr int NB = 3;
-  f4 wt_b[NB][2][2];
+  h8 wt_b[NB][2][2];   // [slot][ks][hi | lo]
   float c_b[NB][RV], g_b[NB][RV];
   auto fetch = [&](auto slot, int i) {
     constexpr int sl = decltype(slot)::value;
-    const uint32_t swo = (uint32_t)i * NT * 16 * DIN * 4;
+    const uint32_t swo = (uint32_t)i * NT * 16 * DIN * 2;
     const uint32_t sc = (uint32_t)i * JP * Fs * 4;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        wt_b[sl][ks][q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs_w, wo[ks][q], swo, 0));
+      for (int p = 0; p < 2; ++p)
+        wt_b[sl][ks][p] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs_w, wo[ks][p], swo, 0));
 #pragma unroll
     for (int r = 0; r < RV; ++r) {
       c_b[sl][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_c, co, sc + r * cblk_b, 0));
@@ -1000,7 +999,7 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
     xpair32(m, ma, mb);
     const int eg = srf_split_exp(fmaxf(ma, mb));
     const float sg = srf_exp2i(eg);
-    h8 ah[2], al[2], bh[2], bl[2];
+    h8 bh[2], bl[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -1009,16 +1008,13 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
         srf_split2h(gu[8 * ks + k] * sg, a1, a2);
         bh[ks][k] = a1;
         bl[ks][k] = a2;
-        srf_split2h(wt_b[sl][ks][k >> 2][k & 3] * sw, a1, a2);
-        ah[ks][k] = a1;
-        al[ks][k] = a2;
       }
     f16v acc = {};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      acc = mfma32h(ah[ks], bh[ks], acc);
-      acc = mfma32h(ah[ks], bl[ks], acc);
-      acc = mfma32h(al[ks], bh[ks], acc);
+      acc = mfma32h(wt_b[sl][ks][0], bh[ks], acc);
+      acc = mfma32h(wt_b[sl][ks][0], bl[ks], acc);
+      acc = mfma32h(wt_b[sl][ks][1], bh[ks], acc);
     }
     const float un = srf_exp2i(-(aw + eg));
     const int ts = loc.t + w - lpad;
@@ -1390,11 +1386,34 @@ __global__ __launch_bounds__(256) void route_gw2_kernel(
 //   * at most 168 registers, so three workgroups share a CU.
 // The stored couplings and logit gradients are 0 for frames past F (the 32x32
 // passes store zeros there) and x^T is 0 past F, so gu is 0 on padded frames.
+// gW workgroup order.  Plain: frame split fastest, then row group, then capsule chunk.
+// xcd (SRF_GW_XCD=1): the capsule chunks of one (row group, frame split) -- which read
+// the same per-frame vectors -- are consecutive in a per-XCD range of the logical
+// order (dispatch places block b on XCD b % 8, a speed-only assumption), so they run
+// together behind one L2.
+__device__ __forceinline__ void gw_block(int xcd, int S, int n_rt, int& s, int& rtg, int& cc) {
+  int L = blockIdx.x;
+  if (xcd) {
+    const int nb = gridDim.x, per = nb / 8;
+    if (L < per * 8) L = (L % 8) * per + L / 8;
+    const int ncc = nb / (S * n_rt);
+    cc = L % ncc;
+    L /= ncc;
+    s = L % S;
+    rtg = L / S;
+  } else {
+    s = L % S;
+    L /= S;
+    rtg = L % n_rt;
+    cc = L / n_rt;
+  }
+}
+
 template <int D, int R, int CAP>
 __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_kernel(
     const float* __restrict__ xT, const float* __restrict__ saved, const float* __restrict__ gs,
     const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp, int in_n, int J, int mask_first,
-    int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride) {
+    int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride, int xcd) {
   static_assert(R >= 2, "stored couplings exist for iters >= 2");
   constexpr int NCT = (D + 15) / 16;
   constexpr int RV = R - 1;
@@ -1419,11 +1438,8 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
   const size_t cblk = (size_t)in_n * JP * Fs;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l16 = lane & 15, kk = lane >> 4;
-  int b = blockIdx.x;
-  const int s = b % S;
-  b /= S;
-  const int rtg = b % n_rt;
-  const int cc = b / n_rt;
+  int s, rtg, cc;
+  gw_block(xcd, S, n_rt, s, rtg, cc);
   const int tg = rtg * 4 + wv;
   const int row = min(tg * 16 + l16, JD - 1);
   const bool rvalid = tg < NT && tg * 16 + l16 < JD;
@@ -1581,7 +1597,7 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
     const float* __restrict__ xT, const float* __restrict__ hdr, const float* __restrict__ saved,
     const float* __restrict__ gs, const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp,
     int in_n, int J, int mask_first, int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp,
-    float* __restrict__ gbp, size_t pstride) {
+    float* __restrict__ gbp, size_t pstride, int xcd) {
   static_assert(R >= 2, "stored couplings exist for iters >= 2");
   constexpr int D = 32, RV = R - 1;
   constexpr int CG = RV * 2 * 4 * 16;    // couplings per capsule: [r][c|gl][4 j][16 frames] floats
@@ -1595,11 +1611,8 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
   const size_t cblk = (size_t)in_n * JP * Fs;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n = lane & 31, h = lane >> 5;
-  int b = blockIdx.x;
-  const int s = b % S;
-  b /= S;
-  const int rtg = b % n_rt;
-  const int cc = b / n_rt;
+  int s, rtg, cc;
+  gw_block(xcd, S, n_rt, s, rtg, cc);
   const int jw = rtg * 4 + wv;
   const bool wave_on = jw < J;
   const int j = min(jw, J - 1);
@@ -1990,16 +2003,19 @@ int gu_n_per(const Geom& g, int nw) {
   return best;
 }
 
-// route_gux16_kernel (split-fp16 32x32 tiles) for din = dout = 32 with stored
-// couplings; SRF_GUX16=0 keeps route_gux_kernel (A/B).
-inline bool use_gux16(const Geom& g) {
-  const char* e = getenv("SRF_GUX16");   // read per launch (tests toggle it)
-  return !(e && e[0] == '0') && g.din == 32 && g.dout == 32 && g.iters >= 2 && g.iters <= 4;   // R = 5 spills
-}
 inline size_t gux16_lds_bytes(const Geom& g, int n_per) {
   return (size_t)kGux16NW * (31 + gu_window(g)) * (n_per * 32 + 4) * sizeof(float);
 }
 constexpr size_t kGux16LdsMax = 76 * 1024;   // two workgroups per CU
+// route_gux16_kernel (split-fp16 32x32 tiles) for din = dout = 32 with stored
+// couplings; SRF_GUX16=0 keeps route_gux_kernel (A/B).  Read by the forward too: its
+// prep then writes the kernel's split W^T planes in place of the fp32 W^T, so the
+// switch must not change between a layer's forward and backward.
+inline bool use_gux16(const Geom& g) {
+  const char* e = getenv("SRF_GUX16");   // read per launch (tests toggle it)
+  return !(e && e[0] == '0') && g.din == 32 && g.dout == 32 && g.iters >= 2 && g.iters <= 4 &&   // R = 5 spills
+         gux16_lds_bytes(g, 1) <= kGux16LdsMax;
+}
 // n-chunk size: fewest rounds of two workgroups per CU, then fewest capsules each
 int gux16_n_per(const Geom& g) {
   const int base = (g.F() + 31) / 32 * ((g.J + kGux16NW - 1) / kGux16NW);
@@ -2036,7 +2052,7 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
                const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st,
                const float* cst, const float* glst, int JP, const float* hdr = nullptr) {
   if constexpr (R >= 2 && D == 32) {
-    if (cst != nullptr && hdr != nullptr && use_gux16(g) && gux16_lds_bytes(g, 1) <= kGux16LdsMax) {
+    if (cst != nullptr && hdr != nullptr && use_gux16(g)) {
       launch_gux16<R>(g, WT, hdr, saved, gs, g_emb, cst, glst, JP, st);
       return;
     }
@@ -2151,6 +2167,10 @@ Gw2Plan gw2_plan_for(const Geom& g, bool g16) {
   return p;
 }
 Gw2Plan gw2_plan(const Geom& g) { return gw2_plan_for(g, use_gw16(g)); }
+inline int gw_xcd() {
+  const char* e = getenv("SRF_GW_XCD");
+  return (e && e[0] == '1') ? 1 : 0;
+}
 // partial-slab floats for either gW kernel (the workspace must not depend on SRF_GW16)
 size_t gw2_part_floats(const Geom& g) {
   size_t n = gw2_plan_for(g, false).S;
@@ -2168,11 +2188,11 @@ int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* sa
       if (g.iters == 2)
         hipLaunchKernelGGL((route_gw16_kernel<2, kGw16Cap>), dim3(grid), dim3(256), 0, st, xT, hdr, saved, gs, cst,
                            glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp,
-                           gbp, p.pstride);
+                           gbp, p.pstride, gw_xcd());
       else
         hipLaunchKernelGGL((route_gw16_kernel<3, kGw16Cap>), dim3(grid), dim3(256), 0, st, xT, hdr, saved, gs, cst,
                            glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp,
-                           gbp, p.pstride);
+                           gbp, p.pstride, gw_xcd());
       SRF_LAUNCH_CHECK("route_gw16");
       return SRF_OK;
     }
@@ -2181,7 +2201,8 @@ int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* sa
     if (gw3_cap(g)) {
 #define SRF_GW3(R_, C_)                                                                                           \
   hipLaunchKernelGGL((route_gw3_kernel<D, R_, C_>), dim3(grid), dim3(256), 0, st, xT, saved, gs, cst, glst, g.F(), \
-                     padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride)
+                     padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride, \
+                     gw_xcd())
 #define SRF_GW3C(R_) \
   if (p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, 8);
       switch (g.iters) {   // gw3_cap() is 0 past 3 iterations
@@ -2269,7 +2290,7 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
       scratch = static_cast<char*>(static_cast<void*>(slab)) + srf::fwd32_planes_bytes(plan);
     }
     const int rc = srf::fwd32_prepare(plan, emb, W, bias, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, planes,
-                                      scratch, WT, xT, st);
+                                      scratch, WT, xT, st, WT != nullptr && use_gux16(g));
     if (rc) return rc;
   } else {
     const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;

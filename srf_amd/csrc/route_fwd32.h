@@ -46,10 +46,11 @@ const float* fwd32_hdr(const Fwd32Plan& p, const void* planes);
 // split W / emb into scaled fp16 planes, bias into bf16 planes, and the i-chunk bias
 // sums (two launches per forward: absmax, prep);
 // WT / xT (nullable): also the fp32 W^T [in_n][din][JD] and window^T [in_n][din][Fp]
-// operands of the backward gx / gW contractions
+// operands of the backward gx / gW contractions; wt16 (din 32): WT instead holds the
+// split-fp16 A planes of route_gux16_kernel (same bytes)
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
                   int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
-                  hipStream_t st);
+                  hipStream_t st, bool wt16 = false);
 // one routing pass: partial s over i-chunks into fwd32_slab(p, scratch); passes r >= 1
 // also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr.  With
 // p.split and split_ws (fwd32_split_bytes) a pass r >= 1 runs as the three split kernels.

@@ -179,6 +179,7 @@ struct PrepArgs {
   const float* part;   // absmax_kernel block maxima
   float* hdr;
   int in_n, JD, JDp, din, n_chunks, chunk_len, F, N, T, lpad, Fp;
+  int wt16;            // WT holds route_gux16_kernel's split-fp16 A planes instead of fp32
   size_t xplane;
   size_t n_a, n_b, n_c, n_d, n_e;   // thread counts of the first five ranges
   size_t n_f, xt_block0;             // xT: 64-frame tiles, one block each from block xt_block0 on
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
   __shared__ int sexp[2];
   const size_t b0 = (size_t)blockIdx.x * blockDim.x, b1 = b0 + blockDim.x;
   const size_t ec = P.n_a + P.n_b, sd = ec + P.n_c, ed = sd + P.n_d;
-  const bool split_work = b0 < ec || (b1 > sd && b0 < ed);
+  const bool split_work = b0 < ec || (b1 > sd && b0 < ed) || (P.wt16 && b1 > ed && b0 < ed + P.n_e);
   if (split_work && threadIdx.x < 128) {
     const int y = threadIdx.x >> 6, l = threadIdx.x & 63;
     float m = 0.f;
@@ -288,6 +289,32 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
     return;
   }
   idx -= P.n_d;
+  if (P.wt16 && idx < P.n_e) {
+    // split-fp16 A planes of route_gux16_kernel (din 32): [i][t][h][e][8] hi, then lo,
+    // = 2^aw W[i][16t + 8h + 0..7][e] (0 past JD); one 16-byte run per plane
+    const int e = idx % P.din;
+    const size_t r1 = idx / P.din;
+    const int h = r1 % 2;
+    const size_t r2 = r1 / 2;
+    const int nt16 = (P.JD + 15) / 16;
+    const int t = r2 % nt16;
+    const size_t i = r2 / nt16;
+    const int row = t * 16 + 8 * h;
+    const float* w = P.W + (i * P.JD + min(row, P.JD - 1)) * P.din + e;
+    const float s = exp2i(aw);
+    h8 p1, p2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      _Float16 a1, a2;
+      split2h(row + k < P.JD ? w[(size_t)k * P.din] * s : 0.f, a1, a2);
+      p1[k] = a1;
+      p2[k] = a2;
+    }
+    _Float16* d = reinterpret_cast<_Float16*>(P.WT);
+    *reinterpret_cast<h8*>(d + idx * 8) = p1;
+    *reinterpret_cast<h8*>(d + P.n_e * 8 + idx * 8) = p2;
+    return;
+  }
   if (idx < P.n_e) {   // WT[i][t][g][e][0..3] = W[i][16t + 4g + 0..3][e] (0 past JD)
     const int e = idx % P.din;
     const size_t r1 = idx / P.din;
@@ -1688,7 +1715,7 @@ size_t fwd32_lds(const Fwd32Plan& p) {
 
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
                   int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
-                  hipStream_t st) {
+                  hipStream_t st, bool wt16) {
   char* base = static_cast<char*>(planes);
   float* hdr = reinterpret_cast<float*>(base + p.ws_w + p.ws_b + p.ws_x);
   const int in_n = N * (lpad + rpad + 1);
@@ -1723,7 +1750,9 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   P.n_b = (size_t)P.in_n * p.JDp;
   P.n_c = (size_t)p.n_chunks * P.JD;
   P.n_d = p.xplane / 8;
-  P.n_e = WT ? (size_t)P.in_n * ((P.JD + 15) / 16) * 4 * din : 0;
+  SRF_REQUIRE(!wt16 || din == 32, "prep32: split W^T planes need din 32, got %d", din);
+  P.wt16 = wt16 ? 1 : 0;
+  P.n_e = WT ? (size_t)P.in_n * ((P.JD + 15) / 16) * (wt16 ? 2 : 4) * din : 0;
   SRF_REQUIRE(din <= 32, "prep32: xT tile holds din <= 32, got %d", din);
   P.n_f = xT ? (size_t)P.in_n * ((P.Fp + kXtTile - 1) / kXtTile) : 0;   // xT tiles (one block each)
   P.xt_block0 = (P.n_a + P.n_b + P.n_c + P.n_d + P.n_e + 255) / 256;

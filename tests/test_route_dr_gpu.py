@@ -178,7 +178,7 @@ def test_row_tiles_per_wave_plans_match(cuda, case, var, monkeypatch):
 @pytest.mark.parametrize('case', [(2, 40, 16, 32, 2, 2, 16, 3, False), (2, 23, 16, 32, 2, 2, 32, 3, True),
                                   (1, 35, 8, 32, 1, 2, 8, 2, True), (1, 9, 4, 32, 1, 1, 8, 4, False),
                                   (2, 17, 4, 32, 1, 1, 6, 3, True), (3, 61, 8, 32, 2, 2, 12, 3, False)])
-@pytest.mark.parametrize('var', ['SRF_GUX16', 'SRF_GW16'])
+@pytest.mark.parametrize('var', ['SRF_GUX16', 'SRF_GW16', 'SRF_GW_XCD'])
 def test_split16_grad_passes_match_fp32(cuda, case, var, monkeypatch):
     """The split-fp16 32x32 gradient passes for din = dout = 32 -- gx
     (route_gux16_kernel, SRF_GUX16) and gW / gbias (route_gw16_kernel, SRF_GW16) --
