@@ -1,5 +1,6 @@
 # Issue/wait breakdown (SQ counters, one --pmc pass each) of one bench workload, plus
-# an env A/B of the same workload.  TAG=name WL=wsj_c4 AB="SRF_WEIGHT_STREAM=1" bash scripts/gpu_pmc_sq2.sh
+# an env A/B of the same workload.  TAG=name WL=wsj_c4 AB="SRF_WEIGHT_STREAM=1" [PENV="A=1 B=2"] bash scripts/gpu_pmc_sq2.sh
+# (PENV: environment of the profiled runs)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-pmcsq2}
@@ -16,7 +17,7 @@ timeout -s KILL 60 rocprofv3 -L > $OUT/sq/avail.txt 2>&1 || true
 n=0
 for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS" "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_LDS SQ_WAVES"; do
   n=$((n+1))
-  timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $OUT/sq/p$n -o run -- python3 $B --steps 2 --warmup 1 \
+  env $PENV timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $OUT/sq/p$n -o run -- python3 $B --steps 2 --warmup 1 \
     > $OUT/sq/p$n.log 2>&1 || { tail -5 $OUT/sq/p$n.log; echo "pass $n failed"; }
 done
 echo done
