@@ -884,7 +884,11 @@ __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c)
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-template <int R>
+// PROD (SRF_GUX16=2, A/B): gx = c^0 W^T gs^0 + sum_r c^r W^T gs^r + gL^r W^T Vc^r as
+// 2R - 1 products with capsule-independent B operands -- the frame vectors, scaled
+// per (vector, frame) and split once in the prologue -- combined in fp32 with the
+// per-frame scalars of the capsule: 6(2R - 1) MFMAs per capsule, no per-capsule split.
+template <int R, bool PROD = false>
 __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
     const float* __restrict__ WT, const float* __restrict__ hdr, int F, int T, int N, int lpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
@@ -944,6 +948,32 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
     for (int k = 0; k < 16; ++k) gsr[0][k] *= c0;
   }
   const int aw = (int)hdr[1];
+  constexpr int NV = PROD ? 2 * R - 1 : 1;
+  h8 pvh[NV][2], pvl[NV][2];   // PROD: split frame vectors gs^0 (c^0 folded), gs^r, Vc^r
+  float pun[NV];               // 2^-(aw + e_v) of the lane's frame
+  if constexpr (PROD) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const float* src = v < R ? gsr[v] : vcr[v - R];
+      float m = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m = fmaxf(m, fabsf(src[k]));
+      float ma, mb;
+      xpair32(m, ma, mb);
+      const int e = srf_split_exp(fmaxf(ma, mb));
+      const float sc = srf_exp2i(e);
+      pun[v] = srf_exp2i(-(aw + e));
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          _Float16 a1, a2;
+          srf_split2h(src[8 * ks + k] * sc, a1, a2);
+          pvh[v][ks][k] = a1;
+          pvl[v][ks][k] = a2;
+        }
+    }
+  }
   // split W^T planes (prep32_kernel, wt16) [i][tile][h][e][8 rows] hi, then lo: K step
   // ks of the wave is tile 2j + ks, the lane's 16 bytes sit at (h, e = fl)
   const int Fs = srf::fwd32_frame_stride(F);
@@ -980,7 +1010,38 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
   auto advance = [&](int& ww, int& nn_) {
     if (++nn_ == nn) nn_ = 0, ++ww;
   };
+  auto compute_prod = [&](auto slot) {
+    constexpr int sl = decltype(slot)::value;
+    f16v tot = {};
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      f16v t = {};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        t = mfma32h(wt_b[sl][ks][0], pvh[v][ks], t);
+        t = mfma32h(wt_b[sl][ks][0], pvl[v][ks], t);
+        t = mfma32h(wt_b[sl][ks][1], pvh[v][ks], t);
+      }
+      const float cf = v == 0 ? pun[0] : (v < R ? c_b[sl][v - 1] : g_b[sl][v - R]) * pun[v];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tot[q] = fmaf(t[q], cf, tot[q]);
+    }
+    const int ts = loc.t + w - lpad;
+    if (wave_on && loc.valid && ts >= 0 && ts < T) {
+      float* a = slab + (fl + w) * SROW + nl * DIN + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 v = {tot[4 * q], tot[4 * q + 1], tot[4 * q + 2], tot[4 * q + 3]};
+        st4(a + 8 * q, ld4(a + 8 * q) + v);
+      }
+    }
+    advance(w, nl);
+  };
   auto compute = [&](auto slot) {
+    if constexpr (PROD) {
+      compute_prod(slot);
+      return;
+    }
     constexpr int sl = decltype(slot)::value;
     float gu[16];
     float m = 0.f;
@@ -2042,9 +2103,15 @@ void launch_gux16(const Geom& g, const float* WT, const float* hdr, const float*
   const int n_per = gux16_n_per(g);
   const int n_chunks = (g.N + n_per - 1) / n_per;
   const int grid = (g.F() + 31) / 32 * n_wgroups * n_chunks;
-  hipLaunchKernelGGL((route_gux16_kernel<R>), dim3(grid), dim3(64 * kGux16NW), gux16_lds_bytes(g, n_per), st, WT,
-                     hdr, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs,
-                     g_emb, cst, glst, JP);
+  const char* e = getenv("SRF_GUX16");
+  if (R <= 3 && e && e[0] == '2')   // the product form (A/B; R = 4 would not fit the registers)
+    hipLaunchKernelGGL((route_gux16_kernel<(R <= 3 ? R : 3), true>), dim3(grid), dim3(64 * kGux16NW),
+                       gux16_lds_bytes(g, n_per), st, WT, hdr, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first,
+                       n_wgroups, n_chunks, n_per, saved, gs, g_emb, cst, glst, JP);
+  else
+    hipLaunchKernelGGL((route_gux16_kernel<R>), dim3(grid), dim3(64 * kGux16NW), gux16_lds_bytes(g, n_per), st, WT,
+                       hdr, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved,
+                       gs, g_emb, cst, glst, JP);
 }
 
 template <int D, int R>

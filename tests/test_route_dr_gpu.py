@@ -178,19 +178,20 @@ def test_row_tiles_per_wave_plans_match(cuda, case, var, monkeypatch):
 @pytest.mark.parametrize('case', [(2, 40, 16, 32, 2, 2, 16, 3, False), (2, 23, 16, 32, 2, 2, 32, 3, True),
                                   (1, 35, 8, 32, 1, 2, 8, 2, True), (1, 9, 4, 32, 1, 1, 8, 4, False),
                                   (2, 17, 4, 32, 1, 1, 6, 3, True), (3, 61, 8, 32, 2, 2, 12, 3, False)])
-@pytest.mark.parametrize('var', ['SRF_GUX16', 'SRF_GW16', 'SRF_GW_XCD'])
-def test_split16_grad_passes_match_fp32(cuda, case, var, monkeypatch):
+@pytest.mark.parametrize('var,on', [('SRF_GUX16', '1'), ('SRF_GUX16', '2'), ('SRF_GW16', '1'), ('SRF_GW_XCD', '1')])
+def test_split16_grad_passes_match_fp32(cuda, case, var, on, monkeypatch):
     """The split-fp16 32x32 gradient passes for din = dout = 32 -- gx
     (route_gux16_kernel, SRF_GUX16) and gW / gbias (route_gw16_kernel, SRF_GW16) --
     against the exact-fp32 16x16x4 ones (route_gux_kernel / route_gw3_kernel, the
-    switch at 0): the same gradients to fp32 accuracy, including J not a multiple of
+    switch at 0; SRF_GUX16=2: the gx pass as 2R-1 products on pre-split frame
+    vectors): the same gradients to fp32 accuracy, including J not a multiple of
     the workgroup's 4 output capsules, partial last frame tiles and several frame
     splits of the gW pass (route_gw16_kernel stops at 3 iterations)."""
     emb, W, bias = _mk(case, 14)
     gv = torch.tensor(np.random.default_rng(15).standard_normal(case[:2] + (case[6], case[3])), dtype=torch.float32,
                       device=cuda)
     outs = []
-    for flag in ('1', '0'):
+    for flag in (on, '0'):
         monkeypatch.setenv(var, flag)
         te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
         v.backward(gv)
