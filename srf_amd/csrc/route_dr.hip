@@ -30,6 +30,9 @@ constexpr float kSquashEps = 1e-7f;  // naive:248
 #ifndef SRF_GU_SPLITGX
 #define SRF_GU_SPLITGX 0
 #endif
+#ifndef SRF_GUX16_DBG_NOATOM
+#define SRF_GUX16_DBG_NOATOM 0
+#endif
 
 // Opt-in profiling hook (srf_route_dr_set_timing_events): events recorded on the
 // launch stream around each forward routing-pass kernel of the next
@@ -1125,7 +1128,11 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
     float v = 0.f;
 #pragma unroll
     for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots + s) * SROW + rem];
+#if SRF_GUX16_DBG_NOATOM   // timing experiment only (wrong results): plain stores instead of atomics
+    if (fo >= 0 && fo < F && v != 0.f) g_emb[((size_t)fo * N + n0) * DIN + rem] = v;
+#else
     if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
+#endif
   }
 }
 
