@@ -30,6 +30,9 @@ constexpr float kSquashEps = 1e-7f;  // naive:248
 #ifndef SRF_GU_SPLITGX
 #define SRF_GU_SPLITGX 0
 #endif
+#ifndef SRF_GUX16_OCC
+#define SRF_GUX16_OCC 2   // route_gux16_kernel workgroups (of 4 waves) per CU: 2, or 3 (two-slot ring)
+#endif
 #ifndef SRF_GUX16_DBG_NOATOM
 #define SRF_GUX16_DBG_NOATOM 0
 #endif
@@ -892,7 +895,7 @@ __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c)
 // per (vector, frame) and split once in the prologue -- combined in fp32 with the
 // per-frame scalars of the capsule: 6(2R - 1) MFMAs per capsule, no per-capsule split.
 template <int R, bool PROD = false>
-__global__ __launch_bounds__(256, 2) void route_gux16_kernel(
+__global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
     const float* __restrict__ WT, const float* __restrict__ hdr, int F, int T, int N, int lpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
     const float* __restrict__ gs, float* __restrict__ g_emb, const float* __restrict__ cst,
@@ -991,9 +994,9 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
 #pragma unroll
     for (int p = 0; p < 2; ++p) wo[ks][p] = (uint32_t)((((2 * j + ks) * 2 + h) * DIN + fl) * 16) + p * wplane;
   const uint32_t co = (uint32_t)(j * Fs + fv) * 4;
-  constexpr int NB = 3;
-  h8 wt_b[NB][2][2];   // [slot][ks][hi | lo]
-  float c_b[NB][RV], g_b[NB][RV];
+  constexpr int NB = SRF_GUX16_OCC >= 3 ? 2 : 3;
+  h8 wt_b[3][2][2];    // [slot][ks][hi | lo] (NB of them in use)
+  float c_b[3][RV], g_b[3][RV];
   auto fetch = [&](auto slot, int i) {
     constexpr int sl = decltype(slot)::value;
     const uint32_t swo = (uint32_t)i * NT * 16 * DIN * 2;
@@ -1104,19 +1107,32 @@ __global__ __launch_bounds__(256, 2) void route_gux16_kernel(
 #define SRF_GUX16_FETCH(SL) \
   fetch(SL{}, next_i());    \
   __builtin_amdgcn_sched_barrier(0);
-  if (ncap > 0) {
-    SRF_GUX16_FETCH(S0)
-    SRF_GUX16_FETCH(S1)
-  }
-  for (int k = 0; k < ncap; k += NB) {
-    SRF_GUX16_FETCH(S2)
-    compute(S0{});
-    if (k + 1 >= ncap) break;
-    SRF_GUX16_FETCH(S0)
-    compute(S1{});
-    if (k + 2 >= ncap) break;
-    SRF_GUX16_FETCH(S1)
-    compute(S2{});
+  if constexpr (NB == 3) {
+    if (ncap > 0) {
+      SRF_GUX16_FETCH(S0)
+      SRF_GUX16_FETCH(S1)
+    }
+    for (int k = 0; k < ncap; k += NB) {
+      SRF_GUX16_FETCH(S2)
+      compute(S0{});
+      if (k + 1 >= ncap) break;
+      SRF_GUX16_FETCH(S0)
+      compute(S1{});
+      if (k + 2 >= ncap) break;
+      SRF_GUX16_FETCH(S1)
+      compute(S2{});
+    }
+  } else {   // two slots: capsule k + 1 in flight while capsule k is formed
+    if (ncap > 0) {
+      SRF_GUX16_FETCH(S0)
+    }
+    for (int k = 0; k < ncap; k += 2) {
+      SRF_GUX16_FETCH(S1)
+      compute(S0{});
+      if (k + 1 >= ncap) break;
+      SRF_GUX16_FETCH(S0)
+      compute(S1{});
+    }
   }
 #undef SRF_GUX16_FETCH
   __syncthreads();
@@ -2074,7 +2090,7 @@ int gu_n_per(const Geom& g, int nw) {
 inline size_t gux16_lds_bytes(const Geom& g, int n_per) {
   return (size_t)kGux16NW * (31 + gu_window(g)) * (n_per * 32 + 4) * sizeof(float);
 }
-constexpr size_t kGux16LdsMax = 76 * 1024;   // two workgroups per CU
+constexpr size_t kGux16LdsMax = (160 / SRF_GUX16_OCC - 4) * 1024;   // SRF_GUX16_OCC workgroups per CU
 // route_gux16_kernel (split-fp16 32x32 tiles) for din = dout = 32 with stored
 // couplings; SRF_GUX16=0 keeps route_gux_kernel (A/B).  Read by the forward too: its
 // prep then writes the kernel's split W^T planes in place of the fp32 W^T, so the
@@ -2087,7 +2103,7 @@ inline bool use_gux16(const Geom& g) {
 // n-chunk size: fewest rounds of two workgroups per CU, then fewest capsules each
 int gux16_n_per(const Geom& g) {
   const int base = (g.F() + 31) / 32 * ((g.J + kGux16NW - 1) / kGux16NW);
-  const int slots = 256 * 2;
+  const int slots = 256 * SRF_GUX16_OCC;
   int best = 1;
   double best_cost = 1e30;
   for (int n_per = 1; n_per <= g.N; ++n_per) {
