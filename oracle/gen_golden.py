@@ -187,6 +187,96 @@ def gen_big(only=()):
         print(name, logits.shape, nll, 'margin', float(out['greedy_margin']))
 
 
+# C3 at the reference's own initialisation (W ~ N(0, 0.1), naive:97-103, no W_SCALE):
+# the float64 oracle's logits and NLL next to those of the float32 torch mirror (the
+# same graph in fp32 on CPU), whose distance from the oracle is the chaos-amplified
+# rounding any fp32 implementation carries there.  Gradients: seeded samples of both.
+REFINIT_CASES = {'c3_refinit': (dict(_WSJ, context=True), [60, 47], [9, 6], 23)}
+
+# C5 with the build's opt-in fp8 pose (BASELINE configs[4]): the float64 mirror with
+# the pose replaced by srf_oracle.pose_fp8's declared quantisation (straight-through
+# gradient), u in bf16 on the layers the library streams.  Same parameters / feats
+# as c5_real (W x 0.25); the plain float64 oracle's logits sit in model_c5_real.npz.
+FP8_CASES = {'c5_real_fp8': 'c5_real'}
+
+
+def _c5_bf16_layers(sh):
+    """Layers whose recurrence the library streams (srf_route_sdr_couplings_required):
+    with the fp8 pose they keep u in bf16 (ops.SdrStackPlan.ubf)."""
+    sys.path.insert(0, ROOT)
+    from srf_amd import _lib
+    L = _lib.lib()
+    return [bool(L.srf_route_sdr_couplings_required(in_n, J, D, sh.route_iters))
+            for (in_n, J, D, din) in sh.layer_shapes()]
+
+
+def gen_refinit(only=()):
+    for name, (kw, lens, tlens, seed) in REFINIT_CASES.items():
+        if only and name not in only:
+            continue
+        sh = so.SrfShape(**kw)
+        P = so.init_params(sh, seed=seed)
+        feats = regen_feats(seed, lens, sh.feat_dim)
+        rng = np.random.default_rng(seed + 300)
+        inp_len = np.array(lens, dtype=np.int32)
+        tar_len = np.array(tlens, dtype=np.int32)
+        labels = _labels(rng, tlens, sh.class_n)
+        logits = so.srf_forward(P, sh, feats, inp_len)
+        nll = so.ctc_batch(logits, labels, inp_len, tar_len, sh.class_n)
+        _, _, g64 = _mirror_grads(sh, P, feats, inp_len, labels, tar_len, 1.0 / len(lens), tile=False)
+        m = nm.NaiveMirror(sh, P, dtype=torch.float32, tile=False)
+        T = int(inp_len.max())
+        l32 = m(torch.tensor(feats[:, :T], dtype=torch.float32), torch.tensor(inp_len))
+        pe32 = nm.ctc_per_utt(l32, torch.tensor(labels), torch.tensor(inp_len), torch.tensor(tar_len), sh.class_n)
+        (pe32.sum() / len(lens)).backward()
+        g32 = {k.replace('__', '.'): p.grad.double().numpy() for k, p in m.p.items()}
+        out = {'shape_json': np.array(json.dumps(kw)), 'feats_seed': np.array(seed),
+               'feats_sum': np.array([feats.sum(), np.square(feats).sum()]), 'inp_len': inp_len, 'labels': labels,
+               'tar_len': tar_len, 'logits': logits.astype(np.float32), 'nll': nll, 'seed': np.array(seed),
+               'logits_m32': l32.detach().numpy(), 'nll_m32': pe32.detach().double().numpy()}
+        out.update({'psum.' + k: np.array([v.sum(), np.square(v).sum()]) for k, v in P.items()})
+        _sampled(out, g64, seed)
+        for k, g in g32.items():
+            out['gval32.' + k] = g.reshape(-1)[out['gidx.' + k]].astype(np.float32)
+            out['gstat32.' + k] = np.array([np.abs(g).max(), np.sqrt(np.square(g).sum())])
+        np.savez_compressed(os.path.join(GOLD, f'model_{name}.npz'), **out)
+        print(name, 'oracle vs fp32 mirror: logits', np.abs(l32.detach().numpy() - logits).max(),
+              'nll', np.abs(pe32.detach().numpy() - nll).max())
+
+
+def gen_fp8(only=()):
+    for name, base in FP8_CASES.items():
+        if only and name not in only:
+            continue
+        kw, lens, tlens, seed = BIG_CASES[base]
+        sh = so.SrfShape(**kw)
+        P = scale_w(so.init_params(sh, seed=seed), W_SCALE.get(base, 1.0))
+        feats = regen_feats(seed, lens, sh.feat_dim)
+        rng = np.random.default_rng(seed + 300)
+        inp_len = np.array(lens, dtype=np.int32)
+        tar_len = np.array(tlens, dtype=np.int32)
+        labels = _labels(rng, tlens, sh.class_n)
+        bf = _c5_bf16_layers(sh)
+        m = nm.NaiveMirror(sh, P, tile=False, fp8_pose=bf)
+        T = int(inp_len.max())
+        lt = m(torch.tensor(feats[:, :T]), torch.tensor(inp_len))
+        pe = nm.ctc_per_utt(lt, torch.tensor(labels), torch.tensor(inp_len), torch.tensor(tar_len), sh.class_n)
+        (pe.sum() / len(lens)).backward()
+        grads = {k.replace('__', '.'): p.grad.numpy() for k, p in m.p.items()}
+        logits = lt.detach().numpy()
+        out = {'shape_json': np.array(json.dumps(kw)), 'feats_seed': np.array(seed), 'base': np.array(base),
+               'feats_sum': np.array([feats.sum(), np.square(feats).sum()]), 'inp_len': inp_len, 'labels': labels,
+               'tar_len': tar_len, 'logits': logits.astype(np.float32), 'nll': pe.detach().numpy(),
+               'seed': np.array(seed), 'w_scale': np.array(W_SCALE.get(base, 1.0)),
+               'bf16_layers': np.array(bf, dtype=np.int32)}
+        out.update({'psum.' + k: np.array([v.sum(), np.square(v).sum()]) for k, v in P.items()})
+        _sampled(out, grads, seed)
+        np.savez_compressed(os.path.join(GOLD, f'model_{name}.npz'), **out)
+        ref = np.load(os.path.join(GOLD, f'model_{base}.npz'))
+        print(name, 'bf16 layers', bf, 'fp8-emulated vs fp64 oracle: logits',
+              np.abs(logits - ref['logits']).max(), 'nll', out['nll'], ref['nll'])
+
+
 def gen_dp(only=()):
     for name, (kw, lens, tlens, seed) in DP_CASES.items():
         if only and name not in only:
@@ -288,3 +378,7 @@ if __name__ == '__main__':
         gen_big([n for n in only if n in BIG_CASES])
     if not only or any(n in DP_CASES for n in only):
         gen_dp([n for n in only if n in DP_CASES])
+    if not only or any(n in REFINIT_CASES for n in only):
+        gen_refinit([n for n in only if n in REFINIT_CASES])
+    if not only or any(n in FP8_CASES for n in only):
+        gen_fp8([n for n in only if n in FP8_CASES])

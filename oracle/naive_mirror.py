@@ -113,16 +113,60 @@ def sequential_routing(u, iters, mask_first):
     return torch.stack(outs, 1)
 
 
+def dr_layer_chunked(emb, W, bias, lpad, rpad, iters, mask_first, g_v, frames_per_chunk=128):
+    """One DR layer -- window (naive:150-151), pose (:154-159), routing (:171-185,
+    :199-206) -- and its backward for the upstream gradient g_v, in float64, over
+    frame chunks so that a full-size layer (C4: 5,600 frames x 80 x 32 x 32 u) fits in
+    memory.  DR is independent per frame, so chunking changes nothing but the
+    summation order of g_W / g_bias.  emb [B,T,N,D] -> (v, g_emb, g_W, g_bias)."""
+    emb = torch.as_tensor(emb, dtype=torch.float64)
+    W = torch.as_tensor(W, dtype=torch.float64)
+    bias = torch.as_tensor(bias, dtype=torch.float64)
+    g_v = torch.as_tensor(g_v, dtype=torch.float64)
+    B, T, N, D = emb.shape
+    win = lpad + rpad + 1
+    J, Dv = W.shape[1], W.shape[2]
+    ep = F.pad(emb, (0, 0, 0, 0, lpad, rpad))
+    xw_all = torch.cat([ep[:, w:w + T] for w in range(win)], dim=2).reshape(B * T, N * win, D)
+    gv_all = g_v.reshape(B * T, J, Dv)
+    v_all = torch.empty(B * T, J, Dv, dtype=torch.float64)
+    gx_all = torch.empty_like(xw_all)
+    gW = torch.zeros_like(W)
+    gb = torch.zeros_like(bias)
+    for f0 in range(0, B * T, frames_per_chunk):
+        f1 = min(B * T, f0 + frames_per_chunk)
+        xw = xw_all[f0:f1].clone().requires_grad_(True)
+        Wc = W.clone().requires_grad_(True)
+        bc = bias.clone().requires_grad_(True)
+        u = torch.einsum('ijde,fie->fijd', Wc, xw) + bc
+        v = dynamic_routing(u[None], iters, mask_first)[0]
+        v.backward(gv_all[f0:f1])
+        v_all[f0:f1] = v.detach()
+        gx_all[f0:f1] = xw.grad
+        gW += Wc.grad
+        gb += bc.grad
+    # window adjoint: capsule i = w*N + n of frame t reads emb[t - lpad + w, n]
+    gx = gx_all.reshape(B, T, win, N, D)
+    gep = torch.zeros_like(ep)
+    for w in range(win):
+        gep[:, w:w + T] += gx[:, :, w]
+    return v_all.reshape(B, T, J, Dv), gep[:, lpad:lpad + T], gW, gb
+
+
 class NaiveMirror(torch.nn.Module):
     """Parameters are held in a dict of tensors keyed like ``srf_oracle.init_params``."""
 
-    def __init__(self, shape, params, dtype=torch.float64, tile=True):
+    def __init__(self, shape, params, dtype=torch.float64, tile=True, fp8_pose=None):
         """tile=False contracts the pose with an einsum instead of the reference's
         tf.tile-materialised W (same products, float64; for full-size fixtures,
-        whose tiled W would not fit in memory)."""
+        whose tiled W would not fit in memory).  fp8_pose: per-layer bf16-u flags;
+        the pose then takes the values of ``srf_oracle.pose_fp8`` (the build's opt-in
+        e4m3 pose, not reference arithmetic) with the exact pose's gradient
+        (straight-through), as the build's backward treats the pose as exact."""
         super().__init__()
         self.shape = shape
         self.tile = tile
+        self.fp8_pose = fp8_pose
         self.p = torch.nn.ParameterDict()
         self.buffers_ = {}
         for k, v in params.items():
@@ -177,6 +221,10 @@ class NaiveMirror(torch.nn.Module):
                 u = pose_tiled(xw, self.P(f'W{l}'), self.P(f'b{l}'))
             else:
                 u = torch.einsum('ijde,btie->btijd', self.P(f'W{l}'), xw) + self.P(f'b{l}')
+            if self.fp8_pose is not None:
+                uq = so.pose_fp8(xw.detach().numpy(), self.P(f'W{l}').detach().numpy(),
+                                 self.P(f'b{l}').detach().numpy(), bool(self.fp8_pose[l]))
+                u = u + (torch.as_tensor(uq, dtype=u.dtype) - u).detach()
             if sh.context:
                 v = sequential_routing(u, sh.route_iters, l == L - 1)
             else:

@@ -129,6 +129,53 @@ def pose(x, W, bias):
     return np.einsum('ijde,btie->btijd', W, x) + bias
 
 
+def e4m3_round(a):
+    """OCP e4m3 (fn) round-to-nearest-even of |a| <= 448 (subnormals down to 2^-9).
+    Not reference arithmetic: the numerics of the build's opt-in fp8 pose
+    (``include/srf.h`` srf_route_sdr_pose_n mode 1/2), restated to check it."""
+    a = np.asarray(a, dtype=np.float64)
+    mag = np.abs(a)
+    e = np.floor(np.log2(np.where(mag > 0, mag, 1.0)))
+    q = np.exp2(np.maximum(e, -6.0) - 3.0)      # 3 mantissa bits; exponent floor -6
+    return np.sign(a) * np.round(mag / q) * q   # np.round: half to even
+
+
+def e4m3_scale_exp(amax):
+    """Per-vector power-of-two scale 2^e with amax * 2^e in (224, 448]: e = e0 - 1
+    where 448/amax = m 2^e0, m in [0.5, 1), the quotient rounded to float32 as the
+    kernel computes it; 0 for an all-zero vector; clamped to [-100, 100]."""
+    amax = np.asarray(amax, dtype=np.float32)
+    with np.errstate(divide='ignore'):
+        q = np.float32(448.0) / np.where(amax > 0, amax, np.float32(1.0))
+    _, e0 = np.frexp(q)
+    e = np.clip(e0.astype(np.int64) - 1, -100, 100)
+    return np.where(amax > 0, e, 0)
+
+
+def bf16_round(a):
+    """float32 -> bf16 round to nearest even, back to float64."""
+    x = np.asarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    x = (x + 0x7FFF + ((x >> 16) & 1)) >> 16 << 16
+    return x.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def pose_fp8(x, W, bias, bf16_u=False):
+    """The fp8 pose transform as the build declares it (not reference arithmetic):
+    every frame's input capsule x[b,t,i,:] and every row W[i,j,d,:] rounded to
+    float32, scaled by its own 2^e (``e4m3_scale_exp``) and rounded to e4m3; exact
+    products summed, scaled back, float32 bias added; u optionally stored as bf16.
+    x [B,T,I,E], W [I,J,D,E] -> u [B,T,I,J,D]."""
+    x32 = np.asarray(x, np.float32).astype(np.float64)
+    W32 = np.asarray(W, np.float32).astype(np.float64)
+    ex = e4m3_scale_exp(np.abs(x32).max(-1))
+    ew = e4m3_scale_exp(np.abs(W32).max(-1))
+    xq = e4m3_round(x32 * np.exp2(ex)[..., None])
+    wq = e4m3_round(W32 * np.exp2(ew)[..., None])
+    u = np.einsum('ijde,btie->btijd', wq, xq)
+    u = u * np.exp2(-ex)[..., None, None] * np.exp2(-ew)[None, None] + np.asarray(bias, np.float32)
+    return bf16_round(u) if bf16_u else np.asarray(u, np.float32).astype(np.float64)
+
+
 def dynamic_routing(u, iters, mask_first):
     """DR, ``sequence_router_naive.py:171-185`` + ``_loop_body`` ``:199-206``.
 

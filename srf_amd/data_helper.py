@@ -86,9 +86,11 @@ def _shared_seed(seed, world):
     return int(t.item())
 
 
-def _dist_rank():
+def _dist_rank_world():
     import torch.distributed as dist
-    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
 
 
 def create_ds_for_training(config, logger, num_gpus, manual_bucket_batch_sizes=None, seed=None, rank=None,
@@ -97,12 +99,15 @@ def create_ds_for_training(config, logger, num_gpus, manual_bucket_batch_sizes=N
     frames (buckets from get_bucket_info(frames, num_gpus, 241, 10000, 150)) or
     fixed-size batches.
 
-    ``rank`` / ``world`` (defaults: the process-group rank, or 0, and one replica
-    per GPU, world = num_gpus) give the per-process view of MirroredStrategy's
-    distributed dataset: each yielded batch is this replica's slice of a global
-    batch (distribute_dataset)."""
-    world = num_gpus if world is None else world
-    rank = _dist_rank() if rank is None else rank
+    ``rank`` / ``world`` (defaults: the process group's rank and size, or 0 and 1
+    without one) give the per-process view of MirroredStrategy's distributed
+    dataset: each yielded batch is this replica's slice of a global batch
+    (distribute_dataset).  ``num_gpus`` sizes the buckets only, as in the reference
+    (get_bucket_info), so a single process asking for num_gpus > 1 gets whole
+    global batches, never a silent 1/num_gpus slice."""
+    g_rank, g_world = _dist_rank_world()
+    world = g_world if world is None else world
+    rank = g_rank if rank is None else rank
     seed = _shared_seed(seed, world)
     train_ds, valid_ds = _create_global(config, logger, num_gpus, manual_bucket_batch_sizes, seed)
     return distribute_dataset(train_ds, rank, world), distribute_dataset(valid_ds, rank, world)

@@ -101,6 +101,10 @@ class SequenceRouter(torch.nn.Module):
         if self.replica_id:
             self._seed_base = int(np.random.default_rng([self._seed_base, self.replica_id]).integers(1, 2 ** 62))
         self._calls = 0
+        # grad_hook(names): called from the backward once the gradient kernels of those
+        # parameters are enqueued (trainer_sr.GradBuckets); None: no hooks
+        self.grad_hook = None
+        self.grad_buckets = None
 
         w = self.window
         if self.enc_num > 1:   # (in_n, out_n, out_d, in_d), naive:88-95
@@ -246,6 +250,15 @@ class SequenceRouter(torch.nn.Module):
             self._geoms[key] = p
         return p
 
+    def _on_grad(self, t, names):
+        """Tell grad_hook that ``names``' gradients are enqueued once the backward has
+        produced the gradient of ``t`` (the input of the op that writes them)."""
+        hook = self.grad_hook
+        if hook is not None and t.requires_grad and torch.is_grad_enabled():
+            def fire(g, names=tuple(names)):
+                hook(names)
+            t.register_hook(fire)
+
     def _next_seed(self):
         self._calls += 1
         return (self._seed_base * 0x9E3779B1 + self._calls) % (1 << 63)
@@ -264,6 +277,7 @@ class SequenceRouter(torch.nn.Module):
                                              'bn1_moving_var')]
         x = ops.cnnfe(feats.contiguous(), il32, [self.P(k) for k in ops.CNNFE_PARAMS], moving, training,
                       CNN_DROPOUT if drop else 0.0, seed)
+        self._on_grad(x, ops.CAPS_PARAMS)
         emb = ops.primary_caps(x, il32, self.caps_inp_n, self.caps_inp_d, training, CNN_DROPOUT if drop else 0.0,
                                self.inp_dropout if drop else 0.0, seed, [self.P(k) for k in ops.CAPS_PARAMS],
                                self.proj_scale, self.caps_type == 'einsum')
@@ -275,7 +289,11 @@ class SequenceRouter(torch.nn.Module):
             last = self.enc_num - 1
             params = [self.P(f'{w}{l}') for l in range(self.enc_num) for w in ('W', 'b')]
             params += [self.P(f'ln_mid{l + 1}_{t}') for l in range(last) for t in ('gamma', 'beta')]
+            self._on_grad(emb, [f'{w}{l}' for l in range(self.enc_num) for w in ('W', 'b')]
+                          + [f'ln_mid{l + 1}_{t}' for l in range(last) for t in ('gamma', 'beta')])
             v = ops.sdr_stack(emb, self._stack_plan(B, T2), training, p_mid, seed, params)
+            self._on_grad(v, [f'ln_mid{last + 1}_gamma', f'ln_mid{last + 1}_beta', 'ln_output_gamma',
+                              'ln_output_beta'])
             return ops.CapsHead.apply(v, self.P(f'ln_mid{last + 1}_gamma'), self.P(f'ln_mid{last + 1}_beta'),
                                       self.P('ln_output_gamma'), self.P('ln_output_beta'), training, p_mid, seed,
                                       last, self.length_eps)
@@ -287,7 +305,10 @@ class SequenceRouter(torch.nn.Module):
                 # so that "backward writes every gradient" holds for this variant too
                 self.P(f'W{l}').grad.zero_()
                 self.P(f'b{l}').grad.zero_()
+            self._on_grad(emb, [f'W{l}', f'b{l}'])
             v = route(emb, W, bias, self._geom(l, B, T2))
+            norms = [f'ln_mid{l + 1}_gamma', f'ln_mid{l + 1}_beta']
+            self._on_grad(v, norms if l < self.enc_num - 1 else norms + ['ln_output_gamma', 'ln_output_beta'])
             if l < self.enc_num - 1:
                 emb = ops.CapsNorm.apply(v, self.P(f'ln_mid{l + 1}_gamma'), self.P(f'ln_mid{l + 1}_beta'), training,
                                          p_mid, seed, l)

@@ -52,6 +52,22 @@ class Sum(Mean):
         return self._total()
 
 
+def reduce_metrics(*metrics):
+    """Cross-replica read of Mean / Sum metrics: the reference's metrics are
+    sync-on-read variables that every replica updates, and its log line
+    (trainer_sr.py:218-221) and epoch-end early-stop check (:263-279) read them
+    across replicas.  One SUM all-reduce of (total, count) per metric; every rank
+    calls it and gets the same values.  The metrics themselves are left alone."""
+    if _world() <= 1:
+        return [m.result() for m in metrics]
+    dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else 'cpu'
+    t = torch.tensor([[m._total(), float(m.count)] for m in metrics], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    t = t.cpu()
+    return [float(tot) if isinstance(m, Sum) else (float(tot) / float(cnt) if cnt else 0.0)
+            for m, (tot, cnt) in zip(metrics, t.tolist())]
+
+
 def _crop(feats, inp_len):
     """trainer_sr.py:59-60: crop the padded batch to the longest utterance.  With
     host-resident lengths (what the data pipeline yields) this needs no device sync."""
@@ -68,8 +84,92 @@ def _world():
 
 
 def allreduce_grads(model):
+    """The flat form: one SUM all-reduce of the whole gradient after the backward."""
     if _world() > 1:
         dist.all_reduce(model.flat_grad, op=dist.ReduceOp.SUM)
+
+
+class GradBuckets:
+    """Bucketed gradient all-reduce overlapped with the backward: the
+    reference's implicit all-reduce inside apply_gradients (trainer_sr.py:71,213)
+    issued in pieces as the top-down backward completes them.
+
+    The model's parameters are views into one flat buffer in constructor order
+    (CNN front end, primary capsules, routing layers 0..L-1, output head), and the
+    backward writes them in the reverse order, so a bucket is a contiguous range of
+    flat_grad cut at parameter boundaries from the end, >= ``bucket_mb`` each.  The
+    model calls ``ready(names)`` from tensor hooks once the backward kernels of those
+    parameters are enqueued (SequenceRouter.grad_hook); a bucket whose parameters are
+    all ready is all-reduced asynchronously (RCCL orders it after the kernels already
+    on the stream, then runs it beside the rest of the backward).  Buckets launch in
+    index order on every rank, so the collectives match.  ``finish()`` launches what
+    is left (the CNN front end's parameters, whose backward is last) and makes the
+    current stream wait for every bucket.
+
+    ``force`` runs the collectives at world size 1 too (the RCCL path test)."""
+
+    def __init__(self, model, bucket_mb=25.0, force=False):
+        self.model, self.force = model, force
+        names = [name for name, _, _ in model._spec]
+        limit = max(1, int(bucket_mb * 2 ** 20 / 4))
+        self.buckets = []      # (lo, hi, parameter names), in backward order
+        hi, cur = model.n_flat, []
+        for i in reversed(range(len(names))):
+            cur.append(names[i])
+            lo = model.offsets[names[i]]
+            if hi - lo >= limit or i == 0:
+                self.buckets.append((lo, hi, cur))
+                hi, cur = lo, []
+        self.of = {n: k for k, (_, _, ns) in enumerate(self.buckets) for n in ns}
+        self.begin()
+
+    def active(self):
+        return self.force or _world() > 1
+
+    def begin(self):
+        self.pending = [set(ns) for _, _, ns in self.buckets]
+        self.launched = 0
+        self.works = []
+
+    def ready(self, names):
+        for n in names:
+            self.pending[self.of[n]].discard(n)
+        while self.launched < len(self.buckets) and not self.pending[self.launched]:
+            self._launch()
+
+    def _launch(self):
+        lo, hi, _ = self.buckets[self.launched]
+        self.launched += 1
+        if self.active():
+            self.works.append(dist.all_reduce(self.model.flat_grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+
+    def finish(self):
+        while self.launched < len(self.buckets):
+            self._launch()
+        for w in self.works:
+            w.wait()
+        self.begin()
+
+
+def _reduce(model):
+    b = getattr(model, 'grad_buckets', None)
+    if b is not None:
+        b.finish()
+    else:
+        allreduce_grads(model)
+
+
+def use_grad_buckets(model, bucket_mb=25.0, force=False):
+    """Switch ``model`` to the bucketed, backward-overlapped all-reduce (GradBuckets);
+    returns the buckets.  ``None`` as bucket_mb restores the flat form."""
+    if bucket_mb is None:
+        model.grad_buckets = None
+        model.grad_hook = None
+        return None
+    b = GradBuckets(model, bucket_mb, force)
+    model.grad_buckets = b
+    model.grad_hook = b.ready
+    return b
 
 
 def replica_mean_moving_statistics(model):
@@ -102,13 +202,16 @@ def process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_s
     feats = _crop(feats, inp_len)
     host_len = inp_len
     inp_len = inp_len.to(feats.device, non_blocking=True)
+    b = getattr(model, 'grad_buckets', None)
+    if b is not None:
+        b.begin()
     y_pred = model(feats, input_lengths=inp_len, training=True)
     # loss = sum(nll) / (B * n_gpus): its logit gradient comes out of the CTC launch
     # already scaled, and seeds the backward directly (no scalar autograd ops)
     pe_loss, g_logits = ctc.ctc_loss_and_grad(labels, y_pred, tar_len, ceil_div(inp_len, in_len_div), blank_idx,
                                               1.0 / float(batch * n_gpus))
     y_pred.backward(g_logits)
-    allreduce_grads(model)
+    _reduce(model)
     optimizer.apply_gradients(model)
     if loss_state is not None:
         loss_state.update_state(pe_loss)
@@ -165,7 +268,8 @@ class GraphedTrainStep:
     from the captured batch.
     """
 
-    def __init__(self, in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=2, label_capacity=None):
+    def __init__(self, in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=2, label_capacity=None,
+                 pool=None):
         self.model, self.optimizer = model, optimizer
         self.in_len_div, self.n_gpus, self.blank_idx = in_len_div, n_gpus, blank_idx
         feats, labels, inp_len, tar_len = inputs
@@ -181,15 +285,33 @@ class GraphedTrainStep:
         self.tar_len = torch.zeros(self.batch, dtype=torch.int32, device=dev)
         self.refill(feats, labels, inp_len, tar_len)
         self.counter = seed_counter(dev)
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                self._fwd_bwd()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.nll = self._fwd_bwd()
+        # bucketed all-reduce inside the graph (RCCL collectives captured with the
+        # backward they overlap) when the model asks for buckets on an nccl group;
+        # otherwise one flat all-reduce after each replay
+        b = getattr(model, 'grad_buckets', None)
+        self.buckets = b if (b is not None and b.active() and dist.is_initialized()
+                             and dist.get_backend() == 'nccl') else None
+        hook = getattr(model, 'grad_hook', None)
+        if self.buckets is None:
+            model.grad_hook = None
+        # the warm-up steps run the training forward, which updates the BatchNorm moving
+        # statistics: restore them, so that building a graph changes no model state
+        buffers = [b_.clone() for b_ in model.buffers()]
+        try:
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self._fwd_bwd()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, pool=pool):
+                self.nll = self._fwd_bwd()
+        finally:
+            model.grad_hook = hook
+        with torch.no_grad():
+            for b_, saved in zip(model.buffers(), buffers):
+                b_.copy_(saved)
 
     def accepts(self, feats, labels, inp_len):
         return (feats.shape[0] == self.batch and int(torch.as_tensor(inp_len).max()) == self.T
@@ -213,11 +335,15 @@ class GraphedTrainStep:
 
     def _fwd_bwd(self):
         self.counter.add_(1)
+        if self.buckets is not None:
+            self.buckets.begin()
         y_pred = self.model(self.feats, input_lengths=self.inp_len, training=True)
         logit_len = ceil_div(self.inp_len, self.in_len_div)
         pe_loss, g_logits = ctc.ctc_loss_and_grad(self.labels, y_pred, self.tar_len, logit_len, self.blank_idx,
                                                   1.0 / float(self.batch * self.n_gpus))
         y_pred.backward(g_logits)
+        if self.buckets is not None:
+            self.buckets.finish()
         return pe_loss
 
     @property
@@ -231,40 +357,68 @@ class GraphedTrainStep:
 
     def __call__(self, loss_state=None, frame_state=None, samples=None):
         self.graph.replay()
-        allreduce_grads(self.model)
+        # the per-utterance NLL lives in the graph's memory pool, which graphs of a
+        # GraphCache share: hand out a copy a later replay cannot overwrite
+        nll = self.nll.clone()
+        if self.buckets is None:
+            allreduce_grads(self.model)
         self.optimizer.apply_gradients(self.model)
         if loss_state is not None:
-            loss_state.update_state(self.nll)
+            loss_state.update_state(nll)
         if frame_state is not None:
             frame_state.update_state(self.host_len.sum())
         if samples is not None:
             samples.update_state(self.batch)
-        return self.nll
+        return nll
 
 
 class GraphCache:
-    """One GraphedTrainStep per batch shape (B, T), least recently used evicted
-    past ``max_graphs``.  Bucketed batches (load_speech_data.create_ds_bucket) come
-    in a bounded set of shapes; a new label length beyond a cached graph's capacity
-    re-captures that shape with a larger one."""
+    """Captured training steps per batch shape (B, T), least recently used evicted
+    past ``max_graphs``.
 
-    def __init__(self, in_len_div, model, optimizer, n_gpus, blank_idx, max_graphs=32, warmup=1):
+    The key is the exact shape: process_train_step crops each batch to its longest
+    utterance (trainer_sr.py:59-60), and padding a batch further would change its
+    results -- the BatchNorm batch statistics count the masked padded positions
+    (sequence_router.py:78-80) and the routing window reads padded frames into valid
+    ones (naive:150-151).  Bucketed data (load_speech_data.create_ds_bucket) gives a
+    bounded number of batch sizes but many crop lengths, so a shape is captured only
+    once it has been seen ``min_hits`` times; until then its steps run eagerly
+    (process_train_step), which costs no more than an uncaptured step.  All graphs
+    share one memory pool (they never run concurrently), so the cache holds one
+    step's worth of activations, not one per shape.  A new label length beyond a
+    cached graph's capacity re-captures that shape with a larger one."""
+
+    def __init__(self, in_len_div, model, optimizer, n_gpus, blank_idx, max_graphs=32, warmup=1, min_hits=2):
         self.args = (in_len_div, model, optimizer, n_gpus, blank_idx)
-        self.max_graphs, self.warmup = max_graphs, warmup
+        self.max_graphs, self.warmup, self.min_hits = max_graphs, warmup, max(1, int(min_hits))
         self.graphs = OrderedDict()
+        self.seen = OrderedDict()    # shape -> times seen, bounded like the graphs
         self.captures = 0
+        self.eager_steps = 0
+        self.pool = None
 
     def step(self, inputs, loss_state=None, frame_state=None, samples=None):
         feats, labels, inp_len, tar_len = inputs
         key = (feats.shape[0], int(torch.as_tensor(inp_len).max()))
+        in_len_div, model, optimizer, n_gpus, blank_idx = self.args
         g = self.graphs.get(key)
         if g is not None and not g.accepts(feats, labels, inp_len):
             g.close()
             del self.graphs[key]
             g = None
         if g is None:
-            in_len_div, model, optimizer, n_gpus, blank_idx = self.args
-            g = GraphedTrainStep(in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=self.warmup)
+            hits = self.seen.pop(key, 0) + 1
+            self.seen[key] = hits
+            while len(self.seen) > 4 * self.max_graphs:
+                self.seen.popitem(last=False)
+            if hits < self.min_hits:
+                self.eager_steps += 1
+                return process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_state, n_gpus,
+                                          blank_idx, samples)
+            if self.pool is None:
+                self.pool = torch.cuda.graph_pool_handle()
+            g = GraphedTrainStep(in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=self.warmup,
+                                 pool=self.pool)
             self.captures += 1
             self.graphs[key] = g
             while len(self.graphs) > self.max_graphs:
@@ -308,9 +462,12 @@ def distributed_train_step(dataset, in_len_div, model, optimizer, loss_state, fr
                                samples)
         else:
             graphs.step(inputs, loss_state, frame_state, samples)
-        if index % 50 == 0 and index > 0 and log is not None:
-            prog = samples.result() / train_num * 100 if train_num else float('nan')
-            log('STEP', optimizer.iterations, prog, loss_state.result(), optimizer.current_lr())
+        if index % 50 == 0 and index > 0 and samples is not None and loss_state is not None:
+            # every rank joins the cross-replica read, logging or not (:218-221)
+            n_samples, loss = reduce_metrics(samples, loss_state)
+            if log is not None:
+                prog = n_samples / train_num * 100 if train_num else float('nan')
+                log('STEP', optimizer.iterations, prog, loss, optimizer.current_lr())
         index += 1
     return index
 

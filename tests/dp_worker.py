@@ -59,6 +59,22 @@ def main():
     out['nll_err'] = float(np.abs(nll.cpu().double().numpy() - ref_nll).max() / max(1.0, np.abs(ref_nll).max()))
     out['eager_bad'] = [list(map(str, b)) for b in gradient_mismatches(z, grad_of(model))]
 
+    # bucketed all-reduce issued from the backward (GradBuckets), several buckets
+    modelb = build()
+    b = trainer_sr.use_grad_buckets(modelb, bucket_mb=0.02)
+    out['n_buckets'] = len(b.buckets)
+    trainer_sr.process_train_step(4, inputs, modelb, train_helper.get_optimizer(cfg), None, None, world,
+                                  sh.class_n - 1, None)
+    torch.cuda.synchronize()
+    out['bucketed_bad'] = [list(map(str, x)) for x in gradient_mismatches(z, grad_of(modelb))]
+    out['bucketed_vs_flat'] = float((modelb.flat_grad - model.flat_grad).abs().max() /
+                                    model.flat_grad.abs().max())
+    # a gloo group cannot be captured: the graphed step falls back to the flat form
+    gb = trainer_sr.GraphedTrainStep(4, inputs, modelb, train_helper.get_optimizer(cfg), world, sh.class_n - 1,
+                                     warmup=1)
+    out['graphed_bucket_fallback'] = gb.buckets is None
+    gb.close()
+
     # the same through the captured step
     model2 = build()
     g = trainer_sr.GraphedTrainStep(4, inputs, model2, train_helper.get_optimizer(cfg), world, sh.class_n - 1,

@@ -305,7 +305,8 @@ def test_training_datasets_split_per_replica(tmp_path):
     cfg.train_batch_frame = 1400
     world = 2
     glob_train, _ = data_helper.create_ds_for_training(cfg, None, world, seed=3, rank=0, world=1)
-    parts = [data_helper.create_ds_for_training(cfg, None, world, seed=3, rank=r)[0] for r in range(world)]
+    parts = [data_helper.create_ds_for_training(cfg, None, world, seed=3, rank=r, world=world)[0]
+             for r in range(world)]
     glob = list(glob_train)
     per_rank = [list(p) for p in parts]
     assert len(glob) > 0 and all(len(p) == len(glob) for p in per_rank)
@@ -314,4 +315,9 @@ def test_training_datasets_split_per_replica(tmp_path):
         for comp in range(4):
             np.testing.assert_array_equal(np.concatenate([p[k][comp] for p in per_rank]), g[comp])
     with pytest.raises(ValueError):
-        data_helper.create_ds_for_training(cfg, None, world, seed=None, rank=0)
+        data_helper.create_ds_for_training(cfg, None, world, seed=None, rank=0, world=world)
+    # no process group: one replica (whole global batches), whatever num_gpus says
+    single = list(data_helper.create_ds_for_training(cfg, None, world, seed=3)[0])
+    assert len(single) == len(glob)
+    for a, b in zip(single, glob):
+        np.testing.assert_array_equal(a[0], b[0])

@@ -111,3 +111,60 @@ def test_gloo_checkpoint_holds_replica_mean_bn_statistics(tmp_path):
     st = ck.read_checkpoint(os.path.join(str(tmp_path), 'ckpt-1'))
     assert float(st['model/conv/bn_layers/0/moving_mean/' + ck.VALUE][0]) == 1.5
     assert float(st['model/conv/bn_layers/1/moving_variance/' + ck.VALUE][0]) == 3.0
+
+
+class SpecModel:
+    """Flat-buffer stand-in with the SequenceRouter layout fields GradBuckets reads."""
+
+    def __init__(self, sizes, seed):
+        self._spec = [(f'p{i}', (n,), None) for i, n in enumerate(sizes)]
+        self.offsets, off = {}, 0
+        for i, n in enumerate(sizes):
+            self.offsets[f'p{i}'] = off
+            off += (n + 63) // 64 * 64
+        self.n_flat = off
+        self.flat_grad = torch.randn(off, generator=torch.Generator().manual_seed(seed))
+
+
+_SIZES = [700, 64, 5000, 33, 12000, 900, 4100, 10]
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    m = SpecModel(_SIZES, seed=10 + rank)
+    mine = m.flat_grad.clone()
+    b = trainer_sr.GradBuckets(m, bucket_mb=3000 * 4 / 2 ** 20)
+    # the backward's order: the last parameters first, in uneven groups
+    names = [n for n, _, _ in m._spec][::-1]
+    for grp in (names[:1], names[1:4], names[4:5], names[5:7]):
+        b.ready(grp)
+    b.finish()                      # the rest (the first parameter) and the waits
+    q.put((rank, mine.numpy().copy(), m.flat_grad.numpy().copy(),
+           [(lo, hi) for lo, hi, _ in b.buckets]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_bucketed_allreduce_equals_flat():
+    """GradBuckets over gloo (world 2): buckets tile the flat buffer from the end at
+    parameter boundaries, and the bucketed result equals the flat SUM all-reduce."""
+    import numpy as np
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total = res[0][1] + res[1][1]
+    for _, _, got, buckets in res:
+        np.testing.assert_allclose(got, total, rtol=1e-6, atol=1e-6)
+        assert len(buckets) >= 3
+        assert buckets[0][1] == len(total) and buckets[-1][0] == 0
+        assert all(buckets[k + 1][1] == buckets[k][0] for k in range(len(buckets) - 1))

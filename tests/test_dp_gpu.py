@@ -9,7 +9,8 @@ its own longest utterance with its own BN batch statistics, as MirroredStrategy
 computes it (trainer_sr.py:58-71) -- at the model-test tolerance
 (2e-3 * max|ref| + 1e-5 per parameter); per-replica NLL within 1e-4; and the
 replicas draw different dropout masks (equal logits with dropout off, different
-with it on).
+with it on).  The bucketed all-reduce (trainer_sr.GradBuckets, issued from the
+backward's tensor hooks) gives the flat form's gradient.
 """
 import json
 import os
@@ -63,6 +64,27 @@ def test_two_replicas_allreduce_to_fixture_gradient(cuda, name):
         assert d['nll_err'] <= 1e-4, d
         assert not d['eager_bad'], d['eager_bad']
         assert not d['graphed_bad'], d['graphed_bad']
+        assert d['n_buckets'] > 2 and not d['bucketed_bad'], d
+        assert d['bucketed_vs_flat'] <= 1e-6, d
+        assert d['graphed_bucket_fallback'], d
         assert d['dropout_off_equal'], d
         assert d['dropout_on_differs'], d
     assert res[0]['seed_base'] != res[1]['seed_base']
+
+
+def test_rccl_world1_flat_bucketed_and_captured():
+    """The nccl (RCCL) process group and its collectives, at world size 1 in a child
+    process (tests/rccl_worker.py): flat, bucketed-from-the-backward and
+    graph-captured bucketed all-reduce all leave the fixture's gradient."""
+    env = dict(os.environ, RANK='0', WORLD_SIZE='1', LOCAL_RANK='0', MASTER_ADDR='127.0.0.1',
+               MASTER_PORT=str(_free_port()))
+    p = subprocess.run([sys.executable, '-u', os.path.join(HERE, 'rccl_worker.py')], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith('RESULT ')]
+    assert line, p.stdout[-3000:]
+    d = json.loads(line[-1][7:])
+    assert d['backend'] == 'nccl' and d['world'] == 1, d
+    assert d['n_buckets'] > 2, d
+    assert not d['flat_bad'] and not d['bucketed_bad'] and not d['graphed_bad'], d
+    assert d['captured_collectives'], d

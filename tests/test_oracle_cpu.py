@@ -125,3 +125,53 @@ def test_lowmemory_routes_once_and_ignores_W_in_dr():
     assert np.abs(so.srf_forward(P2, sh, feats, inp_len) - outs[1]).max() == 0
     sh_n = so.SrfShape(enc_num=2, iters=3, lpad=1, rpad=1, ph=4, pd=8, ch=4, cd=8, vd=8, class_n=9)
     assert np.abs(so.srf_forward(P, sh_n, feats, inp_len) - outs[1]).max() > 1e-3
+
+
+def test_dr_layer_chunked_matches_mirror_autograd():
+    """The chunked float64 DR layer (used at C4 bench size) equals the numpy oracle's
+    forward and the tiled mirror's autograd gradients on a small ragged case."""
+    rng = np.random.default_rng(0)
+    B, T, N, D, lp, rp, J = 2, 9, 3, 8, 2, 1, 5
+    emb = rng.standard_normal((B, T, N, D))
+    W = rng.standard_normal((N * 4, J, D, D)) * 0.1
+    b = rng.standard_normal((N * 4, J, D)) * 0.1
+    gv = rng.standard_normal((B, T, J, D))
+    v, ge, gW, gb = nm.dr_layer_chunked(emb, W, b, lp, rp, 3, True, gv, frames_per_chunk=5)
+    assert np.abs(v.numpy() - so.dynamic_routing(so.pose(so.window(emb, lp, rp), W, b), 3, True)).max() < 1e-13
+    ce, cW, cb = (torch.tensor(a, requires_grad=True) for a in (emb, W, b))
+    ep = torch.nn.functional.pad(ce, (0, 0, 0, 0, lp, rp))
+    xw = torch.cat([ep[:, w:w + T] for w in range(lp + rp + 1)], 2)
+    nm.dynamic_routing(nm.pose_tiled(xw, cW, cb), 3, True).backward(torch.tensor(gv))
+    for got, ref in ((ge, ce), (gW, cW), (gb, cb)):
+        assert (got - ref.grad).abs().max().item() < 1e-12
+
+
+def test_e4m3_and_bf16_emulation_match_torch_casts():
+    """The fp8-pose restatement's rounding (srf_oracle.e4m3_round / bf16_round) equals
+    torch's float8_e4m3fn / bfloat16 casts (round to nearest even, e4m3 subnormals),
+    and the per-vector scale puts every absmax in (224, 448]."""
+    rng = np.random.default_rng(1)
+    a = (rng.standard_normal(100000) * np.exp2(rng.uniform(-12, 8, 100000))).astype(np.float32)
+    a = np.clip(a, -448, 448).astype(np.float64)
+    ref = torch.tensor(a, dtype=torch.float32).to(torch.float8_e4m3fn).to(torch.float64).numpy()
+    assert np.array_equal(so.e4m3_round(a), ref)
+    b = rng.standard_normal(10000).astype(np.float32)
+    assert np.array_equal(so.bf16_round(b), torch.tensor(b).to(torch.bfloat16).double().numpy())
+    am = (np.abs(rng.standard_normal(10000)) * np.exp2(rng.integers(-30, 30, 10000))).astype(np.float32)
+    s = am.astype(np.float64) * np.exp2(so.e4m3_scale_exp(am))
+    assert s.min() > 224 and s.max() <= 448
+    assert so.e4m3_scale_exp(np.float32(0)) == 0
+
+
+def test_fp8_pose_error_within_declared_bound():
+    """pose_fp8 against the exact pose: |u - u_exact| <= 0.13 sum_k |W||x| + fp32
+    (the bound include/srf.h states for srf_route_sdr_pose_n modes 1 and 2)."""
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal((2, 3, 5, 32)) * np.exp2(rng.uniform(-10, 4, (2, 3, 5, 1)))
+    W = rng.standard_normal((5, 4, 8, 32)) * 0.1
+    bias = rng.standard_normal((5, 4, 8)) * 0.1
+    exact = so.pose(x, W, bias)
+    bound = 0.13 * np.einsum('ijde,btie->btijd', np.abs(W), np.abs(x)) + 1e-6 * (1 + np.abs(exact))
+    for bf in (False, True):
+        err = np.abs(so.pose_fp8(x, W, bias, bf) - exact)
+        assert np.all(err <= bound + (np.abs(exact) * 2.0 ** -8 if bf else 0))

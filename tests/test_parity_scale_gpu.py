@@ -1,0 +1,138 @@
+"""Parity at the sizes and initialisations the bench actually runs (round-4 verdict
+item 1), against the CPU oracle.
+
+* C4 DR layers at the bench's own plan (B = 28 utterances, T' = 200 frames: 5,600
+  frames, the auto-picked i-chunks, gW frame splits, gx n-chunks and row tiles per
+  wave), every frame's v and the FULL g_emb / g_W / g_bias against the float64
+  chunked mirror (``oracle.naive_mirror.dr_layer_chunked``) -- not sampled entries.
+  One ragged case (T' = 199: the last 32-frame tile is partial).
+* C3 (SDR) at the reference's own init (W ~ N(0, 0.1), naive:97-103): the deep SDR
+  recurrence amplifies rounding (an fp32 run of the same graph on CPU differs from the
+  float64 oracle by 0.145 in the logits), so the GPU is held to a multiple of that
+  fp32 mirror's own distance from the oracle, row by row.
+* C5 with the opt-in fp8 pose (BASELINE configs[4]) end to end through
+  ``SequenceRouter(model_pose_fp8=True)``: against the float64 mirror whose pose takes
+  the build's declared e4m3 quantisation (``oracle.srf_oracle.pose_fp8``, bf16 u on
+  the streamed layers) at fp32 tolerances, and against the plain float64 oracle
+  within the emulation's own distance from it plus that fp32 tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import naive_mirror as nm
+from tests.helpers import config_from_shape, gradient_mismatches, load_model_fixture
+
+pytestmark = pytest.mark.gpu
+
+C4_LAYERS = [
+    # B, T', N, din, lpad, rpad, J, dout, iters, mask_first
+    pytest.param((28, 200, 16, 32, 2, 2, 16, 32, 3, False), id='c4_inner_bench'),
+    pytest.param((28, 200, 16, 32, 2, 2, 32, 32, 3, True), id='c4_last_bench'),
+    pytest.param((28, 199, 16, 32, 2, 2, 16, 32, 3, False), id='c4_inner_ragged_tile'),
+]
+
+
+@pytest.mark.parametrize('case', C4_LAYERS)
+def test_c4_dr_layer_at_bench_size(cuda, case):
+    """Forward v at all frames: |err| <= 2e-5 (1 + |ref|) (the layer tests' bound).
+    Gradients, every entry: |err| <= 1e-4 max(1, max|ref|) per tensor."""
+    from srf_amd.ops import RouteGeom, dynamic_routing
+    B, T, N, din, lp, rp, J, dout, it, mf = case
+    rng = np.random.default_rng(41 + J + T)
+    in_n = N * (lp + rp + 1)
+    emb = rng.standard_normal((B, T, N, din))            # LN output scale
+    W = rng.standard_normal((in_n, J, dout, din)) * 0.1   # naive:97-103
+    bias = rng.standard_normal((in_n, J, dout)) * 0.1
+    gv = rng.standard_normal((B, T, J, dout))
+    g = RouteGeom(B, T, N, din, lp, rp, J, dout, it, mf)
+    assert g.n_chunks > 1, 'the bench plan splits the input capsules into chunks'
+    te, tW, tb = (torch.tensor(a, dtype=torch.float32, device=cuda, requires_grad=True) for a in (emb, W, bias))
+    v = dynamic_routing(te, tW, tb, g)
+    v.backward(torch.tensor(gv, dtype=torch.float32, device=cuda))
+    torch.cuda.synchronize()
+    ref_v, ref_ge, ref_gW, ref_gb = nm.dr_layer_chunked(emb, W, bias, lp, rp, it, mf, gv)
+    got = v.detach().cpu().double().numpy()
+    ref = ref_v.numpy()
+    bad = np.abs(got - ref) > 2e-5 * (1 + np.abs(ref))
+    assert not bad.any(), (int(bad.sum()), np.argwhere(bad)[:8].tolist(), np.abs(got - ref).max())
+    for name, gt, rf in (('g_emb', te.grad, ref_ge), ('g_W', tW.grad, ref_gW), ('g_bias', tb.grad, ref_gb)):
+        gt, rf = gt.cpu().double().numpy(), rf.numpy()
+        err = np.abs(gt - rf).max()
+        assert err <= 1e-4 * max(1.0, np.abs(rf).max()), (name, err, np.abs(rf).max())
+
+
+def _model(name, dev, **over):
+    from srf_amd.sequence_router import SequenceRouter
+    kw, sh, P, z = load_model_fixture(name)
+    model = SequenceRouter(config_from_shape(kw, **over), None, sh.class_n, device=dev)
+    model.load_params(P)
+    model.dropout_enabled = False
+    return model, sh, z
+
+
+def _fwd_bwd(model, sh, z, dev):
+    from srf_amd import ctc
+    feats = torch.tensor(z['feats'], dtype=torch.float32, device=dev)
+    inp_len = torch.tensor(z['inp_len'], device=dev)
+    model.zero_grad()
+    logits = model(feats, input_lengths=inp_len, training=True)
+    nll = ctc.ctc_loss(torch.tensor(z['labels'], device=dev), logits, torch.tensor(z['tar_len'], device=dev),
+                       (inp_len + 3) // 4, blank_index=sh.class_n - 1)
+    (nll.sum() / feats.shape[0]).backward()
+    torch.cuda.synchronize()
+    return logits.detach().cpu().double().numpy(), nll.detach().cpu().double().numpy()
+
+
+def test_c3_reference_init_within_fp32_chaos(cuda):
+    """C3 at W ~ N(0, 0.1).  Per logit row r (one frame):
+        max_c |gpu - o64| <= 4 max_c |m32 - o64| + 1e-4 (1 + max_c |o64|),
+    o64 the float64 oracle, m32 the float32 torch mirror (same graph, CPU).  The
+    additive term is the fixed-init fixtures' bound, so rows the chaos leaves alone
+    are held to it.  NLL likewise per utterance; gradients per parameter over the
+    stored samples: max|gpu - g64| <= 4 max|g32 - g64| + 2e-3 max|g64| + 1e-5."""
+    model, sh, z = _model('c3_refinit', cuda)
+    got, nll = _fwd_bwd(model, sh, z, cuda)
+    ref, m32 = z['logits'].astype(np.float64), z['logits_m32'].astype(np.float64)
+    e_gpu = np.abs(got - ref).max(-1)
+    e_m32 = np.abs(m32 - ref).max(-1)
+    lim = 4 * e_m32 + 1e-4 * (1 + np.abs(ref).max(-1))
+    assert np.all(e_gpu <= lim), (e_gpu.max(), e_m32.max(), np.argwhere(e_gpu > lim)[:8].tolist())
+    assert np.all(np.abs(nll - z['nll']) <= 4 * np.abs(z['nll_m32'] - z['nll']) + 1e-4 * np.maximum(1, np.abs(z['nll'])))
+    bad = []
+    for key in z:
+        if not key.startswith('gidx.'):
+            continue
+        name = key[5:]
+        g = model.P(name.replace('.', '_')).grad.detach().cpu().double().numpy().reshape(-1)[z[key]]
+        g64, g32 = z['gval.' + name].astype(np.float64), z['gval32.' + name].astype(np.float64)
+        err, err32 = np.abs(g - g64).max(), np.abs(g32 - g64).max()
+        if err > 4 * err32 + 2e-3 * z['gstat.' + name][0] + 1e-5:
+            bad.append((name, err, err32))
+    assert not bad, bad
+
+
+def test_c5_fp8_pose_end_to_end(cuda):
+    """C5 with SequenceRouter(model_pose_fp8=True).  The library's plan must keep u in
+    bf16 on exactly the layers the fixture emulated.  Against the fp8-emulating float64
+    mirror (the kernel's quantisation restated): logits |err| <= 1e-3 (1 + |ref|), NLL
+    <= 1e-3 max(1, |ref|), gradients at the full-model fixtures' bound (2e-3 max|g| +
+    1e-5, norms within 2e-3).  The 1e-3 (not 1e-4) covers the bf16 stores of u: where
+    the GPU's fp32 sum and the emulation's differ by an ulp across a bf16 rounding
+    boundary the stored u differs by 2^-8 relative (about 1e-4 of the elements).
+    Against the plain float64 oracle (model_c5_real.npz): within the emulation's own
+    distance from it (the fp8 error the build declares) plus that tolerance."""
+    model, sh, z = _model('c5_real_fp8', cuda, model_pose_fp8=True)
+    assert model.pose_fp8
+    plan = model._stack_plan(1, -(-int(z['inp_len'].max()) // 4))
+    assert [bool(b) for b in plan.ubf] == [bool(b) for b in z['bf16_layers']]
+    got, nll = _fwd_bwd(model, sh, z, cuda)
+    ref = z['logits'].astype(np.float64)
+    assert np.all(np.abs(got - ref) <= 1e-3 * (1 + np.abs(ref))), np.abs(got - ref).max()
+    assert np.all(np.abs(nll - z['nll']) <= 1e-3 * np.maximum(1, np.abs(z['nll']))), (nll, z['nll'])
+    bad = gradient_mismatches(z, lambda p: model.P(p).grad.detach().cpu().double().numpy())
+    assert not bad, bad
+    _, _, _, z64 = load_model_fixture(str(z['base']))
+    o64 = z64['logits'].astype(np.float64)
+    assert np.all(np.abs(got - o64) <= np.abs(ref - o64) + 1e-3 * (1 + np.abs(ref))), np.abs(got - o64).max()
+    assert np.all(np.abs(nll - z64['nll']) <= np.abs(z['nll'] - z64['nll']) + 1e-3 * np.maximum(1, np.abs(z['nll'])))

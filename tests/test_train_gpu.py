@@ -10,7 +10,9 @@ and the captured step serving real bucketed TFRecord batches.
   bucketed by length into three batch sizes (two batches share one (B, T) shape
   with different lengths, so the cached graph is refilled), each batch's gradient
   from GraphCache equal to the eager process_train_step's
-  (|err| <= 1e-4 * max|g|), and distributed_train_step over the same dataset.
+  (|err| <= 1e-4 * max|g|), and distributed_train_step over the same dataset; the
+  BatchNorm moving statistics equal the eager model's after both (graph building
+  must not update them).
 """
 import numpy as np
 import pytest
@@ -108,14 +110,26 @@ def test_graph_cache_serves_bucketed_batches(cuda, tmp_path):
         err = (graphed.flat_grad - eager.flat_grad).abs().max().item()
         assert err <= 1e-4 * eager.flat_grad.abs().max().item(), (shapes[-1], err)
     assert shapes == [(4, 28), (3, 44), (4, 28), (2, 60), (3, 44), (2, 57)], shapes
-    assert cache.captures == 4          # (4, 28) and (3, 44) were refilled, not re-captured
+    # a shape is captured on its second sighting, its first step runs eagerly
+    assert cache.captures == 2 and cache.eager_steps == 4
     assert torch.equal(graphed.flat_params, eager.flat_params)
+    _same_bn(graphed, eager)            # building a graph does not update BN a second time
 
-    # the hot loop itself, on the cached graphs
+    # the hot loop itself, on the cached graphs; the eager model through the same loop
     loss, frames, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
     n = trainer_sr.distributed_train_step(ds, 4, graphed, cache.args[2], loss, frames, 1, sh.class_n - 1,
                                           samples, train_num=len(_LENGTHS), graphs=cache, log=None)
     assert n == 6 and samples.result() == 18 and np.isfinite(loss.result())
-    assert cache.captures == 4
+    assert cache.captures == 4          # (2, 60) and (2, 57) on their second sighting; the rest replayed
+    trainer_sr.distributed_train_step(ds, 4, eager, opt_e, trainer_sr.Mean(), trainer_sr.Mean(), 1, sh.class_n - 1,
+                                      trainer_sr.Sum(), log=None)
+    torch.cuda.synchronize()
+    _same_bn(graphed, eager)
     for g in cache.graphs.values():
         g.close()
+
+
+def _same_bn(a, b):
+    for name in ('bn0_moving_mean', 'bn0_moving_var', 'bn1_moving_mean', 'bn1_moving_var'):
+        x, y = getattr(a, name), getattr(b, name)
+        assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), (name, (x - y).abs().max().item())
