@@ -19,4 +19,3 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kernel_stats_c4.csv
 
 cd $GRAFT_REPO_ROOT
-TAG=$T/ab WL=wsj_c4 STEPS=20 VARIANTS="SRF_GW_XCD=0;SRF_GW_XCD=1;SRF_GW_XCD=0;SRF_GW_XCD=1" bash scripts/gpu_ab_env.sh

@@ -763,12 +763,8 @@ int srf_primary_caps_fwd_ex(const float* X, const int* inp_len, int B, int T, in
   hipStream_t st = static_cast<hipStream_t>(stream);
   constexpr int FW = 2;
   const dim3 gvec((F + 4 * FW - 1) / (4 * FW));
-  static const bool proj_mfma = [] {
-    const char* e = getenv("SRF_PROJ_MFMA");
-    return !(e && e[0] == '0');
-  }();
   const int Kq = ((K + kProjWaves - 1) / kProjWaves + 15) / 16 * 16;
-  if (proj_mfma && K % 4 == 0 && (PH == 4 || PH == 8 || PH == 16)) {
+  if (K % 4 == 0 && (PH == 4 || PH == 8 || PH == 16)) {
     const dim3 gm((F + 15) / 16), bm(64 * kProjWaves);
     if (PH == 4)
       hipLaunchKernelGGL((proj_fwd_mfma_kernel<4>), gm, bm, 0, st, X, F, K, Wp, bp, sv.e, T, proj_scale, pos_enc, Kq);

@@ -292,203 +292,6 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
   }
 }
 
-// Pack both stage-2 kernels [3][3][C][C] (kh, kw, cin, cout) into the MFMA B
-// image wp[tap][n = ab*C + cout][cin].
-__global__ void pack_w2_kernel(const float* __restrict__ ka, const float* __restrict__ kb, float* __restrict__ wp) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= 9 * 2 * C * C) return;
-  const int cin = idx % C;
-  const int n = (idx / C) % (2 * C);
-  const int tap = idx / (2 * C * C);
-  const float* k = n < C ? ka : kb;
-  wp[idx] = k[((size_t)tap * C + cin) * C + (n % C)];
-}
-
-// ---------------------------------------------------------------- conv2 (MFMA)
-// Workgroup = 4 waves = 64 output pixels x 128 outputs (conv a and b, 64 each).
-// Wave w owns output channels [16w, 16w+16) of both convs: N-tile 0 = conv a,
-// N-tile 1 = conv b, so the maxout pairs land in the same lane.
-constexpr int kLdsStride = C + 4;  // row padding against LDS bank conflicts
-
-// Per tap: the A tile (64 px x 64 cin, BN1 + mask1 applied) is staged in LDS,
-// double-buffered (the next tap's gather is in flight during this tap's MFMAs);
-// each wave streams its own B columns (the packed weights) straight into
-// registers, one tap ahead, since no other wave reads them.
-struct A2Gather {
-  f4 x[4];
-  unsigned ok;   // bit q: slot q holds a live pixel
-};
-
-// Tap-independent coordinates of the 4 A slots a thread stages (no divisions per tap).
-struct A2Slots {
-  int b[4], t2[4], f2[4], len1[4];
-  unsigned live;
-};
-
-__device__ __forceinline__ A2Slots a2_slots(const int* __restrict__ inp_len, const Dims& d, int p0, int tid) {
-  const int P2 = d.B * d.T2 * d.F2;
-  A2Slots sl;
-  sl.live = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int px = (q * 256 + tid) >> 4;
-    const int p = min(p0 + px, P2 - 1);
-    sl.f2[q] = p % d.F2;
-    sl.t2[q] = (p / d.F2) % d.T2;
-    sl.b[q] = p / (d.F2 * d.T2);
-    sl.len1[q] = ceil_div_len(inp_len[sl.b[q]], 2);
-    sl.live |= (p0 + px < P2 ? 1u : 0u) << q;
-  }
-  return sl;
-}
-
-__device__ __forceinline__ A2Gather gather_a2(const float* __restrict__ y1, const A2Slots& sl, const Dims& d,
-                                              int tap, int tid) {
-  const int dt = tap / 3, df = tap - dt * 3;
-  A2Gather r;
-  r.ok = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c4 = ((q * 256 + tid) & 15) * 4;
-    const int t1 = 2 * sl.t2[q] - d.pt2 + dt;
-    const int f1 = 2 * sl.f2[q] - d.pf2 + df;
-    const bool ok = ((sl.live >> q) & 1u) && t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 && t1 < sl.len1[q];
-    const int t1c = min(max(t1, 0), d.T1 - 1), f1c = min(max(f1, 0), d.F1 - 1);
-    r.x[q] = *reinterpret_cast<const f4*>(y1 + (((size_t)sl.b[q] * d.T1 + t1c) * d.F1 + f1c) * C + c4);
-    r.ok |= (ok ? 1u : 0u) << q;
-  }
-  return r;
-}
-
-__device__ __forceinline__ void put_a2(float* As, const A2Gather& r, const float* __restrict__ stats1, int tid) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int idx = q * 256 + tid;
-    const int px = idx >> 4, c4 = (idx & 15) * 4;
-    const f4 sc = *reinterpret_cast<const f4*>(stats1 + 2 * C + c4);
-    const f4 sf = *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
-    const f4 v = ((r.ok >> q) & 1u) ? r.x[q] * sc + sf : f4{0.f, 0.f, 0.f, 0.f};
-    *reinterpret_cast<f4*>(&As[px * kLdsStride + c4]) = v;
-  }
-}
-
-__device__ __forceinline__ void load_b2(const float* __restrict__ wp, int tap, int wv, int l16, int g,
-                                        f4 (&b)[4][2]) {
-#pragma unroll
-  for (int s = 0; s < C / 16; ++s)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      b[s][nt] = *reinterpret_cast<const f4*>(wp + ((size_t)tap * 2 * C + nt * C + 16 * wv + l16) * C + 16 * s + 4 * g);
-}
-
-__global__ __launch_bounds__(256) void conv2_fwd_kernel(
-    const float* __restrict__ y1, const float* __restrict__ stats1, const int* __restrict__ inp_len, Dims d,
-    const float* __restrict__ wp, const float* __restrict__ ba, const float* __restrict__ bb, int training,
-    float drop_p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, float* __restrict__ y2, unsigned char* __restrict__ sel2,
-    float* __restrict__ part) {
-  seed = srf_step_seed(seed, seed_src);
-  __shared__ __attribute__((aligned(16))) float As[2][64 * kLdsStride];
-  __shared__ float red[3][4][4][16];   // [n|mean|M2][wave][lane group][channel]
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int P2 = d.B * d.T2 * d.F2;
-  const int p0 = blockIdx.x * 64;
-
-  f4 acc[4][2];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
-
-  f4 bcur[4][2], bnxt[4][2];
-  load_b2(wp, 0, wv, l16, g, bcur);
-  const A2Slots slots = a2_slots(inp_len, d, p0, tid);
-  {
-    const A2Gather r = gather_a2(y1, slots, d, 0, tid);
-    put_a2(As[0], r, stats1, tid);
-  }
-  __syncthreads();
-  for (int tap = 0; tap < 9; ++tap) {
-    const bool more = tap + 1 < 9;
-    A2Gather r;
-    if (more) {
-      r = gather_a2(y1, slots, d, tap + 1, tid);
-      load_b2(wp, tap + 1, wv, l16, g, bnxt);
-    }
-    const float* Ab = As[tap & 1];
-#pragma unroll
-    for (int s = 0; s < C / 16; ++s) {
-      const int k0 = 16 * s + 4 * g;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const f4 a = *reinterpret_cast<const f4*>(&Ab[(mt * 16 + l16) * kLdsStride + k0]);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          acc[mt][0] = mfma16x16x4(a[kk], bcur[s][0][kk], acc[mt][0]);
-          acc[mt][1] = mfma16x16x4(a[kk], bcur[s][1][kk], acc[mt][1]);
-        }
-      }
-    }
-    if (more) {
-      put_a2(As[(tap + 1) & 1], r, stats1, tid);
-#pragma unroll
-      for (int s = 0; s < C / 16; ++s) bcur[s][0] = bnxt[s][0], bcur[s][1] = bnxt[s][1];
-    }
-    __syncthreads();
-  }
-
-  // epilogue: lane (c = 16*wv + l16, g) holds pixels mt*16 + 4g + k
-  const int c = 16 * wv + l16;
-  const float bia = ba[c], bib = bb[c];
-  const float keep_scale = 1.f / (1.f - drop_p);
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    // coordinates of the first of the 4 consecutive pixels, then stepped
-    const int pb = min(p0 + mt * 16 + 4 * g, P2 - 1);
-    int f2 = pb % d.F2, t2 = (pb / d.F2) % d.T2, b = pb / (d.F2 * d.T2);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int p = p0 + mt * 16 + 4 * g + k;
-      if (k > 0 && ++f2 == d.F2) {
-        f2 = 0;
-        if (++t2 == d.T2) {
-          t2 = 0;
-          ++b;
-        }
-      }
-      if (p >= P2) continue;
-      const size_t o = (size_t)p * C + c;
-      float a = acc[mt][0][k] + bia, bv = acc[mt][1][k] + bib;
-      if (training && drop_p > 0.f) {
-        bool ka, kb;
-        srf_keep2(seed, kStreamConv1a, o, drop_p, ka, kb);
-        a *= ka ? keep_scale : 0.f;
-        bv *= kb ? keep_scale : 0.f;
-      }
-      const bool sel = a >= bv;
-      float y = sel ? a : bv;
-      if (t2 >= ceil_div_len(inp_len[b], 4)) y = 0.f;
-      y2[o] = y;
-      sel2[o] = sel ? 1 : 0;
-      n += 1.f;
-      const float delta = y - mean;
-      mean += delta / n;
-      m2 += delta * (y - mean);
-    }
-  }
-  red[0][wv][g][l16] = n; red[1][wv][g][l16] = mean; red[2][wv][g][l16] = m2;
-  // combine the 4 lane groups of this wave (same channel) through LDS
-  __syncthreads();
-  if (g == 0) {
-    for (int r = 1; r < 4; ++r)
-      chan_merge(n, mean, m2, red[0][wv][r][l16], red[1][wv][r][l16], red[2][wv][r][l16]);
-    part[((size_t)blockIdx.x * 3 + 0) * C + c] = n;
-    part[((size_t)blockIdx.x * 3 + 1) * C + c] = mean;
-    part[((size_t)blockIdx.x * 3 + 2) * C + c] = m2;
-  }
-}
-
-
 // ---------------------------------------------------------------- conv2 (split-fp16 MFMA)
 // The same implicit GEMM on v_mfma_f32_32x32x16_f16 with fp32-accurate 2-term fp16
 // splits of power-of-two scaled operands (as the routing pose, route_fwd32.hip:
@@ -500,7 +303,8 @@ __global__ __launch_bounds__(256) void conv2_fwd_kernel(
 // lane).  Per k-block (one tap, 16 input channels) the A fragments are gathered
 // straight into registers (BN1 + mask1 + split on the VALU, one k-block ahead) and
 // the B fragments (packed, pre-split weights, shared by both waves) are staged in
-// LDS, double-buffered, one k-block ahead.  Epilogue as conv2_fwd_kernel.
+// LDS, double-buffered, one k-block ahead.  The epilogue fuses bias, dropout, maxout,
+// mask and the BN2 Welford partials.
 typedef __bf16 cbf8 __attribute__((ext_vector_type(8)));
 typedef float cf16 __attribute__((ext_vector_type(16)));
 
@@ -883,132 +687,6 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
   }
 }
 
-// Transposed weight image for the data gradient: wq[tap][cin][n].
-__global__ void pack_w2t_kernel(const float* __restrict__ ka, const float* __restrict__ kb, float* __restrict__ wq) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= 9 * 2 * C * C) return;
-  const int n = idx % (2 * C);
-  const int cin = (idx / (2 * C)) % C;
-  const int tap = idx / (2 * C * C);
-  const float* k = n < C ? ka : kb;
-  wq[idx] = k[((size_t)tap * C + cin) * C + (n % C)];
-}
-
-constexpr int kNStride = 2 * C + 4;
-
-// Data gradient of stage 2 for the input pixels of one stride-parity class
-// (t1 % 2 == qt, f1 % 2 == qf): only taps with the matching parity reach such a
-// pixel, so the implicit GEMM (M = 64 pixels, N = 64 cin, K = taps x 128) runs
-// without zero taps.  g_x1[p1][cin] = sum_tap sum_n g_ab[o(p1,tap)][n] wq[tap][cin][n].
-// A (64 px x 128 n, gathered from g_ab) is double-buffered in LDS with the next
-// tap's gather in flight; each wave streams its 16 cin rows of wq into registers.
-__global__ __launch_bounds__(256) void conv2_dgrad_kernel(const float* __restrict__ g_ab,
-                                                          const float* __restrict__ wq, Dims d, int qt, int qf,
-                                                          float* __restrict__ g_x1) {
-  __shared__ __attribute__((aligned(16))) float As[2][64 * kNStride];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int nkt = (d.T1 - qt + 1) / 2, nkf = (d.F1 - qf + 1) / 2;
-  const int Pc = d.B * nkt * nkf;
-  const int q0 = blockIdx.x * 64;
-  const int dt0 = (qt + d.pt2) & 1, df0 = (qf + d.pf2) & 1;
-  const int ntf = (3 - df0 + 1) / 2;                       // taps per parity class: ntt x ntf
-  const int ntaps = ((3 - dt0 + 1) / 2) * ntf;
-  // tap-independent slot coordinates: slot q = pixel (q*256 + tid) >> 5
-  int sb[8], skt[8], skf[8];
-  unsigned live = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int pc = q0 + ((q * 256 + tid) >> 5);
-    const int pcc = min(pc, Pc - 1);
-    skf[q] = pcc % nkf;
-    skt[q] = (pcc / nkf) % nkt;
-    sb[q] = pcc / (nkf * nkt);
-    live |= (pc < Pc ? 1u : 0u) << q;
-  }
-  const int n4 = (tid & 31) * 4;
-  auto tap_of = [&](int k) {
-    const int dt = dt0 + 2 * (k / ntf), df = df0 + 2 * (k % ntf);
-    return dt * 3 + df;
-  };
-  auto gather = [&](int tap, f4 (&v)[8], unsigned& ok) {
-    const int dt = tap / 3, df = tap - dt * 3;
-    ok = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int t2 = (qt + 2 * skt[q] + d.pt2 - dt) / 2, f2 = (qf + 2 * skf[q] + d.pf2 - df) / 2;
-      const bool in = ((live >> q) & 1u) && t2 >= 0 && t2 < d.T2 && f2 >= 0 && f2 < d.F2;
-      const int t2c = min(max(t2, 0), d.T2 - 1), f2c = min(max(f2, 0), d.F2 - 1);
-      v[q] = *reinterpret_cast<const f4*>(g_ab + (((size_t)sb[q] * d.T2 + t2c) * d.F2 + f2c) * 2 * C + n4);
-      ok |= (in ? 1u : 0u) << q;
-    }
-  };
-  auto put = [&](float* A, const f4 (&v)[8], unsigned ok) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int px = (q * 256 + tid) >> 5;
-      *reinterpret_cast<f4*>(&A[px * kNStride + n4]) = ((ok >> q) & 1u) ? v[q] : f4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto load_b = [&](int tap, f4 (&bw)[8]) {
-#pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2)
-      bw[s2] = *reinterpret_cast<const f4*>(wq + ((size_t)tap * C + 16 * wv + l16) * 2 * C + 16 * s2 + 4 * g);
-  };
-  f4 acc[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
-  f4 bcur[8], bnxt[8], av[8];
-  unsigned aok;
-  load_b(tap_of(0), bcur);
-  gather(tap_of(0), av, aok);
-  put(As[0], av, aok);
-  __syncthreads();
-  for (int k = 0; k < ntaps; ++k) {
-    const bool more = k + 1 < ntaps;
-    if (more) {
-      gather(tap_of(k + 1), av, aok);
-      load_b(tap_of(k + 1), bnxt);
-    }
-    const float* Ab = As[k & 1];
-#pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2) {
-      const int k0 = 16 * s2 + 4 * g;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const f4 a = *reinterpret_cast<const f4*>(&Ab[(mt * 16 + l16) * kNStride + k0]);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) acc[mt] = mfma16x16x4(a[kk], bcur[s2][kk], acc[mt]);
-      }
-    }
-    if (more) {
-      put(As[(k + 1) & 1], av, aok);
-#pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) bcur[s2] = bnxt[s2];
-    }
-    __syncthreads();
-  }
-  const int ci = 16 * wv + l16;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int pb = min(q0 + mt * 16 + 4 * g, Pc - 1);
-    int kf = pb % nkf, kt = (pb / nkf) % nkt, b = pb / (nkf * nkt);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int pc = q0 + mt * 16 + 4 * g + k;
-      if (k > 0 && ++kf == nkf) {
-        kf = 0;
-        if (++kt == nkt) {
-          kt = 0;
-          ++b;
-        }
-      }
-      if (pc >= Pc) continue;
-      const int t1 = qt + 2 * kt, f1 = qf + 2 * kf;
-      g_x1[(((size_t)b * d.T1 + t1) * d.F1 + f1) * C + ci] = acc[mt][k];
-    }
-  }
-}
 
 // ---------------------------------------------------------------- dgrad (split-bf16 MFMA)
 // The data gradient on v_mfma_f32_32x32x16_bf16 with 3-term splits, structured as
@@ -1077,7 +755,6 @@ __device__ __forceinline__ void pack_w2t_f16_body(int idx, const float* __restri
 
 constexpr int kD2Waves = 4;
 constexpr int kD2Px = 32 * kD2Waves;
-constexpr int kD2BChunks = 3 * C * 2;   // 16-byte B chunks per k-block (planes x cin x halves)
 
 // H = true: 2-term fp16 splits of power-of-two scaled operands (A = 2^ea g_ab with ea
 // from conv2_bwd_prep's block maxima, reduced by every workgroup; B = 2^e_cin k from
@@ -1273,116 +950,12 @@ __global__ __launch_bounds__(64 * kD2Waves) __attribute__((amdgpu_waves_per_eu(2
 
 // Weight gradient of stage 2 for one tap and one pixel split:
 // part[s][tap][cin][n] = sum_{p in split} xbn1(p, tap)[cin] * g_ab[p][n].
-// K = pixels in chunks of kWgChunk, staged row-major (A [px][cin] with BN1 + mask1
-// applied, B [px][n]) and double-buffered; a wave owns n in [32w, 32w+32) for all
-// 64 cin.  Row strides = 16 mod 64 words keep the per-lane b32 operand reads
-// (lane group g = pixel) bank-conflict free.
+// K = pixels in chunks of kWgChunk.
 constexpr int kWgChunk = 32;
-constexpr int kWgAStr = C + 16;
-constexpr int kWgBStr = 2 * C + 16;
 
 struct WgDiv {
   FastDiv f2, t2;
 };
-
-__global__ __launch_bounds__(256) void conv2_wgrad_kernel(const float* __restrict__ y1,
-                                                          const float* __restrict__ stats1,
-                                                          const int* __restrict__ inp_len,
-                                                          const float* __restrict__ g_ab, Dims d, WgDiv dv,
-                                                          int nsplit, int split_len, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float As[2][kWgChunk * kWgAStr];
-  __shared__ __attribute__((aligned(16))) float Bs[2][kWgChunk * kWgBStr];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int l16 = lane & 15, g = lane >> 4;
-  const int tap = blockIdx.x / nsplit, sp = blockIdx.x - tap * nsplit;
-  const int dt = tap / 3, df = tap - dt * 3;
-  const int P2 = d.B * d.T2 * d.F2;
-  const int pbeg = sp * split_len, pend = min(P2, pbeg + split_len);
-  const int c4 = (tid & 15) * 4;                       // A slot channel (both A slots)
-  const f4 sc = *reinterpret_cast<const f4*>(stats1 + 2 * C + c4);
-  const f4 sf = *reinterpret_cast<const f4*>(stats1 + 3 * C + c4);
-  const int n4 = (tid & 31) * 4;                       // B slot column (all B slots)
-
-  f4 xa[2], xb[4];
-  unsigned oka = 0, okb = 0;
-  auto gather = [&](int pc0) {
-    oka = okb = 0;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int p = pc0 + ((q * 256 + tid) >> 4);
-      const unsigned pcl = (unsigned)min(p, P2 - 1);
-      const unsigned r1 = fdiv(pcl, dv.f2);
-      const int f2 = (int)(pcl - r1 * d.F2);
-      const unsigned b = fdiv(r1, dv.t2);
-      const int t2 = (int)(r1 - b * d.T2);
-      const int t1 = 2 * t2 - d.pt2 + dt, f1 = 2 * f2 - d.pf2 + df;
-      const bool ok = p < pend && t1 >= 0 && t1 < d.T1 && f1 >= 0 && f1 < d.F1 &&
-                      t1 < ceil_div_len(inp_len[b], 2);
-      const int t1c = min(max(t1, 0), d.T1 - 1), f1c = min(max(f1, 0), d.F1 - 1);
-      xa[q] = *reinterpret_cast<const f4*>(y1 + (((size_t)b * d.T1 + t1c) * d.F1 + f1c) * C + c4);
-      oka |= (ok ? 1u : 0u) << q;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int p = pc0 + ((q * 256 + tid) >> 5);
-      xb[q] = *reinterpret_cast<const f4*>(g_ab + (size_t)min(p, P2 - 1) * 2 * C + n4);
-      okb |= (p < pend ? 1u : 0u) << q;
-    }
-  };
-  auto put = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int px = (q * 256 + tid) >> 4;
-      *reinterpret_cast<f4*>(&As[buf][px * kWgAStr + c4]) =
-          ((oka >> q) & 1u) ? xa[q] * sc + sf : f4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int px = (q * 256 + tid) >> 5;
-      *reinterpret_cast<f4*>(&Bs[buf][px * kWgBStr + n4]) = ((okb >> q) & 1u) ? xb[q] : f4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-
-  f4 acc[4][2];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
-  const int nch = (pend - pbeg + kWgChunk - 1) / kWgChunk;
-  if (nch > 0) {
-    gather(pbeg);
-    put(0);
-  }
-  __syncthreads();
-  for (int ch = 0; ch < nch; ++ch) {
-    const bool more = ch + 1 < nch;
-    if (more) gather(pbeg + (ch + 1) * kWgChunk);
-    const float* A = As[ch & 1];
-    const float* Bm = Bs[ch & 1];
-#pragma unroll
-    for (int ks = 0; ks < kWgChunk / 4; ++ks) {
-      const int px = ks * 4 + g;
-      float a[4], bv[2];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) a[mt] = A[px * kWgAStr + mt * 16 + l16];
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) bv[nt] = Bm[px * kWgBStr + 32 * wv + nt * 16 + l16];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16x16x4(a[mt], bv[nt], acc[mt][nt]);
-    }
-    if (more) put((ch + 1) & 1);
-    __syncthreads();
-  }
-  // C layout: col = n (l16 within the N-tile), rows = cin mt*16 + 4g + k
-  float* dst = part + ((size_t)sp * 9 + tap) * C * 2 * C;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        dst[(size_t)(mt * 16 + 4 * g + k) * 2 * C + 32 * wv + 16 * nt + l16] = acc[mt][nt][k];
-}
 
 // ---------------------------------------------------------------- wgrad (split-bf16 MFMA)
 // g_ab [P2][n] -> pixel-minor split planes gsT3[plane][n][P2p] (zero past P2), the B
@@ -1784,13 +1357,6 @@ FwdWs fwd_ws_layout(const Dims& d, void* base) {
   return w;
 }
 
-// The split-bf16 stage-2 kernels serve by default; SRF_CONV2_32=0 selects the
-// fp32-MFMA ones (A/B runs).
-inline bool use_conv2_32() {
-  const char* e = getenv("SRF_CONV2_32");
-  return !(e && e[0] == '0');
-}
-
 int check_dims(int B, int T, int Fin, int nfilt) {
   SRF_REQUIRE(B > 0 && T > 0 && Fin > 0, "bad CNN-FE shape B=%d T=%d F=%d", B, T, Fin);
   SRF_REQUIRE(nfilt == C, "model-conv-filter-num must be %d (got %d)", C, nfilt);
@@ -1843,8 +1409,7 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
   const size_t P2 = (size_t)d.B * d.T2 * d.F2;
   const int nb2 = (int)((P2 + 63) / 64);
   int nparts2 = nb2;
-  const bool c2_32 = use_conv2_32();
-  const int npack = c2_32 ? (kPackW2Threads + 64 * kRows1 - 1) / (64 * kRows1) : 0;
+  const int npack = (kPackW2Threads + 64 * kRows1 - 1) / (64 * kRows1);
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3(conv1_blocks(d) + npack), dim3(64 * kRows1), conv1_lds(d), st, feats,
                      inp_len, d, k0a, b0a, k0b, b0b, training, drop_p, seed, srf::seed_source(), sv.y1, sv.sel1,
                      w.part1, conv1_blocks(d), k1a, k1b, w.wp2, w.wsc, w.ymax);
@@ -1853,19 +1418,13 @@ int srf_cnnfe_fwd(const float* feats, const int* inp_len, int B, int T, int feat
                         w.ymax, conv1_blocks(d))))
     return rc;
   SRF_LAUNCH_CHECK("bn_finalize(1)");
-  if (c2_32) {   // split weights packed by the conv1 launch
+  {   // split weights packed by the conv1 launch
     const int nb32 = (int)((P2 + kC2Px - 1) / kC2Px);
     hipLaunchKernelGGL(conv2_fwd32_kernel, dim3(nb32), dim3(64 * kC2Waves), 0, st, sv.y1, sv.stats1, inp_len, d,
                        w.wp2, w.wsc, b1a, b1b, training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2,
                        w.part2);
     SRF_LAUNCH_CHECK("conv2_fwd32");
     nparts2 = nb32;
-  } else {
-    hipLaunchKernelGGL(pack_w2_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wp);
-    SRF_LAUNCH_CHECK("pack_w2");
-    hipLaunchKernelGGL(conv2_fwd_kernel, dim3(nb2), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, d, w.wp, b1a, b1b,
-                       training, drop_p, seed, srf::seed_source(), sv.y2, sv.sel2, w.part2);
-    SRF_LAUNCH_CHECK("conv2_fwd");
   }
   if ((rc = bn_finalize(w.part2, nparts2, w.merged, gamma1, beta1, mmean1, mvar1, training, sv.stats2, st)))
     return rc;
@@ -1889,17 +1448,9 @@ struct BwdWs2 {
 };
 
 constexpr int kBnBlocks = 1024;
-constexpr int kWgradSplits = 64;
 constexpr int kWgrad32SplitsMax = 128;
-// pixel splits of conv2_wgrad32_kernel (a multiple of 8; SRF_WG32_SPLITS overrides)
-inline int wgrad32_splits() {
-  static const int v = [] {
-    const char* e = getenv("SRF_WG32_SPLITS");
-    const int s = e ? atoi(e) : 56;
-    return std::max(8, std::min(kWgrad32SplitsMax, s / 8 * 8));
-  }();
-  return v;
-}
+// pixel splits of conv2_wgrad32_kernel (a multiple of 8)
+constexpr int kWgrad32Splits = 56;
 
 BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   const size_t P1 = (size_t)d.B * d.T1 * d.F1, P2 = (size_t)d.B * d.T2 * d.F2;
@@ -1911,7 +1462,7 @@ BwdWs2 bwd_ws_layout(const Dims& d, void* base) {
   };
   const size_t obp = take((size_t)kBnBlocks * 2 * C * 4), os2 = take(2 * C * 4), os1 = take(2 * C * 4),
                oab = take(P2 * 2 * C * 4), obias = take((size_t)kBnBlocks * 2 * C * 4), ogx = take(P1 * C * 4),
-               owq = take((size_t)9 * 2 * C * C * 4), owp = take((size_t)std::max(kWgradSplits, kWgrad32SplitsMax) * 9 * C * 2 * C * 4),
+               owq = take((size_t)9 * 2 * C * C * 4), owp = take((size_t)kWgrad32SplitsMax * 9 * C * 2 * C * 4),
                oc1 = take((size_t)conv1_blocks(d) * 20 * C * 4), oc1s = take(20 * C * 4),
                oscr = take(srf::colsum_scratch_floats(std::max(conv1_blocks(d), kBnBlocks), 20 * C) * 4);
   const int P2p = (int)((P2 + kTpPx - 1) / kTpPx * kTpPx);
@@ -1973,77 +1524,40 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   SRF_LAUNCH_CHECK("bn_bwd_reduce(2)");
   if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st, srf::ColSplit{{g_beta1, g_gamma1, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
-  const bool c2_32 = use_conv2_32();
-  // split-fp16 data gradient (SRF_DGRAD_F16=0: the split-bf16 one)
-  const bool dg16 = c2_32 && !(getenv("SRF_DGRAD_F16") && getenv("SRF_DGRAD_F16")[0] == '0');
-  __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);   // 3 bf16 planes fit the fp32 image
+  __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);
   _Float16* wq2h = reinterpret_cast<_Float16*>(w.wq);
-  const int npack = c2_32 ? ((dg16 ? kPackW2tF16Threads : kPackW2tThreads) + 255) / 256 : 0;
+  const int npack = (kPackW2tF16Threads + 255) / 256;
   hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks + npack), dim3(256), 0, st, g_out, sv.y2, sv.sel2,
                      sv.stats2, gamma1, w.bnsum2, inp_len, d, drop_p, seed, srf::seed_source(), w.g_ab, w.biaspart,
-                     kBnBlocks, k1a, k1b, wq3, dg16 ? wq2h : nullptr, w.wdsc, w.gmax);
+                     kBnBlocks, k1a, k1b, wq3, wq2h, w.wdsc, w.gmax);
   SRF_LAUNCH_CHECK("conv2_bwd_prep");
   if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, nullptr, w.scratch, st, srf::ColSplit{{g_b1a, g_b1b, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
-  // stage-2 data gradient (4 stride-parity classes) and weight gradient
-  if (c2_32) {   // split transposed weights packed by the bwd_prep launch
+  // stage-2 data gradient (4 stride-parity classes, split transposed weights packed by
+  // the bwd_prep launch) and weight gradient, both on split-fp16 operands
+  {
     DgCls cls{};
     for (int c = 0; c < 4; ++c) {
       const int qt = c >> 1, qf = c & 1;
       const int Pc = d.B * ((d.T1 - qt + 1) / 2) * ((d.F1 - qf + 1) / 2);
       cls.boff[c + 1] = cls.boff[c] + (Pc + kD2Px - 1) / kD2Px;
     }
-    if (dg16)
-      hipLaunchKernelGGL(conv2_dgrad32_kernel<true>, dim3(cls.boff[4]), dim3(64 * kD2Waves), 0, st, w.g_ab,
-                         (const void*)wq2h, d, cls, w.g_x1, (const float*)w.gmax, kBnBlocks, (const float*)w.wdsc);
-    else
-      hipLaunchKernelGGL(conv2_dgrad32_kernel<false>, dim3(cls.boff[4]), dim3(64 * kD2Waves), 0, st, w.g_ab,
-                         (const void*)wq3, d, cls, w.g_x1, (const float*)nullptr, 0, (const float*)nullptr);
+    hipLaunchKernelGGL(conv2_dgrad32_kernel<true>, dim3(cls.boff[4]), dim3(64 * kD2Waves), 0, st, w.g_ab,
+                       (const void*)wq2h, d, cls, w.g_x1, (const float*)w.gmax, kBnBlocks, (const float*)w.wdsc);
     SRF_LAUNCH_CHECK("conv2_dgrad32");
-  } else {
-  hipLaunchKernelGGL(pack_w2t_kernel, dim3((9 * 2 * C * C + 255) / 256), dim3(256), 0, st, k1a, k1b, w.wq);
-  SRF_LAUNCH_CHECK("pack_w2t");
-  for (int qt = 0; qt < 2; ++qt) {
-    for (int qf = 0; qf < 2; ++qf) {
-      const int Pc = d.B * ((d.T1 - qt + 1) / 2) * ((d.F1 - qf + 1) / 2);
-      if (Pc <= 0) continue;
-      hipLaunchKernelGGL(conv2_dgrad_kernel, dim3((Pc + 63) / 64), dim3(256), 0, st, w.g_ab, w.wq, d, qt, qf,
-                         w.g_x1);
-      SRF_LAUNCH_CHECK("conv2_dgrad");
-    }
-  }
   }
   const WgDiv dv{make_fastdiv(d.F2), make_fastdiv(d.T2)};
-  int nsplit = kWgradSplits;
-  static const bool wg32 = [] {
-    const char* e = getenv("SRF_WGRAD32");
-    return !(e && e[0] == '0');
-  }();
-  if (use_conv2_32() && wg32) {
+  const int nsplit = kWgrad32Splits;
+  {
     static_assert(kW2Chunk == kWgChunk, "wgrad splits are whole chunks");
-    nsplit = wgrad32_splits();
     const int split_len = ((P2 + nsplit - 1) / nsplit + kWgChunk - 1) / kWgChunk * kWgChunk;
-    // split-fp16 weight gradient with the split-fp16 data gradient (SRF_DGRAD_F16=0: split-bf16)
-    if (dg16) {
-      hipLaunchKernelGGL(gab_split_t_kernel<true>, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p,
-                         (void*)w.gsT3, (const float*)w.gmax, kBnBlocks);
-      SRF_LAUNCH_CHECK("gab_split_t");
-      hipLaunchKernelGGL(conv2_wgrad32_kernel<true>, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len,
-                         (const void*)w.gsT3, w.P2p, d, dv, nsplit, split_len, w.wpart, (const float*)w.gmax,
-                         kBnBlocks);
-    } else {
-      hipLaunchKernelGGL(gab_split_t_kernel<false>, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p,
-                         (void*)w.gsT3, (const float*)nullptr, 0);
-      SRF_LAUNCH_CHECK("gab_split_t");
-      hipLaunchKernelGGL(conv2_wgrad32_kernel<false>, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len,
-                         (const void*)w.gsT3, w.P2p, d, dv, nsplit, split_len, w.wpart, (const float*)nullptr, 0);
-    }
+    hipLaunchKernelGGL(gab_split_t_kernel<true>, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p,
+                       (void*)w.gsT3, (const float*)w.gmax, kBnBlocks);
+    SRF_LAUNCH_CHECK("gab_split_t");
+    hipLaunchKernelGGL(conv2_wgrad32_kernel<true>, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len,
+                       (const void*)w.gsT3, w.P2p, d, dv, nsplit, split_len, w.wpart, (const float*)w.gmax,
+                       kBnBlocks);
     SRF_LAUNCH_CHECK("conv2_wgrad32");
-  } else {
-    const int split_len = ((P2 + nsplit - 1) / nsplit + kWgChunk - 1) / kWgChunk * kWgChunk;
-    hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(9 * nsplit), dim3(256), 0, st, sv.y1, sv.stats1, inp_len, w.g_ab, d,
-                       dv, nsplit, split_len, w.wpart);
-    SRF_LAUNCH_CHECK("conv2_wgrad");
   }
   hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((9 * C * 2 * C + 255) / 256), dim3(256), 0, st, w.wpart,
                      nsplit, g_k1a, g_k1b);

@@ -429,13 +429,10 @@ int srf_ctc_loss(const float* logits, const int* labels, const int* label_len, c
   const bool lp_in_lds = (shmem + lp_bytes) <= 96 * 1024;
   if (lp_in_lds) shmem += lp_bytes;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // wave-resident recursion for up to 512 extended-label states, else the block loop;
-  // SRF_CTC_WAVE=0 selects the block loop (A/B, tests)
-  const char* ev = getenv("SRF_CTC_WAVE");
-  const bool wave = !(ev && ev[0] == '0');
+  // wave-resident recursion for up to 512 extended-label states, else the block loop
   auto pick = [&](auto lds) {
     constexpr bool LDS = decltype(lds)::value;
-    return !wave || Smax > 512 ? ctc_recursion_kernel<0, LDS>
+    return Smax > 512 ? ctc_recursion_kernel<0, LDS>
            : Smax <= 128      ? ctc_recursion_kernel<2, LDS>
            : Smax <= 256      ? ctc_recursion_kernel<4, LDS>
                               : ctc_recursion_kernel<8, LDS>;

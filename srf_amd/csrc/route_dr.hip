@@ -884,22 +884,21 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
 // flushed into g_emb by one atomic add per element, as in route_gux_kernel.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 constexpr int kGux16NW = 4;
 
 __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// PROD (SRF_GUX16=2, A/B): gx = c^0 W^T gs^0 + sum_r c^r W^T gs^r + gL^r W^T Vc^r as
-// 2R - 1 products with capsule-independent B operands -- the frame vectors, scaled
-// per (vector, frame) and split once in the prologue -- combined in fp32 with the
-// per-frame scalars of the capsule: 6(2R - 1) MFMAs per capsule, no per-capsule split.
-template <int R, bool PROD = false>
+// The lane max of |gu| also goes to *gumax (one atomic max per wave; the caller zeroes
+// it): route_gw16s_kernel takes its per-layer exponent from it.
+template <int R>
 __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
     const float* __restrict__ WT, const float* __restrict__ hdr, int F, int T, int N, int lpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
     const float* __restrict__ gs, float* __restrict__ g_emb, const float* __restrict__ cst,
-    const float* __restrict__ glst, int JP) {
+    const float* __restrict__ glst, int JP, float* __restrict__ gumax) {
   static_assert(R >= 2, "stored couplings exist for iters >= 2");
   constexpr int DIN = 32, RV = R - 1, NW = kGux16NW;
   extern __shared__ __attribute__((aligned(16))) float gacc[];
@@ -954,32 +953,6 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
     for (int k = 0; k < 16; ++k) gsr[0][k] *= c0;
   }
   const int aw = (int)hdr[1];
-  constexpr int NV = PROD ? 2 * R - 1 : 1;
-  h8 pvh[NV][2], pvl[NV][2];   // PROD: split frame vectors gs^0 (c^0 folded), gs^r, Vc^r
-  float pun[NV];               // 2^-(aw + e_v) of the lane's frame
-  if constexpr (PROD) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const float* src = v < R ? gsr[v] : vcr[v - R];
-      float m = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) m = fmaxf(m, fabsf(src[k]));
-      float ma, mb;
-      xpair32(m, ma, mb);
-      const int e = srf_split_exp(fmaxf(ma, mb));
-      const float sc = srf_exp2i(e);
-      pun[v] = srf_exp2i(-(aw + e));
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          _Float16 a1, a2;
-          srf_split2h(src[8 * ks + k] * sc, a1, a2);
-          pvh[v][ks][k] = a1;
-          pvl[v][ks][k] = a2;
-        }
-    }
-  }
   // split W^T planes (prep32_kernel, wt16) [i][tile][h][e][8 rows] hi, then lo: K step
   // ks of the wave is tile 2j + ks, the lane's 16 bytes sit at (h, e = fl)
   const int Fs = srf::fwd32_frame_stride(F);
@@ -1016,38 +989,8 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
   auto advance = [&](int& ww, int& nn_) {
     if (++nn_ == nn) nn_ = 0, ++ww;
   };
-  auto compute_prod = [&](auto slot) {
-    constexpr int sl = decltype(slot)::value;
-    f16v tot = {};
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f16v t = {};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        t = mfma32h(wt_b[sl][ks][0], pvh[v][ks], t);
-        t = mfma32h(wt_b[sl][ks][0], pvl[v][ks], t);
-        t = mfma32h(wt_b[sl][ks][1], pvh[v][ks], t);
-      }
-      const float cf = v == 0 ? pun[0] : (v < R ? c_b[sl][v - 1] : g_b[sl][v - R]) * pun[v];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) tot[q] = fmaf(t[q], cf, tot[q]);
-    }
-    const int ts = loc.t + w - lpad;
-    if (wave_on && loc.valid && ts >= 0 && ts < T) {
-      float* a = slab + (fl + w) * SROW + nl * DIN + 4 * h;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f4 v = {tot[4 * q], tot[4 * q + 1], tot[4 * q + 2], tot[4 * q + 3]};
-        st4(a + 8 * q, ld4(a + 8 * q) + v);
-      }
-    }
-    advance(w, nl);
-  };
+  float gmax = 0.f;
   auto compute = [&](auto slot) {
-    if constexpr (PROD) {
-      compute_prod(slot);
-      return;
-    }
     constexpr int sl = decltype(slot)::value;
     float gu[16];
     float m = 0.f;
@@ -1062,6 +1005,7 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
       gu[k] = a;
       m = fmaxf(m, fabsf(a));
     }
+    gmax = fmaxf(gmax, m);
     float ma, mb;
     xpair32(m, ma, mb);
     const int eg = srf_split_exp(fmaxf(ma, mb));
@@ -1135,6 +1079,9 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
     }
   }
 #undef SRF_GUX16_FETCH
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) gmax = fmaxf(gmax, __shfl_xor(gmax, o, 64));
+  if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(gumax), __float_as_uint(gmax));   // gmax >= 0
   __syncthreads();
   const int f0 = ft * 32 - lpad;
   const int row = nn * DIN;
@@ -1470,34 +1417,11 @@ __global__ __launch_bounds__(256) void route_gw2_kernel(
 //   * at most 168 registers, so three workgroups share a CU.
 // The stored couplings and logit gradients are 0 for frames past F (the 32x32
 // passes store zeros there) and x^T is 0 past F, so gu is 0 on padded frames.
-// gW workgroup order.  Plain: frame split fastest, then row group, then capsule chunk.
-// xcd (SRF_GW_XCD=1): the capsule chunks of one (row group, frame split) -- which read
-// the same per-frame vectors -- are consecutive in a per-XCD range of the logical
-// order (dispatch places block b on XCD b % 8, a speed-only assumption), so they run
-// together behind one L2.
-__device__ __forceinline__ void gw_block(int xcd, int S, int n_rt, int& s, int& rtg, int& cc) {
-  int L = blockIdx.x;
-  if (xcd) {
-    const int nb = gridDim.x, per = nb / 8;
-    if (L < per * 8) L = (L % 8) * per + L / 8;
-    const int ncc = nb / (S * n_rt);
-    cc = L % ncc;
-    L /= ncc;
-    s = L % S;
-    rtg = L / S;
-  } else {
-    s = L % S;
-    L /= S;
-    rtg = L % n_rt;
-    cc = L / n_rt;
-  }
-}
-
 template <int D, int R, int CAP>
 __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_kernel(
     const float* __restrict__ xT, const float* __restrict__ saved, const float* __restrict__ gs,
     const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp, int in_n, int J, int mask_first,
-    int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride, int xcd) {
+    int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride) {
   static_assert(R >= 2, "stored couplings exist for iters >= 2");
   constexpr int NCT = (D + 15) / 16;
   constexpr int RV = R - 1;
@@ -1522,8 +1446,11 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
   const size_t cblk = (size_t)in_n * JP * Fs;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l16 = lane & 15, kk = lane >> 4;
-  int s, rtg, cc;
-  gw_block(xcd, S, n_rt, s, rtg, cc);
+  int L = blockIdx.x;   // frame split fastest, then row group, then capsule chunk
+  const int s = L % S;
+  L /= S;
+  const int rtg = L % n_rt;
+  const int cc = L / n_rt;
   const int tg = rtg * 4 + wv;
   const int row = min(tg * 16 + l16, JD - 1);
   const bool rvalid = tg < NT && tg * 16 + l16 < JD;
@@ -1661,31 +1588,36 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
   }
 }
 
-// gW pass on 32x32x16 split-fp16 MFMA (din = dout = 32; route_gux16_kernel's
-// scheme with K = frames): gW^T_i[e][row] = sum_f x_i^T[e][f] gu_i[f][row].
-//   * x' = 2^bx x (the forward's exponent, hdr[2]), split once per tile by the
-//     staging threads into fp16 hi / lo planes in LDS;
-//   * gu (formed from the per-frame vectors and the staged c^r / gL^r) scaled per
-//     row and 16-frame K step by 2^eg (the row's max |gu| over those frames), split;
-//   * three MFMAs per capsule and K step into a temporary tile that is added to the
-//     fp32 sum scaled back by 2^-(bx + eg) (the K steps carry different scales).
+// gW pass on 32x32x16 split-fp16 MFMA (din = dout = 32, iters 2..3 with stored
+// couplings: the C3 / C4 DR layers): gW^T_i[e][row] = sum_f x_i^T[e][f] gu_i[f][row].
+//   * x' = 2^bx x (the forward's exponent, hdr[2]), split by the forward's prep into
+//     fp16 hi / lo planes blocked per 16 frames (xt16: [i][f/16][hi|lo][e][16]);
+//   * gu' = 2^eg gu with ONE exponent for the layer, from max|gu| that the gx pass
+//     (route_gux16_kernel) leaves in *gumax, so max|gu'| < 2^14; split into fp16
+//     hi / lo by masking: hi = gu' with its low 13 mantissa bits cleared (exact in
+//     fp16 in the normal range), lo = f16(gu' - hi).  Products of one exponent pair
+//     sum straight into the fp32 accumulator: three MFMAs per capsule and 16-frame K
+//     step (x1 g1 + x1 g2 + x2 g1, the dropped x2 g2 <= 2^-21 |x' gu'|), scaled back by
+//     2^-(bx + eg) once at the end.  Errors are absolute at the layer's scale (below
+//     2^-24 of max|x'| max|gu'| per product), as in the forward's per-tensor split.
 // Workgroup = 4 waves x 32 rows (one output capsule j each) x CAP capsules x one of S
 // frame splits; lane l holds row 32j + (l & 31) and frames 8(l >> 5) + 0..7 of each
-// K step (B map), e = 8q + 4(l >> 5) + 0..3 of its C map.  Tile t + 1 is staged while
-// tile t computes (one barrier per tile), the per-frame vectors one tile ahead.
-// LDS x planes: row e = 16 halves = two 8-half chunks, chunk c of row e at
-// c ^ ((e >> 3) & 1): the ds_read_b128 lane groups then cover 64 distinct banks.
+// K step (B map), e = 8q + 4(l >> 5) + 0..3 of its C map.  Tile t + 1's couplings and
+// x planes are staged while tile t computes (one barrier per tile), the per-frame
+// vectors one tile ahead in registers.  LDS x planes: row e = 16 halves = two 8-half
+// chunks, chunk c of row e at c ^ ((e >> 3) & 1): the ds_read_b128 lane groups then
+// cover 64 distinct banks.
 constexpr int kGw16Cap = 4;
 template <int R, int CAP>
-__global__ __launch_bounds__(256, 2) void route_gw16_kernel(
-    const float* __restrict__ xT, const float* __restrict__ hdr, const float* __restrict__ saved,
-    const float* __restrict__ gs, const float* __restrict__ cst, const float* __restrict__ glst, int F, int Fp,
-    int in_n, int J, int mask_first, int JP, int n_rt, int S, int ft_per, float* __restrict__ gwp,
-    float* __restrict__ gbp, size_t pstride, int xcd) {
-  static_assert(R >= 2, "stored couplings exist for iters >= 2");
+__global__ __launch_bounds__(256, 2) void route_gw16s_kernel(
+    const _Float16* __restrict__ x16, const float* __restrict__ hdr, const float* __restrict__ gumax,
+    const float* __restrict__ saved, const float* __restrict__ gs, const float* __restrict__ cst,
+    const float* __restrict__ glst, int F, int Fp, int in_n, int J, int mask_first, int JP, int n_rt, int S,
+    int ft_per, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride) {
+  static_assert(R >= 2 && R <= 3, "stored couplings exist for iters >= 2; registers hold R <= 3");
   constexpr int D = 32, RV = R - 1;
   constexpr int CG = RV * 2 * 4 * 16;    // couplings per capsule: [r][c|gl][4 j][16 frames] floats
-  constexpr int PQ = CG / 4 + D * 4;     // float4 staged per capsule (couplings + x^T [e][16])
+  constexpr int PQ = CG / 4 + 128;       // 16-byte pieces staged per capsule (couplings + x hi/lo)
   constexpr int PCB = CG * 4 + 2 * D * 16 * 2;   // LDS bytes per capsule: couplings, x hi, x lo
   constexpr int NQ = (CAP * PQ + 255) / 256;
   __shared__ __attribute__((aligned(16))) unsigned char stg[2][CAP * PCB];
@@ -1695,8 +1627,11 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
   const size_t cblk = (size_t)in_n * JP * Fs;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n = lane & 31, h = lane >> 5;
-  int s, rtg, cc;
-  gw_block(xcd, S, n_rt, s, rtg, cc);
+  int b = blockIdx.x;
+  const int s = b % S;
+  b /= S;
+  const int rtg = b % n_rt;
+  const int cc = b / n_rt;
   const int jw = rtg * 4 + wv;
   const bool wave_on = jw < J;
   const int j = min(jw, J - 1);
@@ -1707,16 +1642,16 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
   const int NFT = Fp >> 4;
   const int ft0 = s * ft_per, ft1 = min(NFT, ft0 + ft_per);
   const int bx = (int)hdr[2];
-  const float sx = srf_exp2i(bx);
+  const int eg = srf_split_exp(*gumax);
+  const float sg = srf_exp2i(eg);
 
-  // staging: float4 q of a tile <-> (capsule k, part): couplings (r, c|gl, jw, frame
-  // quad) or x^T (e, frame quad); per-thread sources fixed, tile t + 1 is 16 floats on
-  const float* src[NQ];
-  int dst[NQ];     // LDS byte offset; x parts: of the hi plane (lo = + D*16*2)
-  bool isx[NQ];
-  // the CAP * CG / 4 coupling float4s first, then the x^T ones: at RV = 2, CAP = 4 each
-  // thread's q = 0 is a coupling and q >= 1 an x^T float4 (no branch in stage_store)
+  // staging: 16-byte piece q of a tile <-> (capsule k, part): couplings (r, c|gl, jq,
+  // frame quad) or an x chunk (plane, e, 8-frame half); per-thread sources fixed, the
+  // next tile is 64 bytes (couplings) or 2 KiB (x planes) on
   constexpr int NCPL = CAP * CG / 4;
+  const char* src[NQ];
+  int dst[NQ];
+  int step[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int idx = min(q * 256 + (int)threadIdx.x, CAP * PQ - 1);
@@ -1725,44 +1660,30 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
       const int i = i0 + min(k, ncap - 1);
       const int fq = rem & 3, jq = (rem >> 2) & 3, cg = rem >> 4;   // cg = r * 2 + (0: c, 1: gL)
       const int jj = min(rtg * 4 + jq, JP - 1);
-      src[q] = ((cg & 1) ? glst : cst) + (size_t)(cg >> 1) * cblk + ((size_t)i * JP + jj) * Fs + 4 * fq;
+      src[q] = reinterpret_cast<const char*>(((cg & 1) ? glst : cst) + (size_t)(cg >> 1) * cblk +
+                                             ((size_t)i * JP + jj) * Fs + 4 * fq);
       dst[q] = k * PCB + rem * 16;
-      isx[q] = false;
+      step[q] = 64;
     } else {
-      const int x = idx - NCPL, k = x / (D * 4), xr = x - k * (D * 4), e = xr >> 2, fq = xr & 3;
+      const int x = idx - NCPL, k = x >> 7, xr = x & 127;
+      const int p = xr >> 6, e = (xr >> 1) & 31, hf = xr & 1;
       const int i = i0 + min(k, ncap - 1);
-      src[q] = xT + ((size_t)i * D + e) * Fp + 4 * fq;
-      dst[q] = k * PCB + CG * 4 + (e * 16 + (((fq >> 1) ^ ((e >> 3) & 1)) * 8) + (fq & 1) * 4) * 2;
-      isx[q] = true;
+      src[q] = reinterpret_cast<const char*>(x16 + (((size_t)i * NFT * 2 + p) * 32 + e) * 16 + hf * 8);
+      dst[q] = k * PCB + CG * 4 + p * (D * 16 * 2) + (e * 16 + ((hf ^ ((e >> 3) & 1)) * 8)) * 2;
+      step[q] = 2 * 32 * 16 * 2;
     }
   }
   f4 sv[NQ];
   auto stage_load = [&](int ft) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) sv[q] = ld4(src[q] + ft * 16);
+    for (int q = 0; q < NQ; ++q) sv[q] = *reinterpret_cast<const f4*>(src[q] + (size_t)ft * step[q]);
   };
   auto stage_store = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int idx = q * 256 + threadIdx.x;
       if ((CAP * PQ) % 256 != 0 && idx >= CAP * PQ) continue;
-      unsigned char* p = &stg[buf][dst[q]];
-      const bool xq = q * 256 >= NCPL ? true : (q + 1) * 256 <= NCPL ? false : isx[q];
-      if (xq) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        h4 a, c;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          _Float16 a1, a2;
-          srf_split2h(sv[q][v] * sx, a1, a2);
-          a[v] = a1;
-          c[v] = a2;
-        }
-        *reinterpret_cast<h4*>(p) = a;
-        *reinterpret_cast<h4*>(p + D * 16 * 2) = c;
-      } else {
-        *reinterpret_cast<f4*>(p) = sv[q];
-      }
+      *reinterpret_cast<f4*>(&stg[buf][dst[q]]) = sv[q];
     }
   };
   // per-frame vectors of the lane's row, frames 8h + 0..7 of a tile: buffer loads, 0 past F
@@ -1790,10 +1711,10 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
   };
 
   f16v acc[CAP];
-  float gb[CAP];
+  f2 gb[CAP];
 #pragma unroll
   for (int k = 0; k < CAP; ++k) {
-    gb[k] = 0.f;
+    gb[k] = f2{0.f, 0.f};
     acc[k] = f16v{};
   }
   if (ft0 < ft1) {
@@ -1803,13 +1724,17 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
     if (ft0 + 1 < ft1) stage_load(ft0 + 1);
   }
   const int xoff = CG * 4 + (n * 16 + ((h ^ ((n >> 3) & 1)) * 8)) * 2;
+  const float s0 = c0 * sg;
   for (int ft = ft0; ft < ft1; ++ft) {
     const int buf = (ft - ft0) & 1;
-    float fv[R + RV][8];
+    // this tile's vectors, scaled by 2^eg (c^0 folded into gs^0): frame pairs (v, v + 1)
+    f2 fv[R + RV][4];
 #pragma unroll
-    for (int a = 0; a < R + RV; ++a)
+    for (int v = 0; v < 4; ++v) {
+      fv[0][v] = f2{nx[0][2 * v], nx[0][2 * v + 1]} * s0;
 #pragma unroll
-      for (int v = 0; v < 8; ++v) fv[a][v] = nx[a][v];
+      for (int a = 1; a < R + RV; ++a) fv[a][v] = f2{nx[a][2 * v], nx[a][2 * v + 1]} * sg;
+    }
     __syncthreads();   // tile ft staged in buf; buf ^ 1 (tile ft - 1) is free
     if (ft + 1 < ft1) {
       stage_store(buf ^ 1);
@@ -1821,67 +1746,58 @@ __global__ __launch_bounds__(256, 2) void route_gw16_kernel(
     for (int k = 0; k < CAP; ++k) {
       const unsigned char* ck = sb + k * PCB;
       const float* ckf = reinterpret_cast<const float*>(ck);
-      float gu[8];
+      f2 gu[4];
 #pragma unroll
-      for (int v = 0; v < 8; ++v) gu[v] = c0 * fv[0][v];
+      for (int v = 0; v < 4; ++v) gu[v] = fv[0][v];
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
         const float* cp = ckf + ((r * 2 + 0) * 4 + wv) * 16 + 8 * h;
         const float* gp = ckf + ((r * 2 + 1) * 4 + wv) * 16 + 8 * h;
         const f4 ca = ld4(cp), cb = ld4(cp + 4), ga = ld4(gp), gbv = ld4(gp + 4);
+        const f2 c2[4] = {f2{ca[0], ca[1]}, f2{ca[2], ca[3]}, f2{cb[0], cb[1]}, f2{cb[2], cb[3]}};
+        const f2 g2[4] = {f2{ga[0], ga[1]}, f2{ga[2], ga[3]}, f2{gbv[0], gbv[1]}, f2{gbv[2], gbv[3]}};
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          gu[v] = fmaf(ca[v], fv[r + 1][v], gu[v]);
-          gu[v] = fmaf(ga[v], fv[R + r][v], gu[v]);
-          gu[v + 4] = fmaf(cb[v], fv[r + 1][v + 4], gu[v + 4]);
-          gu[v + 4] = fmaf(gbv[v], fv[R + r][v + 4], gu[v + 4]);
+          gu[v] = __builtin_elementwise_fma(c2[v], fv[r + 1][v], gu[v]);
+          gu[v] = __builtin_elementwise_fma(g2[v], fv[R + r][v], gu[v]);
         }
       }
-      float m = 0.f, sum = 0.f;
-#pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        m = fmaxf(m, fabsf(gu[v]));
-        sum += gu[v];
-      }
-      gb[k] += sum;
-      float ma, mb;
-      xpair32(m, ma, mb);
-      const int eg = srf_split_exp(fmaxf(ma, mb));
-      const float sg = srf_exp2i(eg);
+      gb[k] += (gu[0] + gu[1]) + (gu[2] + gu[3]);
       h8 bh, bl;
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        _Float16 a1, a2;
-        srf_split2h(gu[v] * sg, a1, a2);
-        bh[v] = a1;
-        bl[v] = a2;
+      for (int v = 0; v < 4; ++v) {
+        // hi: the low 13 mantissa bits cleared (exact in fp16); lo = f16(gu' - hi)
+        const f2 hi = __builtin_bit_cast(f2, __builtin_bit_cast(u2, gu[v]) & 0xFFFFE000u);
+        const f2 lo = gu[v] - hi;
+        const h2 ph = __builtin_convertvector(hi, h2);   // v_cvt_pk_f16_f32 (exact for hi)
+        const h2 pl = __builtin_convertvector(lo, h2);
+        bh[2 * v] = ph[0];
+        bh[2 * v + 1] = ph[1];
+        bl[2 * v] = pl[0];
+        bl[2 * v + 1] = pl[1];
       }
       const h8 xh = *reinterpret_cast<const h8*>(ck + xoff);
       const h8 xl = *reinterpret_cast<const h8*>(ck + xoff + D * 16 * 2);
-      f16v t = {};
-      t = mfma32h(xh, bh, t);
-      t = mfma32h(xh, bl, t);
-      t = mfma32h(xl, bh, t);
-      const float un = srf_exp2i(-(bx + eg));
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[k][v] = fmaf(t[v], un, acc[k][v]);
-      __builtin_amdgcn_sched_barrier(0);   // one capsule in flight at a time (registers)
+      acc[k] = mfma32h(xh, bh, acc[k]);
+      acc[k] = mfma32h(xh, bl, acc[k]);
+      acc[k] = mfma32h(xl, bh, acc[k]);
     }
   }
   float* gw = gwp + (size_t)s * pstride;
   float* gbo = gbp + (size_t)s * pstride;
+  const float un = srf_exp2i(-(bx + eg)), ug = srf_exp2i(-eg);
 #pragma unroll
   for (int k = 0; k < CAP; ++k) {
-    const float a = gb[k];
+    const float a = gb[k][0] + gb[k][1];
     float pa, pb;
     xpair32(a, pa, pb);
     if (k >= ncap || !wave_on) continue;
     const int i = i0 + k;
-    if (h == 0) gbo[(size_t)i * JD + row] = pa + pb;
+    if (h == 0) gbo[(size_t)i * JD + row] = (pa + pb) * ug;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       st4(gw + ((size_t)i * JD + row) * D + 8 * q + 4 * h,
-          f4{acc[k][4 * q], acc[k][4 * q + 1], acc[k][4 * q + 2], acc[k][4 * q + 3]});
+          f4{acc[k][4 * q] * un, acc[k][4 * q + 1] * un, acc[k][4 * q + 2] * un, acc[k][4 * q + 3] * un});
   }
 }
 
@@ -2092,12 +2008,11 @@ inline size_t gux16_lds_bytes(const Geom& g, int n_per) {
 }
 constexpr size_t kGux16LdsMax = (160 / SRF_GUX16_OCC - 4) * 1024;   // SRF_GUX16_OCC workgroups per CU
 // route_gux16_kernel (split-fp16 32x32 tiles) for din = dout = 32 with stored
-// couplings; SRF_GUX16=0 keeps route_gux_kernel (A/B).  Read by the forward too: its
-// prep then writes the kernel's split W^T planes in place of the fp32 W^T, so the
-// switch must not change between a layer's forward and backward.
+// couplings (route_gux_kernel otherwise).  A function of the geometry only: the
+// forward's prep writes the kernel's split W^T planes in place of the fp32 W^T under
+// the same test.
 inline bool use_gux16(const Geom& g) {
-  const char* e = getenv("SRF_GUX16");   // read per launch (tests toggle it)
-  return !(e && e[0] == '0') && g.din == 32 && g.dout == 32 && g.iters >= 2 && g.iters <= 4 &&   // R = 5 spills
+  return g.din == 32 && g.dout == 32 && g.iters >= 2 && g.iters <= 4 &&   // R = 5 spills
          gux16_lds_bytes(g, 1) <= kGux16LdsMax;
 }
 // n-chunk size: fewest rounds of two workgroups per CU, then fewest capsules each
@@ -2121,29 +2036,23 @@ int gux16_n_per(const Geom& g) {
 
 template <int R>
 void launch_gux16(const Geom& g, const float* WT, const float* hdr, const float* saved, const float* gs,
-                  float* g_emb, const float* cst, const float* glst, int JP, hipStream_t st) {
+                  float* g_emb, const float* cst, const float* glst, int JP, float* gumax, hipStream_t st) {
   const int n_wgroups = (g.J + kGux16NW - 1) / kGux16NW;
   const int n_per = gux16_n_per(g);
   const int n_chunks = (g.N + n_per - 1) / n_per;
   const int grid = (g.F() + 31) / 32 * n_wgroups * n_chunks;
-  const char* e = getenv("SRF_GUX16");
-  if (R <= 3 && e && e[0] == '2')   // the product form (A/B; R = 4 would not fit the registers)
-    hipLaunchKernelGGL((route_gux16_kernel<(R <= 3 ? R : 3), true>), dim3(grid), dim3(64 * kGux16NW),
-                       gux16_lds_bytes(g, n_per), st, WT, hdr, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first,
-                       n_wgroups, n_chunks, n_per, saved, gs, g_emb, cst, glst, JP);
-  else
-    hipLaunchKernelGGL((route_gux16_kernel<R>), dim3(grid), dim3(64 * kGux16NW), gux16_lds_bytes(g, n_per), st, WT,
-                       hdr, g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved,
-                       gs, g_emb, cst, glst, JP);
+  hipLaunchKernelGGL((route_gux16_kernel<R>), dim3(grid), dim3(64 * kGux16NW), gux16_lds_bytes(g, n_per), st, WT, hdr,
+                     g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, g_emb,
+                     cst, glst, JP, gumax);
 }
 
 template <int D, int R>
 void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
                const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st,
-               const float* cst, const float* glst, int JP, const float* hdr = nullptr) {
+               const float* cst, const float* glst, int JP, const float* hdr = nullptr, float* gumax = nullptr) {
   if constexpr (R >= 2 && D == 32) {
-    if (cst != nullptr && hdr != nullptr && use_gux16(g)) {
-      launch_gux16<R>(g, WT, hdr, saved, gs, g_emb, cst, glst, JP, st);
+    if (cst != nullptr && hdr != nullptr && gumax != nullptr && use_gux16(g)) {
+      launch_gux16<R>(g, WT, hdr, saved, gs, g_emb, cst, glst, JP, gumax, st);
       return;
     }
   }
@@ -2178,13 +2087,14 @@ void launch_gu(const Geom& g, const float* emb, const float* W, const float* WT,
 template <int D>
 void launch_gu_r(const Geom& g, const float* emb, const float* W, const float* WT, const float* bias,
                  const float* saved, const float* gs, const float* stats, float* gu_t, float* g_emb, hipStream_t st,
-                 const float* cst = nullptr, const float* glst = nullptr, int JP = 0, const float* hdr = nullptr) {
+                 const float* cst = nullptr, const float* glst = nullptr, int JP = 0, const float* hdr = nullptr,
+                 float* gumax = nullptr) {
   switch (g.iters) {
     case 1: launch_gu<D, 1>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, nullptr, nullptr, 0); break;
-    case 2: launch_gu<D, 2>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
-    case 3: launch_gu<D, 3>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
-    case 4: launch_gu<D, 4>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
-    default: launch_gu<D, 5>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr); break;
+    case 2: launch_gu<D, 2>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr, gumax); break;
+    case 3: launch_gu<D, 3>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr, gumax); break;
+    case 4: launch_gu<D, 4>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr, gumax); break;
+    default: launch_gu<D, 5>(g, emb, W, WT, bias, saved, gs, stats, gu_t, g_emb, st, cst, glst, JP, hdr, gumax); break;
   }
 }
 
@@ -2197,34 +2107,22 @@ struct Gw2Plan {
 
 inline int gw2_cap_rt(int d) { return d <= 16 ? 8 : (d == 32 ? 4 : 2); }
 
-// route_gw3_kernel (default; SRF_GW3=0 selects route_gw2_kernel) with SRF_GW3_CAP
-// capsules per workgroup (8 or 4).
+// route_gw3_kernel (iters 2..3, din <= 32): 8 capsules per workgroup for din <= 16,
+// 4 for din 32 (two 16-column accumulators per capsule; 8 measured the same at C4);
+// 0: route_gw2_kernel (deeper routing spills at 168 registers, din 64).
 inline int gw3_cap(const Geom& g) {
-  static const int v = [] {
-    const char* e = getenv("SRF_GW3");
-    if (e && e[0] == '0') return 0;
-    const char* c = getenv("SRF_GW3_CAP");
-    return (c && atoi(c) == 4) ? 4 : 8;
-  }();
-  if (g.iters > 3 || v == 0) return 0;   // deeper routing spills at 168 registers
-  if (g.din <= 16) return v;
-  if (g.din != 32) return 0;
-  static const int v32 = [] {   // din 32: two 16-column accumulators per capsule (SRF_GW3_CAP32=8 for A/B)
-    const char* c = getenv("SRF_GW3_CAP32");
-    return (c && atoi(c) == 8) ? 8 : 4;
-  }();
-  return v32;
+  if (g.iters > 3) return 0;
+  return g.din <= 16 ? 8 : g.din == 32 ? 4 : 0;
 }
 
-// route_gw16_kernel (split-fp16 32x32 tiles) for din = dout = 32, iters 2..3 with
-// stored couplings, opt-in (SRF_GW16=1): at C4 it measured 9.81 against 9.68 ms per
-// step with route_gw3_kernel (276 vs 250 us per launch).
-inline bool use_gw16(const Geom& g) {
-  const char* e = getenv("SRF_GW16");   // read per launch (tests toggle it)
-  return (e && e[0] == '1') && g.din == 32 && g.dout == 32 && g.iters >= 2 && g.iters <= 3;
-}
+// route_gw16s_kernel (split-fp16 32x32 tiles, one gu exponent per layer from the gx
+// pass) wherever route_gux16_kernel runs and the routing has at most 3 iterations: the
+// C3 / C4 DR layers.  A function of the geometry only: the forward's prep writes the
+// x^T planes this kernel reads (xt16) under the same test.
+inline bool use_gw16s(const Geom& g) { return use_gux16(g) && g.iters <= 3; }
 
-Gw2Plan gw2_plan_for(const Geom& g, bool g16) {
+Gw2Plan gw2_plan(const Geom& g) {
+  const bool g16 = use_gw16s(g);
   Gw2Plan p{};
   const int NT = g.NT();
   const int NCT = g16 ? 2 : (g.din + 15) / 16;
@@ -2232,21 +2130,19 @@ Gw2Plan gw2_plan_for(const Geom& g, bool g16) {
   p.cap = g16 ? kGw16Cap : gw3_cap(g) ? gw3_cap(g) : gw2_cap_rt(g.din);
   // workgroups resident at once; route_gw3_kernel (latency-bound) is planned for two
   // resident rounds: at C4 S = 8 frame splits (1280 workgroups) beat S = 4 (640, one
-  // round) by 2 %, at C2 the slab term keeps S = 5; route_gw16_kernel: two per CU
-  const int slots = g16 ? 2 * 512 : gw3_cap(g) ? 2 * 768 : 512;
+  // round) by 2 %, at C2 the slab term keeps S = 5; route_gw16s_kernel: two per CU
+  const int slots = g16 ? 512 : gw3_cap(g) ? 2 * 768 : 512;
+  const double per_tile = g16 ? 120.0 : 200.0;   // cycles per capsule, K step and column tile
   p.n_cc = (g.in_n() + p.cap - 1) / p.cap;
   const int NFT = padded_frames(g) / 16;
   p.pstride = (size_t)g.in_n() * g.JD() * (g.din + 1);
-  const char* fs = getenv("SRF_GW2_SPLITS");
-  const int forced = fs ? atoi(fs) : 0;
   const int base = p.n_rt * p.n_cc;
   double best = 1e30;
   for (int S0 = 1; S0 <= NFT; ++S0) {
-    if (forced > 0 && S0 != std::min(forced, NFT)) continue;
     const int ft_per = (NFT + S0 - 1) / S0;
     const int S = (NFT + ft_per - 1) / ft_per;
     const int rounds = (base * S + slots - 1) / slots;
-    const double work = (double)rounds * ft_per * p.cap * NCT * 200.0 / 2.4e9;
+    const double work = (double)rounds * ft_per * p.cap * NCT * per_tile / 2.4e9;
     const double slab = S > 1 ? 2.0 * S * p.pstride * 4 / 4e12 : 0.0;
     if (work + slab < best) {
       best = work + slab;
@@ -2256,34 +2152,27 @@ Gw2Plan gw2_plan_for(const Geom& g, bool g16) {
   }
   return p;
 }
-Gw2Plan gw2_plan(const Geom& g) { return gw2_plan_for(g, use_gw16(g)); }
-inline int gw_xcd() {
-  const char* e = getenv("SRF_GW_XCD");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-// partial-slab floats for either gW kernel (the workspace must not depend on SRF_GW16)
-size_t gw2_part_floats(const Geom& g) {
-  size_t n = gw2_plan_for(g, false).S;
-  if (g.din == 32 && g.dout == 32) n = std::max(n, (size_t)gw2_plan_for(g, true).S);
-  return n * gw2_plan_for(g, false).pstride;
-}
+size_t gw2_part_floats(const Geom& g) { return (size_t)gw2_plan(g).S * gw2_plan(g).pstride; }
 
 template <int D>
 int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* saved, const float* gs,
                const float* cst, const float* glst, int JP, float* gwp, float* gbp, hipStream_t st,
-               const float* hdr = nullptr) {
+               const float* hdr = nullptr, const float* gumax = nullptr) {
   const int grid = p.n_rt * p.n_cc * p.S;
   if constexpr (D == 32) {
-    if (hdr != nullptr && use_gw16(g) && p.cap == kGw16Cap) {
+    if (use_gw16s(g)) {
+      SRF_REQUIRE(hdr != nullptr && gumax != nullptr, "route_gw16s: needs the forward's header and the gx pass's max");
+      const _Float16* x16 = reinterpret_cast<const _Float16*>(xT);
+#define SRF_GW16S(R_)                                                                                              \
+  hipLaunchKernelGGL((route_gw16s_kernel<R_, kGw16Cap>), dim3(grid), dim3(256), 0, st, x16, hdr, gumax, saved, gs, \
+                     cst, glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, \
+                     gbp, p.pstride)
       if (g.iters == 2)
-        hipLaunchKernelGGL((route_gw16_kernel<2, kGw16Cap>), dim3(grid), dim3(256), 0, st, xT, hdr, saved, gs, cst,
-                           glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp,
-                           gbp, p.pstride, gw_xcd());
+        SRF_GW16S(2);
       else
-        hipLaunchKernelGGL((route_gw16_kernel<3, kGw16Cap>), dim3(grid), dim3(256), 0, st, xT, hdr, saved, gs, cst,
-                           glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp,
-                           gbp, p.pstride, gw_xcd());
-      SRF_LAUNCH_CHECK("route_gw16");
+        SRF_GW16S(3);
+#undef SRF_GW16S
+      SRF_LAUNCH_CHECK("route_gw16s");
       return SRF_OK;
     }
   }
@@ -2291,8 +2180,7 @@ int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* sa
     if (gw3_cap(g)) {
 #define SRF_GW3(R_, C_)                                                                                           \
   hipLaunchKernelGGL((route_gw3_kernel<D, R_, C_>), dim3(grid), dim3(256), 0, st, xT, saved, gs, cst, glst, g.F(), \
-                     padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride, \
-                     gw_xcd())
+                     padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, gbp, p.pstride)
 #define SRF_GW3C(R_) \
   if (p.cap == 4) SRF_GW3(R_, 4); else SRF_GW3(R_, 8);
       switch (g.iters) {   // gw3_cap() is 0 past 3 iterations
@@ -2320,13 +2208,9 @@ int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* sa
   return SRF_OK;
 }
 
-// The 32x32 split-bf16 pass (route_fwd32.hip) serves the shapes it supports;
-// SRF_ROUTE_FWD32=0 in the environment selects route_pass_kernel instead (A/B runs).
-inline bool use_fwd32(const Geom& g) {
-  const char* e = getenv("SRF_ROUTE_FWD32");
-  if (e && e[0] == '0') return false;
-  return srf::fwd32_supported(g.din, g.dout, g.J);
-}
+// The 32x32 split-fp16 passes (route_fwd32.hip) serve the shapes they support,
+// route_pass_kernel (exact fp32 16x16x4 tiles) the others (din 64, J*dout > 1024).
+inline bool use_fwd32(const Geom& g) { return srf::fwd32_supported(g.din, g.dout, g.J); }
 
 // Coupling storage is used when the split-bf16 forward runs and the gu pass from
 // stored couplings (route_gux_kernel) fits its window accumulator in LDS; otherwise
@@ -2369,7 +2253,7 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   void* planes = slab;
   void* scratch = slab;
   if (p32) {
-    plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, n_chunks);
     float *WT = nullptr, *xT = nullptr;
     if (couplings != nullptr) {
       cl = srf::fwd32_cpl_layout(plan, g.F(), g.in_n(), g.din, g.dout, g.J, g.iters);
@@ -2380,7 +2264,8 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
       scratch = static_cast<char*>(static_cast<void*>(slab)) + srf::fwd32_planes_bytes(plan);
     }
     const int rc = srf::fwd32_prepare(plan, emb, W, bias, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, planes,
-                                      scratch, WT, xT, st, WT != nullptr && use_gux16(g));
+                                      scratch, WT, xT, st, WT != nullptr && use_gux16(g),
+                                      xT != nullptr && use_gw16s(g));
     if (rc) return rc;
   } else {
     const int chunk_len = (g.in_n() + n_chunks - 1) / n_chunks;
@@ -2398,9 +2283,8 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
         cst = couplings + cl.c + (size_t)(r - 1) * blk * (plan.JDp / g.dout);
         lzst = couplings + cl.lz + (size_t)(r - 1) * blk;
       }
-      const int rc = srf::fwd32_pass(plan, r == 0, planes, scratch,
-                                     static_cast<char*>(scratch) + srf::fwd32_scratch_bytes(plan), g.B, g.T, g.N,
-                                     g.din, g.lpad, g.rpad, g.J, g.dout, g.mask_first, vc, cst, lzst, st);
+      const int rc = srf::fwd32_pass(plan, r == 0, planes, scratch, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J,
+                                     g.dout, g.mask_first, vc, cst, lzst, st);
       if (rc) return rc;
     } else {
       dispatch_pass<D, MODE_FWD>(g, pc, n_chunks, emb, W, bias, r, vc, r == 0 ? bsum : nullptr, slab, nullptr, 1, st);
@@ -2408,7 +2292,7 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     SRF_LAUNCH_CHECK("route_pass(fwd)");
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev1[r], st));
     launch_fwd_finish<D>(g, p32 ? srf::fwd32_slab(plan, scratch) : slab,
-                         p32 ? srf::fwd32_pass_chunks(plan, r == 0) : n_chunks, vc,
+                         p32 ? plan.n_chunks : n_chunks, vc,
                          saved + (size_t)(2 * r) * FJD, saved + (size_t)(2 * r + 1) * FJD,
                          r == g.iters - 1 ? v_out : nullptr, st);
     SRF_LAUNCH_CHECK("fwd_finish");
@@ -2421,6 +2305,7 @@ struct BwdWs {
   void* p32;          // scratch (bias sums + partial slabs) of the B1 passes from stored couplings
   float* gl;          // gL^r of those passes [iters-1][in_n][JP][Fs], read by the gu / gW passes
   float* gwpart;      // partial gW | gbias slabs of route_gw2_kernel (S frame splits)
+  float* gumax;       // max |gu| of the layer (route_gux16_kernel -> route_gw16s_kernel)
   size_t bytes;
 };
 
@@ -2436,8 +2321,9 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
                ostats = take((size_t)(g.iters - 1) * F * in_n * 2), ogu = take(in_n * (size_t)g.NT() * 16 * Fp),
                oxt = take(in_n * g.din * Fp), owt = take(in_n * JD * g.din);
   size_t op32 = 0, ogl = 0, ogwp = 0;
+  const size_t ogm = take(64);
   if (use_fwd32(g)) {
-    const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, n_chunks);
     op32 = take((srf::fwd32_scratch_bytes(plan) + 3) / 4);
     ogl = take((size_t)std::max(g.iters - 1, 1) * srf::fwd32_frame_stride(g.F()) * in_n * (plan.JDp / g.dout));
     ogwp = take(gw2_part_floats(g));
@@ -2454,6 +2340,7 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   w.p32 = op32 ? (void*)(b + op32) : nullptr;
   w.gl = ogl ? (float*)(b + ogl) : nullptr;
   w.gwpart = ogwp ? (float*)(b + ogwp) : nullptr;
+  w.gumax = (float*)(b + ogm);
   w.bytes = off;
   return w;
 }
@@ -2475,7 +2362,7 @@ int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias,
     float* gwp = direct ? g_W : w.gwpart;
     float* gbp = direct ? g_bias : w.gwpart + (size_t)g.in_n() * g.JD() * g.din;
     int rc = launch_gw2<D>(g, p, couplings + cl.xT, saved, w.gs, couplings + cl.c, w.gl, plan.JDp / g.dout, gwp, gbp,
-                           st, srf::fwd32_hdr(plan, couplings + cl.planes));
+                           st, srf::fwd32_hdr(plan, couplings + cl.planes), w.gumax);
     if (rc || direct) return rc;
     const size_t nw4 = (size_t)g.in_n() * g.JD() * g.din / 4, n4 = p.pstride / 4;
     hipLaunchKernelGGL(gw_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, w.gwpart, p.S, n4, p.pstride, g_W,
@@ -2521,7 +2408,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   srf::Fwd32Cpl cl{};
   if (p32) {
     // B1 from the forward's stored couplings and operand planes on the split-bf16 32x32 tiles
-    plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout);
+    plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, n_chunks);
     cl = srf::fwd32_cpl_layout(plan, g.F(), g.in_n(), g.din, g.dout, g.J, g.iters);
   }
   for (int r = R - 1; r >= 1; --r) {
@@ -2553,10 +2440,11 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
                        w.WT, g_emb, n_emb);
     SRF_LAUNCH_CHECK("transpose_w");
   }
-  if (p32)
+  if (p32) {
+    SRF_HIP_TRY(hipMemsetAsync(w.gumax, 0, sizeof(float), st));
     launch_gu_r<D>(g, emb, W, couplings + cl.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st, couplings + cl.c,
-                   w.gl, plan.JDp / g.dout, srf::fwd32_hdr(plan, couplings + cl.planes));
-  else
+                   w.gl, plan.JDp / g.dout, srf::fwd32_hdr(plan, couplings + cl.planes), w.gumax);
+  } else
     launch_gu_r<D>(g, emb, W, w.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st);
   SRF_LAUNCH_CHECK("route_gu");
   (void)Fp;
@@ -2577,6 +2465,7 @@ int srf_route_dr_set_timing_events(void* const* starts, void* const* stops, int 
 
 int srf_route_dr_auto_chunks(int B, int T, int N, int din, int lpad, int rpad, int J, int dout) {
   Geom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  if (use_fwd32(g)) return srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout).n_chunks;
   return auto_chunks(g, pass_cfg(g).NW);
 }
 
@@ -2591,7 +2480,7 @@ size_t srf_route_dr_fwd_workspace(int B, int T, int N, int din, int lpad, int rp
   size_t need = (size_t)n_chunks * ((size_t)B * T + 1) * J * dout * sizeof(float);
   Geom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
   if (use_fwd32(g))
-    need = std::max(need, srf::fwd32_workspace(srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout)));
+    need = std::max(need, srf::fwd32_workspace(srf::fwd32_plan(B, T, N, din, lpad, rpad, J, dout, n_chunks)));
   return need;
 }
 

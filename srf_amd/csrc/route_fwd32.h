@@ -22,23 +22,19 @@ struct Fwd32Plan {
   int n_chunks, chunk_len, n_ftiles;
   size_t xplane;       // elements per x plane (data + zero row)
   size_t ws_w, ws_b, ws_x, ws_h, ws_bsum, ws_slab;   // workspace regions (bytes)
-  // split passes r >= 1 (route_logit / route_lse / route_acc): NWS waves per workgroup,
-  // n_rb row blocks of 64*NWS rows, n_fb 64-frame blocks, logit i-chunks nchL x clenL
-  bool split;
-  int NWS, n_rb, n_fb, nchL, clenL, nchA, clenA;   // route_acc i-chunks nchA x clenA (its slabs)
-  size_t ws_lg, ws_part, ws_lz;   // logits, row-block partials, logZ (bytes)
 };
 
 bool fwd32_supported(int din, int dout, int J);
-Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout);
+// n_chunks: the input-capsule chunks (workgroups per frame tile) of the routing passes,
+// 0 = the cost model's choice (srf_route_dr_auto_chunks returns it)
+Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int n_chunks = 0);
 // Operand planes (split W, bias, x and their scale header: written by fwd32_prepare,
 // read by every pass)
 // and per-pass scratch (i-chunk bias sums + partial slabs) may live apart: a
 // training forward keeps its planes for the backward (coupling storage).
 size_t fwd32_planes_bytes(const Fwd32Plan& p);
 size_t fwd32_scratch_bytes(const Fwd32Plan& p);
-size_t fwd32_split_bytes(const Fwd32Plan& p);   // logits / partials / logZ of the split passes
-size_t fwd32_workspace(const Fwd32Plan& p);   // planes + scratch + split
+size_t fwd32_workspace(const Fwd32Plan& p);   // planes + scratch
 size_t fwd32_lds(const Fwd32Plan& p);
 float* fwd32_slab(const Fwd32Plan& p, void* scratch);
 // the planes' scale header {2^-(aw+bx), aw, bx} (written by fwd32_prepare)
@@ -47,16 +43,15 @@ const float* fwd32_hdr(const Fwd32Plan& p, const void* planes);
 // sums (two launches per forward: absmax, prep);
 // WT / xT (nullable): also the fp32 W^T [in_n][din][JD] and window^T [in_n][din][Fp]
 // operands of the backward gx / gW contractions; wt16 (din 32): WT instead holds the
-// split-fp16 A planes of route_gux16_kernel (same bytes)
+// split-fp16 A planes of route_gux16_kernel (same bytes); xt16 (din 32): xT instead
+// holds route_gw16s_kernel's blocked split-fp16 B planes [in_n][Fp/16][2][din][16]
+// (same bytes)
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
                   int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
-                  hipStream_t st, bool wt16 = false);
+                  hipStream_t st, bool wt16 = false, bool xt16 = false);
 // one routing pass: partial s over i-chunks into fwd32_slab(p, scratch); passes r >= 1
-// also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr.  With
-// p.split and split_ws (fwd32_split_bytes) a pass r >= 1 runs as the three split kernels.
-// i-chunk slabs a pass leaves for fwd_finish
-inline int fwd32_pass_chunks(const Fwd32Plan& p, bool first) { return !first && p.split ? p.nchA : p.n_chunks; }
-int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, void* split_ws, int B, int T,
+// also store the couplings c^r (cst) and logZ^r (lzst) when cst != nullptr.
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T,
                int N, int din, int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst,
                float* lzst, hipStream_t st);
 // Coupling storage of one training forward (float offsets): c^r [iters-1][in_n][JP][Fs],

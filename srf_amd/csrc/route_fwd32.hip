@@ -180,6 +180,7 @@ struct PrepArgs {
   float* hdr;
   int in_n, JD, JDp, din, n_chunks, chunk_len, F, N, T, lpad, Fp;
   int wt16;            // WT holds route_gux16_kernel's split-fp16 A planes instead of fp32
+  int xt16;            // xT holds route_gw16s_kernel's blocked split-fp16 B planes instead of fp32
   size_t xplane;
   size_t n_a, n_b, n_c, n_d, n_e;   // thread counts of the first five ranges
   size_t n_f, xt_block0;             // xT: 64-frame tiles, one block each from block xt_block0 on
@@ -191,12 +192,23 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
   if (P.n_f && blockIdx.x >= P.xt_block0) {
     // xT[i][e][f] (capsule i = w*N + n of frame f is emb[f + w - lpad][n] inside the
     // utterance, 0 past F): the tile's 64 window rows are read along e (coalesced),
-    // transposed through LDS and written as din runs of 64 consecutive frames
+    // transposed through LDS and written as din runs of 64 consecutive frames.
+    // xt16 (din 32, route_gw16s_kernel): instead fp16 hi / lo planes of 2^bx x in
+    // 16-frame blocks, xT16[i][f / 16][hi | lo][e][16 frames] (1 KiB per plane and
+    // block: the B operand of one K step, read as 16 bytes per lane)
     __shared__ float tile[kXtTile][32 + 1];
+    __shared__ int sbx;
     const int ntile = (P.Fp + kXtTile - 1) / kXtTile;
     const int blk = blockIdx.x - (int)P.xt_block0;
     const int i = blk / ntile, f0 = (blk - i * ntile) * kXtTile;
     const int w = i / P.N, n = i - w * P.N;
+    if (P.xt16 && threadIdx.x < 64) {
+      float m = 0.f;
+      for (int k = threadIdx.x; k < kAbsBlocks; k += 64) m = fmaxf(m, P.part[kAbsBlocks + k]);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      if (threadIdx.x == 0) sbx = split_exp(m);
+    }
     for (int k = threadIdx.x; k < kXtTile * P.din; k += blockDim.x) {
       const int fl = k / P.din, e = k - fl * P.din;
       const int f = f0 + fl;
@@ -209,6 +221,28 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
       tile[fl][e] = v;
     }
     __syncthreads();
+    if (P.xt16) {
+      // item = (16-frame block kb of the tile, e, 8-frame half hf): 8 frames -> 16 bytes per plane
+      const float sc = exp2i(sbx);
+      _Float16* x16 = reinterpret_cast<_Float16*>(P.xT);
+      for (int k = threadIdx.x; k < (kXtTile / 16) * 32 * 2; k += blockDim.x) {
+        const int hf = k & 1, e = (k >> 1) & 31, kb = k >> 6;
+        const int fb = f0 + kb * 16;
+        if (fb >= P.Fp) continue;
+        h8 p1, p2;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          _Float16 a1, a2;
+          split2h(tile[kb * 16 + hf * 8 + q][e] * sc, a1, a2);
+          p1[q] = a1;
+          p2[q] = a2;
+        }
+        const size_t base = (((size_t)i * (P.Fp / 16) + fb / 16) * 2 * 32 + e) * 16 + hf * 8;
+        *reinterpret_cast<h8*>(x16 + base) = p1;
+        *reinterpret_cast<h8*>(x16 + base + 32 * 16) = p2;
+      }
+      return;
+    }
     for (int k = threadIdx.x; k < kXtTile * P.din; k += blockDim.x) {
       const int e = k / kXtTile, fl = k - e * kXtTile;
       const int f = f0 + fl;
@@ -588,26 +622,7 @@ struct Args32 {
   float* cst;
   float* lzst;
   int JP, Fs;
-  // split passes (route_logit_kernel / route_lse_kernel / route_acc_kernel)
-  float* lg;       // logits L^r [in_n][JP][Fs] (the couplings overwrite them in place when cst == lg)
-  float2* part;    // per-row-block (max, sum exp) [in_n][n_rb][Fs]
-  float* lz;       // logZ^r [in_n][Fs]
-  int n_rb, n_fb, nchL, clenL;
-  // XCD-aware block order (routing passes r >= 1, forward and B1): > 0 = the number of
-  // (frame tile, i-chunk) workgroups, the grid padded to a multiple of 8 (kXcds)
-  int xcd_nwg;
 };
-
-// The dispatcher deals consecutive workgroups round-robin to the 8 XCDs (each with its
-// own L2).  Block b runs logical workgroup (b % 8) * (grid / 8) + b / 8, so the
-// i-chunk workgroups of one frame tile (consecutive logical ids) share an XCD and its
-// L2 copy of the tile's Vc rows / gs rows instead of each fetching them from HBM.
-constexpr int kXcds = 8;
-__device__ __forceinline__ int xcd_block(int nwg) {
-  if (nwg <= 0) return blockIdx.x;
-  const int per = gridDim.x / kXcds;
-  return (blockIdx.x % kXcds) * per + blockIdx.x / kXcds;
-}
 
 
 
@@ -618,7 +633,6 @@ __device__ __forceinline__ int xcd_block(int nwg) {
 // accumulators; the chunk's bias sum is added at the end.  Operands are double
 // buffered: capsule k+1's loads are issued before capsule k's MFMAs, into the
 // registers capsule k-1 used, so no load waits on a queued MFMA's operand read.
-constexpr int kSplitMaxCl = 32;   // capsules per route_logit_kernel workgroup (LDS partials)
 constexpr int kFTW = 2;   // row tiles per wave
 constexpr int kFFB = 2;   // frame tiles per wave
 
@@ -715,8 +729,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int JD = A.J * DOUT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int bid = xcd_block(A.xcd_nwg);
-  if (A.xcd_nwg > 0 && bid >= A.xcd_nwg) return;   // grid padding
+  const int bid = blockIdx.x;
   const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
   const int f = ft * 32 + r;
   const int fc = min(f, A.F - 1);
@@ -999,8 +1012,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int JD = A.J * DOUT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int bid = xcd_block(A.xcd_nwg);
-  if (A.xcd_nwg > 0 && bid >= A.xcd_nwg) return;   // grid padding
+  const int bid = blockIdx.x;
   const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
   const int f = ft * 32 + r;
   const int fc = min(f, A.F - 1);
@@ -1206,401 +1218,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 }
 
 
-// ------------------------------------------------------------------ split passes
-// A routing pass r >= 1 as three launches instead of one (route_fwd32_kernel keeps
-// all J*dout rows of 32 frames on one CU, which ties its waves together at one
-// softmax barrier per input capsule and re-streams all of W for every 32 frames):
-//   route_logit_kernel: L_ij = <u_ij, Vc_j> for a block of rows x 64 frames and an
-//       i-chunk (pose on the split-fp16 tiles; no softmax, no accumulator), plus the
-//       block's (max, sum exp) over its j;
-//   route_lse_kernel:   logZ_i = log sum_j exp L_ij from the row-block partials;
-//   route_acc_kernel:   c_ij = exp(L_ij - logZ_i) (stored over L as the coupling
-//       storage when training) and s_j += c_ij u_ij over an i-chunk (pose recomputed).
-// A wave owns 2 row tiles x 2 frame tiles (64 rows x 64 frames), so each W fragment
-// serves two frame tiles and each x fragment two row tiles.  Supported: dout 16, 32.
-template <int DIN>
-struct Frags22 {
-  h8 a[2][SplitFrags<DIN>::NA];
-  bf8 bias[2];
-  h8 x[2][2];
-};
-
-// Loads in the order the pose consumes them (bias, then the operands of each product
-// step), so a wait for the first step leaves the rest in flight.
-template <int DIN>
-__device__ __forceinline__ void fetch22(const Rsrc3& rs, uint32_t wvo, uint32_t bvo, const uint32_t (&xvo)[2], int h,
-                                        uint32_t wplane_b, uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
-                                        uint32_t bcap_b, Frags22<DIN>& fr) {
-  constexpr uint32_t TSTEP = 32 * DIN * 2;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap_b, 0);
-    fr.bias[t] = __builtin_bit_cast(bf8, (unsigned __attribute__((ext_vector_type(4)))){v2[0], v2[1], 0u, 0u});
-  }
-  if constexpr (DIN == 16) {
-    // W2 x1, W1 x2, W1 x1
-#pragma unroll
-    for (int b = 0; b < 2; ++b) fr.x[b][0] = hload(rs.x, xvo[b], 0);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) fr.a[t][1] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b);
-#pragma unroll
-    for (int b = 0; b < 2; ++b) fr.x[b][1] = hload(rs.x, xvo[b], xplane_b);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) fr.a[t][0] = hload(rs.w, wvo + t * TSTEP, wcap_b);
-  } else {
-    // W1 x2, W1 x1 (+ W2 x1)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) fr.a[t][0] = hload(rs.w, wvo + t * TSTEP + (h ? wplane_b : 0), wcap_b);
-#pragma unroll
-    for (int b = 0; b < 2; ++b) fr.x[b][1] = hload(rs.x, h ? zero_off : xvo[b], h ? 0u : xplane_b);
-#pragma unroll
-    for (int b = 0; b < 2; ++b) fr.x[b][0] = hload(rs.x, xvo[b], 0);
-  }
-}
-
-// u[b] = pose tiles (row tile t, frame tiles b = 0, 1) of one capsule, bias first
-template <int DIN>
-__device__ __forceinline__ void pose22t(const Frags22<DIN>& fr, int t, const bf8& ones, f16v (&u)[2]) {
-#pragma unroll
-  for (int b = 0; b < 2; ++b) u[b] = pose_chain<DIN>(fr.a[t], fr.x[b], mfma32(fr.bias[t], ones, f16v{}));
-}
-
-// all four tiles, the four chains interleaved step by step (same products and order
-// as pose_chain, so the tiles are bit-identical to pose22t's)
-template <int DIN>
-__device__ __forceinline__ void pose22(const Frags22<DIN>& fr, const bf8& ones, f16v (&u)[2][2]) {
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) u[t][b] = mfma32(fr.bias[t], ones, f16v{});
-  if constexpr (DIN == 16) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][1], fr.x[b][0], u[t][b]);
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][0], fr.x[b][1], u[t][b]);
-  } else {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][0], fr.x[b][1], u[t][b]);
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) u[t][b] = mfma32h(fr.a[t][0], fr.x[b][0], u[t][b]);
-}
-
-// shared setup of the split kernels: one wave = row tiles 2*(rb*NWv + w) + {0,1},
-// frame tiles 2*fbk + {0,1}
-struct Tile22 {
-  int tg, f[2], ftt[2];
-  bool fv[2];
-  uint32_t wvo, bvo;
-};
-template <int DIN>
-__device__ __forceinline__ Tile22 tile22(const Args32& A, int rb, int NWv, int w, int fbk, int r, int h) {
-  Tile22 T;
-  T.tg = 2 * (rb * NWv + w);
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    T.f[b] = (2 * fbk + b) * 32 + r;
-    const int fc = min(T.f[b], A.F - 1);
-    T.ftt[b] = fc - (fc / A.T) * A.T;
-    T.fv[b] = T.f[b] < A.F;
-  }
-  T.wvo = (uint32_t)(((T.tg * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
-  T.bvo = (uint32_t)((T.tg * 32 + r) * 8);
-  return T;
-}
-
-template <int DIN>
-__device__ __forceinline__ void xvo22(const Args32& A, const Tile22& T, int i, int h, uint32_t (&xvo)[2]) {
-#pragma unroll
-  for (int b = 0; b < 2; ++b) xvo[b] = x_voff<DIN>(i, A.N, A.lpad, A.T, A.F, T.f[b], T.ftt[b], T.fv[b], h, A.zero_off);
-}
-
-// grid: n_fb * n_rb * nchL (chunk fastest); block: NWL waves; LDS: the Vc tile
-// (64 x (64 NWL + 4) floats), then clenL * NWL * 64 float2 partials
-template <int DIN, int DOUT, int NWL>
-__global__ __launch_bounds__(64 * NWL) __attribute__((amdgpu_waves_per_eu(2))) void route_logit_kernel(Args32 A) {
-  static_assert(DOUT == 16 || DOUT == 32, "split passes: dout 16 or 32");
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float2* pst = reinterpret_cast<float2*>(lds);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int chunk = blockIdx.x % A.nchL;
-  const int rest = blockIdx.x / A.nchL;
-  const int rb = rest % A.n_rb, fbk = rest / A.n_rb;
-  const int JD = A.J * DOUT;
-  const Tile22 T = tile22<DIN>(A, rb, NWL, w, fbk, r, h);
-  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
-  const int i0 = chunk * A.clenL, i1 = min(A.in_n, i0 + A.clenL);
-  const __amdgpu_buffer_rsrc_t lrs = make_rsrc(A.lg, (size_t)A.in_n * A.JP * A.Fs * 4);
-  // Vc of the workgroup's 64 frames x 64*NWL rows, staged through LDS with coalesced
-  // row loads ([frame][row], row stride padded by 4 floats), then the wave's four tiles
-  // into registers (rows past JD and frames past F: 0)
-  constexpr int RW = 64 * NWL, RS = RW + 4;
-  {
-    const int row0 = rb * RW;
-    for (int k = threadIdx.x; k < 64 * RW / 4; k += 64 * NWL) {
-      const int fr = k / (RW / 4), c4 = (k - fr * (RW / 4)) * 4;
-      const int f = fbk * 64 + fr, row = row0 + c4;
-      const f4 v = (f < A.F && row < JD) ? *reinterpret_cast<const f4*>(A.vc + (size_t)f * JD + row)
-                                         : f4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f4*>(lds + fr * RS + c4) = v;
-    }
-  }
-  __syncthreads();
-  f4 vcr[2][2][4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        vcr[t][b][q] = *reinterpret_cast<const f4*>(lds + (b * 32 + r) * RS + (2 * w + t) * 32 + 8 * q + 4 * h);
-  __syncthreads();   // the LDS is reused for the partials
-  // owned capsules (DOUT 16: lane half h owns j = 2(tg+t) + h; DOUT 32: j = tg + t) and their masks
-  float mk[2];
-  int jo[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    jo[t] = DOUT == 16 ? 2 * (T.tg + t) + h : T.tg + t;
-    mk[t] = (jo[t] < A.J && !(A.mask_first && jo[t] == 0)) ? 0.f : -INFINITY;
-  }
-  const bf8 ones = ones_frag(h);
-  const float inv = A.hdr[0];
-  const uint32_t capw = (uint32_t)A.JDp * DIN * 2, capb = (uint32_t)A.JDp * 8;
-  const uint32_t capl = (uint32_t)A.JP * A.Fs * 4;   // bytes per capsule of L / c
-  auto fetch = [&](int i, Frags22<DIN>& fr) {
-    uint32_t xvo[2];
-    xvo22<DIN>(A, T, i, h, xvo);
-    fetch22<DIN>(rs, T.wvo, T.bvo, xvo, h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i * capw,
-                 (uint32_t)i * capb, fr);
-  };
-  auto body = [&](int i, const Frags22<DIN>& fr) {
-    float Lg[2][2];   // [t][b]
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f16v u[2];
-      pose22t<DIN>(fr, t, ones, u);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        f2 p0 = {0.f, 0.f}, p1 = {0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f4 vv = vcr[t][b][q];
-          f2& pp = (DOUT == 16 && q >= 2) ? p1 : p0;
-          pp += f2{u[b][4 * q], u[b][4 * q + 1]} * f2{vv.x, vv.y};
-          pp += f2{u[b][4 * q + 2], u[b][4 * q + 3]} * f2{vv.z, vv.w};
-        }
-        float l;
-        if constexpr (DOUT == 16) {
-          // reduce-scatter over the lane halves: half h gets the logit of j = 2(tg+t) + h
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0.x + p0.y),
-                                                           __float_as_uint(p1.x + p1.y), false, false);
-          l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-        } else {
-          l = xor32_sum(p0.x + p0.y);
-        }
-        Lg[t][b] = l * inv + mk[t];
-      }
-    }
-    // store L (frame-minor) and the wave's (max, sum exp) over its capsules per frame
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const bool st = T.f[b] < A.Fs && (DOUT == 16 || h == 0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        bstore(lrs, Lg[t][b], st ? (uint32_t)(jo[t] * A.Fs + T.f[b]) * 4u : kNoStore, (uint32_t)i * capl);
-      float m = fmaxf(Lg[0][b], Lg[1][b]);
-      float z = m == -INFINITY ? 0.f : __expf(Lg[0][b] - m) + __expf(Lg[1][b] - m);
-      if constexpr (DOUT == 16) {
-        float m0, m1, z0, z1;
-        xpair32(m, m0, m1);
-        xpair32(z, z0, z1);
-        m = fmaxf(m0, m1);
-        z = m == -INFINITY ? 0.f : z0 * __expf(m0 - m) + z1 * __expf(m1 - m);
-      }
-      pst[((i - i0) * NWL + w) * 64 + b * 32 + r] = make_float2(m, z);   // both halves hold the same pair
-    }
-  };
-  // operands double buffered: capsule k+1's loads go out before capsule k's work; the
-  // loads are unconditional (a clamped capsule past the end) so vmcnt waits stay exact
-  if (i0 < i1) {
-    Frags22<DIN> f0, f1;
-    fetch(i0, f0);
-    for (int i = i0; i < i1; i += 2) {
-      fetch(min(i + 1, i1 - 1), f1);
-      body(i, f0);
-      fetch(min(i + 2, i1 - 1), f0);
-      if (i + 1 < i1) body(i + 1, f1);
-    }
-  }
-  __syncthreads();
-  // combine the waves' partials: one (max, sum exp) per capsule, row block and frame
-  const int n = (i1 - i0) * 64;
-  for (int k = threadIdx.x; k < n; k += 64 * NWL) {
-    const int ci = k >> 6, fr = k & 63;
-    const int f = fbk * 64 + fr;
-    float m = -INFINITY;
-#pragma unroll
-    for (int v = 0; v < NWL; ++v) m = fmaxf(m, pst[(ci * NWL + v) * 64 + fr].x);
-    float z = 0.f;
-    if (m != -INFINITY) {
-#pragma unroll
-      for (int v = 0; v < NWL; ++v) {
-        const float2 pv = pst[(ci * NWL + v) * 64 + fr];
-        z += pv.y * __expf(pv.x - m);
-      }
-    }
-    if (f < A.Fs) A.part[((size_t)(i0 + ci) * A.n_rb + rb) * A.Fs + f] = make_float2(m, z);
-  }
-}
-
-// logZ_i(f) from the row-block partials; grid over in_n * Fs
-__global__ __launch_bounds__(256) void route_lse_kernel(const float2* __restrict__ part, int n_rb, int Fs,
-                                                        size_t n, float* __restrict__ lz) {
-  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const size_t i = k / Fs, f = k - i * Fs;
-  const float2* p = part + i * n_rb * Fs + f;
-  float m = -INFINITY;
-  for (int v = 0; v < n_rb; ++v) m = fmaxf(m, p[(size_t)v * Fs].x);
-  float z = 0.f;
-  for (int v = 0; v < n_rb; ++v) {
-    const float2 pv = p[(size_t)v * Fs];
-    z += pv.y * __expf(pv.x - m);
-  }
-  lz[k] = m + __logf(z);
-}
-
-// grid: n_fb * n_rb * n_chunks (chunk fastest); block: NWA waves
-template <int DIN, int DOUT, int NWA>
-__global__ __launch_bounds__(64 * NWA) __attribute__((amdgpu_waves_per_eu(2))) void route_acc_kernel(Args32 A) {
-  static_assert(DOUT == 16 || DOUT == 32, "split passes: dout 16 or 32");
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int chunk = blockIdx.x % A.n_chunks;
-  const int rest = blockIdx.x / A.n_chunks;
-  const int rb = rest % A.n_rb, fbk = rest / A.n_rb;
-  const int JD = A.J * DOUT;
-  const Tile22 T = tile22<DIN>(A, rb, NWA, w, fbk, r, h);
-  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
-  const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
-  const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
-  const bf8 ones = ones_frag(h);
-  const float inv = A.hdr[0];
-  const uint32_t capw = (uint32_t)A.JDp * DIN * 2, capb = (uint32_t)A.JDp * 8;
-  const uint32_t capl = (uint32_t)A.JP * A.Fs * 4;   // bytes per capsule of L / c
-  // the capsules j of each tile: DOUT 16 rows q = 0,1 -> j = 2(tg+t), q = 2,3 -> j + 1; DOUT 32: j = tg + t
-  int fcl[2];
-#pragma unroll
-  for (int b = 0; b < 2; ++b) fcl[b] = min(T.f[b], A.Fs - 1);
-  f16v acc[2][2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[t][b] = f16v{};
-  constexpr int NJ = DOUT == 16 ? 2 : 1;   // capsules per row tile
-  auto load_l = [&](int i, float (&lv)[2][2][NJ], float (&zv)[2]) {
-    const float* lrow = A.lg + (size_t)i * A.JP * A.Fs;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      zv[b] = A.lz[(size_t)i * A.Fs + fcl[b]];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int k = 0; k < NJ; ++k) lv[t][b][k] = lrow[(size_t)(NJ * (T.tg + t) + k) * A.Fs + fcl[b]];
-    }
-  };
-  auto fetch = [&](int i, Frags22<DIN>& fr) {
-    uint32_t xvo[2];
-    xvo22<DIN>(A, T, i, h, xvo);
-    fetch22<DIN>(rs, T.wvo, T.bvo, xvo, h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i * capw,
-                 (uint32_t)i * capb, fr);
-  };
-  float lv[2][2][NJ], zv[2];
-  auto body = [&](int i, const Frags22<DIN>& fr) {
-    // couplings of this capsule (their loads were issued a capsule ahead)
-    float cv[2][2][NJ];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int k = 0; k < NJ; ++k) cv[t][b][k] = T.fv[b] ? __expf(lv[t][b][k] - zv[b]) : 0.f;
-    load_l(min(i + 1, i1 - 1), lv, zv);
-    // coupling storage (over the logits when training): lane half h stores capsule
-    // NJ(tg+t) + h (DOUT 16) / half 0 stores tg + t (DOUT 32); frames F..Fs-1 get 0.
-    // Without storage the descriptor has no records and every store is dropped.
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const bool st = T.f[b] < A.Fs && (DOUT == 16 || h == 0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        bstore(crs, DOUT == 16 ? (h ? cv[t][b][NJ - 1] : cv[t][b][0]) : cv[t][b][0],
-               st ? (uint32_t)((NJ * (T.tg + t) + (DOUT == 16 ? h : 0)) * A.Fs + T.f[b]) * 4u : kNoStore,
-               (uint32_t)i * capl);
-    }
-    // one row tile at a time (32 registers of pose tiles; the partner wave on the SIMD
-    // keeps the matrix pipe busy during the accumulation)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f16v u[2];
-#if SRF_SPLIT_DBG == 2   // timing experiment: no pose MFMAs
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) u[b][v] = (float)fr.a[t][0][v & 7] + (float)fr.x[b][0][v & 7] + (float)fr.bias[t][0];
-#else
-      pose22t<DIN>(fr, t, ones, u);
-#endif
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int v = 0; v < 16; v += 2) {
-          const float c = cv[t][b][(DOUT == 16 && v >= 8) ? NJ - 1 : 0];
-          f2 a2 = {acc[t][b][v], acc[t][b][v + 1]};
-          a2 += f2{c, c} * f2{u[b][v], u[b][v + 1]};
-          acc[t][b][v] = a2.x;
-          acc[t][b][v + 1] = a2.y;
-        }
-    }
-  };
-  if (i0 < i1) {
-    Frags22<DIN> f0, f1;
-    load_l(i0, lv, zv);
-    fetch(i0, f0);
-    for (int i = i0; i < i1; i += 2) {
-#if SRF_SPLIT_DBG == 1   // timing experiment: every fetch re-reads the first capsule (cache-hot operands)
-      fetch(i0, f1);
-      body(i, f0);
-      fetch(i0, f0);
-#else
-      fetch(min(i + 1, i1 - 1), f1);
-      body(i, f0);
-      fetch(min(i + 2, i1 - 1), f0);
-#endif
-      if (i + 1 < i1) body(i + 1, f1);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = (T.tg + t) * 32 + 8 * q + 4 * h;
-        if (T.fv[b] && row < JD) {
-          f4 v = {acc[t][b][4 * q], acc[t][b][4 * q + 1], acc[t][b][4 * q + 2], acc[t][b][4 * q + 3]};
-          *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + T.f[b]) * JD + row) = v * inv;
-        }
-      }
-}
-
 }  // namespace
 
 namespace srf {
@@ -1611,21 +1228,16 @@ bool fwd32_supported(int din, int dout, int J) {
 }
 
 // Row tiles per wave: kTW, except (a) din 32 with J*dout <= 512, where the six-MFMA
-// pose keeps 2 tiles per wave (SRF_FWD32_TW32=4 forces 4 for A/B runs), and (b) small
-// din <= 16 layers (J*dout <= 128, C2 layers 1-2), which run 2 tiles on each of two
-// waves instead of 4 on one: twice the waves on the one-wave-per-SIMD grid, the
-// softmax across the pair through LDS (C2 step -0.5 to -1 %; SRF_FWD32_TW16=4 restores)
+// pose keeps 2 tiles per wave (4 measured the same at C4), and (b) small din <= 16
+// layers (J*dout <= 128, C2 layers 1-2), which run 2 tiles on each of two waves
+// instead of 4 on one: twice the waves on the one-wave-per-SIMD grid, the softmax
+// across the pair through LDS (C2 step -0.5 to -1 %)
 static int plan_tw(int din, int JD) {
-  if (din <= 16) {   // small layers (J*dout <= 128): two-wave workgroups (SRF_FWD32_TW16=4: one wave)
-    const char* e = getenv("SRF_FWD32_TW16");
-    return (JD <= 128 && !(e && atoi(e) == 4)) ? 2 : kTW;
-  }
-  if (din != 32 || JD > 32 * 2 * kMaxNW) return kTW;
-  const char* e = getenv("SRF_FWD32_TW32");   // read per plan: tests switch it
-  return (e && atoi(e) == 4) ? 4 : 2;
+  if (din <= 16) return JD <= 128 ? 2 : kTW;
+  return (din == 32 && JD <= 32 * 2 * kMaxNW) ? 2 : kTW;
 }
 
-Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout) {
+Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, int dout, int n_chunks) {
   Fwd32Plan p;
   const int in_n = N * (lpad + rpad + 1);
   const int JD = J * dout;
@@ -1639,17 +1251,11 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   const int n_ftiles = (F + 31) / 32;
   // NW > 1: as many workgroups per CU as the waves (2 per SIMD) and the LDS (Vc
   // slabs) allow; single-wave workgroups: up to 4 per CU.
-  static const int slots1 = [] {
-    const char* e = getenv("SRF_FWD32_SLOTS1");
-    return e ? atoi(e) : 1024;
-  }();
   const int per_cu = std::max(1, std::min(8 / p.NW, (int)(160 * 1024 / fwd32_lds(p))));
-  const int slots = p.NW > 1 ? 256 * per_cu : slots1;
+  const int slots = p.NW > 1 ? 256 * per_cu : 1024;
   int best = 1;
   double best_cost = 1e30;
-  const char* env = getenv("SRF_FWD32_CHUNKS");
-  const char* envb = getenv("SRF_FWD32_CHUNKS_BIG");   // A/B: forces only multi-wave (NW > 1, JD > 128) plans
-  const int forced = env ? atoi(env) : (envb && p.NW > 1 && JD > 128 ? atoi(envb) : 0);
+  const int forced = n_chunks;
   for (int c = 1; c <= std::min(in_n, 96); ++c) {
     const int rounds = (n_ftiles * c + slots - 1) / slots;
     const int len = (in_n + c - 1) / c;
@@ -1670,29 +1276,6 @@ Fwd32Plan fwd32_plan(int B, int T, int N, int din, int lpad, int rpad, int J, in
   p.ws_h = (size_t)(2 * kAbsBlocks + 64) * 4;   // header + absmax block maxima
   p.ws_bsum = srf::align_up((size_t)best * JD * 4, 256);
   p.ws_slab = srf::align_up((size_t)best * F * JD * 4, 256);
-  // split passes (route_logit / route_lse / route_acc)
-  // opt-in (SRF_FWD32_SPLIT=1, read per plan so tests can switch it): at C2 the split
-  // passes measured slower than route_fwd32_kernel (layer 3: 29 + 5 + 27 us against 37 us)
-  const char* se = getenv("SRF_FWD32_SPLIT");
-  p.split = se != nullptr && se[0] == '1' && (dout == 16 || dout == 32) && din <= 16;
-  p.NWS = std::min(4, p.JDp / 64);
-  p.n_rb = p.JDp / (64 * p.NWS);
-  p.n_fb = (F + 63) / 64;
-  const int Fs = fwd32_frame_stride(F);
-  // one round of workgroups: 2 waves per SIMD (both kernels' register budgets), so
-  // 2048 / (64 NWS) workgroups per 256 CUs
-  const int base_wg = p.n_fb * p.n_rb;
-  const int sslots = 256 * 8 / p.NWS;
-  p.nchL = std::min(in_n, std::max((in_n + kSplitMaxCl - 1) / kSplitMaxCl, std::max(1, sslots / base_wg)));
-  p.clenL = (in_n + p.nchL - 1) / p.nchL;
-  p.nchL = (in_n + p.clenL - 1) / p.clenL;
-  p.nchA = std::min(std::min(in_n, 24), std::max(1, sslots / base_wg));
-  p.clenA = (in_n + p.nchA - 1) / p.nchA;
-  p.nchA = (in_n + p.clenA - 1) / p.clenA;
-  if (p.split && p.nchA > best) p.ws_slab = srf::align_up((size_t)p.nchA * F * JD * 4, 256);
-  p.ws_lg = srf::align_up((size_t)in_n * (p.JDp / dout) * Fs * 4, 256);
-  p.ws_part = srf::align_up((size_t)in_n * p.n_rb * Fs * 8, 256);
-  p.ws_lz = srf::align_up((size_t)in_n * Fs * 4, 256);
   return p;
 }
 
@@ -1701,10 +1284,7 @@ const float* fwd32_hdr(const Fwd32Plan& p, const void* planes) {
 }
 size_t fwd32_planes_bytes(const Fwd32Plan& p) { return p.ws_w + p.ws_b + p.ws_x + p.ws_h; }
 size_t fwd32_scratch_bytes(const Fwd32Plan& p) { return p.ws_bsum + p.ws_slab; }
-size_t fwd32_split_bytes(const Fwd32Plan& p) { return p.split ? p.ws_lg + p.ws_part + p.ws_lz : 0; }
-size_t fwd32_workspace(const Fwd32Plan& p) {
-  return fwd32_planes_bytes(p) + fwd32_scratch_bytes(p) + fwd32_split_bytes(p);
-}
+size_t fwd32_workspace(const Fwd32Plan& p) { return fwd32_planes_bytes(p) + fwd32_scratch_bytes(p); }
 float* fwd32_slab(const Fwd32Plan& p, void* scratch) {
   return reinterpret_cast<float*>(static_cast<char*>(scratch) + p.ws_bsum);
 }
@@ -1715,7 +1295,7 @@ size_t fwd32_lds(const Fwd32Plan& p) {
 
 int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const float* bias, int B, int T, int N,
                   int din, int lpad, int rpad, int J, int dout, void* planes, void* scratch, float* WT, float* xT,
-                  hipStream_t st, bool wt16) {
+                  hipStream_t st, bool wt16, bool xt16) {
   char* base = static_cast<char*>(planes);
   float* hdr = reinterpret_cast<float*>(base + p.ws_w + p.ws_b + p.ws_x);
   const int in_n = N * (lpad + rpad + 1);
@@ -1752,6 +1332,8 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   P.n_d = p.xplane / 8;
   SRF_REQUIRE(!wt16 || din == 32, "prep32: split W^T planes need din 32, got %d", din);
   P.wt16 = wt16 ? 1 : 0;
+  SRF_REQUIRE(!xt16 || din == 32, "prep32: split x^T planes need din 32, got %d", din);
+  P.xt16 = xt16 ? 1 : 0;
   P.n_e = WT ? (size_t)P.in_n * ((P.JD + 15) / 16) * (wt16 ? 2 : 4) * din : 0;
   SRF_REQUIRE(din <= 32, "prep32: xT tile holds din <= 32, got %d", din);
   P.n_f = xT ? (size_t)P.in_n * ((P.Fp + kXtTile - 1) / kXtTile) : 0;   // xT tiles (one block each)
@@ -1761,27 +1343,13 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   return SRF_OK;
 }
 
-// Opt-in (SRF_XCD_REMAP=1).  Measured: C4 step 10.12 -> 10.10 ms (noise level), but the
-// layer-6 pass fetches 146 instead of 104 MB per launch (PMC): in the plain order
-// the dispatcher already gives each XCD one or two i-chunks of every frame tile,
-// i.e. a quarter of W (2.6 MB, L2-resident), which beats sharing the Vc rows.
-static bool xcd_remap() {
-  const char* e = getenv("SRF_XCD_REMAP");
-  return e && e[0] == '1';
-}
-static int xcd_grid(int nwg) { return xcd_remap() ? (nwg + kXcds - 1) / kXcds * kXcds : nwg; }
-static Args32 xcd_args(Args32 a, const Fwd32Plan& p) {
-  a.xcd_nwg = xcd_remap() ? p.n_ftiles * p.n_chunks : 0;
-  return a;
-}
-
 template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_rpass(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
   auto kern = route_fwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3(xcd_grid(p.n_ftiles * p.n_chunks)), dim3(64 * NW), lds, st, xcd_args(a, p));
+  hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a);
   SRF_LAUNCH_CHECK("route_fwd32");
   return SRF_OK;
 }
@@ -1818,31 +1386,6 @@ static int launch_pass32_t(const Fwd32Plan& p, bool first, const Args32& a, hipS
   }
 }
 
-template <int DIN, int DOUT, int NWS>
-static int launch_split(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
-  const size_t lds = std::max((size_t)p.clenL * NWS * 64 * sizeof(float2), (size_t)64 * (64 * NWS + 4) * sizeof(float));
-  auto lk = route_logit_kernel<DIN, DOUT, NWS>;
-  if (lds > 64 * 1024)
-    SRF_HIP_TRY(hipFuncSetAttribute((const void*)lk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(lk, dim3(p.n_fb * p.n_rb * p.nchL), dim3(64 * NWS), lds, st, a);
-  SRF_LAUNCH_CHECK("route_logit");
-  const size_t n = (size_t)a.in_n * a.Fs;
-  hipLaunchKernelGGL(route_lse_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a.part, p.n_rb, a.Fs, n, a.lz);
-  SRF_LAUNCH_CHECK("route_lse");
-  Args32 b = a;
-  b.n_chunks = p.nchA;
-  b.chunk_len = p.clenA;
-  hipLaunchKernelGGL((route_acc_kernel<DIN, DOUT, NWS>), dim3(p.n_fb * p.n_rb * p.nchA), dim3(64 * NWS), 0, st, b);
-  SRF_LAUNCH_CHECK("route_acc");
-  return SRF_OK;
-}
-
-template <int DIN, int DOUT>
-static int launch_split_t(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
-  if (p.NWS == 2) return launch_split<DIN, DOUT, 2>(p, a, st);
-  return launch_split<DIN, DOUT, 4>(p, a, st);
-}
-
 static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din,
                           int lpad, int rpad, int J, int dout, int mask_first) {
   const int in_n = N * (lpad + rpad + 1);
@@ -1876,10 +1419,6 @@ static Args32 make_args32(const Fwd32Plan& p, const void* planes, void* scratch,
   a.lzst = nullptr;
   a.JP = p.JDp / dout;
   a.Fs = fwd32_frame_stride(B * T);
-  a.lg = nullptr;
-  a.part = nullptr;
-  a.lz = nullptr;
-  a.n_rb = a.n_fb = a.nchL = a.clenL = 0;
   return a;
 }
 
@@ -1901,30 +1440,13 @@ Fwd32Cpl fwd32_cpl_layout(const Fwd32Plan& p, int F, int in_n, int din, int dout
   return c;
 }
 
-int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, void* split_ws, int B, int T,
+int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T,
                int N, int din, int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst,
                float* lzst, hipStream_t st) {
   Args32 a = make_args32(p, planes, scratch, B, T, N, din, lpad, rpad, J, dout, mask_first);
   a.vc = vc;
   a.cst = first ? nullptr : cst;
   a.lzst = first ? nullptr : lzst;
-  if (!first && p.split && split_ws != nullptr) {
-    char* sb = static_cast<char*>(split_ws);
-    a.lg = cst != nullptr ? cst : reinterpret_cast<float*>(sb);
-    a.part = reinterpret_cast<float2*>(sb + p.ws_lg);
-    a.lz = lzst != nullptr ? lzst : reinterpret_cast<float*>(sb + p.ws_lg + p.ws_part);
-    a.n_rb = p.n_rb;
-    a.n_fb = p.n_fb;
-    a.nchL = p.nchL;
-    a.clenL = p.clenL;
-#define SRF_S32(DI, DO) \
-  if (din == DI && dout == DO) return launch_split_t<DI, DO>(p, a, st);
-    SRF_S32(8, 16)
-    SRF_S32(8, 32)
-    SRF_S32(16, 16)
-    SRF_S32(16, 32)
-#undef SRF_S32
-  }
   SRF_REQUIRE(2 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
 #define SRF_P32(DI, DO) \
   if (din == DI && dout == DO) return launch_pass32_t<DI, DO>(p, first, a, st);
@@ -1945,7 +1467,7 @@ static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b,
   auto kern = route_bwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, dim3(xcd_grid(p.n_ftiles * p.n_chunks)), dim3(64 * NW), lds, st, xcd_args(a, p), b);
+  hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a, b);
   SRF_LAUNCH_CHECK("route_bwd32");
   return SRF_OK;
 }

@@ -66,6 +66,7 @@ __device__ __forceinline__ unsigned fdiv(unsigned n, const FastDiv& f) {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
 
 // v_mfma_f32_16x16x4_f32: lane l holds A[row=l&15][k=l>>4], B[k=l>>4][col=l&15];
 // C/D lane l holds col = l&15, rows 4*(l>>4) + reg.

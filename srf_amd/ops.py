@@ -44,27 +44,6 @@ def _returned(target_flags):
     return [None if inplace else t for t, inplace in target_flags]
 
 
-# Side stream for the DR weight-gradient pass (srf_route_dr_bwd_weights): forked from
-# the autograd stream after a layer's data pass, joined by join_weight_streams() --
-# PrimaryCaps.backward calls it, which runs after every routing layer's backward.
-_side_streams = {}
-_pending_joins = []
-
-
-def _weight_stream(dev):
-    s = _side_streams.get(dev)
-    if s is None:
-        s = _side_streams[dev] = torch.cuda.Stream(device=dev)
-    return s
-
-
-def join_weight_streams():
-    """Make the current stream wait for every forked weight-gradient pass."""
-    cur = torch.cuda.current_stream()
-    while _pending_joins:
-        cur.wait_stream(_pending_joins.pop())
-
-
 class RouteGeom:
     """Static geometry of one DR layer (sequence_router_naive.py:146-147)."""
 
@@ -74,7 +53,9 @@ class RouteGeom:
         self.iters, self.mask_first = iters, int(bool(mask_first))
         self.in_n = N * (lpad + rpad + 1)
         self.timing = None   # optional (starts, stops) hipEvent_t arrays for the profiling hook
-        self.side_stream = False   # run the weight-gradient pass on a forked stream (SequenceRouter sets it)
+        # a training forward keeps the couplings for the backward (srf_route_dr_fwd_ex's
+        # coupling storage); False: it keeps nothing and the backward recomputes them
+        self.store_couplings = True
         L = _lib.lib()
         if n_chunks <= 0:
             n_chunks = L.srf_route_dr_auto_chunks(B, T, N, din, lpad, rpad, J, dout)
@@ -116,7 +97,7 @@ class DynamicRouting(torch.autograd.Function):
         # under no_grad or on non-trainable inputs stores nothing; grad mode is off
         # inside Function.forward, so the caller decides, see dynamic_routing)
         nc = L.srf_route_dr_coupling_floats(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, g.iters) \
-            if need_bwd and os.environ.get('SRF_ROUTE_COUPLINGS', '1') != '0' else 0
+            if need_bwd and g.store_couplings else 0
         cpl = torch.empty(nc, device=dev, dtype=torch.float32) if nc else None
         rc = L.srf_route_dr_fwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(v), _ptr(saved),
                                    _ptr(cpl) if cpl is not None else None, _ptr(ws), ws_bytes, _stream())
@@ -141,23 +122,9 @@ class DynamicRouting(torch.autograd.Function):
         cpl = ctx.couplings
         ctx.couplings = None
         cp = _ptr(cpl) if cpl is not None else None
-        if not g.side_stream:
-            rc = L.srf_route_dr_bwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
-                                       _ptr(g_emb), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
-            _lib.check(rc, 'srf_route_dr_bwd_ex')
-            return (g_emb, *_returned([tW, tb]), None, None)
-        rc = L.srf_route_dr_bwd_data_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
-                                        _ptr(g_emb), _ptr(ws), ws_bytes, _stream())
-        _lib.check(rc, 'srf_route_dr_bwd_data_ex')
-        side = _weight_stream(emb.device)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            rc = L.srf_route_dr_bwd_weights_ex(_ptr(emb), *g.args(), _ptr(saved), cp, _ptr(g_W), _ptr(g_b), _ptr(ws),
-                                               ws_bytes, ctypes_void(side.cuda_stream))
-        _lib.check(rc, 'srf_route_dr_bwd_weights_ex')
-        for t in (ws, emb, g_W, g_b, saved) + ((cpl,) if cpl is not None else ()):
-            t.record_stream(side)
-        _pending_joins.append(side)
+        rc = L.srf_route_dr_bwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
+                                   _ptr(g_emb), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
+        _lib.check(rc, 'srf_route_dr_bwd_ex')
         return (g_emb, *_returned([tW, tb]), None, None)
 
 
@@ -318,7 +285,6 @@ class PrimaryCaps(torch.autograd.Function):
                                        proj_scale, _ptr(saved), _ptr(g_z.contiguous()), _ptr(g_X),
                                        *[_ptr(G[k]) for k in CAPS_PARAMS], _ptr(ws), wb, _stream())
         _lib.check(rc, 'srf_primary_caps_bwd_ex')
-        join_weight_streams()
         return (g_X, None, None, None, None, None, None, None, None, *_returned(targets))
 
 

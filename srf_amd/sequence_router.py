@@ -231,11 +231,6 @@ class SequenceRouter(torch.nn.Module):
             N = in_n // self.window
             g = ops.RouteGeom(B, T, N, in_d, self.lpad, self.rpad, out_n, out_d, self.route_iters,
                               l == self.enc_num - 1, self.n_chunks_override.get(l, 0))
-            # SRF_WEIGHT_STREAM=1 runs the DR weight gradients on a forked stream that
-            # PrimaryCaps' backward joins.  Off by default: measured slower at C2 (1.896
-            # vs 1.806 ms/step, hipGraph) and equal at C4 -- the overlapped gW pass takes
-            # CUs from the latency-bound backward of the layers below.
-            g.side_stream = os.environ.get('SRF_WEIGHT_STREAM', '0') == '1'
             self._geoms[key] = g
         return g
 

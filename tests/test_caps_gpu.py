@@ -123,17 +123,15 @@ def test_ctc_infeasible_is_inf_with_zero_grad(cuda):
     assert torch.count_nonzero(lg.grad) == 0
 
 
-@pytest.mark.parametrize('B,T,C,L,wave', [(3, 150, 12, 70, '0'), (2, 420, 32, 200, '0'), (3, 150, 12, 70, '1'),
-                                          (2, 420, 32, 200, '1'), (2, 90, 63, 40, '1'),
-                                          (1, 2100, 32, 1000, '1'),    # gradient stages 4 frames per block
-                                          (1, 11300, 8, 5600, '0')])   # gradient reads alpha/beta from HBM
-def test_ctc_long_labels_cross_state_groups(cuda, B, T, C, L, wave, monkeypatch):
+@pytest.mark.parametrize('B,T,C,L', [(3, 150, 12, 70), (2, 420, 32, 200), (2, 90, 63, 40),
+                                     (1, 2100, 32, 1000),    # block loop; gradient stages 4 frames per block
+                                     (1, 11300, 8, 5600)])   # gradient reads alpha/beta from HBM
+def test_ctc_long_labels_cross_state_groups(cuda, B, T, C, L):
     """Extended-label lengths past 64 states exercise the group boundaries of the
-    wave-resident recursion (KM = 4, 8); SRF_CTC_WAVE=0 runs the block loop.  The
+    wave-resident recursion (KM = 4, 8); past 512 states the block loop runs.  The
     longest cases exceed the gradient kernel's 16-frame LDS staging (fewer frames
     per block, then no staging)."""
     from srf_amd import ops
-    monkeypatch.setenv('SRF_CTC_WAVE', wave)
     rng = np.random.default_rng(B * 1000 + T)
     logits = rng.standard_normal((B, T, C)) * 2
     lab_len = rng.integers(L // 2, L + 1, size=B).astype(np.int32)

@@ -104,62 +104,3 @@ def test_cnnfe_inference_uses_moving_stats(cuda):
     assert np.abs(out.cpu().double().numpy() - x.numpy()).max() < 2e-4 * (1 + np.abs(x.numpy()).max())
     assert torch.allclose(moving[0].cpu().double(), mm[0].float().double())   # untouched
 
-
-def test_conv2_split_bf16_matches_fp32_mfma(cuda, monkeypatch):
-    """The split-bf16 stage-2 convolution (conv2_fwd32_kernel, 3-term bf16 splits on
-    32x32x16 MFMA) against the fp32-MFMA one (SRF_CONV2_32=0): same CNN-FE output
-    to fp32 accuracy, dropout included (same counter-based masks)."""
-    from srf_amd import ops
-    torch.manual_seed(3)
-    B, T, Fd = 3, 45, 123
-    feats = torch.randn(B, T, Fd, device=cuda)
-    il = torch.tensor([45, 31, 12], dtype=torch.int32, device=cuda)
-    params = []
-    for k in range(2):
-        cin = 1 if k == 0 else 64
-        for _ in range(2):
-            params += [torch.randn(3, 3, cin, 64, device=cuda) * 0.1, torch.randn(64, device=cuda) * 0.1]
-        params += [1 + 0.1 * torch.randn(64, device=cuda), 0.1 * torch.randn(64, device=cuda)]
-    outs = []
-    for flag in ('1', '0'):
-        monkeypatch.setenv('SRF_CONV2_32', flag)
-        moving = [torch.zeros(64, device=cuda), torch.ones(64, device=cuda), torch.zeros(64, device=cuda),
-                  torch.ones(64, device=cuda)]
-        outs.append(ops.cnnfe(feats, il, params, moving, True, 0.2, 1234).cpu().double().numpy())
-    err = np.abs(outs[0] - outs[1]).max()
-    assert err <= 2e-5 * max(1.0, np.abs(outs[1]).max()), err
-
-
-def test_conv2_bwd_split_fp16_matches_split_bf16(cuda, monkeypatch):
-    """The split-fp16 stage-2 data and weight gradients (conv2_dgrad32_kernel<true>,
-    conv2_wgrad32_kernel<true>: scaled 2-term fp16 operands, three f16 MFMAs per tile)
-    against the split-bf16 ones (SRF_DGRAD_F16=0, six bf16 MFMAs): the same gradients
-    of every CNN-FE parameter to fp32 accuracy, dropout included."""
-    from srf_amd import ops
-    torch.manual_seed(5)
-    B, T, Fd = 3, 45, 123
-    il = torch.tensor([45, 31, 12], dtype=torch.int32, device=cuda)
-    base = []
-    for k in range(2):
-        cin = 1 if k == 0 else 64
-        for _ in range(2):
-            base += [torch.randn(3, 3, cin, 64, device=cuda) * 0.1, torch.randn(64, device=cuda) * 0.1]
-        base += [1 + 0.1 * torch.randn(64, device=cuda), 0.1 * torch.randn(64, device=cuda)]
-    feats0 = torch.randn(B, T, Fd, device=cuda)
-    gout = None
-    grads = []
-    for flag in ('1', '0'):
-        monkeypatch.setenv('SRF_DGRAD_F16', flag)
-        feats = feats0.clone()
-        params = [p.clone().requires_grad_() for p in base]
-        moving = [torch.zeros(64, device=cuda), torch.ones(64, device=cuda), torch.zeros(64, device=cuda),
-                  torch.ones(64, device=cuda)]
-        out = ops.cnnfe(feats, il, params, moving, True, 0.2, 77)
-        if gout is None:
-            gout = torch.randn_like(out)
-        out.backward(gout)
-        # stage-1 parameters (conv1 kernels/biases, BN1) see the stage-2 data gradient,
-        # the stage-2 kernels the weight gradient
-        grads.append([p.grad.cpu().double().numpy() for p in params])
-    for a, b in zip(grads[0], grads[1]):
-        assert np.abs(a - b).max() <= 2e-5 * max(1.0, np.abs(b).max()), np.abs(a - b).max()

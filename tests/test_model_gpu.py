@@ -69,13 +69,6 @@ def test_gradients(cuda, name):
     assert not bad, bad
 
 
-def test_gradients_with_weight_stream(cuda, monkeypatch):
-    """SRF_WEIGHT_STREAM=1: the DR weight gradients run on a forked stream joined in
-    PrimaryCaps' backward; same gradients as the one-stream path."""
-    monkeypatch.setenv('SRF_WEIGHT_STREAM', '1')
-    test_gradients(cuda, 'c2_mini')
-
-
 def test_train_step_runs_and_updates(cuda):
     """process_train_step: loss finite, params move after step 2 (lr(0) == 0)."""
     from srf_amd import train_helper, trainer_sr
