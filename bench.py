@@ -206,7 +206,7 @@ def sdr_roofline(model, tms):
     R = model.route_iters
     stream = bool(_lib.lib().srf_route_sdr_couplings_required(in_n, J, D, R))
     reads = R if stream else 1
-    elt = 2 if (stream and model.pose_fp8 and os.environ.get('SRF_SDR_U_BF16', '1') != '0') else 4   # bf16 u
+    elt = 2 if (stream and model.pose_fp8 and model.sdr_options.get('u_bf16', True)) else 4   # bf16 u
     per_frame = reads * in_n * J * D * elt + J * D * 4
     ms = sum(t for t, _ in tms)
     frames = sum(f for _, f in tms)
@@ -308,8 +308,7 @@ def measure(workload, args, world, rank, dev):
     kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
     kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
     in_n, J, D, Din = model.layer_shapes[last]
-    fwd32 = Din in (8, 16, 32) and D in (8, 16, 32) and Din <= D and J * D <= 1024 and \
-        os.environ.get('SRF_ROUTE_FWD32', '1') != '0'
+    fwd32 = Din in (8, 16, 32) and D in (8, 16, 32) and Din <= D and J * D <= 1024
     frames_prime = B * Tp
     # algorithmic FLOPs per launch: the layer's pose contraction (once per
     # forward, spread over its R pass launches) + one routing iteration

@@ -979,6 +979,181 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 }
 
 
+// Routing pass r >= 1, software-pipelined over the input capsules: while the matrix
+// cores form capsule i + 1's pose tiles (pose_prog, which also streams in capsule
+// i + 2's operands), the VALU finishes capsule i -- the cross-wave softmax statistics
+// behind last iteration's barrier, the coupling stores and s += c u -- so the one
+// barrier per capsule no longer leaves the matrix pipe idle while the waves meet.
+// Same tiles, LDS and results as route_fwd32_kernel (one more u set in registers).
+template <int DIN, int DOUT, int NW, int TW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesPerEU))) void route_fwd32p_kernel(Args32 A) {
+  constexpr int CP = TW * 32 / DOUT;   // capsule partials per lane
+  constexpr int OWN = CP / 2;          // capsules whose logit this lane owns
+  static_assert(NW > 1, "the pipelined pass exchanges softmax stats between waves");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int JD = A.J * DOUT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int bid = blockIdx.x;
+  const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
+  const int f = ft * 32 + r;
+  const int fc = min(f, A.F - 1);
+  const int fb = fc / A.T, ftt = fc - fb * A.T;
+  const bool fvalid = f < A.F;
+  const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
+  const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
+  const int j0 = tbase * 32 / DOUT;
+  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
+  const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
+  const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
+  const __amdgpu_buffer_rsrc_t lzs = make_rsrc(A.lzst, A.cst ? (size_t)A.in_n * A.Fs * 4 : 0);
+  f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
+  float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (fvalid && row < JD) v = *reinterpret_cast<const f4*>(A.vc + (size_t)f * JD + row);
+      vcl[(t * 4 + q) * 64 + lane] = v;
+    }
+  float mk[OWN];
+#pragma unroll
+  for (int a = 0; a < OWN; ++a) {
+    const int j = j0 + 2 * a + h;
+    mk[a] = (j < A.J && !(A.mask_first && j == 0)) ? 0.f : -INFINITY;
+  }
+  const bf8 ones = ones_frag(h);
+  const float inv = A.hdr[0];   // 2^-(aw+bx): the pose tiles hold 2^(aw+bx) u
+  f16v acc[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) acc[t] = f16v{};
+  if (i0 < i1) {
+    Frags32<DIN, TW> fr;
+    fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
+                           fr);
+    f16v uc[TW], un[TW];
+    float e[OWN], m;   // the pending capsule's exponentials and lane max
+    // the logits of one capsule's tiles -> e, m; the wave's (max, sum) -> LDS slot
+    auto logits = [&](const f16v (&u)[TW], int slot_par) {
+      f2 P2[CP];
+#pragma unroll
+      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 vv = vcl[(t * 4 + q) * 64 + lane];
+          const int k = kpart<DOUT>(t, 4 * q);
+          P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv.x, vv.y};
+          P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv.z, vv.w};
+        }
+      float L[OWN];
+      m = -1e30f;
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        const float pa = P2[2 * a].x + P2[2 * a].y, pb = P2[2 * a + 1].x + P2[2 * a + 1].y;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa), __float_as_uint(pb), false, false);
+        L[a] = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) * inv + mk[a];
+        m = fmaxf(m, L[a]);
+      }
+      float z = 0.f;
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        e[a] = __expf(L[a] - m);
+        z += e[a];
+      }
+      float m0, m1, z0, z1;
+      xpair32(m, m0, m1);
+      xpair32(z, z0, z1);
+      const float M = fmaxf(m0, m1);
+      const float Z = z0 * __expf(m0 - M) + z1 * __expf(m1 - M);
+      if (h == 0) st[(slot_par * NW + wv) * 32 + r] = make_float2(M, Z);
+    };
+    int par = 0;
+    pose_prog<DIN, TW>(fr, ones, uc, rs, wvo, bvo,
+                       x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                       A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
+                       (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8);
+    logits(uc, par);
+    __syncthreads();
+    for (int i = i0; i < i1; ++i) {
+      const bool more = i + 1 < i1;
+      if (more) {   // capsule i + 1's tiles on the matrix cores (operands of i + 2 streamed in)
+        const int in = min(i + 2, i1 - 1);
+        pose_prog<DIN, TW>(fr, ones, un, rs, wvo, bvo,
+                           x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                           A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
+      }
+      // finish capsule i: softmax over all waves' rows, couplings, s += c u
+      float M, Z;
+      {
+        constexpr int HW = NW / 2;
+        const float2* slot = st + par * NW * 32;
+        float2 sv[HW];
+#pragma unroll
+        for (int w = 0; w < HW; ++w) sv[w] = slot[(h * HW + w) * 32 + r];
+        float mh = sv[0].x;
+#pragma unroll
+        for (int w = 1; w < HW; ++w) mh = fmaxf(mh, sv[w].x);
+        float zh = 0.f;
+#pragma unroll
+        for (int w = 0; w < HW; ++w) zh += sv[w].y * __expf(sv[w].x - mh);
+        float m0, m1, z0, z1;
+        xpair32(mh, m0, m1);
+        xpair32(zh, z0, z1);
+        M = fmaxf(m0, m1);
+        Z = z0 * __expf(m0 - M) + z1 * __expf(m1 - M);
+      }
+      const float sc = __expf(m - M) / Z;
+#pragma unroll
+      for (int a = 0; a < OWN; ++a)
+        bstore(crs, fvalid ? e[a] * sc : 0.f, (uint32_t)((j0 + h + 2 * a) * A.Fs + f) * 4u,
+               (uint32_t)i * A.JP * A.Fs * 4u);
+      bstore(lzs, M + __logf(Z), (h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore,
+             (uint32_t)i * A.Fs * 4u);
+      float c[CP];
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        float c0, c1;
+        xpair32(e[a] * sc, c0, c1);
+        c[2 * a] = c0;
+        c[2 * a + 1] = c1;
+      }
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const float cv = c[kpart<DOUT>(t, v)];
+          f2 a2 = {acc[t][v], acc[t][v + 1]};
+          a2 += f2{cv, cv} * f2{uc[t][v], uc[t][v + 1]};
+          acc[t][v] = a2.x;
+          acc[t][v + 1] = a2.y;
+        }
+      if (more) {   // capsule i + 1's logits and stats, then the one barrier
+        par ^= 1;
+        logits(un, par);
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < TW; ++t) uc[t] = un[t];
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      if (fvalid && row < JD) {
+        f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v * inv;
+      }
+    }
+}
+
 // ------------------------------------------------------------------ backward pass
 // Backward routing pass r >= 1 (the adjoint of _loop_body, naive:199-206), on the
 // forward's tiles and split-bf16 pose.  The couplings c^r come from the forward
@@ -1218,6 +1393,167 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 }
 
 
+// Backward pass r >= 1, software-pipelined as route_fwd32p_kernel: capsule i + 1's
+// pose tiles run on the matrix cores while the VALU finishes capsule i (sigma over all
+// waves from behind last iteration's barrier, the stats / gL stores, gVc += gL u).
+template <int DIN, int DOUT, int NW, int TW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesPerEU))) void route_bwd32p_kernel(
+    Args32 A, Bwd32Args Bk) {
+  constexpr int CP = TW * 32 / DOUT;
+  constexpr int OWN = CP / 2;
+  static_assert(NW > 1, "the pipelined pass exchanges sigma partials between waves");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int JD = A.J * DOUT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int bid = blockIdx.x;
+  const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
+  const int f = ft * 32 + r;
+  const int fc = min(f, A.F - 1);
+  const int fb = fc / A.T, ftt = fc - fb * A.T;
+  const bool fvalid = f < A.F;
+  const int i0 = chunk * A.chunk_len, i1 = min(A.in_n, i0 + A.chunk_len);
+  const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
+  const int j0 = tbase * 32 / DOUT;
+  const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
+  const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
+  const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
+  f4* gsl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
+  float* st = lds + (size_t)NW * TW * 4 * 64 * 4;
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (fvalid && row < JD) v = *reinterpret_cast<const f4*>(Bk.gs + (size_t)f * JD + row);
+      gsl[(t * 4 + q) * 64 + lane] = v;
+    }
+  const bf8 ones = ones_frag(h);
+  const float inv = A.hdr[0];
+  f16v acc[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t) acc[t] = f16v{};
+  const float* crow = Bk.cst + (size_t)(j0 + h) * A.Fs + fc;
+  const __amdgpu_buffer_rsrc_t sts = make_rsrc(Bk.stats, (size_t)A.F * A.in_n * 8);
+  const size_t cstep = (size_t)A.JP * A.Fs;
+  if (i0 < i1) {
+    Frags32<DIN, TW> fr;
+    fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
+                           fr);
+    f16v uc[TW], un[TW];
+    float cc[OWN], cn[OWN], Q[OWN];   // couplings of the pending / next capsule; the pending capsule's q
+    // q = <gs_j, u_ij> of the owned capsules, the wave's sigma partial -> LDS slot
+    auto dots = [&](const f16v (&u)[TW], const float (&c)[OWN], int slot_par) {
+      f2 P2[CP];
+#pragma unroll
+      for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 gv = gsl[(t * 4 + q) * 64 + lane];
+          const int k = kpart<DOUT>(t, 4 * q);
+          P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{gv.x, gv.y};
+          P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{gv.z, gv.w};
+        }
+      float sp = 0.f;
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        const float pa = P2[2 * a].x + P2[2 * a].y, pb = P2[2 * a + 1].x + P2[2 * a + 1].y;
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(pa), __float_as_uint(pb), false, false);
+        Q[a] = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) * inv;
+        sp += c[a] * Q[a];
+      }
+      float s0, s1;
+      xpair32(sp, s0, s1);
+      if (h == 0) st[(slot_par * NW + wv) * 32 + r] = s0 + s1;
+    };
+    int par = 0;
+    load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cc);
+    pose_prog<DIN, TW>(fr, ones, uc, rs, wvo, bvo,
+                       x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                       A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
+                       (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8);
+    dots(uc, cc, par);
+    __syncthreads();
+    for (int i = i0; i < i1; ++i) {
+      const bool more = i + 1 < i1;
+      if (more) {
+        load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
+        const int in = min(i + 2, i1 - 1);
+        pose_prog<DIN, TW>(fr, ones, un, rs, wvo, bvo,
+                           x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                           A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
+      }
+      // finish capsule i: sigma over all waves, stats, gL, gVc += gL u
+      float S;
+      {
+        constexpr int HW = NW / 2;
+        const float* slot = st + par * NW * 32;
+        float sh = 0.f;
+#pragma unroll
+        for (int w = 0; w < HW; ++w) sh += slot[(h * HW + w) * 32 + r];
+        float s0, s1;
+        xpair32(sh, s0, s1);
+        S = s0 + s1;
+      }
+      {
+        const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
+        __builtin_amdgcn_raw_buffer_store_b64(
+            (unsigned __attribute__((ext_vector_type(2)))){__float_as_uint(lzv), __float_as_uint(S)}, sts,
+            (wv == 0 && h == 0 && fvalid) ? (uint32_t)(f * A.in_n) * 8u : kNoStore, (uint32_t)i * 8u, 0);
+      }
+      float gown[OWN];
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) gown[a] = cc[a] * (Q[a] - S);
+      {
+        float* dst = Bk.glst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
+#pragma unroll
+        for (int a = 0; a < OWN; ++a) dst[(size_t)2 * a * A.Fs] = fvalid ? gown[a] : 0.f;
+      }
+      float g[CP];
+#pragma unroll
+      for (int a = 0; a < OWN; ++a) {
+        float g0, g1;
+        xpair32(gown[a], g0, g1);
+        g[2 * a] = g0;
+        g[2 * a + 1] = g1;
+      }
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const float gv = g[kpart<DOUT>(t, v)];
+          f2 a2 = {acc[t][v], acc[t][v + 1]};
+          a2 += f2{gv, gv} * f2{uc[t][v], uc[t][v + 1]};
+          acc[t][v] = a2.x;
+          acc[t][v + 1] = a2.y;
+        }
+      if (more) {
+        par ^= 1;
+        dots(un, cn, par);
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < OWN; ++a) cc[a] = cn[a];
+#pragma unroll
+        for (int t = 0; t < TW; ++t) uc[t] = un[t];
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (tbase + t) * 32 + 8 * q + 4 * h;
+      if (fvalid && row < JD) {
+        f4 v = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+        *reinterpret_cast<f4*>(A.slab + ((size_t)chunk * A.F + f) * JD + row) = v * inv;
+      }
+    }
+}
+
 }  // namespace
 
 namespace srf {
@@ -1343,10 +1679,15 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   return SRF_OK;
 }
 
+#ifndef SRF_FWD32_PIPE
+#define SRF_FWD32_PIPE 1   // multi-wave passes r >= 1 on route_fwd32p_kernel (0: route_fwd32_kernel, A/B builds)
+#endif
 template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_rpass(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
-  auto kern = route_fwd32_kernel<DIN, DOUT, NW, TW>;
+  // the pipelined pass holds a second u set: TW = 4 would spill
+  auto kern = (SRF_FWD32_PIPE && NW > 1 && TW <= 2) ? route_fwd32p_kernel<DIN, DOUT, (NW > 1 ? NW : 2), (TW <= 2 ? TW : 2)>
+                                                    : route_fwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a);
@@ -1464,7 +1805,8 @@ int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch
 template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
-  auto kern = route_bwd32_kernel<DIN, DOUT, NW, TW>;
+  auto kern = (SRF_FWD32_PIPE && NW > 1 && TW <= 2) ? route_bwd32p_kernel<DIN, DOUT, (NW > 1 ? NW : 2), (TW <= 2 ? TW : 2)>
+                                                    : route_bwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(p.n_ftiles * p.n_chunks), dim3(64 * NW), lds, st, a, b);

@@ -884,12 +884,9 @@ __global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int 
 // Which contraction runs on the 32x32-tile kernels, by din (scripts/bench_sdr_gemm.py,
 // one frame range alone on the GPU, us 32x32 vs 16x16): C5 din 64 pose 850 vs 973, gx
 // 1228 vs 1174, gW 937 vs 1073; C3 din 32 pose 46 vs 33, gx 47 vs 53, gW 91 vs 65.
-// SRF_SDR_MFMA32=0 / 1 forces one family for all three (A/B).
 enum class SdrGemm { kPose, kGx, kGw };
 bool use_mfma32(int din, int JD, SdrGemm k) {
   if ((din != 32 && din != 64) || JD % 8) return false;
-  const char* e = getenv("SRF_SDR_MFMA32");
-  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
   return din == 64 ? k != SdrGemm::kGx : k == SdrGemm::kGx;
 }
 
@@ -903,13 +900,8 @@ int check_sgeom(const SGeom& g) {
   return SRF_OK;
 }
 
-// Frame state beyond one CU's 160 KiB LDS goes to global memory (workspace); so does
-// every state when SRF_SDR_GSTATE=1 (test hook for the global-state kernels).
-bool sdr_gstate(size_t bytes) {
-  if (bytes > 160 * 1024) return true;
-  const char* e = getenv("SRF_SDR_GSTATE");
-  return e && e[0] == '1';
-}
+// Frame state beyond one CU's 160 KiB LDS goes to global memory (workspace).
+bool sdr_gstate(size_t bytes) { return bytes > 160 * 1024; }
 
 // per-workgroup slice of the global frame state, in floats (256-B aligned slices)
 size_t gstate_stride(size_t state_bytes) { return srf::align_up(state_bytes, 256) / sizeof(float); }
@@ -1019,23 +1011,9 @@ int recur_fwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
   return SRF_OK;
 }
 
-// SRF_SDR_BWD_STREAM=1 (A/B): register-path layers whose stored couplings have the
-// streaming layout too (J a power of two, record sizes equal) run the streaming backward
-bool bwd_stream(const SGeom& g) {
-  const char* e = getenv("SRF_SDR_BWD_STREAM");   // 1: every such layer, 2: J*dout >= 1024 only
-  if (!(e && (e[0] == '1' || (e[0] == '2' && g.J * g.dout >= 1024)))) return false;
-  const int in_n = g.in_n();
-  if (!srf::sdr_seq_supported(in_n, g.J, g.dout, g.iters) || !srf::sdr_stream_supported(in_n, g.J, g.dout, g.iters))
-    return false;
-  return (g.J & (g.J - 1)) == 0 &&
-         srf::sdr_seq_cs_floats(in_n, g.J, g.dout, g.iters) == srf::sdr_stream_cs_floats(in_n, g.J, g.dout, g.iters);
-}
-
 int recur_bwd_n(const SGeom& g, const srf::SeqItems& it, hipStream_t st) {
   if (it.n == 0) return SRF_OK;
   if (int rc = u_type_ok(g, it)) return rc;
-  if (bwd_stream(g) && it.it[0].cs && it.it[0].ws)
-    return srf::sdr_stream_bwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, st);
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_seq_bwd(it, g.B, g.T, g.in_n(), g.J, g.dout, g.iters, g.mask_first, st);
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
@@ -1062,7 +1040,6 @@ srf::SeqItems one_seq_item(const srf::SeqItem& I) {
 }
 
 size_t recur_workspace(const SGeom& g) {
-  if (bwd_stream(g)) return srf::sdr_stream_workspace_floats(g.B, g.in_n(), g.J, g.dout, g.iters) * sizeof(float);
   if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters)) return 0;
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_stream_workspace_floats(g.B, g.in_n(), g.J, g.dout, g.iters) * sizeof(float);

@@ -142,11 +142,6 @@ extern "C" int srf_seq_fwd_stamp_buffer(void* p) {
 namespace srf {
 
 bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm) {
-  const char* e = getenv("SRF_SDR_SEQ");
-  if (e && e[0] == '0') return false;
-  // A/B hook: layers with J*dout above this run on the streaming kernels instead
-  const char* mj = getenv("SRF_SDR_SEQ_MAXJD");
-  if (mj && mj[0] && J * dout > atoi(mj)) return false;
   if (J < 2 || J > 64 || iters < 1 || iters > 5 || in_n < 1) return false;
   if (dout != 8 && dout != 16 && dout != 32) return false;
   const int JP = srf_seq::pow2_at_least(J);

@@ -468,8 +468,6 @@ int launch_bwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, hi
 namespace srf {
 
 bool sdr_stream_supported(int in_n, int J, int dout, int iters) {
-  const char* e = getenv("SRF_SDR_STREAM");
-  if (e && e[0] == '0') return false;
   if (iters < 1 || iters > kRM || in_n < kNW) return false;
   const int JD = J * dout;
   if (JD % 64) return false;

@@ -1,6 +1,5 @@
 """torch.autograd wrappers around the C ABI (device memory from torch's caching
 allocator, launches on torch's current HIP stream)."""
-import os
 
 import torch
 
@@ -433,16 +432,24 @@ class SdrStackPlan:
     frame t0 - rpad, i.e. (l + 1, k), and the carry of (l, k + 1).
     layers: [(N, din, J, dout, mask_first)] per layer."""
 
-    def __init__(self, B, T, layers, lpad, rpad, iters, n_chunks=0, pose_fp8=False):
+    def __init__(self, B, T, layers, lpad, rpad, iters, n_chunks=0, pose_fp8=False, u_bf16=True,
+                 store_couplings=True, store_u_bytes=None):
+        """n_chunks: frame ranges per utterance (0: ~10 frames each); pose_fp8 / u_bf16: the
+        opt-in e4m3 pose, and u kept in bf16 on its streamed layers; store_couplings:
+        the forward keeps each frame's couplings for the backward (else recomputed where
+        the layer's kernels can); store_u_bytes: budget for keeping every layer's u from
+        the forward (None: 55 % of the device's memory; 0: recompute per range)."""
         self.B, self.T, self.lpad, self.rpad, self.iters = B, T, lpad, rpad, iters
         self.pose_fp8 = bool(pose_fp8)
+        self.store_couplings = bool(store_couplings)
+        self.store_u_bytes = store_u_bytes
         self.layers = layers
         self.L = len(layers)
         self.win = lpad + rpad + 1
         if n_chunks <= 0:
             # ~10 frames per range (C3 step: 20-frame ranges 25.3 ms, 10-frame 23.95, 8-frame
             # 23.9, 5-frame 25.3: shorter ranges shorten the wavefront's fill and drain)
-            n_chunks = int(os.environ.get('SRF_SDR_CHUNKS', '0') or 0) or max(1, min(32, -(-T // 10)))
+            n_chunks = max(1, min(32, -(-T // 10)))
         # ranges of S frames on one grid, layer l's shifted down by l * rpad; the grid
         # runs M >= K ranges so that no layer's shifted range is clipped into a long
         # one (C5: rpad = 20 frames per layer would otherwise leave the last layer one
@@ -462,8 +469,8 @@ class SdrStackPlan:
         L_ = _lib.lib()
         self.rws = [L_.srf_route_sdr_recur_workspace(B, N * self.win, J, D, iters) for (N, din, J, D, mf) in layers]
         # fp8 pose: layers on the streaming recurrence keep u in bf16 (half the bytes of
-        # every read; 2^-9 against the e4m3 operands' 2^-4); SRF_SDR_U_BF16=0 keeps fp32
-        self.ubf = [self.pose_fp8 and os.environ.get('SRF_SDR_U_BF16', '1') != '0'
+        # every read; 2^-9 against the e4m3 operands' 2^-4); u_bf16=False keeps fp32
+        self.ubf = [self.pose_fp8 and bool(u_bf16)
                     and bool(L_.srf_route_sdr_couplings_required(N * self.win, J, D, iters))
                     for (N, din, J, D, mf) in layers]
 
@@ -507,8 +514,6 @@ def _layer_streams(dev, n, role):
     in the forward (caller's thread) and again in the backward (torch's autograd device
     thread) crashes at capture end on this ROCm, while forking them twice from one
     thread, or disjoint streams per role, capture fine (scripts/dbg/capture_probe*.py)."""
-    if os.environ.get('SRF_SDR_STREAMS', '') == '1':   # A/B and debugging: the wavefront on one stream
-        return [torch.cuda.current_stream(dev)] * n
     ss = _stack_streams.setdefault((dev, role), [])
     while len(ss) < n:
         ss.append(torch.cuda.Stream(device=dev))
@@ -517,20 +522,12 @@ def _layer_streams(dev, n, role):
 
 def _store_u(plan, dev):
     """Keep every layer's pose output u from the forward for the backward (instead of
-    recomputing it per range) when it fits SRF_SDR_STORE_U_GB, by default 55 % of the
+    recomputing it per range) when it fits plan.store_u_bytes, by default 55 % of the
     device's memory: C5 keeps 135 GB of u on a 288 GB MI355X, C3 5.5 GB."""
-    gb = os.environ.get('SRF_SDR_STORE_U_GB', '')
-    budget = float(gb) * 2 ** 30 if gb else 0.55 * torch.cuda.get_device_properties(dev).total_memory
+    budget = plan.store_u_bytes
+    if budget is None:
+        budget = 0.55 * torch.cuda.get_device_properties(dev).total_memory
     return sum(plan.u_bytes(l, plan.T) for l in range(plan.L)) <= budget
-
-
-def _whole_gu(plan):
-    """Keep each layer's whole gu (instead of one frame range at a time) so its weight
-    gradient runs once per layer, off the wavefront, on a stream of its own.  Off by
-    default (SRF_SDR_WHOLE_GU_GB=0): at C3 the concurrent gW passes slow the
-    latency-bound recurrences more than they save (32.2 vs 30.6 ms per step)."""
-    budget = float(os.environ.get('SRF_SDR_WHOLE_GU_GB', '0')) * 2 ** 30
-    return sum(plan.u_floats(l, plan.T) for l in range(plan.L)) * 4 <= budget
 
 
 def _sdr_r(**kw):
@@ -577,9 +574,9 @@ class SdrStack(torch.autograd.Function):
         for l, (N, din, J, D, mf) in enumerate(P.layers):
             vs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
             # each frame's couplings and s^r, for a backward without the recompute
-            # (SRF_SDR_CS=0: recompute them, where the shape's kernels can)
+            # (store_couplings=False: recompute them, where the shape's kernels can)
             ncs = L_.srf_route_sdr_coupling_floats(P.in_n(l), J, D, P.iters) \
-                if need_bwd and (os.environ.get('SRF_SDR_CS', '1') != '0'
+                if need_bwd and (P.store_couplings
                                  or L_.srf_route_sdr_couplings_required(P.in_n(l), J, D, P.iters)) else 0
             css.append(torch.empty(B * T * ncs, device=dev, dtype=torch.float32) if ncs else None)
             if l < L - 1:
@@ -595,8 +592,7 @@ class SdrStack(torch.autograd.Function):
         pa, pb, pc = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream), ctypes_void(sc.cuda_stream)
         # the last layer's pose runs ahead of its recurrence on stream C when u is kept
         # whole (a range buffer would be overwritten by the next pose)
-        pose_ahead = (store or not need_bwd and P.u_bytes(L - 1, T) <= 2 ** 30) and \
-            os.environ.get('SRF_SDR_POSE_AHEAD', '1') != '0'
+        pose_ahead = store or not need_bwd and P.u_bytes(L - 1, T) <= 2 ** 30
         if pose_ahead and not store:
             us[L - 1] = P.u_empty(L - 1, T, dev)
 
@@ -703,14 +699,6 @@ class SdrStack(torch.autograd.Function):
                                    dtype=torch.uint8) if l < L - 1 else None)
         main = torch.cuda.current_stream(dev)
         sa, sb = _layer_streams(dev, 2, 'bwd')
-        # The last layer's gW runs on stream A, off B's critical chain, when its whole gu
-        # fits SRF_SDR_GW_SIDE_GB (default 0, off: at C3 26.8 vs 25.2 ms, stream A is as
-        # critical as B; the last layer's whole gu is 1.8 GB): B then never reuses a gu range
-        # buffer that A still reads, so A waits on B only.  (B waiting on A as well --
-        # two side streams ordered both ways -- crashes this ROCm's capture_end.)
-        gw_side = L > 1 and P.u_floats(L - 1, T) * 4 <= float(os.environ.get('SRF_SDR_GW_SIDE_GB', '0')) * 2 ** 30
-        if gw_side:
-            gus[L - 1] = torch.empty(P.u_floats(L - 1, T), device=dev)
         ev_b = P.events('bwd_b', P.K)   # the last layer's range k has its gu and gx
         for s_ in (sa, sb):
             s_.wait_stream(main)
@@ -727,8 +715,7 @@ class SdrStack(torch.autograd.Function):
                           u=_ptr(urs[l]), v0=v0, vn=vn, v=_ptr(vs[l]),
                           couplings=_ptr(cs) if cs is not None else None, workspace=_ptr(rws[l]),
                           workspace_bytes=rws[l].numel(), g_v=_ptr(g_vs[l]), carry=_ptr(carries[l]),
-                          gu=_ptr(gus[l]), g0=0 if (gw_side and l == L - 1) else t0,
-                          gn=T if (gw_side and l == L - 1) else P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
+                          gu=_ptr(gus[l]), g0=t0, gn=P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
                           g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1), u_bf16=int(P.ubf[l]))
 
         def run(sp, ls, ks, ev=None, gw=True):
@@ -773,7 +760,7 @@ class SdrStack(torch.autograd.Function):
         for e in range(P.K + L - 1):
             k = P.K - 1 - e
             if k >= 0:   # last layer, range k, on stream B
-                run(pb, [L - 1], [k], ev=ev_b[k], gw=not gw_side)
+                run(pb, [L - 1], [k], ev=ev_b[k])
             groups = {}
             for l in range(L - 1):
                 kk = P.K - 1 - (e - (L - 2 - l))
@@ -784,8 +771,6 @@ class SdrStack(torch.autograd.Function):
             kl = P.K - 1 - e   # (L-2, kl) is in this diagonal: it needs the last layer's range kl
             if L > 1 and 0 <= kl < P.K:
                 sa.wait_event(ev_b[kl])
-                if gw_side:
-                    gw_ranges(pa, [L - 1], [kl])
             for g in groups.values():
                 run(pa, [l for l, _ in g], [kk for _, kk in g])
         for s_ in (sa, sb):
@@ -794,179 +779,8 @@ class SdrStack(torch.autograd.Function):
         return (g_embs[0], None, None, None, None, *_returned(targets))
 
 
-class SdrStackPerLayer(torch.autograd.Function):
-    """The round-3 first form of the stack (one HIP stream per layer, one launch per
-    range), kept for A/B runs (SRF_SDR_BATCH=0): the layer streams share the process's
-    four in-order hardware queues, so a range waiting on another layer blocks the
-    ranges queued behind it (measured concurrency 1-2 recurrences at C3/C5)."""
-
-    """emb0 [B,T,N0,din0] -> v of the last layer [B,T,J,D]; in between, layer l's v
-    goes through drop(LN_mid{l+1}(v)) (the CapsNorm of naive:187-191) into layer
-    l+1.  params: W_l, b_l for every layer, then gamma_l, beta_l for l < L-1."""
-
-    @staticmethod
-    def forward(ctx, emb0, plan, training, p_mid, seed, *params):
-        L_ = _lib.lib()
-        P, B, T, L = plan, plan.B, plan.T, plan.L
-        dev = emb0.device
-        Ws, bs = params[0:2 * L:2], params[1:2 * L:2]
-        gammas, betas = params[2 * L::2], params[2 * L + 1::2]
-        _check_dev('emb0', emb0, (B, T, P.layers[0][0], P.layers[0][1]))
-        need_bwd = P.need_bwd
-        store = need_bwd and _store_u(P, emb0.device)
-        tr = int(bool(training))
-        embs, vs, stats, us, rws, css = [emb0], [], [], [], [], []
-        for l, (N, din, J, D, mf) in enumerate(P.layers):
-            vs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
-            # each frame's couplings and s^r, for a backward without the recompute
-            # (SRF_SDR_CS=0: recompute them, where the shape's kernels can)
-            ncs = L_.srf_route_sdr_coupling_floats(P.in_n(l), J, D, P.iters) \
-                if need_bwd and (os.environ.get('SRF_SDR_CS', '1') != '0'
-                                 or L_.srf_route_sdr_couplings_required(P.in_n(l), J, D, P.iters)) else 0
-            css.append(torch.empty(B * T * ncs, device=dev, dtype=torch.float32) if ncs else None)
-            if l < L - 1:
-                embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
-                stats.append(torch.empty((B * T, 4), device=dev, dtype=torch.float32))
-            us.append(torch.empty(P.u_floats(l, T if store else P.nmax), device=dev, dtype=torch.float32))
-            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
-        main = torch.cuda.current_stream(dev)
-        streams = _layer_streams(dev, L, 'fwd')
-        done = P.events('fwd')
-        for s in streams:
-            s.wait_stream(main)
-        # issue along anti-diagonals d = k + l: the streams share a few hardware queues
-        # (in-order), so items are queued in the order they become ready
-        for k, l in ((d - l, l) for d in range(P.K + L - 1) for l in range(L) if 0 <= d - l < P.K):
-            N, din, J, D, mf = P.layers[l]
-            s = streams[l]
-            t0, t1 = P.fwd[l][k], P.fwd[l][k + 1]
-            if l > 0:
-                s.wait_event(done[l - 1][k])
-            if t1 > t0:
-                sp = ctypes_void(s.cuda_stream)
-                v0, vn = (0, T) if store else (t0, P.nmax)
-                pose = L_.srf_route_sdr_pose_fp8 if P.pose_fp8 else L_.srf_route_sdr_pose
-                _lib.check(pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din, P.lpad,
-                                P.rpad, J, D, t0, t1, _ptr(us[l]), v0, vn, sp), 'sdr_pose')
-                _lib.check(L_.srf_route_sdr_recur_fwd(_ptr(us[l]), v0, vn, B, T, P.in_n(l), J, D, P.iters, mf, t0,
-                                                      t1, _ptr(vs[l]), _ptr(css[l]) if css[l] is not None else None,
-                                                      _ptr(rws[l]), rws[l].numel(), sp), 'sdr_recur_fwd')
-                if l < L - 1:
-                    _lib.check(L_.srf_capsnorm_fwd_range(_ptr(vs[l]), B, T, t0, t1, J * D, _ptr(gammas[l]),
-                                                         _ptr(betas[l]), tr, float(p_mid), int(seed), l,
-                                                         _ptr(embs[l + 1]), _ptr(stats[l]), sp), 'capsnorm_range')
-            done[l][k].record(s)
-        for s in streams:
-            main.wait_stream(s)
-        ctx.plan, ctx.meta = P, (tr, float(p_mid), int(seed), store)
-        ctx.params = params
-        ctx.css = css
-        ctx.save_for_backward(*embs, *vs, *stats, *(us if store else []), *params)
-        return vs[-1]
-
-    @staticmethod
-    def backward(ctx, g_v_last):
-        L_ = _lib.lib()
-        P = ctx.plan
-        B, T, L = P.B, P.T, P.L
-        tr, p_mid, seed, store = ctx.meta
-        saved = list(ctx.saved_tensors)
-        embs, saved = saved[:L], saved[L:]
-        vs, saved = saved[:L], saved[L:]
-        stats, saved = saved[:L - 1], saved[L - 1:]
-        if store:
-            us, saved = saved[:L], saved[L:]
-        params = saved
-        Ws, bs = params[0:2 * L:2], params[1:2 * L:2]
-        gammas, betas = params[2 * L::2], params[2 * L + 1::2]
-        dev = g_v_last.device
-        g_v_last = g_v_last.contiguous()
-        whole_gu = _whole_gu(P)
-        targets = [_grad_target(p) for p in ctx.params]
-        gWs, gbs = [targets[2 * l][0] for l in range(L)], [targets[2 * l + 1][0] for l in range(L)]
-        ggs = [targets[2 * L + 2 * l][0] for l in range(L - 1)]
-        gbts = [targets[2 * L + 2 * l + 1][0] for l in range(L - 1)]
-        g_embs = [torch.zeros_like(e) for e in embs]           # gx scatter targets
-        g_vs, gparts, carries, WTs, gus, urs, rws, pws = [], [], [], [], [], [], [], []
-        for l, (N, din, J, D, mf) in enumerate(P.layers):
-            n = J * D
-            g_vs.append(torch.empty((B, T, J, D), device=dev) if l < L - 1 else g_v_last)
-            gparts.append(torch.empty((B * T, 2 * n), device=dev) if l < L - 1 else None)
-            carries.append(torch.zeros((B, n), device=dev))
-            WTs.append(torch.empty(Ws[l].numel(), device=dev))
-            gus.append(torch.empty(P.u_floats(l, T if whole_gu else P.nmax), device=dev))
-            urs.append(us[l] if store else torch.empty(P.u_floats(l, P.nmax), device=dev))
-            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
-            pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
-                                   dtype=torch.uint8) if l < L - 1 else None)
-        main = torch.cuda.current_stream(dev)
-        streams = _layer_streams(dev, L, 'bwd')
-        ws = _layer_streams(dev, 1, 'weights')[0]
-        ws.wait_stream(main)
-        done = P.events('bwd')
-        for s in streams:
-            s.wait_stream(main)
-        for l, (N, din, J, D, mf) in enumerate(P.layers):
-            _lib.check(L_.srf_route_sdr_transpose_w(_ptr(Ws[l]), P.in_n(l), J, D, din, _ptr(WTs[l]),
-                                                    ctypes_void(streams[l].cuda_stream)), 'sdr_transpose_w')
-        # anti-diagonals of (range position from the end, layer position from the top)
-        for k, l in ((P.K - 1 - (d - (L - 1 - l)), l) for d in range(P.K + L - 1) for l in reversed(range(L))
-                     if 0 <= d - (L - 1 - l) < P.K):
-            N, din, J, D, mf = P.layers[l]
-            s = streams[l]
-            sp = ctypes_void(s.cuda_stream)
-            t0, t1 = P.bwd[l][k], P.bwd[l][k + 1]
-            if l < L - 1:
-                s.wait_event(done[l + 1][k])
-            if t1 > t0:
-                if l < L - 1:
-                    _lib.check(L_.srf_capsnorm_bwd_range(_ptr(vs[l]), B, T, t0, t1, J * D, _ptr(gammas[l]),
-                                                         _ptr(betas[l]), tr, p_mid, seed, l, _ptr(stats[l]),
-                                                         _ptr(g_embs[l + 1]), _ptr(g_vs[l]), _ptr(gparts[l]), sp),
-                               'capsnorm_bwd_range')
-                v0, vn = (0, T) if store else (t0, P.nmax)
-                if not store:
-                    pose = L_.srf_route_sdr_pose_fp8 if P.pose_fp8 else L_.srf_route_sdr_pose
-                    _lib.check(pose(_ptr(embs[l]), _ptr(Ws[l]), _ptr(bs[l]), B, T, N, din,
-                                    P.lpad, P.rpad, J, D, t0, t1, _ptr(urs[l]), v0, vn, sp), 'sdr_pose')
-                cs = ctx.css[l]
-                g0, gn = (0, T) if whole_gu else (t0, P.nmax)
-                _lib.check(L_.srf_route_sdr_recur_bwd(_ptr(urs[l]), v0, vn, _ptr(vs[l]),
-                                                      _ptr(cs) if cs is not None else None, _ptr(g_vs[l]), B, T,
-                                                      P.in_n(l), J, D, P.iters, mf, t0, t1, _ptr(carries[l]),
-                                                      _ptr(gus[l]), g0, gn, _ptr(rws[l]), rws[l].numel(),
-                                                      sp), 'sdr_recur_bwd')
-                _lib.check(L_.srf_route_sdr_gx(_ptr(gus[l]), g0, gn, _ptr(WTs[l]), B, T, N, din, P.lpad,
-                                               P.rpad, J, D, t0, t1, _ptr(g_embs[l]), sp), 'sdr_gx')
-                if not whole_gu:
-                    _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), t0, P.nmax, _ptr(embs[l]), B, T, N, din, P.lpad,
-                                                   P.rpad, J, D, t0, t1, int(k != P.K - 1), _ptr(gWs[l]),
-                                                   _ptr(gbs[l]), sp), 'sdr_gw')
-            elif k == P.K - 1 and not whole_gu:   # empty first range: the accumulation still starts from zero
-                _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), 0, P.nmax, _ptr(embs[l]), B, T, N, din, P.lpad,
-                                               P.rpad, J, D, 0, 0, 0, _ptr(gWs[l]), _ptr(gbs[l]), sp), 'sdr_gw')
-            done[l][k].record(s)
-            if k == 0 and whole_gu:
-                # the layer's whole gu is written: its gW / gbias on the weights stream,
-                # overlapping the recurrences of the layers below
-                ws.wait_event(done[l][0])
-                _lib.check(L_.srf_route_sdr_gw(_ptr(gus[l]), 0, T, _ptr(embs[l]), B, T, N, din, P.lpad, P.rpad,
-                                               J, D, 0, T, 0, _ptr(gWs[l]), _ptr(gbs[l]),
-                                               ctypes_void(ws.cuda_stream)), 'sdr_gw')
-            if k == 0 and l < L - 1:
-                _lib.check(L_.srf_capsnorm_bwd_params(_ptr(gparts[l]), B * T, J * D, _ptr(ggs[l]),
-                                                      _ptr(gbts[l]), _ptr(pws[l]), pws[l].numel(), sp),
-                           'capsnorm_bwd_params')
-        for s in streams + [ws]:
-            main.wait_stream(s)
-        ctx.css = None
-        return (g_embs[0], None, None, None, None, *_returned(targets))
-
-
 def sdr_stack(emb0, plan, training, p_mid, seed, params):
     """SdrStack.apply; the forward keeps the pose outputs for the backward only when
     one will run (grad mode on and something requires a gradient)."""
     plan.need_bwd = torch.is_grad_enabled() and (emb0.requires_grad or any(p.requires_grad for p in params))
-    if os.environ.get('SRF_SDR_BATCH', '1') == '0':
-        return SdrStackPerLayer.apply(emb0, plan, training, p_mid, seed, *params)
     return SdrStack.apply(emb0, plan, training, p_mid, seed, *params)

@@ -14,7 +14,6 @@ Dropout masks come from a counter-based RNG keyed by a per-call seed, so the
 backward kernels regenerate them instead of storing them.
 """
 import math
-import os
 
 import numpy as np
 import torch
@@ -89,9 +88,13 @@ class SequenceRouter(torch.nn.Module):
         # Opt-in fp8 (e4m3) pose transform for SDR stacks (BASELINE C5 "fp8 pose-transform
         # MFMA"; not a reference flag: the reference is fp32 throughout).  Its bound is
         # stated in include/srf.h (srf_route_sdr_pose_fp8); gradients stay fp32.
-        self.pose_fp8 = bool(getattr(config, 'model_pose_fp8', False)) or os.environ.get('SRF_POSE_FP8', '') == '1'
+        self.pose_fp8 = bool(getattr(config, 'model_pose_fp8', False))
         self.dropout_enabled = True     # test hook: parity runs use BN batch stats without dropout
-        self.n_chunks_override = {}     # layer -> n_chunks (tuning hook)
+        self.n_chunks_override = {}     # DR layer -> input-capsule chunks of its routing passes (plan argument)
+        # SDR: every layer as one layer-pipelined wavefront (ops.SdrStack; False: layer by
+        # layer), with ops.SdrStackPlan options (n_chunks, store_couplings, store_u_bytes, u_bf16)
+        self.sdr_stack = True
+        self.sdr_options = {}
         # Dropout seed base.  Parameters are initialised from `seed` identically on every
         # replica (MirroredStrategy mirrors one set of variables), but each replica draws
         # its own dropout masks, so the replica id is mixed in (rank 0 keeps the plain
@@ -241,7 +244,8 @@ class SequenceRouter(torch.nn.Module):
             layers = []
             for l, (in_n, out_n, out_d, in_d) in enumerate(self.layer_shapes):
                 layers.append((in_n // self.window, in_d, out_n, out_d, int(l == self.enc_num - 1)))
-            p = ops.SdrStackPlan(B, T, layers, self.lpad, self.rpad, self.route_iters, pose_fp8=self.pose_fp8)
+            p = ops.SdrStackPlan(B, T, layers, self.lpad, self.rpad, self.route_iters, pose_fp8=self.pose_fp8,
+                                 **self.sdr_options)
             self._geoms[key] = p
         return p
 
@@ -278,7 +282,7 @@ class SequenceRouter(torch.nn.Module):
                                self.proj_scale, self.caps_type == 'einsum')
         B, T2 = emb.shape[:2]
         p_mid = self.inn_dropout if drop else 0.0
-        if self.is_context and self.enc_num > 1 and os.environ.get('SRF_SDR_STACK', '1') != '0':
+        if self.is_context and self.enc_num > 1 and self.sdr_stack:
             # every SDR layer (and the LN + dropout between them) as one layer-pipelined
             # wavefront (ops.SdrStack); the head as below
             last = self.enc_num - 1

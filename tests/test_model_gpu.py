@@ -232,26 +232,24 @@ def test_graphed_dropout_gradient_matches_finite_difference(cuda):
         g.close()
 
 
-@pytest.mark.parametrize('name,chunks,cs,store', [('c3_mini_sdr', 1, '1', ''), ('c3_mini_sdr', 3, '1', ''),
-                                                  ('c3_mini_sdr', 64, '1', ''), ('c3_real', 4, '1', ''),
-                                                  ('c3_real', 4, '0', ''), ('c3_real', 4, '1', '0'),
-                                                  ('c5_real', 3, '1', ''), ('c5_real', 3, '1', '0'),
-                                                  ('c3_mini_sdr_lowmemory', 2, '1', '')])
-def test_sdr_stack_matches_layer_by_layer(cuda, name, chunks, cs, store, monkeypatch):
+@pytest.mark.parametrize('name,chunks,cs,store', [('c3_mini_sdr', 1, True, None), ('c3_mini_sdr', 3, True, None),
+                                                  ('c3_mini_sdr', 64, True, None), ('c3_real', 4, True, None),
+                                                  ('c3_real', 4, False, None), ('c3_real', 4, True, 0),
+                                                  ('c5_real', 3, True, None), ('c5_real', 3, True, 0),
+                                                  ('c3_mini_sdr_lowmemory', 2, True, None)])
+def test_sdr_stack_matches_layer_by_layer(cuda, name, chunks, cs, store):
     """The layer-pipelined SDR stack (ops.SdrStack: frame ranges of every layer as a
-    wavefront over one HIP stream per layer) against the layer-by-layer path
-    (SRF_SDR_STACK=0): the same logits and gradients to fp32 reassociation, for one
-    range, several, and one frame per range (64 > T'); its backward from the
-    forward's stored couplings (SRF_SDR_CS=1) and recomputing them (0); u kept from
-    the forward (default) and recomputed per range (SRF_SDR_STORE_U_GB=0)."""
+    wavefront) against the layer-by-layer path (model.sdr_stack = False): the same
+    logits and gradients to fp32 reassociation, for one range, several, and one frame
+    per range (64 > T'); its backward from the forward's stored couplings
+    (store_couplings) and recomputing them; u kept from the forward (default) and
+    recomputed per range (store_u_bytes = 0)."""
     from srf_amd import ctc
-    monkeypatch.setenv('SRF_SDR_CS', cs)
-    monkeypatch.setenv('SRF_SDR_STORE_U_GB', store)
     outs = []
-    for stack in ('1', '0'):
-        monkeypatch.setenv('SRF_SDR_STACK', stack)
-        monkeypatch.setenv('SRF_SDR_CHUNKS', str(chunks))
+    for stack in (True, False):
         model, sh, z = _build(name, cuda)
+        model.sdr_stack = stack
+        model.sdr_options = dict(n_chunks=chunks, store_couplings=cs, store_u_bytes=store)
         feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
         inp_len = torch.tensor(z['inp_len'], device=cuda)
         model.zero_grad()

@@ -30,11 +30,19 @@ CASES = [
     (1, 10, 8, 16, 4, 4, 63, 3, True),    # TIMIT-sized last layer: J = 63 (padded to 64), in_n = 72
     (2, 6, 4, 8, 0, 0, 3, 2, True),       # J = 3 (padded to 4), D = 8, no window
 ]
-# shapes run again through the first (LDS-state, one workgroup per utterance) recurrence kernels
-LEGACY = [CASES[0], CASES[2], CASES[3], CASES[5]]
+# shapes outside the register-resident (dout 8 | 16 | 32) and streaming (dout 32 | 64)
+# kernels' cases, which run on the general LDS-state recurrence kernels (one workgroup
+# per utterance); the optional last element is dout (default: = din)
+LEGACY = [
+    (2, 9, 4, 16, 1, 1, 5, 3, True, 12),
+    (1, 7, 8, 8, 2, 2, 16, 3, False, 4),
+    (2, 6, 4, 32, 2, 2, 6, 5, True, 20),
+]
+# ... and one whose frame state (in_n = 656 capsules x 8, five iterations) exceeds one
+# CU's LDS: the same kernels keep it in the global workspace
+GSTATE = [(1, 4, 16, 8, 20, 20, 8, 5, True, 4)]
 # shapes of the streaming recurrence (route_sdr_stream.hip: dout 32 | 64, J*dout in
-# {512, 1024, 2048}), run with SRF_SDR_SEQ=0 so that shapes the register path also
-# takes come here too
+# {512, 1024, 2048}) that the register path does not take
 STREAM = [
     (1, 3, 16, 64, 20, 20, 16, 5, False),  # C5 inner layer: in_n = 656, J*D = 1024, five iterations
     (2, 6, 4, 64, 2, 2, 16, 3, True),      # in_n = 20, last-layer mask
@@ -45,20 +53,25 @@ STREAM = [
 ]
 
 
+def _dims(case):
+    B, T, N, D, lp, rp, J, it, mf = case[:9]
+    return B, T, N, D, lp, rp, J, it, mf, (case[9] if len(case) > 9 else D)
+
+
 def _mk(case, seed):
-    B, T, N, D, lp, rp, J, it, mf = case
+    B, T, N, D, lp, rp, J, it, mf, Do = _dims(case)
     rng = np.random.default_rng(seed)
     in_n = N * (lp + rp + 1)
     emb = rng.standard_normal((B, T, N, D)) * 0.5
-    W = rng.standard_normal((in_n, J, D, D)) * 0.1
-    bias = rng.standard_normal((in_n, J, D)) * 0.1
+    W = rng.standard_normal((in_n, J, Do, D)) * 0.1
+    bias = rng.standard_normal((in_n, J, Do)) * 0.1
     return emb, W, bias
 
 
 def _run_gpu(case, emb, W, bias, dev):
     from srf_amd.ops import RouteGeom, sequential_routing
-    B, T, N, D, lp, rp, J, it, mf = case
-    g = RouteGeom(B, T, N, D, lp, rp, J, D, it, mf)
+    B, T, N, D, lp, rp, J, it, mf, Do = _dims(case)
+    g = RouteGeom(B, T, N, D, lp, rp, J, Do, it, mf)
     te = torch.tensor(emb, dtype=torch.float32, device=dev, requires_grad=True)
     tW = torch.tensor(W, dtype=torch.float32, device=dev, requires_grad=True)
     tb = torch.tensor(bias, dtype=torch.float32, device=dev, requires_grad=True)
@@ -68,7 +81,7 @@ def _run_gpu(case, emb, W, bias, dev):
 def _check_forward(case, dev):
     emb, W, bias = _mk(case, 11)
     _, _, _, v = _run_gpu(case, emb, W, bias, dev)
-    B, T, N, D, lp, rp, J, it, mf = case
+    B, T, N, D, lp, rp, J, it, mf, Do = _dims(case)
     ref = so.sequential_routing(so.pose(so.window(emb, lp, rp), W, bias), it, mf)
     got = v.detach().cpu().double().numpy()
     assert np.all(np.abs(got - ref) <= 2e-5 * (1 + np.abs(ref))), np.abs(got - ref).max()
@@ -80,20 +93,17 @@ def test_route_sdr_forward(cuda, case):
 
 
 @pytest.mark.parametrize('case', LEGACY)
-def test_route_sdr_legacy_kernels(cuda, case, monkeypatch):
-    """SRF_SDR_SEQ=0 selects the LDS-state recurrence kernels (the path for
-    shapes beyond the register-resident kernels' budget)."""
-    monkeypatch.setenv('SRF_SDR_SEQ', '0')
-    monkeypatch.setenv('SRF_SDR_STREAM', '0')
+def test_route_sdr_legacy_kernels(cuda, case):
+    """The LDS-state recurrence kernels (the general path for capsule widths the
+    register-resident and streaming kernels do not cover)."""
     _check_forward(case, cuda)
     _check_backward(case, cuda)
 
 
 @pytest.mark.parametrize('case', STREAM)
-def test_route_sdr_stream_kernels(cuda, case, monkeypatch):
+def test_route_sdr_stream_kernels(cuda, case):
     """The streaming recurrence (u_t re-read per iteration, stored couplings for the
     backward): forward and backward against the oracle."""
-    monkeypatch.setenv('SRF_SDR_SEQ', '0')
     _check_forward(case, cuda)
     _check_backward(case, cuda)
 
@@ -108,7 +118,7 @@ def _check_backward(case, cuda):
     te, tW, tb, v = _run_gpu(case, emb, W, bias, cuda)
     gv = np.random.default_rng(13).standard_normal(v.shape)
     v.backward(torch.tensor(gv, dtype=torch.float32, device=cuda))
-    B, T, N, D, lp, rp, J, it, mf = case
+    B, T, N, D, lp, rp, J, it, mf, Do = _dims(case)
     ce = torch.tensor(emb, requires_grad=True)
     cW = torch.tensor(W, requires_grad=True)
     cb = torch.tensor(bias, requires_grad=True)
@@ -123,13 +133,10 @@ def _check_backward(case, cuda):
         assert err <= 1e-4 * max(1.0, np.abs(ref).max()), (name, err, np.abs(ref).max())
 
 
-@pytest.mark.parametrize('case', LEGACY[:2])
-def test_route_sdr_global_state_kernels(cuda, case, monkeypatch):
-    """SRF_SDR_GSTATE=1 moves the legacy kernels' frame state from LDS to the
-    global-memory workspace (the path of shapes whose state exceeds one CU's LDS)."""
-    monkeypatch.setenv('SRF_SDR_SEQ', '0')
-    monkeypatch.setenv('SRF_SDR_STREAM', '0')
-    monkeypatch.setenv('SRF_SDR_GSTATE', '1')
+@pytest.mark.parametrize('case', GSTATE)
+def test_route_sdr_global_state_kernels(cuda, case):
+    """The LDS-state kernels with their frame state in the global-memory workspace
+    (shapes whose state exceeds one CU's LDS)."""
     _check_forward(case, cuda)
     _check_backward(case, cuda)
 
@@ -183,17 +190,6 @@ def test_sdr_pose_fp8_bound(cuda, din, J, D):
     assert np.all(err <= 0.13 * mag + 1e-6 * (np.abs(ref) + 1e-30)), (err - 0.13 * mag).max()
     rel = err[mag > 0] / mag[mag > 0]
     assert np.median(rel) < 0.02, np.median(rel)
-
-
-@pytest.mark.parametrize('mf', ['0', '1'])
-@pytest.mark.parametrize('case', [CASES[2], CASES[3], STREAM[1]])
-def test_route_sdr_gemm_families(cuda, case, mf, monkeypatch):
-    """Both kernel families of the frame-parallel contractions (pose, gx, gW; 16x16
-    f32 MFMA tiles and 32x32 ones, chosen per contraction and din by default) forced
-    for all three, din 32 and 64, against the oracle."""
-    monkeypatch.setenv('SRF_SDR_MFMA32', mf)
-    _check_forward(case, cuda)
-    _check_backward(case, cuda)
 
 
 @pytest.mark.parametrize('J,D,iters,mf', [(16, 64, 5, False), (32, 64, 3, True)])
