@@ -10,15 +10,19 @@ write one back:
     Key "" holds BundleHeaderProto, every other key a BundleEntryProto
     (dtype=1, shape=2, shard_id=3, offset=4, size=5, crc32c=6 (masked), slices=7);
   * ``<prefix>.data-SSSSS-of-NNNNN``: raw little-endian tensor bytes.
-Only numeric dense tensors are decoded (DT_STRING entries such as
-_CHECKPOINTABLE_OBJECT_GRAPH are listed but skipped), and only uncompressed
-tables (TF writes its bundles uncompressed).  Written bundles carry no object
-graph, so TF reads them with tf.train.load_checkpoint / list_variables rather
-than Checkpoint.restore.
+Numeric dense tensors are decoded, and the scalar DT_STRING tensor
+``_CHECKPOINTABLE_OBJECT_GRAPH`` (read_object_graph); only uncompressed tables
+(TF writes its bundles uncompressed).  Written bundles carry that object graph --
+a TrackableObjectGraph (trackable_object_graph.proto) whose children follow the
+object paths of the keys (``model/conv/conv_layers/0/0/kernel`` ...), with the
+optimizer's slot variables -- so ``tf.train.Checkpoint(optimizer=, model=)
+.restore(prefix)`` (misc_helper.py:141-156, average_ckpt_sr.py:122-123) can match
+them to the live objects by attribute name.
 
-Parity: restated from the public table / tensor_bundle.proto formats; no
-TF-written bundle ships in the reference and TF is not installed, so it is
-pinned only by its own round trip and hand-built tables (parity unpinned).
+Parity: restated from the public table / tensor_bundle.proto /
+trackable_object_graph.proto formats; no TF-written bundle ships in the reference
+and TF is not installed, so it is pinned by its own round trip, hand-built tables
+and protobuf's own serialisation of the object graph (parity against TF unpinned).
 """
 import os
 import struct
@@ -222,6 +226,117 @@ def _entries(prefix):
     return out
 
 
+OBJECT_GRAPH_KEY = '_CHECKPOINTABLE_OBJECT_GRAPH'
+_ATTR = '/.ATTRIBUTES/VARIABLE_VALUE'
+_SLOT = '/.OPTIMIZER_SLOT/'
+
+
+def _ls(field, text):
+    return _ld(field, text.encode())
+
+
+def object_graph(keys):
+    """TrackableObjectGraph of a checkpoint whose variables sit at ``keys`` (TF2
+    object paths ``<path>/.ATTRIBUTES/VARIABLE_VALUE``; optimizer slots as
+    ``<variable path>/.OPTIMIZER_SLOT/<optimizer path>/<slot>/.ATTRIBUTES/...``).
+    Returns [{'children': [(local_name, node)], 'attributes': [(name, full_name,
+    checkpoint_key)], 'slots': [(original_node, slot_name, slot_node)]}], node 0 the
+    root; nodes in breadth-first order of the object tree, slot variables last."""
+    nodes = [{'children': [], 'attributes': [], 'slots': []}]
+    index = {(): 0}
+
+    def node(path):
+        path = tuple(path)
+        if path not in index:
+            parent = node(path[:-1])
+            index[path] = len(nodes)
+            nodes.append({'children': [], 'attributes': [], 'slots': []})
+            nodes[parent]['children'].append((path[-1], index[path]))
+        return index[path]
+
+    plain = sorted(k for k in keys if k.endswith(_ATTR) and _SLOT not in k)
+    for depth in range(1, max((k.count('/') for k in plain), default=0) + 2):   # breadth first
+        for k in plain:
+            parts = k[:-len(_ATTR)].split('/')
+            if len(parts) >= depth:
+                node(parts[:depth])
+    for k in plain:
+        path = k[:-len(_ATTR)]
+        nodes[node(path.split('/'))]['attributes'].append(('VARIABLE_VALUE', path, k))
+    for k in sorted(k for k in keys if k.endswith(_ATTR) and _SLOT in k):
+        var, rest = k[:-len(_ATTR)].split(_SLOT)
+        opt, slot = rest.rsplit('/', 1)
+        sid = len(nodes)
+        nodes.append({'children': [], 'attributes': [('VARIABLE_VALUE', f'{var}/{slot}', k)], 'slots': []})
+        nodes[node(opt.split('/'))]['slots'].append((node(var.split('/')), slot, sid))
+    return nodes
+
+
+def encode_object_graph(nodes):
+    """Wire bytes of TrackableObjectGraph {repeated TrackableObject nodes = 1}, with
+    TrackableObject {children = 1 (ObjectReference {node_id = 1, local_name = 2}),
+    attributes = 2 (SerializedTensor {name = 1, full_name = 2, checkpoint_key = 3}),
+    slot_variables = 3 (SlotVariableReference {original_variable_node_id = 1,
+    slot_name = 2, slot_variable_node_id = 3})} -- fields in number order, as
+    protobuf serialises them."""
+    out = b''
+    for n in nodes:
+        body = b''.join(_ld(1, _vi(1, nid) + _ls(2, name)) for name, nid in n['children'])
+        body += b''.join(_ld(2, _ls(1, a) + _ls(2, fn) + _ls(3, ck)) for a, fn, ck in n['attributes'])
+        body += b''.join(_ld(3, _vi(1, o) + _ls(2, sl) + _vi(3, sn)) for o, sl, sn in n['slots'])
+        out += _ld(1, body)
+    return out
+
+
+def decode_object_graph(buf):
+    nodes = []
+    for f, _, v in _fields(buf):
+        if f != 1:
+            continue
+        n = {'children': [], 'attributes': [], 'slots': []}
+        for g, _, w in _fields(v):
+            d = {h: x for h, _, x in _fields(w)}
+            if g == 1:
+                n['children'].append((bytes(d.get(2, b'')).decode(), d.get(1, 0)))
+            elif g == 2:
+                n['attributes'].append(tuple(bytes(d.get(h, b'')).decode() for h in (1, 2, 3)))
+            elif g == 3:
+                n['slots'].append((d.get(1, 0), bytes(d.get(2, b'')).decode(), d.get(3, 0)))
+        nodes.append(n)
+    return nodes
+
+
+def _string_tensor(values):
+    """tensor_bundle.cc's DT_STRING data: varint64 lengths, the masked CRC-32C of the
+    length bytes, then the strings; returns (bytes, masked crc of all of them)."""
+    lens = b''.join(_put_varint(len(v)) for v in values)
+    data = lens + struct.pack('<I', _crc_masked(lens)) + b''.join(values)
+    return data, _crc_masked(data)
+
+
+def read_object_graph(prefix, raw=False):
+    """The decoded _CHECKPOINTABLE_OBJECT_GRAPH of a bundle (raw=True: its wire
+    bytes), or None."""
+    header = {}
+    for key, value in _read_table(prefix + '.index'):
+        if key == b'':
+            header = {f: v for f, _, v in _fields(value)}
+        elif key == OBJECT_GRAPH_KEY.encode():
+            e = _parse_entry(value)
+            n_shards = header.get(1, 1) or 1
+            raw_bytes = raw
+            raw = open(f'{prefix}.data-{e["shard_id"]:05d}-of-{n_shards:05d}', 'rb').read()[
+                e['offset']:e['offset'] + e['size']]
+            if e['crc32c'] is not None and _crc_masked(raw) != e['crc32c']:
+                raise ValueError('object graph CRC mismatch')
+            n, pos = _varint(raw, 0)
+            if _crc_masked(raw[:pos]) != struct.unpack('<I', raw[pos:pos + 4])[0]:
+                raise ValueError('object graph length CRC mismatch')
+            graph = bytes(raw[pos + 4:pos + 4 + n])
+            return graph if raw_bytes else decode_object_graph(graph)
+    return None
+
+
 def load_checkpoint(prefix, verify_crc=True):
     """{name: numpy array} of every numeric tensor in the bundle."""
     ents = _entries(prefix)
@@ -247,13 +362,21 @@ def load_checkpoint(prefix, verify_crc=True):
     return out
 
 
-def save_checkpoint(prefix, tensors):
-    """Write {name: array} as a single-shard bundle (keys sorted, as TF's table needs)."""
+def save_checkpoint(prefix, tensors, with_object_graph=True):
+    """Write {name: array} as a single-shard bundle (keys sorted, as TF's table needs),
+    with the object graph of its keys (object_graph) unless with_object_graph=False."""
     os.makedirs(os.path.dirname(os.path.abspath(prefix)), exist_ok=True)
     data = bytearray()
     entries = [(b'', _vi(1, 1) + _vi(2, 0) + _ld(3, _vi(1, 1)))]   # num_shards=1, LITTLE, version{producer=1}
-    for name in sorted(tensors):
-        a = np.ascontiguousarray(tensors[name])
+    names = sorted(tensors) + ([OBJECT_GRAPH_KEY] if with_object_graph else [])
+    for name in sorted(names):
+        if name == OBJECT_GRAPH_KEY:
+            raw, crc = _string_tensor([encode_object_graph(object_graph(list(tensors)))])
+            entries.append((name.encode(), _encode_entry(DT_STRING, (), 0, len(data), len(raw), crc)))
+            data += raw
+            continue
+        a = np.asarray(tensors[name])
+        a = a if a.flags['C_CONTIGUOUS'] else a.copy(order='C')   # scalars stay 0-d (TF scalar variables)
         dt = _DTYPE_IDS.get(a.dtype)
         if dt is None:
             raise ValueError(f'{name}: dtype {a.dtype} not supported')
