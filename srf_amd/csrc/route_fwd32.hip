@@ -979,6 +979,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 }
 
 
+#ifndef SRF_FWD32P_VREG
+#define SRF_FWD32P_VREG 0   // 1: route_fwd32p_kernel keeps the Vc fragments in registers (LDS: stats only)
+#endif
 // Routing pass r >= 1, software-pipelined over the input capsules: while the matrix
 // cores form capsule i + 1's pose tiles (pose_prog, which also streams in capsule
 // i + 2's operands), the VALU finishes capsule i -- the cross-wave softmax statistics
@@ -1008,8 +1011,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
   const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
   const __amdgpu_buffer_rsrc_t lzs = make_rsrc(A.lzst, A.cst ? (size_t)A.in_n * A.Fs * 4 : 0);
+#if SRF_FWD32P_VREG
+  // this lane's Vc fragments in registers (no LDS reads per capsule)
+  float2* st = reinterpret_cast<float2*>(lds);
+  f4 vcr[TW][4];
+#else
   f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
+#endif
 #pragma unroll
   for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1017,7 +1026,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       const int row = (tbase + t) * 32 + 8 * q + 4 * h;
       f4 v = {0.f, 0.f, 0.f, 0.f};
       if (fvalid && row < JD) v = *reinterpret_cast<const f4*>(A.vc + (size_t)f * JD + row);
+#if SRF_FWD32P_VREG
+      vcr[t][q] = v;
+#else
       vcl[(t * 4 + q) * 64 + lane] = v;
+#endif
     }
   float mk[OWN];
 #pragma unroll
@@ -1046,7 +1059,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       for (int t = 0; t < TW; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+#if SRF_FWD32P_VREG
+          const f4 vv = vcr[t][q];
+#else
           const f4 vv = vcl[(t * 4 + q) * 64 + lane];
+#endif
           const int k = kpart<DOUT>(t, 4 * q);
           P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv.x, vv.y};
           P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv.z, vv.w};
