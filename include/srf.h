@@ -148,6 +148,13 @@ typedef struct {
   int accumulate;              /* gW: add to g_W / g_bias (else overwrite) */
   int u_bf16;                  /* u holds bf16 (written by pose_n mode 2; read by the streaming
                                   recurrence kernels only, i.e. srf_route_sdr_couplings_required) */
+  int group;                   /* recur_fwd_n / recur_bwd_n on the streaming kernels: workgroups per
+                                  utterance (0 or 1: one; at most 8, equal over a launch's ranges).
+                                  A group splits the input capsules and adds its partial sums inside
+                                  the launch, spin-waiting on its members: the launch's
+                                  B * n * group workgroups must be resident together, so it is
+                                  refused above the device's CU count and the caller runs no other
+                                  grouped launch concurrently.  Other shapes ignore it. */
 } srf_sdr_range;
 /* pose_n fp8: 0 fp32 pose, 1 fp8 pose (fp32 u), 2 fp8 pose storing u in bf16 */
 int srf_route_sdr_pose_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,

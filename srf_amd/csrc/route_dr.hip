@@ -992,34 +992,38 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
   float gmax = 0.f;
   auto compute = [&](auto slot) {
     constexpr int sl = decltype(slot)::value;
-    float gu[16];
+    // gu on packed pairs (v_pk_fma_f32), the lane's max |gu| for the frame's exponent
+    f2 gu[8];
     float m = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      float a = gsr[0][k];
+    for (int k = 0; k < 8; ++k) {
+      f2 a = f2{gsr[0][2 * k], gsr[0][2 * k + 1]};
 #pragma unroll
       for (int r = 0; r < RV; ++r) {
-        a = fmaf(c_b[sl][r], gsr[r + 1][k], a);
-        a = fmaf(g_b[sl][r], vcr[r][k], a);
+        a = __builtin_elementwise_fma(f2{c_b[sl][r], c_b[sl][r]}, f2{gsr[r + 1][2 * k], gsr[r + 1][2 * k + 1]}, a);
+        a = __builtin_elementwise_fma(f2{g_b[sl][r], g_b[sl][r]}, f2{vcr[r][2 * k], vcr[r][2 * k + 1]}, a);
       }
       gu[k] = a;
-      m = fmaxf(m, fabsf(a));
+      m = fmaxf(m, fmaxf(fabsf(a[0]), fabsf(a[1])));
     }
     gmax = fmaxf(gmax, m);
     float ma, mb;
     xpair32(m, ma, mb);
     const int eg = srf_split_exp(fmaxf(ma, mb));
     const float sg = srf_exp2i(eg);
+    // split by masking: hi = gu' with the low 13 mantissa bits cleared (exact in fp16),
+    // lo = f16(gu' - hi); packed conversions
     h8 bh[2], bl[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        _Float16 a1, a2;
-        srf_split2h(gu[8 * ks + k] * sg, a1, a2);
-        bh[ks][k] = a1;
-        bl[ks][k] = a2;
-      }
+    for (int k = 0; k < 8; ++k) {
+      const f2 a = gu[k] * sg;
+      const f2 hi = __builtin_bit_cast(f2, __builtin_bit_cast(u2, a) & 0xFFFFE000u);
+      const h2 ph = __builtin_convertvector(hi, h2), pl = __builtin_convertvector(a - hi, h2);
+      bh[k >> 2][2 * (k & 3)] = ph[0];
+      bh[k >> 2][2 * (k & 3) + 1] = ph[1];
+      bl[k >> 2][2 * (k & 3)] = pl[0];
+      bl[k >> 2][2 * (k & 3) + 1] = pl[1];
+    }
     f16v acc = {};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {

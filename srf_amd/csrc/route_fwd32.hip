@@ -635,6 +635,9 @@ struct Args32 {
 // registers capsule k-1 used, so no load waits on a queued MFMA's operand read.
 constexpr int kFTW = 2;   // row tiles per wave
 constexpr int kFFB = 2;   // frame tiles per wave
+#ifndef SRF_FIRST_XCD
+#define SRF_FIRST_XCD 1   // XCD-aware task order (0: row-group-fastest, A/B builds)
+#endif
 
 template <int DIN>
 struct FirstFrags {
@@ -645,11 +648,30 @@ struct FirstFrags {
 template <int DIN, int DOUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void route_fwd32_first_kernel(Args32 A) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+#if SRF_FIRST_XCD
+  // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs, so
+  // XCD x receives blocks x, x+8, ...; remap them to one contiguous range of tasks,
+  // ordered (i-chunk, frame pair, row group).  An XCD then works through one or two
+  // i-chunks (their W slice stays in its L2) and reads each frame pair's x slice once,
+  // where the row-group-fastest order had every XCD read all of x.
+  int blk = blockIdx.x;
+  {
+    const int nb = gridDim.x, q = nb >> 3, rem = nb & 7, x = blk & 7, idx = blk >> 3;
+    blk = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + idx;
+  }
+  const int task = blk * 4 + (threadIdx.x >> 6);
+  const int nfp = (A.F + 32 * kFFB - 1) / (32 * kFFB);
+  const int tg = task % A.n_tgroups;
+  const int rest = task / A.n_tgroups;
+  const int fp = rest % nfp, chunk = rest / nfp;
+  if (chunk >= A.n_chunks) return;
+#else
   const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int chunk = task % A.n_chunks;
   const int rest = task / A.n_chunks;
   const int tg = rest % A.n_tgroups, fp = rest / A.n_tgroups;
   if (fp * 32 * kFFB >= A.F) return;
+#endif
   const int tbase = tg * kFTW;
   const int JD = A.J * DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};

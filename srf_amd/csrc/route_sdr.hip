@@ -1262,6 +1262,7 @@ srf::SeqItems seq_items(const srf_sdr_range* r, int n, int T, bool bwd, bool kee
     I.rg = bwd ? srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, r[k].g0, r[k].gn, r[k].carry}
                : srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, 0, T, nullptr};
     I.u_bf16 = r[k].u_bf16;
+    I.group = r[k].group;
   }
   return it;
 }

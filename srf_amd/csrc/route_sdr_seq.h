@@ -38,6 +38,7 @@ struct SeqItem {
   float* ws;
   SeqRange rg;
   int u_bf16;
+  int group;        // streaming kernels: workgroups per utterance (0, 1: one; route_sdr_stream.hip)
 };
 struct SeqItems {
   SeqItem it[kMaxItems];
@@ -46,7 +47,7 @@ struct SeqItems {
 
 // True when sdr_seq_fwd/bwd handle (in_n, J, dout, iters): dout in {8,16,32},
 // J <= 64 (padded to a power of two JP, dout*JP <= 1024), in_n within the
-// per-lane register budget.  Disabled by SRF_SDR_SEQ=0 (A/B runs, legacy tests).
+// per-lane register budget.
 bool sdr_seq_supported(int in_n, int J, int dout, int iters);
 
 // u [B*T][in_n][J*dout] (pose output) -> v_out [B*T][J*dout]; one workgroup per utterance.
@@ -71,7 +72,8 @@ bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm);
 // 1024), in_n >= 8.  u_t is re-read from HBM once per iteration.  The forward
 // stores per frame c^r [iters][in_n][J] and s^r [iters][J*dout]
 // (sdr_stream_cs_floats, 256-B padded); the backward requires them and a scratch of
-// sdr_stream_workspace_floats (gL^r of every utterance).  Disabled by SRF_SDR_STREAM=0.
+// sdr_stream_workspace_floats (gL^r of every utterance, and the exchange area of
+// grouped launches: SeqItem::group > 1 workgroups per utterance).
 bool sdr_stream_supported(int in_n, int J, int dout, int iters);
 size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters);
 size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters);

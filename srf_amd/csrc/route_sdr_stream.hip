@@ -28,6 +28,7 @@
 //   gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j  (a pass without u: the lane's
 //   gs^r / Vc^r slices in registers, the 2R scalars of (i, j) per capsule).
 // HBM per frame: forward R reads of u_t; backward R reads of u_t + one write of gu_t.
+#include <algorithm>
 #include <cstdlib>
 
 #include "route_sdr_seq.h"
@@ -139,6 +140,88 @@ __device__ __forceinline__ float dot_slice(const float (&x)[KD], const float (&w
   return p0 + p1;
 }
 
+// ---- workgroup groups: G > 1 workgroups per utterance split its input capsules
+// (workgroup g of the group takes capsules (g * kNW + wave) + kNW * G * m) and add
+// their per-iteration partial sums through the item's workspace inside the launch.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1
+// table): every partial is stored write-through (sc1, 16 B), each storing wave drains
+// its stores, one lane per workgroup adds to the utterance's arrival counter (agent
+// scope), one lane polls it with sc1 loads, and every wave then reads the G partials
+// with sc1 loads only.  All G workgroups sum the partials in the same order, so they
+// hold bit-identical s / gVc and need no second exchange.  The G * B * items
+// workgroups must be resident together (one per CU): the host checks B * items * G
+// <= CUs, and the caller runs at most one grouped launch at a time.  Each spin is
+// bounded: past kSpinMax polls a workgroup sets the item's timeout word, stops
+// waiting (its results are then wrong, never a hang) and every later wait returns
+// at once.
+constexpr int kMaxGroup = 8;
+constexpr unsigned kSpinMax = 1u << 20;
+
+struct Grp {
+  int G;                // workgroups per utterance (1: no exchange)
+  int B;                // utterances of the launch
+  unsigned xoff, coff;  // floats from the item's workspace to the exchange area / the counters
+};
+
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+// floats of the item workspace: gL scratch (backward), counters [B] + timeout word
+// (256-B padded), exchange [2][B][kMaxGroup][JD]
+__host__ __device__ inline size_t gl_floats(int B, int in_n, int J, int R) { return (size_t)B * R * in_n * J; }
+__host__ __device__ inline size_t grp_coff(int B, int in_n, int J, int R) {
+  return (gl_floats(B, in_n, J, R) + 63) / 64 * 64;
+}
+__host__ __device__ inline size_t grp_xoff(int B, int in_n, int J, int R) {
+  return grp_coff(B, in_n, J, R) + ((size_t)B + 1 + 63) / 64 * 64;
+}
+__host__ __device__ inline size_t grp_floats(int B, int in_n, int J, int D, int R) {
+  return grp_xoff(B, in_n, J, R) + (size_t)2 * B * kMaxGroup * J * D;
+}
+
+// part [kNW][JD] (LDS, this workgroup's wave partials) -> part[0 .. JD) = the sum over
+// the whole group's capsules, for exchange phase `phase` (counted from 0 in the launch)
+template <int JD>
+__device__ __forceinline__ void group_allreduce(float* part, float* ws, const Grp& X, int b, int g,
+                                                unsigned phase, int tid) {
+  constexpr int NV = JD / 4;
+  float* xch = ws + X.xoff;
+  unsigned* cnt = reinterpret_cast<unsigned*>(ws + X.coff);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(xch, 0, (int)((size_t)2 * X.B * X.G * JD * 4), 0x00020000);
+  const uint32_t slot = (uint32_t)(((phase & 1) * X.B + b) * X.G) * JD * 4;
+  f4 mine = {0.f, 0.f, 0.f, 0.f};
+  if (tid < NV) {
+#pragma unroll
+    for (int w2 = 0; w2 < kNW; ++w2) mine += *reinterpret_cast<const f4*>(part + w2 * JD + 4 * tid);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, mine), rs, slot + (uint32_t)(g * JD + 4 * tid) * 4,
+                                           0, 16);   // aux 16: sc1 (write-through)
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its partial
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_fetch_add(cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned want = (unsigned)X.G * (phase + 1);
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      if (__hip_atomic_load(cnt + X.B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // gave up earlier
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kSpinMax) {
+        __hip_atomic_store(cnt + X.B, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < NV) {
+    f4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int g2 = 0; g2 < X.G; ++g2)
+      s += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, slot + (uint32_t)(g2 * JD + 4 * tid) * 4,
+                                                                        0, 16));   // sc1 loads only
+    *reinterpret_cast<f4*>(part + 4 * tid) = s;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ float squash_fac(float n2) {
   return n2 * __builtin_amdgcn_rcpf(1.f + n2) * __builtin_amdgcn_rsqf(n2 + kEps);
 }
@@ -157,9 +240,9 @@ __device__ __forceinline__ float dsquash(float s, float a) {
 
 // ------------------------------------------------------------------ forward
 // LDS: wl [JD] (Vc of the iteration), part [kNW][JD].
-template <int D, int KD, class TU>
+template <int D, int KD, class TU, bool GRP>
 __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items, int T, int in_n, int iters,
-                                                             int mask_first, int NMp) {
+                                                             int mask_first, int NMp, Grp X) {
   using C = SC<D, KD>;
   const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
   const TU* __restrict__ u = reinterpret_cast<const TU*>(I.u);
@@ -173,7 +256,10 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: capsule indices in SGPRs
   if (rg.t0 >= rg.t1) return;
-  const int b = blockIdx.x;
+  const int b = GRP ? blockIdx.x / X.G : blockIdx.x;
+  const int gm = GRP ? blockIdx.x - b * X.G : 0;   // member of the utterance's group
+  const int gw = gm * kNW + wv, cstep = GRP ? kNW * X.G : kNW;   // capsule i = gw + cstep * m
+  const bool lead = gm == 0;                                    // stores s^r and v
   const int j = lane / C::RQ;
   const bool q0 = (lane % C::RQ) == 0;
   const bool jm = !(mask_first && j == 0);
@@ -193,7 +279,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
   Cur lc{rg.t0, 0, 0};
   auto issue = [&](float(&x)[KD]) {
     const int tc = min(lc.t, rg.t1 - 1);
-    const int i = min(wv + kNW * lc.m, in_n - 1);
+    const int i = min(gw + cstep * lc.m, in_n - 1);
     load_slice<KD>(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD, x);
     lc.adv(NMp, iters, 1);
   };
@@ -211,7 +297,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
       for (int m0 = 0; m0 < NMp; m0 += PD) {
 #pragma unroll
         for (int p = 0; p < PD; ++p) {
-          const int i = wv + kNW * (m0 + p);
+          const int i = gw + cstep * (m0 + p);
           const bool iv = i < in_n;
           const float lg = group_sum<1, C::RQ>(dot_slice<KD>(xr[p], w));
           const float x = jm ? lg : -INFINITY;
@@ -229,16 +315,21 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
       for (int d = 0; d < KD; d += 4)
         *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{acc[d], acc[d + 1], acc[d + 2], acc[d + 3]};
       __syncthreads();
+      if constexpr (GRP) group_allreduce<JD>(part, I.ws, X, b, gm, (unsigned)((t - rg.t0) * iters + r), tid);
 #pragma unroll
       for (int n = 0; n < NE; ++n) {
         const int e = tid + n * kNT;
         float s = 0.f;
+        if constexpr (GRP) {
+          s = part[e];
+        } else {
 #pragma unroll
-        for (int w2 = 0; w2 < kNW; ++w2) s += part[w2 * JD + e];
+          for (int w2 = 0; w2 < kNW; ++w2) s += part[w2 * JD + e];
+        }
         const float v = s * squash_fac(group_sum<1, D>(s * s));
-        bstore(csf, s, (uint32_t)(iters * in_n * J + r * JD + e) * 4);
+        bstore(csf, s, lead ? (uint32_t)(iters * in_n * J + r * JD + e) * 4 : kDrop);
         if (r == iters - 1) {
-          vo[(size_t)t * JD + e] = v;
+          if (lead) vo[(size_t)t * JD + e] = v;
           vc[n] = v;   // v_t: Vc^0 of frame t + 1
         } else {
           vc[n] += v;
@@ -253,9 +344,9 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
 // ------------------------------------------------------------------ backward
 // LDS: part [kNW][JD], gsl [kRM][JD] (gs^r), vcl [kRM][JD] (Vc^r).
 // gls: per-utterance scratch gL^r [R][in_n][J].
-template <int D, int KD, class TU>
+template <int D, int KD, class TU, bool GRP>
 __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items, int T, int in_n, int iters,
-                                                             int NMp) {
+                                                             int NMp, Grp X) {
   using C = SC<D, KD>;
   const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
   const TU* __restrict__ u = reinterpret_cast<const TU*>(I.u);
@@ -273,7 +364,10 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: capsule indices in SGPRs
   if (rg.t0 >= rg.t1) return;
-  const int b = blockIdx.x;
+  const int b = GRP ? blockIdx.x / X.G : blockIdx.x;
+  const int gm = GRP ? blockIdx.x - b * X.G : 0;   // member of the utterance's group
+  const int gw = gm * kNW + wv, cstep = GRP ? kNW * X.G : kNW;   // capsule i = gw + cstep * m
+  const bool lead = gm == 0;                                    // writes the carry out
   const int R = iters;
   const int j = lane / C::RQ;
   const bool q0 = (lane % C::RQ) == 0;
@@ -296,7 +390,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
   Cur lc{rg.t1 - 1, 0, 0};
   auto issue = [&](float(&x)[KD], float& c) {
     const int tc = max(lc.t, rg.t0);
-    const int i = min(wv + kNW * lc.m, in_n - 1);
+    const int i = min(gw + cstep * lc.m, in_n - 1);
     load_slice<KD>(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD, x);
     c = csb[(size_t)tc * csr + (size_t)(R - 1 - lc.p) * PJ + (size_t)i * J + j];
     lc.adv(NMp, R, -1);
@@ -336,7 +430,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
       for (int m0 = 0; m0 < NMp; m0 += PD) {
 #pragma unroll
         for (int pp = 0; pp < PD; ++pp) {
-          const int i = wv + kNW * (m0 + pp);
+          const int i = gw + cstep * (m0 + pp);
           const bool iv = i < in_n;
           const float qd = group_sum<1, C::RQ>(dot_slice<KD>(xr[pp], g));
           const float c = iv ? cr[pp] : 0.f;
@@ -353,12 +447,17 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
       for (int d = 0; d < KD; d += 4)
         *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{gacc[d], gacc[d + 1], gacc[d + 2], gacc[d + 3]};
       __syncthreads();
+      if constexpr (GRP) group_allreduce<JD>(part, I.ws, X, b, gm, (unsigned)((rg.t1 - 1 - t) * R + p), tid);
 #pragma unroll
       for (int n = 0; n < NE; ++n) {
         const int e = tid + n * kNT;
         float gvc = 0.f;
+        if constexpr (GRP) {
+          gvc = part[e];
+        } else {
 #pragma unroll
-        for (int w2 = 0; w2 < kNW; ++w2) gvc += part[w2 * JD + e];
+          for (int w2 = 0; w2 < kNW; ++w2) gvc += part[w2 * JD + e];
+        }
         carry[n] += gvc;      // dL/dv_{t-1} = sum_r gVc^r
         gv[n] += gvc;         // dL/dv^{r-1} = sum_{r' >= r} gVc^{r'}
         if (r > 0) gsl[(r - 1) * JD + e] = dsquash<D>(sn[n], gv[n]);
@@ -383,7 +482,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
       // scalars of capsule i for the lane's j, one capsule ahead
       float sc[2][2 * kRM];
       auto fetch = [&](int m, float(&s)[2 * kRM]) {
-        const int i = min(wv + kNW * m, in_n - 1);
+        const int i = min(gw + cstep * m, in_n - 1);
 #pragma unroll
         for (int r = 0; r < kRM; ++r) {
           const int rr = min(r, R - 1);
@@ -397,7 +496,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
         for (int pp = 0; pp < 2; ++pp) {
           const int m = m0 + pp;
           fetch(m + 1, sc[pp ^ 1]);
-          const int i = wv + kNW * m;
+          const int i = gw + cstep * m;
           float o[HD];
 #pragma unroll
           for (int d = 0; d < HD; ++d) o[d] = 0.f;
@@ -418,7 +517,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
     }
     __syncthreads();   // gsl / vcl / the gL scratch are rewritten by frame t - 1
   }
-  if (carry_io)
+  if (carry_io && lead)
 #pragma unroll
     for (int n = 0; n < NE; ++n) carry_io[tid + n * kNT] = carry[n];
 }
@@ -426,24 +525,50 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
 // ------------------------------------------------------------------ host
 // capsule slots per wave and pass: a multiple of the ring depth PD (the ring's slots
 // are static registers) and of 2 (the gu pass walks slots in pairs)
-int nm_padded(int in_n, int pd) {
+int nm_padded(int in_n, int pd, int G) {
   const int step = pd % 2 ? 2 * pd : pd;
-  const int nm = (in_n + kNW - 1) / kNW;
+  const int nm = (in_n + kNW * G - 1) / (kNW * G);
   return (nm + step - 1) / step * step;
 }
 
 size_t fwd_lds(int JD) { return (size_t)(1 + kNW) * JD * sizeof(float); }
 size_t bwd_lds(int JD) { return (size_t)(kNW + 2 * kRM) * JD * sizeof(float); }
 
+// the launch's group size (items agree; 1 when ungrouped) and its exchange geometry;
+// grouped launches zero their items' arrival counters first (memset nodes under capture)
+static int group_setup(const srf::SeqItems& items, int B, int in_n, int J, int iters, Grp& X, hipStream_t st) {
+  const int G = std::max(1, items.it[0].group);
+  for (int k = 1; k < items.n; ++k)
+    SRF_REQUIRE(std::max(1, items.it[k].group) == G, "sdr_stream: launch items differ in group size");
+  SRF_REQUIRE(G <= kMaxGroup, "sdr_stream: group %d above %d", G, kMaxGroup);
+  X = Grp{G, B, (unsigned)grp_xoff(B, in_n, J, iters), (unsigned)grp_coff(B, in_n, J, iters)};
+  if (G == 1) return SRF_OK;
+  int dev = 0, cus = 0;
+  SRF_HIP_TRY(hipGetDevice(&dev));
+  SRF_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  SRF_REQUIRE((long)B * items.n * G <= cus,
+              "sdr_stream: %d utterances x %d ranges x group %d workgroups exceed the %d CUs they must share", B,
+              items.n, G, cus);
+  for (int k = 0; k < items.n; ++k) {
+    SRF_REQUIRE(items.it[k].ws, "sdr_stream: a grouped launch needs the range workspace");
+    SRF_HIP_TRY(hipMemsetAsync(items.it[k].ws + X.coff, 0, srf::align_up((size_t)(B + 1) * 4, 16), st));
+  }
+  return SRF_OK;
+}
+
 template <int D, int KD>
 int launch_fwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, int mask_first, hipStream_t st) {
   using C = SC<D, KD>;
   const size_t lds = fwd_lds(C::JD);
-  auto k = items.it[0].u_bf16 ? sdr_stream_fwd_kernel<D, KD, unsigned short> : sdr_stream_fwd_kernel<D, KD, float>;
+  Grp X;
+  if (int rc = group_setup(items, B, in_n, C::J, iters, X, st)) return rc;
+  const bool bf = items.it[0].u_bf16;
+  auto k = X.G > 1 ? (bf ? sdr_stream_fwd_kernel<D, KD, unsigned short, true> : sdr_stream_fwd_kernel<D, KD, float, true>)
+                   : (bf ? sdr_stream_fwd_kernel<D, KD, unsigned short, false> : sdr_stream_fwd_kernel<D, KD, float, false>);
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kNT), lds, st, items, T, in_n, iters, mask_first,
-                     nm_padded(in_n, C::PDF));
+  hipLaunchKernelGGL(k, dim3(B * X.G, items.n), dim3(kNT), lds, st, items, T, in_n, iters, mask_first,
+                     nm_padded(in_n, C::PDF, X.G), X);
   SRF_LAUNCH_CHECK("sdr_stream_fwd");
   return SRF_OK;
 }
@@ -452,10 +577,15 @@ template <int D, int KD>
 int launch_bwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, hipStream_t st) {
   using C = SC<D, KD>;
   const size_t lds = bwd_lds(C::JD);
-  auto k = items.it[0].u_bf16 ? sdr_stream_bwd_kernel<D, KD, unsigned short> : sdr_stream_bwd_kernel<D, KD, float>;
+  Grp X;
+  if (int rc = group_setup(items, B, in_n, C::J, iters, X, st)) return rc;
+  const bool bf = items.it[0].u_bf16;
+  auto k = X.G > 1 ? (bf ? sdr_stream_bwd_kernel<D, KD, unsigned short, true> : sdr_stream_bwd_kernel<D, KD, float, true>)
+                   : (bf ? sdr_stream_bwd_kernel<D, KD, unsigned short, false> : sdr_stream_bwd_kernel<D, KD, float, false>);
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kNT), lds, st, items, T, in_n, iters, nm_padded(in_n, C::PDB));
+  hipLaunchKernelGGL(k, dim3(B * X.G, items.n), dim3(kNT), lds, st, items, T, in_n, iters,
+                     nm_padded(in_n, C::PDB, X.G), X);
   SRF_LAUNCH_CHECK("sdr_stream_bwd");
   return SRF_OK;
 }
@@ -484,7 +614,7 @@ size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters) {
 }
 
 size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters) {
-  return sdr_stream_supported(in_n, J, dout, iters) ? (size_t)B * iters * in_n * J : 0;
+  return sdr_stream_supported(in_n, J, dout, iters) ? grp_floats(B, in_n, J, dout, iters) : 0;
 }
 
 // the items of one launch share the u element type

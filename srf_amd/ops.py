@@ -433,12 +433,15 @@ class SdrStackPlan:
     layers: [(N, din, J, dout, mask_first)] per layer."""
 
     def __init__(self, B, T, layers, lpad, rpad, iters, n_chunks=0, pose_fp8=False, u_bf16=True,
-                 store_couplings=True, store_u_bytes=None):
+                 store_couplings=True, store_u_bytes=None, last_group=None):
         """n_chunks: frame ranges per utterance (0: ~10 frames each); pose_fp8 / u_bf16: the
         opt-in e4m3 pose, and u kept in bf16 on its streamed layers; store_couplings:
         the forward keeps each frame's couplings for the backward (else recomputed where
         the layer's kernels can); store_u_bytes: budget for keeping every layer's u from
-        the forward (None: 55 % of the device's memory; 0: recompute per range)."""
+        the forward (None: 55 % of the device's memory; 0: recompute per range);
+        last_group: workgroups per utterance for the last layer's recurrence when it runs
+        on the streaming kernels (srf_sdr_range.group; None: as many as the CUs left
+        beside the inner layers' batched recurrences allow, at most 8)."""
         self.B, self.T, self.lpad, self.rpad, self.iters = B, T, lpad, rpad, iters
         self.pose_fp8 = bool(pose_fp8)
         self.store_couplings = bool(store_couplings)
@@ -473,6 +476,23 @@ class SdrStackPlan:
         self.ubf = [self.pose_fp8 and bool(u_bf16)
                     and bool(L_.srf_route_sdr_couplings_required(N * self.win, J, D, iters))
                     for (N, din, J, D, mf) in layers]
+        self.streamed = [bool(L_.srf_route_sdr_couplings_required(N * self.win, J, D, iters))
+                         for (N, din, J, D, mf) in layers]
+        self.last_group = last_group
+
+    def group(self, l, dev):
+        """srf_sdr_range.group of layer l's recurrence launches.  Only the last layer's
+        (stream B, one range per launch) are grouped: its B * G workgroups spin-wait on
+        each other, so they must be resident next to stream A's batched inner-layer
+        recurrence (B workgroups per streamed inner layer, one CU each) -- the one
+        grouped launch in flight at any time."""
+        if l != self.L - 1 or not self.streamed[l]:
+            return 1
+        if self.last_group is not None:
+            return max(1, int(self.last_group))
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        inner = self.B * sum(self.streamed[:self.L - 1])
+        return max(1, min(8, (cus - inner) // self.B))
 
     def pose_mode(self, l):
         """srf_route_sdr_pose_n mode: 0 fp32, 1 fp8, 2 fp8 with bf16 u."""
@@ -601,7 +621,8 @@ class SdrStack(torch.autograd.Function):
             v0, vn = (0, T) if (store or (pose_ahead and l == L - 1)) else (t0, P.nmax)
             return _sdr_r(t0=t0, t1=t1, emb=_ptr(embs[l]), W=_ptr(Ws[l]), bias=_ptr(bs[l]), u=_ptr(us[l]), v0=v0,
                           vn=vn, v=_ptr(vs[l]), couplings=_ptr(css[l]) if css[l] is not None else None,
-                          workspace=_ptr(rws[l]), workspace_bytes=rws[l].numel(), u_bf16=int(P.ubf[l]))
+                          workspace=_ptr(rws[l]), workspace_bytes=rws[l].numel(), u_bf16=int(P.ubf[l]),
+                          group=P.group(l, dev))
 
         def pose(sp, ls, ks):
             N, din, J, D, mf = P.layers[ls[0]]
@@ -716,7 +737,8 @@ class SdrStack(torch.autograd.Function):
                           couplings=_ptr(cs) if cs is not None else None, workspace=_ptr(rws[l]),
                           workspace_bytes=rws[l].numel(), g_v=_ptr(g_vs[l]), carry=_ptr(carries[l]),
                           gu=_ptr(gus[l]), g0=t0, gn=P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
-                          g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1), u_bf16=int(P.ubf[l]))
+                          g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1), u_bf16=int(P.ubf[l]),
+                          group=P.group(l, dev))
 
         def run(sp, ls, ks, ev=None, gw=True):
             """backward of ranges (ls[i], ks[i]) of same-shaped layers, batched: LN

@@ -242,3 +242,62 @@ def test_sdr_stream_bf16_u_equals_fp32(cuda, J, D, iters, mf):
         _lib.check(L.srf_route_sdr_pose_n((_lib.SdrRange * 1)(r), 1, B, T, N, din, lp, rp, J, D, mode, st), 'pose')
     torch.cuda.synchronize()
     assert torch.equal(uf.to(torch.bfloat16), ub)
+
+
+@pytest.mark.parametrize('J,D,iters,mf,N,lp,rp', [(16, 64, 5, False, 16, 20, 20), (32, 64, 3, True, 8, 4, 4),
+                                                   (16, 32, 2, False, 3, 1, 1)])
+def test_sdr_stream_groups_match_one_workgroup(cuda, J, D, iters, mf, N, lp, rp):
+    """srf_sdr_range.group > 1 splits each utterance's input capsules over G workgroups
+    that add their per-iteration partial sums inside the launch (route_sdr_stream.hip).
+    Forward v / couplings and backward gu / carry equal the one-workgroup launch up to
+    the reassociation of the partial sums, for groups of 2, 3 and 8 (8 x 8 waves > in_n
+    = 12 leaves members without capsules), over two frame ranges in one launch, and no
+    member gave up waiting (the timeout word stays 0)."""
+    import ctypes
+    from srf_amd import _lib
+    L = _lib.lib()
+    B, T = 3, 6
+    in_n, JD = N * (lp + rp + 1), J * D
+    rng = torch.Generator().manual_seed(7)
+    u = (torch.randn(B * T * in_n * JD, generator=rng) * 0.3).to(cuda)
+    g_v = torch.randn(B, T, JD, generator=rng).to(cuda)
+    ncs = L.srf_route_sdr_coupling_floats(in_n, J, D, iters)
+    ws_n = L.srf_route_sdr_recur_workspace(B, in_n, J, D, iters)
+    assert ncs > 0 and L.srf_route_sdr_couplings_required(in_n, J, D, iters)
+    coff = -(-B * iters * in_n * J // 64) * 64   # route_sdr_stream.hip grp_coff: counters, then the timeout word
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for G in (1, 2, 3, 8):
+        v = torch.zeros(B, T, JD, device=cuda)
+        cs = torch.zeros(B * T * ncs, device=cuda)
+        gu = torch.zeros(B * T * in_n * JD, device=cuda)
+        carry = torch.zeros(B, JD, device=cuda)
+        wss = [torch.zeros(ws_n // 4 + 4, device=cuda) for _ in range(2)]
+        cut = 2
+        rr = []
+        for k, (t0, t1) in enumerate(((0, cut), (cut, T))):
+            rr.append(_lib.SdrRange(t0=t0, t1=t1, u=p(u), v0=0, vn=T, v=p(v), couplings=p(cs), workspace=p(wss[k]),
+                                    workspace_bytes=ws_n, group=G, g_v=p(g_v), carry=p(carry), gu=p(gu), g0=0, gn=T))
+        # the forward's ranges in order (range 1 starts from range 0's v), the backward's in reverse
+        for k in (0, 1):
+            _lib.check(L.srf_route_sdr_recur_fwd_n((_lib.SdrRange * 1)(rr[k]), 1, B, T, in_n, J, D, iters, int(mf),
+                                                   st), 'fwd')
+        for k in (1, 0):
+            _lib.check(L.srf_route_sdr_recur_bwd_n((_lib.SdrRange * 1)(rr[k]), 1, B, T, in_n, J, D, iters, int(mf),
+                                                   st), 'bwd')
+        # and both ranges' forward in one two-item launch, each into a v buffer of its own
+        # (range 1 then starts from a zero v_{t0-1}): per-item counters, against G = 1
+        v2 = torch.zeros(2, B, T, JD, device=cuda)
+        r2 = [_lib.SdrRange(t0=t0, t1=t1, u=p(u), v0=0, vn=T, v=p(v2[k]), workspace=p(wss[k]), workspace_bytes=ws_n,
+                            group=G) for k, (t0, t1) in enumerate(((0, cut), (cut, T)))]
+        _lib.check(L.srf_route_sdr_recur_fwd_n((_lib.SdrRange * 2)(*r2), 2, B, T, in_n, J, D, iters, int(mf), st),
+                   'fwd2')
+        torch.cuda.synchronize()
+        if G > 1:
+            for w in wss:
+                assert w[coff + B].view(torch.int32).item() == 0, 'a group member timed out'
+        outs.append((G, v, cs, gu, carry, v2))
+    for G, *got in outs[1:]:
+        for name, a, b in zip(('v', 'cs', 'gu', 'carry', 'v2'), outs[0][1:], got):
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (G, name, (a - b).abs().max().item())
