@@ -30,6 +30,7 @@
 #include "srf_common.h"
 #include "srf_reduce.h"
 #include "route_sdr_seq.h"
+#include "srf_group.h"
 #include "../../include/srf.h"
 
 namespace {
@@ -1040,7 +1041,8 @@ srf::SeqItems one_seq_item(const srf::SeqItem& I) {
 }
 
 size_t recur_workspace(const SGeom& g) {
-  if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters)) return 0;
+  // register kernels: only the exchange area of grouped launches (srf_group.h)
+  if (srf::sdr_seq_supported(g.in_n(), g.J, g.dout, g.iters)) return srf_grp::floats(0, g.B, g.JD()) * sizeof(float);
   if (srf::sdr_stream_supported(g.in_n(), g.J, g.dout, g.iters))
     return srf::sdr_stream_workspace_floats(g.B, g.in_n(), g.J, g.dout, g.iters) * sizeof(float);
   return std::max(gstate_bytes(g, sdr_fwd_smem(g.in_n(), g.J, g.dout)),

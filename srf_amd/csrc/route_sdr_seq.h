@@ -64,8 +64,9 @@ int sdr_seq_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, 
                 hipStream_t st);
 
 // Template choice for a shape: per-lane input-capsule count NIM in {2, 5, 10} and
-// the iteration bound RM of the backward in {3, 5}.  False when unsupported.
-bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm);
+// the iteration bound RM of the backward in {3, 5}, for `group` workgroups per
+// utterance (SeqItem::group).  False when unsupported.
+bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm, int group = 1);
 
 // Streaming recurrence (route_sdr_stream.hip) for frames beyond the register budget
 // (BASELINE C5): dout in {32, 64} with J*dout in {512, 1024, 2048} (dout 32: 512,

@@ -19,10 +19,12 @@
 // swaps; ds_swizzle only for a lone xor 4).  Two barriers per iteration;
 // the next frame's u is loaded while the last reduction and squash of the
 // current frame run.  HBM traffic per frame: u_t once (in_n*J*D floats) + v_t.
+#include <algorithm>
 #include <cstdlib>
 
 #include "route_sdr_seq.h"
 #include "route_sdr_seq_dev.h"
+#include "srf_group.h"
 
 // Timing experiments (never in the shipped build): 1 = next frame's loads hit the
 // cache (wrong results), 2 = uniform couplings (no softmax reductions).
@@ -41,10 +43,11 @@ constexpr unsigned long long* g_stamps = nullptr;
 #endif
 
 // LDS: w [JD] (agreement input of the iteration: v_{t-1} at r = 0, then v^{r-1}),
-// part [16][JD].
-template <int D, int JP, int NIM>
+// part [16][JD].  GRP: X.G workgroups per utterance split its input capsules
+// (srf_group.h); member 0 stores v and s^r, every member its own capsules' c^r.
+template <int D, int JP, int NIM, bool GRP>
 __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems items, int T, int in_n, int J,
-                                                               int iters, int mask_first) {
+                                                               int iters, int mask_first, srf_grp::Grp X) {
   using C = Cfg<D, JP, NIM>;
   const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
   const float* __restrict__ u = I.u;
@@ -56,10 +59,13 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
   float* wl = lds;
   float* part = lds + ((JD + 3) & ~3);
   const int tid = threadIdx.x;
-  const Lane L = lane_map<C>(in_n, J, mask_first);
+  const int utt = GRP ? blockIdx.x / X.G : blockIdx.x;   // utterance
+  const int gm = GRP ? blockIdx.x - utt * X.G : 0;       // member of its group
+  const bool lead = gm == 0;
+  const Lane L = lane_map<C>(in_n, J, mask_first, gm, GRP ? X.G : 1);
   const size_t ff = (size_t)in_n * JD;
-  const float* ub = u + (size_t)blockIdx.x * rg.tu_n * ff;   // frame t at ub + (t - tu0) * ff
-  float* vo = v_out + (size_t)blockIdx.x * T * JD;
+  const float* ub = u + (size_t)utt * rg.tu_n * ff;   // frame t at ub + (t - tu0) * ff
+  float* vo = v_out + (size_t)utt * T * JD;
   const bool owner_wave = (tid >> 6) * 64 < JD;   // waves holding elements e = tid < JD
   const bool ev = tid < JD;
   const size_t csr = (size_t)iters * (in_n * JP + JD);   // coupling record per frame (cs != nullptr)
@@ -78,7 +84,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
       lds_slice<C::KD>(wl + L.eoff, L.jv, w);
       logits_softmax<C>(ur, w, L, b, c);
       row_partial<C>(c, ur, L, JD, part);
-      if (cs) store_ij<C>(c, L, cs + ((size_t)blockIdx.x * T + t) * csr + (size_t)r * in_n * JP);
+      if (cs) store_ij<C>(c, L, cs + ((size_t)utt * T + t) * csr + (size_t)r * in_n * JP);
 #if SRF_SEQ_DBG == 1   // timing experiment: re-load the current (cache-hot) frame
       if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(t - rg.tu0) * ff, JD, L, ur);
 #else
@@ -86,14 +92,17 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
 #endif
       SEQ_MARK(0);   // logits, softmax, row partials (+ next frame's loads issued)
       __syncthreads();
+      if constexpr (GRP) srf_grp::allreduce<kWaves, kThreads>(part, JD, I.ws, X, utt, gm, (t - rg.t0) * iters + r, tid);
       SEQ_MARK(1);
       if (owner_wave) {
-        const float s = ev ? sum_parts(part, JD, tid) : 0.f;
+        const float s = ev ? (GRP ? part[tid] : sum_parts(part, JD, tid)) : 0.f;
         const float v = squash_elem<D>(s);
         if (ev) {
           wl[tid] = v;
-          if (r == iters - 1) vo[(size_t)t * JD + tid] = v;
-          if (cs) cs[((size_t)blockIdx.x * T + t) * csr + (size_t)iters * in_n * JP + r * JD + tid] = s;
+          if (lead) {
+            if (r == iters - 1) vo[(size_t)t * JD + tid] = v;
+            if (cs) cs[((size_t)utt * T + t) * csr + (size_t)iters * in_n * JP + r * JD + tid] = s;
+          }
         }
       }
       SEQ_MARK(2);   // wave sums + squash (owner waves)
@@ -109,24 +118,24 @@ size_t fwd_lds(int J, int D) {
 }
 
 template <int D, int JP, int NIM>
-int launch_fwd(const srf::SeqItems& items, int B, int T, int in_n, int J, int iters, int mask_first,
-               hipStream_t st) {
+int launch_fwd(const srf::SeqItems& items, const srf_grp::Grp& X, int B, int T, int in_n, int J, int iters,
+               int mask_first, hipStream_t st) {
   const size_t lds = fwd_lds(J, D);
-  auto k = sdr_seq_fwd_kernel<D, JP, NIM>;
+  auto k = X.G > 1 ? sdr_seq_fwd_kernel<D, JP, NIM, true> : sdr_seq_fwd_kernel<D, JP, NIM, false>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kThreads), lds, st, items, T, in_n, J, iters, mask_first);
+  hipLaunchKernelGGL(k, dim3(B * X.G, items.n), dim3(kThreads), lds, st, items, T, in_n, J, iters, mask_first, X);
   SRF_LAUNCH_CHECK("sdr_seq_fwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
-int fwd_nim(int nim, const srf::SeqItems& items, int B, int T, int in_n, int J, int iters, int mask_first,
-            hipStream_t st) {
-  if (nim == 2) return launch_fwd<D, JP, 2>(items, B, T, in_n, J, iters, mask_first, st);
-  if (nim == 5) return launch_fwd<D, JP, 5>(items, B, T, in_n, J, iters, mask_first, st);
+int fwd_nim(int nim, const srf::SeqItems& items, const srf_grp::Grp& X, int B, int T, int in_n, int J, int iters,
+            int mask_first, hipStream_t st) {
+  if (nim == 2) return launch_fwd<D, JP, 2>(items, X, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 5) return launch_fwd<D, JP, 5>(items, X, B, T, in_n, J, iters, mask_first, st);
   if constexpr (seq_kd(D, JP) <= 8)
-    return launch_fwd<D, JP, 10>(items, B, T, in_n, J, iters, mask_first, st);
+    return launch_fwd<D, JP, 10>(items, X, B, T, in_n, J, iters, mask_first, st);
   srf::set_error("sdr_seq: no forward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -141,14 +150,15 @@ extern "C" int srf_seq_fwd_stamp_buffer(void* p) {
 
 namespace srf {
 
-bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm) {
+bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm, int group) {
   if (J < 2 || J > 64 || iters < 1 || iters > 5 || in_n < 1) return false;
   if (dout != 8 && dout != 16 && dout != 32) return false;
   const int JP = srf_seq::pow2_at_least(J);
   if (dout * JP > 1024) return false;
   const int KD = srf_seq::seq_kd(dout, JP);
   const int G = srf_seq::seq_slots(dout, JP);
-  const int NI = (in_n + G - 1) / G;
+  const int ng = std::max(1, group), blk = (in_n + ng - 1) / ng;   // a group member's block (lane_map)
+  const int NI = (blk + G - 1) / G;
   const int m = NI <= 2 ? 2 : NI <= 5 ? 5 : (NI <= 10 && KD <= 8) ? 10 : 0;
   if (m == 0) return false;
   const int r = iters <= 3 ? 3 : 5;
@@ -170,13 +180,15 @@ size_t sdr_seq_cs_floats(int in_n, int J, int dout, int iters) {
 int sdr_seq_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
                 hipStream_t st) {
   int nim = 0, rm = 0;
-  if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
+  srf_grp::Grp X;
+  if (int rc = srf_grp::setup(items, B, 0, X, st)) return rc;
+  if (!sdr_seq_plan(in_n, J, dout, iters, nullptr, nullptr) || !sdr_seq_plan(in_n, J, dout, iters, &nim, &rm, X.G)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
     return SRF_EUNSUPPORTED;
   }
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_F(DD, PP) \
-  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, items, B, T, in_n, J, iters, mask_first, st);
+  if (dout == DD && JP == PP) return fwd_nim<DD, PP>(nim, items, X, B, T, in_n, J, iters, mask_first, st);
   SRF_SEQ_CASES(SRF_SEQ_F)
 #undef SRF_SEQ_F
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

@@ -18,6 +18,7 @@
 
 #include "route_sdr_seq.h"
 #include "route_sdr_seq_dev.h"
+#include "srf_group.h"
 
 namespace {
 
@@ -42,9 +43,11 @@ constexpr bool cl_wanted(int nim, int kd) { return nim * kd >= 40; }
 // others from L2 where the adjoint uses them (once per iteration), and the gu pass
 // accumulates GR rows at a time per LDS read of gs^r / Vc^r: the J = 32 last layer
 // otherwise needs more than the 128 registers a 1024-thread workgroup allows.
-template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, int GR = NIM>
+// GRP (with CS): X.G workgroups per utterance split its input capsules (srf_group.h)
+// and add their gVc^r partials inside the launch; member 0 writes the carry out.
+template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, int GR = NIM, bool GRP = false>
 __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems items, int T, int in_n, int J,
-                                                               int iters, int mask_first) {
+                                                               int iters, int mask_first, srf_grp::Grp X) {
   using C = Cfg<D, JP, NIM>;
   const srf::SeqItem& I = items.it[blockIdx.y];   // the frame range of this launch item
   const float* __restrict__ u = I.u;
@@ -65,15 +68,18 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
   float* cl = part + kWaves * JD;          // [RM][in_n][JP] (CL only)
   float* gll = cl + RM * in_n * JP;        // [RM][in_n][JP] (CL only)
   const int tid = threadIdx.x;
-  const Lane L = lane_map<C>(in_n, J, mask_first);
+  static_assert(CS || !GRP, "grouped backward reads the stored couplings");
+  const int utt = GRP ? blockIdx.x / X.G : blockIdx.x;   // utterance
+  const int gm = GRP ? blockIdx.x - utt * X.G : 0;       // member of its group
+  const Lane L = lane_map<C>(in_n, J, mask_first, gm, GRP ? X.G : 1);
   const size_t ff = (size_t)in_n * JD;
-  const size_t f0 = (size_t)blockIdx.x * T;
-  const float* ub = u + (size_t)blockIdx.x * rg.tu_n * ff;    // frame t at ub + (t - tu0) * ff
-  float* gub = gu + (size_t)blockIdx.x * rg.tg_n * ff;        // frame t at gub + (t - tg0) * ff
+  const size_t f0 = (size_t)utt * T;
+  const float* ub = u + (size_t)utt * rg.tu_n * ff;    // frame t at ub + (t - tu0) * ff
+  float* gub = gu + (size_t)utt * rg.tg_n * ff;        // frame t at gub + (t - tg0) * ff
   const bool owner_wave = (tid >> 6) * 64 < JD;
   const bool ev = tid < JD;
   if (rg.t0 >= rg.t1) return;
-  float* carry_io = rg.carry ? rg.carry + (size_t)blockIdx.x * JD : nullptr;
+  float* carry_io = rg.carry ? rg.carry + (size_t)utt * JD : nullptr;
   // dL/dv_t carried back from frame t+1 (owner threads), from the later range
   float carry = (carry_io && ev) ? carry_io[tid] : 0.f;
   constexpr int KRES = CS ? KR : C::NIM;   // rows of u held in registers
@@ -249,9 +255,11 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
         }
         SEQ_MARK(3);     // q, sigma, gL, gVc partials (+ re-read rows)
         __syncthreads();
+        if constexpr (GRP)
+          srf_grp::allreduce<kWaves, kThreads>(part, JD, I.ws, X, utt, gm, (rg.t1 - 1 - t) * R + (R - 1 - r), tid);
         SEQ_MARK(4);
         if (ev) {
-          const float g = sum_parts(part, JD, tid);   // gVc^r_e
+          const float g = GRP ? part[tid] : sum_parts(part, JD, tid);   // gVc^r_e
           carry += g;
           grun = (r == R - 1) ? g : grun + g;
           a = grun;
@@ -346,7 +354,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
     SEQ_MARK(7);
   }
   SEQ_FLUSH(g_stamps);
-  if (carry_io && ev) carry_io[tid] = carry;   // dL/dv_{t0-1} for the earlier range
+  if (carry_io && ev && gm == 0) carry_io[tid] = carry;   // dL/dv_{t0-1} for the earlier range
 }
 
 size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
@@ -357,8 +365,8 @@ size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
 }
 
 template <int D, int JP, int NIM, int RM>
-int launch_bwd(const srf::SeqItems& items, bool cs, int B, int T, int in_n, int J, int iters, int mask_first,
-               hipStream_t st) {
+int launch_bwd(const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, int B, int T, int in_n, int J, int iters,
+               int mask_first, hipStream_t st) {
   constexpr bool want = cl_wanted(NIM, seq_kd(D, JP));
   const bool cl = want && bwd_lds(J, D, RM, in_n, true) <= 160 * 1024;
   const size_t lds = bwd_lds(J, D, RM, in_n, cl);
@@ -367,25 +375,28 @@ int launch_bwd(const srf::SeqItems& items, bool cs, int B, int T, int in_n, int 
   constexpr int KD = seq_kd(D, JP);
   constexpr int KR = NIM * KD > 48 ? 32 / KD : NIM;
   constexpr int GR = 1;
-  auto k = cs ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, GR>
-                    : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, GR>)
-              : (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, false>
-                    : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, false>);
+  SRF_REQUIRE(cs || X.G == 1, "sdr_seq: a grouped backward needs the forward's stored couplings");
+  auto k = X.G > 1 ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, GR, true>
+                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, GR, true>)
+           : cs    ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, GR>
+                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, GR>)
+                   : (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, false>
+                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, false>);
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kThreads), lds, st, items, T, in_n, J, iters, mask_first);
+  hipLaunchKernelGGL(k, dim3(B * X.G, items.n), dim3(kThreads), lds, st, items, T, in_n, J, iters, mask_first, X);
   SRF_LAUNCH_CHECK("sdr_seq_bwd");
   return SRF_OK;
 }
 
 template <int D, int JP>
-int bwd_nim(int nim, int rm, const srf::SeqItems& items, bool cs, int B, int T, int in_n, int J, int iters,
-            int mask_first, hipStream_t st) {
-  if (rm == 5) return launch_bwd<D, JP, 2, 5>(items, cs, B, T, in_n, J, iters, mask_first, st);
-  if (nim == 2) return launch_bwd<D, JP, 2, 3>(items, cs, B, T, in_n, J, iters, mask_first, st);
-  if (nim == 5) return launch_bwd<D, JP, 5, 3>(items, cs, B, T, in_n, J, iters, mask_first, st);
+int bwd_nim(int nim, int rm, const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, int B, int T, int in_n,
+            int J, int iters, int mask_first, hipStream_t st) {
+  if (rm == 5) return launch_bwd<D, JP, 2, 5>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 2) return launch_bwd<D, JP, 2, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 5) return launch_bwd<D, JP, 5, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
   if constexpr (seq_kd(D, JP) <= 8)
-    return launch_bwd<D, JP, 10, 3>(items, cs, B, T, in_n, J, iters, mask_first, st);
+    return launch_bwd<D, JP, 10, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
   srf::set_error("sdr_seq: no backward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -407,14 +418,16 @@ int sdr_seq_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, 
   for (int k = 1; k < items.n; ++k)
     SRF_REQUIRE((items.it[k].cs != nullptr) == cs, "sdr_seq: launch items mix stored and recomputed couplings");
   int nim = 0, rm = 0;
-  if (!sdr_seq_plan(in_n, J, dout, iters, &nim, &rm)) {
+  srf_grp::Grp X;
+  if (int rc = srf_grp::setup(items, B, 0, X, st)) return rc;
+  if (!sdr_seq_plan(in_n, J, dout, iters, nullptr, nullptr) || !sdr_seq_plan(in_n, J, dout, iters, &nim, &rm, X.G)) {
     srf::set_error("sdr_seq: unsupported shape in_n=%d J=%d dout=%d iters=%d", in_n, J, dout, iters);
     return SRF_EUNSUPPORTED;
   }
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_B(DD, PP)     \
   if (dout == DD && JP == PP) \
-    return bwd_nim<DD, PP>(nim, rm, items, cs, B, T, in_n, J, iters, mask_first, st);
+    return bwd_nim<DD, PP>(nim, rm, items, X, cs, B, T, in_n, J, iters, mask_first, st);
   SRF_SEQ_CASES(SRF_SEQ_B)
 #undef SRF_SEQ_B
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

@@ -122,15 +122,21 @@ struct Lane {
   bool q0;      // first of the Q lanes of its capsule
 };
 
+// gm / ng: this workgroup's member index and the group size (srf_group.h): member gm
+// takes the block of ceil(in_n / ng) input capsules starting at gm * ceil(in_n / ng),
+// its row slots stepping through the block by G (a compile-time stride)
 template <class C>
-__device__ __forceinline__ Lane lane_map(int in_n, int J, int mask_first) {
+__device__ __forceinline__ Lane lane_map(int in_n, int J, int mask_first, int gm = 0, int ng = 1) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int sub = lane / C::ROWL, rl = lane % C::ROWL;
+  const int blk = (in_n + ng - 1) / ng, base = gm * blk;
+  const int nloc = max(0, min(in_n, base + blk) - base);
+  const int gl = wv * C::SUB + sub;
   Lane L;
   L.j = rl / C::Q;
-  L.g = wv * C::SUB + sub;
+  L.g = base + gl;
   L.eoff = L.j * C::D + (rl % C::Q) * C::KD;
-  L.NI = L.g < in_n ? (in_n - L.g + C::G - 1) / C::G : 0;
+  L.NI = gl < nloc ? (nloc - gl + C::G - 1) / C::G : 0;
   L.jv = L.j < J;
   L.jm = L.jv && !(mask_first && L.j == 0);
   L.q0 = (rl % C::Q) == 0;

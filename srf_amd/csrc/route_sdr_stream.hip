@@ -33,6 +33,7 @@
 
 #include "route_sdr_seq.h"
 #include "route_sdr_seq_dev.h"
+#include "srf_group.h"
 
 namespace {
 
@@ -140,87 +141,12 @@ __device__ __forceinline__ float dot_slice(const float (&x)[KD], const float (&w
   return p0 + p1;
 }
 
-// ---- workgroup groups: G > 1 workgroups per utterance split its input capsules
-// (workgroup g of the group takes capsules (g * kNW + wave) + kNW * G * m) and add
-// their per-iteration partial sums through the item's workspace inside the launch.
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1
-// table): every partial is stored write-through (sc1, 16 B), each storing wave drains
-// its stores, one lane per workgroup adds to the utterance's arrival counter (agent
-// scope), one lane polls it with sc1 loads, and every wave then reads the G partials
-// with sc1 loads only.  All G workgroups sum the partials in the same order, so they
-// hold bit-identical s / gVc and need no second exchange.  The G * B * items
-// workgroups must be resident together (one per CU): the host checks B * items * G
-// <= CUs, and the caller runs at most one grouped launch at a time.  Each spin is
-// bounded: past kSpinMax polls a workgroup sets the item's timeout word, stops
-// waiting (its results are then wrong, never a hang) and every later wait returns
-// at once.
-constexpr int kMaxGroup = 8;
-constexpr unsigned kSpinMax = 1u << 20;
-
-struct Grp {
-  int G;                // workgroups per utterance (1: no exchange)
-  int B;                // utterances of the launch
-  unsigned xoff, coff;  // floats from the item's workspace to the exchange area / the counters
-};
-
-typedef unsigned u4 __attribute__((ext_vector_type(4)));
-
-// floats of the item workspace: gL scratch (backward), counters [B] + timeout word
-// (256-B padded), exchange [2][B][kMaxGroup][JD]
+// Workgroup groups (srf_group.h): G > 1 workgroups per utterance take capsules
+// (member * kNW + wave) + kNW * G * m and add their partial sums inside the launch.
+using srf_grp::Grp;
+using srf_grp::kMaxGroup;
+// floats of the stream backward's gL scratch [B][R][in_n][J] at the item workspace's start
 __host__ __device__ inline size_t gl_floats(int B, int in_n, int J, int R) { return (size_t)B * R * in_n * J; }
-__host__ __device__ inline size_t grp_coff(int B, int in_n, int J, int R) {
-  return (gl_floats(B, in_n, J, R) + 63) / 64 * 64;
-}
-__host__ __device__ inline size_t grp_xoff(int B, int in_n, int J, int R) {
-  return grp_coff(B, in_n, J, R) + ((size_t)B + 1 + 63) / 64 * 64;
-}
-__host__ __device__ inline size_t grp_floats(int B, int in_n, int J, int D, int R) {
-  return grp_xoff(B, in_n, J, R) + (size_t)2 * B * kMaxGroup * J * D;
-}
-
-// part [kNW][JD] (LDS, this workgroup's wave partials) -> part[0 .. JD) = the sum over
-// the whole group's capsules, for exchange phase `phase` (counted from 0 in the launch)
-template <int JD>
-__device__ __forceinline__ void group_allreduce(float* part, float* ws, const Grp& X, int b, int g,
-                                                unsigned phase, int tid) {
-  constexpr int NV = JD / 4;
-  float* xch = ws + X.xoff;
-  unsigned* cnt = reinterpret_cast<unsigned*>(ws + X.coff);
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(xch, 0, (int)((size_t)2 * X.B * X.G * JD * 4), 0x00020000);
-  const uint32_t slot = (uint32_t)(((phase & 1) * X.B + b) * X.G) * JD * 4;
-  f4 mine = {0.f, 0.f, 0.f, 0.f};
-  if (tid < NV) {
-#pragma unroll
-    for (int w2 = 0; w2 < kNW; ++w2) mine += *reinterpret_cast<const f4*>(part + w2 * JD + 4 * tid);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, mine), rs, slot + (uint32_t)(g * JD + 4 * tid) * 4,
-                                           0, 16);   // aux 16: sc1 (write-through)
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its partial
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_fetch_add(cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned want = (unsigned)X.G * (phase + 1);
-    unsigned spins = 0;
-    while (__hip_atomic_load(cnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      if (__hip_atomic_load(cnt + X.B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;   // gave up earlier
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > kSpinMax) {
-        __hip_atomic_store(cnt + X.B, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid < NV) {
-    f4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int g2 = 0; g2 < X.G; ++g2)
-      s += __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, slot + (uint32_t)(g2 * JD + 4 * tid) * 4,
-                                                                        0, 16));   // sc1 loads only
-    *reinterpret_cast<f4*>(part + 4 * tid) = s;
-  }
-  __syncthreads();
-}
 
 __device__ __forceinline__ float squash_fac(float n2) {
   return n2 * __builtin_amdgcn_rcpf(1.f + n2) * __builtin_amdgcn_rsqf(n2 + kEps);
@@ -315,7 +241,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
       for (int d = 0; d < KD; d += 4)
         *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{acc[d], acc[d + 1], acc[d + 2], acc[d + 3]};
       __syncthreads();
-      if constexpr (GRP) group_allreduce<JD>(part, I.ws, X, b, gm, (unsigned)((t - rg.t0) * iters + r), tid);
+      if constexpr (GRP) srf_grp::allreduce<kNW, kNT>(part, JD, I.ws, X, b, gm, (unsigned)((t - rg.t0) * iters + r), tid);
 #pragma unroll
       for (int n = 0; n < NE; ++n) {
         const int e = tid + n * kNT;
@@ -447,7 +373,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
       for (int d = 0; d < KD; d += 4)
         *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{gacc[d], gacc[d + 1], gacc[d + 2], gacc[d + 3]};
       __syncthreads();
-      if constexpr (GRP) group_allreduce<JD>(part, I.ws, X, b, gm, (unsigned)((rg.t1 - 1 - t) * R + p), tid);
+      if constexpr (GRP) srf_grp::allreduce<kNW, kNT>(part, JD, I.ws, X, b, gm, (unsigned)((rg.t1 - 1 - t) * R + p), tid);
 #pragma unroll
       for (int n = 0; n < NE; ++n) {
         const int e = tid + n * kNT;
@@ -534,34 +460,12 @@ int nm_padded(int in_n, int pd, int G) {
 size_t fwd_lds(int JD) { return (size_t)(1 + kNW) * JD * sizeof(float); }
 size_t bwd_lds(int JD) { return (size_t)(kNW + 2 * kRM) * JD * sizeof(float); }
 
-// the launch's group size (items agree; 1 when ungrouped) and its exchange geometry;
-// grouped launches zero their items' arrival counters first (memset nodes under capture)
-static int group_setup(const srf::SeqItems& items, int B, int in_n, int J, int iters, Grp& X, hipStream_t st) {
-  const int G = std::max(1, items.it[0].group);
-  for (int k = 1; k < items.n; ++k)
-    SRF_REQUIRE(std::max(1, items.it[k].group) == G, "sdr_stream: launch items differ in group size");
-  SRF_REQUIRE(G <= kMaxGroup, "sdr_stream: group %d above %d", G, kMaxGroup);
-  X = Grp{G, B, (unsigned)grp_xoff(B, in_n, J, iters), (unsigned)grp_coff(B, in_n, J, iters)};
-  if (G == 1) return SRF_OK;
-  int dev = 0, cus = 0;
-  SRF_HIP_TRY(hipGetDevice(&dev));
-  SRF_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  SRF_REQUIRE((long)B * items.n * G <= cus,
-              "sdr_stream: %d utterances x %d ranges x group %d workgroups exceed the %d CUs they must share", B,
-              items.n, G, cus);
-  for (int k = 0; k < items.n; ++k) {
-    SRF_REQUIRE(items.it[k].ws, "sdr_stream: a grouped launch needs the range workspace");
-    SRF_HIP_TRY(hipMemsetAsync(items.it[k].ws + X.coff, 0, srf::align_up((size_t)(B + 1) * 4, 16), st));
-  }
-  return SRF_OK;
-}
-
 template <int D, int KD>
 int launch_fwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, int mask_first, hipStream_t st) {
   using C = SC<D, KD>;
   const size_t lds = fwd_lds(C::JD);
   Grp X;
-  if (int rc = group_setup(items, B, in_n, C::J, iters, X, st)) return rc;
+  if (int rc = srf_grp::setup(items, B, gl_floats(B, in_n, C::J, iters), X, st)) return rc;
   const bool bf = items.it[0].u_bf16;
   auto k = X.G > 1 ? (bf ? sdr_stream_fwd_kernel<D, KD, unsigned short, true> : sdr_stream_fwd_kernel<D, KD, float, true>)
                    : (bf ? sdr_stream_fwd_kernel<D, KD, unsigned short, false> : sdr_stream_fwd_kernel<D, KD, float, false>);
@@ -578,7 +482,7 @@ int launch_bwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, hi
   using C = SC<D, KD>;
   const size_t lds = bwd_lds(C::JD);
   Grp X;
-  if (int rc = group_setup(items, B, in_n, C::J, iters, X, st)) return rc;
+  if (int rc = srf_grp::setup(items, B, gl_floats(B, in_n, C::J, iters), X, st)) return rc;
   const bool bf = items.it[0].u_bf16;
   auto k = X.G > 1 ? (bf ? sdr_stream_bwd_kernel<D, KD, unsigned short, true> : sdr_stream_bwd_kernel<D, KD, float, true>)
                    : (bf ? sdr_stream_bwd_kernel<D, KD, unsigned short, false> : sdr_stream_bwd_kernel<D, KD, float, false>);
@@ -614,7 +518,7 @@ size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters) {
 }
 
 size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters) {
-  return sdr_stream_supported(in_n, J, dout, iters) ? grp_floats(B, in_n, J, dout, iters) : 0;
+  return sdr_stream_supported(in_n, J, dout, iters) ? srf_grp::floats(gl_floats(B, in_n, J, iters), B, J * dout) : 0;
 }
 
 // the items of one launch share the u element type

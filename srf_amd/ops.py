@@ -439,9 +439,9 @@ class SdrStackPlan:
         the forward keeps each frame's couplings for the backward (else recomputed where
         the layer's kernels can); store_u_bytes: budget for keeping every layer's u from
         the forward (None: 55 % of the device's memory; 0: recompute per range);
-        last_group: workgroups per utterance for the last layer's recurrence when it runs
-        on the streaming kernels (srf_sdr_range.group; None: as many as the CUs left
-        beside the inner layers' batched recurrences allow, at most 8)."""
+        last_group: workgroups per utterance for the last layer's recurrence
+        (srf_sdr_range.group; None: as many as the CUs left beside the inner layers'
+        batched recurrences allow, at most 8; 1: one)."""
         self.B, self.T, self.lpad, self.rpad, self.iters = B, T, lpad, rpad, iters
         self.pose_fp8 = bool(pose_fp8)
         self.store_couplings = bool(store_couplings)
@@ -482,17 +482,17 @@ class SdrStackPlan:
 
     def group(self, l, dev):
         """srf_sdr_range.group of layer l's recurrence launches.  Only the last layer's
-        (stream B, one range per launch) are grouped: its B * G workgroups spin-wait on
-        each other, so they must be resident next to stream A's batched inner-layer
-        recurrence (B workgroups per streamed inner layer, one CU each) -- the one
-        grouped launch in flight at any time."""
-        if l != self.L - 1 or not self.streamed[l]:
+        (stream B, one range per launch: the critical chain of the stack) are grouped:
+        its B * G workgroups spin-wait on each other, so they must be resident next to
+        stream A's batched inner-layer recurrence (B workgroups per inner layer, one CU
+        each) -- the one grouped launch in flight at any time.  The register kernels'
+        grouped backward reads the stored couplings."""
+        if l != self.L - 1 or not (self.streamed[l] or self.store_couplings):
             return 1
         if self.last_group is not None:
             return max(1, int(self.last_group))
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        inner = self.B * sum(self.streamed[:self.L - 1])
-        return max(1, min(8, (cus - inner) // self.B))
+        return max(1, min(8, (cus - self.B * (self.L - 1)) // self.B))
 
     def pose_mode(self, l):
         """srf_route_sdr_pose_n mode: 0 fp32, 1 fp8, 2 fp8 with bf16 u."""

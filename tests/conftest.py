@@ -18,3 +18,18 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip('no HIP device')
     return torch.device('cuda:0')
+
+
+@pytest.fixture(autouse=True)
+def _fresh_dropout_seed_source():
+    """Each test starts without the process-wide dropout step counter
+    (srf_set_seed_source): a training-step test attaches one, and the kernel tests
+    that restate dropout masks (tests/torch_ref.py) assume the per-call seeds alone."""
+    yield
+    from srf_amd import trainer_sr
+    if trainer_sr._SEED_COUNTERS:
+        import torch
+        from srf_amd import _lib
+        torch.cuda.synchronize()
+        _lib.check(_lib.lib().srf_set_seed_source(None), 'srf_set_seed_source')
+        trainer_sr._SEED_COUNTERS.clear()
