@@ -1,6 +1,6 @@
 """Times the SDR layer's frame-parallel contractions (srf_route_sdr_pose / _gx / _gw)
-on one frame range of the C3 / C5 stack, alone on the GPU, with the 32x32-tile MFMA
-kernels (default) and the 16x16 ones (SRF_SDR_MFMA32=0).
+on one frame range of the C3 / C5 stack, alone on the GPU (the kernel family the
+library picks per din; A/B other families with SRF_LIB_PATH=ab/x.so builds).
     python scripts/bench_sdr_gemm.py [--shapes c3,c5] [--reps 20]"""
 import argparse
 import ctypes
@@ -49,8 +49,7 @@ def main():
             'gw': lambda: L.srf_route_sdr_gw(p(u), t0, nt, p(emb), B, T, N, din, lp, rp, J, D, t0, t1, 1, p(gW),
                                              p(gb), st),
         }
-        for mf in ('1', '0', ''):
-            os.environ['SRF_SDR_MFMA32'] = mf   # '' = the library's per-kernel default
+        for lib_path in (_lib.LIB_PATH,):
             res = {}
             for k, fn in calls.items():
                 _lib.check(fn(), k)
@@ -63,7 +62,7 @@ def main():
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.reps
                 res[k] = {'us': round(us, 1), 'tflops': round(flop / us / 1e6, 1)}
-            print(json.dumps({'shape': name, 'mfma32': mf, 'gflop': round(flop / 1e9, 2), **res}), flush=True)
+            print(json.dumps({'shape': name, 'lib': lib_path, 'gflop': round(flop / 1e9, 2), **res}), flush=True)
 
 
 if __name__ == '__main__':

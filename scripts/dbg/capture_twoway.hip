@@ -29,7 +29,10 @@ constexpr int kN = 1 << 16;
 static void launch(float* p, float v, hipStream_t s) { hipLaunchKernelGGL(add_k, dim3(kN / 256), dim3(256), 0, s, p, v, kN); }
 
 // case: 0 fork/join once, 1 two-way (A -> B, then B -> A), 2 fork twice, 3 fork from a second thread,
-// 4 two-way with both edges on events recorded before either wait (A <-> B crossing)
+// 4 two-way with both edges on events recorded before either wait (A <-> B crossing),
+// 5 the SdrStack pattern in global mode: fork/join A, B from the capturing thread, then
+//   fork/join the SAME A, B again from a second thread (torch's autograd thread runs the
+//   backward of a captured step), 6 as 5 with the second thread ordering A and B both ways
 static int run_case(int c, float* buf, float* out) {
   hipStream_t O, A, B;
   CK(hipStreamCreateWithFlags(&O, hipStreamNonBlocking));
@@ -41,6 +44,32 @@ static int run_case(int c, float* buf, float* out) {
   CK(hipStreamSynchronize(O));
   float *a = buf, *b = buf + kN, *o = buf + 2 * kN;
   CK(hipStreamBeginCapture(O, c == 3 ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeGlobal));
+  hipError_t terr = hipSuccess;
+  auto other_thread = [&](bool twoway) {
+    std::thread th([&] {
+      auto ck = [&](hipError_t e) { if (e != hipSuccess && terr == hipSuccess) terr = e; };
+      ck(hipEventRecord(ev[6], O));
+      ck(hipStreamWaitEvent(A, ev[6], 0));
+      ck(hipStreamWaitEvent(B, ev[6], 0));
+      launch(a, 6.f, A);
+      launch(b, 7.f, B);
+      if (twoway) {
+        ck(hipEventRecord(ev[2], A));
+        ck(hipStreamWaitEvent(B, ev[2], 0));
+        launch(b, 8.f, B);
+        ck(hipEventRecord(ev[3], B));
+        ck(hipStreamWaitEvent(A, ev[3], 0));
+        launch(a, 9.f, A);
+      }
+      ck(hipEventRecord(ev[4], A));
+      ck(hipEventRecord(ev[5], B));
+      ck(hipStreamWaitEvent(O, ev[4], 0));
+      ck(hipStreamWaitEvent(O, ev[5], 0));
+    });
+    th.join();
+    if (terr != hipSuccess) printf("  second thread: %d (%s)\n", (int)terr, hipGetErrorString(terr));
+    return (int)terr;
+  };
   auto fork = [&](int e0) -> int {
     CK(hipEventRecord(ev[e0], O));
     CK(hipStreamWaitEvent(A, ev[e0], 0));
@@ -90,6 +119,10 @@ static int run_case(int c, float* buf, float* out) {
       launch(b, 4.f, B);
     }
     if ((rc = join(4))) return rc;
+    if (c == 5 || c == 6) {   // the same side streams forked again, from another thread
+      launch(o, 2.f, O);
+      if ((rc = other_thread(c == 6))) return rc;
+    }
     if (c == 2) {   // the same side streams forked again
       if ((rc = fork(6))) return rc;
       launch(a, 6.f, A);
@@ -119,9 +152,10 @@ int main() {
   float* buf;
   if (hipMalloc(&buf, 3 * kN * sizeof(float)) != hipSuccess) return 1;
   static float out[3 * kN];
-  const char* names[] = {"fork_join", "two_way", "fork_twice", "second_thread", "two_way_crossed"};
+  const char* names[] = {"fork_join",       "two_way",           "fork_twice",          "second_thread",
+                         "two_way_crossed", "refork_other_thread", "refork_other_twoway"};
   int bad = 0;
-  for (int c = 0; c < 5; ++c) {
+  for (int c = 0; c < 7; ++c) {
     printf("case %s\n", names[c]);
     const int rc = run_case(c, buf, out);
     printf("case %s rc=%d\n", names[c], rc);

@@ -1,5 +1,5 @@
 # Issue/wait breakdown (SQ counters, one --pmc pass each) of one bench workload, plus
-# an env A/B of the same workload.  TAG=name WL=wsj_c4 AB="SRF_WEIGHT_STREAM=1" [PENV="A=1 B=2"] bash scripts/gpu_pmc_sq2.sh
+# an env A/B of the same workload.  TAG=name WL=wsj_c4 AB="SRF_LIB_PATH=ab/x.so" [PENV="A=1 B=2"] bash scripts/gpu_pmc_sq2.sh
 # (PENV: environment of the profiled runs)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
