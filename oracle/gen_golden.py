@@ -210,6 +210,9 @@ def _c5_bf16_layers(sh):
             for (in_n, J, D, din) in sh.layer_shapes()]
 
 
+REFINIT_PERTURB = 4
+
+
 def gen_refinit(only=()):
     for name, (kw, lens, tlens, seed) in REFINIT_CASES.items():
         if only and name not in only:
@@ -230,18 +233,37 @@ def gen_refinit(only=()):
         pe32 = nm.ctc_per_utt(l32, torch.tensor(labels), torch.tensor(inp_len), torch.tensor(tar_len), sh.class_n)
         (pe32.sum() / len(lens)).backward()
         g32 = {k.replace('__', '.'): p.grad.double().numpy() for k, p in m.p.items()}
+        # the spread of fp32 implementations: the same fp32 mirror on inputs whose last
+        # mantissa bit is flipped at random (REFINIT_PERTURB runs)
+        lp, np_, gp = [], [], []
+        prng = np.random.default_rng(seed + 500)
+        f32 = feats[:, :T].astype(np.float32)
+        for _ in range(REFINIT_PERTURB):
+            flip = prng.random(f32.shape) < 0.5
+            fp = np.where(flip, np.nextafter(f32, np.where(prng.random(f32.shape) < 0.5, np.inf, -np.inf)
+                                             .astype(np.float32)), f32).astype(np.float32)
+            mk = nm.NaiveMirror(sh, P, dtype=torch.float32, tile=False)
+            lk = mk(torch.tensor(fp), torch.tensor(inp_len))
+            pk = nm.ctc_per_utt(lk, torch.tensor(labels), torch.tensor(inp_len), torch.tensor(tar_len), sh.class_n)
+            (pk.sum() / len(lens)).backward()
+            lp.append(lk.detach().numpy())
+            np_.append(pk.detach().double().numpy())
+            gp.append({k.replace('__', '.'): q.grad.double().numpy() for k, q in mk.p.items()})
         out = {'shape_json': np.array(json.dumps(kw)), 'feats_seed': np.array(seed),
                'feats_sum': np.array([feats.sum(), np.square(feats).sum()]), 'inp_len': inp_len, 'labels': labels,
                'tar_len': tar_len, 'logits': logits.astype(np.float32), 'nll': nll, 'seed': np.array(seed),
-               'logits_m32': l32.detach().numpy(), 'nll_m32': pe32.detach().double().numpy()}
+               'logits_m32': l32.detach().numpy(), 'nll_m32': pe32.detach().double().numpy(),
+               'logits_m32p': np.stack(lp), 'nll_m32p': np.stack(np_)}
         out.update({'psum.' + k: np.array([v.sum(), np.square(v).sum()]) for k, v in P.items()})
         _sampled(out, g64, seed)
         for k, g in g32.items():
             out['gval32.' + k] = g.reshape(-1)[out['gidx.' + k]].astype(np.float32)
             out['gstat32.' + k] = np.array([np.abs(g).max(), np.sqrt(np.square(g).sum())])
+            out['gval32p.' + k] = np.stack([gk[k].reshape(-1)[out['gidx.' + k]] for gk in gp]).astype(np.float32)
         np.savez_compressed(os.path.join(GOLD, f'model_{name}.npz'), **out)
         print(name, 'oracle vs fp32 mirror: logits', np.abs(l32.detach().numpy() - logits).max(),
-              'nll', np.abs(pe32.detach().numpy() - nll).max())
+              'nll', np.abs(pe32.detach().numpy() - nll).max(), 'perturbed runs:',
+              [float(np.abs(x - logits).max()) for x in lp])
 
 
 def gen_fp8(only=()):

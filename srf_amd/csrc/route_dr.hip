@@ -2280,6 +2280,14 @@ int fwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   for (int r = 0; r < g.iters; ++r) {
     const float* vc = r > 0 ? saved + (size_t)(2 * (r - 1) + 1) * FJD : nullptr;
     if (r < nev) SRF_HIP_TRY(hipEventRecord(ev0[r], st));
+    if (p32 && r == 0 && srf::fwd32_first_full_supported(plan, g.din, g.dout)) {
+      // iteration 0 with its finish fused: s^0, Vc^1 (and v for one iteration) directly
+      const int rc = srf::fwd32_first_full(plan, planes, scratch, g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout,
+                                           g.mask_first, saved, saved + FJD, g.iters == 1 ? v_out : nullptr, st);
+      if (rc) return rc;
+      if (r < nev) SRF_HIP_TRY(hipEventRecord(ev1[r], st));
+      continue;
+    }
     if (p32) {
       float *cst = nullptr, *lzst = nullptr;
       if (couplings != nullptr && r > 0) {

@@ -54,6 +54,12 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
 int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T,
                int N, int din, int lpad, int rpad, int J, int dout, int mask_first, const float* vc, float* cst,
                float* lzst, hipStream_t st);
+// iteration 0 over all input capsules with the finish fused: writes s^0 (s_out),
+// Vc^1 = v^0 (vc_out) and, for one-iteration layers, v (v_out); din = dout = 32
+bool fwd32_first_full_supported(const Fwd32Plan& p, int din, int dout);
+int fwd32_first_full(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int mask_first, float* s_out, float* vc_out, float* v_out,
+                     hipStream_t st);
 // Coupling storage of one training forward (float offsets): c^r [iters-1][in_n][JP][Fs],
 // logZ^r [iters-1][in_n][Fs], the operand planes, WT, xT; JP = JDp / dout,
 // Fs = fwd32_frame_stride(F).

@@ -638,6 +638,9 @@ constexpr int kFFB = 2;   // frame tiles per wave
 #ifndef SRF_FIRST_XCD
 #define SRF_FIRST_XCD 1   // XCD-aware task order (0: row-group-fastest, A/B builds)
 #endif
+#ifndef SRF_FWD32_FULL0
+#define SRF_FWD32_FULL0 1   // din 32: iteration 0 over all capsules with the finish fused (0: chunked, A/B builds)
+#endif
 
 template <int DIN>
 struct FirstFrags {
@@ -738,6 +741,157 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
         }
       }
     }
+}
+
+// Iteration-0 pass over ALL input capsules, din = dout = 32 (the C3/C4 DR layers):
+// s^0 = c0 (sum_i W_i x_i + sum_i b_i) and its squash in the epilogue, so this pass
+// writes s^0 and Vc^1 = v^0 itself: no i-chunk slabs, no finish launch.
+// Workgroup = 128 rows x 64 frames, 4 waves (2 row halves x 2 frame tiles; a wave
+// owns 2 row tiles x 1 frame tile).  The split-fp16 operands of one capsule (W: 128
+// rows, x: 64 frames, hi and lo planes, 64 B per row and plane) are staged global ->
+// LDS by global_load_lds (16 B per lane, no registers, no ds_write) into two buffers,
+// one capsule ahead.  LDS image per plane: [rows][4 slots of 16 B], chunk c of row r
+// in slot 4r + (c ^ ((r >> 2) & 3)): the fragment reads (ds_read_b128, rows 0-31 of a
+// tile, one chunk) then hit 16 distinct slots per lane group; the DMA writes slots
+// lane-linearly, so each lane fetches the chunk its slot holds.  XCD-aware block
+// order: the row tiles of a frame tile run on one XCD (x read once per XCD).
+constexpr int kFfBM = 128, kFfBN = 64;
+constexpr int kFfA = 2 * kFfBM * 64;   // A bytes per stage (two planes)
+constexpr int kFfB = 2 * kFfBN * 64;   // B bytes per stage
+constexpr int kFfStage = kFfA + kFfB;  // 24 KiB; two stages
+
+__device__ __forceinline__ uint32_t ff_slot(int r, int c) { return (uint32_t)(4 * r + (c ^ ((r >> 2) & 3))); }
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void route_fwd32_first_full_kernel(
+    Args32 A, float* __restrict__ s_out, float* __restrict__ vc_out, float* __restrict__ v_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int n_rt = A.JDp / kFfBM;
+  int blk = blockIdx.x;
+  {
+    const int nb = gridDim.x, q = nb >> 3, rem = nb & 7, x = blk & 7, idx = blk >> 3;
+    blk = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + idx;
+  }
+  const int rt = blk % n_rt, ft = blk / n_rt;
+  const int row0 = rt * kFfBM, f0 = ft * kFfBN;
+  const int wr = wv >> 1, wc = wv & 1;   // row half, frame tile of this wave
+  const char* Wb = static_cast<const char*>(A.Ws);
+  const char* Xb = static_cast<const char*>(A.xs);
+  const size_t capb = (size_t)A.JDp * 64;   // bytes of one capsule's W rows per plane
+  // DMA roles: wave wv fills A pieces 4wv..4wv+3 and B pieces 2wv, 2wv+1 (1 KiB each)
+  // A piece q: plane q >> 3, slots (q & 7) * 64 + lane -> row = slot >> 2
+  uint32_t a_src[4];   // byte offset of this lane's A chunk (capsule 0, plane 0 base added later)
+  uint32_t a_pl[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int q = 4 * wv + k;
+    const int slot = (q & 7) * 64 + lane, r = slot >> 2, c = (slot & 3) ^ ((r >> 2) & 3);
+    a_src[k] = (uint32_t)((row0 + r) * 64 + c * 16);
+    a_pl[k] = (uint32_t)(q >> 3);
+  }
+  int b_frame[2], b_c[2], b_pl[2], b_tt[2];
+  bool b_ok[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = 2 * wv + k;
+    const int slot = (q & 3) * 64 + lane, r = slot >> 2;
+    b_c[k] = (slot & 3) ^ ((r >> 2) & 3);
+    b_pl[k] = q >> 2;
+    b_frame[k] = f0 + r;
+    b_ok[k] = b_frame[k] < A.F;
+    const int fc = min(b_frame[k], A.F - 1);
+    b_tt[k] = fc - (fc / A.T) * A.T;
+  }
+  auto stage = [&](int i, int buf) {
+    char* dst = smem + buf * kFfStage;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = 4 * wv + k;
+      glds16(Wb + (size_t)a_pl[k] * A.wplane_b + (size_t)i * capb + a_src[k], dst + q * 1024);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = 2 * wv + k;
+      const uint32_t xo = x_voff<32>(i, A.N, A.lpad, A.T, A.F, b_frame[k], b_tt[k], b_ok[k], 0, A.zero_off);
+      glds16(Xb + (size_t)b_pl[k] * A.xplane_b + xo + b_c[k] * 16, dst + kFfA + q * 1024);
+    }
+  };
+  // fragment reads: A rows wr*64 + t*32 + r32, B frames wc*32 + r32, chunk 2s + h
+  auto afrag = [&](const char* base, int t, int plane, int sstep) -> h8 {
+    const int r = wr * 64 + t * 32 + r32;
+    return *reinterpret_cast<const h8*>(base + plane * (kFfBM * 64) + ff_slot(r, 2 * sstep + h) * 16);
+  };
+  auto bfrag = [&](const char* base, int plane, int sstep) -> h8 {
+    const int r = wc * 32 + r32;
+    return *reinterpret_cast<const h8*>(base + kFfA + plane * (kFfBN * 64) + ff_slot(r, 2 * sstep + h) * 16);
+  };
+  f16v acc[2] = {f16v{}, f16v{}};
+  const int n_in = A.in_n;
+  stage(0, 0);
+  for (int i = 0; i < n_in; ++i) {
+    const int buf = i & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of capsule i has landed
+    __syncthreads();                                    // ... and every wave's; buf ^ 1 no longer read
+    if (i + 1 < n_in) stage(i + 1, buf ^ 1);
+    const char* base = smem + buf * kFfStage;
+    h8 b[4];
+    b[0] = bfrag(base, 0, 0);   // x hi, k-step 0
+    b[1] = bfrag(base, 1, 0);   // x lo
+    b[2] = bfrag(base, 0, 1);
+    b[3] = bfrag(base, 1, 1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      h8 a[4];
+      a[0] = afrag(base, t, 0, 0);   // W hi, k-step 0
+      a[1] = afrag(base, t, 1, 0);   // W lo
+      a[2] = afrag(base, t, 0, 1);
+      a[3] = afrag(base, t, 1, 1);
+      acc[t] = pose_chain<32>(a, b, acc[t]);
+    }
+  }
+  // epilogue: s = c0 (2^-(aw+bx) acc + sum_i b_i), v = squash over the capsule's 32 rows
+  // (16 in this lane, 16 in lane ^ 32), Vc^1 = v
+  const int f = f0 + wc * 32 + r32;
+  const bool fv = f < A.F;
+  const int JD = A.J * 32;
+  const int Jeff = A.J - (A.mask_first ? 1 : 0);
+  const float inv = A.hdr[0];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int rbase = row0 + wr * 64 + t * 32;   // one output capsule j = rbase / 32
+    const int j = rbase / 32;
+    const float c0 = (j < A.J && !(A.mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
+    f4 sv[4];
+    float n2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = rbase + 8 * q + 4 * h;
+      f4 bs = {0.f, 0.f, 0.f, 0.f};
+      if (row < JD)
+        for (int ch = 0; ch < A.n_chunks; ++ch) bs += *reinterpret_cast<const f4*>(A.bsum + (size_t)ch * JD + row);
+      const f4 u = {acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]};
+      sv[q] = (u * inv + bs) * c0;
+      n2 += (sv[q].x * sv[q].x + sv[q].y * sv[q].y) + (sv[q].z * sv[q].z + sv[q].w * sv[q].w);
+    }
+    n2 = xor32_sum(n2);
+    const float fac = n2 / (1.f + n2) / sqrtf(n2 + 1e-7f);   // squash (naive:247-252)
+    if (fv && rbase < JD) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const size_t o = (size_t)f * JD + rbase + 8 * q + 4 * h;
+        *reinterpret_cast<f4*>(s_out + o) = sv[q];
+        const f4 v = sv[q] * fac;
+        *reinterpret_cast<f4*>(vc_out + o) = v;
+        if (v_out) *reinterpret_cast<f4*>(v_out + o) = v;
+      }
+    }
+  }
 }
 
 // Routing pass r >= 1.  grid: n_ftiles * n_chunks (chunk = blockIdx % n_chunks);
@@ -1818,6 +1972,24 @@ Fwd32Cpl fwd32_cpl_layout(const Fwd32Plan& p, int F, int in_n, int din, int dout
   off += ((size_t)in_n * din * ((F + 15) / 16 * 16) + 63) / 64 * 64;
   c.total = off;
   return c;
+}
+
+// Iteration-0 pass with its finish fused (route_fwd32_first_full_kernel): din = dout = 32.
+bool fwd32_first_full_supported(const Fwd32Plan& p, int din, int dout) {
+  return SRF_FWD32_FULL0 && din == 32 && dout == 32 && p.JDp % kFfBM == 0;
+}
+
+int fwd32_first_full(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din, int lpad,
+                     int rpad, int J, int dout, int mask_first, float* s_out, float* vc_out, float* v_out,
+                     hipStream_t st) {
+  SRF_REQUIRE(fwd32_first_full_supported(p, din, dout), "fwd32_first_full: din %d dout %d JDp %d", din, dout, p.JDp);
+  SRF_REQUIRE(2 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
+  const Args32 a = make_args32(p, planes, scratch, B, T, N, din, lpad, rpad, J, dout, mask_first);
+  const int nb = (p.JDp / kFfBM) * ((B * T + kFfBN - 1) / kFfBN);
+  const size_t lds = 2 * kFfStage;
+  hipLaunchKernelGGL(route_fwd32_first_full_kernel, dim3(nb), dim3(256), lds, st, a, s_out, vc_out, v_out);
+  SRF_LAUNCH_CHECK("route_fwd32_first_full");
+  return SRF_OK;
 }
 
 int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch, int B, int T,

@@ -485,12 +485,17 @@ class SdrStackPlan:
         (stream B, one range per launch: the critical chain of the stack) are grouped:
         its B * G workgroups spin-wait on each other, so they must be resident next to
         stream A's batched inner-layer recurrence (B workgroups per inner layer, one CU
-        each) -- the one grouped launch in flight at any time.  The register kernels'
-        grouped backward reads the stored couplings."""
+        each) -- the one grouped launch in flight at any time.  By default only a
+        streamed last layer is grouped (C5: 955 -> 800 ms per step at G = 2); the
+        register kernels' groups (C3, explicit last_group; their backward reads the
+        stored couplings) measured slower, 24.0 -> 24.4 / 25.0 ms at G = 2 / 4: their
+        per-iteration exchange costs more than the shorter per-member recurrence saves."""
         if l != self.L - 1 or not (self.streamed[l] or self.store_couplings):
             return 1
         if self.last_group is not None:
             return max(1, int(self.last_group))
+        if not self.streamed[l]:
+            return 1
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         return max(1, min(8, (cus - self.B * (self.L - 1)) // self.B))
 

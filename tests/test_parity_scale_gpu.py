@@ -86,33 +86,39 @@ def _fwd_bwd(model, sh, z, dev):
 
 def test_c3_reference_init_within_fp32_chaos(cuda):
     """C3 at W ~ N(0, 0.1), where each SDR layer amplifies fp32 rounding ~10^4-fold
-    (DESIGN §2), so no fp32 implementation tracks the float64 oracle o64 row by row:
-    two fp32 orderings diverge from it along different paths.  The bound is therefore
-    per utterance, against the float32 torch mirror m32 of the same graph (CPU):
-        max over its rows |gpu - o64| <= 4 max over its rows |m32 - o64| + 1e-4 (1 + max|o64|),
-    and, so that the GPU does not merely stay inside a loose envelope, its median row
-    error is at most 4x the mirror's.  NLL per utterance likewise; gradients per
-    parameter over the stored samples: max|gpu - g64| <= 4 max|g32 - g64| + 2e-3
-    max|g64| + 1e-5."""
+    (DESIGN §2): no fp32 implementation tracks the float64 oracle o64 row by row, and
+    two fp32 runs that differ in one input bit already end up 0.13-0.69 apart.  The
+    fixture therefore holds an envelope of fp32 runs: the float32 torch mirror on the
+    exact inputs and on REFINIT_PERTURB copies with random last-bit flips
+    (oracle/gen_golden.py).  Per utterance, the GPU must stay inside 1.5x the widest of
+    them plus the fixed-init bound,
+        max |gpu - o64| <= 1.5 max_k max |m32_k - o64| + 1e-4 (1 + max |o64|),
+    its median row error within 2x the runs' median, the NLL likewise per utterance,
+    and every sampled gradient entry set within 1.5x the runs' widest deviation from
+    the float64 gradient + 2e-3 max|g64| + 1e-5."""
     model, sh, z = _model('c3_refinit', cuda)
     got, nll = _fwd_bwd(model, sh, z, cuda)
-    ref, m32 = z['logits'].astype(np.float64), z['logits_m32'].astype(np.float64)
-    e_gpu = np.abs(got - ref).max(-1)   # [B, T'] per row
-    e_m32 = np.abs(m32 - ref).max(-1)
-    lim = 4 * e_m32.max(-1) + 1e-4 * (1 + np.abs(ref).max((-2, -1)))
-    assert np.all(e_gpu.max(-1) <= lim), (e_gpu.max(-1), e_m32.max(-1))
-    assert np.median(e_gpu) <= 4 * np.median(e_m32) + 1e-5, (np.median(e_gpu), np.median(e_m32))
-    assert np.all(np.abs(nll - z['nll']) <= 4 * np.abs(z['nll_m32'] - z['nll']) + 1e-4 * np.maximum(1, np.abs(z['nll'])))
+    ref = z['logits'].astype(np.float64)
+    runs = np.concatenate([z['logits_m32'][None], z['logits_m32p']]).astype(np.float64)   # [K, B, T', C]
+    e_gpu = np.abs(got - ref).max(-1)                 # [B, T'] per row
+    e_run = np.abs(runs - ref[None]).max(-1)          # [K, B, T']
+    lim = 1.5 * e_run.max((0, 2)) + 1e-4 * (1 + np.abs(ref).max((-2, -1)))
+    assert np.all(e_gpu.max(-1) <= lim), (e_gpu.max(-1), e_run.max((0, 2)))
+    assert np.median(e_gpu) <= 2 * np.median(e_run) + 1e-5, (np.median(e_gpu), np.median(e_run))
+    nruns = np.concatenate([z['nll_m32'][None], z['nll_m32p']]).astype(np.float64)
+    nlim = 1.5 * np.abs(nruns - z['nll'][None]).max(0) + 1e-4 * np.maximum(1, np.abs(z['nll']))
+    assert np.all(np.abs(nll - z['nll']) <= nlim), (nll, z['nll'], nlim)
     bad = []
     for key in z:
         if not key.startswith('gidx.'):
             continue
         name = key[5:]
         g = model.P(name.replace('.', '_')).grad.detach().cpu().double().numpy().reshape(-1)[z[key]]
-        g64, g32 = z['gval.' + name].astype(np.float64), z['gval32.' + name].astype(np.float64)
-        err, err32 = np.abs(g - g64).max(), np.abs(g32 - g64).max()
-        if err > 4 * err32 + 2e-3 * z['gstat.' + name][0] + 1e-5:
-            bad.append((name, err, err32))
+        g64 = z['gval.' + name].astype(np.float64)
+        gr = np.concatenate([z['gval32.' + name][None], z['gval32p.' + name]]).astype(np.float64)
+        err, err_run = np.abs(g - g64).max(), np.abs(gr - g64[None]).max()
+        if err > 1.5 * err_run + 2e-3 * z['gstat.' + name][0] + 1e-5:
+            bad.append((name, err, err_run))
     assert not bad, bad
 
 
@@ -128,9 +134,13 @@ def test_c5_fp8_pose_end_to_end(cuda):
       * per utterance, max |gpu - o64| <= 1.5 max |emul - o64| + 1e-3 (1 + max|o64|)
         (logits), the same for the NLL, and per parameter over the stored gradient
         samples max |g_gpu - g64| <= 1.5 max |g_emul - g64| + 2e-3 max|g64| + 1e-5;
-      * the GPU is the emulated quantisation, not just as far off: its median logit
-        distance from the emulation is under a tenth of the emulation's median
-        distance from o64."""
+      * and typically as far off as the emulation: median |gpu - o64| <= 1.5 median
+        |emul - o64|.
+    Element by element the two need not agree: a quantisation flip is itself a 2^-4
+    perturbation that flips further operands downstream (the fp8 network is
+    discontinuous), so that the pose kernel IS the emulated quantisation is checked
+    where inputs are identical, layer by layer: tests/test_route_sdr_gpu.py
+    test_sdr_pose_fp8_matches_emulation."""
     model, sh, z = _model('c5_real_fp8', cuda, model_pose_fp8=True)
     assert model.pose_fp8
     plan = model._stack_plan(1, -(-int(z['inp_len'].max()) // 4))
@@ -142,8 +152,8 @@ def test_c5_fp8_pose_end_to_end(cuda):
     ax = tuple(range(1, got.ndim))
     lim = 1.5 * np.abs(emul - o64).max(ax) + 1e-3 * (1 + np.abs(o64).max(ax))
     assert np.all(np.abs(got - o64).max(ax) <= lim), (np.abs(got - o64).max(ax), lim)
-    assert np.median(np.abs(got - emul)) <= 0.1 * np.median(np.abs(emul - o64)), \
-        (np.median(np.abs(got - emul)), np.median(np.abs(emul - o64)))
+    assert np.median(np.abs(got - o64)) <= 1.5 * np.median(np.abs(emul - o64)), \
+        (np.median(np.abs(got - o64)), np.median(np.abs(emul - o64)))
     nlim = 1.5 * np.abs(z['nll'] - z64['nll']) + 1e-3 * np.maximum(1, np.abs(z64['nll']))
     assert np.all(np.abs(nll - z64['nll']) <= nlim), (nll, z['nll'], z64['nll'])
     bad = []

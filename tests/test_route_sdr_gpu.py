@@ -192,6 +192,50 @@ def test_sdr_pose_fp8_bound(cuda, din, J, D):
     assert np.median(rel) < 0.02, np.median(rel)
 
 
+@pytest.mark.parametrize('din,J,D', [(64, 16, 64), (32, 16, 32)])
+def test_sdr_pose_fp8_matches_emulation(cuda, din, J, D):
+    """The fp8 pose kernel (pose_n mode 1: fp32 u; mode 2: bf16 u) computes exactly the
+    quantisation oracle/srf_oracle.pose_fp8 restates (per-vector power-of-two scales,
+    e4m3 round to nearest even, exact products, fp32 bias, bf16 rounding of u): on
+    identical fp32 inputs the two differ only by the order of the fp32 accumulation,
+    |gpu - emul| <= 1e-6 sum_k |W_q||x_q| (+ one bf16 ulp of u in mode 2), with
+    operands spanning 2^-20 .. 2^4 and zero frames."""
+    import ctypes
+    from srf_amd import _lib
+    L = _lib.lib()
+    B, T, N, lp, rp = 2, 7, 3, 1, 2
+    in_n, JD = N * (lp + rp + 1), J * D
+    rng = np.random.default_rng(31)
+    emb = (rng.standard_normal((B, T, N, din)) * 2.0 ** rng.uniform(-20, 4, (B, T, N, 1))).astype(np.float32)
+    emb[0, 3] = 0.0
+    W = (rng.standard_normal((in_n, JD, din)) * 0.1 * 2.0 ** rng.uniform(-20, 4, (in_n, JD, 1))).astype(np.float32)
+    bias = (rng.standard_normal((in_n, JD)) * 0.1).astype(np.float32)
+    x = so.window(emb.astype(np.float64), lp, rp)                                   # [B, T, in_n, din]
+    Wr = W.astype(np.float64).reshape(in_n, J, D, din)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    te, tW, tb = (torch.tensor(a, device=cuda) for a in (emb, W, bias))
+    ex = so.e4m3_scale_exp(np.abs(x).max(-1))
+    ew = so.e4m3_scale_exp(np.abs(Wr).max(-1))
+    xq = so.e4m3_round(x * np.exp2(ex)[..., None]) * np.exp2(-ex)[..., None]
+    wq = so.e4m3_round(Wr * np.exp2(ew)[..., None]) * np.exp2(-ew)[..., None]
+    mag = np.einsum('ijdk,btik->btijd', np.abs(wq), np.abs(xq)).reshape(B, T, in_n, JD)
+    for mode in (1, 2):
+        ref = so.pose_fp8(x, Wr, bias.astype(np.float64).reshape(in_n, J, D), bf16_u=(mode == 2))
+        ref = ref.reshape(B, T, in_n, JD)
+        if mode == 1:
+            u = torch.full((B * T * in_n * JD,), float('nan'), device=cuda)
+        else:
+            u = torch.zeros(B * T * in_n * JD, device=cuda, dtype=torch.bfloat16)
+        r = _lib.SdrRange(t0=0, t1=T, emb=p(te), W=p(tW), bias=p(tb), u=p(u), v0=0, vn=T, u_bf16=int(mode == 2))
+        _lib.check(L.srf_route_sdr_pose_n((_lib.SdrRange * 1)(r), 1, B, T, N, din, lp, rp, J, D, mode, st), 'pose')
+        torch.cuda.synchronize()
+        got = u.float().cpu().double().numpy().reshape(B, T, in_n, JD)
+        tol = 1e-6 * mag + 1e-7 * np.abs(ref) + (2.0 ** -8 * np.abs(ref) if mode == 2 else 0.0)
+        err = np.abs(got - ref)
+        assert np.all(err <= tol), (mode, (err - tol).max(), np.argwhere(err > tol)[:4].tolist())
+
+
 @pytest.mark.parametrize('J,D,iters,mf', [(16, 64, 5, False), (32, 64, 3, True)])
 def test_sdr_stream_bf16_u_equals_fp32(cuda, J, D, iters, mf):
     """The streaming recurrence reading u stored in bf16 (the fp8 C5 variant) computes
