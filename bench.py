@@ -195,7 +195,7 @@ def _timed(step, steps, world, dev):
     return elapsed
 
 
-def sdr_roofline(model, tms):
+def sdr_roofline(model, tms, group=1):
     """HBM roofline of the SDR recurrence (the last layer's forward launches, one
     workgroup per utterance walking its frames; sequence_router_naive.py:162-170).
     Algorithmic bytes per frame: the frame's u_t read once per routing iteration by
@@ -215,7 +215,8 @@ def sdr_roofline(model, tms):
     gbs = per_frame * frames / (ms * 1e-3) / 1e9
     return {'kernel': ('sdr_stream_fwd_kernel<%d,%d>' % (D, J * D // 64) if stream else
                        'sdr_seq_fwd_kernel<%d,%d,...>' % (D, J)) +
-            ' (layer %d SDR recurrence, forward, one workgroup per utterance)' % model.enc_num,
+            ' (layer %d SDR recurrence, forward, %s per utterance)' % (
+                model.enc_num, 'one workgroup' if group <= 1 else '%d workgroups' % group),
             'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
             'avg_launch_us': round(ms / len(tms) * 1e3, 2), 'bytes_per_launch': per_frame * frames / len(tms),
@@ -305,7 +306,7 @@ def measure(workload, args, world, rank, dev):
         torch.cuda.synchronize()
         tms = [(e0.elapsed_time(e1), fr) for e0, e1, fr in plan.timing]
         plan.timing = None
-        sdr_roof = sdr_roofline(model, tms)
+        sdr_roof = sdr_roofline(model, tms, plan.group(plan.L - 1, dev))
 
     kern_ms = [ev.elapsed_ms(a[r], b[r]) for a, b in ev_pairs for r in range(R)]
     kern_avg_ms = sum(kern_ms) / len(kern_ms) if kern_ms else float('nan')
@@ -320,10 +321,13 @@ def measure(workload, args, world, rank, dev):
     achieved_tflops = flops_launch / (kern_avg_ms * 1e-3) / 1e12
 
     traffic, traffic_src = None, PMC_TRAFFIC.get(workload)
+    tw = 4 if (Din < 32 or J * D > 512) else 2     # row tiles per wave (route_fwd32.hip Fwd32Plan::TW)
+    # iteration 0: the full-K pass with its finish fused for din = dout = 32, else the chunked GEMM
+    first = 'route_fwd32_first_full_kernel' if (Din == 32 and D == 32) else f'void route_fwd32_first_kernel<{Din}, {D}>'
+    # r >= 1: the software-pipelined pass where it has two row tiles per wave (route_fwd32.hip launch_rpass)
+    rpass = f'void route_fwd32{"p" if tw <= 2 else ""}_kernel<{Din}, {D}, 8, {tw}>'
     if fwd32 and traffic_src:
-        tw = 4 if (Din < 32 or J * D > 512) else 2     # row tiles per wave (route_fwd32.hip Fwd32Plan::TW)
-        traffic = pmc_traffic(traffic_src, [f'void route_fwd32_first_kernel<{Din}, {D}>',
-                                            f'void route_fwd32_kernel<{Din}, {D}, 8, {tw}>'], [1.0, R - 1.0])
+        traffic = pmc_traffic(traffic_src, [first, rpass], [1.0, R - 1.0])
     res = {
         'value': round(B * T * world * args.steps / elapsed, 1), 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
         'config': {'workload': f'{workload}: SRF L={cfg.model_encoder_num} PH=CH={cfg.model_caps_primary_num} '
@@ -333,9 +337,9 @@ def measure(workload, args, world, rank, dev):
                                f'train step (fwd+bwd+allreduce+Adam)',
                    'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
                    'parallelism': f'dp{world}', 'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
-        'roofline': {'kernel': (f'route_fwd32_first_kernel + route_fwd32_kernel<{Din},{D}> (layer {last + 1} DR forward '
-                                f'passes, R={R}; pose on v_mfma_f32_32x32x16_f16 as 2-term fp16 splits of power-of-two '
-                                f'scaled operands + one bf16 bias MFMA = fp32-accurate)'
+        'roofline': {'kernel': (f'{first.replace("void ", "")} + {rpass.replace("void ", "")} (layer {last + 1} DR '
+                                f'forward passes, R={R}; pose on v_mfma_f32_32x32x16_f16 as 2-term fp16 splits of '
+                                f'power-of-two scaled operands + one bf16 bias MFMA = fp32-accurate)'
                                 if fwd32 else f'route_pass_kernel<{Din},{D},8,FWD> (layer {last + 1} DR forward pass)'),
                      'bound': 'mfma', 'achieved': round(achieved_tflops, 3), 'peak': FP32_MFMA_PEAK_TFLOPS,
                      'unit': 'TFLOP/s', 'frac': round(achieved_tflops / FP32_MFMA_PEAK_TFLOPS, 4),

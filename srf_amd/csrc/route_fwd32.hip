@@ -1156,7 +1156,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 
 
 #ifndef SRF_FWD32P_VREG
-#define SRF_FWD32P_VREG 0   // 1: route_fwd32p_kernel keeps the Vc fragments in registers (LDS: stats only)
+#define SRF_FWD32P_VREG 1   // 1: route_fwd32p_kernel keeps the Vc fragments in registers (LDS: stats only; C4 step 9.13 -> 9.06 ms)
 #endif
 // Routing pass r >= 1, software-pipelined over the input capsules: while the matrix
 // cores form capsule i + 1's pose tiles (pose_prog, which also streams in capsule
