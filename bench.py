@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`, averaged per dispatch by
 # scripts/pmcsum.py (KiB per dispatch), per workload
 PMC_TRAFFIC = {'timit_c2': os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4h.json'),
-               'wsj_c4': os.path.join(HERE, 'profiles', 'r03_pmc_traffic_c4.json')}
+               'wsj_c4': os.path.join(HERE, 'profiles', 'r04_pmc_c4.json')}
 
 
 def make_config(kw):

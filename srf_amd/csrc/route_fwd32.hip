@@ -1102,7 +1102,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #if SRF_FWD32_FASTDIV
       const float sc = __expf(m - M) * __builtin_amdgcn_rcpf(Z);
 #else
-      const float sc = __expf(m - M) / Z;
+      const float sc = __expf(m - M) * __builtin_amdgcn_rcpf(Z);   // Z >= 1: 1-ulp v_rcp
 #endif
       {
         // lane half h owns capsules j0 + 2a + h after the logit reduce-scatter; frames
@@ -1112,7 +1112,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         for (int a = 0; a < OWN; ++a)
           bstore(crs, fvalid ? e[a] * sc : 0.f, (uint32_t)((j0 + h + 2 * a) * A.Fs + f) * 4u,
                  (uint32_t)i * A.JP * A.Fs * 4u);
-        bstore(lzs, M + __logf(Z), (h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore,
+        bstore(lzs, M + __builtin_amdgcn_logf(Z) * 0.69314718f, (h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore,
                (uint32_t)i * A.Fs * 4u);
       }
       float c[CP];
@@ -1155,6 +1155,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 }
 
 
+#ifndef SRF_FWD32P_DBG
+#define SRF_FWD32P_DBG 0   // timing experiments of the pipelined passes (never shipped)
+#endif
 #ifndef SRF_FWD32P_VREG
 #define SRF_FWD32P_VREG 1   // 1: route_fwd32p_kernel keeps the Vc fragments in registers (LDS: stats only; C4 step 9.13 -> 9.06 ms)
 #endif
@@ -1273,13 +1276,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
                        (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8);
     logits(uc, par);
     __syncthreads();
-    for (int i = i0; i < i1; ++i) {
+    // one capsule: i + 1's tiles into unext while capsule i (in ucur) is finished; the loop
+    // runs two steps with the roles swapped, so no register copy moves u between them
+    auto step = [&](int i, f16v (&ucur)[TW], f16v (&unext)[TW]) __attribute__((always_inline)) {
       const bool more = i + 1 < i1;
       if (more) {   // capsule i + 1's tiles on the matrix cores (operands of i + 2 streamed in)
         const int in = min(i + 2, i1 - 1);
-        pose_prog<DIN, TW>(fr, ones, un, rs, wvo, bvo,
-                           x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                           A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
+#if SRF_FWD32P_DBG
+        // timing experiment (wrong results): 1 = x of the chunk's first capsule (cache-hot),
+        // 2 = W and bias of the first capsule, 3 = both
+        const int inx = (SRF_FWD32P_DBG & 1) ? i0 : in, inw = (SRF_FWD32P_DBG & 2) ? i0 : in;
+#else
+        const int inx = in, inw = in;
+#endif
+        pose_prog<DIN, TW>(fr, ones, unext, rs, wvo, bvo,
+                           x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                           A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8);
       }
       // finish capsule i: softmax over all waves' rows, couplings, s += c u
       float M, Z;
@@ -1301,12 +1313,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         M = fmaxf(m0, m1);
         Z = z0 * __expf(m0 - M) + z1 * __expf(m1 - M);
       }
-      const float sc = __expf(m - M) / Z;
+      const float sc = __expf(m - M) * __builtin_amdgcn_rcpf(Z);   // Z >= 1: 1-ulp v_rcp
 #pragma unroll
       for (int a = 0; a < OWN; ++a)
         bstore(crs, fvalid ? e[a] * sc : 0.f, (uint32_t)((j0 + h + 2 * a) * A.Fs + f) * 4u,
                (uint32_t)i * A.JP * A.Fs * 4u);
-      bstore(lzs, M + __logf(Z), (h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore,
+      bstore(lzs, M + __builtin_amdgcn_logf(Z) * 0.69314718f, (h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore,
              (uint32_t)i * A.Fs * 4u);
       float c[CP];
 #pragma unroll
@@ -1322,17 +1334,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         for (int v = 0; v < 16; v += 2) {
           const float cv = c[kpart<DOUT>(t, v)];
           f2 a2 = {acc[t][v], acc[t][v + 1]};
-          a2 += f2{cv, cv} * f2{uc[t][v], uc[t][v + 1]};
+          a2 += f2{cv, cv} * f2{ucur[t][v], ucur[t][v + 1]};
           acc[t][v] = a2.x;
           acc[t][v + 1] = a2.y;
         }
       if (more) {   // capsule i + 1's logits and stats, then the one barrier
         par ^= 1;
-        logits(un, par);
+        logits(unext, par);
+#if SRF_FWD32P_DBG & 4
+        __builtin_amdgcn_sched_barrier(0);   // timing experiment: no barrier (wrong results)
+#else
         __syncthreads();
-#pragma unroll
-        for (int t = 0; t < TW; ++t) uc[t] = un[t];
+#endif
       }
+    };
+    for (int i = i0; i < i1; i += 2) {
+      step(i, uc, un);
+      if (i + 1 < i1) step(i + 1, un, uc);
     }
   }
 #pragma unroll
@@ -1671,14 +1689,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
                        (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8);
     dots(uc, cc, par);
     __syncthreads();
-    for (int i = i0; i < i1; ++i) {
+    // one capsule, as route_fwd32p_kernel's step: two steps per loop turn with the roles of
+    // (uc, cc) and (un, cn) swapped, so no copies
+    auto step = [&](int i, f16v (&ucur)[TW], f16v (&unext)[TW], float (&ccur)[OWN], float (&cnext)[OWN])
+        __attribute__((always_inline)) {
       const bool more = i + 1 < i1;
       if (more) {
-        load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
+        load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cnext);
         const int in = min(i + 2, i1 - 1);
-        pose_prog<DIN, TW>(fr, ones, un, rs, wvo, bvo,
-                           x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                           A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
+#if SRF_FWD32P_DBG
+        // timing experiment (wrong results): 1 = x of the chunk's first capsule (cache-hot),
+        // 2 = W and bias of the first capsule, 3 = both
+        const int inx = (SRF_FWD32P_DBG & 1) ? i0 : in, inw = (SRF_FWD32P_DBG & 2) ? i0 : in;
+#else
+        const int inx = in, inw = in;
+#endif
+        pose_prog<DIN, TW>(fr, ones, unext, rs, wvo, bvo,
+                           x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                           A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8);
       }
       // finish capsule i: sigma over all waves, stats, gL, gVc += gL u
       float S;
@@ -1700,7 +1728,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       }
       float gown[OWN];
 #pragma unroll
-      for (int a = 0; a < OWN; ++a) gown[a] = cc[a] * (Q[a] - S);
+      for (int a = 0; a < OWN; ++a) gown[a] = ccur[a] * (Q[a] - S);
       {
         float* dst = Bk.glst + ((size_t)i * A.JP + j0 + h) * A.Fs + f;
 #pragma unroll
@@ -1720,19 +1748,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         for (int v = 0; v < 16; v += 2) {
           const float gv = g[kpart<DOUT>(t, v)];
           f2 a2 = {acc[t][v], acc[t][v + 1]};
-          a2 += f2{gv, gv} * f2{uc[t][v], uc[t][v + 1]};
+          a2 += f2{gv, gv} * f2{ucur[t][v], ucur[t][v + 1]};
           acc[t][v] = a2.x;
           acc[t][v + 1] = a2.y;
         }
       if (more) {
         par ^= 1;
-        dots(un, cn, par);
+        dots(unext, cnext, par);
         __syncthreads();
-#pragma unroll
-        for (int a = 0; a < OWN; ++a) cc[a] = cn[a];
-#pragma unroll
-        for (int t = 0; t < TW; ++t) uc[t] = un[t];
       }
+    };
+    for (int i = i0; i < i1; i += 2) {
+      step(i, uc, un, cc, cn);
+      if (i + 1 < i1) step(i + 1, un, uc, cn, cc);
     }
   }
 #pragma unroll
