@@ -1366,10 +1366,8 @@ __global__ __launch_bounds__(256) void route_gw2_kernel(
     }
     __syncthreads();   // buffer buf staged; the other buffer is free
     const bool more = ft + 1 < ft1;
-    if (more) {
-      stage_load(ft + 1);
-      vec_load(ft + 1);
-    }
+    if (more) stage_load(ft + 1);
+    vec_load(more ? ft + 1 : ft);   // unconditional: no register merge of old and new vectors
     const float* sb = stg[buf];
 #pragma unroll
     for (int k = 0; k < CAP; ++k) {
@@ -1550,8 +1548,10 @@ __global__ __launch_bounds__(256, (D >= 32 && CAP >= 8) ? 2 : 3) void route_gw3_
     if (ft + 1 < ft1) {
       stage_store(buf ^ 1);
       if (ft + 2 < ft1) stage_load(ft + 2);
-      vec_load(ft + 1);
     }
+    // unconditional (the last tile reloads itself): a conditional load merges the old
+    // and new vectors and costs a register copy of every vector per tile
+    vec_load(ft + 1 < ft1 ? ft + 1 : ft);
     const float* sb = stg[buf];
 #pragma unroll
     for (int k = 0; k < CAP; ++k) {
@@ -1701,15 +1701,17 @@ __global__ __launch_bounds__(256, 2) void route_gw16s_kernel(
                                                       (int)nrec, 0x00020000);
   }
   const uint32_t vo0 = (uint32_t)((8 * h) * JD + row) * 4;
-  float nx[R + RV][8];
+  // the next tile's per-frame vectors, held as frame pairs so that the scaling below is
+  // one packed multiply per pair with no register shuffles
+  f2 nx[R + RV][4];
   auto vec_load = [&](int ft) {
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
       const uint32_t so = (uint32_t)((ft * 16 + v) * JD) * 4;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        nx[r][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g[r], vo0, so, 0));
-        if (r > 0) nx[R + r - 1][v] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_v[r - 1], vo0, so, 0));
+        nx[r][v >> 1][v & 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g[r], vo0, so, 0));
+        if (r > 0) nx[R + r - 1][v >> 1][v & 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_v[r - 1], vo0, so, 0));
       }
     }
   };
@@ -1735,16 +1737,18 @@ __global__ __launch_bounds__(256, 2) void route_gw16s_kernel(
     f2 fv[R + RV][4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      fv[0][v] = f2{nx[0][2 * v], nx[0][2 * v + 1]} * s0;
+      fv[0][v] = nx[0][v] * s0;
 #pragma unroll
-      for (int a = 1; a < R + RV; ++a) fv[a][v] = f2{nx[a][2 * v], nx[a][2 * v + 1]} * sg;
+      for (int a = 1; a < R + RV; ++a) fv[a][v] = nx[a][v] * sg;
     }
     __syncthreads();   // tile ft staged in buf; buf ^ 1 (tile ft - 1) is free
     if (ft + 1 < ft1) {
       stage_store(buf ^ 1);
       if (ft + 2 < ft1) stage_load(ft + 2);
-      vec_load(ft + 1);
     }
+    // unconditional (the last tile reloads itself): a conditional load merges the old
+    // and new vectors and costs a register copy of every vector per tile
+    vec_load(ft + 1 < ft1 ? ft + 1 : ft);
     const unsigned char* sb = stg[buf];
 #pragma unroll
     for (int k = 0; k < CAP; ++k) {
@@ -2435,7 +2439,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
                                      w.gs + (size_t)r * FJD, stats_r, w.gl + (size_t)(r - 1) * blk * JP, st);
       if (rc) return rc;
       launch_bwd_finish<D>(g, srf::fwd32_slab(plan, w.p32), plan.n_chunks, nullptr, w.A,
-                           saved + (size_t)(2 * (r - 1)) * FJD, w.gs + (size_t)(r - 1) * FJD, st);
+                             saved + (size_t)(2 * (r - 1)) * FJD, w.gs + (size_t)(r - 1) * FJD, st);
     } else {
       dispatch_pass<D, MODE_BWD>(g, pc, n_chunks, emb, W, bias, r, vc, w.gs + (size_t)r * FJD, w.slab, stats_r, 1,
                                  st);

@@ -196,10 +196,13 @@ def test_sdr_pose_fp8_bound(cuda, din, J, D):
 def test_sdr_pose_fp8_matches_emulation(cuda, din, J, D):
     """The fp8 pose kernel (pose_n mode 1: fp32 u; mode 2: bf16 u) computes exactly the
     quantisation oracle/srf_oracle.pose_fp8 restates (per-vector power-of-two scales,
-    e4m3 round to nearest even, exact products, fp32 bias, bf16 rounding of u): on
-    identical fp32 inputs the two differ only by the order of the fp32 accumulation,
-    |gpu - emul| <= 1e-6 sum_k |W_q||x_q| (+ one bf16 ulp of u in mode 2), with
-    operands spanning 2^-20 .. 2^4 and zero frames."""
+    e4m3 round to nearest even, exact products, fp32 bias, bf16 rounding of u), with
+    operands spanning 2^-20 .. 2^4 and zero frames.  The emulation sums exactly; the
+    fp8 MFMA does not accumulate its K block in full fp32: measured on gfx950 (r04g
+    dump, both din) its sums differ from the exact sum of the same e4m3 products by
+    up to 2^-14.3 sum_k |W_q||x_q| (2^-12.3 of the largest single product).  The bound
+    is 2^-12 sum_k |W_q||x_q| + 2 fp32 ulps of u (+ one bf16 ulp in mode 2): one
+    wrongly rounded or wrongly scaled operand of weight above 2^-8 of the sum fails it."""
     import ctypes
     from srf_amd import _lib
     L = _lib.lib()
@@ -231,7 +234,7 @@ def test_sdr_pose_fp8_matches_emulation(cuda, din, J, D):
         _lib.check(L.srf_route_sdr_pose_n((_lib.SdrRange * 1)(r), 1, B, T, N, din, lp, rp, J, D, mode, st), 'pose')
         torch.cuda.synchronize()
         got = u.float().cpu().double().numpy().reshape(B, T, in_n, JD)
-        tol = 1e-6 * mag + 1e-7 * np.abs(ref) + (2.0 ** -8 * np.abs(ref) if mode == 2 else 0.0)
+        tol = 2.0 ** -12 * mag + 2.0 ** -22 * np.abs(ref) + (2.0 ** -8 * np.abs(ref) if mode == 2 else 0.0)
         err = np.abs(got - ref)
         assert np.all(err <= tol), (mode, (err - tol).max(), np.argwhere(err > tol)[:4].tolist())
 
