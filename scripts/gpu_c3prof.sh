@@ -1,13 +1,18 @@
-# C3 (SDR) profile: per-frame recurrence times of the two C3 layer shapes (shipped
-# library, then the stamp build's phase shares), and the kernel-trace statistics of
-# the wsj_c3 bench step.
-#   TAG=name bash scripts/gpu_c3prof.sh
+# C3 (SDR) profile: per-frame recurrence times of the two C3 layer shapes against the
+# group size (shipped library, then each library in ABLIBS), the stamp build's phase
+# shares, and the kernel-trace statistics of the wsj_c3 bench step.
+#   TAG=name [ABLIBS="ab/x.so ..."] bash scripts/gpu_c3prof.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-c3prof}
 mkdir -p $OUT
-timeout -k 10 150 python3 -u scripts/seq_stamps.py > $OUT/stamps_ship.log 2>&1 || { tail -5 $OUT/stamps_ship.log; exit 1; }
-cat $OUT/stamps_ship.log
+timeout -k 10 150 python3 -u scripts/sdr_group_frames.py > $OUT/groups.log 2>&1 || { tail -5 $OUT/groups.log; exit 1; }
+cat $OUT/groups.log
+for lib in $ABLIBS; do
+  n=$(basename $lib .so)
+  SRF_LIB_PATH=$lib timeout -k 10 150 python3 -u scripts/sdr_group_frames.py > $OUT/groups_$n.log 2>&1 || { tail -5 $OUT/groups_$n.log; exit 1; }
+  echo "[$lib]"; cat $OUT/groups_$n.log
+done
 if [ -f ab/stamp.so ]; then
   SRF_LIB_PATH=ab/stamp.so timeout -k 10 150 python3 -u scripts/seq_stamps.py > $OUT/stamps.log 2>&1 || { tail -5 $OUT/stamps.log; exit 1; }
   cat $OUT/stamps.log

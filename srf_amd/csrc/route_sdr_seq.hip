@@ -42,8 +42,8 @@ __device__ unsigned long long* g_stamps;   // diagnostic builds: phase cycle sum
 constexpr unsigned long long* g_stamps = nullptr;
 #endif
 
-// LDS: w [JD] (agreement input of the iteration: v_{t-1} at r = 0, then v^{r-1}),
-// part [16][JD].  GRP: X.G workgroups per utterance split its input capsules
+// LDS: w [JP * D] (agreement input of the iteration: v_{t-1} at r = 0, then v^{r-1};
+// the padded capsules' tail zero), part [16][JD].  GRP: X.G workgroups per utterance split its input capsules
 // (srf_group.h); member 0 stores v and s^r, every member its own capsules' c^r.
 template <int D, int JP, int NIM, bool GRP>
 __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems items, int T, int in_n, int J,
@@ -56,8 +56,9 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
   const srf::SeqRange rg = I.rg;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = J * D;
+  constexpr int JDp = JP * D;
   float* wl = lds;
-  float* part = lds + ((JD + 3) & ~3);
+  float* part = lds + JDp;
   const int tid = threadIdx.x;
   const int utt = GRP ? blockIdx.x / X.G : blockIdx.x;   // utterance
   const int gm = GRP ? blockIdx.x - utt * X.G : 0;       // member of its group
@@ -71,6 +72,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
   const size_t csr = (size_t)iters * (in_n * JP + JD);   // coupling record per frame (cs != nullptr)
   if (rg.t0 >= rg.t1) return;
   if (ev) wl[tid] = rg.t0 > 0 ? vo[(size_t)(rg.t0 - 1) * JD + tid] : 0.f;   // v_{t0-1} (v_{-1} = 0)
+  zero_tail(wl, 1, JD, JDp);
   float ur[C::NIM][C::KD];
   load_frame<C>(ub + (size_t)(rg.t0 - rg.tu0) * ff, JD, L, ur);
   __syncthreads();
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
     for (int k = 0; k < C::NIM; ++k) b[k] = 0.f;
     for (int r = 0; r < iters; ++r) {
       float w[C::KD];
-      lds_slice<C::KD>(wl + L.eoff, L.jv, w);
+      lds_slice<C::KD>(wl, L.eoff, w);
       logits_softmax<C>(ur, w, L, b, c);
       row_partial<C>(c, ur, L, JD, part);
       if (cs) store_ij<C>(c, L, cs + ((size_t)utt * T + t) * csr + (size_t)r * in_n * JP);
@@ -114,7 +116,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
 }
 
 size_t fwd_lds(int J, int D) {
-  return ((((size_t)J * D + 3) & ~(size_t)3) + (size_t)kWaves * J * D) * sizeof(float);
+  return ((size_t)pow2_at_least(J) * D + (size_t)kWaves * J * D) * sizeof(float);
 }
 
 template <int D, int JP, int NIM>
@@ -133,6 +135,8 @@ template <int D, int JP>
 int fwd_nim(int nim, const srf::SeqItems& items, const srf_grp::Grp& X, int B, int T, int in_n, int J, int iters,
             int mask_first, hipStream_t st) {
   if (nim == 2) return launch_fwd<D, JP, 2>(items, X, B, T, in_n, J, iters, mask_first, st);
+  if constexpr (D == 32 && JP == 32)
+    if (nim == 3) return launch_fwd<D, JP, 3>(items, X, B, T, in_n, J, iters, mask_first, st);
   if (nim == 5) return launch_fwd<D, JP, 5>(items, X, B, T, in_n, J, iters, mask_first, st);
   if constexpr (seq_kd(D, JP) <= 8)
     return launch_fwd<D, JP, 10>(items, X, B, T, in_n, J, iters, mask_first, st);
@@ -159,7 +163,13 @@ bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm, int g
   const int G = srf_seq::seq_slots(dout, JP);
   const int ng = std::max(1, group), blk = (in_n + ng - 1) / ng;   // a group member's block (lane_map)
   const int NI = (blk + G - 1) / G;
-  const int m = NI <= 2 ? 2 : NI <= 5 ? 5 : (NI <= 10 && KD <= 8) ? 10 : 0;
+  // 3 rows per lane only for dout = JP = 32 (the C3 last layer split over two
+  // workgroups: 48 registers of u instead of 80, no spills, every row resident backward)
+  const int m = NI <= 2                                ? 2
+                : (NI <= 3 && dout == 32 && JP == 32) ? 3
+                : NI <= 5                              ? 5
+                : (NI <= 10 && KD <= 8)                ? 10
+                                                       : 0;
   if (m == 0) return false;
   const int r = iters <= 3 ? 3 : 5;
   if (r == 5 && m != 2) return false;   // five-iteration backward kept for small layers only

@@ -35,7 +35,8 @@ constexpr unsigned long long* g_stamps = nullptr;
 // [RM][in_n][JP] (written by the first lane of each capsule, read by all Q lanes).
 constexpr bool cl_wanted(int nim, int kd) { return nim * kd >= 40; }
 
-// LDS: w [JDa], Vc [RM][JDa], gs [RM][JDa], part [16][JD] (+ c, gL [RM][in_n][JP]).
+// LDS: w [JDp], Vc [RM][JDp], gs [RM][JDp], part [16][JD] (+ c, gL [RM][in_n][JP]);
+// JDp = JP * D, the padded capsules' tails zero (lds_slice reads them unconditionally).
 // CS: the forward stored each frame's couplings c^r and s^r (srf::sdr_seq_cs_floats
 // per frame): the backward reads them instead of recomputing the R iterations, so
 // only the adjoint runs per frame (and the logits no longer hold registers).
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
   constexpr int RR = CL ? 1 : RM;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = J * D;
-  const int JDa = (JD + 3) & ~3;
+  constexpr int JDa = JP * D;
   const int R = iters;
   float* wl = lds;
   float* vcl = wl + JDa;
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
 #pragma unroll
   for (int r = 0; r < RM; ++r) sr[r] = 0.f;
   load_rows<C, KRES>(ub + (size_t)(rg.t1 - 1 - rg.tu0) * ff, JD, L, ur);
+  zero_tail(wl, 1 + 2 * RM, JD, JDa);   // w, Vc, gs are consecutive
   SEQ_STAMP_DECL
   for (int t = rg.t1 - 1; t >= rg.t0; --t) {
     const size_t f = f0 + t;
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
     for (int r = 0; r < RM; ++r) {
       if (r < R) {
         float w[C::KD], cc[C::NIM];
-        lds_slice<C::KD>(wl + L.eoff, L.jv, w);
+        lds_slice<C::KD>(wl, L.eoff, w);
         logits_softmax<C>(ur, w, L, b, cc);
         row_partial<C>(cc, ur, L, JD, part);
         if constexpr (CL) {
@@ -183,7 +185,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
         SEQ_MARK(2);     // squash adjoint
 
         float gsv[C::KD], cc[C::NIM], gg[C::NIM];
-        lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
+        lds_slice<C::KD>(gsl + r * JDa, L.eoff, gsv);
         if constexpr (CL) {
           load_ij<C>(cl + r * in_n * JP, L, cc);
         } else {
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
             __builtin_amdgcn_sched_barrier(0);   // one re-read row in flight at a time
             if (k < L.NI) {
               float urow[C::KD];
-              lds_slice<C::KD>(uf + (size_t)(L.g + k * C::G) * JD + L.eoff, L.jv, urow);
+              load_row<C>(uf, JD, L, k, urow);
               adjoint(k, urow);
 #pragma unroll
               for (int d = 0; d < C::KD; ++d) sp[d] += gg[k] * urow[d];
@@ -282,8 +284,8 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
         for (int r = 0; r < RM; ++r) {
           if (r < R) {
             float gsv[C::KD], vcv[C::KD];
-            lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
-            lds_slice<C::KD>(vcl + r * JDa + L.eoff, L.jv, vcv);
+            lds_slice<C::KD>(gsl + r * JDa, L.eoff, gsv);
+            lds_slice<C::KD>(vcl + r * JDa, L.eoff, vcv);
 #pragma unroll
             for (int kk = 0; kk < GR; ++kk) {
               const int k = k0 + kk;
@@ -325,8 +327,8 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
         for (int r = 0; r < RM; ++r) {
           if (r < R) {
             float gsv[C::KD], vcv[C::KD];
-            lds_slice<C::KD>(gsl + r * JDa + L.eoff, L.jv, gsv);
-            lds_slice<C::KD>(vcl + r * JDa + L.eoff, L.jv, vcv);
+            lds_slice<C::KD>(gsl + r * JDa, L.eoff, gsv);
+            lds_slice<C::KD>(vcl + r * JDa, L.eoff, vcv);
             float ck, gk;
             if constexpr (CL) {
               const int idx = (L.g + k * C::G) * JP + L.j;
@@ -358,8 +360,8 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
 }
 
 size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
-  const size_t JDa = ((size_t)J * D + 3) & ~(size_t)3;
   const size_t JP = (size_t)pow2_at_least(J);
+  const size_t JDa = JP * D;
   return (JDa * (1 + 2 * (size_t)RM) + (size_t)kWaves * J * D + (cl ? 2 * (size_t)RM * in_n * JP : 0)) *
          sizeof(float);
 }
@@ -394,6 +396,8 @@ int bwd_nim(int nim, int rm, const srf::SeqItems& items, const srf_grp::Grp& X, 
             int J, int iters, int mask_first, hipStream_t st) {
   if (rm == 5) return launch_bwd<D, JP, 2, 5>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
   if (nim == 2) return launch_bwd<D, JP, 2, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
+  if constexpr (D == 32 && JP == 32)
+    if (nim == 3) return launch_bwd<D, JP, 3, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
   if (nim == 5) return launch_bwd<D, JP, 5, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
   if constexpr (seq_kd(D, JP) <= 8)
     return launch_bwd<D, JP, 10, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);

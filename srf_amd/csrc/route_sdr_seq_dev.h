@@ -156,18 +156,21 @@ __device__ __forceinline__ void load_ij(const float* __restrict__ src, const Lan
   for (int k = 0; k < C::NIM; ++k) v[k] = k < L.NI ? src[(L.g + k * C::G) * C::JP + L.j] : 0.f;
 }
 
-// the lane's rows of u_t -> registers (zeros for padded capsules and rows)
-template <class C>
-__device__ __forceinline__ void load_frame(const float* __restrict__ ut, int JD, const Lane& L,
-                                           float (&ur)[C::NIM][C::KD]) {
+// the lane's first KR rows of u_t -> registers, zeros for padded capsules and rows past
+// the lane's: one buffer resource over the frame, and an invalid row reads an offset past
+// its range, which the buffer unit returns as zeros (no branch per row)
+template <class C, int KR>
+__device__ __forceinline__ void load_rows(const float* __restrict__ ut, int JD, const Lane& L,
+                                          float (&ur)[KR][C::KD]) {
+  constexpr uint32_t kOff = 0x7FFFFF00u;   // past any frame (in_n * JD * 4 < 2^31)
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ut), 0, (int)kOff, 0x00020000);
 #pragma unroll
-  for (int k = 0; k < C::NIM; ++k) {
+  for (int k = 0; k < KR; ++k) {
     const bool ok = L.jv && k < L.NI;
-    const float* p = ut + (size_t)(L.g + k * C::G) * JD + L.eoff;
+    const uint32_t o = ok ? (uint32_t)(((L.g + k * C::G) * JD + L.eoff) * 4) : kOff;
 #pragma unroll
     for (int c = 0; c < C::KD; c += 4) {
-      f4 x = {0.f, 0.f, 0.f, 0.f};
-      if (ok) x = *reinterpret_cast<const f4*>(p + c);
+      const f4 x = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + c * 4, 0, 0));
       ur[k][c] = x.x;
       ur[k][c + 1] = x.y;
       ur[k][c + 2] = x.z;
@@ -176,24 +179,11 @@ __device__ __forceinline__ void load_frame(const float* __restrict__ ut, int JD,
   }
 }
 
-// the lane's first KR rows of u_t -> registers (load_frame for KR = NIM)
-template <class C, int KR>
-__device__ __forceinline__ void load_rows(const float* __restrict__ ut, int JD, const Lane& L,
-                                          float (&ur)[KR][C::KD]) {
-#pragma unroll
-  for (int k = 0; k < KR; ++k) {
-    const bool ok = L.jv && k < L.NI;
-    const float* p = ut + (size_t)(L.g + k * C::G) * JD + L.eoff;
-#pragma unroll
-    for (int c = 0; c < C::KD; c += 4) {
-      f4 x = {0.f, 0.f, 0.f, 0.f};
-      if (ok) x = *reinterpret_cast<const f4*>(p + c);
-      ur[k][c] = x.x;
-      ur[k][c + 1] = x.y;
-      ur[k][c + 2] = x.z;
-      ur[k][c + 3] = x.w;
-    }
-  }
+// the lane's rows of u_t -> registers
+template <class C>
+__device__ __forceinline__ void load_frame(const float* __restrict__ ut, int JD, const Lane& L,
+                                           float (&ur)[C::NIM][C::KD]) {
+  load_rows<C, C::NIM>(ut, JD, L, ur);
 }
 
 // sp summed over the wave's rows; the first row's lanes write it to part[wave][eoff ..]
@@ -208,12 +198,37 @@ __device__ __forceinline__ void partial_out(float (&sp)[C::KD], const Lane& L, i
   }
 }
 
+// KD values at base + off: the [JP * D] LDS vectors (the padded capsules' tail zeroed
+// once per launch by zero_tail), so every lane reads, no branch or select
 template <int KD>
-__device__ __forceinline__ void lds_slice(const float* __restrict__ src, bool ok, float (&w)[KD]) {
+__device__ __forceinline__ void lds_slice(const float* __restrict__ base, int off, float (&w)[KD]) {
 #pragma unroll
   for (int c = 0; c < KD; c += 4) {
-    f4 x = {0.f, 0.f, 0.f, 0.f};
-    if (ok) x = *reinterpret_cast<const f4*>(src + c);
+    const f4 x = *reinterpret_cast<const f4*>(base + off + c);
+    w[c] = x.x;
+    w[c + 1] = x.y;
+    w[c + 2] = x.z;
+    w[c + 3] = x.w;
+  }
+}
+
+// the padded capsules' entries [JD, JDp) of n LDS vectors of stride JDp -> 0
+__device__ __forceinline__ void zero_tail(float* __restrict__ v, int n, int JD, int JDp) {
+  const int w = JDp - JD;
+  for (int k = threadIdx.x; k < n * w; k += kThreads) v[(k / w) * JDp + JD + k % w] = 0.f;
+}
+
+// row k of the lane's rows of u_t (a global re-read), zeros where !L.jv: one buffer
+// resource over the frame, the padded capsules' lanes read past its range
+template <class C>
+__device__ __forceinline__ void load_row(const float* __restrict__ ut, int JD, const Lane& L, int k,
+                                         float (&w)[C::KD]) {
+  constexpr uint32_t kOff = 0x7FFFFF00u;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ut), 0, (int)kOff, 0x00020000);
+  const uint32_t o = L.jv ? (uint32_t)(((L.g + k * C::G) * JD + L.eoff) * 4) : kOff;
+#pragma unroll
+  for (int c = 0; c < C::KD; c += 4) {
+    const f4 x = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + c * 4, 0, 0));
     w[c] = x.x;
     w[c + 1] = x.y;
     w[c + 2] = x.z;

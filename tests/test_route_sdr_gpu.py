@@ -201,7 +201,8 @@ def test_sdr_pose_fp8_matches_emulation(cuda, din, J, D):
     fp8 MFMA does not accumulate its K block in full fp32: measured on gfx950 (r04g
     dump, both din) its sums differ from the exact sum of the same e4m3 products by
     up to 2^-14.3 sum_k |W_q||x_q| (2^-12.3 of the largest single product).  The bound
-    is 2^-12 sum_k |W_q||x_q| + 2 fp32 ulps of u (+ one bf16 ulp in mode 2): one
+    is 2^-12 sum_k |W_q||x_q| + 2 fp32 ulps of u (+ one bf16 ulp, 2^-7 |u|, in mode 2:
+    a sum that differs in its last fp32 bits may round to the other bf16 neighbour): one
     wrongly rounded or wrongly scaled operand of weight above 2^-8 of the sum fails it."""
     import ctypes
     from srf_amd import _lib
@@ -234,7 +235,7 @@ def test_sdr_pose_fp8_matches_emulation(cuda, din, J, D):
         _lib.check(L.srf_route_sdr_pose_n((_lib.SdrRange * 1)(r), 1, B, T, N, din, lp, rp, J, D, mode, st), 'pose')
         torch.cuda.synchronize()
         got = u.float().cpu().double().numpy().reshape(B, T, in_n, JD)
-        tol = 2.0 ** -12 * mag + 2.0 ** -22 * np.abs(ref) + (2.0 ** -8 * np.abs(ref) if mode == 2 else 0.0)
+        tol = 2.0 ** -12 * mag + 2.0 ** -22 * np.abs(ref) + (2.0 ** -7 * np.abs(ref) if mode == 2 else 0.0)
         err = np.abs(got - ref)
         assert np.all(err <= tol), (mode, (err - tol).max(), np.argwhere(err > tol)[:4].tolist())
 
@@ -295,7 +296,7 @@ def test_sdr_stream_bf16_u_equals_fp32(cuda, J, D, iters, mf):
     (16, 64, 5, False, 16, 20, 20),   # streaming: C5 inner layer
     (32, 64, 3, True, 8, 4, 4),       # streaming: J * D = 2048
     (16, 64, 2, False, 3, 1, 1),      # streaming: in_n = 9 (members without capsules)
-    (32, 32, 3, True, 16, 2, 2),      # register kernels: C3 last layer
+    (32, 32, 3, True, 16, 2, 2),      # register kernels: C3 last layer (G = 2: three rows per lane)
     (16, 32, 3, False, 16, 2, 2),     # register kernels: C3 inner layer
     (16, 16, 5, True, 4, 1, 1),       # register kernels: five iterations, in_n = 12
 ])
