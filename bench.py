@@ -236,7 +236,8 @@ def measure(workload, args, world, rank, dev):
     cfg = make_config(kw)
     model = SequenceRouter(cfg, None, class_n, device=dev, seed=1234)   # same init on every rank
     if args.sdr_last_group is not None:
-        model.sdr_options['last_group'] = args.sdr_last_group
+        g = [int(x) for x in args.sdr_last_group.split(',')]
+        model.sdr_options['last_group'] = (g[0], g[-1])
     opt = train_helper.get_optimizer(cfg)
     batch = synthetic_batch(B, T, class_n, rank, dev)
     loss_state, frame_state, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
@@ -376,9 +377,9 @@ def main():
                     help='comma-separated workloads also measured, reported under "extra" (empty: none)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--sdr-last-group', type=int, default=None,
-                    help='SDR stack: workgroups per utterance of the last layer on the streaming kernels '
-                         '(default: as many as the CUs beside the inner layers allow)')
+    ap.add_argument('--sdr-last-group', default=None,
+                    help='SDR stack: workgroups per utterance of the last layer\'s recurrence, "G" or '
+                         '"G_forward,G_backward" (default: SdrStackPlan.group)')
     ap.add_argument('--eager', action='store_true', help='launch every kernel from Python each step (no hipGraph)')
     args = ap.parse_args()
 

@@ -71,6 +71,6 @@ if __name__ == '__main__':
     B = int(os.environ.get('B', 28))
     T = int(os.environ.get('T', 200))
     frames = int(os.environ.get('FRAMES', 20))
-    groups = [int(x) for x in os.environ.get('GROUPS', '1,2,4,8').split(',')]
+    groups = [int(x) for x in os.environ.get('SDR_GROUPS', '1,2,4,8').split(',')]
     run('last (80x32x32)', B, T, 80, 32, 32, 3, 1, frames, groups)
     run('inner (80x16x32)', B, T, 80, 16, 32, 3, 0, frames, groups)

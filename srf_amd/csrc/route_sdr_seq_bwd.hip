@@ -42,11 +42,11 @@ constexpr bool cl_wanted(int nim, int kd) { return nim * kd >= 40; }
 // only the adjoint runs per frame (and the logits no longer hold registers).
 // With CS the lane keeps only its first KR rows of u in registers and re-reads the
 // others from L2 where the adjoint uses them (once per iteration), and the gu pass
-// accumulates GR rows at a time per LDS read of gs^r / Vc^r: the J = 32 last layer
-// otherwise needs more than the 128 registers a 1024-thread workgroup allows.
+// runs over quarter slices of every row per LDS read of gs^r / Vc^r: the J = 32 last
+// layer otherwise needs more than the 128 registers a 1024-thread workgroup allows.
 // GRP (with CS): X.G workgroups per utterance split its input capsules (srf_group.h)
 // and add their gVc^r partials inside the launch; member 0 writes the carry out.
-template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, int GR = NIM, bool GRP = false>
+template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, bool GRP = false>
 __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems items, int T, int in_n, int J,
                                                                int iters, int mask_first, srf_grp::Grp X) {
   using C = Cfg<D, JP, NIM>;
@@ -269,50 +269,48 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
         SEQ_MARK(5);
       }
     }
-    // ---- gu, one input capsule of the lane at a time (u is dead: its registers
-    // take the next frame's loads, issued right after); with CS, GR capsules per
-    // read of gs^r / Vc^r
+    // ---- gu (u is dead: its registers take the next frame's loads, issued right
+    // after); without CS one input capsule of the lane at a time
     if constexpr (CS) {
+      // four of the lane's KD values per pass, every row at once: one LDS read of each
+      // gs^r / Vc^r quarter slice per pass serves all NIM rows
+      constexpr int HD = 4;
 #pragma unroll
-      for (int k0 = 0; k0 < C::NIM; k0 += GR) {
-        float acc[GR][C::KD];
+      for (int d0 = 0; d0 < C::KD; d0 += HD) {
+        float acc[C::NIM][HD];
 #pragma unroll
-        for (int kk = 0; kk < GR; ++kk)
+        for (int k = 0; k < C::NIM; ++k)
 #pragma unroll
-          for (int d = 0; d < C::KD; ++d) acc[kk][d] = 0.f;
+          for (int d = 0; d < HD; ++d) acc[k][d] = 0.f;
 #pragma unroll
         for (int r = 0; r < RM; ++r) {
           if (r < R) {
-            float gsv[C::KD], vcv[C::KD];
-            lds_slice<C::KD>(gsl + r * JDa, L.eoff, gsv);
-            lds_slice<C::KD>(vcl + r * JDa, L.eoff, vcv);
+            float gsv[HD], vcv[HD];
+            lds_slice<HD>(gsl + r * JDa, L.eoff + d0, gsv);
+            lds_slice<HD>(vcl + r * JDa, L.eoff + d0, vcv);
 #pragma unroll
-            for (int kk = 0; kk < GR; ++kk) {
-              const int k = k0 + kk;
-              if (k < C::NIM && k < L.NI) {
+            for (int k = 0; k < C::NIM; ++k) {
+              if (k < L.NI) {
                 float ck, gk;
                 if constexpr (CL) {
                   const int idx = (L.g + k * C::G) * JP + L.j;
                   ck = cl[r * in_n * JP + idx];
                   gk = gll[r * in_n * JP + idx];
                 } else {
-                  ck = cr[r][k < C::NIM ? k : 0];
-                  gk = gl[r][k < C::NIM ? k : 0];
+                  ck = cr[r][k];
+                  gk = gl[r][k];
                 }
 #pragma unroll
-                for (int d = 0; d < C::KD; ++d) acc[kk][d] += ck * gsv[d] + gk * vcv[d];
+                for (int d = 0; d < HD; ++d) acc[k][d] += ck * gsv[d] + gk * vcv[d];
               }
             }
           }
         }
 #pragma unroll
-        for (int kk = 0; kk < GR; ++kk) {
-          const int k = k0 + kk;
-          if (k < C::NIM && k < L.NI && L.jv) {
-            float* dst = gub + (size_t)(t - rg.tg0) * ff + (size_t)(L.g + k * C::G) * JD + L.eoff;
-#pragma unroll
-            for (int c = 0; c < C::KD; c += 4)
-              *reinterpret_cast<f4*>(dst + c) = f4{acc[kk][c], acc[kk][c + 1], acc[kk][c + 2], acc[kk][c + 3]};
+        for (int k = 0; k < C::NIM; ++k) {
+          if (k < L.NI && L.jv) {
+            float* dst = gub + (size_t)(t - rg.tg0) * ff + (size_t)(L.g + k * C::G) * JD + L.eoff + d0;
+            *reinterpret_cast<f4*>(dst) = f4{acc[k][0], acc[k][1], acc[k][2], acc[k][3]};
           }
         }
       }
@@ -376,12 +374,11 @@ int launch_bwd(const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, int B
   // of the 128 registers (the J = 32, dout = 32 last layer: 5 rows of 16 values)
   constexpr int KD = seq_kd(D, JP);
   constexpr int KR = NIM * KD > 48 ? 32 / KD : NIM;
-  constexpr int GR = 1;
   SRF_REQUIRE(cs || X.G == 1, "sdr_seq: a grouped backward needs the forward's stored couplings");
-  auto k = X.G > 1 ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, GR, true>
-                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, GR, true>)
-           : cs    ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, GR>
-                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, GR>)
+  auto k = X.G > 1 ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, true>
+                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, true>)
+           : cs    ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR>
+                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR>)
                    : (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, false>
                          : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, false>);
   if (lds > 64 * 1024)

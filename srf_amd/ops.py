@@ -440,8 +440,8 @@ class SdrStackPlan:
         the layer's kernels can); store_u_bytes: budget for keeping every layer's u from
         the forward (None: 55 % of the device's memory; 0: recompute per range);
         last_group: workgroups per utterance for the last layer's recurrence
-        (srf_sdr_range.group; None: as many as the CUs left beside the inner layers'
-        batched recurrences allow, at most 8; 1: one)."""
+        (srf_sdr_range.group), one number for both directions or a (forward, backward)
+        pair; None: the defaults of group()."""
         self.B, self.T, self.lpad, self.rpad, self.iters = B, T, lpad, rpad, iters
         self.pose_fp8 = bool(pose_fp8)
         self.store_couplings = bool(store_couplings)
@@ -478,25 +478,29 @@ class SdrStackPlan:
                     for (N, din, J, D, mf) in layers]
         self.streamed = [bool(L_.srf_route_sdr_couplings_required(N * self.win, J, D, iters))
                          for (N, din, J, D, mf) in layers]
-        self.last_group = last_group
+        if last_group is None or isinstance(last_group, (tuple, list)):
+            self.last_group = None if last_group is None else tuple(int(g) for g in last_group)
+        else:
+            self.last_group = (int(last_group), int(last_group))
 
-    def group(self, l, dev):
+    def group(self, l, dev, backward=False):
         """srf_sdr_range.group of layer l's recurrence launches.  Only the last layer's
         (stream B, one range per launch: the critical chain of the stack) are grouped:
         its B * G workgroups spin-wait on each other, so they must be resident next to
         stream A's batched inner-layer recurrence (B workgroups per inner layer, one CU
-        each) -- the one grouped launch in flight at any time.  By default only a
-        streamed last layer is grouped (C5: 955 -> 800 ms per step at G = 2); the
-        register kernels' groups (C3, explicit last_group; their backward reads the
-        stored couplings) measured slower, 24.0 -> 24.4 / 25.0 ms at G = 2 / 4: their
-        per-iteration exchange costs more than the shorter per-member recurrence saves."""
+        each) -- the one grouped launch in flight at any time.  A streamed last layer
+        (C5): as many as the CUs allow, both directions (955 -> 800 ms per step at
+        G = 2).  Register kernels (C3; the grouped backward reads the stored couplings):
+        the backward only, G = 2 -- its frame moves 2x the forward's bytes through one
+        CU, so halving them pays for the three exchanges (r04n: 21.9 -> 21.2 ms), while
+        the forward's exchanges cost more than they save (G = 2 / 4 slower)."""
         if l != self.L - 1 or not (self.streamed[l] or self.store_couplings):
             return 1
         if self.last_group is not None:
-            return max(1, int(self.last_group))
-        if not self.streamed[l]:
-            return 1
+            return max(1, self.last_group[int(backward)])
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        if not self.streamed[l]:
+            return 2 if backward and self.store_couplings and self.B * (self.L + 1) <= cus else 1
         return max(1, min(8, (cus - self.B * (self.L - 1)) // self.B))
 
     def pose_mode(self, l):
@@ -743,7 +747,7 @@ class SdrStack(torch.autograd.Function):
                           workspace_bytes=rws[l].numel(), g_v=_ptr(g_vs[l]), carry=_ptr(carries[l]),
                           gu=_ptr(gus[l]), g0=t0, gn=P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
                           g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1), u_bf16=int(P.ubf[l]),
-                          group=P.group(l, dev))
+                          group=P.group(l, dev, backward=True))
 
         def run(sp, ls, ks, ev=None, gw=True):
             """backward of ranges (ls[i], ks[i]) of same-shaped layers, batched: LN
