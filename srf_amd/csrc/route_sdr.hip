@@ -886,9 +886,14 @@ __global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int 
 // one frame range alone on the GPU, us 32x32 vs 16x16): C5 din 64 pose 850 vs 973, gx
 // 1228 vs 1174, gW 937 vs 1073; C3 din 32 pose 46 vs 33, gx 47 vs 53, gW 91 vs 65.
 enum class SdrGemm { kPose, kGx, kGw };
+#ifndef SRF_SDR_MFMA32_DIN32
+#define SRF_SDR_MFMA32_DIN32 2   // bit 0 pose, bit 1 gx, bit 2 gW: the 32x32 kernels at din 32
+#endif
 bool use_mfma32(int din, int JD, SdrGemm k) {
   if ((din != 32 && din != 64) || JD % 8) return false;
-  return din == 64 ? k != SdrGemm::kGx : k == SdrGemm::kGx;
+  if (din == 64) return k != SdrGemm::kGx;
+  const int bit = k == SdrGemm::kPose ? 1 : k == SdrGemm::kGx ? 2 : 4;
+  return (SRF_SDR_MFMA32_DIN32 & bit) != 0;
 }
 
 // ------------------------------------------------------------------ host
