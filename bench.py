@@ -235,6 +235,9 @@ def measure(workload, args, world, rank, dev):
     kw, class_n, B, T = WORKLOADS[workload]
     cfg = make_config(kw)
     model = SequenceRouter(cfg, None, class_n, device=dev, seed=1234)   # same init on every rank
+    if args.sdr_separate_gxgw:
+        from srf_amd import ops
+        ops.SDR_FUSED_GXGW = False
     if args.sdr_last_group is not None:
         g = [int(x) for x in args.sdr_last_group.split(',')]
         model.sdr_options['last_group'] = (g[0], g[-1])
@@ -380,6 +383,8 @@ def main():
     ap.add_argument('--sdr-last-group', default=None,
                     help='SDR stack: workgroups per utterance of the last layer\'s recurrence, "G" or '
                          '"G_forward,G_backward" (default: SdrStackPlan.group)')
+    ap.add_argument('--sdr-separate-gxgw', action='store_true',
+                    help='SDR stack: the gx and gW launches of din-32 layers separately (default: fused)')
     ap.add_argument('--eager', action='store_true', help='launch every kernel from Python each step (no hipGraph)')
     args = ap.parse_args()
 

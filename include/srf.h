@@ -167,6 +167,10 @@ int srf_route_sdr_gx_n(const srf_sdr_range* ranges, int n, int B, int T, int N, 
                        int dout, void* stream);
 int srf_route_sdr_gw_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
                        int dout, void* stream);
+/* gx_n and gw_n of the same ranges in one launch that reads gu once (din 32; other
+ * shapes run the two entry points above).  Reads W (not WT) besides their fields. */
+int srf_route_sdr_gx_gw_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad,
+                          int J, int dout, void* stream);
 
 /* ---- The SDR layer in frame ranges (the layer-pipelined SDR stack) ----------
  * srf_route_sdr_fwd/bwd split into calls over frames [t0, t1) of every utterance,
@@ -297,6 +301,27 @@ int srf_capsnorm_fwd_range(const float* x, int B, int T, int t0, int t1, int n, 
 int srf_capsnorm_bwd_range(const float* x, int B, int T, int t0, int t1, int n, const float* gamma, const float* beta,
                            int training, float p, unsigned long long seed, int layer, const float* stat,
                            const float* g_y, float* g_x, float* gpart, void* stream);
+/* The ranges of up to SRF_CAPSNORM_MAX_ITEMS same-width layers (n = J*D) in one launch
+ * (the layer-pipelined SDR stack's inner layers, one anti-diagonal at a time): the
+ * *_range calls above for each entry, non-head (ln_mid%d + dropout_mid_%d of `layer`).
+ * The forward reads x / gamma / beta, writes y / stat; the backward reads x / gamma /
+ * beta / stat / g_y, writes g_x / gpart.  Empty ranges are skipped. */
+#define SRF_CAPSNORM_MAX_ITEMS 8
+typedef struct {
+  int t0, t1, layer;
+  const float* x;
+  const float* gamma;
+  const float* beta;
+  float* y;
+  float* stat;
+  const float* g_y;
+  float* g_x;
+  float* gpart;
+} srf_capsnorm_range;
+int srf_capsnorm_fwd_range_n(const srf_capsnorm_range* ranges, int n_ranges, int B, int T, int n, int training,
+                             float p, unsigned long long seed, void* stream);
+int srf_capsnorm_bwd_range_n(const srf_capsnorm_range* ranges, int n_ranges, int B, int T, int n, int training,
+                             float p, unsigned long long seed, void* stream);
 size_t srf_capsnorm_params_workspace(int F, int n);
 int srf_capsnorm_bwd_params(const float* gpart, int F, int n, float* g_gamma, float* g_beta, void* workspace,
                             size_t workspace_bytes, void* stream);

@@ -65,6 +65,7 @@ _SIGNATURES = {
     'srf_route_sdr_recur_bwd_n': (_c_int, [_ranges] + [_c_int] * 8 + [_vp]),
     'srf_route_sdr_gx_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
     'srf_route_sdr_gw_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
+    'srf_route_sdr_gx_gw_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
     'srf_cnnfe_out_dims': (_c_int, [_c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
     'srf_cnnfe_saved_bytes': (_c_size, [_c_int] * 4),
     'srf_cnnfe_fwd_workspace': (_c_size, [_c_int] * 4),

@@ -743,6 +743,123 @@ __global__ __launch_bounds__(256, 2) void sdr_gw32_kernel(GemmItems items, int N
   }
 }
 
+// gx and gW of din-32 layers in one pass over gu (C3): both contract the same gu, over
+// rows (gx) and over frames (gW), so one launch reads it once instead of twice.
+// Workgroup = 16 waves = one capsule i x 512 rows (32 per wave) x every frame of the
+// item, in tiles of 32 frames; per tile and wave, on v_mfma_f32_32x32x2_f32:
+//   gW^T tile  [rows][e] += gu[f][row] x_i(f)[e]   (A: gu, lane = row, as loaded;
+//                                                  B: x through the window, lane = e)
+//   gx^T part  [e][f]    = W_i[row][e] gu[f][row]  (A: W, lane = e, held for the whole
+//                                                  launch; B: gu, lane = frame, read
+//                                                  back transposed from a per-wave LDS
+//                                                  tile [f][34] -- conflict-free reads)
+// the 16 waves' gx parts summed through LDS [wave][f][33] and added into g_emb through
+// the window adjoint (coalesced over e); gW / gbias stored at the end, one writer per
+// element (accumulate adds, as sdr_gw_kernel).
+struct GxwItem {
+  const float* gu;
+  const float* W;
+  const float* emb;
+  float* g_emb;
+  float* gW;
+  float* gbias;
+  int acc, Q;
+  FrameMap fm;
+};
+struct GxwItems {
+  GxwItem it[srf::kMaxItems];
+  int n;
+};
+constexpr int kGxwWaves = 16;
+constexpr int kGxwRows = 32 * kGxwWaves;   // rows per workgroup
+constexpr int kGxwTS = 34;                 // row stride of a wave's transposed tile
+constexpr int kGxwPS = 33;                 // row stride of a wave's gx part
+constexpr size_t kGxwLds = (size_t)kGxwWaves * 32 * (kGxwTS + kGxwPS) * sizeof(float) + 2 * 2 * 32 * sizeof(long long);
+
+__global__ __launch_bounds__(1024) void sdr_gxw32_kernel(GxwItems items, int N, int lpad, int in_n, int JD) {
+  const GxwItem& G = items.it[blockIdx.z];
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* tT = lds;                                  // [wave][32 frames][kGxwTS]
+  float* part = tT + kGxwWaves * 32 * kGxwTS;       // [wave][32 frames][kGxwPS]
+  long long* finfo = reinterpret_cast<long long*>(part + kGxwWaves * 32 * kGxwPS);   // [2][gu | x][32]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int i = blockIdx.y;
+  const int r0 = blockIdx.x * kGxwRows + wv * 32;
+  const bool won = r0 < JD;   // JD % 32 == 0 (host)
+  const int w = i / N, n = i - w * N;
+  // gx's A operand, W_i[r0 + 2s + h][e = l32], for the whole launch
+  float wa[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wa[s] = won ? G.W[((size_t)i * JD + r0 + 2 * s + h) * 32 + l32] : 0.f;
+  f16v agw;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) agw[r] = 0.f;
+  float sb = 0.f;
+  float* tw = tT + wv * 32 * kGxwTS;
+  float* pw = part + wv * 32 * kGxwPS;
+  for (int f0 = 0, par = 0; f0 < Q; f0 += 32, par ^= 1) {
+    long long* fi = finfo + par * 64;   // double-buffered: the previous tile's atomics may still read it
+    if (tid < 32) {
+      const int q = f0 + tid;
+      int b, t;
+      fm.frame(min(q, Q - 1), b, t);
+      const int ts = t + w - lpad;
+      fi[tid] = q < Q ? (long long)(fm.view(b, t) * in_n + i) * JD : -1;
+      fi[32 + tid] = (q < Q && ts >= 0 && ts < fm.T) ? ((long long)(b * fm.T + ts) * N + n) * 32 : -1;
+    }
+    __syncthreads();
+    // gu of frames f0 + 2s + h at the wave's rows (A of gW), x of the same frames (B)
+    float a[16], xb[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const long long go = fi[2 * s + h], xo = fi[32 + 2 * s + h];
+      a[s] = (won && go >= 0) ? G.gu[go + r0 + l32] : 0.f;
+      xb[s] = xo >= 0 ? G.emb[xo + l32] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      sb += a[s];
+      agw = mfma32x32x2(a[s], xb[s], agw);
+      tw[(2 * s + h) * kGxwTS + l32] = a[s];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f16v agx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) agx[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) agx = mfma32x32x2(wa[s], tw[l32 * kGxwTS + 2 * s + h], agx);
+    // agx: C[m = e][n = f]: lane (f = l32, h), reg r -> e = mfma32_row(r, h)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pw[l32 * kGxwPS + mfma32_row(r, h)] = agx[r];
+    __syncthreads();
+    {
+      const int f = tid >> 5, e = tid & 31;
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < kGxwWaves; ++k) v += part[(k * 32 + f) * kGxwPS + e];
+      const long long xo = fi[32 + f];
+      if (xo >= 0) atomicAdd(G.g_emb + xo + e, v);
+    }
+  }
+  sb += __shfl_xor(sb, 32, 64);
+  if (!won) return;
+  if (h == 0) {
+    float* gb = G.gbias + (size_t)i * JD + r0 + l32;
+    *gb = G.acc ? *gb + sb : sb;
+  }
+  // agw: C[m = row][n = e]: lane (e = l32, h), reg r -> row r0 + mfma32_row(r, h)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float* dst = G.gW + ((size_t)i * JD + r0 + mfma32_row(r, h)) * 32 + l32;
+    *dst = G.acc ? *dst + agw[r] : agw[r];
+  }
+}
+
 // ---- fp8 pose (opt-in, BASELINE C5 "fp8 pose-transform MFMA"): OCP e4m3 operands on
 // v_mfma_f32_32x32x16_fp8_fp8, fp32 accumulation.  Every frame's x_i(f) and every row
 // of W_i gets its own power-of-two scale 2^e with max|a 2^e| in (224, 448] (e4m3's
@@ -887,7 +1004,7 @@ __global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int 
 // 1228 vs 1174, gW 937 vs 1073; C3 din 32 pose 46 vs 33, gx 47 vs 53, gW 91 vs 65.
 enum class SdrGemm { kPose, kGx, kGw };
 #ifndef SRF_SDR_MFMA32_DIN32
-#define SRF_SDR_MFMA32_DIN32 2   // bit 0 pose, bit 1 gx, bit 2 gW: the 32x32 kernels at din 32
+#define SRF_SDR_MFMA32_DIN32 3   // bit 0 pose, bit 1 gx, bit 2 gW: the 32x32 kernels at din 32 (r04q: pose + gx)
 #endif
 bool use_mfma32(int din, int JD, SdrGemm k) {
   if ((din != 32 && din != 64) || JD % 8) return false;
@@ -1084,6 +1201,23 @@ int gx_range(const SGeom& g, const float* gu, const float* WT, const FrameMap& f
   it.it[0] = GemmItem{gu, WT, nullptr, g_emb, nullptr, 0, g.B * fm.nt, fm};
   it.n = 1;
   return gx_n(g, it, st);
+}
+
+// gx + gW of din-32 layers in one launch (sdr_gxw32_kernel); false: not this shape
+bool gxw_supported(const SGeom& g) { return g.din == 32 && g.JD() % 32 == 0; }
+
+int gxw_n(const SGeom& g, const GxwItems& it, hipStream_t st) {
+  if (it.n == 0) return SRF_OK;
+  static bool attr = false;   // one-time raise of the kernel's LDS limit (above 64 KiB)
+  if (!attr) {
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)sdr_gxw32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kGxwLds));
+    attr = true;
+  }
+  const dim3 grid((g.JD() + kGxwRows - 1) / kGxwRows, g.in_n(), it.n);
+  hipLaunchKernelGGL(sdr_gxw32_kernel, grid, dim3(64 * kGxwWaves), kGxwLds, st, it, g.N, g.lpad, g.in_n(), g.JD());
+  SRF_LAUNCH_CHECK("sdr_gxw32");
+  return SRF_OK;
 }
 
 // items with Q == 0 still run when they start the accumulation (acc == 0: zeros)
@@ -1420,6 +1554,25 @@ int srf_route_sdr_gw(const float* gu, int g0, int gn, const float* emb, int B, i
   r.t0 = t0, r.t1 = t1, r.gu = const_cast<float*>(gu), r.g0 = g0, r.gn = gn, r.emb = emb, r.g_W = g_W;
   r.g_bias = g_bias, r.accumulate = accumulate;
   return srf_route_sdr_gw_n(&r, 1, B, T, N, din, lpad, rpad, J, dout, stream);
+}
+
+int srf_route_sdr_gx_gw_n(const srf_sdr_range* r, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                          int dout, void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, 1, 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = items_ok(g, r, n, false, true))) return rc;
+  if (!gxw_supported(g)) {   // the two contractions' own kernels
+    if ((rc = srf_route_sdr_gx_n(r, n, B, T, N, din, lpad, rpad, J, dout, stream))) return rc;
+    return srf_route_sdr_gw_n(r, n, B, T, N, din, lpad, rpad, J, dout, stream);
+  }
+  GxwItems it{};
+  for (int k = 0; k < n; ++k) {
+    if (r[k].t0 >= r[k].t1 && r[k].accumulate) continue;   // an empty range still starts the sum
+    SRF_REQUIRE(r[k].gu && r[k].W && r[k].emb && r[k].g_emb && r[k].g_W && r[k].g_bias, "null pointer argument");
+    it.it[it.n++] = GxwItem{r[k].gu, r[k].W, r[k].emb, r[k].g_emb, r[k].g_W, r[k].g_bias, r[k].accumulate,
+                            B * std::max(0, r[k].t1 - r[k].t0), frame_map(T, r[k].t0, r[k].t1, r[k].g0, r[k].gn)};
+  }
+  return gxw_n(g, it, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

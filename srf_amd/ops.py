@@ -566,6 +566,11 @@ def _sdr_r(**kw):
     return r
 
 
+# din-32 SDR layers: gx and gW in one launch that reads gu once (srf_route_sdr_gx_gw_n);
+# False runs the two contractions' own launches (bench --sdr-separate-gxgw, for A/B)
+SDR_FUSED_GXGW = True
+
+
 def _sdr_call(fn, ranges, *args, what):
     """fn(ranges, n, *args) for up to SDR_MAX_ITEMS ranges per launch."""
     for c in range(0, len(ranges), _lib.SDR_MAX_ITEMS):
@@ -762,16 +767,20 @@ class SdrStack(torch.autograd.Function):
                                                          _ptr(betas[l]), tr, p_mid, seed, l, _ptr(stats[l]),
                                                          _ptr(g_embs[l + 1]), _ptr(g_vs[l]), _ptr(gparts[l]), sp),
                                'capsnorm_bwd_range')
+            fused = gw and din == 32 and SDR_FUSED_GXGW   # gx + gW in one pass over gu
             if live:
                 if not store:
                     _sdr_call(L_.srf_route_sdr_pose_n, live, B, T, N, din, P.lpad, P.rpad, J, D, P.pose_mode(ls[0]),
                               sp, what='sdr_pose_n')
                 _sdr_call(L_.srf_route_sdr_recur_bwd_n, live, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
                           what='sdr_recur_bwd_n')
-                _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')
+                if not fused:
+                    _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')
+            if fused:
+                _sdr_call(L_.srf_route_sdr_gx_gw_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_gw_n')
             if ev is not None:
                 ev.record(sa if sp is pa else sb)
-            if gw:
+            if gw and not fused:
                 gw_ranges(sp, ls, ks)
             for l, k in zip(ls, ks):
                 if k == 0 and l < L - 1:

@@ -359,3 +359,47 @@ def test_sdr_groups_match_one_workgroup(cuda, J, D, iters, mf, N, lp, rp):
         for name, a, b in zip(('v', 'cs', 'gu', 'carry', 'v2'), outs[0][1:], got):
             err, mag = (a - b).abs().max().item(), a.abs().max().item()
             assert err <= 1e-5 * mag + 1e-7, (G, name, err, mag)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('J,N,lp,rp', [(16, 16, 2, 2), (32, 16, 2, 2), (8, 3, 1, 1)])
+def test_sdr_gx_gw_fused_matches_separate(cuda, J, N, lp, rp):
+    """srf_route_sdr_gx_gw_n (din 32: one pass over gu, sdr_gxw32_kernel) computes what
+    srf_route_sdr_gx_n + srf_route_sdr_gw_n compute on the same ranges: g_emb through the
+    window adjoint (added), gW / gbias overwritten by a range with accumulate == 0
+    (also an empty one) and added by the next; C3's inner and last layer shapes and one
+    with idle waves (J*dout = 256 < 512 rows per workgroup).  Both sum in fp32 in
+    different orders (and g_emb by atomics): 1e-5 of each output's magnitude."""
+    import ctypes
+    from srf_amd import _lib
+    L = _lib.lib()
+    din, D, B, T = 32, 32, 3, 9
+    in_n, JD = N * (lp + rp + 1), J * D
+    g = torch.Generator().manual_seed(11)
+    emb = torch.randn(B, T, N, din, generator=g).to(cuda)
+    W = (torch.randn(in_n, JD, din, generator=g) * 0.1).to(cuda)
+    WT = W.permute(0, 2, 1).contiguous()
+    gu = torch.randn(B * T * in_n * JD, generator=g).to(cuda)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    init_W, init_b = torch.randn(in_n, JD, din, generator=g).to(cuda), torch.randn(in_n, JD, generator=g).to(cuda)
+    outs = []
+    for fused in (False, True):
+        g_emb = torch.zeros_like(emb)
+        gW, gb = init_W.clone(), init_b.clone()
+        for t0, t1, acc in ((0, 0, 0), (0, 4, 1), (4, 9, 1), (9, 9, 1)):
+            r = _lib.SdrRange(t0=t0, t1=t1, emb=p(emb), W=p(W), WT=p(WT), gu=p(gu), g0=0, gn=T, g_emb=p(g_emb),
+                              g_W=p(gW), g_bias=p(gb), accumulate=acc)
+            rr = (_lib.SdrRange * 1)(r)
+            args = (rr, 1, B, T, N, din, lp, rp, J, D, st)
+            if fused:
+                _lib.check(L.srf_route_sdr_gx_gw_n(*args), 'gx_gw_n')
+            else:
+                if t1 > t0:
+                    _lib.check(L.srf_route_sdr_gx_n(*args), 'gx_n')
+                _lib.check(L.srf_route_sdr_gw_n(*args), 'gw_n')
+        torch.cuda.synchronize()
+        outs.append((g_emb, gW, gb))
+    for name, a, b in zip(('g_emb', 'gW', 'gbias'), *outs):
+        err, mag = (a - b).abs().max().item(), a.abs().max().item()
+        assert mag > 0 and err <= 1e-5 * mag, (name, err, mag)
