@@ -238,6 +238,9 @@ def measure(workload, args, world, rank, dev):
     if args.sdr_separate_gxgw:
         from srf_amd import ops
         ops.SDR_FUSED_GXGW = False
+    if args.sdr_capsnorm_per_layer:
+        from srf_amd import ops
+        ops.SDR_CAPSNORM_BATCHED = False
     if args.sdr_last_group is not None:
         g = [int(x) for x in args.sdr_last_group.split(',')]
         model.sdr_options['last_group'] = (g[0], g[-1])
@@ -385,6 +388,8 @@ def main():
                          '"G_forward,G_backward" (default: SdrStackPlan.group)')
     ap.add_argument('--sdr-separate-gxgw', action='store_true',
                     help='SDR stack: the gx and gW launches of din-32 layers separately (default: fused)')
+    ap.add_argument('--sdr-capsnorm-per-layer', action='store_true',
+                    help='SDR stack: one LN/dropout launch per inner layer and range (default: one per diagonal)')
     ap.add_argument('--eager', action='store_true', help='launch every kernel from Python each step (no hipGraph)')
     args = ap.parse_args()
 

@@ -26,6 +26,17 @@ class SdrRange(ctypes.Structure):
 
 _ranges = ctypes.POINTER(SdrRange)
 
+CAPSNORM_MAX_ITEMS = 8   # SRF_CAPSNORM_MAX_ITEMS
+
+
+class CapsnormRange(ctypes.Structure):
+    """srf_capsnorm_range: one layer's frame range for srf_capsnorm_{fwd,bwd}_range_n."""
+    _fields_ = [('t0', _c_int), ('t1', _c_int), ('layer', _c_int), ('x', _vp), ('gamma', _vp), ('beta', _vp),
+                ('y', _vp), ('stat', _vp), ('g_y', _vp), ('g_x', _vp), ('gpart', _vp)]
+
+
+_cn_ranges = ctypes.POINTER(CapsnormRange)
+
 # name -> (restype, argtypes); mirrors include/srf.h one to one.
 _SIGNATURES = {
     'srf_version': (_c_int, []),
@@ -92,6 +103,8 @@ _SIGNATURES = {
                                   _vp, _vp, _vp]),
     'srf_capsnorm_bwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong, _c_int]
                          + [_vp] * 6 + [_c_size, _vp]),
+    'srf_capsnorm_fwd_range_n': (_c_int, [_cn_ranges] + [_c_int] * 5 + [ctypes.c_float, ctypes.c_ulonglong, _vp]),
+    'srf_capsnorm_bwd_range_n': (_c_int, [_cn_ranges] + [_c_int] * 5 + [ctypes.c_float, ctypes.c_ulonglong, _vp]),
     'srf_capsnorm_fwd_range': (_c_int, [_vp] + [_c_int] * 5 + [_vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong,
                                                              _c_int, _vp, _vp, _vp]),
     'srf_capsnorm_bwd_range': (_c_int, [_vp] + [_c_int] * 5 + [_vp, _vp, _c_int, ctypes.c_float, ctypes.c_ulonglong,

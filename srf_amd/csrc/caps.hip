@@ -524,20 +524,17 @@ struct RowMap {
 
 // y = drop(LN(x)) over vectors of length n (one frame per workgroup); also the
 // output head: logits = LN_out(length_D(drop(LN_mid(v)))) when head != 0.
-__global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restrict__ x, int n,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, int training, float p,
-                                                           unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream,
-                                                           float* __restrict__ y, float* __restrict__ stat, int head,
-                                                           int J, int D, const float* __restrict__ gamma_o,
-                                                           const float* __restrict__ beta_o,
-                                                           float* __restrict__ logits, float* __restrict__ lens,
-                                                           float len_eps, RowMap rmap) {
+__device__ __forceinline__ void capsnorm_fwd_row(const float* __restrict__ x, int n, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, int training, float p,
+                                                 unsigned long long seed, const unsigned long long* __restrict__ seed_src,
+                                                 unsigned stream, float* __restrict__ y, float* __restrict__ stat,
+                                                 int head, int J, int D, const float* __restrict__ gamma_o,
+                                                 const float* __restrict__ beta_o, float* __restrict__ logits,
+                                                 float* __restrict__ lens, float len_eps, int f) {
   seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* v = sm;           // n
   float* red = v + n;      // 8
-  const int f = rmap.row(blockIdx.x);
   float s1 = 0.f, dummy = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const float a = x[(size_t)f * n + i];
@@ -597,17 +594,17 @@ __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(const float* __restri
 // head: gpart[f][2n..2n+J) g_gamma_out, [2n+J..2n+2J) g_beta_out.
 //   head: o = drop(LN_mid(x)), L_j = sqrt(|o_j|^2 + eps), logits = LN_out(L)
 //         g_o = g_L_j * o / L_j (naive:255-258)
-__global__ __launch_bounds__(256) void capsnorm_bwd_kernel(
+__device__ __forceinline__ void capsnorm_bwd_row(
     const float* __restrict__ x, int n, const float* __restrict__ gamma, const float* __restrict__ beta,
-    int training, float p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream, const float* __restrict__ stat,
-    const float* __restrict__ g_in, int head, int J, int D, const float* __restrict__ gamma_o,
-    const float* __restrict__ lens, float* __restrict__ g_x, float* __restrict__ gpart, RowMap rmap) {
+    int training, float p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream,
+    const float* __restrict__ stat, const float* __restrict__ g_in, int head, int J, int D,
+    const float* __restrict__ gamma_o, const float* __restrict__ lens, float* __restrict__ g_x,
+    float* __restrict__ gpart, int f) {
   seed = srf_step_seed(seed, seed_src);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* gy = sm;          // n
   float* red = gy + n;     // 8
   float* gl = red + 8;     // J
-  const int f = rmap.row(blockIdx.x);
   const float mean = stat[4 * f], rstd = stat[4 * f + 1];
   const size_t stride = head ? (size_t)2 * n + 2 * J : (size_t)2 * n;
   if (head) {
@@ -656,6 +653,50 @@ __global__ __launch_bounds__(256) void capsnorm_bwd_kernel(
     const float xh = (x[gi] - mean) * rstd;
     g_x[gi] = rstd * (gy[i] - a1 / n - xh * a2 / n);
   }
+}
+
+__global__ __launch_bounds__(256) void capsnorm_fwd_kernel(
+    const float* __restrict__ x, int n, const float* __restrict__ gamma, const float* __restrict__ beta, int training,
+    float p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream,
+    float* __restrict__ y, float* __restrict__ stat, int head, int J, int D, const float* __restrict__ gamma_o,
+    const float* __restrict__ beta_o, float* __restrict__ logits, float* __restrict__ lens, float len_eps,
+    RowMap rmap) {
+  capsnorm_fwd_row(x, n, gamma, beta, training, p, seed, seed_src, stream, y, stat, head, J, D, gamma_o, beta_o,
+                   logits, lens, len_eps, rmap.row(blockIdx.x));
+}
+
+__global__ __launch_bounds__(256) void capsnorm_bwd_kernel(
+    const float* __restrict__ x, int n, const float* __restrict__ gamma, const float* __restrict__ beta, int training,
+    float p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream,
+    const float* __restrict__ stat, const float* __restrict__ g_in, int head, int J, int D,
+    const float* __restrict__ gamma_o, const float* __restrict__ lens, float* __restrict__ g_x,
+    float* __restrict__ gpart, RowMap rmap) {
+  capsnorm_bwd_row(x, n, gamma, beta, training, p, seed, seed_src, stream, stat, g_in, head, J, D, gamma_o, lens, g_x,
+                   gpart, rmap.row(blockIdx.x));
+}
+
+// The frame ranges of several same-width layers in one launch (grid.y = range): the
+// layer-pipelined SDR stack's inner layers, one anti-diagonal at a time.
+struct CnItems {
+  srf_capsnorm_range it[SRF_CAPSNORM_MAX_ITEMS];
+  int B, T, n_items;
+};
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void capsnorm_range_n_kernel(CnItems items, int n, int training, float p,
+                                                               unsigned long long seed,
+                                                               const unsigned long long* __restrict__ seed_src) {
+  const srf_capsnorm_range& r = items.it[blockIdx.y];
+  const int nt = r.t1 - r.t0;
+  if ((int)blockIdx.x >= items.B * nt) return;
+  const int f = RowMap{items.T, r.t0, nt}.row(blockIdx.x);
+  const unsigned stream = (unsigned)(kStreamMid0 + r.layer);
+  if constexpr (BWD)
+    capsnorm_bwd_row(r.x, n, r.gamma, r.beta, training, p, seed, seed_src, stream, r.stat, r.g_y, 0, 0, 0, nullptr,
+                     nullptr, r.g_x, r.gpart, f);
+  else
+    capsnorm_fwd_row(r.x, n, r.gamma, r.beta, training, p, seed, seed_src, stream, r.y, r.stat, 0, 0, 0, nullptr,
+                     nullptr, nullptr, nullptr, kLengthEps, f);
 }
 
 // ---------------------------------------------------------------- host
@@ -903,6 +944,44 @@ int srf_capsnorm_bwd_range(const float* x, int B, int T, int t0, int t1, int n, 
                      g_x, gpart, RowMap{T, t0, t1 - t0});
   SRF_LAUNCH_CHECK("capsnorm_bwd_range");
   return SRF_OK;
+}
+
+static int capsnorm_range_n(const srf_capsnorm_range* r, int n_items, int B, int T, int n, int training, float p,
+                             unsigned long long seed, void* stream, bool bwd) {
+  SRF_REQUIRE(r && n_items >= 0 && n_items <= SRF_CAPSNORM_MAX_ITEMS && B > 0 && T > 0 && n > 0 && n <= kMaxVec,
+              "bad capsnorm range_n arguments");
+  CnItems it{};
+  it.B = B, it.T = T;
+  int rows = 0;
+  for (int k = 0; k < n_items; ++k) {
+    const srf_capsnorm_range& q = r[k];
+    SRF_REQUIRE(0 <= q.t0 && q.t0 <= q.t1 && q.t1 <= T, "capsnorm range [%d, %d) outside [0, %d)", q.t0, q.t1, T);
+    if (q.t0 == q.t1) continue;
+    SRF_REQUIRE(q.x && q.gamma && q.beta && q.stat && (bwd ? (q.g_y && q.g_x && q.gpart) : q.y != nullptr),
+                "null pointer argument");
+    it.it[it.n_items++] = q;
+    rows = std::max(rows, B * (q.t1 - q.t0));
+  }
+  if (it.n_items == 0) return SRF_OK;
+  const dim3 grid(rows, it.n_items);
+  if (bwd)
+    hipLaunchKernelGGL(capsnorm_range_n_kernel<true>, grid, dim3(256), (size_t)(n + 8) * 4,
+                       static_cast<hipStream_t>(stream), it, n, training, p, seed, srf::seed_source());
+  else
+    hipLaunchKernelGGL(capsnorm_range_n_kernel<false>, grid, dim3(256), (size_t)(n + 8) * 4,
+                       static_cast<hipStream_t>(stream), it, n, training, p, seed, srf::seed_source());
+  SRF_LAUNCH_CHECK("capsnorm_range_n");
+  return SRF_OK;
+}
+
+int srf_capsnorm_fwd_range_n(const srf_capsnorm_range* r, int n_items, int B, int T, int n, int training, float p,
+                             unsigned long long seed, void* stream) {
+  return capsnorm_range_n(r, n_items, B, T, n, training, p, seed, stream, false);
+}
+
+int srf_capsnorm_bwd_range_n(const srf_capsnorm_range* r, int n_items, int B, int T, int n, int training, float p,
+                             unsigned long long seed, void* stream) {
+  return capsnorm_range_n(r, n_items, B, T, n, training, p, seed, stream, true);
 }
 
 size_t srf_capsnorm_params_workspace(int F, int n) { return srf::colsum_scratch_floats(F, 2 * n) * 4; }

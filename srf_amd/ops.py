@@ -566,9 +566,19 @@ def _sdr_r(**kw):
     return r
 
 
+def _cn_call(fn, ranges, *args, what):
+    """fn(ranges, n, *args) for up to CAPSNORM_MAX_ITEMS capsnorm ranges per launch."""
+    for c in range(0, len(ranges), _lib.CAPSNORM_MAX_ITEMS):
+        part = ranges[c:c + _lib.CAPSNORM_MAX_ITEMS]
+        _lib.check(fn((_lib.CapsnormRange * len(part))(*part), len(part), *args), what)
+
+
 # din-32 SDR layers: gx and gW in one launch that reads gu once (srf_route_sdr_gx_gw_n);
 # False runs the two contractions' own launches (bench --sdr-separate-gxgw, for A/B)
 SDR_FUSED_GXGW = True
+# the inner layers' LN + dropout of one anti-diagonal in one launch (srf_capsnorm_*_range_n);
+# False: one launch per layer (bench --sdr-capsnorm-per-layer, for A/B)
+SDR_CAPSNORM_BATCHED = True
 
 
 def _sdr_call(fn, ranges, *args, what):
@@ -662,11 +672,14 @@ class SdrStack(torch.autograd.Function):
             if tm:
                 ev1.record(sb)
                 timing.append((ev0, ev1, B * sum(r.t1 - r.t0 for r in rr)))
-            for l, r in zip(ls, rr):
-                if l < L - 1:
-                    _lib.check(L_.srf_capsnorm_fwd_range(_ptr(vs[l]), B, T, r.t0, r.t1, J * D, _ptr(gammas[l]),
-                                                         _ptr(betas[l]), tr, float(p_mid), int(seed), l,
-                                                         _ptr(embs[l + 1]), _ptr(stats[l]), sp), 'capsnorm_range')
+            # LN + dropout of the inner layers' ranges, one launch
+            cn = [_lib.CapsnormRange(t0=r.t0, t1=r.t1, layer=l, x=_ptr(vs[l]), gamma=_ptr(gammas[l]),
+                                     beta=_ptr(betas[l]), y=_ptr(embs[l + 1]), stat=_ptr(stats[l]))
+                  for l, r in zip(ls, rr) if l < L - 1]
+            for c in ([cn] if SDR_CAPSNORM_BATCHED else [[x] for x in cn]):
+                if c:
+                    _cn_call(L_.srf_capsnorm_fwd_range_n, c, B, T, J * D, tr, float(p_mid), int(seed), sp,
+                             what='capsnorm_fwd_range_n')
 
         for d in range(P.K + L - 1):
             # inner layers: diagonal d on stream A, grouped by layer shape
@@ -761,12 +774,14 @@ class SdrStack(torch.autograd.Function):
             N, din, J, D, mf = P.layers[ls[0]]
             rr = [item(l, k) for l, k in zip(ls, ks)]
             live = [r for r in rr if r.t1 > r.t0]
-            for l, r in zip(ls, rr):
-                if l < L - 1 and r.t1 > r.t0:
-                    _lib.check(L_.srf_capsnorm_bwd_range(_ptr(vs[l]), B, T, r.t0, r.t1, J * D, _ptr(gammas[l]),
-                                                         _ptr(betas[l]), tr, p_mid, seed, l, _ptr(stats[l]),
-                                                         _ptr(g_embs[l + 1]), _ptr(g_vs[l]), _ptr(gparts[l]), sp),
-                               'capsnorm_bwd_range')
+            cn = [_lib.CapsnormRange(t0=r.t0, t1=r.t1, layer=l, x=_ptr(vs[l]), gamma=_ptr(gammas[l]),
+                                     beta=_ptr(betas[l]), stat=_ptr(stats[l]), g_y=_ptr(g_embs[l + 1]),
+                                     g_x=_ptr(g_vs[l]), gpart=_ptr(gparts[l]))
+                  for l, r in zip(ls, rr) if l < L - 1 and r.t1 > r.t0]
+            for c in ([cn] if SDR_CAPSNORM_BATCHED else [[x] for x in cn]):
+                if c:   # LN + dropout backward of the inner layers' ranges, one launch
+                    _cn_call(L_.srf_capsnorm_bwd_range_n, c, B, T, J * D, tr, float(p_mid), int(seed), sp,
+                             what='capsnorm_bwd_range_n')
             fused = gw and din == 32 and SDR_FUSED_GXGW   # gx + gW in one pass over gu
             if live:
                 if not store:
