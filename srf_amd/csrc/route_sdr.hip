@@ -770,13 +770,17 @@ struct GxwItems {
   GxwItem it[srf::kMaxItems];
   int n;
 };
-constexpr int kGxwWaves = 16;
+#ifndef SRF_GXW_WAVES
+#define SRF_GXW_WAVES 16
+#endif
+constexpr int kGxwWaves = SRF_GXW_WAVES;
+constexpr int kGxwThreads = 64 * kGxwWaves;
 constexpr int kGxwRows = 32 * kGxwWaves;   // rows per workgroup
 constexpr int kGxwTS = 34;                 // row stride of a wave's transposed tile
 constexpr int kGxwPS = 33;                 // row stride of a wave's gx part
 constexpr size_t kGxwLds = (size_t)kGxwWaves * 32 * (kGxwTS + kGxwPS) * sizeof(float) + 2 * 2 * 32 * sizeof(long long);
 
-__global__ __launch_bounds__(1024) void sdr_gxw32_kernel(GxwItems items, int N, int lpad, int in_n, int JD) {
+__global__ __launch_bounds__(kGxwThreads) void sdr_gxw32_kernel(GxwItems items, int N, int lpad, int in_n, int JD) {
   const GxwItem& G = items.it[blockIdx.z];
   const int Q = G.Q;
   const FrameMap fm = G.fm;
@@ -837,8 +841,8 @@ __global__ __launch_bounds__(1024) void sdr_gxw32_kernel(GxwItems items, int N, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) pw[l32 * kGxwPS + mfma32_row(r, h)] = agx[r];
     __syncthreads();
-    {
-      const int f = tid >> 5, e = tid & 31;
+    for (int el = tid; el < 32 * 32; el += kGxwThreads) {
+      const int f = el >> 5, e = el & 31;
       float v = 0.f;
 #pragma unroll
       for (int k = 0; k < kGxwWaves; ++k) v += part[(k * 32 + f) * kGxwPS + e];
@@ -1215,7 +1219,7 @@ int gxw_n(const SGeom& g, const GxwItems& it, hipStream_t st) {
     attr = true;
   }
   const dim3 grid((g.JD() + kGxwRows - 1) / kGxwRows, g.in_n(), it.n);
-  hipLaunchKernelGGL(sdr_gxw32_kernel, grid, dim3(64 * kGxwWaves), kGxwLds, st, it, g.N, g.lpad, g.in_n(), g.JD());
+  hipLaunchKernelGGL(sdr_gxw32_kernel, grid, dim3(kGxwThreads), kGxwLds, st, it, g.N, g.lpad, g.in_n(), g.JD());
   SRF_LAUNCH_CHECK("sdr_gxw32");
   return SRF_OK;
 }
