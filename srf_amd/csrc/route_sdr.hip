@@ -608,6 +608,121 @@ __global__ __launch_bounds__(256, 2) void sdr_pose32_kernel(GemmItems items, int
     }
 }
 
+// The same pose on v_mfma_f32_32x32x16_bf16 with every fp32 operand split into three
+// bf16 terms by truncation (a = t1 + t2 + t3 + e, each residual exact in fp32, |e| <
+// 2^-24 |a| in the normal range): six products per 16-wide K step (t1 t1, t1 t2, t2 t1,
+// t1 t3, t2 t2, t3 t1; the dropped ones are below 2^-24 of |W x|), fp32 accumulation,
+// the bias in the accumulator's start as before.  Same tiles and lane maps as
+// sdr_pose32_kernel; lane half h holds k = 16 s + 8 h .. + 7 of K step s on both operands.
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3_bf16(const f4& p, const f4& q, bf8 (&t)[3]) {
+  const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+  unsigned h[3][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const unsigned u = __float_as_uint(v[k]);
+    h[0][k] = u & 0xFFFF0000u;
+    const float r1 = v[k] - __uint_as_float(h[0][k]);
+    h[1][k] = __float_as_uint(r1) & 0xFFFF0000u;
+    const float r2 = r1 - __uint_as_float(h[1][k]);
+    h[2][k] = __float_as_uint(r2);
+  }
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    u4v w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_perm(h[m][2 * j + 1], h[m][2 * j], 0x07060302u);
+    t[m] = __builtin_bit_cast(bf8, w);
+  }
+}
+
+__device__ __forceinline__ f16v mfma32bf(const bf8& a, const bf8& b, const f16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int DIN>
+__global__ __launch_bounds__(256, 2) void sdr_pose3b_kernel(GemmItems items, int N, int lpad, int in_n, int JD,
+                                                            int nrb) {
+  const GemmItem& G = items.it[blockIdx.z];
+  const float* __restrict__ emb = G.x;
+  const float* __restrict__ W = G.w;
+  const float* __restrict__ bias = G.b;
+  float* __restrict__ u = G.o;
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  if ((int)(blockIdx.x / nrb) * 128 >= Q) return;
+  constexpr int KS = DIN / 16;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int i = blockIdx.y;
+  const int rb = blockIdx.x % nrb, fb = blockIdx.x / nrb;
+  const int w = i / N, n = i - w * N;
+  const int f0 = fb * 128 + (wv & 1) * 64, r0 = rb * 128 + (wv >> 1) * 64;
+  bf8 xa[2][KS][3];
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft) {
+    const int q = f0 + ft * 32 + l32;
+    int b, t;
+    fm.frame(min(q, Q - 1), b, t);
+    const int ts = t + w - lpad;
+    const bool ok = q < Q && ts >= 0 && ts < fm.T;
+    const float* xp = emb + ((size_t)(b * fm.T + min(max(ts, 0), fm.T - 1)) * N + n) * DIN + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      f4 p = {0.f, 0.f, 0.f, 0.f}, pq = {0.f, 0.f, 0.f, 0.f};
+      if (ok) {
+        p = *reinterpret_cast<const f4*>(xp + 16 * s);
+        pq = *reinterpret_cast<const f4*>(xp + 16 * s + 4);
+      }
+      split3_bf16(p, pq, xa[ft][s]);
+    }
+  }
+  f16v acc[2][2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int row = min(r0 + rt * 32 + l32, JD - 1);
+    const float* wp = W + ((size_t)i * JD + row) * DIN + 8 * h;
+    const float bv = bias[(size_t)i * JD + row];
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ft][rt][r] = bv;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf8 wb[3];
+      split3_bf16(*reinterpret_cast<const f4*>(wp + 16 * s), *reinterpret_cast<const f4*>(wp + 16 * s + 4), wb);
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft) {
+        f16v c = acc[ft][rt];
+        c = mfma32bf(xa[ft][s][2], wb[0], c);   // smallest terms first
+        c = mfma32bf(xa[ft][s][1], wb[1], c);
+        c = mfma32bf(xa[ft][s][0], wb[2], c);
+        c = mfma32bf(xa[ft][s][1], wb[0], c);
+        c = mfma32bf(xa[ft][s][0], wb[1], c);
+        c = mfma32bf(xa[ft][s][0], wb[0], c);
+        acc[ft][rt] = c;
+      }
+    }
+  }
+#pragma unroll
+  for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = f0 + ft * 32 + mfma32_row(r, h);
+      if (q >= Q) continue;
+      int b, t;
+      fm.frame(q, b, t);
+      float* up = u + (fm.view(b, t) * in_n + i) * JD;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int row = r0 + rt * 32 + l32;
+        if (row < JD) up[row] = acc[ft][rt][r];
+      }
+    }
+}
+
 // gx_i(f)[e] = sum_row gu[f][i][row] W_i[row][e], added into g_emb through the window
 // adjoint.  Workgroup = one capsule, 128 frames; wave = 32 frames x din (din/32 tiles);
 // K = JD in chunks of 64 (A = gu rows along k, B = W^T [i][e][row] along k), the next
@@ -1007,6 +1122,9 @@ __global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int 
 // one frame range alone on the GPU, us 32x32 vs 16x16): C5 din 64 pose 850 vs 973, gx
 // 1228 vs 1174, gW 937 vs 1073; C3 din 32 pose 46 vs 33, gx 47 vs 53, gW 91 vs 65.
 enum class SdrGemm { kPose, kGx, kGw };
+#ifndef SRF_SDR_POSE_BF3
+#define SRF_SDR_POSE_BF3 1   // din 32 / 64 fp32 pose on bf16 MFMA, three-term split operands
+#endif
 #ifndef SRF_SDR_MFMA32_DIN32
 #define SRF_SDR_MFMA32_DIN32 3   // bit 0 pose, bit 1 gx, bit 2 gW: the 32x32 kernels at din 32 (r04q: pose + gx)
 #endif
@@ -1068,6 +1186,14 @@ int pose_n(const SGeom& g, const GemmItems& it, hipStream_t st, int mode = 0) {
     }
 #undef SRF_POSE8
     SRF_LAUNCH_CHECK("sdr_pose8");
+    return SRF_OK;
+  }
+  if (SRF_SDR_POSE_BF3 && (g.din == 32 || g.din == 64) && g.JD() % 8 == 0) {
+    if (g.din == 32)
+      hipLaunchKernelGGL(sdr_pose3b_kernel<32>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
+    else
+      hipLaunchKernelGGL(sdr_pose3b_kernel<64>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
+    SRF_LAUNCH_CHECK("sdr_pose3b");
     return SRF_OK;
   }
   if (use_mfma32(g.din, g.JD(), SdrGemm::kPose)) {

@@ -403,3 +403,38 @@ def test_sdr_gx_gw_fused_matches_separate(cuda, J, N, lp, rp):
     for name, a, b in zip(('g_emb', 'gW', 'gbias'), *outs):
         err, mag = (a - b).abs().max().item(), a.abs().max().item()
         assert mag > 0 and err <= 1e-5 * mag, (name, err, mag)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('din,J,D', [(32, 16, 32), (32, 32, 32), (64, 16, 64)])
+def test_sdr_pose_fp32_accuracy(cuda, din, J, D):
+    """The fp32 pose (pose_n mode 0; din 32 / 64 on bf16 MFMA with three-term split
+    operands, sdr_pose3b_kernel) against u = W x + b in float64: fp32-level error,
+    |u - u64| <= 2^-18 (sum_k |W||x| + |b|) -- the accumulator starts at the bias and
+    each MFMA rounds the running sum in fp32 (a one-term bf16 split would miss the bound
+    by 2^10) -- with operands spanning 2^-20 .. 2^4, a zero frame and the window's edge
+    frames."""
+    import ctypes
+    from srf_amd import _lib
+    L = _lib.lib()
+    B, T, N, lp, rp = 2, 7, 3, 1, 2
+    in_n, JD = N * (lp + rp + 1), J * D
+    rng = np.random.default_rng(5)
+    emb = (rng.standard_normal((B, T, N, din)) * 2.0 ** rng.uniform(-20, 4, (B, T, N, 1))).astype(np.float32)
+    emb[0, 3] = 0.0
+    W = (rng.standard_normal((in_n, JD, din)) * 0.1 * 2.0 ** rng.uniform(-20, 4, (in_n, JD, 1))).astype(np.float32)
+    bias = (rng.standard_normal((in_n, JD)) * 0.1).astype(np.float32)
+    x = so.window(emb.astype(np.float64), lp, rp)                                   # [B, T, in_n, din]
+    ref = np.einsum('ijk,btik->btij', W.astype(np.float64), x) + bias.astype(np.float64)
+    mag = np.einsum('ijk,btik->btij', np.abs(W.astype(np.float64)), np.abs(x))
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    te, tW, tb = (torch.tensor(a, device=cuda) for a in (emb, W, bias))
+    u = torch.full((B * T * in_n * JD,), float('nan'), device=cuda)
+    r = _lib.SdrRange(t0=0, t1=T, emb=p(te), W=p(tW), bias=p(tb), u=p(u), v0=0, vn=T)
+    _lib.check(L.srf_route_sdr_pose_n((_lib.SdrRange * 1)(r), 1, B, T, N, din, lp, rp, J, D, 0, st), 'pose')
+    torch.cuda.synchronize()
+    got = u.double().cpu().numpy().reshape(B, T, in_n, JD)
+    err = np.abs(got - ref)
+    tol = 2.0 ** -18 * (mag + np.abs(bias.astype(np.float64)))
+    assert np.all(err <= tol), ((err - tol).max(), np.argwhere(err > tol)[:4].tolist())
