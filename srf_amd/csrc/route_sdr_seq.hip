@@ -45,7 +45,17 @@ constexpr unsigned long long* g_stamps = nullptr;
 // LDS: w [JP * D] (agreement input of the iteration: v_{t-1} at r = 0, then v^{r-1};
 // the padded capsules' tail zero), part [16][JD].  GRP: X.G workgroups per utterance split its input capsules
 // (srf_group.h); member 0 stores v and s^r, every member its own capsules' c^r.
-template <int D, int JP, int NIM, bool GRP>
+// KS > 0: the lane's last KS rows of frame t + 1 come through LDS, staged by
+// global_load_lds (no registers) while frame t computes -- one CU fetches its frame at
+// about 10 B/cycle, so the burst of loads at the frame's end is most of the frame; the
+// stage [KS][KD/4][16 waves][64 lanes][16 B] is written lane-linearly by each wave's DMA
+// and read back by the same lanes (a wave's own vmcnt orders it).
+__device__ __forceinline__ void glds16(const float* src, float* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <int D, int JP, int NIM, bool GRP, int KS = 0>
 __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems items, int T, int in_n, int J,
                                                                int iters, int mask_first, srf_grp::Grp X) {
   using C = Cfg<D, JP, NIM>;
@@ -59,6 +69,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
   constexpr int JDp = JP * D;
   float* wl = lds;
   float* part = lds + JDp;
+  float* stage = part + kWaves * JD;   // KS > 0
   const int tid = threadIdx.x;
   const int utt = GRP ? blockIdx.x / X.G : blockIdx.x;   // utterance
   const int gm = GRP ? blockIdx.x - utt * X.G : 0;       // member of its group
@@ -74,26 +85,89 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
   if (ev) wl[tid] = rg.t0 > 0 ? vo[(size_t)(rg.t0 - 1) * JD + tid] : 0.f;   // v_{t0-1} (v_{-1} = 0)
   zero_tail(wl, 1, JD, JDp);
   float ur[C::NIM][C::KD];
+  constexpr int KF = C::NIM - KS;   // rows from global memory into registers
+  constexpr int NC = C::KD / 4;
+  const int lane = tid & 63, wv = tid >> 6;
+  // DMA of the lane's rows KF.. of the frame at ut into the stage (absent rows read the
+  // frame's first row and are zeroed when taken)
+  auto stage_issue = [&](const float* ut) {
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int k = KF + kk;
+      const bool ok = L.jv && k < L.NI;
+      const float* src = ut + (ok ? (size_t)(L.g + k * C::G) * JD + L.eoff : 0);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) glds16(src + 4 * c, stage + ((kk * NC + c) * kWaves + wv) * 256);
+    }
+  };
+  auto stage_take = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA has landed
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int k = KF + kk;
+      const bool ok = L.jv && k < L.NI;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const f4 x = *reinterpret_cast<const f4*>(stage + (((kk * NC + c) * kWaves + wv) * 64 + lane) * 4);
+        ur[k][4 * c] = ok ? x.x : 0.f;
+        ur[k][4 * c + 1] = ok ? x.y : 0.f;
+        ur[k][4 * c + 2] = ok ? x.z : 0.f;
+        ur[k][4 * c + 3] = ok ? x.w : 0.f;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the next DMA overwrites it
+  };
+  auto& urf = *reinterpret_cast<float(*)[KF > 0 ? KF : 1][C::KD]>(&ur[0][0]);
+  // the iteration inlined twice (the last one unconditionally loading the next frame)
+  // where the registers allow; frames of more than 48 registers (the J = 32 last layer,
+  // at the 1024-thread limit of 128) keep one copy and branch around the loads
+  constexpr bool UNC = KS > 0 || C::NIM * C::KD <= 48;
+  // KS > 0: barriers without the vmcnt(0) of __syncthreads, so the next frames' loads and
+  // DMA stay in flight across them; LDS ordering by lgkmcnt(0) (global stores of this
+  // kernel are never read back by it)
+  auto bar = [&]() {
+    if constexpr (KS > 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
   load_frame<C>(ub + (size_t)(rg.t0 - rg.tu0) * ff, JD, L, ur);
+  if constexpr (KS > 0) stage_issue(ub + (size_t)(min(rg.t0 + 1, rg.t1 - 1) - rg.tu0) * ff);
   __syncthreads();
   SEQ_STAMP_DECL
   for (int t = rg.t0; t < rg.t1; ++t) {
     float b[C::NIM], c[C::NIM];
 #pragma unroll
     for (int k = 0; k < C::NIM; ++k) b[k] = 0.f;
-    for (int r = 0; r < iters; ++r) {
+#if SRF_SEQ_DBG == 1   // timing experiment: re-load the current (cache-hot) frame
+    const int tn = t;
+#else
+    const int tn = min(t + 1, rg.t1 - 1);   // the next frame (the range's last reloads itself)
+#endif
+    // one routing iteration; the last one also loads frame tn into the registers u_t
+    // leaves.  The loads are unconditional: a branch around them would merge the old and
+    // new registers and wait for the loads right there, instead of at their first use
+    // (iteration 0 of the next frame), past the barriers and the squash in between.
+    auto iteration = [&](int r, bool last) __attribute__((always_inline)) {
       float w[C::KD];
       lds_slice<C::KD>(wl, L.eoff, w);
       logits_softmax<C>(ur, w, L, b, c);
       row_partial<C>(c, ur, L, JD, part);
       if (cs) store_ij<C>(c, L, cs + ((size_t)utt * T + t) * csr + (size_t)r * in_n * JP);
-#if SRF_SEQ_DBG == 1   // timing experiment: re-load the current (cache-hot) frame
-      if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(t - rg.tu0) * ff, JD, L, ur);
-#else
-      if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(t + 1 - rg.tu0) * ff, JD, L, ur);   // u_t is dead
-#endif
+      if (last) {   // u_t is dead
+        if constexpr (KS > 0) {
+          stage_take();   // frame tn's staged rows (the wait covers only the DMA issued a frame ago)
+          load_rows<C, KF>(ub + (size_t)(tn - rg.tu0) * ff, JD, L, urf);
+          stage_issue(ub + (size_t)(min(tn + 1, rg.t1 - 1) - rg.tu0) * ff);
+        } else {
+          load_frame<C>(ub + (size_t)(tn - rg.tu0) * ff, JD, L, ur);
+        }
+      }
       SEQ_MARK(0);   // logits, softmax, row partials (+ next frame's loads issued)
-      __syncthreads();
+      bar();
       if constexpr (GRP) srf_grp::allreduce<kWaves, kThreads>(part, JD, I.ws, X, utt, gm, (t - rg.t0) * iters + r, tid);
       SEQ_MARK(1);
       if (owner_wave) {
@@ -102,14 +176,46 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
         if (ev) {
           wl[tid] = v;
           if (lead) {
-            if (r == iters - 1) vo[(size_t)t * JD + tid] = v;
+            if (last) vo[(size_t)t * JD + tid] = v;
             if (cs) cs[((size_t)utt * T + t) * csr + (size_t)iters * in_n * JP + r * JD + tid] = s;
           }
         }
       }
       SEQ_MARK(2);   // wave sums + squash (owner waves)
-      __syncthreads();
+      bar();
       SEQ_MARK(3);
+    };
+    if constexpr (UNC) {
+      for (int r = 0; r + 1 < iters; ++r) iteration(r, false);
+      iteration(iters - 1, true);
+    } else {   // one copy of the iteration (registers): the next frame's loads under a branch
+      for (int r = 0; r < iters; ++r) {
+        float w[C::KD];
+        lds_slice<C::KD>(wl, L.eoff, w);
+        logits_softmax<C>(ur, w, L, b, c);
+        row_partial<C>(c, ur, L, JD, part);
+        if (cs) store_ij<C>(c, L, cs + ((size_t)utt * T + t) * csr + (size_t)r * in_n * JP);
+        if (r == iters - 1 && t + 1 < rg.t1) load_frame<C>(ub + (size_t)(tn - rg.tu0) * ff, JD, L, ur);
+        SEQ_MARK(0);
+        bar();
+        if constexpr (GRP)
+          srf_grp::allreduce<kWaves, kThreads>(part, JD, I.ws, X, utt, gm, (t - rg.t0) * iters + r, tid);
+        SEQ_MARK(1);
+        if (owner_wave) {
+          const float s = ev ? (GRP ? part[tid] : sum_parts(part, JD, tid)) : 0.f;
+          const float v = squash_elem<D>(s);
+          if (ev) {
+            wl[tid] = v;
+            if (lead) {
+              if (r == iters - 1) vo[(size_t)t * JD + tid] = v;
+              if (cs) cs[((size_t)utt * T + t) * csr + (size_t)iters * in_n * JP + r * JD + tid] = s;
+            }
+          }
+        }
+        SEQ_MARK(2);
+        bar();
+        SEQ_MARK(3);
+      }
     }
   }
   SEQ_FLUSH(g_stamps);
@@ -119,9 +225,30 @@ size_t fwd_lds(int J, int D) {
   return ((size_t)pow2_at_least(J) * D + (size_t)kWaves * J * D) * sizeof(float);
 }
 
+#ifndef SRF_SEQ_STAGE
+#define SRF_SEQ_STAGE 1
+#endif
+// rows per lane staged through LDS (sdr_seq_fwd_kernel KS): the C3 inner layers, three of
+// five (96 KB beside w and the partials); the J = 32 last layer has no registers to spare
+// for the second copy of the iteration that keeps the loads unconditional
+constexpr int stage_rows(int D, int JP, int NIM) {
+  return (SRF_SEQ_STAGE && D == 32 && NIM == 5 && JP == 16) ? 3 : 0;
+}
+
 template <int D, int JP, int NIM>
 int launch_fwd(const srf::SeqItems& items, const srf_grp::Grp& X, int B, int T, int in_n, int J, int iters,
                int mask_first, hipStream_t st) {
+  constexpr int KS = stage_rows(D, JP, NIM);
+  if constexpr (KS > 0) {
+    const size_t lds = fwd_lds(J, D) + (size_t)KS * kThreads * seq_kd(D, JP) * sizeof(float);
+    if (X.G == 1 && lds <= 160 * 1024) {
+      auto k = sdr_seq_fwd_kernel<D, JP, NIM, false, KS>;
+      SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k, dim3(B, items.n), dim3(kThreads), lds, st, items, T, in_n, J, iters, mask_first, X);
+      SRF_LAUNCH_CHECK("sdr_seq_fwd");
+      return SRF_OK;
+    }
+  }
   const size_t lds = fwd_lds(J, D);
   auto k = X.G > 1 ? sdr_seq_fwd_kernel<D, JP, NIM, true> : sdr_seq_fwd_kernel<D, JP, NIM, false>;
   if (lds > 64 * 1024)
