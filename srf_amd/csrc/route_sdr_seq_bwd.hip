@@ -89,8 +89,22 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
   float sr[RM];        // s^r of the owned element
 #pragma unroll
   for (int r = 0; r < RM; ++r) sr[r] = 0.f;
-  load_rows<C, KRES>(ub + (size_t)(rg.t1 - 1 - rg.tu0) * ff, JD, L, ur);
+  if constexpr (!CS) load_rows<C, KRES>(ub + (size_t)(rg.t1 - 1 - rg.tu0) * ff, JD, L, ur);
   zero_tail(wl, 1 + 2 * RM, JD, JDa);   // w, Vc, gs are consecutive
+  // ungrouped: barriers that wait on LDS only (no global data is exchanged inside the
+  // kernel).  With CS the frame's rows of u are loaded right after its couplings are
+  // requested, unconditionally, and stay in flight through the s^r / Vc^r phase and its
+  // barriers to their first use in the adjoint (the group exchange drains all memory
+  // operations anyway)
+  auto bar = [&]() {
+    if constexpr (!GRP) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
   SEQ_STAMP_DECL
   for (int t = rg.t1 - 1; t >= rg.t0; --t) {
     const size_t f = f0 + t;
@@ -116,14 +130,18 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
           }
         }
       }
-      __syncthreads();   // Vc^0 (above) before the owner threads extend it
+      // s^r of the owned element before the rows of u: waiting for them then leaves
+      // the (younger) row loads in flight
+#pragma unroll
+      for (int r = 0; r < RM; ++r) sr[r] = (r < R && ev) ? rec[(size_t)R * P + r * JD + tid] : 0.f;
+      load_rows<C, KRES>(ub + (size_t)(t - rg.tu0) * ff, JD, L, ur);
+      bar();   // Vc^0 (above) before the owner threads extend it
       SEQ_MARK(0);       // v_{t-1}, g_v, c^r loads (+ the previous frame's barrier)
       if (owner_wave) {
 #pragma unroll
         for (int r = 0; r < RM; ++r) {
           if (r < R) {
-            const float s = ev ? rec[(size_t)R * P + r * JD + tid] : 0.f;
-            sr[r] = s;
+            const float s = sr[r];
             if (r + 1 < R) {
               const float v = squash_elem<D>(s);
               if (ev) vcl[(r + 1) * JDa + tid] = vcl[r * JDa + tid] + v;
@@ -131,10 +149,10 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
           }
         }
       }
-      __syncthreads();
+      bar();
       SEQ_MARK(1);       // s^r loads, Vc^r
     } else {
-    __syncthreads();
+    bar();
     // ---- recompute the frame's iterations: c^r, s^r, Vc^r
     float b[C::NIM];
 #pragma unroll
@@ -152,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
 #pragma unroll
           for (int k = 0; k < C::NIM; ++k) cr[r][k] = cc[k];
         }
-        __syncthreads();
+        bar();
         if (owner_wave) {
           const float s = ev ? sum_parts(part, JD, tid) : 0.f;
           sr[r] = s;
@@ -162,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
             if (r + 1 < R) vcl[(r + 1) * JDa + tid] = vcl[r * JDa + tid] + v;
           }
         }
-        __syncthreads();
+        bar();
       }
     }
     }   // recompute
@@ -181,7 +199,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
           const float dg2 = 2.f * rs * ip * (ip - 0.5f * n2 * rs * rs) * sa;
           if (ev) gsl[r * JDa + tid] = gfac * a + dg2 * s;
         }
-        __syncthreads();
+        bar();
         SEQ_MARK(2);     // squash adjoint
 
         float gsv[C::KD], cc[C::NIM], gg[C::NIM];
@@ -256,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
           for (int k = 0; k < C::NIM; ++k) gl[r][k] = gg[k];
         }
         SEQ_MARK(3);     // q, sigma, gL, gVc partials (+ re-read rows)
-        __syncthreads();
+        bar();
         if constexpr (GRP)
           srf_grp::allreduce<kWaves, kThreads>(part, JD, I.ws, X, utt, gm, (rg.t1 - 1 - t) * R + (R - 1 - r), tid);
         SEQ_MARK(4);
@@ -349,8 +367,9 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
     }
     }   // CS gu
     SEQ_MARK(6);       // gu
-    if (t > rg.t0) load_rows<C, KRES>(ub + (size_t)(t - 1 - rg.tu0) * ff, JD, L, ur);
-    __syncthreads();   // the next frame overwrites w, Vc^0 and the c / gL slabs
+    if constexpr (!CS)   // unconditional (the range's first frame reloads itself): no register merge
+      load_rows<C, KRES>(ub + (size_t)(max(t - 1, rg.t0) - rg.tu0) * ff, JD, L, ur);
+    bar();   // the next frame overwrites w, Vc^0 and the c / gL slabs
     SEQ_MARK(7);
   }
   SEQ_FLUSH(g_stamps);
