@@ -1548,6 +1548,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         S = s0 + s1;
         par ^= 1;
       }
+      // logZ of capsule i before the next capsule's operand loads: waiting for it at its
+      // store then leaves those (younger) loads in flight
+      const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
       __builtin_amdgcn_sched_barrier(0);
       if (!(SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) && !SRF_FWD32_PROG && i + 1 < i1) {
         fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
@@ -1557,7 +1560,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       __builtin_amdgcn_sched_barrier(0);
       {
         // (logZ, sigma) of frame f, capsule i: branch-free (wave 0, half 0, valid frames)
-        const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
         __builtin_amdgcn_raw_buffer_store_b64(
             (unsigned __attribute__((ext_vector_type(2)))){__float_as_uint(lzv), __float_as_uint(S)}, sts,
             (wv == 0 && h == 0 && fvalid) ? (uint32_t)(f * A.in_n) * 8u : kNoStore, (uint32_t)i * 8u, 0);
@@ -1694,8 +1696,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     auto step = [&](int i, f16v (&ucur)[TW], f16v (&unext)[TW], float (&ccur)[OWN], float (&cnext)[OWN])
         __attribute__((always_inline)) {
       const bool more = i + 1 < i1;
-      if (more) {
-        load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cnext);
+      // logZ of capsule i before the next capsule's loads: waiting for it at its store
+      // then leaves those (younger) loads in flight
+      const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
+      // the next capsules' loads and pose run unconditionally (the chunk's last capsule
+      // re-reads itself, its pose unused): with a branch around them the compiler cannot
+      // count the loads in flight and waits for all of them at the stores below
+      {
+        load_c<OWN>(crow + (size_t)min(i + 1, i1 - 1) * cstep, A.Fs, cnext);
         const int in = min(i + 2, i1 - 1);
 #if SRF_FWD32P_DBG
         // timing experiment (wrong results): 1 = x of the chunk's first capsule (cache-hot),
@@ -1720,12 +1728,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         xpair32(sh, s0, s1);
         S = s0 + s1;
       }
-      {
-        const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
-        __builtin_amdgcn_raw_buffer_store_b64(
-            (unsigned __attribute__((ext_vector_type(2)))){__float_as_uint(lzv), __float_as_uint(S)}, sts,
-            (wv == 0 && h == 0 && fvalid) ? (uint32_t)(f * A.in_n) * 8u : kNoStore, (uint32_t)i * 8u, 0);
-      }
+      __builtin_amdgcn_raw_buffer_store_b64(
+          (unsigned __attribute__((ext_vector_type(2)))){__float_as_uint(lzv), __float_as_uint(S)}, sts,
+          (wv == 0 && h == 0 && fvalid) ? (uint32_t)(f * A.in_n) * 8u : kNoStore, (uint32_t)i * 8u, 0);
       float gown[OWN];
 #pragma unroll
       for (int a = 0; a < OWN; ++a) gown[a] = ccur[a] * (Q[a] - S);
