@@ -130,6 +130,40 @@ __device__ __forceinline__ void load_slice(const float* __restrict__ p, float (&
   }
 }
 
+// A ring slot: the raw words of a u_ij slice as loaded (bf16 pairs stay packed, so the
+// load is not waited for at issue) and their fp32 values at the use
+template <class TU, int KD>
+struct Slot;
+template <int KD>
+struct Slot<float, KD> {
+  float w[KD];
+  __device__ __forceinline__ void load(const float* __restrict__ p) { load_slice<KD>(p, w); }
+  __device__ __forceinline__ void widen(float (&x)[KD]) const {
+#pragma unroll
+    for (int d = 0; d < KD; ++d) x[d] = w[d];
+  }
+};
+template <int KD>
+struct Slot<unsigned short, KD> {
+  static_assert(KD % 8 == 0, "bf16 slices load 8 values per 16 bytes");
+  unsigned w[KD / 2];
+  __device__ __forceinline__ void load(const unsigned short* __restrict__ p) {
+#pragma unroll
+    for (int c = 0; c < KD / 2; c += 4) {
+      const auto q = *reinterpret_cast<const unsigned __attribute__((ext_vector_type(4)))*>(p + 2 * c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[c + k] = q[k];
+    }
+  }
+  __device__ __forceinline__ void widen(float (&x)[KD]) const {
+#pragma unroll
+    for (int k = 0; k < KD / 2; ++k) {
+      x[2 * k] = __uint_as_float(w[k] << 16);
+      x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+};
+
 template <int KD>
 __device__ __forceinline__ float dot_slice(const float (&x)[KD], const float (&w)[KD]) {
   float p0 = 0.f, p1 = 0.f;
@@ -147,6 +181,33 @@ using srf_grp::Grp;
 using srf_grp::kMaxGroup;
 // floats of the stream backward's gL scratch [B][R][in_n][J] at the item workspace's start
 __host__ __device__ inline size_t gl_floats(int B, int in_n, int J, int R) { return (size_t)B * R * in_n * J; }
+
+// Workgroup barrier that orders LDS only (no vmcnt(0)), so the register ring's loads stay
+// in flight across it; for barriers with no global data exchanged between waves of the
+// kernel (the grouped launches exchange through srf_group.h and keep __syncthreads)
+#ifndef SRF_STREAM_LDSBAR
+#define SRF_STREAM_LDSBAR 1
+#endif
+template <bool LDS_ONLY>
+__device__ __forceinline__ void wg_bar() {
+  if constexpr (LDS_ONLY && SRF_STREAM_LDSBAR) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    __syncthreads();
+  }
+}
+
+// the accumulators computed here: no sinking of their updates past this point (IR or
+// scheduler), and no global load hoisted above it
+template <int K>
+__device__ __forceinline__ void pin(float (&a)[K]) {
+#pragma unroll
+  for (int d = 0; d < K; ++d) asm volatile("" : "+v"(a[d]));
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 __device__ __forceinline__ float squash_fac(float n2) {
   return n2 * __builtin_amdgcn_rcpf(1.f + n2) * __builtin_amdgcn_rsqf(n2 + kEps);
@@ -201,17 +262,17 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
     vc[n] = rg.t0 > 0 ? vo[(size_t)(rg.t0 - 1) * JD + e] : 0.f;
     wl[e] = vc[n];
   }
-  float xr[PD][KD];
+  Slot<TU, KD> xr[PD];
   Cur lc{rg.t0, 0, 0};
-  auto issue = [&](float(&x)[KD]) {
+  auto issue = [&](Slot<TU, KD>& x) {
     const int tc = min(lc.t, rg.t1 - 1);
     const int i = min(gw + cstep * lc.m, in_n - 1);
-    load_slice<KD>(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD, x);
+    x.load(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD);
     lc.adv(NMp, iters, 1);
   };
 #pragma unroll
   for (int p = 0; p < PD; ++p) issue(xr[p]);
-  __syncthreads();
+  wg_bar<!GRP>();
 
   for (int t = rg.t0; t < rg.t1; ++t) {
     const __amdgpu_buffer_rsrc_t csf = float_rsrc(cs ? cs + ((size_t)b * T + t) * csr : nullptr, csr);
@@ -220,27 +281,36 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
       load_slice<KD>(wl + lane * KD, w);
 #pragma unroll
       for (int d = 0; d < KD; ++d) acc[d] = 0.f;
-      for (int m0 = 0; m0 < NMp; m0 += PD) {
+      int m0 = 0;
+      do {   // NMp >= PD (nm_padded): no zero-trip path, whose merge would wait on the ring
 #pragma unroll
         for (int p = 0; p < PD; ++p) {
           const int i = gw + cstep * (m0 + p);
           const bool iv = i < in_n;
-          const float lg = group_sum<1, C::RQ>(dot_slice<KD>(xr[p], w));
-          const float x = jm ? lg : -INFINITY;
-          const float mx = group_max<C::RQ, 64>(x);
-          const float ex = __expf(x - mx);
-          const float c = iv ? ex * __builtin_amdgcn_rcpf(group_sum<C::RQ, 64>(ex)) : 0.f;
+          float x[KD];
+          xr[p].widen(x);
+          const float lg = group_sum<1, C::RQ>(dot_slice<KD>(x, w));
+          const float lj = jm ? lg : -INFINITY;
+          const float mx = group_max<C::RQ, 64>(lj);
+          const float ex = __expf(lj - mx);
+          // tail slots masked arithmetically: a select here becomes a uniform branch around the
+          // softmax, which splits the block and sinks the accumulation past the slot's reload
+          const float c = ex * __builtin_amdgcn_rcpf(group_sum<C::RQ, 64>(ex)) * (iv ? 1.f : 0.f);
 #pragma unroll
-          for (int d = 0; d < KD; ++d) acc[d] += c * xr[p][d];
+          for (int d = 0; d < KD; ++d) acc[d] += c * x[d];
           bstore(csf, c, q0 && iv ? (uint32_t)((r * in_n + i) * J + j) * 4 : kDrop);
+          // the slot's last use before its reload, so the load lands in the same registers
+          // (the accumulation sunk past it would need a second set and copies that wait)
+          pin(acc);
           issue(xr[p]);
           __builtin_amdgcn_sched_barrier(0);   // keep the ring order: no hoisting across capsules
         }
-      }
+        m0 += PD;
+      } while (m0 < NMp);
 #pragma unroll
       for (int d = 0; d < KD; d += 4)
         *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{acc[d], acc[d + 1], acc[d + 2], acc[d + 3]};
-      __syncthreads();
+      wg_bar<!GRP>();
       if constexpr (GRP) srf_grp::allreduce<kNW, kNT>(part, JD, I.ws, X, b, gm, (unsigned)((t - rg.t0) * iters + r), tid);
 #pragma unroll
       for (int n = 0; n < NE; ++n) {
@@ -262,7 +332,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
         }
         wl[e] = vc[n];
       }
-      __syncthreads();
+      wg_bar<!GRP>();
     }
   }
 }
@@ -312,12 +382,13 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
   for (int n = 0; n < NE; ++n) carry[n] = carry_io ? carry_io[tid + n * kNT] : 0.f;
 
   // ring of the adjoint passes: u_t slice and c^r_ij of capsule i, pass p <-> r = R-1-p
-  float xr[PD][KD], cr[PD];
+  Slot<TU, KD> xr[PD];
+  float cr[PD];
   Cur lc{rg.t1 - 1, 0, 0};
-  auto issue = [&](float(&x)[KD], float& c) {
+  auto issue = [&](Slot<TU, KD>& x, float& c) {
     const int tc = max(lc.t, rg.t0);
     const int i = min(gw + cstep * lc.m, in_n - 1);
-    load_slice<KD>(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD, x);
+    x.load(ub + (size_t)(tc - rg.tu0) * ff + (size_t)i * JD);
     c = csb[(size_t)tc * csr + (size_t)(R - 1 - lc.p) * PJ + (size_t)i * J + j];
     lc.adv(NMp, R, -1);
   };
@@ -332,7 +403,8 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
     for (int n = 0; n < NE; ++n) {
       const int e = tid + n * kNT;
       const float a = g_v[((size_t)b * T + t) * JD + e] + carry[n];
-      float vcv = t > 0 ? v_saved[((size_t)b * T + t - 1) * JD + e] : 0.f;
+      const float vp = v_saved[((size_t)b * T + max(t - 1, 0)) * JD + e];   // unconditional (see sn)
+      float vcv = t > 0 ? vp : 0.f;
       for (int r = 0; r < R; ++r) {
         const float sv = csf[(size_t)R * PJ + (size_t)r * JD + e];
         vcl[r * JD + e] = vcv;
@@ -342,37 +414,43 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
       carry[n] = 0.f;
       gv[n] = 0.f;
     }
-    __syncthreads();
+    wg_bar<!GRP>();
     // ---- adjoint passes r = R-1 .. 0 over u_t
     for (int p = 0; p < R; ++p) {
       const int r = R - 1 - p;
       float g[KD], gacc[KD], sn[NE];
       load_slice<KD>(gsl + r * JD + lane * KD, g);
 #pragma unroll
-      for (int n = 0; n < NE; ++n)   // s^{r-1}, for gs^{r-1} at the end of the pass
-        sn[n] = r > 0 ? csf[(size_t)R * PJ + (size_t)(r - 1) * JD + tid + n * kNT] : 0.f;
+      for (int n = 0; n < NE; ++n)   // s^{r-1}, for gs^{r-1} at the end of the pass (unused at r = 0:
+        // loaded unconditionally, a load under a branch is waited for at the merge)
+        sn[n] = csf[(size_t)R * PJ + (size_t)max(r - 1, 0) * JD + tid + n * kNT];
 #pragma unroll
       for (int d = 0; d < KD; ++d) gacc[d] = 0.f;
-      for (int m0 = 0; m0 < NMp; m0 += PD) {
+      int m0 = 0;
+      do {   // NMp >= PD, as in the forward
 #pragma unroll
         for (int pp = 0; pp < PD; ++pp) {
           const int i = gw + cstep * (m0 + pp);
           const bool iv = i < in_n;
-          const float qd = group_sum<1, C::RQ>(dot_slice<KD>(xr[pp], g));
+          float x[KD];
+          xr[pp].widen(x);
+          const float qd = group_sum<1, C::RQ>(dot_slice<KD>(x, g));
           const float c = iv ? cr[pp] : 0.f;
           const float sig = group_sum<C::RQ, 64>(c * qd);
           const float gL = c * (qd - sig);
 #pragma unroll
-          for (int d = 0; d < KD; ++d) gacc[d] += gL * xr[pp][d];
+          for (int d = 0; d < KD; ++d) gacc[d] += gL * x[d];
           bstore(glr, gL, q0 && iv ? (uint32_t)((r * in_n + i) * J + j) * 4 : kDrop);
+          pin(gacc);   // reload in place (see the forward)
           issue(xr[pp], cr[pp]);   // runs on into frame t - 1 (the gu pass leaves the ring alone)
           __builtin_amdgcn_sched_barrier(0);
         }
-      }
+        m0 += PD;
+      } while (m0 < NMp);
 #pragma unroll
       for (int d = 0; d < KD; d += 4)
         *reinterpret_cast<f4*>(part + wv * JD + lane * KD + d) = f4{gacc[d], gacc[d + 1], gacc[d + 2], gacc[d + 3]};
-      __syncthreads();
+      wg_bar<!GRP>();
       if constexpr (GRP) srf_grp::allreduce<kNW, kNT>(part, JD, I.ws, X, b, gm, (unsigned)((rg.t1 - 1 - t) * R + p), tid);
 #pragma unroll
       for (int n = 0; n < NE; ++n) {
@@ -388,7 +466,9 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
         gv[n] += gvc;         // dL/dv^{r-1} = sum_{r' >= r} gVc^{r'}
         if (r > 0) gsl[(r - 1) * JD + e] = dsquash<D>(sn[n], gv[n]);
       }
-      __syncthreads();
+      // the gu pass after the last one reads the gL scratch back: there the stores drain
+      if (p + 1 < R) wg_bar<!GRP>();
+      else __syncthreads();
     }
     // ---- gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j, HD outputs per lane per sub-pass
     float* gut = gub + (size_t)(t - rg.tg0) * ff;
