@@ -30,6 +30,7 @@
 // HBM per frame: forward R reads of u_t; backward R reads of u_t + one write of gu_t.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "route_sdr_seq.h"
 #include "route_sdr_seq_dev.h"
@@ -48,6 +49,14 @@ using srf_seq::group_sum;
 #endif
 #ifndef SRF_STREAM_PDF32
 #define SRF_STREAM_PDF32 2
+#endif
+// with u in bf16 (packed slots, half the registers) a deeper forward ring pays (r04ff A/B,
+// C5 fp8: (3, 2) 598 ms, (6, 3) 588; fp32 unchanged at 788 | 790)
+#ifndef SRF_STREAM_PDF16_BF
+#define SRF_STREAM_PDF16_BF 6
+#endif
+#ifndef SRF_STREAM_PDF32_BF
+#define SRF_STREAM_PDF32_BF 3
 #endif
 #ifndef SRF_STREAM_PDB16   // backward ring depths
 #define SRF_STREAM_PDB16 4
@@ -70,6 +79,9 @@ struct SC {
   static constexpr int NE = JD / kNT;         // elements per thread in the element phases
   // capsules in flight per wave in the forward / backward register ring
   static constexpr int PDF = KD <= 8 ? 8 : KD <= 16 ? SRF_STREAM_PDF16 : SRF_STREAM_PDF32;
+  static constexpr int PDF_BF = KD <= 8 ? 8 : KD <= 16 ? SRF_STREAM_PDF16_BF : SRF_STREAM_PDF32_BF;
+  template <class TU>
+  static constexpr int pdf() { return std::is_same<TU, float>::value ? PDF : PDF_BF; }
   static constexpr int PDB = KD <= 16 ? SRF_STREAM_PDB16 : SRF_STREAM_PDB32;
   static constexpr int HD = 8;                 // gu outputs per lane per sub-pass (registers: 2R*HD)
   static_assert(D % KD == 0 && NE >= 1 && KD % 4 == 0 && KD % HD == 0, "unsupported stream shape");
@@ -236,7 +248,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
   float* __restrict__ v_out = I.v;
   float* __restrict__ cs = I.cs;
   const srf::SeqRange rg = I.rg;
-  constexpr int JD = C::JD, J = C::J, PD = C::PDF, NE = C::NE;
+  constexpr int JD = C::JD, J = C::J, PD = C::template pdf<TU>(), NE = C::NE;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* wl = lds;
   float* part = lds + JD;
@@ -552,7 +564,7 @@ int launch_fwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, in
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k, dim3(B * X.G, items.n), dim3(kNT), lds, st, items, T, in_n, iters, mask_first,
-                     nm_padded(in_n, C::PDF, X.G), X);
+                     nm_padded(in_n, bf ? C::PDF_BF : C::PDF, X.G), X);
   SRF_LAUNCH_CHECK("sdr_stream_fwd");
   return SRF_OK;
 }
