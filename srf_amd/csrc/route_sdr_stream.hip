@@ -58,6 +58,14 @@ using srf_seq::group_sum;
 #ifndef SRF_STREAM_PDF32_BF
 #define SRF_STREAM_PDF32_BF 3
 #endif
+// the backward's bf16 ring at the fp32 depths: (6, 3) 599 ms and (8, 4) 602 against (4, 2)
+// 596 (r04hh A/B, C5 fp8)
+#ifndef SRF_STREAM_PDB16_BF
+#define SRF_STREAM_PDB16_BF SRF_STREAM_PDB16
+#endif
+#ifndef SRF_STREAM_PDB32_BF
+#define SRF_STREAM_PDB32_BF SRF_STREAM_PDB32
+#endif
 #ifndef SRF_STREAM_PDB16   // backward ring depths
 #define SRF_STREAM_PDB16 4
 #endif
@@ -83,6 +91,9 @@ struct SC {
   template <class TU>
   static constexpr int pdf() { return std::is_same<TU, float>::value ? PDF : PDF_BF; }
   static constexpr int PDB = KD <= 16 ? SRF_STREAM_PDB16 : SRF_STREAM_PDB32;
+  static constexpr int PDB_BF = KD <= 16 ? SRF_STREAM_PDB16_BF : SRF_STREAM_PDB32_BF;
+  template <class TU>
+  static constexpr int pdb() { return std::is_same<TU, float>::value ? PDB : PDB_BF; }
   static constexpr int HD = 8;                 // gu outputs per lane per sub-pass (registers: 2R*HD)
   static_assert(D % KD == 0 && NE >= 1 && KD % 4 == 0 && KD % HD == 0, "unsupported stream shape");
 };
@@ -364,7 +375,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
   const float* __restrict__ cs = I.cs;
   float* __restrict__ gls = I.ws;
   const srf::SeqRange rg = I.rg;
-  constexpr int JD = C::JD, J = C::J, PD = C::PDB, NE = C::NE, HD = C::HD;
+  constexpr int JD = C::JD, J = C::J, PD = C::template pdb<TU>(), NE = C::NE, HD = C::HD;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* part = lds;
   float* gsl = part + kNW * JD;
@@ -581,7 +592,7 @@ int launch_bwd(const srf::SeqItems& items, int B, int T, int in_n, int iters, hi
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(k, dim3(B * X.G, items.n), dim3(kNT), lds, st, items, T, in_n, iters,
-                     nm_padded(in_n, C::PDB, X.G), X);
+                     nm_padded(in_n, bf ? C::PDB_BF : C::PDB, X.G), X);
   SRF_LAUNCH_CHECK("sdr_stream_bwd");
   return SRF_OK;
 }
