@@ -30,6 +30,9 @@ constexpr float kSquashEps = 1e-7f;  // naive:248
 #ifndef SRF_GU_SPLITGX
 #define SRF_GU_SPLITGX 0
 #endif
+#ifndef SRF_GUX16_PEEL
+#define SRF_GUX16_PEEL 0   // 1: route_gux16_kernel's capsule loop without exits in its body (A/B pending)
+#endif
 #ifndef SRF_GUX16_OCC
 #define SRF_GUX16_OCC 2   // route_gux16_kernel workgroups (of 4 waves) per CU: 2, or 3 (two-slot ring)
 #endif
@@ -1060,6 +1063,24 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
       SRF_GUX16_FETCH(S0)
       SRF_GUX16_FETCH(S1)
     }
+#if SRF_GUX16_PEEL
+    // whole triples in the loop and the one or two capsules left after it: no exit
+    // inside the body, whose path back to the header (the structurizer's) made the
+    // first wait of every triple count one slot in flight instead of two
+    int k = 0;
+    for (; k + NB <= ncap; k += NB) {
+      SRF_GUX16_FETCH(S2)
+      compute(S0{});
+      SRF_GUX16_FETCH(S0)
+      compute(S1{});
+      SRF_GUX16_FETCH(S1)
+      compute(S2{});
+    }
+    if (k < ncap) {
+      compute(S0{});
+      if (k + 1 < ncap) compute(S1{});
+    }
+#else
     for (int k = 0; k < ncap; k += NB) {
       SRF_GUX16_FETCH(S2)
       compute(S0{});
@@ -1070,6 +1091,7 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
       SRF_GUX16_FETCH(S1)
       compute(S2{});
     }
+#endif
   } else {   // two slots: capsule k + 1 in flight while capsule k is formed
     if (ncap > 0) {
       SRF_GUX16_FETCH(S0)
