@@ -31,7 +31,7 @@ constexpr float kSquashEps = 1e-7f;  // naive:248
 #define SRF_GU_SPLITGX 0
 #endif
 #ifndef SRF_GUX16_PEEL
-#define SRF_GUX16_PEEL 0   // 1: route_gux16_kernel's capsule loop without exits in its body (A/B pending)
+#define SRF_GUX16_PEEL 0   // 1: route_gux16_kernel's capsule loop without exits in its body (C4 r04ii A/B: no change)
 #endif
 #ifndef SRF_GUX16_OCC
 #define SRF_GUX16_OCC 2   // route_gux16_kernel workgroups (of 4 waves) per CU: 2, or 3 (two-slot ring)
