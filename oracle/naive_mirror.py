@@ -12,6 +12,7 @@ Parity: unpinned against TensorFlow (see ``oracle/__init__.py``).
 """
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -151,6 +152,134 @@ def dr_layer_chunked(emb, W, bias, lpad, rpad, iters, mask_first, g_v, frames_pe
     for w in range(win):
         gep[:, w:w + T] += gx[:, :, w]
     return v_all.reshape(B, T, J, Dv), gep[:, lpad:lpad + T], gW, gb
+
+
+def _pose_fp8_tbjid(xw, W, bias, bf16_u):
+    """``srf_oracle.pose_fp8`` (same quantisation: per-vector 2^e scales, e4m3 operands,
+    exact products summed in float64, scaled back, float32 bias, float32 or bf16 u) with
+    the contraction on torch: xw [T,B,I,D] -> u [T,B,J,I,Dv] (float64)."""
+    T, B, I, D = xw.shape
+    J, Dv = W.shape[1], W.shape[2]
+    x32 = xw.numpy().astype(np.float32).astype(np.float64)
+    W32 = W.numpy().astype(np.float32).astype(np.float64)
+    ex = so.e4m3_scale_exp(np.abs(x32).max(-1))                  # [T,B,I]
+    ew = so.e4m3_scale_exp(np.abs(W32).max(-1))                  # [I,J,Dv]
+    xq = torch.as_tensor(so.e4m3_round(x32 * np.exp2(ex)[..., None]))
+    wq = torch.as_tensor(so.e4m3_round(W32 * np.exp2(ew)[..., None]))
+    u = torch.bmm(wq.reshape(I, J * Dv, D), xq.permute(2, 3, 0, 1).reshape(I, D, T * B))
+    u = u.reshape(I, J, Dv, T, B).permute(3, 4, 1, 0, 2)         # [T,B,J,I,Dv]
+    u = u * torch.as_tensor(np.exp2(-ex.astype(np.float64))).permute(0, 1, 2)[:, :, None, :, None]
+    u = u * torch.as_tensor(np.exp2(-ew.astype(np.float64))).permute(1, 0, 2)[None, None]
+    u = (u + torch.as_tensor(bias.numpy().astype(np.float32).astype(np.float64)).permute(1, 0, 2)).numpy()
+    return torch.as_tensor(so.bf16_round(u) if bf16_u else u.astype(np.float32).astype(np.float64))
+
+
+def sdr_stack_frames(emb, Ws, bs, gammas, betas, lpad, rpad, iters, g_v, dtype=torch.float64, fp8_pose=None,
+                     mask_last=True):
+    """An SDR stack -- per layer window (naive:150-151), pose (:154-159), the frame
+    recurrence (:162-170 with body_context :231-245, the last layer masked by
+    pad_body_context :212-229) and, between layers, LN_mid (:187-191, dropout off) --
+    and its backward for the upstream gradient g_v of the last layer's v, frame by
+    frame, so that a bench-size stack (C3: 28 utterances x 200 frames x 80 x 32 x 32
+    u per layer) runs under autograd without materialising u or its gradient: each
+    frame's pose is formed from its own window, every intermediate is one frame.
+
+    emb [B,T,N,D]; Ws[l] [in_n,J,Dv,D]; gammas / betas for the L-1 inner LNs.
+    fp8_pose: None, or per-layer bf16-u flags -- the pose then takes the values of
+    ``srf_oracle.pose_fp8`` (the build's opt-in e4m3 pose) with the exact pose's
+    gradient, like ``NaiveMirror(fp8_pose=...)``.  mask_last: the last layer is the
+    model's output layer (its capsule 0 masked); False for a stack cut out of a model.
+    Returns (v_last [B,T,J,Dv], g_emb, [g_W], [g_bias], [g_gamma], [g_beta])."""
+    def leaf(a):
+        return torch.as_tensor(a).to(dtype).clone().requires_grad_(True)
+    e0 = leaf(emb)
+    Wl, bl = [leaf(w) for w in Ws], [leaf(b) for b in bs]
+    gl, btl = [leaf(g) for g in gammas], [leaf(b) for b in betas]
+    B, T = e0.shape[:2]
+    L = len(Wl)
+    x = [e0[:, t] for t in range(T)]            # layer input, one [B,N,D] per frame
+    for l in range(L):
+        W, bias = Wl[l], bl[l]
+        I, J, Dv, D = W.shape
+        N = x[0].shape[1]
+        # the layer's pose for all frames in one product, held as [T, B, J, I, Dv] and
+        # unbound into frames: its backward is one stack of the frames' gradients and
+        # one product for g_W (no per-frame copies of W's gradient); per frame the
+        # logits and s are batched matmuls that keep a reference to u_t, with no
+        # u-sized temporaries per iteration
+        zero = torch.zeros(B, N, D, dtype=dtype)
+        xp = torch.stack([zero] * lpad + x + [zero] * rpad, 0)                       # [T+w-1, B, N, D]
+        xw = torch.cat([xp[w:w + T] for w in range(lpad + rpad + 1)], 2)            # [T, B, I, D]
+        u = torch.bmm(W.reshape(I, J * Dv, D), xw.permute(2, 3, 0, 1).reshape(I, D, T * B))
+        u = u.reshape(I, J, Dv, T, B).permute(3, 4, 1, 0, 2).contiguous() + bias.permute(1, 0, 2)
+        if fp8_pose is not None:
+            u = u + (_pose_fp8_tbjid(xw.detach(), W.detach(), bias.detach(), bool(fp8_pose[l])).to(dtype)
+                     - u).detach()
+        m = torch.zeros(J, I, dtype=dtype)
+        masked = mask_last and l == L - 1
+        if masked:
+            m[0] = so.MASK_LOGIT
+        v = torch.zeros(B, J, Dv, dtype=dtype)
+        outs = []
+        for ut in u.unbind(0):
+            b = torch.zeros(B, J, I, dtype=dtype)
+            for _ in range(iters):
+                b = b + torch.matmul(ut, v.unsqueeze(-1)).squeeze(-1)      # <u_ij, v_j>
+                if masked:
+                    b = b + m
+                c = torch.softmax(b, dim=1)                                 # over j
+                v = squash(torch.matmul(c.unsqueeze(2), ut).squeeze(2), -1)
+            outs.append(v)
+        del u
+        if l < L - 1:
+            x = [layer_norm(o.reshape(B, J * Dv), gl[l], btl[l]).reshape(B, J, Dv) for o in outs]
+        else:
+            vl = torch.stack(outs, 1)
+    vl.backward(torch.as_tensor(g_v, dtype=dtype))
+    return (vl.detach(), e0.grad, [w.grad for w in Wl], [b.grad for b in bl], [g.grad for g in gl],
+            [b.grad for b in btl])
+
+
+def sdr_layer_teacher_forced(emb, W, bias, v_run, lpad, rpad, iters, masked, fp8_bf16=None, frames_per_chunk=16):
+    """One SDR layer's frames, each routed from the run's own previous output:
+    frame t of the recurrence (naive:162-170, :231-245 / :212-229) in float64 with
+    v_{t-1} taken from ``v_run`` (the implementation under test) instead of from this
+    computation.  Every frame becomes an independent one-step check, so the bound
+    does not have to cover the recurrence's amplification of rounding over time
+    (at the reference init two fp32 runs of one C3 layer drift apart to ~0.3 by frame
+    200).  fp8_bf16: None (exact fp32 pose) or the bf16-u flag of the opt-in fp8 pose
+    (``_pose_fp8_tbjid``).  emb [B,T,N,D], v_run [B,T,J,Dv] -> v [B,T,J,Dv] float64."""
+    emb = torch.as_tensor(emb, dtype=torch.float64)
+    W = torch.as_tensor(W, dtype=torch.float64)
+    bias = torch.as_tensor(bias, dtype=torch.float64)
+    v_run = torch.as_tensor(v_run, dtype=torch.float64)
+    B, T, N, D = emb.shape
+    I, J, Dv, _ = W.shape
+    ep = F.pad(emb, (0, 0, 0, 0, lpad, rpad)).transpose(0, 1)                  # [T+w-1, B, N, D]
+    m = torch.zeros(J, I, dtype=torch.float64)
+    if masked:
+        m[0] = so.MASK_LOGIT
+    out = torch.empty(B, T, J, Dv, dtype=torch.float64)
+    for t0 in range(0, T, frames_per_chunk):
+        t1 = min(T, t0 + frames_per_chunk)
+        xw = torch.cat([ep[t0 + w:t1 + w] for w in range(lpad + rpad + 1)], 2)   # [n, B, I, D]
+        n = t1 - t0
+        if fp8_bf16 is None:
+            u = torch.bmm(W.reshape(I, J * Dv, D), xw.permute(2, 3, 0, 1).reshape(I, D, n * B))
+            u = u.reshape(I, J, Dv, n, B).permute(3, 4, 1, 0, 2) + bias.permute(1, 0, 2)
+        else:
+            u = _pose_fp8_tbjid(xw, W, bias, bool(fp8_bf16))                  # [n, B, J, I, Dv]
+        v = torch.zeros(n, B, J, Dv, dtype=torch.float64)
+        v[max(0, 1 - t0):] = v_run[:, max(t0 - 1, 0):t1 - 1].transpose(0, 1)
+        b = torch.zeros(n, B, J, I, dtype=torch.float64)
+        for _ in range(iters):
+            b = b + torch.matmul(u, v.unsqueeze(-1)).squeeze(-1)
+            if masked:
+                b = b + m
+            c = torch.softmax(b, dim=2)
+            v = squash(torch.matmul(c.unsqueeze(3), u).squeeze(3), -1)
+        out[:, t0:t1] = v.transpose(0, 1)
+    return out
 
 
 class NaiveMirror(torch.nn.Module):

@@ -146,6 +146,70 @@ def test_dr_layer_chunked_matches_mirror_autograd():
         assert (got - ref.grad).abs().max().item() < 1e-12
 
 
+def test_sdr_stack_frames_matches_oracle_and_tiled_mirror():
+    """The frame-by-frame float64 SDR stack (used at C3 / C5 bench size) equals the
+    numpy oracle's layer-by-layer forward and the tiled mirror's autograd gradients on
+    a small ragged 2-layer case with LN between the layers; its fp8 pose is the
+    oracle's ``pose_fp8``."""
+    rng = np.random.default_rng(2)
+    B, T, N, D, lp, rp, J = 2, 7, 3, 8, 2, 1, 4
+    I = N * (lp + rp + 1)
+    emb = rng.standard_normal((B, T, N, D))
+    Ws = [rng.standard_normal((I, N, D, D)) * 0.3, rng.standard_normal((I, J, D, D)) * 0.3]
+    bs = [rng.standard_normal((I, N, D)) * 0.1, rng.standard_normal((I, J, D)) * 0.1]
+    gam, bet = [1 + 0.1 * rng.standard_normal(N * D)], [0.1 * rng.standard_normal(N * D)]
+    gv = rng.standard_normal((B, T, J, D))
+    v, ge, gW, gb, gg, gbt = nm.sdr_stack_frames(emb, Ws, bs, gam, bet, lp, rp, 3, gv)
+    x = emb
+    for l in range(2):
+        y = so.sequential_routing(so.pose(so.window(x, lp, rp), Ws[l], bs[l]), 3, l == 1)
+        if l == 0:
+            x = so.layer_norm(y.reshape(B, T, -1), gam[0], bet[0]).reshape(B, T, N, D)
+    assert np.abs(v.numpy() - y).max() < 1e-13
+    ce = torch.tensor(emb, requires_grad=True)
+    cW = [torch.tensor(w, requires_grad=True) for w in Ws]
+    cb = [torch.tensor(b, requires_grad=True) for b in bs]
+    cg, cbt = torch.tensor(gam[0], requires_grad=True), torch.tensor(bet[0], requires_grad=True)
+    x = ce
+    for l in range(2):
+        ep = torch.nn.functional.pad(x, (0, 0, 0, 0, lp, rp))
+        xw = torch.cat([ep[:, w:w + T] for w in range(lp + rp + 1)], 2)
+        y = nm.sequential_routing(nm.pose_tiled(xw, cW[l], cb[l]), 3, l == 1)
+        if l == 0:
+            x = nm.layer_norm(y.reshape(B, T, -1), cg, cbt).reshape(B, T, N, D)
+    y.backward(torch.tensor(gv))
+    pairs = [(ge, ce), (gW[0], cW[0]), (gW[1], cW[1]), (gb[0], cb[0]), (gb[1], cb[1]), (gg[0], cg), (gbt[0], cbt)]
+    for got, ref in pairs:
+        assert (got - ref.grad).abs().max().item() < 1e-12
+    # fp8 pose, bf16 u on the first layer
+    v8 = nm.sdr_stack_frames(emb, Ws, bs, gam, bet, lp, rp, 3, gv, fp8_pose=[True, False])[0]
+    x = emb
+    for l in range(2):
+        y = so.sequential_routing(so.pose_fp8(so.window(x, lp, rp), Ws[l], bs[l], l == 0), 3, l == 1)
+        if l == 0:
+            x = so.layer_norm(y.reshape(B, T, -1), gam[0], bet[0]).reshape(B, T, N, D)
+    assert np.abs(v8.numpy() - y).max() < 1e-12
+
+
+def test_sdr_teacher_forced_is_one_step_of_the_recurrence():
+    """sdr_layer_teacher_forced fed a float64 run's own output reproduces it (to float64 rounding);
+    fed a float32 run's output it stays at rounding level while the free-running float32
+    run has drifted (reference init: the recurrence amplifies rounding along the frames)."""
+    rng = np.random.default_rng(3)
+    B, T, N, D, lp = 4, 60, 16, 32, 2   # the C3 layer shape
+    I = N * (2 * lp + 1)
+    emb = rng.standard_normal((B, T, N, D))
+    W, b = rng.standard_normal((I, 16, D, D)) * 0.1, rng.standard_normal((I, 16, D)) * 0.1
+    gv = rng.standard_normal((B, T, 16, D))
+    v64 = nm.sdr_stack_frames(emb, [W], [b], [], [], lp, lp, 3, gv, mask_last=False)[0]
+    v32 = nm.sdr_stack_frames(emb, [W], [b], [], [], lp, lp, 3, gv, dtype=torch.float32, mask_last=False)[0]
+    v32 = v32.double()
+    assert (nm.sdr_layer_teacher_forced(emb, W, b, v64, lp, lp, 3, False, frames_per_chunk=7) - v64).abs().max() < 1e-14
+    tf = nm.sdr_layer_teacher_forced(emb, W, b, v32, lp, lp, 3, False)
+    assert ((tf - v32).abs() / (1 + v32.abs())).max() < 2e-6
+    assert ((v32 - v64).abs() / (1 + v64.abs())).max() > 1e-5
+
+
 def test_e4m3_and_bf16_emulation_match_torch_casts():
     """The fp8-pose restatement's rounding (srf_oracle.e4m3_round / bf16_round) equals
     torch's float8_e4m3fn / bfloat16 casts (round to nearest even, e4m3 subnormals),
