@@ -244,6 +244,12 @@ def measure(workload, args, world, rank, dev):
     if args.sdr_last_group is not None:
         g = [int(x) for x in args.sdr_last_group.split(',')]
         model.sdr_options['last_group'] = (g[0], g[-1])
+    # N > 1: the gradient all-reduce in 25 MB buckets launched as the backward completes
+    # them, captured inside the step's hipGraph with the backward they overlap
+    # (trainer_sr.GradBuckets; --flat-allreduce: one all-reduce after each replay)
+    bucketed = world > 1 and not args.flat_allreduce
+    if bucketed:
+        trainer_sr.use_grad_buckets(model, 25.0)
     opt = train_helper.get_optimizer(cfg)
     batch = synthetic_batch(B, T, class_n, rank, dev)
     loss_state, frame_state, samples = trainer_sr.Mean(), trainer_sr.Mean(), trainer_sr.Sum()
@@ -259,7 +265,17 @@ def measure(workload, args, world, rank, dev):
         step = eager_step
     else:
         # forward + CTC + backward as one hipGraph; all-reduce and Adam eager per step
-        graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
+        try:
+            graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
+        except RuntimeError as e:
+            if not bucketed:
+                raise
+            # every rank fails the same capture: fall back to the flat form on all of them
+            print(f'[bench] capturing the bucketed all-reduce failed ({e}); flat all-reduce instead',
+                  file=sys.stderr)
+            bucketed = False
+            trainer_sr.use_grad_buckets(model, None)
+            graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
         for _ in range(args.warmup):
             graphed(loss_state, frame_state, samples)
         torch.cuda.synchronize()
@@ -343,7 +359,11 @@ def measure(workload, args, world, rank, dev):
                                f'{"fp8 (e4m3) pose MFMA, " if model.pose_fp8 else ""}'
                                f'train step (fwd+bwd+allreduce+Adam)',
                    'utterances_per_gpu': B, 'frames_per_utterance': T, 'global_batch': B * world,
-                   'parallelism': f'dp{world}', 'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
+                   'parallelism': f'dp{world}',
+                   'allreduce': (None if world == 1 else
+                                 'RCCL SUM in 25 MB buckets launched as the backward completes them, captured in '
+                                 'the step graph' if bucketed else 'one flat RCCL SUM after each replay'),
+                   'launch': 'eager' if args.eager else 'hipgraph (fwd+CTC+bwd)'},
         'roofline': {'kernel': (f'{first.replace("void ", "")} + {rpass.replace("void ", "")} (layer {last + 1} DR '
                                 f'forward passes, R={R}; pose on v_mfma_f32_32x32x16_f16 as 2-term fp16 splits of '
                                 f'power-of-two scaled operands + one bf16 bias MFMA = fp32-accurate)'
@@ -369,6 +389,8 @@ def measure(workload, args, world, rank, dev):
                          'ms_per_step': round(fwd_elapsed / args.steps * 1e3, 4),
                          'mode': 'model(feats, training=False), eager launches'},
     }
+    from srf_amd import ops
+    ops.check_faults()   # a grouped SDR recurrence that timed out made this run's results wrong
     return res, model, cfg, class_n, T
 
 
@@ -390,6 +412,8 @@ def main():
                     help='SDR stack: the gx and gW launches of din-32 layers separately (default: fused)')
     ap.add_argument('--sdr-capsnorm-per-layer', action='store_true',
                     help='SDR stack: one LN/dropout launch per inner layer and range (default: one per diagonal)')
+    ap.add_argument('--flat-allreduce', action='store_true',
+                    help='N > 1: one flat all-reduce after each step instead of backward-overlapped buckets (A/B)')
     ap.add_argument('--eager', action='store_true', help='launch every kernel from Python each step (no hipGraph)')
     args = ap.parse_args()
 

@@ -79,6 +79,12 @@ int srf_route_dr_bwd_data_ex(const float* emb, const float* W, const float* bias
  * not per thread).  One process drives one GPU, so the host keeps one counter per
  * process and never detaches it (srf_amd.trainer_sr.seed_counter). */
 int srf_set_seed_source(const void* step_counter);
+/* Fault word -- PROCESS-GLOBAL state like the step counter: a device uint32 that a
+ * grouped SDR recurrence (srf_sdr_range.group > 1) sets to nonzero when a member gave
+ * up waiting for the others (they were not resident together), i.e. when the launch's
+ * results are wrong.  Kernels only set it; the caller reads and clears it at its next
+ * synchronisation (srf_amd.ops.check_faults).  NULL: no reporting. */
+int srf_set_fault_flag(void* flag);
 /* Gradients are written (not accumulated): g_emb [B*T][N][din], g_W like W,
  * g_bias like bias. */
 int srf_route_dr_bwd(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
@@ -152,9 +158,13 @@ typedef struct {
                                   utterance (0 or 1: one; at most 8, equal over a launch's ranges).
                                   A group splits the input capsules and adds its partial sums inside
                                   the launch, spin-waiting on its members: the launch's
-                                  B * n * group workgroups must be resident together, so it is
-                                  refused above the device's CU count and the caller runs no other
-                                  grouped launch concurrently.  Other shapes ignore it. */
+                                  B * n * group workgroups must be resident together.  The library
+                                  cannot see what else holds CUs: it refuses a launch above the
+                                  device's CU count less 4, and the caller keeps other grouped
+                                  launches, and kernels that occupy CUs for long (collectives),
+                                  off the device meanwhile.  A member that waits too long stops
+                                  and sets the fault word (srf_set_fault_flag): the results of
+                                  that launch are then wrong.  Other shapes ignore it. */
 } srf_sdr_range;
 /* pose_n fp8: 0 fp32 pose, 1 fp8 pose (fp32 u), 2 fp8 pose storing u in bf16 */
 int srf_route_sdr_pose_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,

@@ -42,6 +42,7 @@ _SIGNATURES = {
     'srf_version': (_c_int, []),
     'srf_last_error': (ctypes.c_char_p, []),
     'srf_set_seed_source': (_c_int, [_vp]),
+    'srf_set_fault_flag': (_c_int, [_vp]),
     'srf_route_dr_auto_chunks': (_c_int, [_c_int] * 8),
     'srf_route_dr_saved_floats': (_c_size, [_c_int] * 5),
     'srf_route_dr_fwd_workspace': (_c_size, [_c_int] * 10),

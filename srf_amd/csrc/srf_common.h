@@ -8,6 +8,8 @@ namespace srf {
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 // device step counter set by srf_set_seed_source for this process (NULL: none)
 const unsigned long long* seed_source();
+// device word set by srf_set_fault_flag for this process (NULL: none)
+unsigned* fault_flag();
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 }  // namespace srf
 

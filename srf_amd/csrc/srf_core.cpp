@@ -12,6 +12,7 @@ thread_local char g_err[512] = "";
 // tensors on its own per-device worker thread, and the backward kernels must
 // rebuild the forward's dropout masks from the same counter.
 std::atomic<const unsigned long long*> g_seed_src{nullptr};
+std::atomic<unsigned*> g_fault{nullptr};
 }
 
 namespace srf {
@@ -22,6 +23,7 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 const unsigned long long* seed_source() { return g_seed_src.load(std::memory_order_acquire); }
+unsigned* fault_flag() { return g_fault.load(std::memory_order_acquire); }
 }  // namespace srf
 
 extern "C" {
@@ -29,6 +31,10 @@ int srf_version(void) { return 1; }
 
 int srf_set_seed_source(const void* step_counter) {
   g_seed_src.store(static_cast<const unsigned long long*>(step_counter), std::memory_order_release);
+  return 0;
+}
+int srf_set_fault_flag(void* flag) {
+  g_fault.store(static_cast<unsigned*>(flag), std::memory_order_release);
   return 0;
 }
 const char* srf_last_error(void) { return g_err; }

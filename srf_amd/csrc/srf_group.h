@@ -14,9 +14,14 @@
 // Residency: the members spin-wait on each other, so all B * items * G workgroups of
 // a launch must be resident together (one per CU for these kernels): the host checks
 // B * items * G <= CUs, and the caller runs at most one grouped launch at a time.
-// Each spin is bounded: past kSpinMax polls a member sets the item's timeout word and
-// stops waiting (its results are then wrong, never a hang), and every later wait of
-// the launch returns at once.
+// That is an assumption about the device, not something a launch can check: another
+// stream's kernels (the stack's own inner layers, RCCL collectives overlapping a
+// backward) hold CUs too, so the host check keeps kReserveCUs free and the callers
+// size G for what else they run.  Each spin is therefore bounded: past kSpinMax polls a
+// member sets the item's timeout word and the process's fault word (srf_set_fault_flag)
+// and stops waiting -- its results are then wrong, never a hang -- and every later wait
+// of the launch returns at once; the host reads the fault word at its next sync
+// (srf_amd.ops.check_faults) and fails the step.
 #pragma once
 #include <algorithm>
 
@@ -27,11 +32,13 @@ namespace srf_grp {
 
 constexpr int kMaxGroup = 8;
 constexpr unsigned kSpinMax = 1u << 20;
+constexpr int kReserveCUs = 4;   // CUs a grouped launch leaves to other streams
 
 struct Grp {
   int G;                // workgroups per utterance (1: no exchange)
   int B;                // utterances of the launch
   unsigned xoff, coff;  // floats from the item's workspace to the exchange area / the counters
+  unsigned* fault;      // the process's fault word (srf_set_fault_flag), or NULL
 };
 
 // Item workspace: `pre` floats of the kernel's own (the stream backward's gL scratch),
@@ -42,7 +49,9 @@ __host__ __device__ inline size_t xoff(size_t pre, int B) { return coff(pre) + (
 __host__ __device__ inline size_t floats(size_t pre, int B, int JD) {
   return xoff(pre, B) + (size_t)2 * B * kMaxGroup * JD;
 }
-inline Grp make(int G, int B, size_t pre) { return Grp{G, B, (unsigned)xoff(pre, B), (unsigned)coff(pre)}; }
+inline Grp make(int G, int B, size_t pre) {
+  return Grp{G, B, (unsigned)xoff(pre, B), (unsigned)coff(pre), srf::fault_flag()};
+}
 
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
@@ -76,6 +85,7 @@ __device__ __forceinline__ void allreduce(float* part, int JD, float* ws, const 
       __builtin_amdgcn_s_sleep(2);
       if (++spins > kSpinMax) {
         __hip_atomic_store(cnt + X.B, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (X.fault) __hip_atomic_store(X.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
@@ -104,9 +114,9 @@ inline int setup(const srf::SeqItems& items, int B, size_t pre, Grp& X, hipStrea
   int dev = 0, cus = 0;
   SRF_HIP_TRY(hipGetDevice(&dev));
   SRF_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  SRF_REQUIRE((long)B * items.n * G <= cus,
-              "SDR recurrence: %d utterances x %d ranges x group %d workgroups exceed the %d CUs they must share", B,
-              items.n, G, cus);
+  SRF_REQUIRE((long)B * items.n * G <= cus - kReserveCUs,
+              "SDR recurrence: %d utterances x %d ranges x group %d workgroups exceed the %d CUs they may take (%d "
+              "kept free)", B, items.n, G, cus - kReserveCUs, kReserveCUs);
   for (int k = 0; k < items.n; ++k) {
     SRF_REQUIRE(items.it[k].ws, "SDR recurrence: a grouped launch needs the range workspace");
     SRF_HIP_TRY(hipMemsetAsync(items.it[k].ws + X.coff, 0, srf::align_up((size_t)(B + 1) * 4, 16), st));

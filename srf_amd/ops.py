@@ -417,6 +417,38 @@ def ctc_loss(logits, labels, label_len, logit_len, blank):
 
 
 # ---------------------------------------------------------------------------
+# Fault word of the grouped SDR recurrences (srf_set_fault_flag): one per process
+GROUP_RESERVE_CUS = 4   # CUs a grouped launch leaves free (srf_group.h kReserveCUs)
+_FAULT = {}
+
+
+def fault_flag(dev):
+    """The process's device fault word on ``dev``, created and registered once
+    (srf_set_fault_flag is process-wide; one process drives one GPU)."""
+    dev = torch.device(dev)
+    f = _FAULT.get(dev)
+    if f is None:
+        if _FAULT:
+            raise RuntimeError(f'one process drives one GPU: the fault word already lives on {next(iter(_FAULT))}')
+        f = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().srf_set_fault_flag(f.data_ptr()), 'srf_set_fault_flag')
+        _FAULT[dev] = f
+    return f
+
+
+def check_faults():
+    """Raise if a grouped SDR recurrence gave up waiting for its members since the
+    last check (its results, and every gradient computed from them, are wrong); the
+    word is cleared.  Reads a device word: a synchronisation point."""
+    for dev, f in _FAULT.items():
+        if int(f.item()):
+            f.zero_()
+            raise RuntimeError('a grouped SDR recurrence timed out waiting for its workgroups (they were not '
+                               'resident together): the step\'s results are wrong; run with fewer workgroups per '
+                               'utterance (SdrStackPlan last_group) or less concurrent device work')
+
+
+# ---------------------------------------------------------------------------
 # SDR stack: every SDR layer and the LN + dropout between them, as a wavefront
 class SdrStackPlan:
     """Static plan of an SDR stack (sequence_router_naive.py:145-191 with
@@ -478,6 +510,9 @@ class SdrStackPlan:
                     for (N, din, J, D, mf) in layers]
         self.streamed = [bool(L_.srf_route_sdr_couplings_required(N * self.win, J, D, iters))
                          for (N, din, J, D, mf) in layers]
+        # set by the caller when collectives overlap the backward (SequenceRouter with
+        # grad buckets at world > 1): the last layer's backward is then not grouped
+        self.collectives_overlap = False
         if last_group is None or isinstance(last_group, (tuple, list)):
             self.last_group = None if last_group is None else tuple(int(g) for g in last_group)
         else:
@@ -496,9 +531,15 @@ class SdrStackPlan:
         the forward's exchanges cost more than they save (G = 2 / 4 slower)."""
         if l != self.L - 1 or not (self.streamed[l] or self.store_couplings):
             return 1
+        if backward and self.collectives_overlap:
+            # bucketed all-reduces run beside the backward: RCCL's kernels hold CUs the
+            # group's members would have to share, so the backward is not grouped
+            return 1
         if self.last_group is not None:
             return max(1, self.last_group[int(backward)])
-        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        # the library keeps GROUP_RESERVE_CUS free (srf_group.h); the inner layers'
+        # recurrences hold B CUs each on stream A
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count - GROUP_RESERVE_CUS
         if not self.streamed[l]:
             return 2 if backward and self.store_couplings and self.B * (self.L + 1) <= cus else 1
         return max(1, min(8, (cus - self.B * (self.L - 1)) // self.B))
@@ -608,6 +649,8 @@ class SdrStack(torch.autograd.Function):
         L_ = _lib.lib()
         P, B, T, L = plan, plan.B, plan.T, plan.L
         dev = emb0.device
+        if not torch.cuda.is_current_stream_capturing():
+            fault_flag(dev)   # registered before the first grouped launch (never inside a capture)
         Ws, bs = params[0:2 * L:2], params[1:2 * L:2]
         gammas, betas = params[2 * L::2], params[2 * L + 1::2]
         _check_dev('emb0', emb0, (B, T, P.layers[0][0], P.layers[0][1]))

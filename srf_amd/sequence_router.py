@@ -290,7 +290,10 @@ class SequenceRouter(torch.nn.Module):
             params += [self.P(f'ln_mid{l + 1}_{t}') for l in range(last) for t in ('gamma', 'beta')]
             self._on_grad(emb, [f'{w}{l}' for l in range(self.enc_num) for w in ('W', 'b')]
                           + [f'ln_mid{l + 1}_{t}' for l in range(last) for t in ('gamma', 'beta')])
-            v = ops.sdr_stack(emb, self._stack_plan(B, T2), training, p_mid, seed, params)
+            plan = self._stack_plan(B, T2)
+            # bucketed all-reduces overlapping the backward take CUs a grouped recurrence needs
+            plan.collectives_overlap = self.grad_buckets is not None and self.grad_buckets.active()
+            v = ops.sdr_stack(emb, plan, training, p_mid, seed, params)
             self._on_grad(v, [f'ln_mid{last + 1}_gamma', f'ln_mid{last + 1}_beta', 'ln_output_gamma',
                               'ln_output_beta'])
             return ops.CapsHead.apply(v, self.P(f'ln_mid{last + 1}_gamma'), self.P(f'ln_mid{last + 1}_beta'),

@@ -122,6 +122,10 @@ class GradBuckets:
                 hi, cur = lo, []
         self.of = {n: k for k, (_, _, ns) in enumerate(self.buckets) for n in ns}
         self.begin()
+        if self.active() and dist.is_initialized() and dist.get_backend() == 'nccl':
+            # every rank constructs the buckets at the same point: one collective now sets
+            # up the communicator, so that no rank's first collective is a captured one
+            dist.all_reduce(torch.zeros(1, device=model.flat_grad.device), op=dist.ReduceOp.SUM)
 
     def active(self):
         return self.force or _world() > 1
@@ -292,18 +296,22 @@ class GraphedTrainStep:
         self.buckets = b if (b is not None and b.active() and dist.is_initialized()
                              and dist.get_backend() == 'nccl') else None
         hook = getattr(model, 'grad_hook', None)
-        if self.buckets is None:
-            model.grad_hook = None
         # the warm-up steps run the training forward, which updates the BatchNorm moving
-        # statistics: restore them, so that building a graph changes no model state
+        # statistics: restore them, so that building a graph changes no model state.
+        # They issue no collectives: only this rank may be building a graph at this step
+        # (GraphCache agrees on capture steps, but a direct caller need not), and the
+        # captured collectives do not execute until the replay, which every rank joins
         buffers = [b_.clone() for b_ in model.buffers()]
         try:
+            model.grad_hook = None
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 for _ in range(warmup):
-                    self._fwd_bwd()
+                    self._fwd_bwd(collectives=False)
             torch.cuda.current_stream(dev).wait_stream(side)
+            if self.buckets is not None:
+                model.grad_hook = hook
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, pool=pool):
                 self.nll = self._fwd_bwd()
@@ -333,17 +341,18 @@ class GraphedTrainStep:
         self.inp_len.copy_(host_len, non_blocking=True)
         self.tar_len.copy_(torch.as_tensor(tar_len), non_blocking=True)
 
-    def _fwd_bwd(self):
+    def _fwd_bwd(self, collectives=True):
         self.counter.add_(1)
-        if self.buckets is not None:
-            self.buckets.begin()
+        buckets = self.buckets if collectives else None
+        if buckets is not None:
+            buckets.begin()
         y_pred = self.model(self.feats, input_lengths=self.inp_len, training=True)
         logit_len = ceil_div(self.inp_len, self.in_len_div)
         pe_loss, g_logits = ctc.ctc_loss_and_grad(self.labels, y_pred, self.tar_len, logit_len, self.blank_idx,
                                                   1.0 / float(self.batch * self.n_gpus))
         y_pred.backward(g_logits)
-        if self.buckets is not None:
-            self.buckets.finish()
+        if buckets is not None:
+            buckets.finish()
         return pe_loss
 
     @property
@@ -386,7 +395,14 @@ class GraphCache:
     (process_train_step), which costs no more than an uncaptured step.  All graphs
     share one memory pool (they never run concurrently), so the cache holds one
     step's worth of activations, not one per shape.  A new label length beyond a
-    cached graph's capacity re-captures that shape with a larger one."""
+    cached graph's capacity re-captures that shape with a larger one.
+
+    Under data parallelism each rank crops its own batch, so the ranks see different
+    shapes.  Whether a step replays or captures a graph, or runs eagerly, is agreed
+    over the process group (one int MIN all-reduce per step on a CPU gloo group): a
+    step takes the graph path only when every rank can, so every rank issues the same
+    gradient collectives in the same order (from its replay or its eager backward) and
+    captures only when all do."""
 
     def __init__(self, in_len_div, model, optimizer, n_gpus, blank_idx, max_graphs=32, warmup=1, min_hits=2):
         self.args = (in_len_div, model, optimizer, n_gpus, blank_idx)
@@ -396,6 +412,17 @@ class GraphCache:
         self.captures = 0
         self.eager_steps = 0
         self.pool = None
+        self.flag_group = None
+        if _world() > 1:   # every rank constructs the cache at the same point
+            self.flag_group = dist.group.WORLD if dist.get_backend() == 'gloo' else dist.new_group(backend='gloo')
+
+    def agree(self, want):
+        """True when every rank of the group wants the graph path this step."""
+        if self.flag_group is None:
+            return want
+        t = torch.tensor([int(bool(want))], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.flag_group)
+        return bool(t.item())
 
     def step(self, inputs, loss_state=None, frame_state=None, samples=None):
         feats, labels, inp_len, tar_len = inputs
@@ -406,15 +433,18 @@ class GraphCache:
             g.close()
             del self.graphs[key]
             g = None
+        want = True
         if g is None:
             hits = self.seen.pop(key, 0) + 1
             self.seen[key] = hits
             while len(self.seen) > 4 * self.max_graphs:
                 self.seen.popitem(last=False)
-            if hits < self.min_hits:
-                self.eager_steps += 1
-                return process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_state, n_gpus,
-                                          blank_idx, samples)
+            want = hits >= self.min_hits
+        if not self.agree(want):
+            self.eager_steps += 1
+            return process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_state, n_gpus,
+                                      blank_idx, samples)
+        if g is None:
             if self.pool is None:
                 self.pool = torch.cuda.graph_pool_handle()
             g = GraphedTrainStep(in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=self.warmup,
@@ -465,11 +495,21 @@ def distributed_train_step(dataset, in_len_div, model, optimizer, loss_state, fr
         if index % 50 == 0 and index > 0 and samples is not None and loss_state is not None:
             # every rank joins the cross-replica read, logging or not (:218-221)
             n_samples, loss = reduce_metrics(samples, loss_state)
+            _check_faults(dev)
             if log is not None:
                 prog = n_samples / train_num * 100 if train_num else float('nan')
                 log('STEP', optimizer.iterations, prog, loss, optimizer.current_lr())
         index += 1
+    _check_faults(dev)
     return index
+
+
+def _check_faults(dev):
+    """Fail the run if a grouped SDR recurrence timed out since the last check
+    (ops.check_faults; a device read, so only at points that synchronise anyway)."""
+    if torch.device(dev).type == 'cuda':
+        from . import ops
+        ops.check_faults()
 
 
 @torch.no_grad()

@@ -26,7 +26,8 @@ def _fresh_dropout_seed_source():
     (srf_set_seed_source): a training-step test attaches one, and the kernel tests
     that restate dropout masks (tests/torch_ref.py) assume the per-call seeds alone."""
     yield
-    from srf_amd import trainer_sr
+    from srf_amd import ops, trainer_sr
+    ops.check_faults()   # no grouped SDR recurrence of the test timed out (srf_set_fault_flag)
     if trainer_sr._SEED_COUNTERS:
         import torch
         from srf_amd import _lib

@@ -168,3 +168,78 @@ def test_gloo_bucketed_allreduce_equals_flat():
         assert len(buckets) >= 3
         assert buckets[0][1] == len(total) and buckets[-1][0] == 0
         assert all(buckets[k + 1][1] == buckets[k][0] for k in range(len(buckets) - 1))
+
+
+class _FakeGraphStep:
+    """GraphedTrainStep stand-in: capture issues no collective (the real warm-up issues
+    none since round 5), each replay one (the flat all-reduce or the captured buckets)."""
+    log = None
+
+    def __init__(self, in_len_div, inputs, model, optimizer, n_gpus, blank_idx, warmup=1, pool=None):
+        self.model = model
+        self.shape = (inputs[0].shape[0], int(inputs[2].max()))
+        _FakeGraphStep.log.append('capture')
+
+    def accepts(self, feats, labels, inp_len):
+        return (feats.shape[0], int(inp_len.max())) == self.shape
+
+    def refill(self, *a):
+        pass
+
+    def close(self):
+        pass
+
+    def __call__(self, *a):
+        _FakeGraphStep.log.append('replay')
+        dist.all_reduce(self.model.flat_grad)
+
+
+def _cache_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    log = []
+    _FakeGraphStep.log = log
+
+    def eager(in_len_div, inputs, model, *a):
+        log.append('eager')
+        dist.all_reduce(model.flat_grad)
+    trainer_sr.GraphedTrainStep = _FakeGraphStep
+    trainer_sr.process_train_step = eager
+    model = FlatModel(4)
+    cache = trainer_sr.GraphCache(4, model, None, world, 0, min_hits=2)
+    # each rank crops its own batches: different crop lengths, seen at different steps
+    lens = [[100, 100, 100, 120, 120, 100, 120], [90, 95, 90, 90, 95, 95, 90]][rank]
+    for T in lens:
+        cache.step((torch.zeros(3, T, 1), torch.zeros(3, 2), torch.tensor([T, T - 5, T - 9]), torch.zeros(3)))
+    q.put((rank, log, cache.captures, cache.eager_steps))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_graph_cache_agrees_on_capture_steps():
+    """GraphCache under data parallelism (world 2, gloo): ranks crop to different
+    lengths, so a rank that has seen its shape twice would capture or replay while
+    another still runs eagerly.  The cache agrees over the group: a step takes the
+    graph path only when every rank can, so every rank issues one gradient collective
+    per step in the same order (the run would hang otherwise) and captures only when
+    all do."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cache_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    paths = [[x for x in log if x != 'capture'] for _, log, _, _ in res]
+    graph = [[x == 'replay' for x in p] for p in paths]
+    assert len(paths[0]) == len(paths[1]) == 7 and graph[0] == graph[1]
+    # step 1: rank 0's 100 is ready, rank 1's 95 is not -> both eager; step 2: both
+    # ready (100, 90) -> both capture; step 3: rank 0 sees 120 first -> both eager,
+    # though rank 1 holds a graph for 90; steps 4-6: graph on both
+    assert graph[0] == [False, False, True, False, True, True, True]
+    assert res[0][2] == res[1][2] == 2 and res[0][3] == res[1][3] == 3
