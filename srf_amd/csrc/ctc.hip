@@ -15,10 +15,6 @@
 #include "srf_common.h"
 #include "../../include/srf.h"
 
-#ifndef SRF_CTC_DBG
-#define SRF_CTC_DBG 0
-#endif
-
 namespace {
 
 __device__ __forceinline__ float lse2(float a, float b) {
@@ -191,9 +187,6 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
                                                             int Lmax, int blank, int want_beta,
                                                             float* __restrict__ nll, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-#if SRF_CTC_DBG
-  const unsigned long long t_beg = __builtin_amdgcn_s_memtime();
-#endif
   const int Smax = 2 * Lmax + 1;
   int* ext = reinterpret_cast<int*>(smem);
   float* row = smem + Smax;
@@ -253,9 +246,6 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
     }
   }
   __syncthreads();
-#if SRF_CTC_DBG
-  const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
-#endif
   if constexpr (KM > 0) {
     if (threadIdx.x >= 64) return;
     if (!is_beta) {
@@ -264,12 +254,6 @@ __global__ __launch_bounds__(256) void ctc_recursion_kernel(const float* __restr
     } else {
       beta_wave<KM>(ext, lp, C, S, Tb, Smax, blank, out);
     }
-#if SRF_CTC_DBG
-    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0 && b == 0)
-      printf("ctc blk %d beta %d: prologue %llu recursion %llu (S=%d Tb=%d C=%d)\n", b, (int)is_beta, t_pro - t_beg,
-             t_end - t_pro, S, Tb, C);
-#endif
     return;
   }
   if (!is_beta) {

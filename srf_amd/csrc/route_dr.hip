@@ -27,18 +27,6 @@
 namespace {
 
 constexpr float kSquashEps = 1e-7f;  // naive:248
-#ifndef SRF_GU_SPLITGX
-#define SRF_GU_SPLITGX 0
-#endif
-#ifndef SRF_GUX16_PEEL
-#define SRF_GUX16_PEEL 0   // 1: route_gux16_kernel's capsule loop without exits in its body (C4 r04ii A/B: no change)
-#endif
-#ifndef SRF_GUX16_OCC
-#define SRF_GUX16_OCC 2   // route_gux16_kernel workgroups (of 4 waves) per CU: 2, or 3 (two-slot ring)
-#endif
-#ifndef SRF_GUX16_DBG_NOATOM
-#define SRF_GUX16_DBG_NOATOM 0
-#endif
 
 // Opt-in profiling hook (srf_route_dr_set_timing_events): events recorded on the
 // launch stream around each forward routing-pass kernel of the next
@@ -644,24 +632,11 @@ __global__ __launch_bounds__(256, (DIN <= 16 ? 4 : 3)) void route_gu_kernel(
       f4 gx[NCT];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
-#if SRF_GU_SPLITGX
-        // two independent accumulator chains (A/B variant)
-        f4 ga0 = f4{0.f, 0.f, 0.f, 0.f}, ga1 = ga0;
-#pragma unroll
-        for (int t = 0; t < TW; ++t)
-#pragma unroll
-          for (int k = 0; k < 4; k += 2) {
-            ga0 = mfma16x16x4(wt[ct][t][k], ga[t][k], ga0);
-            ga1 = mfma16x16x4(wt[ct][t][k + 1], ga[t][k + 1], ga1);
-          }
-        gx[ct] = ga0 + ga1;
-#else
         gx[ct] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < TW; ++t)
 #pragma unroll
           for (int k = 0; k < 4; ++k) gx[ct] = mfma16x16x4(wt[ct][t][k], ga[t][k], gx[ct]);
-#endif
       }
       const int w = i / N, n = i - w * N;
       const int ts = loc.t + w - lpad;
@@ -889,6 +864,7 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 constexpr int kGux16NW = 4;
+constexpr int kGux16Occ = 2;   // workgroups per CU (three, with a two-slot ring, measured slower)
 
 __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -897,7 +873,7 @@ __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c)
 // The lane max of |gu| also goes to *gumax (one atomic max per wave; the caller zeroes
 // it): route_gw16s_kernel takes its per-layer exponent from it.
 template <int R>
-__global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
+__global__ __launch_bounds__(256, kGux16Occ) void route_gux16_kernel(
     const float* __restrict__ WT, const float* __restrict__ hdr, int F, int T, int N, int lpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
     const float* __restrict__ gs, float* __restrict__ g_emb, const float* __restrict__ cst,
@@ -970,9 +946,9 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
 #pragma unroll
     for (int p = 0; p < 2; ++p) wo[ks][p] = (uint32_t)((((2 * j + ks) * 2 + h) * DIN + fl) * 16) + p * wplane;
   const uint32_t co = (uint32_t)(j * Fs + fv) * 4;
-  constexpr int NB = SRF_GUX16_OCC >= 3 ? 2 : 3;
-  h8 wt_b[3][2][2];    // [slot][ks][hi | lo] (NB of them in use)
-  float c_b[3][RV], g_b[3][RV];
+  constexpr int NB = 3;   // operand ring slots
+  h8 wt_b[NB][2][2];   // [slot][ks][hi | lo]
+  float c_b[NB][RV], g_b[NB][RV];
   auto fetch = [&](auto slot, int i) {
     constexpr int sl = decltype(slot)::value;
     const uint32_t swo = (uint32_t)i * NT * 16 * DIN * 2;
@@ -1058,51 +1034,19 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
 #define SRF_GUX16_FETCH(SL) \
   fetch(SL{}, next_i());    \
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (NB == 3) {
-    if (ncap > 0) {
-      SRF_GUX16_FETCH(S0)
-      SRF_GUX16_FETCH(S1)
-    }
-#if SRF_GUX16_PEEL
-    // whole triples in the loop and the one or two capsules left after it: no exit
-    // inside the body, whose path back to the header (the structurizer's) made the
-    // first wait of every triple count one slot in flight instead of two
-    int k = 0;
-    for (; k + NB <= ncap; k += NB) {
-      SRF_GUX16_FETCH(S2)
-      compute(S0{});
-      SRF_GUX16_FETCH(S0)
-      compute(S1{});
-      SRF_GUX16_FETCH(S1)
-      compute(S2{});
-    }
-    if (k < ncap) {
-      compute(S0{});
-      if (k + 1 < ncap) compute(S1{});
-    }
-#else
-    for (int k = 0; k < ncap; k += NB) {
-      SRF_GUX16_FETCH(S2)
-      compute(S0{});
-      if (k + 1 >= ncap) break;
-      SRF_GUX16_FETCH(S0)
-      compute(S1{});
-      if (k + 2 >= ncap) break;
-      SRF_GUX16_FETCH(S1)
-      compute(S2{});
-    }
-#endif
-  } else {   // two slots: capsule k + 1 in flight while capsule k is formed
-    if (ncap > 0) {
-      SRF_GUX16_FETCH(S0)
-    }
-    for (int k = 0; k < ncap; k += 2) {
-      SRF_GUX16_FETCH(S1)
-      compute(S0{});
-      if (k + 1 >= ncap) break;
-      SRF_GUX16_FETCH(S0)
-      compute(S1{});
-    }
+  if (ncap > 0) {
+    SRF_GUX16_FETCH(S0)
+    SRF_GUX16_FETCH(S1)
+  }
+  for (int k = 0; k < ncap; k += NB) {
+    SRF_GUX16_FETCH(S2)
+    compute(S0{});
+    if (k + 1 >= ncap) break;
+    SRF_GUX16_FETCH(S0)
+    compute(S1{});
+    if (k + 2 >= ncap) break;
+    SRF_GUX16_FETCH(S1)
+    compute(S2{});
   }
 #undef SRF_GUX16_FETCH
 #pragma unroll
@@ -1117,11 +1061,7 @@ __global__ __launch_bounds__(256, SRF_GUX16_OCC) void route_gux16_kernel(
     float v = 0.f;
 #pragma unroll
     for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots + s) * SROW + rem];
-#if SRF_GUX16_DBG_NOATOM   // timing experiment only (wrong results): plain stores instead of atomics
-    if (fo >= 0 && fo < F && v != 0.f) g_emb[((size_t)fo * N + n0) * DIN + rem] = v;
-#else
     if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
-#endif
   }
 }
 
@@ -2036,7 +1976,7 @@ int gu_n_per(const Geom& g, int nw) {
 inline size_t gux16_lds_bytes(const Geom& g, int n_per) {
   return (size_t)kGux16NW * (31 + gu_window(g)) * (n_per * 32 + 4) * sizeof(float);
 }
-constexpr size_t kGux16LdsMax = (160 / SRF_GUX16_OCC - 4) * 1024;   // SRF_GUX16_OCC workgroups per CU
+constexpr size_t kGux16LdsMax = (160 / kGux16Occ - 4) * 1024;   // kGux16Occ workgroups per CU
 // route_gux16_kernel (split-fp16 32x32 tiles) for din = dout = 32 with stored
 // couplings (route_gux_kernel otherwise).  A function of the geometry only: the
 // forward's prep writes the kernel's split W^T planes in place of the fp32 W^T under
@@ -2048,7 +1988,7 @@ inline bool use_gux16(const Geom& g) {
 // n-chunk size: fewest rounds of two workgroups per CU, then fewest capsules each
 int gux16_n_per(const Geom& g) {
   const int base = (g.F() + 31) / 32 * ((g.J + kGux16NW - 1) / kGux16NW);
-  const int slots = 256 * SRF_GUX16_OCC;
+  const int slots = 256 * kGux16Occ;
   int best = 1;
   double best_cost = 1e30;
   for (int n_per = 1; n_per <= g.N; ++n_per) {

@@ -7,10 +7,7 @@
 namespace srf {
 
 // Row tiles (of 32 rows) per wave of route_fwd32 / route_bwd32 for din 8, 16.
-#ifndef SRF_FWD32_TW
-#define SRF_FWD32_TW 4
-#endif
-constexpr int kFwd32TW = SRF_FWD32_TW;
+constexpr int kFwd32TW = 4;
 // Frame stride of the stored couplings (frame-minor layout, 32-frame aligned).
 __host__ __device__ inline int fwd32_frame_stride(int F) { return (F + 31) / 32 * 32; }
 

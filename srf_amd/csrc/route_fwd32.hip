@@ -37,53 +37,18 @@
 #include "srf_common.h"
 #include "route_fwd32.h"
 
-// Timing-experiment variants (never in the shipped build): 1 = no next-capsule
-// loads, 2 = no cross-wave exchange, 3 = no softmax (acc += u only),
-// 4 = s_memtime phase breakdown printed by two waves.
-#ifndef SRF_FWD32_DBG
-#define SRF_FWD32_DBG 0
+// Timing builds of the pipelined passes (wrong results, never shipped; scripts/build_ab.sh
+// + scripts/gpu_ab_route.sh): bit 1 = x of the chunk's first capsule, 2 = its W and bias,
+// 4 = no per-capsule barrier, 8 = no x reloads, 16 = no W reloads.
+#ifndef SRF_FWD32P_DBG
+#define SRF_FWD32P_DBG 0
 #endif
-// 1: issue the next capsule's loads right after the MFMAs (they then wait for the
-// queued MFMAs to read their operand registers); 0: after the softmax barrier.
-// r02: 1 was ~2% faster in the routing microbenchmark but ~4% slower inside the
-// graphed training step (bench.py), so 0 stays the default.
-#ifndef SRF_FWD32_FETCH_EARLY
-#define SRF_FWD32_FETCH_EARLY 0
-#endif
-// 1: the second half of a workgroup's waves runs at s_setprio 1 (pass kernels;
-// MI355X_MICROARCH "static priority for the younger half"): ~3% on the backward pass
-// 1: the next capsule's operands are loaded between the MFMA steps of this capsule,
-// each register group as soon as the last MFMA reading it has issued
-#ifndef SRF_FWD32_PROG
-#define SRF_FWD32_PROG 1
-#endif
-#ifndef SRF_FWD32_PRIO
-#define SRF_FWD32_PRIO 1
-#endif
-// 1: tile-major pose in the r >= 1 forward pass: tile t's MFMA chain, then its operand
-// reloads, then the agreement dots of tile t - 1 (whose Vc fragments were read from
-// LDS before tile t's MFMAs), so the dots overlap the matrix pipe
-#ifndef SRF_FWD32_TM
-#define SRF_FWD32_TM 1
-#endif
-// 1: the tile-major schedule for din 32 as well (A/B knob; pose_prog measured faster)
-#ifndef SRF_FWD32_TM32
-#define SRF_FWD32_TM32 0
-#endif
-// 0: the compiler may move the operand reloads among the tile's MFMAs (A/B knob)
-#ifndef SRF_FWD32_TMSB
-#define SRF_FWD32_TMSB 1
-#endif
-// 1: softmax normaliser by the fast reciprocal instead of an IEEE division
-#ifndef SRF_BWD32_CPREFETCH
-#define SRF_BWD32_CPREFETCH 0   // 1: couplings of capsule i+1 loaded during capsule i (4 more live registers)
-#endif
-#ifndef SRF_SPLIT_DBG
-#define SRF_SPLIT_DBG 0
-#endif
-#ifndef SRF_FWD32_FASTDIV
-#define SRF_FWD32_FASTDIV 0
-#endif
+// Schedule choices of the passes, fixed by measurement (rounds 2-4): the next capsule's
+// operands load between the MFMA steps of this capsule, each register group as soon as
+// its last reader has issued (pose_prog; issuing them all after the MFMAs measured ~4 %
+// slower in the graphed step); din 8 / 16 run the pose tile-major with the agreement dots
+// of tile t - 1 beside tile t's MFMAs (din 32: pose_prog measured faster); the second
+// half of a din <= 16 workgroup's waves runs at s_setprio 1 (~3 % on the backward pass).
 
 namespace {
 
@@ -380,11 +345,7 @@ __global__ __launch_bounds__(256) void prep32_kernel(PrepArgs P) {
 // All operands come through buffer loads: one descriptor per array, the per-lane
 // byte offset in voffset (fixed per tile), the per-capsule / per-plane offset in
 // soffset.  Invalid window frames read the zero row at the end of each x plane.
-#ifndef SRF_FWD32_TW
-#define SRF_FWD32_TW 4
-#endif
-constexpr int kTW = SRF_FWD32_TW;        // 32-row tiles per wave (din 8, 16; din 32: Fwd32Plan::TW)
-static_assert(kTW == srf::kFwd32TW, "route_fwd32.h and route_fwd32.hip disagree on the row tiles per wave");
+constexpr int kTW = srf::kFwd32TW;       // 32-row tiles per wave (din 8, 16; din 32: Fwd32Plan::TW)
 constexpr int kMaxNW = 32 / kTW;         // J*dout <= 1024
 constexpr int kWavesPerEU = 8 / kTW;
 
@@ -508,12 +469,27 @@ __device__ __forceinline__ f16v pose_chain(const h8 (&a)[SplitFrags<DIN>::NA], c
 
 // The pose tiles of one capsule (as pose_chain, bias first) with the next capsule's
 // operands loaded into each register group right after its last reader is issued.
-template <int DIN, int TW>
+// XL (din 32): the next capsule's x fragments come from the workgroup's LDS copy xl
+// (kXlPiece bytes per fragment, this lane's 16 bytes at xl + q * kXlPiece for b[q],
+// staged by x_dma) instead of one global load per wave.
+constexpr int kXlPiece = 1024;
+// LDS read of the shared x fragments as inline asm: a plain read of the buffer the DMA
+// (global_load_lds) fills would make the compiler wait for every DMA in flight (vmcnt(0))
+// before it, draining the operand prefetch; pose_prog waits for these reads (lgkmcnt)
+// itself, before the MFMAs that consume them.
+__device__ __forceinline__ h8 xl_read(const char* p) {
+  h8 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"((uint32_t)reinterpret_cast<uintptr_t>(p)));
+  return r;
+}
+template <int DIN, int TW, bool XL = false>
 __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones, f16v (&u)[TW],
                                           const Rsrc3& rs, uint32_t wvo, uint32_t bvo, uint32_t xvo, int h,
                                           uint32_t wplane_b, uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
-                                          uint32_t bcap_b) {
+                                          uint32_t bcap_b, const char* xl = nullptr) {
   constexpr uint32_t TSTEP = 32 * DIN * 2;
+  if constexpr (XL)   // the x fragments the previous call read from LDS (xl_read) have arrived
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fr.b[0]), "+v"(fr.b[1]), "+v"(fr.b[2]), "+v"(fr.b[3]));
 #pragma unroll
   for (int t = 0; t < TW; ++t) u[t] = mfma32(fr.bias[t], ones, f16v{});
   __builtin_amdgcn_sched_barrier(0);
@@ -532,11 +508,13 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       u[t] = mfma32h(fr.a[t][3], fr.b[2], u[t]);
     }
     __builtin_amdgcn_sched_barrier(0);
+#if !(SRF_FWD32P_DBG & 16)
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
       fr.a[t][1] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b);
       fr.a[t][3] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b + 32);
     }
+#endif
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < TW; ++t) {   // W1 x2
@@ -544,8 +522,15 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       u[t] = mfma32h(fr.a[t][2], fr.b[3], u[t]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    fr.b[1] = hload(rs.x, xvo, xplane_b);
-    fr.b[3] = hload(rs.x, xvo, xplane_b + 32);
+#if !(SRF_FWD32P_DBG & 8)
+    if constexpr (XL) {
+      fr.b[1] = xl_read(xl + 1 * kXlPiece);
+      fr.b[3] = xl_read(xl + 3 * kXlPiece);
+    } else {
+      fr.b[1] = hload(rs.x, xvo, xplane_b);
+      fr.b[3] = hload(rs.x, xvo, xplane_b + 32);
+    }
+#endif
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < TW; ++t) {   // W1 x1
@@ -553,13 +538,22 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       u[t] = mfma32h(fr.a[t][2], fr.b[2], u[t]);
     }
     __builtin_amdgcn_sched_barrier(0);
+#if !(SRF_FWD32P_DBG & 16)
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
       fr.a[t][0] = hload(rs.w, wvo + t * TSTEP, wcap_b);
       fr.a[t][2] = hload(rs.w, wvo + t * TSTEP, wcap_b + 32);
     }
-    fr.b[0] = hload(rs.x, xvo, 0);
-    fr.b[2] = hload(rs.x, xvo, 32);
+#endif
+#if !(SRF_FWD32P_DBG & 8)
+    if constexpr (XL) {
+      fr.b[0] = xl_read(xl);
+      fr.b[2] = xl_read(xl + 2 * kXlPiece);
+    } else {
+      fr.b[0] = hload(rs.x, xvo, 0);
+      fr.b[2] = hload(rs.x, xvo, 32);
+    }
+#endif
     __builtin_amdgcn_sched_barrier(0);
     return;
   } else if constexpr (DIN == 16) {
@@ -635,12 +629,6 @@ struct Args32 {
 // registers capsule k-1 used, so no load waits on a queued MFMA's operand read.
 constexpr int kFTW = 2;   // row tiles per wave
 constexpr int kFFB = 2;   // frame tiles per wave
-#ifndef SRF_FIRST_XCD
-#define SRF_FIRST_XCD 1   // XCD-aware task order (0: row-group-fastest, A/B builds)
-#endif
-#ifndef SRF_FWD32_FULL0
-#define SRF_FWD32_FULL0 1   // din 32: iteration 0 over all capsules with the finish fused (0: chunked, A/B builds)
-#endif
 
 template <int DIN>
 struct FirstFrags {
@@ -651,7 +639,6 @@ struct FirstFrags {
 template <int DIN, int DOUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void route_fwd32_first_kernel(Args32 A) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-#if SRF_FIRST_XCD
   // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs, so
   // XCD x receives blocks x, x+8, ...; remap them to one contiguous range of tasks,
   // ordered (i-chunk, frame pair, row group).  An XCD then works through one or two
@@ -668,13 +655,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
   const int rest = task / A.n_tgroups;
   const int fp = rest % nfp, chunk = rest / nfp;
   if (chunk >= A.n_chunks) return;
-#else
-  const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int chunk = task % A.n_chunks;
-  const int rest = task / A.n_chunks;
-  const int tg = rest % A.n_tgroups, fp = rest / A.n_tgroups;
-  if (fp * 32 * kFFB >= A.F) return;
-#endif
   const int tbase = tg * kFTW;
   const int JD = A.J * DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
@@ -765,6 +745,28 @@ __device__ __forceinline__ uint32_t ff_slot(int r, int c) { return (uint32_t)(4 
 __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+// One capsule's x fragments (din 32: hi / lo plane x two k-halves, 16 bytes per lane
+// each) global -> LDS for all the workgroup's waves, which share them: wave w DMAs
+// fragment q = w & 3 (plane q & 1, k-half q >> 1) of the 64 lanes' frames into
+// dst + q * kXlPiece (lane-linear; waves w and w + 4 write the same bytes).  Every wave
+// issues it (no branch: the compiler keeps counting the loads in flight exactly) and
+// waits for it (xl_wait) before the barrier that publishes it.
+// The DMA is inline asm: issued through the builtin, the compiler stops counting the
+// loads in flight across it and waits for all of them at the next operand use.  Its own
+// waits stay correct, only conservative, with one more load in flight than it knows of.
+__device__ __forceinline__ void x_dma(const char* xs, uint32_t xplane_b, uint32_t xvo, int wv, char* dst) {
+  const int q = wv & 3;
+  const char* src = xs + (q & 1) * xplane_b + xvo + (q >> 1) * 32;
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(dst + q * kXlPiece));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(src) : "memory", "m0");
+}
+// K: the vector-memory instructions the wave issues after the DMA (they may stay in
+// flight); each kernel's count is checked against its ISA (scripts/dbg/check_xl_wait.py)
+template <int K = 0>
+__device__ __forceinline__ void xl_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void route_fwd32_first_full_kernel(
@@ -915,17 +917,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
   const int j0 = tbase * 32 / DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
-#if SRF_FWD32_PRIO
   if (DIN <= 16 && NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);   // din 32: measured faster without
-#endif
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
   const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
   const __amdgpu_buffer_rsrc_t lzs = make_rsrc(A.lzst, A.cst ? (size_t)A.in_n * A.Fs * 4 : 0);
 
-#if SRF_FWD32_DBG == 4
-  const unsigned long long t_body0 = __builtin_amdgcn_s_memtime();
-#endif
   f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
   // Vc rows of this wave's tiles -> private LDS in fragment order
@@ -956,21 +953,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                            A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
                            fr);
-#if SRF_FWD32_DBG == 4
-    unsigned long long tph[5] = {0, 0, 0, 0, 0};
-    unsigned long long tlast = __builtin_amdgcn_s_memtime();
-    const unsigned long long t_loop0 = tlast;
-#define SRF_TMARK(k) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); tph[k] += tn - tlast; tlast = tn; }
-#else
-#define SRF_TMARK(k)
-#endif
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
       // partial agreement dots <u_ij, Vc_j> over this lane's rows (packed FMA pairs)
       f2 P2[CP];
 #pragma unroll
       for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
-      if constexpr (SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) {   // din 32: pose_prog measured faster (C4 A/B)
+      if constexpr (DIN <= 16) {   // tile-major pose; din 32: pose_prog measured faster (C4 A/B)
       {
         constexpr uint32_t TSTEP = 32 * DIN * 2;
         const int in = min(i + 1, i1 - 1);
@@ -991,9 +980,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #pragma unroll
             for (int q = 0; q < 4; ++q) vv[q] = vcl[((t - 1) * 4 + q) * 64 + lane];
           }
-          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
           u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
-          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
           fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, wcap, fr.a[t]);
           {
             const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap, 0);
@@ -1009,21 +998,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         dots(TW - 1);
       }
       } else {
-#if SRF_FWD32_PROG
       const int in = min(i + 1, i1 - 1);
       pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
                          x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
                          A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
-#else
-#pragma unroll
-      for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
-#endif
-      SRF_TMARK(0)
-      if (SRF_FWD32_FETCH_EARLY && i + 1 < i1)
-        fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                               A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
-                               (uint32_t)(i + 1) * A.JDp * 8, fr);
-      if (SRF_FWD32_FETCH_EARLY) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1059,18 +1037,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         M = fmaxf(m0, m1);
         Z = z0 * __expf(m0 - M) + z1 * __expf(m1 - M);
       }
-      if constexpr (SRF_FWD32_DBG == 3) {
-#pragma unroll
-        for (int t = 0; t < TW; ++t) acc[t] += u[t];
-        continue;
-      }
-      if constexpr (NW > 1 && SRF_FWD32_DBG != 2) {
+      if constexpr (NW > 1) {
         // per-wave stats of the 32 frames -> LDS; half h combines waves [h*NW/2, (h+1)*NW/2)
         float2* slot = st + par * NW * 32;
         if (h == 0) slot[wv * 32 + r] = make_float2(M, Z);
-        SRF_TMARK(2)
         __syncthreads();
-        SRF_TMARK(3)
         constexpr int HW = NW / 2;
         float2 sv[HW];
 #pragma unroll
@@ -1092,18 +1063,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       // next capsule's operands: issued once every MFMA result has been consumed
       // (the dots), so no load waits on a queued MFMA's operand read
       __builtin_amdgcn_sched_barrier(0);
-      if (!(SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) && !SRF_FWD32_PROG && !SRF_FWD32_FETCH_EARLY && SRF_FWD32_DBG != 1 && i + 1 < i1)
-        fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                               A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
-                               (uint32_t)(i + 1) * A.JDp * 8, fr);
-      __builtin_amdgcn_sched_barrier(0);
-      SRF_TMARK(1)
       // c = exp(L - M) / Z = e * exp(m - M) / Z; then all-gather over the halves
-#if SRF_FWD32_FASTDIV
-      const float sc = __expf(m - M) * __builtin_amdgcn_rcpf(Z);
-#else
       const float sc = __expf(m - M) * __builtin_amdgcn_rcpf(Z);   // Z >= 1: 1-ulp v_rcp
-#endif
       {
         // lane half h owns capsules j0 + 2a + h after the logit reduce-scatter; frames
         // past F (up to the 32-frame stride) store 0, which the gW pass relies on.
@@ -1133,14 +1094,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
           acc[t][v] = a2.x;
           acc[t][v + 1] = a2.y;
         }
-      SRF_TMARK(4)
     }
-#if SRF_FWD32_DBG == 4
-    if (lane == 0 && (blockIdx.x == 100 || blockIdx.x == 7) && (wv == 0 || wv == NW - 1))
-      printf("fwd32 NW %d blk %d wv %d caps %d: prologue %llu mfma-issue %llu loads-issue %llu softmax1 %llu barrier %llu "
-             "softmax2+acc %llu\n",
-             NW, blockIdx.x, wv, i1 - i0, t_loop0 - t_body0, tph[0], tph[1], tph[2], tph[3], tph[4]);
-#endif
   }
 #pragma unroll
   for (int t = 0; t < TW; ++t)
@@ -1155,12 +1109,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 }
 
 
-#ifndef SRF_FWD32P_DBG
-#define SRF_FWD32P_DBG 0   // timing experiments of the pipelined passes (never shipped)
-#endif
-#ifndef SRF_FWD32P_VREG
-#define SRF_FWD32P_VREG 1   // 1: route_fwd32p_kernel keeps the Vc fragments in registers (LDS: stats only; C4 step 9.13 -> 9.06 ms)
-#endif
 // Routing pass r >= 1, software-pipelined over the input capsules: while the matrix
 // cores form capsule i + 1's pose tiles (pose_prog, which also streams in capsule
 // i + 2's operands), the VALU finishes capsule i -- the cross-wave softmax statistics
@@ -1190,14 +1138,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
   const __amdgpu_buffer_rsrc_t crs = make_rsrc(A.cst, A.cst ? (size_t)A.in_n * A.JP * A.Fs * 4 : 0);
   const __amdgpu_buffer_rsrc_t lzs = make_rsrc(A.lzst, A.cst ? (size_t)A.in_n * A.Fs * 4 : 0);
-#if SRF_FWD32P_VREG
-  // this lane's Vc fragments in registers (no LDS reads per capsule)
+  // this lane's Vc fragments in registers (no LDS reads per capsule); LDS: the softmax
+  // stats, then (din 32) two buffers of the shared x fragments (x_dma)
   float2* st = reinterpret_cast<float2*>(lds);
   f4 vcr[TW][4];
-#else
-  f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
-  float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
-#endif
+  constexpr bool XL = DIN == 32;
+  // a separate LDS object: the compiler then sees no DMA aliasing the stats
+  __shared__ __attribute__((aligned(16))) char xls[XL ? 2 * 4 * kXlPiece : 16];
+  char* xb = xls;
+  const char* xs_b = static_cast<const char*>(A.xs);
+  auto xsrc = [&](int c) { return x_voff<DIN>(min(c, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
+  auto xbuf = [&](int c) { return xb + (c & 1) * 4 * kXlPiece; };
 #pragma unroll
   for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1205,11 +1156,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       const int row = (tbase + t) * 32 + 8 * q + 4 * h;
       f4 v = {0.f, 0.f, 0.f, 0.f};
       if (fvalid && row < JD) v = *reinterpret_cast<const f4*>(A.vc + (size_t)f * JD + row);
-#if SRF_FWD32P_VREG
       vcr[t][q] = v;
-#else
-      vcl[(t * 4 + q) * 64 + lane] = v;
-#endif
     }
   float mk[OWN];
 #pragma unroll
@@ -1229,6 +1176,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
                            fr);
     f16v uc[TW], un[TW];
     float e[OWN], m;   // the pending capsule's exponentials and lane max
+    if constexpr (XL) {   // x of capsules i0 + 1, i0 + 2 into LDS before the first pose
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 1), wv, xbuf(i0 + 1));
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 2), wv, xbuf(i0 + 2));
+      xl_wait();
+      __syncthreads();
+    }
     // the logits of one capsule's tiles -> e, m; the wave's (max, sum) -> LDS slot
     auto logits = [&](const f16v (&u)[TW], int slot_par) {
       f2 P2[CP];
@@ -1238,11 +1191,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       for (int t = 0; t < TW; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-#if SRF_FWD32P_VREG
           const f4 vv = vcr[t][q];
-#else
-          const f4 vv = vcl[(t * 4 + q) * 64 + lane];
-#endif
           const int k = kpart<DOUT>(t, 4 * q);
           P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv.x, vv.y};
           P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv.z, vv.w};
@@ -1270,16 +1219,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       if (h == 0) st[(slot_par * NW + wv) * 32 + r] = make_float2(M, Z);
     };
     int par = 0;
-    pose_prog<DIN, TW>(fr, ones, uc, rs, wvo, bvo,
-                       x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                       A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
-                       (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8);
+    pose_prog<DIN, TW, XL>(fr, ones, uc, rs, wvo, bvo,
+                           x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
+                           (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8, xbuf(i0 + 1) + lane * 16);
     logits(uc, par);
     __syncthreads();
     // one capsule: i + 1's tiles into unext while capsule i (in ucur) is finished; the loop
     // runs two steps with the roles swapped, so no register copy moves u between them
+#if SRF_FWD32P_DBG & 32
+    unsigned long long tph[4] = {0, 0, 0, 0}, tl = __builtin_amdgcn_s_memtime();
+#define SRF_PSTAMP(k) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); tph[k] += tn - tl; tl = tn; }
+#else
+#define SRF_PSTAMP(k)
+#endif
     auto step = [&](int i, f16v (&ucur)[TW], f16v (&unext)[TW]) __attribute__((always_inline)) {
       const bool more = i + 1 < i1;
+      if constexpr (XL)   // x of capsule i + 3 into the buffer capsule i + 1's x left
+        x_dma(xs_b, A.xplane_b, xsrc(i + 3), wv, xbuf(i + 3));
       if (more) {   // capsule i + 1's tiles on the matrix cores (operands of i + 2 streamed in)
         const int in = min(i + 2, i1 - 1);
 #if SRF_FWD32P_DBG
@@ -1289,10 +1246,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #else
         const int inx = in, inw = in;
 #endif
-        pose_prog<DIN, TW>(fr, ones, unext, rs, wvo, bvo,
-                           x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                           A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8);
+        pose_prog<DIN, TW, XL>(fr, ones, unext, rs, wvo, bvo,
+                               x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                               A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8,
+                               xbuf(i + 2) + lane * 16);
       }
+      SRF_PSTAMP(0)
       // finish capsule i: softmax over all waves' rows, couplings, s += c u
       float M, Z;
       {
@@ -1338,20 +1297,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
           acc[t][v] = a2.x;
           acc[t][v + 1] = a2.y;
         }
+      SRF_PSTAMP(1)
       if (more) {   // capsule i + 1's logits and stats, then the one barrier
         par ^= 1;
         logits(unext, par);
+        if constexpr (XL) xl_wait<5 * TW + OWN + 1>();   // capsule i + 3's x has landed before the barrier
+        SRF_PSTAMP(2)
 #if SRF_FWD32P_DBG & 4
         __builtin_amdgcn_sched_barrier(0);   // timing experiment: no barrier (wrong results)
 #else
         __syncthreads();
 #endif
+        SRF_PSTAMP(3)
       }
     };
     for (int i = i0; i < i1; i += 2) {
       step(i, uc, un);
       if (i + 1 < i1) step(i + 1, un, uc);
     }
+#if SRF_FWD32P_DBG & 32
+    if (lane == 0 && (blockIdx.x == 100 || blockIdx.x == 301) && (wv == 0 || wv == NW - 1))
+      printf("fwd32p blk %d wv %d caps %d: pose-issue %llu finish %llu logits %llu barrier %llu\n", blockIdx.x, wv,
+             i1 - i0, tph[0], tph[1], tph[2], tph[3]);
+#endif
+#undef SRF_PSTAMP
+    if constexpr (XL) xl_wait();   // no DMA into LDS outlives the workgroup
   }
 #pragma unroll
   for (int t = 0; t < TW; ++t)
@@ -1408,9 +1378,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const int tbase = __builtin_amdgcn_readfirstlane(wv * TW);
   const int j0 = tbase * 32 / DOUT;
   const Rsrc3 rs{make_rsrc(A.Ws, A.ws_bytes), make_rsrc(A.bs, A.bs_bytes), make_rsrc(A.xs, A.xs_bytes)};
-#if SRF_FWD32_PRIO
   if (DIN <= 16 && NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);   // din 32: measured faster without
-#endif
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
 
@@ -1436,10 +1404,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   int par = 0;
   if (i0 < i1) {
     Frags32<DIN, TW> fr;
-#if SRF_BWD32_CPREFETCH
-    float cn[OWN];
-    load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cn);
-#endif
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                            A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
                            fr);
@@ -1450,7 +1414,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #pragma unroll
       for (int k = 0; k < CP; ++k) P2[k] = f2{0.f, 0.f};
       float cc[OWN];
-      if constexpr (SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) {   // din 32: pose_prog measured faster (C4 A/B)
+      if constexpr (DIN <= 16) {   // tile-major pose; din 32: pose_prog measured faster (C4 A/B)
       // this capsule's couplings, then the tile-major pose with the dots of tile t - 1
       // behind tile t's MFMAs (as route_fwd32_kernel)
       load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
@@ -1474,9 +1438,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #pragma unroll
             for (int q = 0; q < 4; ++q) gq[q] = gsl[((t - 1) * 4 + q) * 64 + lane];
           }
-          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
           u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
-          if (SRF_FWD32_TMSB) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
           fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, wcap, fr.a[t]);
           {
             const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap, 0);
@@ -1492,24 +1456,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         dots(TW - 1);
       }
       } else {
-#if SRF_FWD32_PROG
       const int in = min(i + 1, i1 - 1);
       pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
                          x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
                          A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
-#else
-#pragma unroll
-      for (int t = 0; t < TW; ++t) u[t] = pose_chain<DIN>(fr.a[t], fr.b, mfma32(fr.bias[t], ones, f16v{}));
-#endif
-#if SRF_BWD32_CPREFETCH
-#pragma unroll
-      for (int a = 0; a < OWN; ++a) cc[a] = cn[a];
-      if (i + 1 < i1) load_c<OWN>(crow + (size_t)(i + 1) * cstep, A.Fs, cn);
-#else
       // this capsule's couplings: the pose MFMAs in flight hide their latency (no
       // registers held across capsules)
       load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
-#endif
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1551,12 +1504,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       // logZ of capsule i before the next capsule's operand loads: waiting for it at its
       // store then leaves those (younger) loads in flight
       const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
-      __builtin_amdgcn_sched_barrier(0);
-      if (!(SRF_FWD32_TM && (DIN <= 16 || SRF_FWD32_TM32)) && !SRF_FWD32_PROG && i + 1 < i1) {
-        fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i + 1, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off),
-                               h, A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)(i + 1) * A.JDp * DIN * 2,
-                               (uint32_t)(i + 1) * A.JDp * 8, fr);
-      }
       __builtin_amdgcn_sched_barrier(0);
       {
         // (logZ, sigma) of frame f, capsule i: branch-free (wave 0, half 0, valid frames)
@@ -1633,6 +1580,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
   f4* gsl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float* st = lds + (size_t)NW * TW * 4 * 64 * 4;
+  // din 32: two buffers of the shared x fragments (x_dma) after the sigma partials
+  constexpr bool XL = DIN == 32;
+  // a separate LDS object: the compiler then sees no DMA aliasing the gs / sigma LDS
+  __shared__ __attribute__((aligned(16))) char xls[XL ? 2 * 4 * kXlPiece : 16];
+  char* xb = xls;
+  const char* xs_b = static_cast<const char*>(A.xs);
+  auto xsrc = [&](int c) { return x_voff<DIN>(min(c, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
+  auto xbuf = [&](int c) { return xb + (c & 1) * 4 * kXlPiece; };
 #pragma unroll
   for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1684,11 +1639,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       if (h == 0) st[(slot_par * NW + wv) * 32 + r] = s0 + s1;
     };
     int par = 0;
+    if constexpr (XL) {   // x of capsules i0 + 1, i0 + 2 into LDS before the first pose
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 1), wv, xbuf(i0 + 1));
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 2), wv, xbuf(i0 + 2));
+      xl_wait();
+      __syncthreads();
+    }
     load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cc);
-    pose_prog<DIN, TW>(fr, ones, uc, rs, wvo, bvo,
-                       x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                       A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
-                       (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8);
+    pose_prog<DIN, TW, XL>(fr, ones, uc, rs, wvo, bvo,
+                           x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
+                           (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8, xbuf(i0 + 1) + lane * 16);
     dots(uc, cc, par);
     __syncthreads();
     // one capsule, as route_fwd32p_kernel's step: two steps per loop turn with the roles of
@@ -1696,6 +1657,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     auto step = [&](int i, f16v (&ucur)[TW], f16v (&unext)[TW], float (&ccur)[OWN], float (&cnext)[OWN])
         __attribute__((always_inline)) {
       const bool more = i + 1 < i1;
+      if constexpr (XL)   // x of capsule i + 3 into the buffer capsule i + 1's x left
+        x_dma(xs_b, A.xplane_b, xsrc(i + 3), wv, xbuf(i + 3));
       // logZ of capsule i before the next capsule's loads: waiting for it at its store
       // then leaves those (younger) loads in flight
       const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
@@ -1712,9 +1675,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 #else
         const int inx = in, inw = in;
 #endif
-        pose_prog<DIN, TW>(fr, ones, unext, rs, wvo, bvo,
-                           x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                           A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8);
+        pose_prog<DIN, TW, XL>(fr, ones, unext, rs, wvo, bvo,
+                               x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                               A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8,
+                               xbuf(i + 2) + lane * 16);
       }
       // finish capsule i: sigma over all waves, stats, gL, gVc += gL u
       float S;
@@ -1760,6 +1724,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       if (more) {
         par ^= 1;
         dots(unext, cnext, par);
+        if constexpr (XL) xl_wait<1 + OWN + 5 * TW + 1 + OWN>();   // capsule i + 3's x has landed
         __syncthreads();
       }
     };
@@ -1767,6 +1732,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       step(i, uc, un, cc, cn);
       if (i + 1 < i1) step(i + 1, un, uc, cn, cc);
     }
+    if constexpr (XL) xl_wait();   // no DMA into LDS outlives the workgroup
   }
 #pragma unroll
   for (int t = 0; t < TW; ++t)
@@ -1852,6 +1818,8 @@ float* fwd32_slab(const Fwd32Plan& p, void* scratch) {
 }
 
 size_t fwd32_lds(const Fwd32Plan& p) {
+  // Vc / gs fragment slabs and softmax statistics (the pipelined din-32 passes add their
+  // two shared x buffers, 8 KiB, as a static LDS object)
   return (size_t)p.NW * p.TW * 4 * 64 * 16 + (p.NW > 1 ? (size_t)2 * 32 * p.NW * 8 : 0);
 }
 
@@ -1905,14 +1873,11 @@ int fwd32_prepare(const Fwd32Plan& p, const float* emb, const float* W, const fl
   return SRF_OK;
 }
 
-#ifndef SRF_FWD32_PIPE
-#define SRF_FWD32_PIPE 1   // multi-wave passes r >= 1 on route_fwd32p_kernel (0: route_fwd32_kernel, A/B builds)
-#endif
 template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_rpass(const Fwd32Plan& p, const Args32& a, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
   // the pipelined pass holds a second u set: TW = 4 would spill
-  auto kern = (SRF_FWD32_PIPE && NW > 1 && TW <= 2) ? route_fwd32p_kernel<DIN, DOUT, (NW > 1 ? NW : 2), (TW <= 2 ? TW : 2)>
+  auto kern = (NW > 1 && TW <= 2) ? route_fwd32p_kernel<DIN, DOUT, (NW > 1 ? NW : 2), (TW <= 2 ? TW : 2)>
                                                     : route_fwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2009,7 +1974,7 @@ Fwd32Cpl fwd32_cpl_layout(const Fwd32Plan& p, int F, int in_n, int din, int dout
 
 // Iteration-0 pass with its finish fused (route_fwd32_first_full_kernel): din = dout = 32.
 bool fwd32_first_full_supported(const Fwd32Plan& p, int din, int dout) {
-  return SRF_FWD32_FULL0 && din == 32 && dout == 32 && p.JDp % kFfBM == 0;
+  return din == 32 && dout == 32 && p.JDp % kFfBM == 0;
 }
 
 int fwd32_first_full(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din, int lpad,
@@ -2049,7 +2014,7 @@ int fwd32_pass(const Fwd32Plan& p, bool first, const void* planes, void* scratch
 template <int DIN, int DOUT, int NW, int TW = kTW>
 static int launch_bpass(const Fwd32Plan& p, const Args32& a, const Bwd32Args& b, hipStream_t st) {
   const size_t lds = fwd32_lds(p);
-  auto kern = (SRF_FWD32_PIPE && NW > 1 && TW <= 2) ? route_bwd32p_kernel<DIN, DOUT, (NW > 1 ? NW : 2), (TW <= 2 ? TW : 2)>
+  auto kern = (NW > 1 && TW <= 2) ? route_bwd32p_kernel<DIN, DOUT, (NW > 1 ? NW : 2), (TW <= 2 ? TW : 2)>
                                                     : route_bwd32_kernel<DIN, DOUT, NW, TW>;
   if (lds > 64 * 1024)
     SRF_HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -885,10 +885,7 @@ struct GxwItems {
   GxwItem it[srf::kMaxItems];
   int n;
 };
-#ifndef SRF_GXW_WAVES
-#define SRF_GXW_WAVES 16
-#endif
-constexpr int kGxwWaves = SRF_GXW_WAVES;
+constexpr int kGxwWaves = 16;
 constexpr int kGxwThreads = 64 * kGxwWaves;
 constexpr int kGxwRows = 32 * kGxwWaves;   // rows per workgroup
 constexpr int kGxwTS = 34;                 // row stride of a wave's transposed tile
@@ -1122,17 +1119,12 @@ __global__ __launch_bounds__(256, 2) void sdr_pose8_kernel(GemmItems items, int 
 // one frame range alone on the GPU, us 32x32 vs 16x16): C5 din 64 pose 850 vs 973, gx
 // 1228 vs 1174, gW 937 vs 1073; C3 din 32 pose 46 vs 33, gx 47 vs 53, gW 91 vs 65.
 enum class SdrGemm { kPose, kGx, kGw };
-#ifndef SRF_SDR_POSE_BF3
-#define SRF_SDR_POSE_BF3 1   // din 32 / 64 fp32 pose on bf16 MFMA, three-term split operands
-#endif
-#ifndef SRF_SDR_MFMA32_DIN32
-#define SRF_SDR_MFMA32_DIN32 3   // bit 0 pose, bit 1 gx, bit 2 gW: the 32x32 kernels at din 32 (r04q: pose + gx)
-#endif
+constexpr int kSdrMfma32Din32 = 3;   // bit 0 pose, bit 1 gx, bit 2 gW: the 32x32 kernels at din 32 (r04q: pose + gx)
 bool use_mfma32(int din, int JD, SdrGemm k) {
   if ((din != 32 && din != 64) || JD % 8) return false;
   if (din == 64) return k != SdrGemm::kGx;
   const int bit = k == SdrGemm::kPose ? 1 : k == SdrGemm::kGx ? 2 : 4;
-  return (SRF_SDR_MFMA32_DIN32 & bit) != 0;
+  return (kSdrMfma32Din32 & bit) != 0;
 }
 
 // ------------------------------------------------------------------ host
@@ -1188,7 +1180,7 @@ int pose_n(const SGeom& g, const GemmItems& it, hipStream_t st, int mode = 0) {
     SRF_LAUNCH_CHECK("sdr_pose8");
     return SRF_OK;
   }
-  if (SRF_SDR_POSE_BF3 && (g.din == 32 || g.din == 64) && g.JD() % 8 == 0) {
+  if ((g.din == 32 || g.din == 64) && g.JD() % 8 == 0) {   // fp32 pose on bf16 MFMA, three-term split operands
     if (g.din == 32)
       hipLaunchKernelGGL(sdr_pose3b_kernel<32>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
     else

@@ -26,12 +26,6 @@
 #include "route_sdr_seq_dev.h"
 #include "srf_group.h"
 
-// Timing experiments (never in the shipped build): 1 = next frame's loads hit the
-// cache (wrong results), 2 = uniform couplings (no softmax reductions).
-#ifndef SRF_SEQ_DBG
-#define SRF_SEQ_DBG 0
-#endif
-
 namespace {
 
 using namespace srf_seq;
@@ -142,11 +136,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
     float b[C::NIM], c[C::NIM];
 #pragma unroll
     for (int k = 0; k < C::NIM; ++k) b[k] = 0.f;
-#if SRF_SEQ_DBG == 1   // timing experiment: re-load the current (cache-hot) frame
-    const int tn = t;
-#else
     const int tn = min(t + 1, rg.t1 - 1);   // the next frame (the range's last reloads itself)
-#endif
     // one routing iteration; the last one also loads frame tn into the registers u_t
     // leaves.  The loads are unconditional: a branch around them would merge the old and
     // new registers and wait for the loads right there, instead of at their first use
@@ -225,14 +215,11 @@ size_t fwd_lds(int J, int D) {
   return ((size_t)pow2_at_least(J) * D + (size_t)kWaves * J * D) * sizeof(float);
 }
 
-#ifndef SRF_SEQ_STAGE
-#define SRF_SEQ_STAGE 1
-#endif
 // rows per lane staged through LDS (sdr_seq_fwd_kernel KS): the C3 inner layers, three of
 // five (96 KB beside w and the partials); the J = 32 last layer has no registers to spare
 // for the second copy of the iteration that keeps the loads unconditional
 constexpr int stage_rows(int D, int JP, int NIM) {
-  return (SRF_SEQ_STAGE && D == 32 && NIM == 5 && JP == 16) ? 3 : 0;
+  return (D == 32 && NIM == 5 && JP == 16) ? 3 : 0;
 }
 
 template <int D, int JP, int NIM>

@@ -252,10 +252,6 @@ __device__ __forceinline__ void logits_softmax(const float (&ur)[C::NIM][C::KD],
         p1 += ur[k][d + 1] * w[d + 1];
       }
       b[k] += group_sum<1, C::Q>(p0 + p1);
-#if defined(SRF_SEQ_DBG) && SRF_SEQ_DBG == 2
-      c[k] = L.jm ? b[k] * 1e-30f + 0.0625f : 0.f;
-      continue;
-#endif
       const float x = L.jm ? b[k] : -INFINITY;
       const float m = group_max<C::Q, C::ROWL>(x);
       const float e = __expf(x - m);

@@ -41,37 +41,16 @@ namespace {
 using srf_seq::group_max;
 using srf_seq::group_sum;
 
-// Forward ring depths (A/B builds, scripts/build_ab.sh + gpu_lib_ab_c5.sh, C5 step:
-// (6, 3) 990 ms, (6, 2) 959, (6, 1) 955, (3, 2) 951, (2, 3) 980, (8, 3) 1065, (6, 4)
-// 1131): deeper rings only add register pressure once the eight layers share HBM
-#ifndef SRF_STREAM_PDF16
-#define SRF_STREAM_PDF16 3
-#endif
-#ifndef SRF_STREAM_PDF32
-#define SRF_STREAM_PDF32 2
-#endif
-// with u in bf16 (packed slots, half the registers) a deeper forward ring pays (r04ff A/B,
-// C5 fp8: (3, 2) 598 ms, (6, 3) 588; fp32 unchanged at 788 | 790)
-#ifndef SRF_STREAM_PDF16_BF
-#define SRF_STREAM_PDF16_BF 6
-#endif
-#ifndef SRF_STREAM_PDF32_BF
-#define SRF_STREAM_PDF32_BF 3
-#endif
-// the backward's bf16 ring at the fp32 depths: (6, 3) 599 ms and (8, 4) 602 against (4, 2)
-// 596 (r04hh A/B, C5 fp8)
-#ifndef SRF_STREAM_PDB16_BF
-#define SRF_STREAM_PDB16_BF SRF_STREAM_PDB16
-#endif
-#ifndef SRF_STREAM_PDB32_BF
-#define SRF_STREAM_PDB32_BF SRF_STREAM_PDB32
-#endif
-#ifndef SRF_STREAM_PDB16   // backward ring depths
-#define SRF_STREAM_PDB16 4
-#endif
-#ifndef SRF_STREAM_PDB32
-#define SRF_STREAM_PDB32 2
-#endif
+// Register-ring depths in capsules per wave (forward fp32 | bf16 u, backward), by
+// 16- or 32-capsule-row shapes.  Measured (C5 step): forward fp32 (6, 3) 990 ms, (6, 2)
+// 959, (6, 1) 955, (3, 2) 951, (2, 3) 980, (8, 3) 1065, (6, 4) 1131 -- deeper rings only
+// add register pressure once the eight layers share HBM; with u in bf16 (packed slots,
+// half the registers) a deeper forward ring pays (C5 fp8: (3, 2) 598 ms, (6, 3) 588);
+// the backward's bf16 ring at the fp32 depths ((6, 3) 599 ms and (8, 4) 602 against
+// (4, 2) 596).
+constexpr int kPdF16 = 3, kPdF32 = 2;       // forward, fp32 u
+constexpr int kPdF16Bf = 6, kPdF32Bf = 3;   // forward, bf16 u
+constexpr int kPdB16 = 4, kPdB32 = 2;       // backward (fp32 and bf16 u)
 constexpr int kNT = 512;          // threads per workgroup (two waves per SIMD, 256 VGPRs each)
 constexpr int kNW = kNT / 64;
 constexpr int kRM = 5;            // iteration bound (check_sgeom)
@@ -86,12 +65,12 @@ struct SC {
   static constexpr int RQ = D / KD;           // lanes per output capsule
   static constexpr int NE = JD / kNT;         // elements per thread in the element phases
   // capsules in flight per wave in the forward / backward register ring
-  static constexpr int PDF = KD <= 8 ? 8 : KD <= 16 ? SRF_STREAM_PDF16 : SRF_STREAM_PDF32;
-  static constexpr int PDF_BF = KD <= 8 ? 8 : KD <= 16 ? SRF_STREAM_PDF16_BF : SRF_STREAM_PDF32_BF;
+  static constexpr int PDF = KD <= 8 ? 8 : KD <= 16 ? kPdF16 : kPdF32;
+  static constexpr int PDF_BF = KD <= 8 ? 8 : KD <= 16 ? kPdF16Bf : kPdF32Bf;
   template <class TU>
   static constexpr int pdf() { return std::is_same<TU, float>::value ? PDF : PDF_BF; }
-  static constexpr int PDB = KD <= 16 ? SRF_STREAM_PDB16 : SRF_STREAM_PDB32;
-  static constexpr int PDB_BF = KD <= 16 ? SRF_STREAM_PDB16_BF : SRF_STREAM_PDB32_BF;
+  static constexpr int PDB = KD <= 16 ? kPdB16 : kPdB32;
+  static constexpr int PDB_BF = KD <= 16 ? kPdB16 : kPdB32;
   template <class TU>
   static constexpr int pdb() { return std::is_same<TU, float>::value ? PDB : PDB_BF; }
   static constexpr int HD = 8;                 // gu outputs per lane per sub-pass (registers: 2R*HD)
@@ -208,12 +187,9 @@ __host__ __device__ inline size_t gl_floats(int B, int in_n, int J, int R) { ret
 // Workgroup barrier that orders LDS only (no vmcnt(0)), so the register ring's loads stay
 // in flight across it; for barriers with no global data exchanged between waves of the
 // kernel (the grouped launches exchange through srf_group.h and keep __syncthreads)
-#ifndef SRF_STREAM_LDSBAR
-#define SRF_STREAM_LDSBAR 1
-#endif
 template <bool LDS_ONLY>
 __device__ __forceinline__ void wg_bar() {
-  if constexpr (LDS_ONLY && SRF_STREAM_LDSBAR) {
+  if constexpr (LDS_ONLY) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
