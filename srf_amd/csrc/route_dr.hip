@@ -1771,361 +1771,6 @@ __global__ __launch_bounds__(256, 2) void route_gw16s_kernel(
   }
 }
 
-// ---------------------------------------------------------------- fused gx + gW
-// route_gxw16_kernel (din = dout = 32, R = 2..3, stored couplings): the gx and gW
-// contractions of one DR layer in one pass over gu, which is formed ONCE per element from
-// the stored scalars (naive:154-159, :199-206 backward):
-//   gu_ij(f) = c^0 gs^0_j(f) + sum_{r >= 1} c^r_ij(f) gs^r_j(f) + gL^r_ij(f) Vc^r_j(f)
-//   gW_i^T  += x_i^T gu_i           (K = frames, v_mfma_f32_32x32x16_f16)
-//   gx_i     = W_i^T gu_i           (K = the workgroup's rows, v_mfma_f32_16x16x32_f16)
-// Workgroup = 8 waves = 8 output capsules j (256 rows) x kGxwCap input capsules x one of S
-// frame splits, walking 16-frame tiles.  Lane (n, h) of wave w forms gu of row
-// 32 (8 rg + w) + n for frames 8h .. 8h + 7 of the tile -- the B operand of gW as it
-// stands -- and splits it by a per-(wave, capsule, tile) power of two into fp16 hi / lo
-// (exact hi by masking, as route_gux16_kernel).  The gW accumulators keep a running
-// exponent per capsule (the minimum so far; a smaller one rescales them exactly).  For
-// gx the split tile goes through a per-wave LDS image [32 rows][16 frames] read back
-// transposed (ds_read_b64_tr_b16: lane = frame, 8 consecutive rows) against W^T
-// fragments held in registers for the launch (the forward's split W^T planes).  The 8
-// waves' gx parts are summed through LDS and stored, one row group's part per (frame,
-// capsule), to gxp [rg][F][in_n][32]; route_gxw_window_kernel adds the row groups and
-// the window adjoint into g_emb.  gW | gbias leave as the split's partial slabs
-// (gw_reduce_kernel).  The x^T planes and the couplings of a tile are staged in LDS
-// (register staging, double-buffered, one barrier per tile; a second barrier orders the
-// gx part sums against the next tile's parts).
-constexpr int kGxwNW = 8;    // waves per workgroup (output capsules j per row group)
-constexpr int kGxwCap = 2;   // input capsules per workgroup (3 or 4 spill: W^T fragments + accumulators)
-template <int R>
-struct GxwLds {
-  static constexpr int RV = R - 1;
-  static constexpr int XB = 2 * 32 * 16 * 2;              // x^T hi + lo of one capsule and tile
-  static constexpr int CB = RV * 2 * kGxwNW * 16 * 4;     // its c^r / gL^r for the 8 j, 16 frames
-  static constexpr int PCB = XB + CB;
-  static constexpr int PQ = PCB / 16;                      // 16-byte staging pieces per capsule
-  static constexpr int STAGE = kGxwCap * PCB;
-  static constexpr int TRP = 32 * 32 + 4 * 128;            // one transpose plane: rows of 32 B, +128 B per 8 rows
-  static constexpr int TRB = 2 * TRP;
-  static constexpr int PB = kGxwNW * kGxwCap * 16 * 32 * 4;   // gx parts of one tile
-  static constexpr int BYTES = 2 * STAGE + kGxwNW * kGxwCap * TRB + 2 * PB;
-};
-__device__ __forceinline__ int gxw_tr_row(int n) { return n * 32 + (n >> 3) * 128; }
-typedef short s4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f4 mfma16h(const h8& a, const h8& b, const f4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-// max over the wave on the VALU: DPP within rows of 16 (xor 1, xor 2, half-row and row
-// mirrors), then the v_permlane16 / 32 swaps
-__device__ __forceinline__ float wave_max(float v) {
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0xB1, 0xF, 0xF, false)));
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x4E, 0xF, 0xF, false)));
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x141, 0xF, 0xF, false)));
-  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x140, 0xF, 0xF, false)));
-  float a, b;
-  xpair16(v, a, b);
-  v = fmaxf(a, b);
-  xpair32(v, a, b);
-  return fmaxf(a, b);
-}
-
-template <int R>
-__global__ __launch_bounds__(64 * kGxwNW, 1) void route_gxw16_kernel(
-    const _Float16* __restrict__ x16, const _Float16* __restrict__ wt16, const float* __restrict__ hdr,
-    const float* __restrict__ saved, const float* __restrict__ gs, const float* __restrict__ cst,
-    const float* __restrict__ glst, int F, int Fp, int in_n, int J, int mask_first, int JP, int n_rg, int n_cc,
-    int S, int ft_per, float* __restrict__ gxp, float* __restrict__ gwp, float* __restrict__ gbp, size_t pstride) {
-  static_assert(R >= 2 && R <= 3, "stored couplings exist for iters >= 2; registers hold R <= 3");
-  using L = GxwLds<R>;
-  constexpr int D = 32, RV = R - 1, CAP = kGxwCap, NW = kGxwNW;
-  extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
-  unsigned char* stg = gsm;                                  // [2][STAGE]
-  unsigned char* trw = gsm + 2 * L::STAGE;                   // [NW][CAP][TRB]
-  float* part = reinterpret_cast<float*>(gsm + 2 * L::STAGE + NW * CAP * L::TRB);   // [2][NW][CAP][16][32]
-  const int JD = J * D;
-  const int NT = JD / 16;
-  const size_t FJD = (size_t)F * JD;
-  const int Fs = srf::fwd32_frame_stride(F);
-  const size_t cblk = (size_t)in_n * JP * Fs;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int n = lane & 31, h = lane >> 5;
-  int b = blockIdx.x;
-  const int s = b % S;
-  b /= S;
-  const int rg = b % n_rg;
-  const int cc = b / n_rg;
-  const int j = rg * NW + wv;                                // < J (J % 8 == 0, host)
-  const int row = j * D + n;
-  const int Jeff = J - (mask_first ? 1 : 0);
-  const float c0 = (mask_first && j == 0) ? 0.f : 1.f / (float)Jeff;
-  const int i0 = cc * CAP, ncap = min(in_n, i0 + CAP) - i0;
-  const int NFT = Fp >> 4;
-  const int ft0 = s * ft_per, ft1 = min(NFT, ft0 + ft_per);
-  const int aw = (int)hdr[1], bx = (int)hdr[2];
-
-  // staging pieces: idx < CAP * PQ; piece of capsule k: x (plane, e, 8-frame half) for
-  // rem < 128, else a coupling quad (r, c | gL, jj, frame quad)
-  constexpr int NQ = (CAP * L::PQ + 64 * NW - 1) / (64 * NW);
-  const char* src[NQ];
-  int dst[NQ];
-  int step[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int idx = min(q * 64 * NW + tid, CAP * L::PQ - 1);
-    const int k = idx / L::PQ, rem = idx - k * L::PQ;
-    const int i = i0 + min(k, ncap - 1);
-    if (rem < 128) {
-      const int p = rem >> 6, e = (rem >> 1) & 31, hf = rem & 1;
-      src[q] = reinterpret_cast<const char*>(x16 + (((size_t)i * NFT * 2 + p) * 32 + e) * 16 + hf * 8);
-      dst[q] = k * L::PCB + p * 1024 + (e * 16 + ((hf ^ ((e >> 3) & 1)) * 8)) * 2;
-      step[q] = 2 * 32 * 16 * 2;
-    } else {
-      const int cr = rem - 128, fq = cr & 3, jj = (cr >> 2) & 7, cg = cr >> 5;   // cg = r * 2 + (0: c, 1: gL)
-      const int jc = min(rg * NW + jj, JP - 1);
-      src[q] = reinterpret_cast<const char*>(((cg & 1) ? glst : cst) + (size_t)(cg >> 1) * cblk +
-                                             ((size_t)i * JP + jc) * Fs + 4 * fq);
-      dst[q] = k * L::PCB + L::XB + ((cg * NW + jj) * 16 + 4 * fq) * 4;
-      step[q] = 16 * 4;
-    }
-  }
-  f4 sv[NQ];
-  auto stage_load = [&](int ft) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) sv[q] = *reinterpret_cast<const f4*>(src[q] + (size_t)ft * step[q]);
-  };
-  auto stage_store = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      if ((CAP * L::PQ) % (64 * NW) != 0 && q * 64 * NW + tid >= CAP * L::PQ) continue;
-      *reinterpret_cast<f4*>(&stg[buf * L::STAGE + dst[q]]) = sv[q];
-    }
-  };
-  // per-frame vectors of the lane's row, frames 8h + 0..7 of a tile (0 past F)
-  const uint32_t nrec = (uint32_t)(FJD * 4);
-  __amdgpu_buffer_rsrc_t rs_g[R], rs_v[RV];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    rs_g[r] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gs + (size_t)r * FJD), 0, (int)nrec, 0x00020000);
-    if (r > 0)
-      rs_v[r - 1] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(saved + (size_t)(2 * (r - 1) + 1) * FJD), 0,
-                                                      (int)nrec, 0x00020000);
-  }
-  const uint32_t vo0 = (uint32_t)((8 * h) * JD + row) * 4;
-  f2 vec[R + RV][4];   // gs^0 (times c^0), gs^1 .. , Vc^1 .. : frame pairs (v, v + 1)
-  auto vec_load = [&](int ft) {
-#pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      const uint32_t so = (uint32_t)((ft * 16 + v) * JD) * 4;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        vec[r][v >> 1][v & 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g[r], vo0, so, 0));
-        if (r > 0)
-          vec[R + r - 1][v >> 1][v & 1] =
-              __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_v[r - 1], vo0, so, 0));
-      }
-    }
-  };
-  // gx's A operand for the launch: W^T[e = 16 eh + (l & 15)][rows 8g .. 8g + 7 of j] hi | lo,
-  // g = l >> 4 (the prep's wt16 planes [i][t][h][e][8 rows])
-  const int g = lane >> 4, l16 = lane & 15;
-  const size_t wplane = (size_t)in_n * NT * 16 * D;   // halves per plane
-  h8 wa[CAP][2][2];   // [capsule][eh][hi | lo]
-#pragma unroll
-  for (int k = 0; k < CAP; ++k) {
-    const int i = i0 + min(k, ncap - 1);
-#pragma unroll
-    for (int eh = 0; eh < 2; ++eh)
-#pragma unroll
-      for (int p = 0; p < 2; ++p)
-        wa[k][eh][p] = *reinterpret_cast<const h8*>(
-            wt16 + p * wplane + (size_t)i * NT * 16 * D + ((((2 * j + (g >> 1)) * 2 + (g & 1)) * D) + l16 + 16 * eh) * 8);
-  }
-  f16v acc[CAP];
-  int eacc[CAP];
-  f2 gb[CAP];
-#pragma unroll
-  for (int k = 0; k < CAP; ++k) {
-    acc[k] = f16v{};
-    eacc[k] = 60;
-    gb[k] = f2{0.f, 0.f};
-  }
-  unsigned char* tw = trw + wv * CAP * L::TRB;
-  const int trw_off = gxw_tr_row(n) + h * 16;                          // this lane's 16 bytes of the image
-  const int tq = l16 >> 2, tp = l16 & 3;
-  const int trr0 = gxw_tr_row(8 * g + tq) + 8 * tp, trr1 = gxw_tr_row(8 * g + 4 + tq) + 8 * tp;   // tr reads
-  const int xoff = (n * 16 + ((h ^ ((n >> 3) & 1)) * 8)) * 2;          // gW's A fragment in a staged x plane
-  if (ft0 < ft1) {
-    stage_load(ft0);
-    stage_store(0);
-    if (ft0 + 1 < ft1) stage_load(ft0 + 1);
-    vec_load(ft0);
-  }
-  // the 8 waves' gx parts of tile ft (buffer pb) -> gxp, by CAP x 16 frames x 8 quads threads
-  auto part_sum = [&](int ft, int pb) {
-    static_assert(CAP * 16 * 8 <= 64 * NW, "one float4 of the tile's gx per thread");
-    if (tid < CAP * 16 * 8) {
-      const int k = tid >> 7, f = (tid >> 3) & 15, e4 = tid & 7;
-      const float* pp = part + (size_t)pb * (L::PB / 4);
-      f4 sum = ld4(pp + ((0 * CAP + k) * 16 + f) * 32 + 4 * e4);
-#pragma unroll
-      for (int w = 1; w < NW; ++w) sum += ld4(pp + ((w * CAP + k) * 16 + f) * 32 + 4 * e4);
-      const int fg = ft * 16 + f;
-      if (k < ncap && fg < F) st4(gxp + (((size_t)rg * F + fg) * in_n + i0 + k) * D + 4 * e4, sum);
-    }
-  };
-  for (int ft = ft0; ft < ft1; ++ft) {
-    const int buf = (ft - ft0) & 1;
-    // tile ft staged in buf; every wave's gx parts of tile ft - 1 are in part buffer buf ^ 1
-    __syncthreads();
-    if (ft + 1 < ft1) {
-      stage_store(buf ^ 1);
-      if (ft + 2 < ft1) stage_load(ft + 2);
-    }
-    const unsigned char* sb = stg + buf * L::STAGE;
-    // gu of every capsule first: the per-frame vectors are then free for the next tile's
-    // loads, which land while this tile's MFMAs run
-    f2 gu[CAP][4];
-#pragma unroll
-    for (int k = 0; k < CAP; ++k) {
-      const float* ckf = reinterpret_cast<const float*>(sb + k * L::PCB + L::XB);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) gu[k][v] = vec[0][v] * c0;
-#pragma unroll
-      for (int r = 0; r < RV; ++r) {
-        const float* cp = ckf + ((r * 2 + 0) * NW + wv) * 16 + 8 * h;
-        const float* gp = ckf + ((r * 2 + 1) * NW + wv) * 16 + 8 * h;
-        const f4 ca = ld4(cp), cb = ld4(cp + 4), ga = ld4(gp), gbv = ld4(gp + 4);
-        const f2 c2[4] = {f2{ca[0], ca[1]}, f2{ca[2], ca[3]}, f2{cb[0], cb[1]}, f2{cb[2], cb[3]}};
-        const f2 g2[4] = {f2{ga[0], ga[1]}, f2{ga[2], ga[3]}, f2{gbv[0], gbv[1]}, f2{gbv[2], gbv[3]}};
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          gu[k][v] = __builtin_elementwise_fma(c2[v], vec[r + 1][v], gu[k][v]);
-          gu[k][v] = __builtin_elementwise_fma(g2[v], vec[R + r][v], gu[k][v]);
-        }
-      }
-      gb[k] += (gu[k][0] + gu[k][1]) + (gu[k][2] + gu[k][3]);
-    }
-    vec_load(ft + 1 < ft1 ? ft + 1 : ft);   // unconditional: the last tile reloads itself
-    if (ft > ft0) part_sum(ft - 1, buf ^ 1);
-    float* pw = part + (size_t)buf * (L::PB / 4);
-    // one split exponent for the wave's whole tile (all CAP capsules); the gW
-    // accumulators keep the minimum so far per capsule (a smaller one rescales them)
-    float m = 0.f;
-#pragma unroll
-    for (int k = 0; k < CAP; ++k)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) m = fmaxf(m, fmaxf(fabsf(gu[k][v][0]), fabsf(gu[k][v][1])));
-    const float wm = wave_max(m);
-    const int et = wm > 0.f ? srf_split_exp(wm) : 60;   // an all-zero tile sets nothing
-    int ek[CAP];
-#pragma unroll
-    for (int k = 0; k < CAP; ++k) {
-      const unsigned char* ck = sb + k * L::PCB;
-      const int e = min(eacc[k], et);
-      if (e < eacc[k]) {   // wave-uniform
-        const float rs = srf_exp2i(e - eacc[k]);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[k][q] *= rs;
-        eacc[k] = e;
-      }
-      ek[k] = e;
-      const float sg = srf_exp2i(e);
-      h8 bh, bl;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const f2 a = gu[k][v] * sg;
-        const f2 hi = __builtin_bit_cast(f2, __builtin_bit_cast(u2, a) & 0xFFFFE000u);
-        const h2 ph = __builtin_convertvector(hi, h2), pl = __builtin_convertvector(a - hi, h2);
-        bh[2 * v] = ph[0];
-        bh[2 * v + 1] = ph[1];
-        bl[2 * v] = pl[0];
-        bl[2 * v + 1] = pl[1];
-      }
-      // gW^T_i += x_i^T gu_i
-      const h8 xh = *reinterpret_cast<const h8*>(ck + xoff);
-      const h8 xl = *reinterpret_cast<const h8*>(ck + 1024 + xoff);
-      acc[k] = mfma32h(xh, bh, acc[k]);
-      acc[k] = mfma32h(xh, bl, acc[k]);
-      acc[k] = mfma32h(xl, bh, acc[k]);
-      // the split tile -> this capsule's transpose image
-      *reinterpret_cast<h8*>(tw + k * L::TRB + trw_off) = bh;
-      *reinterpret_cast<h8*>(tw + k * L::TRB + L::TRP + trw_off) = bl;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // gx_i = W_i^T gu_i over this wave's rows, from the images read back transposed
-#pragma unroll
-    for (int k = 0; k < CAP; ++k) {
-      const unsigned char* tk = tw + k * L::TRB;
-      const s4v a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4v*)(reinterpret_cast<uintptr_t>(tk + trr0)));
-      const s4v a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4v*)(reinterpret_cast<uintptr_t>(tk + trr1)));
-      const s4v b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4v*)(reinterpret_cast<uintptr_t>(tk + L::TRP + trr0)));
-      const s4v b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4v*)(reinterpret_cast<uintptr_t>(tk + L::TRP + trr1)));
-      const h8 th = __builtin_bit_cast(h8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
-      const h8 tl = __builtin_bit_cast(h8, __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
-      const float un = srf_exp2i(-(aw + ek[k]));
-#pragma unroll
-      for (int eh = 0; eh < 2; ++eh) {
-        f4 gx = {0.f, 0.f, 0.f, 0.f};
-        gx = mfma16h(wa[k][eh][0], th, gx);
-        gx = mfma16h(wa[k][eh][0], tl, gx);
-        gx = mfma16h(wa[k][eh][1], th, gx);
-        // C map: frame l & 15, e = 16 eh + 4 (l >> 4) + 0..3
-        st4(pw + (((wv * CAP + k) * 16 + l16) * 32 + 16 * eh + 4 * g), gx * un);
-      }
-    }
-    // the images are rewritten in the next tile only after its barrier
-  }
-  if (ft0 < ft1) {   // the last tile's gx parts
-    __syncthreads();
-    part_sum(ft1 - 1, (ft1 - 1 - ft0) & 1);
-  }
-  float* gw = gwp + (size_t)s * pstride;
-  float* gbo = gbp + (size_t)s * pstride;
-#pragma unroll
-  for (int k = 0; k < CAP; ++k) {
-    const float a = gb[k][0] + gb[k][1];
-    float pa, pb;
-    xpair32(a, pa, pb);
-    if (k >= ncap) continue;
-    const int i = i0 + k;
-    const float un = srf_exp2i(-(bx + eacc[k]));
-    if (h == 0) gbo[(size_t)i * JD + row] = pa + pb;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      st4(gw + ((size_t)i * JD + row) * D + 8 * q + 4 * h,
-          f4{acc[k][4 * q] * un, acc[k][4 * q + 1] * un, acc[k][4 * q + 2] * un, acc[k][4 * q + 3] * un});
-  }
-}
-
-// g_emb[b, t, n, :] = sum over the row groups and the window offsets w of the fused pass's
-// gx parts: capsule i = w N + n of frame t - w + lpad (inside the utterance) -- the window
-// adjoint (naive:150-151).  One thread per float4 of g_emb (overwritten).
-__global__ __launch_bounds__(256) void route_gxw_window_kernel(const float* __restrict__ gxp, int F, int T, int N,
-                                                               int W, int lpad, int in_n, int n_rg,
-                                                               float* __restrict__ g_emb) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)F * N * 8;
-  if (idx >= total) return;
-  const int e4 = idx & 7;
-  const size_t fn = idx >> 3;
-  const int nn = fn % N;
-  const int f = fn / N;
-  const int t = f % T;
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int w = 0; w < W; ++w) {
-    const int ts = t - w + lpad;
-    if (ts < 0 || ts >= T) continue;
-    const size_t fs = (size_t)f - t + ts;
-    for (int rg = 0; rg < n_rg; ++rg)
-      acc += ld4(gxp + (((size_t)rg * F + fs) * in_n + w * N + nn) * 32 + 4 * e4);
-  }
-  st4(g_emb + (fn * 32) + 4 * e4, acc);
-}
-
 // gW | gbias = sum of the S partial slabs (float4 per thread).
 __global__ void gw_reduce_kernel(const float* __restrict__ part, int S, size_t n4, size_t stride, float* __restrict__ gW,
                                  size_t nw4, float* __restrict__ gb) {
@@ -2446,43 +2091,6 @@ inline int gw3_cap(const Geom& g) {
 // x^T planes this kernel reads (xt16) under the same test.
 inline bool use_gw16s(const Geom& g) { return use_gux16(g) && g.iters <= 3; }
 
-// route_gxw16_kernel (gx and gW fused, gu formed once) wherever route_gw16s_kernel would
-// run and J is a multiple of the workgroup's 8 output capsules: the C3 / C4 DR layers.
-inline bool use_gxw16(const Geom& g) { return use_gw16s(g) && g.J % kGxwNW == 0; }
-struct GxwPlan {
-  int n_rg, n_cc, S, ft_per;
-  size_t pstride;
-};
-// frame splits: one workgroup per CU (LDS and registers); fewest rounds of tiles per
-// workgroup, then fewest partial gW slabs (each read back by gw_reduce)
-GxwPlan gxw_plan(const Geom& g) {
-  GxwPlan p{};
-  p.n_rg = g.J / kGxwNW;
-  p.n_cc = (g.in_n() + kGxwCap - 1) / kGxwCap;
-  p.pstride = (size_t)g.in_n() * g.JD() * (g.din + 1);
-  const int NFT = padded_frames(g) / 16;
-  const int base = p.n_rg * p.n_cc;
-  double best = 1e30;
-  for (int S0 = 1; S0 <= NFT; ++S0) {
-    const int ft_per = (NFT + S0 - 1) / S0;
-    const int S = (NFT + ft_per - 1) / ft_per;
-    const int rounds = (base * S + 255) / 256;
-    const double work = (double)rounds * ft_per * 2.0e-7;          // ~0.2 us per tile and workgroup
-    const double slab = 2.0 * S * p.pstride * 4 / 5e12;            // partial gW write + reduce read
-    if (work + slab < best) {
-      best = work + slab;
-      p.S = S;
-      p.ft_per = ft_per;
-    }
-  }
-  return p;
-}
-inline size_t gxw_part_floats(const Geom& g) {
-  const GxwPlan p = gxw_plan(g);
-  return (size_t)p.S * p.pstride;
-}
-inline size_t gxw_gx_floats(const Geom& g) { return (size_t)(g.J / kGxwNW) * g.F() * g.in_n() * g.din; }
-
 Gw2Plan gw2_plan(const Geom& g) {
   const bool g16 = use_gw16s(g);
   Gw2Plan p{};
@@ -2676,7 +2284,6 @@ struct BwdWs {
   float* gl;          // gL^r of those passes [iters-1][in_n][JP][Fs], read by the gu / gW passes
   float* gwpart;      // partial gW | gbias slabs of route_gw2_kernel (S frame splits)
   float* gumax;       // max |gu| of the layer (route_gux16_kernel -> route_gw16s_kernel)
-  float* gxp;         // route_gxw16_kernel's gx parts per row group [n_rg][F][in_n][din]
   size_t bytes;
 };
 
@@ -2691,14 +2298,13 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   const size_t oA = take(F * JD), ogs = take((size_t)g.iters * F * JD), oslab = take((size_t)n_chunks * F * JD),
                ostats = take((size_t)(g.iters - 1) * F * in_n * 2), ogu = take(in_n * (size_t)g.NT() * 16 * Fp),
                oxt = take(in_n * g.din * Fp), owt = take(in_n * JD * g.din);
-  size_t op32 = 0, ogl = 0, ogwp = 0, ogxp = 0;
+  size_t op32 = 0, ogl = 0, ogwp = 0;
   const size_t ogm = take(64);
   if (use_fwd32(g)) {
     const srf::Fwd32Plan plan = srf::fwd32_plan(g.B, g.T, g.N, g.din, g.lpad, g.rpad, g.J, g.dout, n_chunks);
     op32 = take((srf::fwd32_scratch_bytes(plan) + 3) / 4);
     ogl = take((size_t)std::max(g.iters - 1, 1) * srf::fwd32_frame_stride(g.F()) * in_n * (plan.JDp / g.dout));
-    ogwp = take(std::max(gw2_part_floats(g), use_gxw16(g) ? gxw_part_floats(g) : (size_t)0));
-    if (use_gxw16(g)) ogxp = take(gxw_gx_floats(g));
+    ogwp = take(gw2_part_floats(g));
   }
   char* b = static_cast<char*>(base);
   BwdWs w;
@@ -2713,7 +2319,6 @@ BwdWs bwd_layout(const Geom& g, int n_chunks, void* base) {
   w.gl = ogl ? (float*)(b + ogl) : nullptr;
   w.gwpart = ogwp ? (float*)(b + ogwp) : nullptr;
   w.gumax = (float*)(b + ogm);
-  w.gxp = ogxp ? (float*)(b + ogxp) : nullptr;
   w.bytes = off;
   return w;
 }
@@ -2725,15 +2330,6 @@ template <int D>
 int bwd_weights_impl(const Geom& g, const float* emb, float* g_W, float* g_bias, const BwdWs& w, hipStream_t st,
                      const float* saved = nullptr, const float* couplings = nullptr) {
   const int Fp = padded_frames(g);
-  if (couplings != nullptr && w.gl != nullptr && g.iters > 1 && use_gxw16(g)) {
-    // the data pass (route_gxw16_kernel) left gW | gbias as per-split partial slabs
-    const GxwPlan p = gxw_plan(g);
-    const size_t nw4 = (size_t)g.in_n() * g.JD() * g.din / 4, n4 = p.pstride / 4;
-    hipLaunchKernelGGL(gw_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, w.gwpart, p.S, n4, p.pstride, g_W,
-                       nw4, g_bias);
-    SRF_LAUNCH_CHECK("gw_reduce");
-    return SRF_OK;
-  }
   if (couplings != nullptr && w.gl != nullptr && g.iters > 1) {
     // gu formed from the stored couplings / logit gradients (never materialised);
     // the forward left the windowed x^T in the coupling storage
@@ -2822,36 +2418,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
                        w.WT, g_emb, n_emb);
     SRF_LAUNCH_CHECK("transpose_w");
   }
-  if (p32 && use_gxw16(g)) {
-    // gx and gW in one pass over gu (route_gxw16_kernel), then the window adjoint of the
-    // row groups' gx parts into g_emb; gW | gbias partial slabs stay for the weights part
-    const GxwPlan gp = gxw_plan(g);
-    const int grid = gp.n_rg * gp.n_cc * gp.S;
-    const size_t lds = g.iters == 2 ? (size_t)GxwLds<2>::BYTES : (size_t)GxwLds<3>::BYTES;
-    const _Float16* x16 = reinterpret_cast<const _Float16*>(couplings + cl.xT);
-    const _Float16* w16 = reinterpret_cast<const _Float16*>(couplings + cl.WT);
-    const float* hdr = srf::fwd32_hdr(plan, couplings + cl.planes);
-    const int JP = plan.JDp / g.dout;
-    float* gbp = w.gwpart + (size_t)g.in_n() * g.JD() * g.din;
-#define SRF_GXW(R_)                                                                                                   \
-  {                                                                                                                   \
-    auto k = route_gxw16_kernel<R_>;                                                                                  \
-    SRF_HIP_TRY(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));           \
-    hipLaunchKernelGGL(k, dim3(grid), dim3(64 * kGxwNW), lds, st, x16, w16, hdr, saved, w.gs, couplings + cl.c, w.gl, \
-                       g.F(), Fp, g.in_n(), g.J, g.mask_first, JP, gp.n_rg, gp.n_cc, gp.S, gp.ft_per, w.gxp,          \
-                       w.gwpart, gbp, gp.pstride);                                                                    \
-  }
-    if (g.iters == 2)
-      SRF_GXW(2)
-    else
-      SRF_GXW(3)
-#undef SRF_GXW
-    SRF_LAUNCH_CHECK("route_gxw16");
-    const size_t n4 = (size_t)g.F() * g.N * (g.din / 4);
-    hipLaunchKernelGGL(route_gxw_window_kernel, dim3((n4 + 255) / 256), dim3(256), 0, st, w.gxp, g.F(), g.T, g.N,
-                       gu_window(g), g.lpad, g.in_n(), gp.n_rg, g_emb);
-    SRF_LAUNCH_CHECK("route_gxw_window");
-  } else if (p32) {
+  if (p32) {
     SRF_HIP_TRY(hipMemsetAsync(w.gumax, 0, sizeof(float), st));
     launch_gu_r<D>(g, emb, W, couplings + cl.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st, couplings + cl.c,
                    w.gl, plan.JDp / g.dout, srf::fwd32_hdr(plan, couplings + cl.planes), w.gumax);
