@@ -241,6 +241,9 @@ def measure(workload, args, world, rank, dev):
     if args.sdr_capsnorm_per_layer:
         from srf_amd import ops
         ops.SDR_CAPSNORM_BATCHED = False
+    if args.sdr_last_gxw_inline:
+        from srf_amd import ops
+        ops.SDR_LAST_GXW_SIDE = False
     if args.sdr_last_group is not None:
         g = [int(x) for x in args.sdr_last_group.split(',')]
         model.sdr_options['last_group'] = (g[0], g[-1])
@@ -412,6 +415,8 @@ def main():
                     help='SDR stack: the gx and gW launches of din-32 layers separately (default: fused)')
     ap.add_argument('--sdr-capsnorm-per-layer', action='store_true',
                     help='SDR stack: one LN/dropout launch per inner layer and range (default: one per diagonal)')
+    ap.add_argument('--sdr-last-gxw-inline', action='store_true',
+                    help='SDR stack: the last layer\'s gx / gW on its recurrence\'s stream (default: a side stream)')
     ap.add_argument('--flat-allreduce', action='store_true',
                     help='N > 1: one flat all-reduce after each step instead of backward-overlapped buckets (A/B)')
     ap.add_argument('--eager', action='store_true', help='launch every kernel from Python each step (no hipGraph)')

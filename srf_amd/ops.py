@@ -617,6 +617,20 @@ def _cn_call(fn, ranges, *args, what):
 # din-32 SDR layers: gx and gW in one launch that reads gu once (srf_route_sdr_gx_gw_n);
 # False runs the two contractions' own launches (bench --sdr-separate-gxgw, for A/B)
 SDR_FUSED_GXGW = True
+# STACK_CAPTURE_ORDER: the stack's graph-captured launches keep each stream's next launch
+# ahead (in issue order) of the other streams' launches that wait on it.  ROCm's graph
+# executor splits the captured DAG into chains by depth-first search -- a node's first
+# child in capture order continues its chain, every other child starts a new chain --
+# and puts the chains on its few hardware queues in turn: a cross-stream child issued
+# first made every last-layer range a new chain that shared a queue with the inner
+# layers' every fourth range (C3 step 18.1 ms; eager 17.3).  scripts/dbg/graph_queues.py:
+# the stack's stream patterns 1.14-1.23x their critical path in a graph, 1.00-1.01x in
+# this order.
+# the last layer's gx / gW of range k run on a third stream beside the recurrence of range
+# k - 1 (the last layer's gu kept for every frame, so the streams are ordered one way
+# only): off the backward's critical chain; False keeps them on the recurrence's stream
+# (bench --sdr-last-gxw-inline, for A/B)
+SDR_LAST_GXW_SIDE = True
 # the inner layers' LN + dropout of one anti-diagonal in one launch (srf_capsnorm_*_range_n);
 # False: one launch per layer (bench --sdr-capsnorm-per-layer, for A/B)
 SDR_CAPSNORM_BATCHED = True
@@ -724,6 +738,18 @@ class SdrStack(torch.autograd.Function):
                     _cn_call(L_.srf_capsnorm_fwd_range_n, c, B, T, J * D, tr, float(p_mid), int(seed), sp,
                              what='capsnorm_fwd_range_n')
 
+        def last(k):
+            """the last layer's recurrence of range k on stream B (its pose too unless ahead)"""
+            if pose_ahead:
+                sb.wait_event(ev_p[k])
+            elif L > 1:
+                sb.wait_event(ev_a[k + L - 2])
+            run(pb, [L - 1], [k], with_pose=not pose_ahead)
+
+        # capture order (STACK_CAPTURE_ORDER): the recurrence of the last layer's range k
+        # is issued one diagonal late, after the pose of range k + 1 (stream C) and inner
+        # diagonal d + 1 (stream A) that follow the launches it waits on
+        pending = None
         for d in range(P.K + L - 1):
             # inner layers: diagonal d on stream A, grouped by layer shape
             groups = {}
@@ -736,16 +762,17 @@ class SdrStack(torch.autograd.Function):
             ev_a[d].record(sa)
             # last layer: range k = d - (L-1) needs (L-2, k), done on diagonal d - 1
             k = d - (L - 1)
-            if 0 <= k < P.K and P.fwd[L - 1][k] < P.fwd[L - 1][k + 1]:
-                if pose_ahead:
-                    if L > 1:
-                        sc.wait_event(ev_a[d - 1])
-                    pose(pc, [L - 1], [k])
-                    ev_p[k].record(sc)
-                    sb.wait_event(ev_p[k])
-                elif L > 1:
-                    sb.wait_event(ev_a[d - 1])
-                run(pb, [L - 1], [k], with_pose=not pose_ahead)
+            live = 0 <= k < P.K and P.fwd[L - 1][k] < P.fwd[L - 1][k + 1]
+            if live and pose_ahead:
+                if L > 1:
+                    sc.wait_event(ev_a[d - 1])
+                pose(pc, [L - 1], [k])
+                ev_p[k].record(sc)
+            if pending is not None:
+                last(pending)
+            pending = k if live else None
+        if pending is not None:
+            last(pending)
         for s_ in (sa, sb, sc):
             main.wait_stream(s_)
         ctx.plan, ctx.meta = P, (tr, float(p_mid), int(seed), store)
@@ -789,11 +816,18 @@ class SdrStack(torch.autograd.Function):
             pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
                                    dtype=torch.uint8) if l < L - 1 else None)
         main = torch.cuda.current_stream(dev)
-        sa, sb = _layer_streams(dev, 2, 'bwd')
+        side = SDR_LAST_GXW_SIDE
+        sa, sb, sc = _layer_streams(dev, 3, 'bwd')
         ev_b = P.events('bwd_b', P.K)   # the last layer's range k has its gu and gx
-        for s_ in (sa, sb):
+        ev_r = P.events('bwd_r', P.K)   # the last layer's range k has its gu (side: gx / gW may start)
+        # side: the last layer's gu covers every frame (C3: 1.8 GB), so the recurrence of
+        # range k - 1 (stream B) never writes what gx / gW of range k (stream C) read: C
+        # waits for B, never B for C (torch's capture crashed on streams ordered both ways)
+        if side:
+            gus[L - 1] = torch.empty(P.u_floats(L - 1, T), device=dev)
+        for s_ in (sa, sb, sc):
             s_.wait_stream(main)
-        pa, pb = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream)
+        pa, pb, pc = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream), ctypes_void(sc.cuda_stream)
         for l, (N, din, J, D, mf) in enumerate(P.layers):
             _lib.check(L_.srf_route_sdr_transpose_w(_ptr(Ws[l]), P.in_n(l), J, D, din, _ptr(WTs[l]),
                                                     pb if l == L - 1 else pa), 'sdr_transpose_w')
@@ -806,38 +840,46 @@ class SdrStack(torch.autograd.Function):
                           u=_ptr(urs[l]), v0=v0, vn=vn, v=_ptr(vs[l]),
                           couplings=_ptr(cs) if cs is not None else None, workspace=_ptr(rws[l]),
                           workspace_bytes=rws[l].numel(), g_v=_ptr(g_vs[l]), carry=_ptr(carries[l]),
-                          gu=_ptr(gus[l]), g0=t0, gn=P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
+                          gu=_ptr(gus[l]), g0=0 if side and l == L - 1 else t0,
+                          gn=T if side and l == L - 1 else P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
                           g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1), u_bf16=int(P.ubf[l]),
                           group=P.group(l, dev, backward=True))
 
-        def run(sp, ls, ks, ev=None, gw=True):
+        def run(sp, ls, ks, ev=None, gw=True, part='all'):
             """backward of ranges (ls[i], ks[i]) of same-shaped layers, batched: LN
             backward of the range's rows (inner layers), pose (when u was not kept),
-            recurrence, gx (window adjoint into the layer below), then (gw) gW / gbias."""
+            recurrence, gx (window adjoint into the layer below), then (gw) gW / gbias;
+            part 'rec' stops after the recurrence, 'grad' is the rest (another stream's
+            launches); ev is recorded behind the part's last launch."""
             N, din, J, D, mf = P.layers[ls[0]]
             rr = [item(l, k) for l, k in zip(ls, ks)]
             live = [r for r in rr if r.t1 > r.t0]
-            cn = [_lib.CapsnormRange(t0=r.t0, t1=r.t1, layer=l, x=_ptr(vs[l]), gamma=_ptr(gammas[l]),
-                                     beta=_ptr(betas[l]), stat=_ptr(stats[l]), g_y=_ptr(g_embs[l + 1]),
-                                     g_x=_ptr(g_vs[l]), gpart=_ptr(gparts[l]))
-                  for l, r in zip(ls, rr) if l < L - 1 and r.t1 > r.t0]
-            for c in ([cn] if SDR_CAPSNORM_BATCHED else [[x] for x in cn]):
-                if c:   # LN + dropout backward of the inner layers' ranges, one launch
-                    _cn_call(L_.srf_capsnorm_bwd_range_n, c, B, T, J * D, tr, float(p_mid), int(seed), sp,
-                             what='capsnorm_bwd_range_n')
             fused = gw and din == 32 and SDR_FUSED_GXGW   # gx + gW in one pass over gu
-            if live:
-                if not store:
-                    _sdr_call(L_.srf_route_sdr_pose_n, live, B, T, N, din, P.lpad, P.rpad, J, D, P.pose_mode(ls[0]),
-                              sp, what='sdr_pose_n')
-                _sdr_call(L_.srf_route_sdr_recur_bwd_n, live, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
-                          what='sdr_recur_bwd_n')
-                if not fused:
-                    _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')
+            if part != 'grad':
+                cn = [_lib.CapsnormRange(t0=r.t0, t1=r.t1, layer=l, x=_ptr(vs[l]), gamma=_ptr(gammas[l]),
+                                         beta=_ptr(betas[l]), stat=_ptr(stats[l]), g_y=_ptr(g_embs[l + 1]),
+                                         g_x=_ptr(g_vs[l]), gpart=_ptr(gparts[l]))
+                      for l, r in zip(ls, rr) if l < L - 1 and r.t1 > r.t0]
+                for c in ([cn] if SDR_CAPSNORM_BATCHED else [[x] for x in cn]):
+                    if c:   # LN + dropout backward of the inner layers' ranges, one launch
+                        _cn_call(L_.srf_capsnorm_bwd_range_n, c, B, T, J * D, tr, float(p_mid), int(seed), sp,
+                                 what='capsnorm_bwd_range_n')
+                if live:
+                    if not store:
+                        _sdr_call(L_.srf_route_sdr_pose_n, live, B, T, N, din, P.lpad, P.rpad, J, D,
+                                  P.pose_mode(ls[0]), sp, what='sdr_pose_n')
+                    _sdr_call(L_.srf_route_sdr_recur_bwd_n, live, B, T, P.in_n(ls[0]), J, D, P.iters, mf, sp,
+                              what='sdr_recur_bwd_n')
+                if part == 'rec':
+                    if ev is not None:
+                        ev.record(streams[id(sp)])
+                    return
+            if live and not fused:
+                _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')
             if fused:
                 _sdr_call(L_.srf_route_sdr_gx_gw_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_gw_n')
             if ev is not None:
-                ev.record(sa if sp is pa else sb)
+                ev.record(streams[id(sp)])
             if gw and not fused:
                 gw_ranges(sp, ls, ks)
             for l, k in zip(ls, ks):
@@ -852,26 +894,38 @@ class SdrStack(torch.autograd.Function):
             rr = [item(l, k) for l, k in zip(ls, ks)]
             _sdr_call(L_.srf_route_sdr_gw_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gw_n')
 
+        streams = {id(pa): sa, id(pb): sb, id(pc): sc}   # ctypes pointers do not hash
         # diagonal e of the inner layers holds (l, k) with (K-1-k) + (L-2-l) = e: (l, k)
         # needs (l+1, k) (diagonal e-1, or the last layer's range k on stream B) and
-        # (l, k+1) (diagonal e-1)
-        for e in range(P.K + L - 1):
+        # (l, k+1) (diagonal e-1).  Capture order (STACK_CAPTURE_ORDER): iteration e issues
+        # the last layer's recurrence of range K-1-e, its gx / gW of the range before
+        # (stream C) and inner diagonal e - 2, so every launch's same-stream successor is
+        # issued before the other streams' launches that wait on it
+        for e in range(P.K + L + 1):
             k = P.K - 1 - e
-            if k >= 0:   # last layer, range k, on stream B
-                run(pb, [L - 1], [k], ev=ev_b[k])
+            if k >= 0:   # last layer, range k, on stream B (gx / gW on stream C when side)
+                if side:
+                    run(pb, [L - 1], [k], ev=ev_r[k], part='rec')
+                else:
+                    run(pb, [L - 1], [k], ev=ev_b[k])
+            kg = k + 1
+            if side and 0 <= kg < P.K:
+                sc.wait_event(ev_r[kg])
+                run(pc, [L - 1], [kg], ev=ev_b[kg], part='grad')
+            ed = e - 2
             groups = {}
             for l in range(L - 1):
-                kk = P.K - 1 - (e - (L - 2 - l))
-                if 0 <= kk < P.K:
+                kk = P.K - 1 - (ed - (L - 2 - l))
+                if ed >= 0 and 0 <= kk < P.K:
                     groups.setdefault(P.layers[l], []).append((l, kk))
             if not groups:
                 continue
-            kl = P.K - 1 - e   # (L-2, kl) is in this diagonal: it needs the last layer's range kl
+            kl = P.K - 1 - ed   # (L-2, kl) is in this diagonal: it needs the last layer's range kl
             if L > 1 and 0 <= kl < P.K:
                 sa.wait_event(ev_b[kl])
             for g in groups.values():
                 run(pa, [l for l, _ in g], [kk for _, kk in g])
-        for s_ in (sa, sb):
+        for s_ in (sa, sb, sc):
             main.wait_stream(s_)
         ctx.css = None
         return (g_embs[0], None, None, None, None, *_returned(targets))
