@@ -106,7 +106,14 @@ class GradBuckets:
     is left (the CNN front end's parameters, whose backward is last) and makes the
     current stream wait for every bucket.
 
-    ``force`` runs the collectives at world size 1 too (the RCCL path test)."""
+    ``force`` runs the collectives at world size 1 too (the RCCL path test).
+
+    On the GPU a ready bucket records an event on the backward's stream and its
+    collective is issued at the next hook (from a side stream that waits on the
+    event), i.e. after more of the backward has been enqueued: in a captured step the
+    backward's next kernel then precedes the collective in capture order, which keeps
+    the backward one chain of ROCm's graph executor instead of a new chain per bucket
+    that may share a hardware queue with the collectives (ops.STACK_CAPTURE_ORDER)."""
 
     def __init__(self, model, bucket_mb=25.0, force=False):
         self.model, self.force = model, force
@@ -121,6 +128,11 @@ class GradBuckets:
                 self.buckets.append((lo, hi, cur))
                 hi, cur = lo, []
         self.of = {n: k for k, (_, _, ns) in enumerate(self.buckets) for n in ns}
+        dev = model.flat_grad.device
+        self.gpu = dev.type == 'cuda'
+        # created once: a captured step must not see its events destroyed before capture ends
+        self.events = [torch.cuda.Event() for _ in self.buckets] if self.gpu else None
+        self.side = torch.cuda.Stream(device=dev) if self.gpu else None
         self.begin()
         if self.active() and dist.is_initialized() and dist.get_backend() == 'nccl':
             # every rank constructs the buckets at the same point: one collective now sets
@@ -134,24 +146,46 @@ class GradBuckets:
         self.pending = [set(ns) for _, _, ns in self.buckets]
         self.launched = 0
         self.works = []
+        self.deferred = []   # ready buckets whose collective is not issued yet
 
     def ready(self, names):
+        self._issue()
         for n in names:
             self.pending[self.of[n]].discard(n)
         while self.launched < len(self.buckets) and not self.pending[self.launched]:
             self._launch()
 
     def _launch(self):
-        lo, hi, _ = self.buckets[self.launched]
+        k = self.launched
         self.launched += 1
-        if self.active():
-            self.works.append(dist.all_reduce(self.model.flat_grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+        if not self.active():
+            return
+        if self.gpu:
+            self.events[k].record()   # the bucket's gradients are enqueued on the current stream
+        self.deferred.append(k)
+        if not self.gpu:
+            self._issue()
+
+    def _issue(self):
+        for k in self.deferred:
+            lo, hi, _ = self.buckets[k]
+            if self.gpu:
+                self.side.wait_event(self.events[k])
+                with torch.cuda.stream(self.side):
+                    self.works.append(dist.all_reduce(self.model.flat_grad[lo:hi], op=dist.ReduceOp.SUM,
+                                                      async_op=True))
+            else:
+                self.works.append(dist.all_reduce(self.model.flat_grad[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+        self.deferred = []
 
     def finish(self):
         while self.launched < len(self.buckets):
             self._launch()
+        self._issue()
         for w in self.works:
             w.wait()
+        if self.gpu and self.works:
+            torch.cuda.current_stream().wait_stream(self.side)
         self.begin()
 
 
