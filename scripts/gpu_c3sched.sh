@@ -17,6 +17,7 @@ for v in "${VS[@]}"; do
       base) ;;
       eager) args="$args --eager" ;;
       --*) args="$args $w" ;;
+      SRF_LIB_PATH=*) envs="$envs SRF_LIB_PATH=$GRAFT_REPO_ROOT/${w#SRF_LIB_PATH=}" ;;
       *) envs="$envs $w" ;;
     esac
   done
@@ -26,7 +27,7 @@ for v in "${VS[@]}"; do
   tail -1 $OUT/b$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('  ms_per_step', d['ms_per_step'])"
   [ -n "$NOTRACE" ] && continue
   ( for e in $envs; do export "$e"; done
-    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/kt$i -o run -- \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt$i -o run -- \
       python3 $B --steps 4 --warmup 2 $args > $OUT/kt$i.log 2>&1 ) || { tail -20 $OUT/kt$i.log; exit 1; }
   python3 $GRAFT_REPO_ROOT/scripts/c3_timeline.py $OUT/kt$i/run_kernel_trace.csv > $OUT/tl$i.txt
   head -9 $OUT/tl$i.txt

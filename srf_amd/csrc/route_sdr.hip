@@ -890,7 +890,8 @@ constexpr int kGxwThreads = 64 * kGxwWaves;
 constexpr int kGxwRows = 32 * kGxwWaves;   // rows per workgroup
 constexpr int kGxwTS = 34;                 // row stride of a wave's transposed tile
 constexpr int kGxwPS = 33;                 // row stride of a wave's gx part
-constexpr size_t kGxwLds = (size_t)kGxwWaves * 32 * (kGxwTS + kGxwPS) * sizeof(float) + 2 * 2 * 32 * sizeof(long long);
+constexpr size_t kGxwLds =
+    (size_t)kGxwWaves * 32 * (kGxwTS + kGxwPS) * sizeof(float) + 3 * 2 * 32 * sizeof(long long) + 2 * 32 * 32 * sizeof(float);
 
 __global__ __launch_bounds__(kGxwThreads) void sdr_gxw32_kernel(GxwItems items, int N, int lpad, int in_n, int JD) {
   const GxwItem& G = items.it[blockIdx.z];
@@ -899,7 +900,8 @@ __global__ __launch_bounds__(kGxwThreads) void sdr_gxw32_kernel(GxwItems items, 
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* tT = lds;                                  // [wave][32 frames][kGxwTS]
   float* part = tT + kGxwWaves * 32 * kGxwTS;       // [wave][32 frames][kGxwPS]
-  long long* finfo = reinterpret_cast<long long*>(part + kGxwWaves * 32 * kGxwPS);   // [2][gu | x][32]
+  long long* finfo = reinterpret_cast<long long*>(part + kGxwWaves * 32 * kGxwPS);   // [3][gu | x][32]
+  float* xs = reinterpret_cast<float*>(finfo + 3 * 64);   // [2][32 frames][32 e]: x of a tile
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int i = blockIdx.y;
@@ -916,29 +918,60 @@ __global__ __launch_bounds__(kGxwThreads) void sdr_gxw32_kernel(GxwItems items, 
   float sb = 0.f;
   float* tw = tT + wv * 32 * kGxwTS;
   float* pw = part + wv * 32 * kGxwPS;
-  for (int f0 = 0, par = 0; f0 < Q; f0 += 32, par ^= 1) {
-    long long* fi = finfo + par * 64;   // double-buffered: the previous tile's atomics may still read it
-    if (tid < 32) {
-      const int q = f0 + tid;
-      int b, t;
-      fm.frame(min(q, Q - 1), b, t);
-      const int ts = t + w - lpad;
-      fi[tid] = q < Q ? (long long)(fm.view(b, t) * in_n + i) * JD : -1;
-      fi[32 + tid] = (q < Q && ts >= 0 && ts < fm.T) ? ((long long)(b * fm.T + ts) * N + n) * 32 : -1;
-    }
-    __syncthreads();
-    // gu of frames f0 + 2s + h at the wave's rows (A of gW), x of the same frames (B)
-    float a[16], xb[16];
+  // per tile of 32 frames: row offsets of gu and x of each frame (-1: none), written by
+  // 32 threads into one of three buffers (tile t's reduction still reads buffer t % 3
+  // while tile t + 1's are written and its loads issued)
+  auto offsets = [&](int f0, long long* fi) {
+    const int q = f0 + tid;
+    int b, t;
+    fm.frame(min(q, Q - 1), b, t);
+    const int ts = t + w - lpad;
+    fi[tid] = q < Q ? (long long)(fm.view(b, t) * in_n + i) * JD : -1;
+    fi[32 + tid] = (q < Q && ts >= 0 && ts < fm.T) ? ((long long)(b * fm.T + ts) * N + n) * 32 : -1;
+  };
+  // gu of frames f0 + 2s + h at the wave's rows (A of gW); x of the tile, one element
+  // per thread (staged in LDS: every wave uses all of it).  Absent rows load a valid
+  // address and are zeroed after (no branch per load: a branch merges, and waits for,
+  // the loads in flight)
+  const int r0c = won ? r0 : 0;
+  auto load = [&](const long long* fi, float (&a)[16], float& xr) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const long long go = fi[2 * s + h], xo = fi[32 + 2 * s + h];
-      a[s] = (won && go >= 0) ? G.gu[go + r0 + l32] : 0.f;
-      xb[s] = xo >= 0 ? G.emb[xo + l32] : 0.f;
+      const long long go = fi[2 * s + h];
+      const float av = G.gu[(go >= 0 ? go : 0) + r0c + l32];
+      a[s] = (won && go >= 0) ? av : 0.f;
     }
+    const long long xo = fi[32 + (tid >> 5)];
+    const float xv = G.emb[(xo >= 0 ? xo : 0) + (tid & 31)];
+    xr = xo >= 0 ? xv : 0.f;
+  };
+  // workgroup barrier on LDS only: no global data is exchanged inside the launch, so
+  // the next tile's loads stay in flight through it (__syncthreads waits for them)
+  auto bar = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  float a[16], xr;
+  if (tid < 32) offsets(0, finfo);
+  bar();
+  load(finfo, a, xr);
+  xs[tid] = xr;
+  for (int f0 = 0, tb = 0, xb = 0; f0 < Q; f0 += 32, tb = tb == 2 ? 0 : tb + 1, xb ^= 1) {
+    long long* fi = finfo + tb * 64;
+    long long* fn = finfo + (tb == 2 ? 0 : tb + 1) * 64;
+    const bool more = f0 + 32 < Q;
+    if (more && tid < 32) offsets(f0 + 32, fn);
+    bar();   // fn and this tile's x visible; every wave is past the previous tile's part reads
+    // the next tile's loads in flight through this tile (the last tile reloads itself:
+    // unconditional, so no branch merges the registers early)
+    float an[16], xn;
+    load(more ? fn : fi, an, xn);
+    const float* xt = xs + xb * 1024;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       sb += a[s];
-      agw = mfma32x32x2(a[s], xb[s], agw);
+      agw = mfma32x32x2(a[s], xt[(2 * s + h) * 32 + l32], agw);
       tw[(2 * s + h) * kGxwTS + l32] = a[s];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -952,7 +985,7 @@ __global__ __launch_bounds__(kGxwThreads) void sdr_gxw32_kernel(GxwItems items, 
     // agx: C[m = e][n = f]: lane (f = l32, h), reg r -> e = mfma32_row(r, h)
 #pragma unroll
     for (int r = 0; r < 16; ++r) pw[l32 * kGxwPS + mfma32_row(r, h)] = agx[r];
-    __syncthreads();
+    bar();
     for (int el = tid; el < 32 * 32; el += kGxwThreads) {
       const int f = el >> 5, e = el & 31;
       float v = 0.f;
@@ -961,6 +994,9 @@ __global__ __launch_bounds__(kGxwThreads) void sdr_gxw32_kernel(GxwItems items, 
       const long long xo = fi[32 + f];
       if (xo >= 0) atomicAdd(G.g_emb + xo + e, v);
     }
+    xs[(xb ^ 1) * 1024 + tid] = xn;   // the next tile's x (its bar() makes it visible)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) a[s] = an[s];
   }
   sb += __shfl_xor(sb, 32, 64);
   if (!won) return;
