@@ -50,8 +50,8 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / f16 MFMA peak
 HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`, averaged per dispatch by
 # scripts/pmcsum.py (KiB per dispatch), per workload
-PMC_TRAFFIC = {'timit_c2': os.path.join(HERE, 'profiles', 'r02_pmc_traffic_c2_s4h.json'),
-               'wsj_c4': os.path.join(HERE, 'profiles', 'r04_pmc_c4.json')}
+PMC_TRAFFIC = {'timit_c2': os.path.join(HERE, 'profiles', 'r05_pmc_traffic_c2.json'),
+               'wsj_c4': os.path.join(HERE, 'profiles', 'r05_pmc_c4.json')}
 
 
 def make_config(kw):

@@ -1,10 +1,10 @@
-# Round-4 check: selected GPU tests, then library / flag A/Bs on bench workloads.
+# Selected GPU tests, then library / flag A/Bs on bench workloads.
 #   TAG=name TESTS="tests/a.py tests/b.py" VARIANTS="SRF_LIB_PATH=...;..." [WL=wsj_c4]
-#   [VARIANTS2="--flag=1;..." WL2=wsj_c5 STEPS2=3] bash scripts/gpu_r04.sh
+#   [VARIANTS2="--flag=1;..." WL2=wsj_c5 STEPS2=3] bash scripts/gpu_ab.sh
 # Test failures (pytest status 1) do not stop the A/Bs; a crash or a timeout does.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-T=${TAG:-r04}
+T=${TAG:-ab}
 rc=0
 if [ -n "$TESTS" ]; then
   TAILN=25 TAG=$T bash scripts/gpu_steps.sh \

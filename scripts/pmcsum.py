@@ -14,7 +14,10 @@ import json
 import re
 import sys
 
-args = [a for a in sys.argv[1:] if not a.startswith('--')]
+argv = sys.argv[1:]
+if '--json' in argv:   # the option's value is not a positional argument
+    del argv[argv.index('--json') + 1]
+args = [a for a in argv if not a.startswith('--')]
 d = args[0]
 flt = args[1] if len(args) > 1 else ''
 out = sys.argv[sys.argv.index('--json') + 1] if '--json' in sys.argv else None
