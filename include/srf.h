@@ -164,7 +164,10 @@ typedef struct {
                                   launches, and kernels that occupy CUs for long (collectives),
                                   off the device meanwhile.  A member that waits too long stops
                                   and sets the fault word (srf_set_fault_flag): the results of
-                                  that launch are then wrong.  Other shapes ignore it. */
+                                  that launch are then wrong.  The group's counters live in the
+                                  workspace: it must be zero before the first grouped launch on
+                                  it, and each grouped launch leaves its counters zero again
+                                  (the timeout word excepted).  Other shapes ignore it. */
 } srf_sdr_range;
 /* pose_n fp8: 0 fp32 pose, 1 fp8 pose (fp32 u), 2 fp8 pose storing u in bf16 */
 int srf_route_sdr_pose_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,

@@ -40,9 +40,6 @@
 // Timing builds of the pipelined passes (wrong results, never shipped; scripts/build_ab.sh
 // + scripts/gpu_ab_route.sh): bit 1 = x of the chunk's first capsule, 2 = its W and bias,
 // 4 = no per-capsule barrier, 8 = no x reloads, 16 = no W reloads.
-#ifndef SRF_FWD32P_DBG
-#define SRF_FWD32P_DBG 0
-#endif
 // Schedule choices of the passes, fixed by measurement (rounds 2-4): the next capsule's
 // operands load between the MFMA steps of this capsule, each register group as soon as
 // its last reader has issued (pose_prog; issuing them all after the MFMAs measured ~4 %
@@ -508,13 +505,11 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       u[t] = mfma32h(fr.a[t][3], fr.b[2], u[t]);
     }
     __builtin_amdgcn_sched_barrier(0);
-#if !(SRF_FWD32P_DBG & 16)
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
       fr.a[t][1] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b);
       fr.a[t][3] = hload(rs.w, wvo + t * TSTEP, wcap_b + wplane_b + 32);
     }
-#endif
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < TW; ++t) {   // W1 x2
@@ -522,7 +517,6 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       u[t] = mfma32h(fr.a[t][2], fr.b[3], u[t]);
     }
     __builtin_amdgcn_sched_barrier(0);
-#if !(SRF_FWD32P_DBG & 8)
     if constexpr (XL) {
       fr.b[1] = xl_read(xl + 1 * kXlPiece);
       fr.b[3] = xl_read(xl + 3 * kXlPiece);
@@ -530,7 +524,6 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       fr.b[1] = hload(rs.x, xvo, xplane_b);
       fr.b[3] = hload(rs.x, xvo, xplane_b + 32);
     }
-#endif
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < TW; ++t) {   // W1 x1
@@ -538,14 +531,11 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       u[t] = mfma32h(fr.a[t][2], fr.b[2], u[t]);
     }
     __builtin_amdgcn_sched_barrier(0);
-#if !(SRF_FWD32P_DBG & 16)
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
       fr.a[t][0] = hload(rs.w, wvo + t * TSTEP, wcap_b);
       fr.a[t][2] = hload(rs.w, wvo + t * TSTEP, wcap_b + 32);
     }
-#endif
-#if !(SRF_FWD32P_DBG & 8)
     if constexpr (XL) {
       fr.b[0] = xl_read(xl);
       fr.b[2] = xl_read(xl + 2 * kXlPiece);
@@ -553,7 +543,6 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       fr.b[0] = hload(rs.x, xvo, 0);
       fr.b[2] = hload(rs.x, xvo, 32);
     }
-#endif
     __builtin_amdgcn_sched_barrier(0);
     return;
   } else if constexpr (DIN == 16) {
@@ -1227,31 +1216,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     __syncthreads();
     // one capsule: i + 1's tiles into unext while capsule i (in ucur) is finished; the loop
     // runs two steps with the roles swapped, so no register copy moves u between them
-#if SRF_FWD32P_DBG & 32
-    unsigned long long tph[4] = {0, 0, 0, 0}, tl = __builtin_amdgcn_s_memtime();
-#define SRF_PSTAMP(k) { const unsigned long long tn = __builtin_amdgcn_s_memtime(); tph[k] += tn - tl; tl = tn; }
-#else
-#define SRF_PSTAMP(k)
-#endif
     auto step = [&](int i, f16v (&ucur)[TW], f16v (&unext)[TW]) __attribute__((always_inline)) {
       const bool more = i + 1 < i1;
       if constexpr (XL)   // x of capsule i + 3 into the buffer capsule i + 1's x left
         x_dma(xs_b, A.xplane_b, xsrc(i + 3), wv, xbuf(i + 3));
       if (more) {   // capsule i + 1's tiles on the matrix cores (operands of i + 2 streamed in)
         const int in = min(i + 2, i1 - 1);
-#if SRF_FWD32P_DBG
-        // timing experiment (wrong results): 1 = x of the chunk's first capsule (cache-hot),
-        // 2 = W and bias of the first capsule, 3 = both
-        const int inx = (SRF_FWD32P_DBG & 1) ? i0 : in, inw = (SRF_FWD32P_DBG & 2) ? i0 : in;
-#else
-        const int inx = in, inw = in;
-#endif
         pose_prog<DIN, TW, XL>(fr, ones, unext, rs, wvo, bvo,
-                               x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                               A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8,
+                               x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                               A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8,
                                xbuf(i + 2) + lane * 16);
       }
-      SRF_PSTAMP(0)
       // finish capsule i: softmax over all waves' rows, couplings, s += c u
       float M, Z;
       {
@@ -1297,30 +1272,17 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
           acc[t][v] = a2.x;
           acc[t][v + 1] = a2.y;
         }
-      SRF_PSTAMP(1)
       if (more) {   // capsule i + 1's logits and stats, then the one barrier
         par ^= 1;
         logits(unext, par);
         if constexpr (XL) xl_wait<5 * TW + OWN + 1>();   // capsule i + 3's x has landed before the barrier
-        SRF_PSTAMP(2)
-#if SRF_FWD32P_DBG & 4
-        __builtin_amdgcn_sched_barrier(0);   // timing experiment: no barrier (wrong results)
-#else
         __syncthreads();
-#endif
-        SRF_PSTAMP(3)
       }
     };
     for (int i = i0; i < i1; i += 2) {
       step(i, uc, un);
       if (i + 1 < i1) step(i + 1, un, uc);
     }
-#if SRF_FWD32P_DBG & 32
-    if (lane == 0 && (blockIdx.x == 100 || blockIdx.x == 301) && (wv == 0 || wv == NW - 1))
-      printf("fwd32p blk %d wv %d caps %d: pose-issue %llu finish %llu logits %llu barrier %llu\n", blockIdx.x, wv,
-             i1 - i0, tph[0], tph[1], tph[2], tph[3]);
-#endif
-#undef SRF_PSTAMP
     if constexpr (XL) xl_wait();   // no DMA into LDS outlives the workgroup
   }
 #pragma unroll
@@ -1668,16 +1630,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       {
         load_c<OWN>(crow + (size_t)min(i + 1, i1 - 1) * cstep, A.Fs, cnext);
         const int in = min(i + 2, i1 - 1);
-#if SRF_FWD32P_DBG
-        // timing experiment (wrong results): 1 = x of the chunk's first capsule (cache-hot),
-        // 2 = W and bias of the first capsule, 3 = both
-        const int inx = (SRF_FWD32P_DBG & 1) ? i0 : in, inw = (SRF_FWD32P_DBG & 2) ? i0 : in;
-#else
-        const int inx = in, inw = in;
-#endif
         pose_prog<DIN, TW, XL>(fr, ones, unext, rs, wvo, bvo,
-                               x_voff<DIN>(inx, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                               A.xplane_b, A.zero_off, (uint32_t)inw * A.JDp * DIN * 2, (uint32_t)inw * A.JDp * 8,
+                               x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
+                               A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8,
                                xbuf(i + 2) + lane * 16);
       }
       // finish capsule i: sigma over all waves, stats, gL, gVc += gL u

@@ -209,6 +209,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_fwd_kernel(srf::SeqItems ite
     }
   }
   SEQ_FLUSH(g_stamps);
+  srf_grp::depart<GRP>(I.ws, X, utt, tid);
 }
 
 size_t fwd_lds(int J, int D) {

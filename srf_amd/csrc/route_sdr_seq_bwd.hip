@@ -374,6 +374,7 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
   }
   SEQ_FLUSH(g_stamps);
   if (carry_io && ev && gm == 0) carry_io[tid] = carry;   // dL/dv_{t0-1} for the earlier range
+  srf_grp::depart<GRP>(I.ws, X, utt, tid);
 }
 
 size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {

@@ -334,6 +334,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_fwd_kernel(srf::SeqItems items
       wg_bar<!GRP>();
     }
   }
+  srf_grp::depart<GRP>(I.ws, X, b, tid);
 }
 
 // ------------------------------------------------------------------ backward
@@ -525,6 +526,7 @@ __global__ __launch_bounds__(kNT) void sdr_stream_bwd_kernel(srf::SeqItems items
   if (carry_io && lead)
 #pragma unroll
     for (int n = 0; n < NE; ++n) carry_io[tid + n * kNT] = carry[n];
+  srf_grp::depart<GRP>(I.ws, X, b, tid);
 }
 
 // ------------------------------------------------------------------ host

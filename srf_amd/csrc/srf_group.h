@@ -42,10 +42,10 @@ struct Grp {
 };
 
 // Item workspace: `pre` floats of the kernel's own (the stream backward's gL scratch),
-// then the counters [B] + the timeout word (256-B padded), then the exchange area
-// [2][B][kMaxGroup][JD].
+// then the arrival counters [B], the timeout word and the departure counters [B]
+// (256-B padded), then the exchange area [2][B][kMaxGroup][JD].
 __host__ __device__ inline size_t coff(size_t pre) { return (pre + 63) / 64 * 64; }
-__host__ __device__ inline size_t xoff(size_t pre, int B) { return coff(pre) + ((size_t)B + 1 + 63) / 64 * 64; }
+__host__ __device__ inline size_t xoff(size_t pre, int B) { return coff(pre) + ((size_t)2 * B + 1 + 63) / 64 * 64; }
 __host__ __device__ inline size_t floats(size_t pre, int B, int JD) {
   return xoff(pre, B) + (size_t)2 * B * kMaxGroup * JD;
 }
@@ -101,9 +101,29 @@ __device__ __forceinline__ void allreduce(float* part, int JD, float* ws, const 
   __syncthreads();
 }
 
+// A grouped launch leaves its counters zero for the next launch on the same workspace
+// (no memset per launch: on the last layer's stream that was a fill kernel per range on
+// the critical chain).  Every member counts itself out after its last exchange; the
+// last of an utterance's G members zeroes the utterance's arrival and departure
+// counters -- by then none of them polls.  The timeout word stays set: the caller
+// zeroes the counter area before the first grouped launch on a workspace.
+template <bool GRP>
+__device__ __forceinline__ void depart(float* ws, const Grp& X, int b, int tid) {
+  if constexpr (GRP) {
+    if (tid == 0) {
+      unsigned* cnt = reinterpret_cast<unsigned*>(ws + X.coff);
+      unsigned* dep = cnt + X.B + 1;
+      const unsigned old = __hip_atomic_fetch_add(dep + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1 == (unsigned)X.G) {
+        __hip_atomic_store(cnt + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dep + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 // The launch's group size (its items agree; 1 when ungrouped) and exchange geometry
-// (`pre` floats of the kernel's own at each item workspace's start); a grouped launch
-// zeroes its items' arrival counters first (memset nodes under stream capture).
+// (`pre` floats of the kernel's own at each item workspace's start).
 inline int setup(const srf::SeqItems& items, int B, size_t pre, Grp& X, hipStream_t st) {
   const int G = std::max(1, items.it[0].group);
   for (int k = 1; k < items.n; ++k)
@@ -117,10 +137,9 @@ inline int setup(const srf::SeqItems& items, int B, size_t pre, Grp& X, hipStrea
   SRF_REQUIRE((long)B * items.n * G <= cus - kReserveCUs,
               "SDR recurrence: %d utterances x %d ranges x group %d workgroups exceed the %d CUs they may take (%d "
               "kept free)", B, items.n, G, cus - kReserveCUs, kReserveCUs);
-  for (int k = 0; k < items.n; ++k) {
+  for (int k = 0; k < items.n; ++k)
     SRF_REQUIRE(items.it[k].ws, "SDR recurrence: a grouped launch needs the range workspace");
-    SRF_HIP_TRY(hipMemsetAsync(items.it[k].ws + X.coff, 0, srf::align_up((size_t)(B + 1) * 4, 16), st));
-  }
+  (void)st;
   return SRF_OK;
 }
 

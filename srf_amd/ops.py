@@ -684,7 +684,7 @@ class SdrStack(torch.autograd.Function):
                 embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
                 stats.append(torch.empty((B * T, 4), device=dev, dtype=torch.float32))
             us.append(P.u_empty(l, T if store else P.nmax, dev))
-            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
+            rws.append(torch.zeros(max(P.rws[l], 16), device=dev, dtype=torch.uint8))   # group counters zero (srf_group.h)
         main = torch.cuda.current_stream(dev)
         sa, sb, sc = _layer_streams(dev, 3, 'fwd')
         ev_a, ev_p = P.events('fwd_a', P.K + L), P.events('fwd_p', P.K)
@@ -812,7 +812,7 @@ class SdrStack(torch.autograd.Function):
             WTs.append(torch.empty(Ws[l].numel(), device=dev))
             gus.append(torch.empty(P.u_floats(l, P.nmax), device=dev))
             urs.append(us[l] if store else P.u_empty(l, P.nmax, dev))
-            rws.append(torch.empty(max(P.rws[l], 16), device=dev, dtype=torch.uint8))
+            rws.append(torch.zeros(max(P.rws[l], 16), device=dev, dtype=torch.uint8))   # group counters zero (srf_group.h)
             pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
                                    dtype=torch.uint8) if l < L - 1 else None)
         main = torch.cuda.current_stream(dev)

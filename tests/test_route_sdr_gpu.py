@@ -306,7 +306,8 @@ def test_sdr_groups_match_one_workgroup(cuda, J, D, iters, mf, N, lp, rp):
     streaming and the register-resident recurrence kernels).  Forward v / couplings and
     backward gu / carry equal the one-workgroup launch up to the reassociation of the
     partial sums, for groups of 2, 3 and 8 (members without capsules included), over
-    two frame ranges, and no member gave up waiting (the timeout word stays 0)."""
+    two frame ranges, and no member gave up waiting (the timeout word stays 0); every
+    launch leaves the workspace's group counters zero (three launches reuse each)."""
     import ctypes
     from srf_amd import _lib
     L = _lib.lib()
@@ -353,6 +354,9 @@ def test_sdr_groups_match_one_workgroup(cuda, J, D, iters, mf, N, lp, rp):
         if G > 1:
             for w in wss:
                 assert w[coff + B].view(torch.int32).item() == 0, 'a group member timed out'
+                # each launch left its arrival / departure counters zero for the next one
+                # (srf_group.h depart: no memset per launch)
+                assert w[coff:coff + 2 * B + 1].view(torch.int32).abs().sum().item() == 0, 'counters left set'
         outs.append((G, v, cs, gu, carry, v2))
     # reassociated fp32 sums, carried through the frames: 1e-5 of each output's magnitude
     for G, *got in outs[1:]:
