@@ -479,14 +479,22 @@ __device__ __forceinline__ h8 xl_read(const char* p) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"((uint32_t)reinterpret_cast<uintptr_t>(p)));
   return r;
 }
-template <int DIN, int TW, bool XL = false>
+// XJ (with XL, din 32): x just in time -- this capsule's fragments are read from xl at
+// the start and not prefetched for the next capsule, so they hold no registers between
+// poses (the four-row-tile passes have none to spare).
+template <int DIN, int TW, bool XL = false, bool XJ = false>
 __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones, f16v (&u)[TW],
                                           const Rsrc3& rs, uint32_t wvo, uint32_t bvo, uint32_t xvo, int h,
                                           uint32_t wplane_b, uint32_t xplane_b, uint32_t zero_off, uint32_t wcap_b,
                                           uint32_t bcap_b, const char* xl = nullptr) {
   constexpr uint32_t TSTEP = 32 * DIN * 2;
-  if constexpr (XL)   // the x fragments the previous call read from LDS (xl_read) have arrived
+  static_assert(!XJ || (XL && DIN == 32), "XJ: the shared x fragments of din 32");
+  if constexpr (XJ) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) fr.b[q] = xl_read(xl + q * kXlPiece);
+  } else if constexpr (XL) {   // the x fragments the previous call read from LDS (xl_read) have arrived
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fr.b[0]), "+v"(fr.b[1]), "+v"(fr.b[2]), "+v"(fr.b[3]));
+  }
 #pragma unroll
   for (int t = 0; t < TW; ++t) u[t] = mfma32(fr.bias[t], ones, f16v{});
   __builtin_amdgcn_sched_barrier(0);
@@ -498,6 +506,8 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
     }
   }
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (XJ)   // this capsule's x fragments (read above, behind the bias MFMAs)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fr.b[0]), "+v"(fr.b[1]), "+v"(fr.b[2]), "+v"(fr.b[3]));
   if constexpr (DIN == 32) {
 #pragma unroll
     for (int t = 0; t < TW; ++t) {   // W2 x1, both k-halves
@@ -517,7 +527,8 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       u[t] = mfma32h(fr.a[t][2], fr.b[3], u[t]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (XL) {
+    if constexpr (XJ) {
+    } else if constexpr (XL) {
       fr.b[1] = xl_read(xl + 1 * kXlPiece);
       fr.b[3] = xl_read(xl + 3 * kXlPiece);
     } else {
@@ -536,7 +547,8 @@ __device__ __forceinline__ void pose_prog(Frags32<DIN, TW>& fr, const bf8& ones,
       fr.a[t][0] = hload(rs.w, wvo + t * TSTEP, wcap_b);
       fr.a[t][2] = hload(rs.w, wvo + t * TSTEP, wcap_b + 32);
     }
-    if constexpr (XL) {
+    if constexpr (XJ) {
+    } else if constexpr (XL) {
       fr.b[0] = xl_read(xl);
       fr.b[2] = xl_read(xl + 2 * kXlPiece);
     } else {
@@ -914,6 +926,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 
   f4* vcl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float2* st = reinterpret_cast<float2*>(lds + (size_t)NW * TW * 4 * 64 * 4);
+  // din 32: each capsule's x fragments DMA'd once per workgroup into LDS (x_dma, two
+  // buffers) and read just in time by the pose (pose_prog XJ): no per-wave x loads, and
+  // no x registers held between poses (a separate LDS object: no aliasing with the stats)
+  constexpr bool XJ = DIN == 32 && NW > 1;
+  __shared__ __attribute__((aligned(16))) char xls[XJ ? 2 * 4 * kXlPiece : 16];
+  const char* xs_b = static_cast<const char*>(A.xs);
+  auto xsrc = [&](int c) { return x_voff<DIN>(min(c, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
+  auto xbuf = [&](int c) { return xls + (c & 1) * 4 * kXlPiece; };
   // Vc rows of this wave's tiles -> private LDS in fragment order
 #pragma unroll
   for (int t = 0; t < TW; ++t)
@@ -942,6 +962,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                            A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
                            fr);
+    if constexpr (XJ) {   // x of capsules i0, i0 + 1 before the first pose
+      x_dma(xs_b, A.xplane_b, xsrc(i0), wv, xbuf(i0));
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 1), wv, xbuf(i0 + 1));
+      xl_wait();
+      __syncthreads();
+    }
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
       // partial agreement dots <u_ij, Vc_j> over this lane's rows (packed FMA pairs)
@@ -988,9 +1014,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       }
       } else {
       const int in = min(i + 1, i1 - 1);
-      pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
-                         x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                         A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
+      pose_prog<DIN, TW, XJ, XJ>(fr, ones, u, rs, wvo, bvo,
+                                 x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                                 A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2,
+                                 (uint32_t)in * A.JDp * 8, xbuf(i) + lane * 16);
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1030,7 +1057,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         // per-wave stats of the 32 frames -> LDS; half h combines waves [h*NW/2, (h+1)*NW/2)
         float2* slot = st + par * NW * 32;
         if (h == 0) slot[wv * 32 + r] = make_float2(M, Z);
+        if constexpr (XJ) xl_wait();   // x of capsule i + 1 (DMA'd after the last barrier) lands before this one
         __syncthreads();
+        // every wave's pose read x of capsule i: its buffer takes capsule i + 2's (unconditional:
+        // past the chunk it reloads the last capsule into a buffer no pose reads any more)
+        if constexpr (XJ) x_dma(xs_b, A.xplane_b, xsrc(i + 2), wv, xbuf(i + 2));
         constexpr int HW = NW / 2;
         float2 sv[HW];
 #pragma unroll
@@ -1346,6 +1377,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
 
   f4* gsl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float* st = lds + (size_t)NW * TW * 4 * 64 * 4;
+  // din 32: shared x fragments read just in time, as route_fwd32_kernel
+  constexpr bool XJ = DIN == 32 && NW > 1;
+  __shared__ __attribute__((aligned(16))) char xls[XJ ? 2 * 4 * kXlPiece : 16];
+  const char* xs_b = static_cast<const char*>(A.xs);
+  auto xsrc = [&](int c) { return x_voff<DIN>(min(c, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
+  auto xbuf = [&](int c) { return xls + (c & 1) * 4 * kXlPiece; };
 #pragma unroll
   for (int t = 0; t < TW; ++t)
 #pragma unroll
@@ -1369,6 +1406,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     fetch32<DIN, TW, true>(rs, wvo, bvo, x_voff<DIN>(i0, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                            A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)i0 * A.JDp * DIN * 2, (uint32_t)i0 * A.JDp * 8,
                            fr);
+    if constexpr (XJ) {   // x of capsules i0, i0 + 1 before the first pose
+      x_dma(xs_b, A.xplane_b, xsrc(i0), wv, xbuf(i0));
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 1), wv, xbuf(i0 + 1));
+      xl_wait();
+      __syncthreads();
+    }
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
       // partial dots <u_ij, gs_j> over this lane's rows
@@ -1419,9 +1462,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       }
       } else {
       const int in = min(i + 1, i1 - 1);
-      pose_prog<DIN, TW>(fr, ones, u, rs, wvo, bvo,
-                         x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h, A.wplane_b,
-                         A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2, (uint32_t)in * A.JDp * 8);
+      pose_prog<DIN, TW, XJ, XJ>(fr, ones, u, rs, wvo, bvo,
+                                 x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                                 A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2,
+                                 (uint32_t)in * A.JDp * 8, xbuf(i) + lane * 16);
       // this capsule's couplings: the pose MFMAs in flight hide their latency (no
       // registers held across capsules)
       load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
@@ -1453,7 +1497,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       if constexpr (NW > 1) {
         float* slot = st + par * NW * 32;
         if (h == 0) slot[wv * 32 + r] = S;
+        if constexpr (XJ) xl_wait();   // x of capsule i + 1 lands before the barrier that publishes it
         __syncthreads();
+        if constexpr (XJ) x_dma(xs_b, A.xplane_b, xsrc(i + 2), wv, xbuf(i + 2));   // into capsule i's buffer
         constexpr int HW = NW / 2;
         float sh = 0.f;
 #pragma unroll

@@ -642,7 +642,9 @@ __device__ __forceinline__ f16v mfma32bf(const bf8& a, const bf8& b, const f16v&
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int DIN>
+// FB: frames per workgroup -- 128 (waves 2 x 2 over 128 frames x 128 rows) or 64 (the
+// four waves stacked over 256 rows): a frame range of B x 10 frames pads less to 64.
+template <int DIN, int FB = 128>
 __global__ __launch_bounds__(256, 2) void sdr_pose3b_kernel(GemmItems items, int N, int lpad, int in_n, int JD,
                                                             int nrb) {
   const GemmItem& G = items.it[blockIdx.z];
@@ -652,14 +654,15 @@ __global__ __launch_bounds__(256, 2) void sdr_pose3b_kernel(GemmItems items, int
   float* __restrict__ u = G.o;
   const int Q = G.Q;
   const FrameMap fm = G.fm;
-  if ((int)(blockIdx.x / nrb) * 128 >= Q) return;
+  if ((int)(blockIdx.x / nrb) * FB >= Q) return;
   constexpr int KS = DIN / 16;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int i = blockIdx.y;
   const int rb = blockIdx.x % nrb, fb = blockIdx.x / nrb;
   const int w = i / N, n = i - w * N;
-  const int f0 = fb * 128 + (wv & 1) * 64, r0 = rb * 128 + (wv >> 1) * 64;
+  const int f0 = FB == 128 ? fb * 128 + (wv & 1) * 64 : fb * 64;
+  const int r0 = FB == 128 ? rb * 128 + (wv >> 1) * 64 : rb * 256 + wv * 64;
   bf8 xa[2][KS][3];
 #pragma unroll
   for (int ft = 0; ft < 2; ++ft) {
@@ -1217,10 +1220,22 @@ int pose_n(const SGeom& g, const GemmItems& it, hipStream_t st, int mode = 0) {
     return SRF_OK;
   }
   if ((g.din == 32 || g.din == 64) && g.JD() % 8 == 0) {   // fp32 pose on bf16 MFMA, three-term split operands
-    if (g.din == 32)
-      hipLaunchKernelGGL(sdr_pose3b_kernel<32>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
-    else
-      hipLaunchKernelGGL(sdr_pose3b_kernel<64>, grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb);
+    // 64-frame workgroups where they pad the range's frames less than 128-frame ones
+    const bool f64 = (Q + 63) / 64 * 64 < (Q + 127) / 128 * 128;
+    const int nrb64 = (g.JD() + 255) / 256;
+    const dim3 grid64(nrb64 * ((Q + 63) / 64), g.in_n(), it.n);
+#define SRF_POSE3B(DIN)                                                                                          \
+  if (f64)                                                                                                       \
+    hipLaunchKernelGGL((sdr_pose3b_kernel<DIN, 64>), grid64, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), \
+                       nrb64);                                                                                   \
+  else                                                                                                           \
+    hipLaunchKernelGGL((sdr_pose3b_kernel<DIN, 128>), grid32, dim3(256), 0, st, it, g.N, g.lpad, g.in_n(), g.JD(), nrb)
+    if (g.din == 32) {
+      SRF_POSE3B(32);
+    } else {
+      SRF_POSE3B(64);
+    }
+#undef SRF_POSE3B
     SRF_LAUNCH_CHECK("sdr_pose3b");
     return SRF_OK;
   }
