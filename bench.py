@@ -244,6 +244,11 @@ def measure(workload, args, world, rank, dev):
     if args.sdr_last_gxw_inline:
         from srf_amd import ops
         ops.SDR_LAST_GXW_SIDE = False
+    if args.dr_chunks:
+        # "l:c,l:c" input-capsule chunks of DR layer l's routing passes (A/B of the plan's choice)
+        for item in args.dr_chunks.split(','):
+            l, c = item.split(':')
+            model.n_chunks_override[int(l)] = int(c)
     if args.sdr_last_group is not None:
         g = [int(x) for x in args.sdr_last_group.split(',')]
         model.sdr_options['last_group'] = (g[0], g[-1])
@@ -415,6 +420,8 @@ def main():
                     help='SDR stack: the gx and gW launches of din-32 layers separately (default: fused)')
     ap.add_argument('--sdr-capsnorm-per-layer', action='store_true',
                     help='SDR stack: one LN/dropout launch per inner layer and range (default: one per diagonal)')
+    ap.add_argument('--dr-chunks', default='',
+                    help='DR: input-capsule chunks per layer, "l:c,..." (default: the plan\'s choice; A/B)')
     ap.add_argument('--sdr-last-gxw-inline', action='store_true',
                     help='SDR stack: the last layer\'s gx / gW on its recurrence\'s stream (default: a side stream)')
     ap.add_argument('--flat-allreduce', action='store_true',

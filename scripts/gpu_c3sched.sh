@@ -1,11 +1,11 @@
 # wsj_c3 bench step under launch variants (env assignments; 'eager' = --eager), each
 # with a kernel trace for scripts/c3_timeline.py:
-#   TAG=name VARIANTS="base;DEBUG_HIP_FORCE_GRAPH_QUEUES=8;eager" [NOTRACE=1] bash scripts/gpu_c3sched.sh
+#   TAG=name VARIANTS="base;DEBUG_HIP_FORCE_GRAPH_QUEUES=8;eager" [NOTRACE=1] [WL=wsj_c4] bash scripts/gpu_c3sched.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-c3sched}
 mkdir -p $OUT
-B="$GRAFT_REPO_ROOT/bench.py --workload wsj_c3 --extra= --no-cpu-baseline"
+B="$GRAFT_REPO_ROOT/bench.py --workload ${WL:-wsj_c3} --extra= --no-cpu-baseline"
 cd /tmp && export TMPDIR=/tmp
 IFS=';' read -ra VS <<< "${VARIANTS:-base}"
 i=0
