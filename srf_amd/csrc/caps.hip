@@ -655,6 +655,111 @@ __device__ __forceinline__ void capsnorm_bwd_row(
   }
 }
 
+// One wave per row for the plain LN + dropout rows (no head) of n = 64 * NPL values:
+// the row in registers as float4 (NPL / 4 per lane), both moments and both backward
+// sums as wave reductions -- no LDS and no barrier.  These rows are 1-4 KB: a 256-thread
+// block per row spent most of its time in its block reductions.  Dropout masks are keyed
+// by the element index, so they do not depend on the mapping.
+template <int NPL>
+__device__ __forceinline__ void capsnorm_fwd_wave(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, bool drop, float p,
+                                                  unsigned long long seed, unsigned stream, float* __restrict__ y,
+                                                  float* __restrict__ stat, int f, int lane) {
+  constexpr int n = 64 * NPL, NV = NPL / 4;
+  const f4* xr = reinterpret_cast<const f4*>(x + (size_t)f * n);
+  f4 v[NV];
+  float s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    v[k] = xr[k * 64 + lane];
+    s1 += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+  }
+  const float mean = wave_sum(s1) / n;
+  float s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const f4 d = v[k] - mean;
+    s2 += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+  }
+  const float rstd = 1.f / sqrtf(wave_sum(s2) / n + kLnEps);
+  f4* yr = reinterpret_cast<f4*>(y + (size_t)f * n);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = k * 64 + lane;
+    const f4 g = reinterpret_cast<const f4*>(gamma)[q], b = reinterpret_cast<const f4*>(beta)[q];
+    const size_t gi = (size_t)f * n + 4 * q;
+    f4 o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = ((v[k][c] - mean) * rstd * g[c] + b[c]) * drop_mult(drop, seed, stream, gi + c, p);
+    yr[q] = o;
+  }
+  if (lane == 0) {
+    stat[4 * f] = mean;
+    stat[4 * f + 1] = rstd;
+  }
+}
+
+template <int NPL>
+__device__ __forceinline__ void capsnorm_bwd_wave(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                  bool drop, float p, unsigned long long seed, unsigned stream,
+                                                  const float* __restrict__ stat, const float* __restrict__ g_in,
+                                                  float* __restrict__ g_x, float* __restrict__ gpart, int f, int lane) {
+  constexpr int n = 64 * NPL, NV = NPL / 4;
+  const float mean = stat[4 * f], rstd = stat[4 * f + 1];
+  const f4* xr = reinterpret_cast<const f4*>(x + (size_t)f * n);
+  const f4* gr = reinterpret_cast<const f4*>(g_in + (size_t)f * n);
+  f4* pg = reinterpret_cast<f4*>(gpart + (size_t)f * 2 * n);
+  f4 xh[NV], t[NV];
+  float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = k * 64 + lane;
+    const f4 xv = xr[q], go = gr[q], gam = reinterpret_cast<const f4*>(gamma)[q];
+    const size_t gi = (size_t)f * n + 4 * q;
+    f4 gxh, gg;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      xh[k][c] = (xv[c] - mean) * rstd;
+      const float g = go[c] * drop_mult(drop, seed, stream, gi + c, p);   // gradient wrt the LN output
+      gxh[c] = g * xh[k][c];
+      gg[c] = g;
+      t[k][c] = g * gam[c];
+      a1 += t[k][c];
+      a2 += t[k][c] * xh[k][c];
+    }
+    pg[q] = gxh;
+    pg[n / 4 + q] = gg;
+  }
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  f4* ox = reinterpret_cast<f4*>(g_x + (size_t)f * n);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    f4 o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = rstd * (t[k][c] - a1 / n - xh[k][c] * a2 / n);
+    ox[k * 64 + lane] = o;
+  }
+}
+
+template <int NPL, bool BWD>
+__global__ __launch_bounds__(256) void capsnorm_wave_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, int training, float p,
+                                                            unsigned long long seed,
+                                                            const unsigned long long* __restrict__ seed_src,
+                                                            unsigned stream, float* __restrict__ y,
+                                                            float* __restrict__ stat, const float* __restrict__ g_in,
+                                                            float* __restrict__ gpart, RowMap rmap, int rows) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= rows) return;   // whole waves: nothing below synchronises
+  const unsigned long long sd = srf_step_seed(seed, seed_src);
+  const bool drop = training && p > 0.f;
+  if constexpr (BWD)
+    capsnorm_bwd_wave<NPL>(x, gamma, drop, p, sd, stream, stat, g_in, y, gpart, rmap.row(w), threadIdx.x & 63);
+  else
+    capsnorm_fwd_wave<NPL>(x, gamma, beta, drop, p, sd, stream, y, stat, rmap.row(w), threadIdx.x & 63);
+}
+
 __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(
     const float* __restrict__ x, int n, const float* __restrict__ gamma, const float* __restrict__ beta, int training,
     float p, unsigned long long seed, const unsigned long long* __restrict__ seed_src, unsigned stream,
@@ -681,6 +786,24 @@ struct CnItems {
   srf_capsnorm_range it[SRF_CAPSNORM_MAX_ITEMS];
   int B, T, n_items;
 };
+
+template <int NPL, bool BWD>
+__global__ __launch_bounds__(256) void capsnorm_range_n_wave_kernel(CnItems items, int training, float p,
+                                                                    unsigned long long seed,
+                                                                    const unsigned long long* __restrict__ seed_src) {
+  const srf_capsnorm_range& r = items.it[blockIdx.y];
+  const int nt = r.t1 - r.t0;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= items.B * nt) return;   // whole waves: nothing below synchronises
+  const int f = RowMap{items.T, r.t0, nt}.row(w);
+  const unsigned stream = (unsigned)(kStreamMid0 + r.layer);
+  const unsigned long long sd = srf_step_seed(seed, seed_src);
+  const bool drop = training && p > 0.f;
+  if constexpr (BWD)
+    capsnorm_bwd_wave<NPL>(r.x, r.gamma, drop, p, sd, stream, r.stat, r.g_y, r.g_x, r.gpart, f, threadIdx.x & 63);
+  else
+    capsnorm_fwd_wave<NPL>(r.x, r.gamma, r.beta, drop, p, sd, stream, r.y, r.stat, f, threadIdx.x & 63);
+}
 
 template <bool BWD>
 __global__ __launch_bounds__(256) void capsnorm_range_n_kernel(CnItems items, int n, int training, float p,
@@ -767,6 +890,23 @@ int check_caps(int B, int T, int PH, int PD) {
 }
 
 }  // namespace
+
+// the wave-per-row kernels for n = 256, 512, 1024 (C2 / C3 / C4 / C5 widths); false: other n
+template <bool BWD>
+static bool capsnorm_wave(int n, int rows, RowMap rm, const float* x, const float* gamma, const float* beta,
+                          int training, float p, unsigned long long seed, unsigned stream, float* y, float* stat,
+                          const float* g_in, float* gpart, hipStream_t st) {
+  const dim3 grid((rows + 3) / 4);
+#define SRF_CN_WAVE(NPL)                                                                                             \
+  hipLaunchKernelGGL((capsnorm_wave_kernel<NPL, BWD>), grid, dim3(256), 0, st, x, gamma, beta, training, p, seed,   \
+                     srf::seed_source(), stream, y, stat, g_in, gpart, rm, rows)
+  if (n == 256) SRF_CN_WAVE(4);
+  else if (n == 512) SRF_CN_WAVE(8);
+  else if (n == 1024) SRF_CN_WAVE(16);
+  else return false;
+#undef SRF_CN_WAVE
+  return true;
+}
 
 extern "C" {
 
@@ -908,6 +1048,11 @@ size_t srf_capsnorm_bwd_workspace(int F, int n, int J) {
 int srf_capsnorm_fwd(const float* x, int F, int n, const float* gamma, const float* beta, int training, float p,
                      unsigned long long seed, int layer, float* y, float* stat, void* stream) {
   SRF_REQUIRE(x && gamma && beta && y && stat && F > 0 && n > 0 && n <= kMaxVec, "bad capsnorm arguments");
+  if (capsnorm_wave<false>(n, F, RowMap::all(F), x, gamma, beta, training, p, seed, (unsigned)(kStreamMid0 + layer), y,
+                           stat, nullptr, nullptr, static_cast<hipStream_t>(stream))) {
+    SRF_LAUNCH_CHECK("capsnorm_fwd");
+    return SRF_OK;
+  }
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, static_cast<hipStream_t>(stream),
                      x, n, gamma, beta, training, p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0,
                      (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (float*)nullptr, kLengthEps,
@@ -923,6 +1068,11 @@ int srf_capsnorm_fwd_range(const float* x, int B, int T, int t0, int t1, int n, 
                   n <= kMaxVec,
               "bad capsnorm range arguments");
   if (t0 == t1) return SRF_OK;
+  if (capsnorm_wave<false>(n, B * (t1 - t0), RowMap{T, t0, t1 - t0}, x, gamma, beta, training, p, seed,
+                           (unsigned)(kStreamMid0 + layer), y, stat, nullptr, nullptr, static_cast<hipStream_t>(stream))) {
+    SRF_LAUNCH_CHECK("capsnorm_fwd_range");
+    return SRF_OK;
+  }
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(B * (t1 - t0)), dim3(256), (size_t)(n + 8) * 4,
                      static_cast<hipStream_t>(stream), x, n, gamma, beta, training, p, seed, srf::seed_source(),
                      (unsigned)(kStreamMid0 + layer), y, stat, 0, 0, 0, (const float*)nullptr, (const float*)nullptr,
@@ -938,6 +1088,12 @@ int srf_capsnorm_bwd_range(const float* x, int B, int T, int t0, int t1, int n, 
                   n > 0 && n <= kMaxVec,
               "bad capsnorm range arguments");
   if (t0 == t1) return SRF_OK;
+  if (capsnorm_wave<true>(n, B * (t1 - t0), RowMap{T, t0, t1 - t0}, x, gamma, beta, training, p, seed,
+                          (unsigned)(kStreamMid0 + layer), g_x, const_cast<float*>(stat), g_y, gpart,
+                          static_cast<hipStream_t>(stream))) {
+    SRF_LAUNCH_CHECK("capsnorm_bwd_range");
+    return SRF_OK;
+  }
   hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(B * (t1 - t0)), dim3(256), (size_t)(n + 8) * 4,
                      static_cast<hipStream_t>(stream), x, n, gamma, beta, training, p, seed, srf::seed_source(),
                      (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr, (const float*)nullptr,
@@ -963,6 +1119,27 @@ static int capsnorm_range_n(const srf_capsnorm_range* r, int n_items, int B, int
     rows = std::max(rows, B * (q.t1 - q.t0));
   }
   if (it.n_items == 0) return SRF_OK;
+  if (n == 256 || n == 512 || n == 1024) {   // one wave per row
+    const dim3 gw((rows + 3) / 4, it.n_items);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+#define SRF_CN_RANGE(NPL)                                                                                    \
+  if (bwd)                                                                                                  \
+    hipLaunchKernelGGL((capsnorm_range_n_wave_kernel<NPL, true>), gw, dim3(256), 0, st, it, training, p, seed,  \
+                       srf::seed_source());                                                                 \
+  else                                                                                                      \
+    hipLaunchKernelGGL((capsnorm_range_n_wave_kernel<NPL, false>), gw, dim3(256), 0, st, it, training, p, seed, \
+                       srf::seed_source())
+    if (n == 256) {
+      SRF_CN_RANGE(4);
+    } else if (n == 512) {
+      SRF_CN_RANGE(8);
+    } else {
+      SRF_CN_RANGE(16);
+    }
+#undef SRF_CN_RANGE
+    SRF_LAUNCH_CHECK("capsnorm_range_n");
+    return SRF_OK;
+  }
   const dim3 grid(rows, it.n_items);
   if (bwd)
     hipLaunchKernelGGL(capsnorm_range_n_kernel<true>, grid, dim3(256), (size_t)(n + 8) * 4,
@@ -1011,9 +1188,11 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
   float* part = static_cast<float*>(workspace);
   float* sum = part + srf::align_up((size_t)F * 2 * n * 4, 256) / 4;
   float* scratch = sum + srf::align_up((size_t)2 * n * 4, 256) / 4;
-  hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, st, x, n, gamma, beta, training, p,
-                     seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1, (const float*)nullptr,
-                     (const float*)nullptr, g_x, part, RowMap::all(F));
+  if (!capsnorm_wave<true>(n, F, RowMap::all(F), x, gamma, beta, training, p, seed, (unsigned)(kStreamMid0 + layer), g_x,
+                           const_cast<float*>(stat), g_y, part, st))
+    hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, st, x, n, gamma, beta, training,
+                       p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1,
+                       (const float*)nullptr, (const float*)nullptr, g_x, part, RowMap::all(F));
   SRF_LAUNCH_CHECK("capsnorm_bwd");
   (void)sum;
   return srf::colsum(part, F, 2 * n, nullptr, scratch, st, srf::ColSplit{{g_gamma, g_beta, nullptr, nullptr}, {n, n, 0, 0}});

@@ -57,11 +57,13 @@ def test_primary_caps(cuda, PH, PD, p):
         assert e <= 1e-3 * want.abs().max().item() + 1e-6, (name, e)
 
 
-@pytest.mark.parametrize('head', [False, True])
+@pytest.mark.parametrize('head,J,D', [(False, 8, 16), (True, 63, 16),
+                                      # the wave-per-row kernels: rows of 256, 512, 1024 values
+                                      (False, 16, 16), (False, 16, 32), (False, 32, 32)])
 @pytest.mark.parametrize('p', [0.0, 0.1])
-def test_capsnorm_and_head(cuda, head, p):
+def test_capsnorm_and_head(cuda, head, J, D, p):
     from srf_amd import ops
-    B, T, J, D = 2, 9, 63 if head else 8, 16
+    B, T = 2, 9   # 18 rows: the last four-row workgroup of the wave kernels is partial
     rng = np.random.default_rng(3)
     v = rng.standard_normal((B, T, J, D)) * 0.3
     g = torch.Generator().manual_seed(2)
