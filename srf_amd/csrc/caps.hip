@@ -249,10 +249,11 @@ __global__ void proj_bwd_w_kernel(const float* __restrict__ X, const float* __re
   const int f0 = ch * fchunk, f1 = min(F, f0 + fchunk);
   const int cols = K * PH + PH;
   if (k < K) {
-    for (int p0 = 0; p0 < PH; p0 += 8) {
-      float acc[8];
+    // 16 outputs per pass: X is read once for PH <= 16 (the C2-C5 widths)
+    for (int p0 = 0; p0 < PH; p0 += 16) {
+      float acc[16];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
       // frames in batches of 8: the batch's X loads are in flight together
       for (int fb = f0; fb < f1; fb += 8) {
         float xv[8];
@@ -262,12 +263,12 @@ __global__ void proj_bwd_w_kernel(const float* __restrict__ X, const float* __re
         for (int u = 0; u < 8; ++u) {
           if (fb + u >= f1) break;
 #pragma unroll
-          for (int q = 0; q < 8; ++q)
+          for (int q = 0; q < 16; ++q)
             if (p0 + q < PH) acc[q] += xv[u] * g_e[(size_t)(fb + u) * PH + p0 + q];
         }
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int q = 0; q < 16; ++q)
         if (p0 + q < PH) part[(size_t)ch * cols + (size_t)k * PH + p0 + q] = acc[q];
     }
   }
