@@ -279,6 +279,53 @@ __global__ void proj_bwd_w_kernel(const float* __restrict__ X, const float* __re
   }
 }
 
+// The same partials on v_mfma_f32_16x16x4_f32 (PH <= 16): part^T[k][p] = X^T[k][f] g_e[f][p]
+// with K = frames.  Wave = 16 rows k x the PH columns p over the chunk's frames, four per
+// MFMA (A: lane l holds X[f0 + (l >> 4)][k0 + (l & 15)], 64-byte row pieces; B: g_e[f0 +
+// (l >> 4)][l & 15]); eight K steps' loads in flight per batch.  fp32 products and
+// accumulation, as the VALU kernel (the sums reassociate).
+__global__ __launch_bounds__(256) void proj_bwd_w_mfma_kernel(const float* __restrict__ X,
+                                                              const float* __restrict__ g_e, int F, int K, int PH,
+                                                              int fchunk, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ch = blockIdx.y;
+  const int k0 = (blockIdx.x * 4 + wv) * 16;
+  const int f0 = ch * fchunk, f1 = min(F, f0 + fchunk);
+  const int cols = K * PH + PH;
+  const int kr = k0 + (lane & 15), fq = lane >> 4, pc = lane & 15;
+  const bool kok = kr < K, pok = pc < PH;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (k0 < K) {
+    constexpr int U = 8;   // K steps per batch
+    for (int fb = f0; fb < f1; fb += 4 * U) {
+      float a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int f = fb + 4 * u + fq;
+        const bool ok = f < f1;
+        const int fc = ok ? f : f0;
+        const float av = X[(size_t)fc * K + (kok ? kr : 0)];
+        const float bv = g_e[(size_t)fc * PH + (pok ? pc : 0)];
+        a[u] = ok && kok ? av : 0.f;
+        b[u] = ok && pok ? bv : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc = mfma16x16x4(a[u], b[u], acc);
+    }
+    // C: lane l holds column p = l & 15 of rows k0 + 4 (l >> 4) + 0..3
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 4 * fq + r;
+      if (k < K && pok) part[(size_t)ch * cols + (size_t)k * PH + pc] = acc[r];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < PH) {
+    float s = 0.f;
+    for (int f = f0; f < f1; ++f) s += g_e[(size_t)f * PH + threadIdx.x];
+    part[(size_t)ch * cols + (size_t)K * PH + threadIdx.x] = s;
+  }
+}
+
 // ---------------------------------------------------------------- encaps
 struct CapsDims {
   int B, T, PH, PD;   // T = T' frames per utterance
@@ -1030,8 +1077,12 @@ int srf_primary_caps_bwd_ex(const float* X, const int* inp_len, int B, int T, in
                        g_X);
   SRF_LAUNCH_CHECK("proj_bwd_x");
   const int fchunk = (F + kProjChunks - 1) / kProjChunks;
-  hipLaunchKernelGGL(proj_bwd_w_kernel, dim3((K + 255) / 256, kProjChunks), dim3(256), 0, st, X, w.g_e, F, K, PH,
-                     fchunk, w.ppart);
+  if (PH <= 16)
+    hipLaunchKernelGGL(proj_bwd_w_mfma_kernel, dim3((K + 63) / 64, kProjChunks), dim3(256), 0, st, X, w.g_e, F, K, PH,
+                       fchunk, w.ppart);
+  else
+    hipLaunchKernelGGL(proj_bwd_w_kernel, dim3((K + 255) / 256, kProjChunks), dim3(256), 0, st, X, w.g_e, F, K, PH,
+                       fchunk, w.ppart);
   SRF_LAUNCH_CHECK("proj_bwd_w");
   const int pcols = K * PH + PH;
   if ((rc = srf::colsum(w.ppart, kProjChunks, pcols, nullptr, w.scratch, st,
