@@ -192,7 +192,7 @@ __global__ __launch_bounds__(64 * kProjWaves) void proj_fwd_mfma_kernel(const fl
 
 // g_X[f][k..k+3] = sum_p g_e[f][p] Wp[k..k+3][p]: a thread writes one float4 of g_X for
 // kProjXF consecutive frames, so the Wp rows it loads serve them all.
-constexpr int kProjXF = 4;
+constexpr int kProjXF = 16;
 template <int PH>
 __global__ __launch_bounds__(256) void proj_bwd_x_vec_kernel(const float* __restrict__ g_e,
                                                              const float* __restrict__ Wp, int F, int K,
