@@ -747,6 +747,90 @@ __device__ __forceinline__ void capsnorm_fwd_wave(const float* __restrict__ x, c
   }
 }
 
+// The output head on one wave per row: LN_mid + dropout as capsnorm_fwd_wave, the
+// capsule lengths over groups of D / 4 lanes (capsule j = element / D; each lane's float4
+// lies in one capsule), LN_out over the J lengths by wave sums (each length is held by
+// its D / 4 lanes).
+template <int NPL>
+__device__ __forceinline__ void caps_head_fwd_wave(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, bool drop, float p,
+                                                   unsigned long long seed, unsigned stream,
+                                                   float* __restrict__ stat, int D, const float* __restrict__ gamma_o,
+                                                   const float* __restrict__ beta_o, float* __restrict__ logits,
+                                                   float* __restrict__ lens, float len_eps, int f, int lane) {
+  constexpr int n = 64 * NPL, NV = NPL / 4;
+  const int LPC = D / 4, J = n / D;
+  const f4* xr = reinterpret_cast<const f4*>(x + (size_t)f * n);
+  f4 v[NV];
+  float s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    v[k] = xr[k * 64 + lane];
+    s1 += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+  }
+  const float mean = wave_sum(s1) / n;
+  float s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const f4 d = v[k] - mean;
+    s2 += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+  }
+  const float rstd = 1.f / sqrtf(wave_sum(s2) / n + kLnEps);
+  float L[NV];
+  float t1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int q = k * 64 + lane;
+    const f4 g = reinterpret_cast<const f4*>(gamma)[q], b = reinterpret_cast<const f4*>(beta)[q];
+    const size_t gi = (size_t)f * n + 4 * q;
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float o = ((v[k][c] - mean) * rstd * g[c] + b[c]) * drop_mult(drop, seed, stream, gi + c, p);
+      ss += o * o;
+    }
+    for (int m = 1; m < LPC; m <<= 1) ss += __shfl_xor(ss, m, 64);
+    L[k] = sqrtf(ss + len_eps);
+    t1 += L[k];
+  }
+  const float mo = wave_sum(t1) / (float)LPC / J;
+  float t2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) t2 += (L[k] - mo) * (L[k] - mo);
+  const float ro = 1.f / sqrtf(wave_sum(t2) / (float)LPC / J + kLnEps);
+  if (lane % LPC == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int j = (k * 64 + lane) / LPC;
+      lens[(size_t)f * J + j] = L[k];
+      logits[(size_t)f * J + j] = (L[k] - mo) * ro * gamma_o[j] + beta_o[j];
+    }
+  }
+  if (lane == 0) {
+    stat[4 * f] = mean;
+    stat[4 * f + 1] = rstd;
+    stat[4 * f + 2] = mo;
+    stat[4 * f + 3] = ro;
+  }
+}
+
+template <int NPL>
+__global__ __launch_bounds__(256) void caps_head_fwd_wave_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, int training, float p,
+                                                                 unsigned long long seed,
+                                                                 const unsigned long long* __restrict__ seed_src,
+                                                                 unsigned stream, float* __restrict__ stat, int D,
+                                                                 const float* __restrict__ gamma_o,
+                                                                 const float* __restrict__ beta_o,
+                                                                 float* __restrict__ logits, float* __restrict__ lens,
+                                                                 float len_eps, int rows) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= rows) return;   // whole waves: nothing below synchronises
+  caps_head_fwd_wave<NPL>(x, gamma, beta, training && p > 0.f, p, srf_step_seed(seed, seed_src), stream, stat, D,
+                          gamma_o, beta_o, logits, lens, len_eps, w, threadIdx.x & 63);
+}
+
 template <int NPL>
 __device__ __forceinline__ void capsnorm_bwd_wave(const float* __restrict__ x, const float* __restrict__ gamma,
                                                   bool drop, float p, unsigned long long seed, unsigned stream,
@@ -1264,6 +1348,24 @@ int srf_caps_head_fwd_ex(const float* v, int F, int J, int D, const float* gamma
   SRF_REQUIRE(v && gamma_mid && beta_mid && gamma_out && beta_out && logits && stat && lens && F > 0 && n > 0 &&
                   n <= kMaxVec,
               "bad head arguments");
+  if ((n == 256 || n == 512 || n == 1024) && D % 4 == 0 && 64 % (D / 4) == 0) {   // one wave per row
+    const dim3 grid((F + 3) / 4);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const unsigned sm = (unsigned)(kStreamMid0 + layer);
+#define SRF_HEAD_WAVE(NPL)                                                                                          \
+  hipLaunchKernelGGL((caps_head_fwd_wave_kernel<NPL>), grid, dim3(256), 0, st, v, gamma_mid, beta_mid, training, p, \
+                     seed, srf::seed_source(), sm, stat, D, gamma_out, beta_out, logits, lens, length_eps, F)
+    if (n == 256) {
+      SRF_HEAD_WAVE(4);
+    } else if (n == 512) {
+      SRF_HEAD_WAVE(8);
+    } else {
+      SRF_HEAD_WAVE(16);
+    }
+#undef SRF_HEAD_WAVE
+    SRF_LAUNCH_CHECK("caps_head_fwd");
+    return SRF_OK;
+  }
   hipLaunchKernelGGL(capsnorm_fwd_kernel, dim3(F), dim3(256), (size_t)(n + 8 + J) * 4,
                      static_cast<hipStream_t>(stream), v, n, gamma_mid, beta_mid, training, p, seed, srf::seed_source(),
                      (unsigned)(kStreamMid0 + layer), (float*)nullptr, stat, 1, J, D, gamma_out, beta_out, logits,

@@ -59,7 +59,8 @@ def test_primary_caps(cuda, PH, PD, p):
 
 @pytest.mark.parametrize('head,J,D', [(False, 8, 16), (True, 63, 16),
                                       # the wave-per-row kernels: rows of 256, 512, 1024 values
-                                      (False, 16, 16), (False, 16, 32), (False, 32, 32)])
+                                      (False, 16, 16), (False, 16, 32), (False, 32, 32),
+                                      (True, 16, 16), (True, 32, 32)])
 @pytest.mark.parametrize('p', [0.0, 0.1])
 def test_capsnorm_and_head(cuda, head, J, D, p):
     from srf_amd import ops
