@@ -244,6 +244,9 @@ def measure(workload, args, world, rank, dev):
     if args.sdr_last_gxw_inline:
         from srf_amd import ops
         ops.SDR_LAST_GXW_SIDE = False
+    if args.dr_gw_inline:
+        from srf_amd import ops
+        ops.DR_GW_SIDE = False
     if args.dr_chunks:
         # "l:c,l:c" input-capsule chunks of DR layer l's routing passes (A/B of the plan's choice)
         for item in args.dr_chunks.split(','):
@@ -420,6 +423,8 @@ def main():
                     help='SDR stack: the gx and gW launches of din-32 layers separately (default: fused)')
     ap.add_argument('--sdr-capsnorm-per-layer', action='store_true',
                     help='SDR stack: one LN/dropout launch per inner layer and range (default: one per diagonal)')
+    ap.add_argument('--dr-gw-inline', action='store_true',
+                    help='DR: each layer\'s gW / gbias on the backward\'s stream (default: a side stream; A/B)')
     ap.add_argument('--dr-chunks', default='',
                     help='DR: input-capsule chunks per layer, "l:c,..." (default: the plan\'s choice; A/B)')
     ap.add_argument('--sdr-last-gxw-inline', action='store_true',

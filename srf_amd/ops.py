@@ -69,6 +69,59 @@ class RouteGeom:
                 self.n_chunks)
 
 
+# DR gW / gbias (srf_route_dr_bwd_weights_ex) on a side stream beside the layers below.
+# Each layer's launch is deferred to the next DR backward (or the gradient buckets' next
+# collective, or dr_side_join), so the backward's next kernel is captured first
+# (STACK_CAPTURE_ORDER).  C4 8.31 -> 8.22 ms (r05ci); False: one stream (bench
+# --dr-gw-inline, for A/B).
+DR_GW_SIDE = True
+_dr_side = {}        # device index -> side stream
+_dr_pending = []     # (device, event, launch(stream_ptr), tensors the launch reads)
+
+
+def _dr_side_stream(dev):
+    s = _dr_side.get(dev.index)
+    if s is None:
+        s = _dr_side[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _dr_issue_pending():
+    while _dr_pending:
+        dev, ev, launch, keep = _dr_pending.pop(0)
+        side = _dr_side_stream(dev)
+        side.wait_event(ev)
+        launch(ctypes_void(side.cuda_stream))
+        for t in keep:
+            if t is not None:
+                t.record_stream(side)   # the allocator must not hand these out before the launch ran
+
+
+def dr_side_join():
+    """Issue the deferred DR gW launches and make the current stream wait for them
+    (the caller's backward is complete; gradients are read next).  The backward does
+    this itself at its end (_dr_backward_done); calling it again is harmless."""
+    _dr_issue_pending()
+    for s in _dr_side.values():
+        torch.cuda.current_stream(s.device).wait_stream(s)
+
+
+_dr_state = {'queued': False, 'main': None}
+
+
+def _dr_backward_done():
+    """End-of-backward callback (queued by the first deferring DR backward): issue what
+    is still deferred and make the backward's stream wait for the side stream, so every
+    gradient is complete when backward() returns, whoever called it."""
+    _dr_state['queued'] = False
+    main, _dr_state['main'] = _dr_state['main'], None
+    _dr_issue_pending()
+    if main is not None:
+        s = _dr_side.get(main.device.index)
+        if s is not None:
+            main.wait_stream(s)
+
+
 class DynamicRouting(torch.autograd.Function):
     """window -> pose (u = W x + b) -> ``iters`` DR iterations, one layer.
 
@@ -121,9 +174,31 @@ class DynamicRouting(torch.autograd.Function):
         cpl = ctx.couplings
         ctx.couplings = None
         cp = _ptr(cpl) if cpl is not None else None
-        rc = L.srf_route_dr_bwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
-                                   _ptr(g_emb), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
-        _lib.check(rc, 'srf_route_dr_bwd_ex')
+        _dr_issue_pending()   # the layer above's gW, behind the kernels enqueued since its gu pass
+        # only where gW / gbias land in the model's flat gradient buffer (written in place,
+        # autograd handed None): a returned gradient is consumed at once on this stream
+        if DR_GW_SIDE and cpl is not None and tW[1] and tb[1]:
+            rc = L.srf_route_dr_bwd_data_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
+                                            _ptr(g_emb), _ptr(ws), ws_bytes, _stream())
+            _lib.check(rc, 'srf_route_dr_bwd_data_ex')
+            ev = getattr(g, '_gw_event', None)   # kept with the geometry: a captured step's events outlive it
+            if ev is None:
+                ev = g._gw_event = torch.cuda.Event()
+            ev.record()
+
+            def launch(st, emb=emb, saved=saved, cpl=cpl, g_W=g_W, g_b=g_b, ws=ws):
+                _lib.check(L.srf_route_dr_bwd_weights_ex(_ptr(emb), *g.args(), _ptr(saved), _ptr(cpl), _ptr(g_W),
+                                                         _ptr(g_b), _ptr(ws), ws_bytes, st),
+                           'srf_route_dr_bwd_weights_ex')
+            _dr_pending.append((emb.device, ev, launch, (emb, saved, cpl, ws)))
+            _dr_state['main'] = torch.cuda.current_stream(emb.device)
+            if not _dr_state['queued']:
+                torch.autograd.Variable._execution_engine.queue_callback(_dr_backward_done)
+                _dr_state['queued'] = True
+        else:
+            rc = L.srf_route_dr_bwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
+                                       _ptr(g_emb), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
+            _lib.check(rc, 'srf_route_dr_bwd_ex')
         return (g_emb, *_returned([tW, tb]), None, None)
 
 

@@ -13,7 +13,7 @@ from collections import OrderedDict
 import torch
 import torch.distributed as dist
 
-from . import ctc
+from . import ctc, ops
 
 
 class Mean:
@@ -167,6 +167,13 @@ class GradBuckets:
             self._issue()
 
     def _issue(self):
+        if self.gpu and self.deferred:
+            # DR gW / gbias deferred onto their side stream (ops.DR_GW_SIDE) write gradients
+            # of these buckets: issue them, and order the collectives after them
+            ops._dr_issue_pending()
+            dr = ops._dr_side.get(self.model.flat_grad.device.index)
+            if dr is not None:
+                self.side.wait_stream(dr)
         for k in self.deferred:
             lo, hi, _ = self.buckets[k]
             if self.gpu:
@@ -249,6 +256,7 @@ def process_train_step(in_len_div, inputs, model, optimizer, loss_state, frame_s
     pe_loss, g_logits = ctc.ctc_loss_and_grad(labels, y_pred, tar_len, ceil_div(inp_len, in_len_div), blank_idx,
                                               1.0 / float(batch * n_gpus))
     y_pred.backward(g_logits)
+    ops.dr_side_join()   # DR gW launches deferred onto a side stream (ops.DR_GW_SIDE)
     _reduce(model)
     optimizer.apply_gradients(model)
     if loss_state is not None:
@@ -385,6 +393,7 @@ class GraphedTrainStep:
         pe_loss, g_logits = ctc.ctc_loss_and_grad(self.labels, y_pred, self.tar_len, logit_len, self.blank_idx,
                                                   1.0 / float(self.batch * self.n_gpus))
         y_pred.backward(g_logits)
+        ops.dr_side_join()
         if buckets is not None:
             buckets.finish()
         return pe_loss

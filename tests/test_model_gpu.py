@@ -69,6 +69,34 @@ def test_gradients(cuda, name):
     assert not bad, bad
 
 
+@pytest.mark.parametrize('name', ['c4_mini', 'c4_real'])
+def test_dr_gw_side_stream_matches(cuda, name):
+    """ops.DR_GW_SIDE (each DR layer's gW / gbias deferred onto a side stream, joined by
+    ops.dr_side_join) computes the gradients of the one-stream backward: the same kernels
+    on the same inputs, only on another stream (up to the order of the gx pass's float
+    atomics into g_emb, which differs run to run either way)."""
+    from srf_amd import ctc, ops
+    model, sh, z = _build(name, cuda)
+    feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
+    inp_len = torch.tensor(z['inp_len'], device=cuda)
+    grads = []
+    for side in (False, True):
+        ops.DR_GW_SIDE = side
+        try:
+            model.zero_grad()
+            logits = model(feats, input_lengths=inp_len, training=True)
+            nll = ctc.ctc_loss(torch.tensor(z['labels'], device=cuda), logits, torch.tensor(z['tar_len'], device=cuda),
+                               (inp_len + 3) // 4, blank_index=sh.class_n - 1)
+            (nll.sum() / feats.shape[0]).backward()
+            ops.dr_side_join()
+            torch.cuda.synchronize()
+            grads.append(model.flat_grad.detach().clone())
+        finally:
+            ops.DR_GW_SIDE = True
+    err, mag = (grads[0] - grads[1]).abs().max().item(), grads[0].abs().max().item()
+    assert err <= 1e-5 * mag, (err, mag)
+
+
 def test_train_step_runs_and_updates(cuda):
     """process_train_step: loss finite, params move after step 2 (lr(0) == 0)."""
     from srf_amd import train_helper, trainer_sr
