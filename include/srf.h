@@ -261,6 +261,23 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
                   float* g_gamma0, float* g_beta0, float* g_k1a, float* g_b1a, float* g_k1b, float* g_b1b,
                   float* g_gamma1, float* g_beta1, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The same backward in parts (bit mask), for a caller that runs the stage-2 weight
+ * gradient on a second stream: PREP (BN2 sums, the stage-2 output gradient g_ab and
+ * the bias gradients) first; then DATA (stage-2 data gradient, BN1, stage 1) and WGRAD
+ * (stage-2 kernel gradients) both read what PREP wrote and nothing of each other, so
+ * they may run concurrently after it.  One workspace for all parts.  ALL = the
+ * sequential srf_cnnfe_bwd. */
+#define SRF_CNNFE_BWD_PREP 1
+#define SRF_CNNFE_BWD_DATA 2
+#define SRF_CNNFE_BWD_WGRAD 4
+#define SRF_CNNFE_BWD_ALL 7
+int srf_cnnfe_bwd_parts(int parts, const float* feats, const int* inp_len, int B, int T, int feat_dim, int nfilt,
+                        const float* gamma0, const float* k1a, const float* k1b, const float* gamma1, float drop_p,
+                        unsigned long long seed, const void* saved, const float* g_out, float* g_k0a, float* g_b0a,
+                        float* g_k0b, float* g_b0b, float* g_gamma0, float* g_beta0, float* g_k1a, float* g_b1a,
+                        float* g_k1b, float* g_b1b, float* g_gamma1, float* g_beta1, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
 /* ---- Primary capsules (sequence_router_naive.py:129-142) -------------------
  * X = CNN-FE output viewed as [B*T][K] (K = F2*64, index f*64 + c as the
  * reference's reshape, :131); Wp [K][PH], bp [PH]; encaps kernels [3][3][1][PD],

@@ -86,6 +86,8 @@ _SIGNATURES = {
                                                                        _vp, _vp, _c_size, _vp, _c_size, _vp]),
     'srf_cnnfe_bwd': (_c_int, [_vp, _vp] + [_c_int] * 4 + [_vp] * 4 + [ctypes.c_float, ctypes.c_ulonglong]
                       + [_vp] * 15 + [_c_size, _vp]),
+    'srf_cnnfe_bwd_parts': (_c_int, [_c_int, _vp, _vp] + [_c_int] * 4 + [_vp] * 4 + [ctypes.c_float, ctypes.c_ulonglong]
+                            + [_vp] * 15 + [_c_size, _vp]),
     'srf_primary_caps_saved_bytes': (_c_size, [_c_int] * 4),
     'srf_primary_caps_bwd_workspace': (_c_size, [_c_int] * 5),
     'srf_primary_caps_fwd': (_c_int, [_vp, _vp] + [_c_int] * 5 + [_vp] * 8 + [_c_int, ctypes.c_float, ctypes.c_float,

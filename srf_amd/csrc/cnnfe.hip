@@ -1503,6 +1503,18 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
                   const void* saved, const float* g_out, float* g_k0a, float* g_b0a, float* g_k0b, float* g_b0b,
                   float* g_gamma0, float* g_beta0, float* g_k1a, float* g_b1a, float* g_k1b, float* g_b1b,
                   float* g_gamma1, float* g_beta1, void* workspace, size_t workspace_bytes, void* stream) {
+  return srf_cnnfe_bwd_parts(SRF_CNNFE_BWD_ALL, feats, inp_len, B, T, feat_dim, nfilt, gamma0, k1a, k1b, gamma1, drop_p,
+                             seed, saved, g_out, g_k0a, g_b0a, g_k0b, g_b0b, g_gamma0, g_beta0, g_k1a, g_b1a, g_k1b,
+                             g_b1b, g_gamma1, g_beta1, workspace, workspace_bytes, stream);
+}
+
+int srf_cnnfe_bwd_parts(int parts, const float* feats, const int* inp_len, int B, int T, int feat_dim, int nfilt,
+                        const float* gamma0, const float* k1a, const float* k1b, const float* gamma1, float drop_p,
+                        unsigned long long seed, const void* saved, const float* g_out, float* g_k0a, float* g_b0a,
+                        float* g_k0b, float* g_b0b, float* g_gamma0, float* g_beta0, float* g_k1a, float* g_b1a,
+                        float* g_k1b, float* g_b1b, float* g_gamma1, float* g_beta1, void* workspace,
+                        size_t workspace_bytes, void* stream) {
+  SRF_REQUIRE(parts > 0 && (parts & ~SRF_CNNFE_BWD_ALL) == 0, "CNN-FE backward: bad parts mask %d", parts);
   int rc = check_dims(B, T, feat_dim, nfilt);
   if (rc) return rc;
   SRF_REQUIRE(feats && inp_len && gamma0 && k1a && k1b && gamma1 && saved && g_out && g_k0a && g_b0a && g_k0b &&
@@ -1518,14 +1530,15 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int P2 = d.B * d.T2 * d.F2;
+  __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);
+  _Float16* wq2h = reinterpret_cast<_Float16*>(w.wq);
+  if (parts & SRF_CNNFE_BWD_PREP) {
   // BN2: sums -> d(beta2) = sum dy, d(gamma2) = sum dy*xh
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, g_out, sv.y2, sv.stats2, inp_len, d.B,
                      d.T2, d.F2, 4, w.bnpart);
   SRF_LAUNCH_CHECK("bn_bwd_reduce(2)");
   if ((rc = srf::colsum(w.bnpart, kBnBlocks, 2 * C, w.bnsum2, w.scratch, st, srf::ColSplit{{g_beta1, g_gamma1, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
-  __bf16* wq3 = reinterpret_cast<__bf16*>(w.wq);
-  _Float16* wq2h = reinterpret_cast<_Float16*>(w.wq);
   const int npack = (kPackW2tF16Threads + 255) / 256;
   hipLaunchKernelGGL(conv2_bwd_prep_kernel, dim3(kBnBlocks + npack), dim3(256), 0, st, g_out, sv.y2, sv.sel2,
                      sv.stats2, gamma1, w.bnsum2, inp_len, d, drop_p, seed, srf::seed_source(), w.g_ab, w.biaspart,
@@ -1533,9 +1546,10 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   SRF_LAUNCH_CHECK("conv2_bwd_prep");
   if ((rc = srf::colsum(w.biaspart, kBnBlocks, 2 * C, nullptr, w.scratch, st, srf::ColSplit{{g_b1a, g_b1b, nullptr, nullptr}, {C, C, 0, 0}})))
     return rc;
+  }
   // stage-2 data gradient (4 stride-parity classes, split transposed weights packed by
   // the bwd_prep launch) and weight gradient, both on split-fp16 operands
-  {
+  if (parts & SRF_CNNFE_BWD_DATA) {
     DgCls cls{};
     for (int c = 0; c < 4; ++c) {
       const int qt = c >> 1, qf = c & 1;
@@ -1548,7 +1562,7 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
   }
   const WgDiv dv{make_fastdiv(d.F2), make_fastdiv(d.T2)};
   const int nsplit = kWgrad32Splits;
-  {
+  if (parts & SRF_CNNFE_BWD_WGRAD) {
     static_assert(kW2Chunk == kWgChunk, "wgrad splits are whole chunks");
     const int split_len = ((P2 + nsplit - 1) / nsplit + kWgChunk - 1) / kWgChunk * kWgChunk;
     hipLaunchKernelGGL(gab_split_t_kernel<true>, dim3(w.P2p / kTpPx), dim3(256), 0, st, w.g_ab, P2, w.P2p,
@@ -1558,10 +1572,11 @@ int srf_cnnfe_bwd(const float* feats, const int* inp_len, int B, int T, int feat
                        (const void*)w.gsT3, w.P2p, d, dv, nsplit, split_len, w.wpart, (const float*)w.gmax,
                        kBnBlocks);
     SRF_LAUNCH_CHECK("conv2_wgrad32");
+    hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((9 * C * 2 * C + 255) / 256), dim3(256), 0, st, w.wpart,
+                       nsplit, g_k1a, g_k1b);
+    SRF_LAUNCH_CHECK("conv2_wgrad_reduce");
   }
-  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((9 * C * 2 * C + 255) / 256), dim3(256), 0, st, w.wpart,
-                     nsplit, g_k1a, g_k1b);
-  SRF_LAUNCH_CHECK("conv2_wgrad_reduce");
+  if (!(parts & SRF_CNNFE_BWD_DATA)) return SRF_OK;
   // BN1 backward sums, then stage-1 gradients
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(kBnBlocks), dim3(256), 0, st, w.g_x1, sv.y1, sv.stats1, inp_len, d.B,
                      d.T1, d.F1, 2, w.bnpart);

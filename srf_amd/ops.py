@@ -122,6 +122,16 @@ def _dr_backward_done():
             main.wait_stream(s)
 
 
+def _defer_side(dev, ev, launch, keep):
+    """Queue ``launch(side stream)`` behind ``ev``; issued by the next deferring op, the
+    gradient buckets' next collective, or the end-of-backward callback queued here."""
+    _dr_pending.append((dev, ev, launch, keep))
+    _dr_state['main'] = torch.cuda.current_stream(dev)
+    if not _dr_state['queued']:
+        torch.autograd.Variable._execution_engine.queue_callback(_dr_backward_done)
+        _dr_state['queued'] = True
+
+
 class DynamicRouting(torch.autograd.Function):
     """window -> pose (u = W x + b) -> ``iters`` DR iterations, one layer.
 
@@ -190,11 +200,7 @@ class DynamicRouting(torch.autograd.Function):
                 _lib.check(L.srf_route_dr_bwd_weights_ex(_ptr(emb), *g.args(), _ptr(saved), _ptr(cpl), _ptr(g_W),
                                                          _ptr(g_b), _ptr(ws), ws_bytes, st),
                            'srf_route_dr_bwd_weights_ex')
-            _dr_pending.append((emb.device, ev, launch, (emb, saved, cpl, ws)))
-            _dr_state['main'] = torch.cuda.current_stream(emb.device)
-            if not _dr_state['queued']:
-                torch.autograd.Variable._execution_engine.queue_callback(_dr_backward_done)
-                _dr_state['queued'] = True
+            _defer_side(emb.device, ev, launch, (emb, saved, cpl, ws))
         else:
             rc = L.srf_route_dr_bwd_ex(_ptr(emb), _ptr(W), _ptr(bias), *g.args(), _ptr(saved), cp, _ptr(g_v),
                                        _ptr(g_emb), _ptr(g_W), _ptr(g_b), _ptr(ws), ws_bytes, _stream())
@@ -259,6 +265,13 @@ CNNFE_PARAMS = ('conv0a_kernel', 'conv0a_bias', 'conv0b_kernel', 'conv0b_bias', 
                 'conv1a_kernel', 'conv1a_bias', 'conv1b_kernel', 'conv1b_bias', 'bn1_gamma', 'bn1_beta')
 
 
+# Stage-2 weight gradient (split-transpose, wgrad, reduce: ~240 us at C4) on the side
+# stream beside the stage-2 data gradient and stage 1 (srf_cnnfe_bwd_parts; the parts share
+# no workspace).  False: one srf_cnnfe_bwd call (bench --cnnfe-wgrad-inline, for A/B).
+CNNFE_WGRAD_SIDE = True
+_cnnfe_events = {}   # device index -> the event after the prep part (one CNN-FE per step)
+
+
 def cnnfe_out_dims(T, feat_dim):
     import ctypes
     t2, f2 = ctypes.c_int(), ctypes.c_int()
@@ -301,10 +314,25 @@ class CnnFe(torch.autograd.Function):
         wb = L.srf_cnnfe_bwd_workspace(B, T, Fd, 64)
         ws = torch.empty(wb, device=feats.device, dtype=torch.uint8)
         g_out = g_out.contiguous()
-        rc = L.srf_cnnfe_bwd(_ptr(feats), _ptr(inp_len), B, T, Fd, 64, _ptr(P['bn0_gamma']), _ptr(P['conv1a_kernel']),
-                             _ptr(P['conv1b_kernel']), _ptr(P['bn1_gamma']), drop_p, seed, _ptr(saved), _ptr(g_out),
-                             *[_ptr(G[k]) for k in CNNFE_PARAMS], _ptr(ws), wb, _stream())
-        _lib.check(rc, 'srf_cnnfe_bwd')
+        args = (_ptr(feats), _ptr(inp_len), B, T, Fd, 64, _ptr(P['bn0_gamma']), _ptr(P['conv1a_kernel']),
+                _ptr(P['conv1b_kernel']), _ptr(P['bn1_gamma']), drop_p, seed, _ptr(saved), _ptr(g_out),
+                *[_ptr(G[k]) for k in CNNFE_PARAMS], _ptr(ws), wb)
+        inplace = dict(zip(CNNFE_PARAMS, [t[1] for t in targets]))
+        if CNNFE_WGRAD_SIDE and inplace['conv1a_kernel'] and inplace['conv1b_kernel']:
+            _dr_issue_pending()
+            _lib.check(L.srf_cnnfe_bwd_parts(1, *args, _stream()), 'srf_cnnfe_bwd_parts(prep)')
+            dev = feats.device
+            ev = _cnnfe_events.get(dev.index)
+            if ev is None:
+                ev = _cnnfe_events[dev.index] = torch.cuda.Event()
+            ev.record()
+            _lib.check(L.srf_cnnfe_bwd_parts(2, *args, _stream()), 'srf_cnnfe_bwd_parts(data)')
+
+            def launch(st):
+                _lib.check(L.srf_cnnfe_bwd_parts(4, *args, st), 'srf_cnnfe_bwd_parts(wgrad)')
+            _defer_side(dev, ev, launch, (feats, inp_len, saved, g_out, ws))
+        else:
+            _lib.check(L.srf_cnnfe_bwd(*args, _stream()), 'srf_cnnfe_bwd')
         return (None, None, None, None, None, None, *_returned(targets))
 
 

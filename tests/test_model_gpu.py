@@ -72,7 +72,8 @@ def test_gradients(cuda, name):
 @pytest.mark.parametrize('name', ['c4_mini', 'c4_real'])
 def test_dr_gw_side_stream_matches(cuda, name):
     """ops.DR_GW_SIDE (each DR layer's gW / gbias deferred onto a side stream, joined by
-    ops.dr_side_join) computes the gradients of the one-stream backward: the same kernels
+    ops.dr_side_join) and ops.CNNFE_WGRAD_SIDE (the CNN front end's stage-2 weight gradient
+    there too) compute the gradients of the one-stream backward: the same kernels
     on the same inputs, only on another stream (up to the order of the gx pass's float
     atomics into g_emb, which differs run to run either way)."""
     from srf_amd import ctc, ops
@@ -81,7 +82,7 @@ def test_dr_gw_side_stream_matches(cuda, name):
     inp_len = torch.tensor(z['inp_len'], device=cuda)
     grads = []
     for side in (False, True):
-        ops.DR_GW_SIDE = side
+        ops.DR_GW_SIDE = ops.CNNFE_WGRAD_SIDE = side
         try:
             model.zero_grad()
             logits = model(feats, input_lengths=inp_len, training=True)
@@ -92,7 +93,7 @@ def test_dr_gw_side_stream_matches(cuda, name):
             torch.cuda.synchronize()
             grads.append(model.flat_grad.detach().clone())
         finally:
-            ops.DR_GW_SIDE = True
+            ops.DR_GW_SIDE = ops.CNNFE_WGRAD_SIDE = True
     err, mag = (grads[0] - grads[1]).abs().max().item(), grads[0].abs().max().item()
     assert err <= 1e-5 * mag, (err, mag)
 
