@@ -577,43 +577,58 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, const float* __rest
 //   g_y = mask_pre * gamma * rstd * (dy - sum(dy)/N - xh * sum(dy*xh)/N)
 // (mask_pre = the mask applied before BN; it equals the post-BN mask here).
 
-// Per-channel partial sums (sum dy, sum dy*xh) over a stream of positions.
+// Per-channel partial sums (sum dy, sum dy*xh) over a stream of positions.  A lane
+// owns 4 channels of one pixel (16 lanes per pixel, 16-byte loads, 4 pixels per wave
+// per load); a wave takes kBnPx consecutive pixels per sweep, all loads issued first.
+constexpr int kBnPx = 16;
+__device__ __forceinline__ f4 wave_sum_px(f4 v) {   // sum over the 4 pixel groups of a wave
+#pragma unroll
+  for (int o = 16; o <= 32; o <<= 1) {
+    v.x += __shfl_xor(v.x, o, 64); v.y += __shfl_xor(v.y, o, 64);
+    v.z += __shfl_xor(v.z, o, 64); v.w += __shfl_xor(v.w, o, 64);
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ y,
                                                             const float* __restrict__ stats,
                                                             const int* __restrict__ inp_len, int B, int Tk, int Fk,
                                                             int div, float* __restrict__ part) {
-  __shared__ float sh[2][4][C];
-  const int c = threadIdx.x & (C - 1);
-  const int row = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // pixels are wave-uniform
-  const float mean = stats[c], rstd = stats[C + c];
+  __shared__ f4 sh[2][4][C / 4];
+  const int lane = threadIdx.x & 63, q = lane & 15, pg = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const f4 mean = reinterpret_cast<const f4*>(stats)[q], rstd = reinterpret_cast<const f4*>(stats + C)[q];
   const int P = B * Tk * Fk;
-  constexpr int PX = 4;
-  float s0 = 0.f, s1 = 0.f;
-  for (int p0 = (blockIdx.x * 4 + row) * PX; p0 < P; p0 += gridDim.x * 4 * PX) {
-    float dy[PX], yv[PX], m[PX];
+  f4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  for (int p0 = (blockIdx.x * 4 + wave) * kBnPx; p0 < P; p0 += gridDim.x * 4 * kBnPx) {
+    constexpr int U = kBnPx / 4;
+    f4 dy[U], yv[U];
+    float m[U];
 #pragma unroll
-    for (int u = 0; u < PX; ++u) {
-      const int p = min(p0 + u, P - 1);
+    for (int u = 0; u < U; ++u) {
+      const int pu = p0 + 4 * u + pg;
+      const int p = min(pu, P - 1);
       const int t = (p / Fk) % Tk;
       const int b = p / (Fk * Tk);
-      m[u] = (p0 + u < P && t < ceil_div_len(inp_len[b], div)) ? 1.f : 0.f;
-      const size_t o = (size_t)p * C + c;
-      dy[u] = g[o];
-      yv[u] = y[o];
+      m[u] = (pu < P && t < ceil_div_len(inp_len[b], div)) ? 1.f : 0.f;
+      dy[u] = reinterpret_cast<const f4*>(g)[(size_t)p * (C / 4) + q];
+      yv[u] = reinterpret_cast<const f4*>(y)[(size_t)p * (C / 4) + q];
     }
 #pragma unroll
-    for (int u = 0; u < PX; ++u) {
-      const float d = dy[u] * m[u];
+    for (int u = 0; u < U; ++u) {
+      const f4 d = dy[u] * m[u];
       s0 += d;
       s1 += d * (yv[u] - mean) * rstd;
     }
   }
-  sh[0][row][c] = s0; sh[1][row][c] = s1;
+  s0 = wave_sum_px(s0);
+  s1 = wave_sum_px(s1);
+  if (pg == 0) { sh[0][wave][q] = s0; sh[1][wave][q] = s1; }
   __syncthreads();
-  if (row == 0) {
-    for (int r = 1; r < 4; ++r) { s0 += sh[0][r][c]; s1 += sh[1][r][c]; }
-    part[((size_t)blockIdx.x * 2 + 0) * C + c] = s0;
-    part[((size_t)blockIdx.x * 2 + 1) * C + c] = s1;
+  if (threadIdx.x < 2 * (C / 4)) {
+    const int k = threadIdx.x / (C / 4), qq = threadIdx.x % (C / 4);
+    const f4 v = sh[k][0][qq] + sh[k][1][qq] + sh[k][2][qq] + sh[k][3][qq];
+    reinterpret_cast<f4*>(part + ((size_t)blockIdx.x * 2 + k) * C)[qq] = v;
   }
 }
 
@@ -644,49 +659,77 @@ __global__ __launch_bounds__(256) void conv2_bwd_prep_kernel(
     return;
   }
   seed = srf_step_seed(seed, seed_src);
-  __shared__ float sh[2][4][C];
-  const int c = threadIdx.x & (C - 1), row = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // as bn_bwd_reduce_kernel: 4 channels of one pixel per lane, kBnPx pixels per wave sweep
+  __shared__ f4 sh[2][4][C / 4];
+  __shared__ float smax[4];
+  const int lane = threadIdx.x & 63, q = lane & 15, pg = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int P = d.B * d.T2 * d.F2;
-  const float mean = stats2[c], rstd = stats2[C + c], gam = gamma2[c];
-  const float sdy_n = bnsum2[c] / (float)P, sdyxh_n = bnsum2[C + c] / (float)P;
+  const f4 mean = reinterpret_cast<const f4*>(stats2)[q], rstd = reinterpret_cast<const f4*>(stats2 + C)[q];
+  const f4 gam = {gamma2[4 * q], gamma2[4 * q + 1], gamma2[4 * q + 2], gamma2[4 * q + 3]};   // a parameter view
+  const f4 sdy_n = reinterpret_cast<const f4*>(bnsum2)[q] / (float)P;
+  const f4 sdyxh_n = reinterpret_cast<const f4*>(bnsum2 + C)[q] / (float)P;
   const float keep_scale = 1.f / (1.f - drop_p);
-  float ga_s = 0.f, gb_s = 0.f, gm = 0.f;
-#pragma unroll 4
-  for (int p = blockIdx.x * 4 + row; p < P; p += nprep * 4) {
-    const int t = (p / d.F2) % d.T2;
-    const int b = p / (d.F2 * d.T2);
-    const float mask = t < ceil_div_len(inp_len[b], 4) ? 1.f : 0.f;
-    const size_t o = (size_t)p * C + c;
-    const float gy = bn_bwd_elem(g_out[o], y2[o], mask, mean, rstd, gam, sdy_n, sdyxh_n);
-    const bool s = sel2[o] != 0;
-    float ga = s ? gy : 0.f, gb = s ? 0.f : gy;
-    if (drop_p > 0.f) {
-      bool ka, kb;
-      srf_keep2(seed, kStreamConv1a, o, drop_p, ka, kb);
-      ga *= ka ? keep_scale : 0.f;
-      gb *= kb ? keep_scale : 0.f;
+  f4 ga_s = {0.f, 0.f, 0.f, 0.f}, gb_s = ga_s;
+  float gm = 0.f;
+  for (int p0 = (blockIdx.x * 4 + wave) * kBnPx; p0 < P; p0 += nprep * 4 * kBnPx) {
+    constexpr int U = kBnPx / 4;
+    f4 gv[U], yv[U];
+    unsigned sv[U];
+    float m[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int pu = p0 + 4 * u + pg;
+      const int p = min(pu, P - 1);
+      const int t = (p / d.F2) % d.T2;
+      const int b = p / (d.F2 * d.T2);
+      m[u] = (pu < P && t < ceil_div_len(inp_len[b], 4)) ? 1.f : 0.f;
+      gv[u] = reinterpret_cast<const f4*>(g_out)[(size_t)p * (C / 4) + q];
+      yv[u] = reinterpret_cast<const f4*>(y2)[(size_t)p * (C / 4) + q];
+      sv[u] = reinterpret_cast<const unsigned*>(sel2)[(size_t)p * (C / 4) + q];
     }
-    g_ab[(size_t)p * 2 * C + c] = ga;
-    g_ab[(size_t)p * 2 * C + C + c] = gb;
-    ga_s += ga;
-    gb_s += gb;
-    gm = fmaxf(gm, fmaxf(fabsf(ga), fabsf(gb)));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int pu = p0 + 4 * u + pg;
+      if (pu >= P) continue;
+      const size_t o0 = (size_t)pu * C + 4 * q;
+      f4 ga, gb;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gy = bn_bwd_elem(gv[u][e], yv[u][e], m[u], mean[e], rstd[e], gam[e], sdy_n[e], sdyxh_n[e]);
+        const bool sel = ((sv[u] >> (8 * e)) & 0xffu) != 0;
+        float a = sel ? gy : 0.f, bb = sel ? 0.f : gy;
+        if (drop_p > 0.f) {
+          bool ka, kb;
+          srf_keep2(seed, kStreamConv1a, o0 + e, drop_p, ka, kb);
+          a *= ka ? keep_scale : 0.f;
+          bb *= kb ? keep_scale : 0.f;
+        }
+        ga[e] = a;
+        gb[e] = bb;
+        gm = fmaxf(gm, fmaxf(fabsf(a), fabsf(bb)));
+      }
+      reinterpret_cast<f4*>(g_ab + (size_t)pu * 2 * C)[q] = ga;
+      reinterpret_cast<f4*>(g_ab + (size_t)pu * 2 * C + C)[q] = gb;
+      ga_s += ga;
+      gb_s += gb;
+    }
   }
-  sh[0][row][c] = ga_s; sh[1][row][c] = gb_s;
+  ga_s = wave_sum_px(ga_s);
+  gb_s = wave_sum_px(gb_s);
+  if (pg == 0) { sh[0][wave][q] = ga_s; sh[1][wave][q] = gb_s; }
   // block max |g_ab| (the data gradient's split exponent, conv2_dgrad32_kernel)
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) gm = fmaxf(gm, __shfl_xor(gm, o, 64));
-  __shared__ float smax[4];
-  if (c == 0) smax[row] = gm;
+  if (lane == 0) smax[wave] = gm;
   __syncthreads();
-  if (row == 0) {
-    for (int r = 1; r < 4; ++r) { ga_s += sh[0][r][c]; gb_s += sh[1][r][c]; }
-    part[(size_t)blockIdx.x * 2 * C + c] = ga_s;
-    part[(size_t)blockIdx.x * 2 * C + C + c] = gb_s;
-    if (c == 0 && gmax != nullptr) gmax[blockIdx.x] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  if (threadIdx.x < 2 * (C / 4)) {
+    const int k = threadIdx.x / (C / 4), qq = threadIdx.x % (C / 4);
+    const f4 v = sh[k][0][qq] + sh[k][1][qq] + sh[k][2][qq] + sh[k][3][qq];
+    reinterpret_cast<f4*>(part + (size_t)blockIdx.x * 2 * C + k * C)[qq] = v;
   }
+  if (threadIdx.x == 0 && gmax != nullptr) gmax[blockIdx.x] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
 }
-
 
 // ---------------------------------------------------------------- dgrad (split-bf16 MFMA)
 // The data gradient on v_mfma_f32_32x32x16_bf16 with 3-term splits, structured as
@@ -1521,6 +1564,8 @@ int srf_cnnfe_bwd_parts(int parts, const float* feats, const int* inp_len, int B
                   g_b0b && g_gamma0 && g_beta0 && g_k1a && g_b1a && g_k1b && g_b1b && g_gamma1 && g_beta1 &&
                   workspace,
               "null pointer argument");
+  SRF_REQUIRE(((uintptr_t)g_out & 15) == 0 && ((uintptr_t)saved & 255) == 0 && ((uintptr_t)workspace & 255) == 0,
+              "CNN-FE backward: g_out must be 16-byte and saved / workspace 256-byte aligned");
   const Dims d = make_dims(B, T, feat_dim);
   FwdSaved sv = saved_layout(d, const_cast<void*>(saved));
   BwdWs2 w = bwd_ws_layout(d, workspace);

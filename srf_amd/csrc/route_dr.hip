@@ -1827,10 +1827,11 @@ template <int DOUT>
 __global__ void bwd_finish_kernel(const float* __restrict__ slab, int n_chunks, size_t FJD,
                                   const float* __restrict__ a_init, float* __restrict__ A,
                                   const float* __restrict__ s, float* __restrict__ gs, float* __restrict__ zero4,
-                                  size_t nz4) {
+                                  size_t nz4, float* __restrict__ zero1) {
   constexpr int Q = DOUT / 4;
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < nz4) st4(zero4 + idx * 4, f4{0.f, 0.f, 0.f, 0.f});
+  if (zero1 != nullptr && idx == 0) *zero1 = 0.f;
   const bool ok = idx < FJD / 4;
   const size_t off = (ok ? idx : 0) * 4;
   f4 a;
@@ -1933,12 +1934,13 @@ void launch_fwd_finish(const Geom& g, const float* slab, int n_chunks, const flo
 
 template <int D>
 void launch_bwd_finish(const Geom& g, const float* slab, int n_chunks, const float* a_init, float* A,
-                       const float* s, float* gs, hipStream_t st, float* zero = nullptr, size_t n_zero = 0) {
+                       const float* s, float* gs, hipStream_t st, float* zero = nullptr, size_t n_zero = 0,
+                       float* zero1 = nullptr) {
   const size_t FJD = (size_t)g.F() * g.JD();
   const size_t nz4 = zero ? n_zero / 4 : 0;
   const size_t n = std::max(FJD / 4, nz4);
   hipLaunchKernelGGL((bwd_finish_kernel<D>), dim3((n + 255) / 256), dim3(256), 0, st, slab, n_chunks, FJD, a_init,
-                     A, s, gs, zero, nz4);
+                     A, s, gs, zero, nz4, zero1);
 }
 
 // row tiles per wave in the gu pass (a wave must hold whole output capsules)
@@ -2380,7 +2382,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
   const size_t n_emb = (size_t)g.F() * g.N * g.din;
   // with stored couplings this launch also zeroes g_emb (the gu pass accumulates into it)
   launch_bwd_finish<D>(g, nullptr, n_chunks, g_v, w.A, saved + (size_t)(2 * (R - 1)) * FJD,
-                       w.gs + (size_t)(R - 1) * FJD, st, p32 ? g_emb : nullptr, n_emb);
+                       w.gs + (size_t)(R - 1) * FJD, st, p32 ? g_emb : nullptr, n_emb, p32 ? w.gumax : nullptr);
   SRF_LAUNCH_CHECK("bwd_finish");
   srf::Fwd32Plan plan{};
   srf::Fwd32Cpl cl{};
@@ -2419,7 +2421,7 @@ int bwd_impl(const Geom& g, int n_chunks, const float* emb, const float* W, cons
     SRF_LAUNCH_CHECK("transpose_w");
   }
   if (p32) {
-    SRF_HIP_TRY(hipMemsetAsync(w.gumax, 0, sizeof(float), st));
+    // w.gumax (the gu pass's atomic max) was zeroed by the first bwd_finish launch
     launch_gu_r<D>(g, emb, W, couplings + cl.WT, bias, saved, w.gs, w.stats, w.gu_t, g_emb, st, couplings + cl.c,
                    w.gl, plan.JDp / g.dout, srf::fwd32_hdr(plan, couplings + cl.planes), w.gumax);
   } else
