@@ -835,12 +835,12 @@ template <int NPL>
 __device__ __forceinline__ void capsnorm_bwd_wave(const float* __restrict__ x, const float* __restrict__ gamma,
                                                   bool drop, float p, unsigned long long seed, unsigned stream,
                                                   const float* __restrict__ stat, const float* __restrict__ g_in,
-                                                  float* __restrict__ g_x, float* __restrict__ gpart, int f, int lane) {
+                                                  float* __restrict__ g_x, f4 (&pgxh)[NPL / 4], f4 (&pgg)[NPL / 4],
+                                                  int f, int lane) {
   constexpr int n = 64 * NPL, NV = NPL / 4;
   const float mean = stat[4 * f], rstd = stat[4 * f + 1];
   const f4* xr = reinterpret_cast<const f4*>(x + (size_t)f * n);
   const f4* gr = reinterpret_cast<const f4*>(g_in + (size_t)f * n);
-  f4* pg = reinterpret_cast<f4*>(gpart + (size_t)f * 2 * n);
   f4 xh[NV], t[NV];
   float a1 = 0.f, a2 = 0.f;
 #pragma unroll
@@ -859,8 +859,8 @@ __device__ __forceinline__ void capsnorm_bwd_wave(const float* __restrict__ x, c
       a1 += t[k][c];
       a2 += t[k][c] * xh[k][c];
     }
-    pg[q] = gxh;
-    pg[n / 4 + q] = gg;
+    pgxh[k] += gxh;
+    pgg[k] += gg;
   }
   a1 = wave_sum(a1);
   a2 = wave_sum(a2);
@@ -874,6 +874,23 @@ __device__ __forceinline__ void capsnorm_bwd_wave(const float* __restrict__ x, c
   }
 }
 
+// the parameter-gradient partials (d gamma | d beta, 2n columns) of the sum over a wave's
+// rows, one partial row per wave
+template <int NPL>
+__device__ __forceinline__ void store_gpart(float* __restrict__ gpart, size_t row, const f4 (&pgxh)[NPL / 4],
+                                            const f4 (&pgg)[NPL / 4], int lane) {
+  constexpr int n = 64 * NPL;
+  f4* pg = reinterpret_cast<f4*>(gpart + row * 2 * n);
+#pragma unroll
+  for (int k = 0; k < NPL / 4; ++k) {
+    pg[k * 64 + lane] = pgxh[k];
+    pg[n / 4 + k * 64 + lane] = pgg[k];
+  }
+}
+
+// BWD: a wave takes rpw consecutive rows; rpw == 1 keeps one partial row per frame at the
+// frame's own index (the range entry points' gpart layout), rpw > 1 writes partial row w
+// (srf_capsnorm_bwd's own workspace: rpw times fewer rows for its column sum)
 template <int NPL, bool BWD>
 __global__ __launch_bounds__(256) void capsnorm_wave_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, int training, float p,
@@ -881,15 +898,25 @@ __global__ __launch_bounds__(256) void capsnorm_wave_kernel(const float* __restr
                                                             const unsigned long long* __restrict__ seed_src,
                                                             unsigned stream, float* __restrict__ y,
                                                             float* __restrict__ stat, const float* __restrict__ g_in,
-                                                            float* __restrict__ gpart, RowMap rmap, int rows) {
+                                                            float* __restrict__ gpart, RowMap rmap, int rows, int rpw) {
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (w >= rows) return;   // whole waves: nothing below synchronises
+  const int lane = threadIdx.x & 63;
   const unsigned long long sd = srf_step_seed(seed, seed_src);
   const bool drop = training && p > 0.f;
-  if constexpr (BWD)
-    capsnorm_bwd_wave<NPL>(x, gamma, drop, p, sd, stream, stat, g_in, y, gpart, rmap.row(w), threadIdx.x & 63);
-  else
-    capsnorm_fwd_wave<NPL>(x, gamma, beta, drop, p, sd, stream, y, stat, rmap.row(w), threadIdx.x & 63);
+  if constexpr (BWD) {
+    const int r0 = w * rpw;
+    if (r0 >= rows) return;   // whole waves: nothing below synchronises
+    f4 pgxh[NPL / 4], pgg[NPL / 4];
+#pragma unroll
+    for (int k = 0; k < NPL / 4; ++k) pgxh[k] = pgg[k] = f4{0.f, 0.f, 0.f, 0.f};
+    const int r1 = min(rows, r0 + rpw);
+    for (int r = r0; r < r1; ++r)
+      capsnorm_bwd_wave<NPL>(x, gamma, drop, p, sd, stream, stat, g_in, y, pgxh, pgg, rmap.row(r), lane);
+    store_gpart<NPL>(gpart, rpw == 1 ? (size_t)rmap.row(r0) : (size_t)w, pgxh, pgg, lane);
+  } else {
+    if (w >= rows) return;
+    capsnorm_fwd_wave<NPL>(x, gamma, beta, drop, p, sd, stream, y, stat, rmap.row(w), lane);
+  }
 }
 
 __global__ __launch_bounds__(256) void capsnorm_fwd_kernel(
@@ -931,9 +958,13 @@ __global__ __launch_bounds__(256) void capsnorm_range_n_wave_kernel(CnItems item
   const unsigned stream = (unsigned)(kStreamMid0 + r.layer);
   const unsigned long long sd = srf_step_seed(seed, seed_src);
   const bool drop = training && p > 0.f;
-  if constexpr (BWD)
-    capsnorm_bwd_wave<NPL>(r.x, r.gamma, drop, p, sd, stream, r.stat, r.g_y, r.g_x, r.gpart, f, threadIdx.x & 63);
-  else
+  if constexpr (BWD) {
+    f4 pgxh[NPL / 4], pgg[NPL / 4];
+#pragma unroll
+    for (int k = 0; k < NPL / 4; ++k) pgxh[k] = pgg[k] = f4{0.f, 0.f, 0.f, 0.f};
+    capsnorm_bwd_wave<NPL>(r.x, r.gamma, drop, p, sd, stream, r.stat, r.g_y, r.g_x, pgxh, pgg, f, threadIdx.x & 63);
+    store_gpart<NPL>(r.gpart, (size_t)f, pgxh, pgg, threadIdx.x & 63);
+  } else
     capsnorm_fwd_wave<NPL>(r.x, r.gamma, r.beta, drop, p, sd, stream, r.y, r.stat, f, threadIdx.x & 63);
 }
 
@@ -1023,15 +1054,19 @@ int check_caps(int B, int T, int PH, int PD) {
 
 }  // namespace
 
+// frames per wave of srf_capsnorm_bwd's wave kernel (4: F / 4 partial rows, a single-launch
+// column sum at C4's F = 5600, and still > 256 workgroups)
+constexpr int kCnRowsPerWave = 4;
+
 // the wave-per-row kernels for n = 256, 512, 1024 (C2 / C3 / C4 / C5 widths); false: other n
 template <bool BWD>
 static bool capsnorm_wave(int n, int rows, RowMap rm, const float* x, const float* gamma, const float* beta,
                           int training, float p, unsigned long long seed, unsigned stream, float* y, float* stat,
-                          const float* g_in, float* gpart, hipStream_t st) {
-  const dim3 grid((rows + 3) / 4);
+                          const float* g_in, float* gpart, hipStream_t st, int rpw = 1) {
+  const dim3 grid(((rows + rpw - 1) / rpw + 3) / 4);
 #define SRF_CN_WAVE(NPL)                                                                                             \
   hipLaunchKernelGGL((capsnorm_wave_kernel<NPL, BWD>), grid, dim3(256), 0, st, x, gamma, beta, training, p, seed,   \
-                     srf::seed_source(), stream, y, stat, g_in, gpart, rm, rows)
+                     srf::seed_source(), stream, y, stat, g_in, gpart, rm, rows, rpw)
   if (n == 256) SRF_CN_WAVE(4);
   else if (n == 512) SRF_CN_WAVE(8);
   else if (n == 1024) SRF_CN_WAVE(16);
@@ -1324,14 +1359,18 @@ int srf_capsnorm_bwd(const float* x, int F, int n, const float* gamma, const flo
   float* part = static_cast<float*>(workspace);
   float* sum = part + srf::align_up((size_t)F * 2 * n * 4, 256) / 4;
   float* scratch = sum + srf::align_up((size_t)2 * n * 4, 256) / 4;
-  if (!capsnorm_wave<true>(n, F, RowMap::all(F), x, gamma, beta, training, p, seed, (unsigned)(kStreamMid0 + layer), g_x,
-                           const_cast<float*>(stat), g_y, part, st))
+  // wave kernels: kCnRowsPerWave frames per wave and one partial row per wave
+  int prow = F;
+  if (capsnorm_wave<true>(n, F, RowMap::all(F), x, gamma, beta, training, p, seed, (unsigned)(kStreamMid0 + layer), g_x,
+                          const_cast<float*>(stat), g_y, part, st, kCnRowsPerWave))
+    prow = (F + kCnRowsPerWave - 1) / kCnRowsPerWave;
+  else
     hipLaunchKernelGGL(capsnorm_bwd_kernel, dim3(F), dim3(256), (size_t)(n + 8) * 4, st, x, n, gamma, beta, training,
                        p, seed, srf::seed_source(), (unsigned)(kStreamMid0 + layer), stat, g_y, 0, 0, 1,
                        (const float*)nullptr, (const float*)nullptr, g_x, part, RowMap::all(F));
   SRF_LAUNCH_CHECK("capsnorm_bwd");
   (void)sum;
-  return srf::colsum(part, F, 2 * n, nullptr, scratch, st, srf::ColSplit{{g_gamma, g_beta, nullptr, nullptr}, {n, n, 0, 0}});
+  return srf::colsum(part, prow, 2 * n, nullptr, scratch, st, srf::ColSplit{{g_gamma, g_beta, nullptr, nullptr}, {n, n, 0, 0}});
 }
 
 int srf_caps_head_fwd(const float* v, int F, int J, int D, const float* gamma_mid, const float* beta_mid,
