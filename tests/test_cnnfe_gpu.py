@@ -104,3 +104,37 @@ def test_cnnfe_inference_uses_moving_stats(cuda):
     assert np.abs(out.cpu().double().numpy() - x.numpy()).max() < 2e-4 * (1 + np.abs(x.numpy()).max())
     assert torch.allclose(moving[0].cpu().double(), mm[0].float().double())   # untouched
 
+
+
+def test_cnnfe_wgrad_side_stream_bitwise(cuda):
+    """ops.CNNFE_WGRAD_SIDE: srf_cnnfe_bwd_parts PREP + DATA on the backward's stream and
+    WGRAD deferred onto the side stream (joined by the end-of-backward callback) gives
+    the gradients of the one-call srf_cnnfe_bwd bit for bit (same kernels, same inputs),
+    read right after backward() without an explicit join."""
+    from srf_amd import ops
+    B, T, lens, p = CASES[1]
+    P = _params(5)
+    rng = np.random.default_rng(11)
+    feats = torch.tensor(rng.standard_normal((B, T, 123)), dtype=torch.float32, device=cuda)
+    inp_len = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    grads = []
+    for side in (False, True):
+        ops.CNNFE_WGRAD_SIDE = side
+        try:
+            Pg = {}
+            for k, v in P.items():
+                t = v.float().to(cuda).requires_grad_()
+                t.grad = torch.full_like(t, float('nan'))   # written in place (flat-buffer views in the model)
+                t._srf_flat = True
+                Pg[k] = t
+            moving = [torch.zeros(64, device=cuda), torch.ones(64, device=cuda)] * 2
+            out = ops.cnnfe(feats, inp_len, [Pg[k] for k in ops.CNNFE_PARAMS], moving, True, p, 77)
+            g = torch.tensor(rng.standard_normal(out.shape) if not grads else gout, dtype=torch.float32)
+            gout = g.numpy()
+            (out * g.to(cuda)).sum().backward()
+            grads.append({k: Pg[k].grad.cpu().clone() for k in ops.CNNFE_PARAMS})
+        finally:
+            ops.CNNFE_WGRAD_SIDE = True
+    for k in ops.CNNFE_PARAMS:
+        assert torch.isfinite(grads[1][k]).all(), k
+        assert torch.equal(grads[0][k], grads[1][k]), (k, (grads[0][k] - grads[1][k]).abs().max())
