@@ -133,7 +133,7 @@ def cpu_baseline(model_gpu, cfg, class_n, T, seconds, threads=None, max_steps=50
               vd=cfg.model_caps_class_dim, class_n=class_n, context=bool(cfg.model_caps_context))
     shape = so.SrfShape(**kw)
     if threads is None:
-        threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16') or 16))
+        threads = len(os.sched_getaffinity(0))   # every core this process may run on
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     params = model_gpu.export_params()
@@ -224,7 +224,7 @@ def sdr_roofline(model, tms, group=1):
                                                                                      reads)}
 
 
-def measure(workload, args, world, rank, dev):
+def measure(workload, args, world, rank, dev, flag_group=None):
     """One workload: W eager + W graphed warmup steps, K timed training steps (the
     hipGraph replay of forward + CTC + backward, then the all-reduce and Adam), K
     eager steps with HIP events around the last layer's forward routing passes,
@@ -278,18 +278,23 @@ def measure(workload, args, world, rank, dev):
     if args.eager:
         step = eager_step
     else:
-        # forward + CTC + backward as one hipGraph; all-reduce and Adam eager per step
-        try:
-            graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
-        except RuntimeError as e:
-            if not bucketed:
-                raise
-            # every rank fails the same capture: fall back to the flat form on all of them
-            print(f'[bench] capturing the bucketed all-reduce failed ({e}); flat all-reduce instead',
-                  file=sys.stderr)
-            bucketed = False
+        # forward + CTC + backward as one hipGraph; all-reduce and Adam eager per step.
+        # With buckets the capture holds their collectives: if any rank fails it, every
+        # rank falls back to the flat all-reduce (agreed over a gloo group)
+        def capture():
+            return trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
+
+        def flat():
             trainer_sr.use_grad_buckets(model, None)
-            graphed = trainer_sr.GraphedTrainStep(4, batch, model, opt, world, class_n - 1)
+            return capture()
+        if bucketed:
+            graphed, err = trainer_sr.capture_agreed(capture, flat, flag_group)
+            if err is not None:
+                bucketed = False
+                print(f'[bench] capturing the bucketed all-reduce failed ({err}); flat all-reduce on every rank',
+                      file=sys.stderr)
+        else:
+            graphed = capture()
         for _ in range(args.warmup):
             graphed(loss_state, frame_state, samples)
         torch.cuda.synchronize()
@@ -454,7 +459,11 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    res, model, cfg, class_n, T = measure(args.workload, args, world, rank, dev)
+    # a CPU side group for host-side agreements (the capture fallback), made on every rank
+    flag_group = None
+    if world > 1:
+        flag_group = dist.group.WORLD if backend == 'gloo' else dist.new_group(backend='gloo')
+    res, model, cfg, class_n, T = measure(args.workload, args, world, rank, dev, flag_group)
     line = {
         'metric': 'acoustic frames/sec through SRF (123-d fbank, 3-iter DR) at 1/2/4/8 MI355X',
         'value': res['value'], 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
@@ -464,7 +473,7 @@ def main():
         'config': res['config'], 'roofline': res['roofline'], 'forward_only': res['forward_only'],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the full host (16 threads on the box) on one utterance of the workload's
+        # the full host (every core in the affinity mask) on one utterance of the workload's
         # length, and one core on a quarter-length utterance (frames/s is per frame)
         cb = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)
         one = cpu_baseline(model, cfg, class_n, max(40, T // 4), args.cpu_seconds / 2, threads=1)
@@ -475,7 +484,7 @@ def main():
     if extra:
         line['extra'] = {}
         for w in extra:
-            r, m, _, _, _ = measure(w, args, world, rank, dev)
+            r, m, _, _, _ = measure(w, args, world, rank, dev, flag_group)
             del m
             line['extra'][w] = r
     if rank == 0:

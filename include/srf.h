@@ -210,6 +210,12 @@ int srf_route_sdr_pose(const float* emb, const float* W, const float* bias, int 
 int srf_route_sdr_pose_fp8(const float* emb, const float* W, const float* bias, int B, int T, int N, int din, int lpad,
                            int rpad, int J, int dout, int t0, int t1, float* u, int v0, int vn, void* stream);
 size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters);
+/* The part of that workspace that must be zero before its first grouped launch (the
+ * group counters and the timeout word, srf_sdr_range.group): *offset_bytes from the
+ * workspace's start, the return value its length in bytes.  The rest (kernel scratch,
+ * exchange area) needs no initialisation.  Shapes on the LDS / global-state kernels
+ * return the whole workspace. */
+size_t srf_route_sdr_recur_zero_range(int B, int in_n, int J, int dout, int iters, size_t* offset_bytes);
 /* Coupling storage per frame (0 when the shape runs on the LDS / global-state
  * kernels): with couplings != NULL ([B][T][this many floats]) recur_fwd stores each
  * frame's couplings c^r and pre-squash s^r, and recur_bwd reads them instead of

@@ -64,6 +64,7 @@ _SIGNATURES = {
     'srf_route_sdr_pose': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _c_int, _c_int, _vp]),
     'srf_route_sdr_pose_fp8': (_c_int, [_vp, _vp, _vp] + [_c_int] * 10 + [_vp, _c_int, _c_int, _vp]),
     'srf_route_sdr_recur_workspace': (_c_size, [_c_int] * 5),
+    'srf_route_sdr_recur_zero_range': (_c_size, [_c_int] * 5 + [ctypes.POINTER(_c_size)]),
     'srf_route_sdr_coupling_floats': (_c_size, [_c_int] * 4),
     'srf_route_sdr_couplings_required': (_c_int, [_c_int] * 4),
     'srf_route_sdr_recur_fwd': (_c_int, [_vp] + [_c_int] * 11 + [_vp, _vp, _vp, _c_size, _vp]),

@@ -192,7 +192,13 @@ class CheckpointManager:
 
     def save(self, checkpoint_number=None, overrides=None):
         """``overrides``: see model_state (data-parallel runs pass the replica-mean
-        BN moving statistics, which is what a MirroredStrategy checkpoint holds)."""
+        BN moving statistics, which is what a MirroredStrategy checkpoint holds).
+        Raises first if a grouped SDR recurrence timed out since the last check
+        (ops.check_faults): no checkpoint of parameters the run cannot vouch for."""
+        fp = getattr(self.model, 'flat_params', None)
+        if fp is not None and fp.is_cuda:
+            from . import ops
+            ops.check_faults()
         self.save_counter += 1
         n = self.save_counter if checkpoint_number is None else int(checkpoint_number)
         name = f'ckpt-{n}'

@@ -6,7 +6,11 @@
 
 namespace {
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, size_t n, float alpha, float b1, float b2, float eps) {
+                            float* __restrict__ v, size_t n, float alpha, float b1, float b2, float eps,
+                            const unsigned* __restrict__ fault) {
+  // a grouped recurrence of this step (or an earlier one not yet checked) gave wrong
+  // results: its gradient must not reach the parameters or the moments
+  if (fault != nullptr && *fault != 0u) return;
   const size_t n4 = n / 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
@@ -44,7 +48,7 @@ extern "C" int srf_adam_step(float* params, const float* grads, float* m, float*
   if (blocks > 2048) blocks = 2048;
   if (blocks == 0) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), params,
-                     grads, m, v, n, alpha, b1, b2, eps);
+                     grads, m, v, n, alpha, b1, b2, eps, static_cast<const unsigned*>(srf::fault_flag()));
   SRF_LAUNCH_CHECK("adam");
   return SRF_OK;
 }

@@ -1620,6 +1620,21 @@ size_t srf_route_sdr_recur_workspace(int B, int in_n, int J, int dout, int iters
   return recur_workspace(g);
 }
 
+size_t srf_route_sdr_recur_zero_range(int B, int in_n, int J, int dout, int iters, size_t* offset_bytes) {
+  SGeom g{B, 1, in_n, 8, 0, 0, J, dout, iters, 0};
+  size_t pre;
+  if (srf::sdr_seq_supported(in_n, J, dout, iters)) {
+    pre = 0;
+  } else if (srf::sdr_stream_supported(in_n, J, dout, iters)) {
+    pre = srf::sdr_stream_pre_floats(B, in_n, J, iters);
+  } else {   // global-state kernels: the whole workspace, as before
+    if (offset_bytes) *offset_bytes = 0;
+    return recur_workspace(g);
+  }
+  if (offset_bytes) *offset_bytes = srf_grp::coff(pre) * sizeof(float);
+  return (srf_grp::xoff(pre, B) - srf_grp::coff(pre)) * sizeof(float);
+}
+
 size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters) {
   const size_t n = srf::sdr_seq_cs_floats(in_n, J, dout, iters);
   return n ? n : srf::sdr_stream_cs_floats(in_n, J, dout, iters);

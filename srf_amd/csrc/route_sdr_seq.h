@@ -78,6 +78,8 @@ bool sdr_seq_plan(int in_n, int J, int dout, int iters, int* nim, int* rm, int g
 bool sdr_stream_supported(int in_n, int J, int dout, int iters);
 size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters);
 size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters);
+// the kernel's own scratch at the workspace start (the `pre` of srf_group.h)
+size_t sdr_stream_pre_floats(int B, int in_n, int J, int iters);
 int sdr_stream_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
                    hipStream_t st);
 int sdr_stream_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, hipStream_t st);

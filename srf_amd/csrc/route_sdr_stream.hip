@@ -598,6 +598,8 @@ size_t sdr_stream_cs_floats(int in_n, int J, int dout, int iters) {
   return sdr_stream_supported(in_n, J, dout, iters) ? cs_rec(in_n, J, dout, iters) : 0;
 }
 
+size_t sdr_stream_pre_floats(int B, int in_n, int J, int iters) { return gl_floats(B, in_n, J, iters); }
+
 size_t sdr_stream_workspace_floats(int B, int in_n, int J, int dout, int iters) {
   return sdr_stream_supported(in_n, J, dout, iters) ? srf_grp::floats(gl_floats(B, in_n, J, iters), B, J * dout) : 0;
 }

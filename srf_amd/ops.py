@@ -1,5 +1,6 @@
 """torch.autograd wrappers around the C ABI (device memory from torch's caching
 allocator, launches on torch's current HIP stream)."""
+import ctypes
 
 import torch
 
@@ -11,7 +12,6 @@ def _ptr(t):
 
 
 def ctypes_void(addr):
-    import ctypes
     return ctypes.c_void_p(addr)
 
 
@@ -120,6 +120,16 @@ def _dr_backward_done():
         s = _dr_side.get(main.device.index)
         if s is not None:
             main.wait_stream(s)
+
+
+def dr_reset():
+    """Drop deferred DR gW launches and the end-of-backward flag after a backward that
+    did not complete (a failed capture): the stale launches hold events recorded in
+    the dead capture, and a flag left set would keep later backwards from installing
+    their join.  GraphedTrainStep calls it when its capture raises."""
+    _dr_pending.clear()
+    _dr_state['queued'] = False
+    _dr_state['main'] = None
 
 
 def _defer_side(dev, ev, launch, keep):
@@ -606,6 +616,11 @@ class SdrStackPlan:
         self.nmax = max(max(b[k + 1] - b[k] for k in range(K)) for b in self.fwd)
         L_ = _lib.lib()
         self.rws = [L_.srf_route_sdr_recur_workspace(B, N * self.win, J, D, iters) for (N, din, J, D, mf) in layers]
+        self.rzs = []   # (offset, bytes) of each workspace's part that starts zero (group counters)
+        for (N, din, J, D, mf) in layers:
+            off = ctypes.c_size_t(0)
+            n = L_.srf_route_sdr_recur_zero_range(B, N * self.win, J, D, iters, ctypes.byref(off))
+            self.rzs.append((off.value, n))
         # fp8 pose: layers on the streaming recurrence keep u in bf16 (half the bytes of
         # every read; 2^-9 against the e4m3 operands' 2^-4); u_bf16=False keeps fp32
         self.ubf = [self.pose_fp8 and bool(u_bf16)
@@ -646,6 +661,15 @@ class SdrStackPlan:
         if not self.streamed[l]:
             return 2 if backward and self.store_couplings and self.B * (self.L + 1) <= cus else 1
         return max(1, min(8, (cus - self.B * (self.L - 1)) // self.B))
+
+    def recur_ws(self, l, dev):
+        """Layer l's recurrence workspace with its group counters zeroed (srf_group.h;
+        srf_route_sdr_recur_zero_range): one small fill, not a memset of the scratch."""
+        ws = torch.empty(max(self.rws[l], 16), device=dev, dtype=torch.uint8)
+        off, n = self.rzs[l]
+        if n:
+            ws[off:off + n].zero_()
+        return ws
 
     def pose_mode(self, l):
         """srf_route_sdr_pose_n mode: 0 fp32, 1 fp8, 2 fp8 with bf16 u."""
@@ -787,7 +811,7 @@ class SdrStack(torch.autograd.Function):
                 embs.append(torch.empty((B, T, J, D), device=dev, dtype=torch.float32))
                 stats.append(torch.empty((B * T, 4), device=dev, dtype=torch.float32))
             us.append(P.u_empty(l, T if store else P.nmax, dev))
-            rws.append(torch.zeros(max(P.rws[l], 16), device=dev, dtype=torch.uint8))   # group counters zero (srf_group.h)
+            rws.append(P.recur_ws(l, dev))
         main = torch.cuda.current_stream(dev)
         sa, sb, sc = _layer_streams(dev, 3, 'fwd')
         ev_a, ev_p = P.events('fwd_a', P.K + L), P.events('fwd_p', P.K)
@@ -915,7 +939,7 @@ class SdrStack(torch.autograd.Function):
             WTs.append(torch.empty(Ws[l].numel(), device=dev))
             gus.append(torch.empty(P.u_floats(l, P.nmax), device=dev))
             urs.append(us[l] if store else P.u_empty(l, P.nmax, dev))
-            rws.append(torch.zeros(max(P.rws[l], 16), device=dev, dtype=torch.uint8))   # group counters zero (srf_group.h)
+            rws.append(P.recur_ws(l, dev))
             pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
                                    dtype=torch.uint8) if l < L - 1 else None)
         main = torch.cuda.current_stream(dev)

@@ -87,6 +87,20 @@ def allreduce_grads(model):
     """The flat form: one SUM all-reduce of the whole gradient after the backward."""
     if _world() > 1:
         dist.all_reduce(model.flat_grad, op=dist.ReduceOp.SUM)
+        agree_faults(model)
+
+
+def agree_faults(model):
+    """MAX all-reduce of the process's fault word (ops.fault_flag) after the gradient
+    collectives, on the stream the optimizer runs on.  A grouped SDR recurrence that
+    timed out on one rank made every rank's summed gradient wrong: with the word
+    agreed, every rank's Adam launch skips the update (adam.hip reads the word) and
+    every rank's ops.check_faults raises at the same step, so no rank is left waiting
+    in a collective its peers never join.  Only models with SDR layers have the word
+    (the SdrStack forward registers it on every rank before the first step)."""
+    if _world() <= 1 or not model.flat_grad.is_cuda or not getattr(model, 'is_context', False):
+        return
+    dist.all_reduce(ops.fault_flag(model.flat_grad.device), op=dist.ReduceOp.MAX)
 
 
 class GradBuckets:
@@ -193,6 +207,8 @@ class GradBuckets:
             w.wait()
         if self.gpu and self.works:
             torch.cuda.current_stream().wait_stream(self.side)
+        if self.works:
+            agree_faults(self.model)
         self.begin()
 
 
@@ -357,6 +373,11 @@ class GraphedTrainStep:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, pool=pool):
                 self.nll = self._fwd_bwd()
+        except BaseException:
+            ops.dr_reset()   # deferred side-stream launches of the failed backward are void
+            if self.buckets is not None:
+                self.buckets.begin()
+            raise
         finally:
             model.grad_hook = hook
         with torch.no_grad():
@@ -422,6 +443,34 @@ class GraphedTrainStep:
         if samples is not None:
             samples.update_state(self.batch)
         return nll
+
+
+def capture_agreed(capture, fallback, group=None):
+    """``capture()`` on every rank, falling back to ``fallback()`` on EVERY rank when
+    any rank's capture raised RuntimeError (one int MIN all-reduce over ``group``, a
+    CPU gloo group, after the attempt).  A rank-local fallback would leave one rank
+    replaying captured bucket collectives while another issues a flat all-reduce:
+    the collective sequences would differ and the job hang.  Returns (result, error)
+    with error the local exception, or a note that a peer failed, when the fallback
+    ran; a capture that succeeded here but not on a peer is closed."""
+    err = None
+    try:
+        g = capture()
+    except RuntimeError as e:
+        g, err = None, e
+    ok = err is None
+    if group is not None:
+        t = torch.tensor([int(ok)], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        ok = bool(t.item())
+    if ok:
+        return g, None
+    if g is not None:
+        close = getattr(g, 'close', None)
+        if close is not None:
+            close()
+        err = RuntimeError('the capture failed on another rank')
+    return fallback(), err
 
 
 class GraphCache:

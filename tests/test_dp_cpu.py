@@ -243,3 +243,66 @@ def test_gloo_graph_cache_agrees_on_capture_steps():
     # though rank 1 holds a graph for 90; steps 4-6: graph on both
     assert graph[0] == [False, False, True, False, True, True, True]
     assert res[0][2] == res[1][2] == 2 and res[0][3] == res[1][3] == 3
+
+
+class _Capture:
+    def __init__(self, form, log):
+        self.form, self.log = form, log
+        self.closed = False
+        log.append('capture ' + form)
+
+    def close(self):
+        self.closed = True
+        self.log.append('close ' + self.form)
+
+
+def _fallback_worker(rank, world, port, fail_rank, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    log = []
+
+    def bucketed():
+        if rank == fail_rank:
+            raise RuntimeError('capture failed (forced)')
+        return _Capture('bucketed', log)
+
+    def flat():
+        return _Capture('flat', log)
+    g, err = trainer_sr.capture_agreed(bucketed, flat, dist.group.WORLD)
+    # the form every rank replays must issue the same collective: one all-reduce per step
+    # whose size tells the form (bucketed: 2 elements, flat: 1); a mismatch would hang
+    t = torch.ones(2 if g.form == 'bucketed' else 1)
+    work = dist.all_reduce(t, async_op=True)
+    work.wait(timeout=__import__('datetime').timedelta(seconds=30))
+    q.put((rank, g.form, err is not None, log, float(t.sum())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('fail_rank', [1, -1])
+def test_gloo_capture_fallback_is_collective(fail_rank):
+    """bench.py's capture of the bucketed step (world 2, gloo): when one rank's capture
+    fails, EVERY rank falls back to the flat all-reduce (a rank whose capture succeeded
+    closes it), so both replay the same collective form; when none fails, both keep the
+    captured buckets."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fallback_worker, args=(r, world, port, fail_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    forms = [r[1] for r in res]
+    if fail_rank < 0:
+        assert forms == ['bucketed', 'bucketed'] and not any(r[2] for r in res)
+        assert all(r[4] == 4.0 for r in res)
+    else:
+        assert forms == ['flat', 'flat'] and all(r[2] for r in res)
+        assert res[1 - fail_rank][3] == ['capture bucketed', 'close bucketed', 'capture flat']
+        assert res[fail_rank][3] == ['capture flat']
+        assert all(r[4] == 2.0 for r in res)

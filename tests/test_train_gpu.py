@@ -63,6 +63,32 @@ def test_adam_matches_oracle(cuda, k, warmup, max_lr):
         assert not np.allclose(model.flat_params.cpu().numpy(), p0.astype(np.float32))
 
 
+def test_adam_skips_update_while_fault_word_set(cuda):
+    """A grouped SDR recurrence that timed out sets the process's fault word
+    (srf_set_fault_flag): until the host has read and cleared it, the fused Adam must
+    not apply a gradient computed from the wrong results (adam.hip reads the word)."""
+    from srf_amd import ops, train_helper
+    n = 1024 + 3
+    cfg = config_from_shape({'feat_dim': 123, 'enc_num': 1, 'iters': 1, 'lpad': 0, 'rpad': 0, 'ph': 4, 'pd': 8,
+                             'ch': 4, 'cd': 8, 'vd': 8, 'context': False},
+                            train_lr_param_k=100.0, train_warmup_n=2, train_lr_max=1e-2)
+    opt = train_helper.get_optimizer(cfg)
+    model = _Flat(np.linspace(-1, 1, n), cuda)
+    model.flat_grad.fill_(1.0)
+    p0 = model.flat_params.clone()
+    f = ops.fault_flag(cuda)
+    f.fill_(1)
+    opt.apply_gradients(model)
+    torch.cuda.synchronize()
+    assert torch.equal(model.flat_params, p0) and not opt._m.abs().max().item()
+    with pytest.raises(RuntimeError, match='timed out'):
+        ops.check_faults()          # reads and clears the word
+    assert int(f.item()) == 0
+    opt.apply_gradients(model)
+    torch.cuda.synchronize()
+    assert (model.flat_params - p0).abs().min().item() > 0
+
+
 # ---------------------------------------------------------------------------
 # bucketed TFRecord batches through the captured step
 _BUCKETS = ([30, 45], [4, 3, 2])
