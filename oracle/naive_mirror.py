@@ -282,6 +282,52 @@ def sdr_layer_teacher_forced(emb, W, bias, v_run, lpad, rpad, iters, masked, fp8
     return out
 
 
+def sdr_layer_backward_teacher_forced(emb, W, bias, v_run, g_bar, lpad, rpad, iters, masked, frames_per_chunk=8):
+    """The adjoint of each frame of one SDR layer, teacher-forced like
+    ``sdr_layer_teacher_forced``: frame t's routing (naive:162-170 with :231-245 /
+    :212-229) as a float64 function of its own pose u_t and of v_{t-1} taken from
+    ``v_run``, differentiated (TF's tape.gradient of the frame, trainer_sr.py:70) for
+    the cotangent ``g_bar[:, t]`` = dL/dv_t as the implementation under test holds it
+    (the loss gradient of frame t plus the carry from frame t + 1).  Every frame is an
+    independent check, so the bound need not cover the recurrence's amplification of
+    rounding along the frames.  Returns (g_u [B,T,I,J,Dv], g_vprev [B,T,J,Dv]) float64:
+    the gradient of the frame's pose and the carry into frame t - 1."""
+    emb = torch.as_tensor(emb, dtype=torch.float64)
+    W = torch.as_tensor(W, dtype=torch.float64)
+    bias = torch.as_tensor(bias, dtype=torch.float64)
+    v_run = torch.as_tensor(v_run, dtype=torch.float64)
+    g_bar = torch.as_tensor(g_bar, dtype=torch.float64)
+    B, T, N, D = emb.shape
+    I, J, Dv, _ = W.shape
+    ep = F.pad(emb, (0, 0, 0, 0, lpad, rpad)).transpose(0, 1)                  # [T+w-1, B, N, D]
+    m = torch.zeros(J, I, dtype=torch.float64)
+    if masked:
+        m[0] = so.MASK_LOGIT
+    g_u = torch.empty(B, T, I, J, Dv, dtype=torch.float64)
+    g_vp = torch.empty(B, T, J, Dv, dtype=torch.float64)
+    for t0 in range(0, T, frames_per_chunk):
+        t1 = min(T, t0 + frames_per_chunk)
+        n = t1 - t0
+        xw = torch.cat([ep[t0 + w:t1 + w] for w in range(lpad + rpad + 1)], 2)   # [n, B, I, D]
+        u = torch.bmm(W.reshape(I, J * Dv, D), xw.permute(2, 3, 0, 1).reshape(I, D, n * B))
+        u = (u.reshape(I, J, Dv, n, B).permute(3, 4, 1, 0, 2) + bias.permute(1, 0, 2)).requires_grad_(True)
+        vp = torch.zeros(n, B, J, Dv, dtype=torch.float64)
+        vp[max(0, 1 - t0):] = v_run[:, max(t0 - 1, 0):t1 - 1].transpose(0, 1)
+        vp.requires_grad_(True)
+        v = vp
+        b = torch.zeros(n, B, J, I, dtype=torch.float64)
+        for _ in range(iters):
+            b = b + torch.matmul(u, v.unsqueeze(-1)).squeeze(-1)
+            if masked:
+                b = b + m
+            c = torch.softmax(b, dim=2)
+            v = squash(torch.matmul(c.unsqueeze(3), u).squeeze(3), -1)
+        gu, gv = torch.autograd.grad(v, (u, vp), g_bar[:, t0:t1].transpose(0, 1))
+        g_u[:, t0:t1] = gu.permute(1, 0, 3, 2, 4)                              # [n,B,J,I,Dv] -> [B,n,I,J,Dv]
+        g_vp[:, t0:t1] = gv.transpose(0, 1)
+    return g_u, g_vp
+
+
 class NaiveMirror(torch.nn.Module):
     """Parameters are held in a dict of tensors keyed like ``srf_oracle.init_params``."""
 

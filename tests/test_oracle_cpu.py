@@ -210,6 +210,43 @@ def test_sdr_teacher_forced_is_one_step_of_the_recurrence():
     assert ((v32 - v64).abs() / (1 + v64.abs())).max() > 1e-5
 
 
+@pytest.mark.parametrize('masked', [False, True])
+def test_sdr_backward_teacher_forced_is_one_frame_of_the_adjoint(masked):
+    """sdr_layer_backward_teacher_forced, fed a float64 run's own v and, per frame, the
+    total dL/dv_t of a float64 autograd backward through the whole recurrence (loss
+    gradient plus the carry from frame t + 1), reproduces that backward's pose gradient
+    for every frame and its carry into frame t - 1 (to float64 rounding)."""
+    import torch.nn.functional as F
+    rng = np.random.default_rng(1)
+    B, T, N, D, J, Dv, lp, rp, iters = 2, 6, 3, 4, 5, 4, 1, 1, 3
+    I = N * (lp + rp + 1)
+    emb = torch.tensor(rng.standard_normal((B, T, N, D)))
+    W = torch.tensor(rng.standard_normal((I, J, Dv, D)) * 0.3)
+    bias = torch.tensor(rng.standard_normal((I, J, Dv)) * 0.1)
+    g_v = torch.tensor(rng.standard_normal((B, T, J, Dv)))
+    ep = F.pad(emb, (0, 0, 0, 0, lp, rp))
+    xw = torch.cat([ep[:, w:w + T] for w in range(lp + rp + 1)], 2)            # [B, T, I, D]
+    u = (torch.einsum('ijek,btik->btije', W, xw) + bias).requires_grad_(True)   # [B, T, I, J, Dv]
+    v = torch.zeros(B, J, Dv, dtype=torch.float64)
+    m = torch.zeros(B, I, J, dtype=torch.float64)
+    if masked:
+        m[..., 0] = -1e9
+    vs = []
+    for t in range(T):
+        b = torch.zeros(B, I, J, dtype=torch.float64)
+        for _ in range(iters):
+            b = b + torch.sum(u[:, t] * v.unsqueeze(1), -1) + m
+            v = nm.squash(torch.sum(torch.softmax(b, 2).unsqueeze(-1) * u[:, t], 1), -1)
+        v.retain_grad()
+        vs.append(v)
+    sum((vs[t] * g_v[:, t]).sum() for t in range(T)).backward()
+    g_bar = torch.stack([x.grad for x in vs], 1)
+    gu, gvp = nm.sdr_layer_backward_teacher_forced(emb, W, bias, torch.stack([x.detach() for x in vs], 1), g_bar,
+                                                   lp, rp, iters, masked, frames_per_chunk=4)
+    assert (gu - u.grad).abs().max() < 1e-13
+    assert (gvp[:, 1:] - (g_bar - g_v)[:, :-1]).abs().max() < 1e-13
+
+
 def test_e4m3_and_bf16_emulation_match_torch_casts():
     """The fp8-pose restatement's rounding (srf_oracle.e4m3_round / bf16_round) equals
     torch's float8_e4m3fn / bfloat16 casts (round to nearest even, e4m3 subnormals),

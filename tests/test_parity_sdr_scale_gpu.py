@@ -218,3 +218,95 @@ def test_c5_first_layer_reference_init_teacher_forced(cuda, pose):
         err = ((vs[0] - ref).abs() / (1 + ref.abs())).max()
         print(pose, 'max |err| / (1 + |ref|) = %.3g' % float(err))
         assert err <= FP8_V_TOL, float(err)
+
+
+# --------------------------------------------------------------------------- reference-init backward
+@pytest.mark.parametrize('layer,group', [((16, 32, 16, 32, 0), 1), ((16, 32, 32, 32, 1), 2)],
+                         ids=['c3_inner', 'c3_last_G2'])
+def test_c3_reference_init_backward_teacher_forced(cuda, layer, group):
+    """The backward of a C3 layer at the reference init W ~ N(0, 0.1), B = 28 (the
+    bench's batch), frame by frame: the recurrence backward runs one frame per launch
+    (srf_route_sdr_recur_bwd_n, the last layer on G = 2 workgroups per utterance as the
+    bench runs it), so the carry the GPU hands each frame (dL/dv_t from frame t + 1) is
+    read back, and every frame's full pose gradient g_u_t and its carry into frame t - 1
+    are checked against the float64 adjoint of that one frame given the run's own
+    v_{t-1} and that carry (``oracle.naive_mirror.sdr_layer_backward_teacher_forced``)
+    at the routing-layer gradient bound.  Then gx (window adjoint of W^T g_u) and
+    gW / gbias (sum over frames of g_u x^T, g_u) of the fused contraction
+    (srf_route_sdr_gx_gw_n) against float64 contractions of the GPU's own g_u.  At this
+    init a free-running float32 mirror drifts from float64 by 6e-5 in v and 8e-4 in
+    the gradients within 10 frames, so per-frame teacher forcing is what makes a tight
+    full-gradient check possible (the scaled-init stack test covers the plan's ranges)."""
+    import ctypes
+    from srf_amd import _lib
+    L = _lib.lib()
+    N, din, J, D, mf = layer
+    lp = rp = 2
+    B, T, iters = 28, 64, 3
+    in_n, JD = N * (lp + rp + 1), J * D
+    rng = np.random.default_rng(308 + J)
+    Ws, bs, _, _ = _params(rng, [layer], lp, rp, 1.0)
+    W64, b64 = Ws[0], bs[0]
+    emb = _f32(rng.standard_normal((B, T, N, din)))
+    g_v = _f32(rng.standard_normal((B, T, J, D)))
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    te = torch.tensor(emb, dtype=torch.float32, device=cuda)
+    tW = torch.tensor(W64, dtype=torch.float32, device=cuda)              # [in_n, J, D, din] = [in_n][J*D][din]
+    tb = torch.tensor(b64, dtype=torch.float32, device=cuda)
+    tg = torch.tensor(g_v, dtype=torch.float32, device=cuda)
+    u = torch.zeros(B * T * in_n * JD, device=cuda)
+    v = torch.zeros(B, T, JD, device=cuda)
+    ncs = L.srf_route_sdr_coupling_floats(in_n, J, D, iters)
+    assert ncs > 0 and not L.srf_route_sdr_couplings_required(in_n, J, D, iters), 'C3: register recurrence'
+    cs = torch.zeros(B * T * ncs, device=cuda)
+    ws_n = L.srf_route_sdr_recur_workspace(B, in_n, J, D, iters)
+    ws = torch.zeros(max(ws_n // 4, 4) + 4, device=cuda)
+    r = _lib.SdrRange(t0=0, t1=T, emb=p(te), W=p(tW), bias=p(tb), u=p(u), v0=0, vn=T, v=p(v), couplings=p(cs),
+                      workspace=p(ws), workspace_bytes=ws.numel() * 4)
+    _lib.check(L.srf_route_sdr_pose_n((_lib.SdrRange * 1)(r), 1, B, T, N, din, lp, rp, J, D, 0, st), 'pose')
+    _lib.check(L.srf_route_sdr_recur_fwd_n((_lib.SdrRange * 1)(r), 1, B, T, in_n, J, D, iters, mf, st), 'fwd')
+    gu = torch.zeros(B * T * in_n * JD, device=cuda)
+    carry = torch.zeros(B, JD, device=cuda)
+    c_in = torch.zeros(B, T, JD, device=cuda)
+    c_out = torch.zeros(B, T, JD, device=cuda)
+    for t in range(T - 1, -1, -1):   # one frame per launch: the carry between frames is read back
+        c_in[:, t] = carry
+        rt = _lib.SdrRange(t0=t, t1=t + 1, u=p(u), v0=0, vn=T, v=p(v), couplings=p(cs), workspace=p(ws),
+                           workspace_bytes=ws.numel() * 4, g_v=p(tg), carry=p(carry), gu=p(gu), g0=0, gn=T,
+                           group=group)
+        _lib.check(L.srf_route_sdr_recur_bwd_n((_lib.SdrRange * 1)(rt), 1, B, T, in_n, J, D, iters, mf, st), 'bwd')
+        c_out[:, t] = carry
+    torch.cuda.synchronize()
+    v_run = v.cpu().double().reshape(B, T, J, D)
+    g_bar = torch.tensor(g_v) + c_in.cpu().double().reshape(B, T, J, D)
+    ref_gu, ref_gvp = nm.sdr_layer_backward_teacher_forced(emb, W64, b64, v_run, g_bar, lp, rp, iters, bool(mf))
+    got_gu = gu.cpu().double().reshape(B, T, in_n, J, D)
+    for name, got, ref in (('g_u', got_gu, ref_gu), ('carry', c_out.cpu().double().reshape(B, T, J, D), ref_gvp)):
+        err, scale = float((got - ref).abs().max()), float(ref.abs().max())
+        print(name, 'max |err| / max(1, max|ref|) = %.3g' % (err / max(1.0, scale)), 'max|ref| %.3g' % scale)
+        assert scale > 0 and err <= G_TOL * max(1.0, scale), (name, err, scale)
+    # the contractions of the GPU's own g_u: gx through the window adjoint, gW, gbias
+    WT = tW.reshape(in_n, JD, din).permute(0, 2, 1).contiguous()
+    g_emb = torch.zeros_like(te)
+    gW = torch.zeros(in_n, JD, din, device=cuda)
+    gb = torch.zeros(in_n, JD, device=cuda)
+    rg = _lib.SdrRange(t0=0, t1=T, emb=p(te), W=p(tW), WT=p(WT), gu=p(gu), g0=0, gn=T, g_emb=p(g_emb), g_W=p(gW),
+                       g_bias=p(gb), accumulate=0)
+    _lib.check(L.srf_route_sdr_gx_gw_n((_lib.SdrRange * 1)(rg), 1, B, T, N, din, lp, rp, J, D, st), 'gx_gw')
+    torch.cuda.synchronize()
+    gu64 = got_gu.reshape(B, T, in_n, JD)
+    xw = torch.nn.functional.pad(torch.tensor(emb), (0, 0, 0, 0, lp, rp))
+    xw = torch.cat([xw[:, w:w + T] for w in range(lp + rp + 1)], 2)                  # [B, T, in_n, din]
+    ref_gW = torch.einsum('btir,btik->irk', gu64, xw)
+    ref_gb = gu64.sum((0, 1))
+    gxw = torch.einsum('btir,irk->btik', gu64, torch.tensor(W64).reshape(in_n, JD, din))   # [B, T, in_n, din]
+    ref_ge = torch.zeros(B, T + lp + rp, N, din, dtype=torch.float64)
+    for w in range(lp + rp + 1):
+        ref_ge[:, w:w + T] += gxw[:, :, w * N:(w + 1) * N]
+    ref_ge = ref_ge[:, lp:lp + T]
+    for name, got, ref in (('g_emb', g_emb, ref_ge), ('g_W', gW, ref_gW), ('g_bias', gb, ref_gb)):
+        got = got.cpu().double().reshape(ref.shape)
+        err, scale = float((got - ref).abs().max()), float(ref.abs().max())
+        print(name, 'max |err| / max(1, max|ref|) = %.3g' % (err / max(1.0, scale)))
+        assert err <= G_TOL * max(1.0, scale), (name, err, scale)
