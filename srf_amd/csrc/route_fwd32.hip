@@ -49,8 +49,7 @@
 // half of a din <= 16 workgroup's waves runs at s_setprio 1 (~3 % on the backward pass).
 
 // SRF_DR_IL (A/B builds only): 1 = the din-32 pipelined passes run the previous capsule's
-// finish between the pose MFMAs (pose_prog32i); 0 = after them (pose_prog); 2 = the
-// forward pass with three capsules in flight (logits and finish in the MFMA gaps).
+// finish between the pose MFMAs (pose_prog32i); 0 = after them (pose_prog).
 #ifndef SRF_DR_IL
 #define SRF_DR_IL 1
 #endif
@@ -1246,21 +1245,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   // stats, then (din 32) two buffers of the shared x fragments (x_dma)
   float2* st = reinterpret_cast<float2*>(lds);
   constexpr bool XL = DIN == 32;
-  // IL3 keeps three capsules' tiles in registers: Vc then lives in the wave's LDS slab
-  // (fragment order, conflict-free ds_read_b128) instead of registers
-  constexpr bool VCL = XL && SRF_DR_IL == 2;
-  f4 vcr[VCL ? 1 : TW][4];
-  __shared__ __attribute__((aligned(16))) f4 vcls[VCL ? NW * TW * 4 * 64 : 1];
+  f4 vcr[TW][4];
   // a separate LDS object: the compiler then sees no DMA aliasing the stats
   __shared__ __attribute__((aligned(16))) char xls[XL ? 2 * 4 * kXlPiece : 16];
   char* xb = xls;
   const char* xs_b = static_cast<const char*>(A.xs);
-  // IL3 runs chunks of 3k + 2 capsules: others start at a virtual capsule i0v < i0 (up to
-  // two leading steps on capsule i0's operands whose couplings are zero and never stored)
-  constexpr bool IL3 = XL && SRF_DR_IL == 2;
-  const int i0v = IL3 ? i0 - (5 - (i1 - i0) % 3) % 3 : i0;
-  auto clampc = [&](int c) { return min(max(c, i0), i1 - 1); };
-  auto xsrc = [&](int c) { return x_voff<DIN>(clampc(c), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
+  auto xsrc = [&](int c) { return x_voff<DIN>(min(c, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
   auto xbuf = [&](int c) { return xb + (c & 1) * 4 * kXlPiece; };
 #pragma unroll
   for (int t = 0; t < TW; ++t)
@@ -1269,10 +1259,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       const int row = (tbase + t) * 32 + 8 * q + 4 * h;
       f4 v = {0.f, 0.f, 0.f, 0.f};
       if (fvalid && row < JD) v = *reinterpret_cast<const f4*>(A.vc + (size_t)f * JD + row);
-      if constexpr (VCL)
-        vcls[((wv * TW + t) * 4 + q) * 64 + lane] = v;
-      else
-        vcr[t][q] = v;
+      vcr[t][q] = v;
     }
   float mk[OWN];
 #pragma unroll
@@ -1292,9 +1279,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
                            fr);
     f16v uc[TW], un[TW];
     float e[OWN], m;   // the pending capsule's exponentials and lane max
-    if constexpr (XL) {   // x of capsules i0v + 1, i0v + 2 into LDS before the first pose
-      x_dma(xs_b, A.xplane_b, xsrc(i0v + 1), wv, xbuf(i0v + 1));
-      x_dma(xs_b, A.xplane_b, xsrc(i0v + 2), wv, xbuf(i0v + 2));
+    if constexpr (XL) {   // x of capsules i0 + 1, i0 + 2 into LDS before the first pose
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 1), wv, xbuf(i0 + 1));
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 2), wv, xbuf(i0 + 2));
       xl_wait();
       __syncthreads();
     }
@@ -1307,11 +1294,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       for (int t = 0; t < TW; ++t)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          f4 vv;
-          if constexpr (VCL)
-            vv = vcls[((wv * TW + t) * 4 + q) * 64 + lane];
-          else
-            vv = vcr[t][q];
+          const f4 vv = vcr[t][q];
           const int k = kpart<DOUT>(t, 4 * q);
           P2[k] += f2{u[t][4 * q], u[t][4 * q + 1]} * f2{vv.x, vv.y};
           P2[k] += f2{u[t][4 * q + 2], u[t][4 * q + 3]} * f2{vv.z, vv.w};
@@ -1340,13 +1323,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     };
     int par = 0;
     pose_prog<DIN, TW, XL>(fr, ones, uc, rs, wvo, bvo,
-                           x_voff<DIN>(clampc(i0v + 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)clampc(i0v + 1) * A.JDp * DIN * 2,
-                           (uint32_t)clampc(i0v + 1) * A.JDp * 8, xbuf(i0v + 1) + lane * 16);
-    if constexpr (!(XL && SRF_DR_IL == 2)) {   // IL3: capsule i0's logits run inside its first step
-      logits(uc, par);
-      __syncthreads();
-    }
+                           x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
+                           (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8, xbuf(i0 + 1) + lane * 16);
+    logits(uc, par);
+    __syncthreads();
     // one capsule: i + 1's tiles into unext while capsule i (in ucur) is finished; the loop
     // runs two steps with the roles swapped, so no register copy moves u between them
     // IL: capsule i's finish between capsule i + 1's pose MFMAs (pose_prog32i)
@@ -1484,87 +1465,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         __syncthreads();
       }
     };
-    // IL3: three capsules in flight -- step3(i) issues capsule i + 1's pose MFMAs and,
-    // between them, capsule i's logits (its tiles finished in the previous step) and
-    // capsule i - 1's finish (its stats published by the previous barrier); one barrier
-    // per step publishes capsule i's stats.  All of a capsule's VALU work then runs in
-    // the MFMA gaps of the next pose instead of after it.
-    auto step3 = [&](int i, f16v (&uprev)[TW], f16v (&ucur)[TW], f16v (&unext)[TW]) __attribute__((always_inline)) {
-      if constexpr (DIN == 32) {
-      const bool fin = i > i0;   // capsule i - 1 exists (virtual capsules i < i0 are not finished)
-      x_dma(xs_b, A.xplane_b, xsrc(i + 3), wv, xbuf(i + 3));   // into the buffer capsule i + 1's x left
-      float ep[OWN];
-#pragma unroll
-      for (int a = 0; a < OWN; ++a) ep[a] = e[a];
-      const float mp = m;
-      constexpr int HW = NW / 2;
-      float2 sv[HW];
-      float c[CP];
-      auto fill = [&](auto stage) __attribute__((always_inline)) {
-        constexpr int S = decltype(stage)::value;
-        if constexpr (S == 0) {   // capsule i - 1's softmax stats of the 4 waves of this lane half
-          const float2* slot = st + ((i - 1 - i0v) & 1) * NW * 32;
-#pragma unroll
-          for (int w = 0; w < HW; ++w) sv[w] = slot[(h * HW + w) * 32 + r];
-        } else if constexpr (S == 1) {
-          logits(ucur, (i - i0v) & 1);   // capsule i: e, m and the wave's stats
-        } else if constexpr (S == 2) {
-          float mh = sv[0].x;
-#pragma unroll
-          for (int w = 1; w < HW; ++w) mh = fmaxf(mh, sv[w].x);
-          float zh = 0.f;
-#pragma unroll
-          for (int w = 0; w < HW; ++w) zh += sv[w].y * __expf(sv[w].x - mh);
-          float m0, m1, z0, z1;
-          xpair32(mh, m0, m1);
-          xpair32(zh, z0, z1);
-          const float M = fmaxf(m0, m1);
-          const float Z = z0 * __expf(m0 - M) + z1 * __expf(m1 - M);
-          const float sc = fin ? __expf(mp - M) * __builtin_amdgcn_rcpf(Z) : 0.f;   // Z >= 1: 1-ulp v_rcp
-          const uint32_t ci = (uint32_t)max(i - 1, 0);
-#pragma unroll
-          for (int a = 0; a < OWN; ++a)
-            bstore(crs, fvalid ? ep[a] * sc : 0.f, fin ? (uint32_t)((j0 + h + 2 * a) * A.Fs + f) * 4u : kNoStore,
-                   ci * A.JP * A.Fs * 4u);
-          bstore(lzs, M + __builtin_amdgcn_logf(Z) * 0.69314718f,
-                 (fin && h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore, ci * A.Fs * 4u);
-#pragma unroll
-          for (int a = 0; a < OWN; ++a) {
-            float c0, c1;
-            xpair32(ep[a] * sc, c0, c1);
-            c[2 * a] = c0;
-            c[2 * a + 1] = c1;
-          }
-        } else {   // s += c u of capsule i - 1 (c = 0 on the first step; uprev is zero there)
-#pragma unroll
-          for (int t = 0; t < TW; ++t) {
-#pragma unroll
-            for (int v = 0; v < 16; ++v) acc[t][v] = fmaf(c[kpart<DOUT>(t, v)], uprev[t][v], acc[t][v]);
-            asm volatile("" : "+v"(acc[t]));   // keeps the FMAs in their MFMA region
-          }
-        }
-      };
-      {   // capsule i + 1's tiles (after the chunk's last capsule: its own operands, unused)
-        const int in = clampc(i + 2);
-        pose_prog32i<TW, 8, 5, 8>(fr, ones, unext, rs, wvo, bvo, A.wplane_b, (uint32_t)in * A.JDp * DIN * 2,
-                                  (uint32_t)in * A.JDp * 8, xbuf(i + 2) + lane * 16, fill);
-      }
-      xl_wait<5 * TW + OWN + 1>();   // capsule i + 3's x has landed before the barrier
-      __syncthreads();
-      }
-    };
-    if constexpr (IL3) {
-      f16v uz[TW];   // the third register set: zero, as capsule "i0v - 1" of the first step
-#pragma unroll
-      for (int t = 0; t < TW; ++t) uz[t] = f16v{};
-      // i1 - i0v + 1 steps (the last one only finishes capsule i1 - 1: its pose and logits
-      // are unused), three per turn
-      for (int i = i0v; i <= i1; i += 3) {
-        step3(i, uz, uc, un);
-        step3(i + 1, uc, un, uz);
-        step3(i + 2, un, uz, uc);
-      }
-    } else if constexpr (XL && SRF_DR_IL) {
+    if constexpr (XL && SRF_DR_IL) {
       for (int i = i0; i < i1; i += 2) {
         step(i, uc, un);
         if (i + 1 < i1) step(i + 1, un, uc);
@@ -1850,11 +1751,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   __shared__ __attribute__((aligned(16))) char xls[XL ? 2 * 4 * kXlPiece : 16];
   char* xb = xls;
   const char* xs_b = static_cast<const char*>(A.xs);
-  // IL3 (as route_fwd32p_kernel): chunks of 3k + 2 capsules, others from a virtual i0v
-  constexpr bool IL3 = XL && SRF_DR_IL == 2;
-  const int i0v = IL3 ? i0 - (5 - (i1 - i0) % 3) % 3 : i0;
-  auto clampc = [&](int c) { return min(max(c, i0), i1 - 1); };
-  auto xsrc = [&](int c) { return x_voff<DIN>(clampc(c), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
+  auto xsrc = [&](int c) { return x_voff<DIN>(min(c, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off); };
   auto xbuf = [&](int c) { return xb + (c & 1) * 4 * kXlPiece; };
 #pragma unroll
   for (int t = 0; t < TW; ++t)
@@ -1908,20 +1805,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
     };
     int par = 0;
     if constexpr (XL) {   // x of capsules i0 + 1, i0 + 2 into LDS before the first pose
-      x_dma(xs_b, A.xplane_b, xsrc(i0v + 1), wv, xbuf(i0v + 1));
-      x_dma(xs_b, A.xplane_b, xsrc(i0v + 2), wv, xbuf(i0v + 2));
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 1), wv, xbuf(i0 + 1));
+      x_dma(xs_b, A.xplane_b, xsrc(i0 + 2), wv, xbuf(i0 + 2));
       xl_wait();
       __syncthreads();
     }
     load_c<OWN>(crow + (size_t)i0 * cstep, A.Fs, cc);
     pose_prog<DIN, TW, XL>(fr, ones, uc, rs, wvo, bvo,
-                           x_voff<DIN>(clampc(i0v + 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
-                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)clampc(i0v + 1) * A.JDp * DIN * 2,
-                           (uint32_t)clampc(i0v + 1) * A.JDp * 8, xbuf(i0v + 1) + lane * 16);
-    if constexpr (!IL3) {   // IL3: capsule i0's dots run inside its first step
-      dots(uc, cc, par);
-      __syncthreads();
-    }
+                           x_voff<DIN>(min(i0 + 1, i1 - 1), A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
+                           A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * DIN * 2,
+                           (uint32_t)min(i0 + 1, i1 - 1) * A.JDp * 8, xbuf(i0 + 1) + lane * 16);
+    dots(uc, cc, par);
+    __syncthreads();
     // one capsule, as route_fwd32p_kernel's step: two steps per loop turn with the roles of
     // (uc, cc) and (un, cn) swapped, so no copies
     // IL: capsule i's finish between capsule i + 1's pose MFMAs (pose_prog32i)
@@ -2059,89 +1954,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         __syncthreads();
       }
     };
-    // IL3: step3(i) issues capsule i + 1's pose MFMAs with capsule i's dots (q, sigma
-    // partial) and capsule i - 1's finish (sigma, stats, gL, gVc += gL u) between them
-    const __amdgpu_buffer_rsrc_t gls = make_rsrc(Bk.glst, (size_t)A.in_n * A.JP * A.Fs * 4);
-    float Q3[OWN];   // q of capsule i - 1 (dots of the previous step)
-    auto step3 = [&](int i, f16v (&uprev)[TW], f16v (&ucur)[TW], f16v (&unext)[TW], float (&cprev)[OWN],
-                     float (&ccur)[OWN], float (&cnext)[OWN]) __attribute__((always_inline)) {
-      if constexpr (DIN == 32) {
-      const bool fin = i > i0;   // capsule i - 1 exists (virtual capsules i < i0 are not finished)
-      const int ip = max(i - 1, i0);
-      x_dma(xs_b, A.xplane_b, xsrc(i + 3), wv, xbuf(i + 3));   // into the buffer capsule i + 1's x left
-      const float lzv = Bk.lz[(size_t)ip * A.Fs + fc];
-      load_c<OWN>(crow + (size_t)clampc(i + 1) * cstep, A.Fs, cnext);
-      float Qp[OWN];
-#pragma unroll
-      for (int a = 0; a < OWN; ++a) Qp[a] = Q3[a];
-      constexpr int HW = NW / 2;
-      float sv[HW];
-      float g[CP];
-      auto fill = [&](auto stage) __attribute__((always_inline)) {
-        constexpr int S = decltype(stage)::value;
-        if constexpr (S == 0) {   // capsule i - 1's sigma partials of the 4 waves of this lane half
-          const float* slot = st + ((i - 1 - i0v) & 1) * NW * 32;
-#pragma unroll
-          for (int w = 0; w < HW; ++w) sv[w] = slot[(h * HW + w) * 32 + r];
-        } else if constexpr (S == 1) {
-          dots(ucur, ccur, (i - i0v) & 1);   // capsule i: q -> Q, the wave's sigma partial
-#pragma unroll
-          for (int a = 0; a < OWN; ++a) Q3[a] = Q[a];
-        } else if constexpr (S == 2) {
-          float sh = 0.f;
-#pragma unroll
-          for (int w = 0; w < HW; ++w) sh += sv[w];
-          float s0, s1;
-          xpair32(sh, s0, s1);
-          const float Sg = s0 + s1;
-          __builtin_amdgcn_raw_buffer_store_b64(
-              (unsigned __attribute__((ext_vector_type(2)))){__float_as_uint(lzv), __float_as_uint(Sg)}, sts,
-              (fin && wv == 0 && h == 0 && fvalid) ? (uint32_t)(f * A.in_n) * 8u : kNoStore, (uint32_t)ip * 8u, 0);
-          float gown[OWN];
-#pragma unroll
-          for (int a = 0; a < OWN; ++a) gown[a] = fin ? cprev[a] * (Qp[a] - Sg) : 0.f;
-#pragma unroll
-          for (int a = 0; a < OWN; ++a)   // gL, laid out as the couplings (0 past F)
-            bstore(gls, fvalid ? gown[a] : 0.f, fin ? (uint32_t)((j0 + h + 2 * a) * A.Fs + f) * 4u : kNoStore,
-                   (uint32_t)ip * A.JP * A.Fs * 4u);
-#pragma unroll
-          for (int a = 0; a < OWN; ++a) {
-            float g0, g1;
-            xpair32(gown[a], g0, g1);
-            g[2 * a] = g0;
-            g[2 * a + 1] = g1;
-          }
-        } else {   // gVc += gL u of capsule i - 1 (g = 0 on virtual steps; uprev is zero there)
-#pragma unroll
-          for (int t = 0; t < TW; ++t) {
-#pragma unroll
-            for (int v = 0; v < 16; ++v) acc[t][v] = fmaf(g[kpart<DOUT>(t, v)], uprev[t][v], acc[t][v]);
-            asm volatile("" : "+v"(acc[t]));   // keeps the FMAs in their MFMA region
-          }
-        }
-      };
-      {   // capsule i + 1's tiles (after the chunk's last capsule: its own operands, unused)
-        const int in = clampc(i + 2);
-        pose_prog32i<TW, 8, 5, 8>(fr, ones, unext, rs, wvo, bvo, A.wplane_b, (uint32_t)in * A.JDp * DIN * 2,
-                                  (uint32_t)in * A.JDp * 8, xbuf(i + 2) + lane * 16, fill);
-      }
-      xl_wait<1 + OWN + 5 * TW + 1 + OWN>();   // capsule i + 3's x has landed
-      __syncthreads();
-      }
-    };
-    if constexpr (IL3) {
-      f16v uz[TW];   // the third register set: zero, as capsule "i0v - 1" of the first step
-#pragma unroll
-      for (int t = 0; t < TW; ++t) uz[t] = f16v{};
-      float cz[OWN];
-#pragma unroll
-      for (int a = 0; a < OWN; ++a) cz[a] = 0.f, Q3[a] = 0.f;
-      for (int i = i0v; i <= i1; i += 3) {
-        step3(i, uz, uc, un, cz, cc, cn);
-        step3(i + 1, uc, un, uz, cc, cn, cz);
-        step3(i + 2, un, uz, uc, cn, cz, cc);
-      }
-    } else if constexpr (XL && SRF_DR_IL) {
+    if constexpr (XL && SRF_DR_IL) {
       for (int i = i0; i < i1; i += 2) {
         step_il(i, uc, un, cc, cn);
         if (i + 1 < i1) step_il(i + 1, un, uc, cn, cc);
