@@ -53,11 +53,6 @@
 #ifndef SRF_DR_IL
 #define SRF_DR_IL 1
 #endif
-// SRF_DR_TMI (A/B builds only): 1 = the din-32 four-row-tile passes pose tile-major with the
-// previous capsule's finish and this capsule's dots between the MFMAs; 0 = pose_prog.
-#ifndef SRF_DR_TMI
-#define SRF_DR_TMI 1
-#endif
 
 namespace {
 
@@ -1056,148 +1051,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       xl_wait();
       __syncthreads();
     }
-    if constexpr (DIN == 32 && TW == 4 && XJ && SRF_DR_TMI) {
-    // Tile-major, interleaved: iteration i finishes capsule i - 1 (stats published by the
-    // previous barrier) and poses capsule i one row tile at a time, so that the finish of
-    // tile t + 1 (s += c u, its u still capsule i - 1's) and the agreement dots of tile
-    // t - 1 (capsule i's, complete) issue between tile t's MFMAs; only the finish of tile
-    // 0, the stats chain and the dots of tile 3 remain outside the MFMA gaps.  No second
-    // u set: each tile is finished before its MFMAs overwrite it (the four-tile pass has
-    // no registers for one).
-    constexpr uint32_t TSTEP = 32 * DIN * 2;
-    f16v u[TW];
-#pragma unroll
-    for (int t = 0; t < TW; ++t) u[t] = f16v{};
-    float e[OWN], m = 0.f;
-#pragma unroll
-    for (int a = 0; a < OWN; ++a) e[a] = 0.f;
-    // capsule k: softmax over all waves (its stats published by the last barrier) -> c
-    // (c = 0 and no stores for k < i0)
-    auto couplings = [&](int k, float (&c)[CP]) __attribute__((always_inline)) {
-      const bool fin = k >= i0;
-      {
-        constexpr int HW = NW / 2;
-        const float2* slot = st + ((k - i0) & 1) * NW * 32;
-        float2 sv[HW];
-#pragma unroll
-        for (int w = 0; w < HW; ++w) sv[w] = slot[(h * HW + w) * 32 + r];
-        float mh = sv[0].x;
-#pragma unroll
-        for (int w = 1; w < HW; ++w) mh = fmaxf(mh, sv[w].x);
-        float zh = 0.f;
-#pragma unroll
-        for (int w = 0; w < HW; ++w) zh += sv[w].y * __expf(sv[w].x - mh);
-        float m0, m1, z0, z1;
-        xpair32(mh, m0, m1);
-        xpair32(zh, z0, z1);
-        const float M = fmaxf(m0, m1);
-        const float Z = z0 * __expf(m0 - M) + z1 * __expf(m1 - M);
-        const float sc = fin ? __expf(m - M) * __builtin_amdgcn_rcpf(Z) : 0.f;   // Z >= 1: 1-ulp v_rcp
-        const uint32_t ci = (uint32_t)max(k, 0);
-#pragma unroll
-        for (int a = 0; a < OWN; ++a)
-          bstore(crs, fvalid ? e[a] * sc : 0.f, fin ? (uint32_t)((j0 + h + 2 * a) * A.Fs + f) * 4u : kNoStore,
-                 ci * A.JP * A.Fs * 4u);
-        bstore(lzs, M + __builtin_amdgcn_logf(Z) * 0.69314718f,
-               (fin && h == 0 && wv == 0 && fvalid) ? (uint32_t)f * 4u : kNoStore, ci * A.Fs * 4u);
-#pragma unroll
-        for (int a = 0; a < OWN; ++a) {
-          float c0, c1;
-          xpair32(e[a] * sc, c0, c1);
-          c[2 * a] = c0;
-          c[2 * a + 1] = c1;
-        }
-      }
-    };
-    for (int i = i0; i < i1; ++i) {
-      // capsule i's x fragments from the workgroup's LDS copy, just in time
-#pragma unroll
-      for (int q = 0; q < 4; ++q) fr.b[q] = xl_read(xbuf(i) + lane * 16 + q * kXlPiece);
-      float c[CP];
-      couplings(i - 1, c);
-      auto finish_tile = [&](int t) __attribute__((always_inline)) {
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[t][v] = fmaf(c[kpart<DOUT>(t, v)], u[t][v], acc[t][v]);
-        asm volatile("" : "+v"(acc[t]));   // keeps the FMAs in their MFMA region
-      };
-      finish_tile(0);
-      {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fr.b[0]), "+v"(fr.b[1]), "+v"(fr.b[2]), "+v"(fr.b[3]));
-        const int in = min(i + 1, i1 - 1);
-        const uint32_t wcap = (uint32_t)in * A.JDp * DIN * 2, bcap = (uint32_t)in * A.JDp * 8;
-        float P[CP];
-#pragma unroll
-        for (int k2 = 0; k2 < CP; ++k2) P[k2] = 0.f;
-        auto dots_tile = [&](int t) __attribute__((always_inline)) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const f4 vv = vcl[(t * 4 + q) * 64 + lane];
-            float d = u[t][4 * q] * vv.x;
-            d = fmaf(u[t][4 * q + 1], vv.y, d);
-            d = fmaf(u[t][4 * q + 2], vv.z, d);
-            d = fmaf(u[t][4 * q + 3], vv.w, d);
-            P[kpart<DOUT>(t, 4 * q)] += d;
-          }
-        };
-#pragma unroll
-        for (int t = 0; t < TW; ++t) {
-          __builtin_amdgcn_sched_barrier(0);
-          u[t] = mfma32(fr.bias[t], ones, f16v{});
-          u[t] = mfma32h(fr.a[t][1], fr.b[0], u[t]);   // W2 x1
-          u[t] = mfma32h(fr.a[t][3], fr.b[2], u[t]);
-          u[t] = mfma32h(fr.a[t][0], fr.b[1], u[t]);   // W1 x2
-          u[t] = mfma32h(fr.a[t][2], fr.b[3], u[t]);
-          u[t] = mfma32h(fr.a[t][0], fr.b[0], u[t]);   // W1 x1
-          u[t] = mfma32h(fr.a[t][2], fr.b[2], u[t]);
-          if (t + 1 < TW) finish_tile(t + 1);
-          if (t >= 1) dots_tile(t - 1);
-          mfma_valu_hint<7, 5>();
-          __builtin_amdgcn_sched_barrier(0);
-          fetch_w<DIN>(rs, wvo + t * TSTEP, h, A.wplane_b, wcap, fr.a[t]);   // capsule i + 1's tile t
-          {
-            const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs.b, bvo + t * 32 * 8, bcap, 0);
-            fr.bias[t] = __builtin_bit_cast(bf8, (unsigned __attribute__((ext_vector_type(4)))){v2[0], v2[1], 0u, 0u});
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        dots_tile(TW - 1);
-        // reduce-scatter over lane halves: half h owns capsule partial 2a + h
-        float L[OWN];
-        m = -1e30f;
-#pragma unroll
-        for (int a = 0; a < OWN; ++a) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(P[2 * a]), __float_as_uint(P[2 * a + 1]),
-                                                           false, false);
-          L[a] = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) * inv + mk[a];
-          m = fmaxf(m, L[a]);
-        }
-        float z = 0.f;
-#pragma unroll
-        for (int a = 0; a < OWN; ++a) {
-          e[a] = __expf(L[a] - m);
-          z += e[a];
-        }
-        float m0, m1, z0, z1;
-        xpair32(m, m0, m1);
-        xpair32(z, z0, z1);
-        const float Mw = fmaxf(m0, m1);
-        const float Zw = z0 * __expf(m0 - Mw) + z1 * __expf(m1 - Mw);
-        if (h == 0) st[(((i - i0) & 1) * NW + wv) * 32 + r] = make_float2(Mw, Zw);
-        xl_wait();   // x of capsule i + 1 (DMA'd after the last barrier) lands before this one
-        __syncthreads();
-        // every wave's pose read x of capsule i: its buffer takes capsule i + 2's
-        x_dma(xs_b, A.xplane_b, xsrc(i + 2), wv, xbuf(i + 2));
-      }
-    }
-    {   // the chunk's last capsule
-      float c[CP];
-      couplings(i1 - 1, c);
-#pragma unroll
-      for (int t = 0; t < TW; ++t)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[t][v] = fmaf(c[kpart<DOUT>(t, v)], u[t][v], acc[t][v]);
-    }
-    } else
     for (int i = i0; i < i1; ++i) {
       f16v u[TW];
       // partial agreement dots <u_ij, Vc_j> over this lane's rows (packed FMA pairs)
