@@ -22,8 +22,9 @@ for v in "${VS[@]}"; do
     esac
   done
   echo "== [$i] $v"
+  echo "== variant [$i]: flags [$args] environment [$envs]" > $OUT/b$i.log
   ( for e in $envs; do export "$e"; done
-    timeout -k 10 200 python3 -X faulthandler $B --steps 10 --warmup 3 $args > $OUT/b$i.log 2>&1 ) || { tail -20 $OUT/b$i.log; exit 1; }
+    timeout -k 10 200 python3 -X faulthandler $B --steps 10 --warmup 3 $args >> $OUT/b$i.log 2>&1 ) || { tail -20 $OUT/b$i.log; exit 1; }
   tail -1 $OUT/b$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('  ms_per_step', d['ms_per_step'])"
   [ -n "$NOTRACE" ] && continue
   ( for e in $envs; do export "$e"; done
