@@ -819,10 +819,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
 // tile, one chunk) then hit 16 distinct slots per lane group; the DMA writes slots
 // lane-linearly, so each lane fetches the chunk its slot holds.  XCD-aware block
 // order: the row tiles of a frame tile run on one XCD (x read once per XCD).
-constexpr int kFfBM = 128, kFfBN = 64;
+constexpr int kFfBM = 128;
 constexpr int kFfA = 2 * kFfBM * 64;   // A bytes per stage (two planes)
-constexpr int kFfB = 2 * kFfBN * 64;   // B bytes per stage
-constexpr int kFfStage = kFfA + kFfB;  // 24 KiB; two stages
+// frames per workgroup BN (32-frame tiles; 2 row halves x BN / 32 frame tiles of waves):
+// a stage holds A (16 KiB) and B (BN x 128 B); two stages
+template <int BN>
+constexpr int ff_stage() { return kFfA + 2 * BN * 64; }
+
 
 __device__ __forceinline__ uint32_t ff_slot(int r, int c) { return (uint32_t)(4 * r + (c ^ ((r >> 2) & 3))); }
 
@@ -853,8 +856,14 @@ __device__ __forceinline__ void xl_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void route_fwd32_first_full_kernel(
+template <int BN>
+__global__ __launch_bounds__(64 * 2 * (BN / 32)) void route_fwd32_first_full_kernel(
     Args32 A, float* __restrict__ s_out, float* __restrict__ vc_out, float* __restrict__ v_out) {
+  constexpr int NWF = BN / 32, NWV = 2 * NWF;         // frame tiles, waves
+  constexpr int NPA = kFfA / 1024, NPB = 2 * BN * 64 / 1024, NP = NPA + NPB;   // 1 KiB DMA pieces
+  constexpr int NPW = (NP + NWV - 1) / NWV;           // pieces per wave (the last ones may idle)
+  constexpr int BPP = BN / 16;                        // B pieces per plane
+  constexpr int kStage = ff_stage<BN>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
@@ -865,47 +874,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
     blk = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + idx;
   }
   const int rt = blk % n_rt, ft = blk / n_rt;
-  const int row0 = rt * kFfBM, f0 = ft * kFfBN;
-  const int wr = wv >> 1, wc = wv & 1;   // row half, frame tile of this wave
+  const int row0 = rt * kFfBM, f0 = ft * BN;
+  const int wr = wv / NWF, wc = wv - wr * NWF;   // row half, frame tile of this wave
   const char* Wb = static_cast<const char*>(A.Ws);
   const char* Xb = static_cast<const char*>(A.xs);
   const size_t capb = (size_t)A.JDp * 64;   // bytes of one capsule's W rows per plane
-  // DMA roles: wave wv fills A pieces 4wv..4wv+3 and B pieces 2wv, 2wv+1 (1 KiB each)
-  // A piece q: plane q >> 3, slots (q & 7) * 64 + lane -> row = slot >> 2
-  uint32_t a_src[4];   // byte offset of this lane's A chunk (capsule 0, plane 0 base added later)
-  uint32_t a_pl[4];
+  // DMA roles: wave wv fills pieces wv, wv + NWV, ... (1 KiB each, 16 B per lane): A piece
+  // q < NPA: plane q / 8, slots (q % 8) * 64 + lane -> row slot >> 2; B piece q - NPA: plane
+  // (q - NPA) / BPP, slots ((q - NPA) % BPP) * 64 + lane -> frame slot >> 2
+  uint32_t src_o[NPW];
+  const char* src_b[NPW];
+  bool is_b[NPW], live[NPW];
+  int bf_[NPW], btt[NPW];
+  bool bok[NPW];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int q = 4 * wv + k;
-    const int slot = (q & 7) * 64 + lane, r = slot >> 2, c = (slot & 3) ^ ((r >> 2) & 3);
-    a_src[k] = (uint32_t)((row0 + r) * 64 + c * 16);
-    a_pl[k] = (uint32_t)(q >> 3);
-  }
-  int b_frame[2], b_c[2], b_pl[2], b_tt[2];
-  bool b_ok[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int q = 2 * wv + k;
-    const int slot = (q & 3) * 64 + lane, r = slot >> 2;
-    b_c[k] = (slot & 3) ^ ((r >> 2) & 3);
-    b_pl[k] = q >> 2;
-    b_frame[k] = f0 + r;
-    b_ok[k] = b_frame[k] < A.F;
-    const int fc = min(b_frame[k], A.F - 1);
-    b_tt[k] = fc - (fc / A.T) * A.T;
+  for (int k = 0; k < NPW; ++k) {
+    const int q = wv + k * NWV;
+    live[k] = q < NP;
+    is_b[k] = q >= NPA;
+    if (!is_b[k]) {
+      const int slot = (q & 7) * 64 + lane, r = slot >> 2, c = (slot & 3) ^ ((r >> 2) & 3);
+      src_b[k] = Wb + (size_t)(q >> 3) * A.wplane_b;
+      src_o[k] = (uint32_t)((row0 + r) * 64 + c * 16);
+      bf_[k] = 0, btt[k] = 0, bok[k] = false;
+    } else {
+      const int qb = q - NPA;
+      const int slot = (qb % BPP) * 64 + lane, r = slot >> 2, c = (slot & 3) ^ ((r >> 2) & 3);
+      src_b[k] = Xb + (size_t)(qb / BPP) * A.xplane_b;
+      src_o[k] = (uint32_t)(c * 16);
+      bf_[k] = f0 + r;
+      bok[k] = bf_[k] < A.F;
+      const int fc = min(bf_[k], A.F - 1);
+      btt[k] = fc - (fc / A.T) * A.T;
+    }
   }
   auto stage = [&](int i, int buf) {
-    char* dst = smem + buf * kFfStage;
+    char* dst = smem + buf * kStage;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int q = 4 * wv + k;
-      glds16(Wb + (size_t)a_pl[k] * A.wplane_b + (size_t)i * capb + a_src[k], dst + q * 1024);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = 2 * wv + k;
-      const uint32_t xo = x_voff<32>(i, A.N, A.lpad, A.T, A.F, b_frame[k], b_tt[k], b_ok[k], 0, A.zero_off);
-      glds16(Xb + (size_t)b_pl[k] * A.xplane_b + xo + b_c[k] * 16, dst + kFfA + q * 1024);
+    for (int k = 0; k < NPW; ++k) {
+      if (!live[k]) continue;   // uniform per wave
+      const int q = wv + k * NWV;
+      if (!is_b[k])
+        glds16(src_b[k] + (size_t)i * capb + src_o[k], dst + q * 1024);
+      else
+        glds16(src_b[k] + x_voff<32>(i, A.N, A.lpad, A.T, A.F, bf_[k], btt[k], bok[k], 0, A.zero_off) + src_o[k],
+               dst + q * 1024);
     }
   };
   // fragment reads: A rows wr*64 + t*32 + r32, B frames wc*32 + r32, chunk 2s + h
@@ -915,7 +928,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
   };
   auto bfrag = [&](const char* base, int plane, int sstep) -> h8 {
     const int r = wc * 32 + r32;
-    return *reinterpret_cast<const h8*>(base + kFfA + plane * (kFfBN * 64) + ff_slot(r, 2 * sstep + h) * 16);
+    return *reinterpret_cast<const h8*>(base + kFfA + plane * (BN * 64) + ff_slot(r, 2 * sstep + h) * 16);
   };
   f16v acc[2] = {f16v{}, f16v{}};
   const int n_in = A.in_n;
@@ -925,7 +938,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of capsule i has landed
     __syncthreads();                                    // ... and every wave's; buf ^ 1 no longer read
     if (i + 1 < n_in) stage(i + 1, buf ^ 1);
-    const char* base = smem + buf * kFfStage;
+    const char* base = smem + buf * kStage;
     h8 b[4];
     b[0] = bfrag(base, 0, 0);   // x hi, k-step 0
     b[1] = bfrag(base, 1, 0);   // x lo
@@ -2215,15 +2228,45 @@ bool fwd32_first_full_supported(const Fwd32Plan& p, int din, int dout) {
   return din == 32 && dout == 32 && p.JDp % kFfBM == 0;
 }
 
+// Frames per workgroup of the iteration-0 GEMM: the widest tile (fewest operand bytes
+// staged per MFMA) that still gives every CU a workgroup -- one 128-row x BN-frame
+// workgroup per CU moves 16 KiB + BN x 128 B per capsule through LDS where BN = 64
+// workgroups three to a CU moved 72 KiB.  SRF_FF_BN (A/B builds) forces one.
+#ifndef SRF_FF_BN
+#define SRF_FF_BN 0
+#endif
+static int ff_frames(int n_rt, int F) {
+  if (SRF_FF_BN) return SRF_FF_BN;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  for (int bn : {192, 128, 96})
+    if ((long)n_rt * ((F + bn - 1) / bn) >= cus * 9 / 10) return bn;
+  return 64;
+}
+
 int fwd32_first_full(const Fwd32Plan& p, const void* planes, void* scratch, int B, int T, int N, int din, int lpad,
                      int rpad, int J, int dout, int mask_first, float* s_out, float* vc_out, float* v_out,
                      hipStream_t st) {
   SRF_REQUIRE(fwd32_first_full_supported(p, din, dout), "fwd32_first_full: din %d dout %d JDp %d", din, dout, p.JDp);
   SRF_REQUIRE(2 * p.xplane * 2 < (1ull << 31) && p.ws_w < (1ull << 31), "fwd32: operand planes exceed 2 GiB");
   const Args32 a = make_args32(p, planes, scratch, B, T, N, din, lpad, rpad, J, dout, mask_first);
-  const int nb = (p.JDp / kFfBM) * ((B * T + kFfBN - 1) / kFfBN);
-  const size_t lds = 2 * kFfStage;
-  hipLaunchKernelGGL(route_fwd32_first_full_kernel, dim3(nb), dim3(256), lds, st, a, s_out, vc_out, v_out);
+  const int bn = ff_frames(p.JDp / kFfBM, B * T);
+  const int nb = (p.JDp / kFfBM) * ((B * T + bn - 1) / bn);
+#define SRF_FF_LAUNCH(BN)                                                                                          \
+  if (bn == BN) {                                                                                                 \
+    const size_t lds = 2 * (size_t)ff_stage<BN>();                                                               \
+    if (lds > 64 * 1024)                                                                                          \
+      SRF_HIP_TRY(hipFuncSetAttribute((const void*)route_fwd32_first_full_kernel<BN>,                             \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                      \
+    hipLaunchKernelGGL(route_fwd32_first_full_kernel<BN>, dim3(nb), dim3(64 * 2 * (BN / 32)), lds, st, a, s_out,  \
+                       vc_out, v_out);                                                                            \
+  }
+  SRF_FF_LAUNCH(64)
+  SRF_FF_LAUNCH(96)
+  SRF_FF_LAUNCH(128)
+  SRF_FF_LAUNCH(192)
+#undef SRF_FF_LAUNCH
   SRF_LAUNCH_CHECK("route_fwd32_first_full");
   return SRF_OK;
 }
