@@ -122,6 +122,21 @@ def _cpu_model():
     return 'unknown'
 
 
+def usable_cpus():
+    """The cores this process may run on: its affinity mask, bounded by the cgroup CPU
+    quota when one is set (a container whose affinity lists every core of the machine
+    but whose quota grants 16 runs 16 threads at a time; more threads only contend)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(model_gpu, cfg, class_n, T, seconds, threads=None, max_steps=50):
     """torch-CPU op-for-op mirror of naive (oracle/naive_mirror.py), fp32,
     one T-frame utterance per step, timed for >= `seconds` (>= 1 step)."""
@@ -133,7 +148,7 @@ def cpu_baseline(model_gpu, cfg, class_n, T, seconds, threads=None, max_steps=50
               vd=cfg.model_caps_class_dim, class_n=class_n, context=bool(cfg.model_caps_context))
     shape = so.SrfShape(**kw)
     if threads is None:
-        threads = len(os.sched_getaffinity(0))   # every core this process may run on
+        threads = usable_cpus()   # every core this process may run on
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     params = model_gpu.export_params()
@@ -473,7 +488,7 @@ def main():
         'config': res['config'], 'roofline': res['roofline'], 'forward_only': res['forward_only'],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the full host (every core in the affinity mask) on one utterance of the workload's
+        # the full host (every usable core: affinity mask within the cgroup quota) on one utterance of the workload's
         # length, and one core on a quarter-length utterance (frames/s is per frame)
         cb = cpu_baseline(model, cfg, class_n, T, args.cpu_seconds)
         one = cpu_baseline(model, cfg, class_n, max(40, T // 4), args.cpu_seconds / 2, threads=1)
