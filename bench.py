@@ -256,6 +256,9 @@ def measure(workload, args, world, rank, dev, flag_group=None):
     if args.sdr_capsnorm_per_layer:
         from srf_amd import ops
         ops.SDR_CAPSNORM_BATCHED = False
+    if args.sdr_gu_factors:
+        from srf_amd import ops
+        ops.SDR_GU_FACTORS = True
     if args.sdr_last_gxw_inline:
         from srf_amd import ops
         ops.SDR_LAST_GXW_SIDE = False
@@ -444,6 +447,9 @@ def main():
                          '"G_forward,G_backward" (default: SdrStackPlan.group)')
     ap.add_argument('--sdr-separate-gxgw', action='store_true',
                     help='SDR stack: the gx and gW launches of din-32 layers separately (default: fused)')
+    ap.add_argument('--sdr-gu-factors', action='store_true',
+                    help='SDR stack: the recurrence backward writes gu factors and gx / gW form gu from them '
+                         '(default: gu; A/B)')
     ap.add_argument('--sdr-capsnorm-per-layer', action='store_true',
                     help='SDR stack: one LN/dropout launch per inner layer and range (default: one per diagonal)')
     ap.add_argument('--dr-gw-inline', action='store_true',

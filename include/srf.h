@@ -168,6 +168,10 @@ typedef struct {
                                   workspace: it must be zero before the first grouped launch on
                                   it, and each grouped launch leaves its counters zero again
                                   (the timeout word excepted).  Other shapes ignore it. */
+  int gu_factored;             /* recur_bwd_n on the register kernels with couplings (C3): gu holds
+                                  each frame's gu factors (srf_route_sdr_fact_floats per frame)
+                                  instead of gu; gx_gw_n reads them (din = dout = 32) */
+  float* gumax;                /* gx_gw_n with gu_factored: one float, zero before the launch */
 } srf_sdr_range;
 /* pose_n fp8: 0 fp32 pose, 1 fp8 pose (fp32 u), 2 fp8 pose storing u in bf16 */
 int srf_route_sdr_pose_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
@@ -184,6 +188,13 @@ int srf_route_sdr_gw_n(const srf_sdr_range* ranges, int n, int B, int T, int N, 
  * shapes run the two entry points above).  Reads W (not WT) besides their fields. */
 int srf_route_sdr_gx_gw_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad,
                           int J, int dout, void* stream);
+/* The same from the recurrence's gu factors (ranges with gu_factored, whose recur_bwd_n
+ * wrote srf_route_sdr_fact_floats per frame into gu): gu_ij = sum_r c^r_ij gs^r_j +
+ * gL^r_ij Vc^r_j is formed inside the contraction with the forward's couplings, so gu
+ * never crosses HBM.  din = dout = 32, J a multiple of 8, iters <= 3.  Reads couplings,
+ * gu (the factors), W, emb; writes as gx_gw_n. */
+int srf_route_sdr_gx_gw_fact_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad,
+                               int J, int dout, int iters, void* stream);
 
 /* ---- The SDR layer in frame ranges (the layer-pipelined SDR stack) ----------
  * srf_route_sdr_fwd/bwd split into calls over frames [t0, t1) of every utterance,
@@ -224,6 +235,10 @@ size_t srf_route_sdr_recur_zero_range(int B, int in_n, int J, int dout, int iter
  * path: srf_route_sdr_couplings_required is 1 and recur_bwd needs them. */
 size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters);
 int srf_route_sdr_couplings_required(int in_n, int J, int dout, int iters);
+/* Floats of one frame's gu factors (srf_sdr_range.gu_factored): gL^r [iters][in_n][JP],
+ * gs^r and Vc^r [iters][J*dout] each (JP = J rounded up to a power of two, at least 4);
+ * 0 where the layer's backward cannot write them (no register kernel for the shape). */
+size_t srf_route_sdr_fact_floats(int in_n, int J, int dout, int iters);
 int srf_route_sdr_recur_fwd(const float* u, int v0, int vn, int B, int T, int in_n, int J, int dout, int iters,
                             int mask_first, int t0, int t1, float* v_out, float* couplings, void* workspace,
                             size_t workspace_bytes, void* stream);

@@ -21,7 +21,8 @@ class SdrRange(ctypes.Structure):
                 ('u', _vp), ('v0', _c_int), ('vn', _c_int), ('v', _vp), ('couplings', _vp),
                 ('workspace', _vp), ('workspace_bytes', _c_size), ('g_v', _vp), ('carry', _vp),
                 ('gu', _vp), ('g0', _c_int), ('gn', _c_int), ('g_emb', _vp), ('g_W', _vp), ('g_bias', _vp),
-                ('accumulate', _c_int), ('u_bf16', _c_int), ('group', _c_int)]
+                ('accumulate', _c_int), ('u_bf16', _c_int), ('group', _c_int), ('gu_factored', _c_int),
+                ('gumax', _vp)]
 
 
 _ranges = ctypes.POINTER(SdrRange)
@@ -67,6 +68,7 @@ _SIGNATURES = {
     'srf_route_sdr_recur_zero_range': (_c_size, [_c_int] * 5 + [ctypes.POINTER(_c_size)]),
     'srf_route_sdr_coupling_floats': (_c_size, [_c_int] * 4),
     'srf_route_sdr_couplings_required': (_c_int, [_c_int] * 4),
+    'srf_route_sdr_fact_floats': (_c_size, [_c_int] * 4),
     'srf_route_sdr_recur_fwd': (_c_int, [_vp] + [_c_int] * 11 + [_vp, _vp, _vp, _c_size, _vp]),
     'srf_route_sdr_recur_bwd': (_c_int, [_vp, _c_int, _c_int, _vp, _vp, _vp] + [_c_int] * 9
                                 + [_vp, _vp, _c_int, _c_int, _vp, _c_size, _vp]),
@@ -79,6 +81,7 @@ _SIGNATURES = {
     'srf_route_sdr_gx_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
     'srf_route_sdr_gw_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
     'srf_route_sdr_gx_gw_n': (_c_int, [_ranges] + [_c_int] * 9 + [_vp]),
+    'srf_route_sdr_gx_gw_fact_n': (_c_int, [_ranges] + [_c_int] * 10 + [_vp]),
     'srf_cnnfe_out_dims': (_c_int, [_c_int, _c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)]),
     'srf_cnnfe_saved_bytes': (_c_size, [_c_int] * 4),
     'srf_cnnfe_fwd_workspace': (_c_size, [_c_int] * 4),

@@ -1015,6 +1015,314 @@ __global__ __launch_bounds__(kGxwThreads) void sdr_gxw32_kernel(GxwItems items, 
   }
 }
 
+// gx + gW + gbias of din = dout = 32 layers from the recurrence's gu factors
+// (SeqItem::fact, C3): the register backward stores per frame gL^r [R][in_n][JP], gs^r and
+// Vc^r [R][JD] (55 KB at the C3 last layer instead of 320 KB of gu), and this pass forms
+//   gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j        (c^r: the forward's couplings)
+// in registers and contracts it at once, on the same f32 MFMAs as sdr_gxw32_kernel (exact
+// fp32 products).  A workgroup takes IW input capsules x 16 output capsules (16 waves, one
+// output capsule j = 32 rows each: 512 rows, as sdr_gxw32_kernel) x every frame of the
+// item in tiles of 16: per tile a lane loads its row of gs^r / Vc^r for 8 frames once
+// (frames 8h + s, s < 8) and forms gu for the IW capsules (gs^r / Vc^r are shared by
+// every input capsule; IW = 2 halves their L2 reads where the grid stays full), R
+// streamed with the next iteration's vectors in flight.  Per capsule:
+//   gW^T [rows][e] += gu[f][row] x_i(f)[e]     v_mfma_f32_32x32x2_f32 (K = frames 8h + s;
+//                                               x staged in LDS per tile [i][h][e][s])
+//   gx^T [e][f]     = W_i[row][e] gu[f][row]   v_mfma_f32_16x16x4_f32 (K = the wave's 32
+//                                               rows, lane = frame; gu transposed through
+//                                               a per-wave LDS tile; W_i in registers)
+// the 8 waves' gx parts add into an LDS tile [i][e][f] (LDS atomics), flushed into g_emb
+// through the window adjoint one tile later; gW / gbias stored at the end (one writer per
+// element; acc adds, as sdr_gxw32_kernel).  Couplings, gL^r and x of the next tile are
+// staged while this one computes; frame offsets four tiles deep.
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+struct GxwfItem {
+  const float* cs;     // couplings [B][T][R (P + JD)]
+  const float* fac;    // gu factors, frame view of fm ([B][gn][R (P + 2 JD)])
+  const float* W;
+  const float* emb;
+  float* g_emb;
+  float* gW;
+  float* gbias;
+  int acc, Q;
+  FrameMap fm;
+};
+struct GxwfItems {
+  GxwfItem it[srf::kMaxItems];
+  int n;
+};
+constexpr int kGxfWaves = 16;
+constexpr int kGxfThreads = 64 * kGxfWaves;
+constexpr int kGxfJ = kGxfWaves;       // output capsules per workgroup (32 rows each)
+constexpr int kGxfXS = 12;             // stride of an x row [s] in LDS (conflict-free b128 reads)
+constexpr int kGxfTS = 36;             // row stride of a wave's transposed gu tile [f][row]
+constexpr int kGxfGS = 20;             // frame stride of the gx tile [i][e][f]
+constexpr uint32_t kGxfOff = 0x7FFFFFFFu;   // an absent frame's factor offset (buffer loads read 0)
+
+#ifndef SRF_GXF_SB
+#define SRF_GXF_SB 1
+#endif
+
+template <int IW, int R>
+constexpr size_t gxf_lds_floats() {
+  return 2 * (size_t)IW * R * 2 * kGxfJ * 16      // couplings / gL^r [buf][i][r][c|gL][j][f]
+         + 2 * (size_t)IW * 2 * 32 * kGxfXS       // x [buf][i][h][e][s]
+         + 2 * (size_t)IW * 32 * kGxfGS           // gx [buf][i][e][f]
+         + (size_t)kGxfWaves * 16 * kGxfTS        // transposed gu per wave
+         + 4 * 4 * 16;                             // frame table [4][fac | cs | b*T | t][16]
+}
+
+template <int IW, int R>
+__global__ __launch_bounds__(kGxfThreads) void sdr_gxw32f_kernel(GxwfItems items, int N, int lpad, int in_n, int J,
+                                                                 int JP) {
+  const GxwfItem& G = items.it[blockIdx.z];
+  const int Q = G.Q;
+  const FrameMap fm = G.fm;
+  const int T = fm.T;
+  const int JD = J * 32, P = in_n * JP;
+  const size_t CSF = (size_t)R * (P + JD), FF = (size_t)R * (P + 2 * JD);
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int CB = IW * R * 2 * kGxfJ * 16, XB = IW * 2 * 32 * kGxfXS, GB = IW * 32 * kGxfGS;
+  float* coef = lds;                       // [2][CB]
+  float* xs = coef + 2 * CB;               // [2][XB]
+  float* gxb = xs + 2 * XB;                // [2][GB]
+  float* tT = gxb + 2 * GB;                // [wave][16][kGxfTS]
+  int* ftab = reinterpret_cast<int*>(tT + kGxfWaves * 16 * kGxfTS);   // [4][4][16]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5, l16 = lane & 15, kg = lane >> 4;
+  const int j0 = blockIdx.x * kGxfJ, j = j0 + wv;
+  const int i0 = blockIdx.y * IW;
+  const int NTl = (Q + 15) / 16;
+  for (int k = tid; k < 2 * GB; k += kGxfThreads) gxb[k] = 0.f;
+  // frame table of tile tt: factor byte offset, couplings offset, b * T, t (absent: t far out)
+  auto frames = [&](int tt) {
+    if (tid < 16) {
+      int* fb = ftab + (tt & 3) * 64;
+      const int q = tt * 16 + tid;
+      const bool ok = q < Q;
+      int b = 0, t = 0;
+      if (ok) fm.frame(q, b, t);
+      fb[tid] = ok ? (int)(fm.view(b, t) * FF * 4) : (int)kGxfOff;
+      fb[16 + tid] = ok ? (int)((size_t)(b * T + t) * CSF) : 0;
+      fb[32 + tid] = b * T;
+      fb[48 + tid] = ok ? t : -(1 << 20);
+    }
+  };
+  // staging of a tile: couplings / gL^r of IW capsules x 8 output capsules x 16 frames (f4
+  // pieces of 4 j), and x of the IW capsules through the window (f4 pieces of 4 e)
+  constexpr int JQ = kGxfJ / 4;   // f4 pieces of the workgroup's j per (frame, capsule, r, kind)
+  constexpr int NCP = 16 * IW * R * 2 * JQ, NCPT = (NCP + kGxfThreads - 1) / kGxfThreads;
+  f4 cv[NCPT], xv;
+  auto stage_load = [&](int tt) {
+    const int* fb = ftab + (tt & 3) * 64;
+#pragma unroll
+    for (int u = 0; u < NCPT; ++u) {
+      const int p = min(tid + u * kGxfThreads, NCP - 1);
+      const int f = p & 15, rest = p >> 4;
+      const int jq = rest % JQ, kind = (rest / JQ) & 1, ir = rest / (2 * JQ), r = ir % R, k = ir / R;
+      const int i = i0 + k;
+      const bool ok = fb[48 + f] > -(1 << 20) && i < in_n;
+      const float* src = kind ? G.fac + (size_t)(uint32_t)fb[f] / 4 : G.cs + (size_t)(uint32_t)fb[16 + f];
+      const f4 v = *reinterpret_cast<const f4*>(ok ? src + (size_t)r * P + (size_t)i * JP + j0 + 4 * jq : G.cs);
+      cv[u] = ok ? v : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    {
+      const int eq = tid & 7, f = (tid >> 3) & 15, k = tid >> 7;   // IW * 16 * 8 <= threads pieces
+      const int i = i0 + k;
+      const int w = i / N, n = i - w * N;
+      const int ts = fb[48 + f] + w - lpad;
+      const bool ok = k < IW && i < in_n && ts >= 0 && ts < T;
+      const f4 v = *reinterpret_cast<const f4*>(ok ? G.emb + ((size_t)(fb[32 + f] + ts) * N + n) * 32 + 4 * eq : G.emb);
+      xv = ok ? v : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto stage_store = [&](int buf) {
+    float* cb = coef + buf * CB;
+#pragma unroll
+    for (int u = 0; u < NCPT; ++u) {
+      const int p = tid + u * kGxfThreads;
+      if (NCP % kGxfThreads != 0 && p >= NCP) continue;
+      const int f = p & 15, rest = p >> 4;
+      const int jq = rest % JQ, kind = (rest / JQ) & 1, ir = rest / (2 * JQ);
+      float* d = cb + ((ir * 2 + kind) * kGxfJ + 4 * jq) * 16 + f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) d[c * 16] = cv[u][c];
+    }
+    {
+      const int eq = tid & 7, f = (tid >> 3) & 15, k = tid >> 7;
+      if (k < IW) {
+        float* d = xs + buf * XB + ((k * 2 + (f >> 3)) * 32 + 4 * eq) * kGxfXS + (f & 7);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[c * kGxfXS] = xv[c];
+      }
+    }
+  };
+  // gs^r / Vc^r of the lane's row, frames 8h + s: buffer loads over the factors (an absent
+  // frame's offset reads zeros)
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.fac), 0, (int)0x7FFFFFFF, 0x00020000);
+  const uint32_t rowb = (uint32_t)(j * 32 + l32) * 4;
+  uint32_t fo[8];
+  auto frame_offsets = [&](int tt) {
+    const int* fb = ftab + (tt & 3) * 64 + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const uint32_t o = (uint32_t)fb[s];
+      fo[s] = o == kGxfOff ? kGxfOff : o + rowb;
+    }
+  };
+  auto vec_load = [&](int r, float (&gsv)[8], float (&vcv)[8]) {
+    const uint32_t sg = (uint32_t)((size_t)R * P + (size_t)r * JD) * 4, sv = sg + (uint32_t)(R * JD) * 4;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      gsv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, fo[s], sg, 0));
+      vcv[s] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, fo[s], sv, 0));
+    }
+  };
+  // gx's A operand, W_i[32 j + 8 kg + st][e = 16 half + l16], for the whole launch
+  float wr[IW][2][8];
+#pragma unroll
+  for (int k = 0; k < IW; ++k)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int i = min(i0 + k, in_n - 1);
+        wr[k][hf][st] = G.W[((size_t)i * JD + j * 32 + 8 * kg + st) * 32 + 16 * hf + l16];
+      }
+  f16v agw[IW];
+  float sb[IW];
+#pragma unroll
+  for (int k = 0; k < IW; ++k) {
+    sb[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) agw[k][r] = 0.f;
+  }
+  float* tw = tT + wv * 16 * kGxfTS;
+  auto bar = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  frames(0);
+  frames(1);
+  __syncthreads();
+  if (NTl > 0) {
+    stage_load(0);
+    stage_store(0);
+  }
+  frame_offsets(0);
+  float gsc[8], vcc[8];
+  vec_load(0, gsc, vcc);
+  __syncthreads();
+  for (int tt = 0; tt < NTl; ++tt) {
+    const int buf = tt & 1;
+    const bool more = tt + 1 < NTl;
+    if (tt + 2 < NTl) frames(tt + 2);
+    stage_load(more ? tt + 1 : tt);
+    const float* cb = coef + buf * CB;
+    float gu[IW][8];
+#pragma unroll
+    for (int k = 0; k < IW; ++k)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) gu[k][s] = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (SRF_GXF_SB) __builtin_amdgcn_sched_barrier(0);   // one iteration's vectors in flight at a time
+      // the next iteration's vectors in flight through this one (the next tile's first
+      // ones are issued after the contractions, to their end of the tile)
+      float gsn[8], vcn[8];
+      if (r + 1 < R) vec_load(r + 1, gsn, vcn);
+#pragma unroll
+      for (int k = 0; k < IW; ++k) {
+        const float* cp = cb + ((k * R + r) * 2 * kGxfJ + wv) * 16 + 8 * h;
+        const float* gp = cp + kGxfJ * 16;
+        const f4 c0 = ld4(cp), c1 = ld4(cp + 4), g0 = ld4(gp), g1 = ld4(gp + 4);
+        const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) gu[k][s] = fmaf(cc[s], gsc[s], fmaf(gg[s], vcc[s], gu[k][s]));
+      }
+      if (r + 1 < R) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          gsc[s] = gsn[s];
+          vcc[s] = vcn[s];
+        }
+      }
+    }
+    const float* xb = xs + buf * XB;
+    float* gxt = gxb + buf * GB;
+#pragma unroll
+    for (int k = 0; k < IW; ++k) {
+      if (SRF_GXF_SB) __builtin_amdgcn_sched_barrier(0);
+      const float* xp = xb + ((k * 2 + h) * 32 + l32) * kGxfXS;
+      const f4 x0 = ld4(xp), x1 = ld4(xp + 4);
+      const float xx[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        sb[k] += gu[k][s];
+        agw[k] = mfma32x32x2(gu[k][s], xx[s], agw[k]);
+        tw[(8 * h + s) * kGxfTS + l32] = gu[k][s];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const f4 b0 = ld4(tw + l16 * kGxfTS + 8 * kg), b1 = ld4(tw + l16 * kGxfTS + 8 * kg + 4);
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      f4 gx[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        gx[0] = mfma16x16x4(wr[k][0][st], bb[st], gx[0]);
+        gx[1] = mfma16x16x4(wr[k][1][st], bb[st], gx[1]);
+      }
+      // C: lane (frame l16, kg) holds e = 16 half + 4 kg + c
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) atomicAdd(gxt + (k * 32 + 16 * hf + 4 * kg + c) * kGxfGS + l16, gx[hf][c]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();   // every lane's tile reads done before the next capsule's writes
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // the next tile's first vectors (the last tile reloads itself: no branch around a load)
+    frame_offsets(more ? tt + 1 : tt);
+    vec_load(0, gsc, vcc);
+    if (more) stage_store(buf ^ 1);
+    bar();   // this tile's gx parts complete; the next tile's staging visible
+    // flush this tile's gx through the window adjoint (and zero it for tile tt + 2)
+    const int* fb = ftab + (tt & 3) * 64;
+    for (int idx = tid; idx < IW * 512; idx += kGxfThreads) {
+      const int k = idx >> 9, f = (idx >> 5) & 15, e = idx & 31;
+      float* g = gxt + (k * 32 + e) * kGxfGS + f;
+      const float v = *g;
+      *g = 0.f;
+      const int i = i0 + k;
+      const int w = i / N, n = i - w * N;
+      const int ts = fb[48 + f] + w - lpad;
+      if (i < in_n && ts >= 0 && ts < T && v != 0.f)
+        atomicAdd(G.g_emb + ((size_t)(fb[32 + f] + ts) * N + n) * 32 + e, v);
+    }
+  }
+  if (j >= J) return;
+#pragma unroll
+  for (int k = 0; k < IW; ++k) {
+    const int i = i0 + k;
+    if (i >= in_n) continue;
+    const float sbt = sb[k] + __shfl_xor(sb[k], 32, 64);
+    if (h == 0) {
+      float* gb = G.gbias + (size_t)i * JD + j * 32 + l32;
+      *gb = G.acc ? *gb + sbt : sbt;
+    }
+    // agw: C[m = row][n = e]: lane (e = l32, h), reg r -> row mfma32_row(r, h)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float* dst = G.gW + ((size_t)i * JD + j * 32 + mfma32_row(r, h)) * 32 + l32;
+      *dst = G.acc ? *dst + agw[k][r] : agw[k][r];
+    }
+  }
+}
+
 // ---- fp8 pose (opt-in, BASELINE C5 "fp8 pose-transform MFMA"): OCP e4m3 operands on
 // v_mfma_f32_32x32x16_fp8_fp8, fp32 accumulation.  Every frame's x_i(f) and every row
 // of W_i gets its own power-of-two scale 2^e with max|a 2^e| in (224, 448] (e4m3's
@@ -1393,6 +1701,48 @@ int gxw_n(const SGeom& g, const GxwItems& it, hipStream_t st) {
   return SRF_OK;
 }
 
+// the padded capsule count of the register recurrence's [in_n][JP] records
+int jp_of(int J) {
+  int p = 4;
+  while (p < J) p <<= 1;
+  return p;
+}
+
+// gx + gW from gu factors (sdr_gxw32f_kernel): din = dout = 32, J % 16 == 0, iters <= 3
+bool gxwf_supported(const SGeom& g) {
+  return g.din == 32 && g.dout == 32 && g.J % kGxfJ == 0 && g.iters >= 1 && g.iters <= 3 &&
+         srf::sdr_seq_fact_floats(g.in_n(), g.J, g.dout, g.iters) != 0;
+}
+
+template <int IW, int R>
+int gxwf_launch(const SGeom& g, const GxwfItems& it, hipStream_t st) {
+  const size_t lds = gxf_lds_floats<IW, R>() * sizeof(float);
+  static bool attr = false;   // one-time raise of the kernel's LDS limit (above 64 KiB)
+  if (!attr) {
+    SRF_HIP_TRY(hipFuncSetAttribute((const void*)sdr_gxw32f_kernel<IW, R>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  const dim3 grid(g.J / kGxfJ, (g.in_n() + IW - 1) / IW, it.n);
+  hipLaunchKernelGGL((sdr_gxw32f_kernel<IW, R>), grid, dim3(kGxfThreads), lds, st, it, g.N, g.lpad, g.in_n(), g.J,
+                     jp_of(g.J));
+  SRF_LAUNCH_CHECK("sdr_gxw32f");
+  return SRF_OK;
+}
+
+int gxwf_n(const SGeom& g, const GxwfItems& it, hipStream_t st) {
+  if (it.n == 0) return SRF_OK;
+  // one input capsule per workgroup: two spill at 128 registers (16 waves)
+#define SRF_GXF(RR) \
+  if (g.iters == RR) return gxwf_launch<1, RR>(g, it, st);
+  SRF_GXF(1)
+  SRF_GXF(2)
+  SRF_GXF(3)
+#undef SRF_GXF
+  srf::set_error("sdr_gxw32f: iters %d", g.iters);
+  return SRF_EUNSUPPORTED;
+}
+
 // items with Q == 0 still run when they start the accumulation (acc == 0: zeros)
 int gw_n(const SGeom& g, const GemmItems& it, hipStream_t st) {
   if (it.n == 0) return SRF_OK;
@@ -1577,6 +1927,11 @@ srf::SeqItems seq_items(const srf_sdr_range* r, int n, int T, bool bwd, bool kee
                : srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, 0, T, nullptr};
     I.u_bf16 = r[k].u_bf16;
     I.group = r[k].group;
+#ifdef SRF_SEQ_FACT_FORCE   // A/B timing builds only: factors from every backward with couplings
+    I.fact = bwd && I.cs != nullptr;
+#else
+    I.fact = bwd && I.cs != nullptr && r[k].gu_factored;
+#endif
   }
   return it;
 }
@@ -1638,6 +1993,10 @@ size_t srf_route_sdr_recur_zero_range(int B, int in_n, int J, int dout, int iter
 size_t srf_route_sdr_coupling_floats(int in_n, int J, int dout, int iters) {
   const size_t n = srf::sdr_seq_cs_floats(in_n, J, dout, iters);
   return n ? n : srf::sdr_stream_cs_floats(in_n, J, dout, iters);
+}
+
+size_t srf_route_sdr_fact_floats(int in_n, int J, int dout, int iters) {
+  return srf::sdr_seq_fact_floats(in_n, J, dout, iters);
 }
 
 int srf_route_sdr_couplings_required(int in_n, int J, int dout, int iters) {
@@ -1753,6 +2112,8 @@ int srf_route_sdr_gx_gw_n(const srf_sdr_range* r, int n, int B, int T, int N, in
     if ((rc = srf_route_sdr_gx_n(r, n, B, T, N, din, lpad, rpad, J, dout, stream))) return rc;
     return srf_route_sdr_gw_n(r, n, B, T, N, din, lpad, rpad, J, dout, stream);
   }
+  for (int k = 0; k < n; ++k)
+    SRF_REQUIRE(!r[k].gu_factored, "gx_gw_n: gu factors go through srf_route_sdr_gx_gw_fact_n");
   GxwItems it{};
   for (int k = 0; k < n; ++k) {
     if (r[k].t0 >= r[k].t1 && r[k].accumulate) continue;   // an empty range still starts the sum
@@ -1761,6 +2122,29 @@ int srf_route_sdr_gx_gw_n(const srf_sdr_range* r, int n, int B, int T, int N, in
                             B * std::max(0, r[k].t1 - r[k].t0), frame_map(T, r[k].t0, r[k].t1, r[k].g0, r[k].gn)};
   }
   return gxw_n(g, it, static_cast<hipStream_t>(stream));
+}
+
+int srf_route_sdr_gx_gw_fact_n(const srf_sdr_range* r, int n, int B, int T, int N, int din, int lpad, int rpad, int J,
+                               int dout, int iters, void* stream) {
+  SGeom g{B, T, N, din, lpad, rpad, J, dout, iters, 0};
+  int rc = check_sgeom(g);
+  if (rc || (rc = items_ok(g, r, n, false, true))) return rc;
+  SRF_REQUIRE(gxwf_supported(g), "gu factors: din = dout = 32, J a multiple of 16, iters <= 3 (din=%d dout=%d J=%d iters=%d)",
+              g.din, g.dout, g.J, iters);
+  const size_t FF = srf::sdr_seq_fact_floats(g.in_n(), J, dout, iters);
+  GxwfItems it{};
+  for (int k = 0; k < n; ++k) {
+    if (r[k].t0 >= r[k].t1 && r[k].accumulate) continue;   // an empty range still starts the sum
+    SRF_REQUIRE(r[k].gu && r[k].couplings && r[k].W && r[k].emb && r[k].g_emb && r[k].g_W && r[k].g_bias,
+                "null pointer argument");
+    SRF_REQUIRE((size_t)B * r[k].gn * FF * 4 < 0x7FFFFF00u, "gu factors above 2 GiB per range buffer");
+    SRF_REQUIRE((size_t)B * T * srf::sdr_seq_cs_floats(g.in_n(), J, dout, iters) < 0x7FFFFFFFu,
+                "couplings above 2^31 floats");
+    it.it[it.n++] = GxwfItem{r[k].couplings, r[k].gu, r[k].W, r[k].emb, r[k].g_emb, r[k].g_W, r[k].g_bias,
+                             r[k].accumulate, B * std::max(0, r[k].t1 - r[k].t0),
+                             frame_map(T, r[k].t0, r[k].t1, r[k].g0, r[k].gn)};
+  }
+  return gxwf_n(g, it, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

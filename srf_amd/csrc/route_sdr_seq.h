@@ -39,6 +39,7 @@ struct SeqItem {
   SeqRange rg;
   int u_bf16;
   int group;        // streaming kernels: workgroups per utterance (0, 1: one; route_sdr_stream.hip)
+  int fact;         // register backward with cs: gu holds the per-frame gu factors (sdr_seq_fact_floats)
 };
 struct SeqItems {
   SeqItem it[kMaxItems];
@@ -55,6 +56,11 @@ bool sdr_seq_supported(int in_n, int J, int dout, int iters);
 // c^r [iters][in_n][JP] and pre-squash s^r [iters][J*dout]; a backward given them
 // skips recomputing the iterations.
 size_t sdr_seq_cs_floats(int in_n, int J, int dout, int iters);
+// gu factors of one frame (SeqItem::fact): gL^r [iters][in_n][JP], gs^r [iters][J*dout],
+// Vc^r [iters][J*dout]; with the forward's c^r they give
+// gu_ij = sum_r c^r_ij gs^r_j + gL^r_ij Vc^r_j (the consumer forms it).  The frame's record
+// sits at gu + (b * tg_n + t - tg0) * sdr_seq_fact_floats.
+size_t sdr_seq_fact_floats(int in_n, int J, int dout, int iters);
 int sdr_seq_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
                 hipStream_t st);
 

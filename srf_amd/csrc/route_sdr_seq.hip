@@ -302,6 +302,11 @@ size_t sdr_seq_cs_floats(int in_n, int J, int dout, int iters) {
   return (size_t)iters * ((size_t)in_n * srf_seq::pow2_at_least(J) + (size_t)J * dout);
 }
 
+size_t sdr_seq_fact_floats(int in_n, int J, int dout, int iters) {
+  if (!sdr_seq_supported(in_n, J, dout, iters)) return 0;
+  return (size_t)iters * ((size_t)in_n * srf_seq::pow2_at_least(J) + 2 * (size_t)J * dout);
+}
+
 int sdr_seq_fwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, int iters, int mask_first,
                 hipStream_t st) {
   int nim = 0, rm = 0;

@@ -46,7 +46,8 @@ constexpr bool cl_wanted(int nim, int kd) { return nim * kd >= 40; }
 // layer otherwise needs more than the 128 registers a 1024-thread workgroup allows.
 // GRP (with CS): X.G workgroups per utterance split its input capsules (srf_group.h)
 // and add their gVc^r partials inside the launch; member 0 writes the carry out.
-template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, bool GRP = false>
+// FACT (with CS): the frame's gu factors instead of gu (SeqItem::fact).
+template <int D, int JP, int NIM, int RM, bool CL, bool CS, int KR = NIM, bool GRP = false, bool FACT = false>
 __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems items, int T, int in_n, int J,
                                                                int iters, int mask_first, srf_grp::Grp X) {
   using C = Cfg<D, JP, NIM>;
@@ -289,7 +290,34 @@ __global__ __launch_bounds__(kThreads) void sdr_seq_bwd_kernel(srf::SeqItems ite
     }
     // ---- gu (u is dead: its registers take the next frame's loads, issued right
     // after); without CS one input capsule of the lane at a time
-    if constexpr (CS) {
+    if constexpr (CS && FACT) {
+      // the frame's gu factors instead of gu (SeqItem::fact): gL^r of the member's input
+      // capsules, gs^r and Vc^r (member 0: the members hold the same sums); the
+      // consumer forms gu with the forward's c^r
+      const int P = in_n * JP;
+      float* rec = gu + ((size_t)utt * rg.tg_n + (t - rg.tg0)) * ((size_t)R * (P + 2 * JD));
+      if constexpr (CL) {
+        const int ng = GRP ? X.G : 1, blk = (in_n + ng - 1) / ng, b0 = gm * blk;
+        const int nl = max(0, min(in_n, b0 + blk) - b0) * JP;
+        for (int idx = tid; idx < R * nl; idx += kThreads) {
+          const int r = idx / nl, o = b0 * JP + idx - r * nl;
+          rec[r * P + o] = gll[r * P + o];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+          if (r < R) store_ij<C>(gl[r], L, rec + r * P);
+      }
+      if (ev && gm == 0) {
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          if (r < R) {
+            rec[R * P + r * JD + tid] = gsl[r * JDa + tid];
+            rec[R * (P + JD) + r * JD + tid] = vcl[r * JDa + tid];
+          }
+        }
+      }
+    } else if constexpr (CS) {
       // four of the lane's KD values per pass, every row at once: one LDS read of each
       // gs^r / Vc^r quarter slice per pass serves all NIM rows
       constexpr int HD = 4;
@@ -385,7 +413,7 @@ size_t bwd_lds(int J, int D, int RM, int in_n, bool cl) {
 }
 
 template <int D, int JP, int NIM, int RM>
-int launch_bwd(const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, int B, int T, int in_n, int J, int iters,
+int launch_bwd(const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, bool fact, int B, int T, int in_n, int J, int iters,
                int mask_first, hipStream_t st) {
   constexpr bool want = cl_wanted(NIM, seq_kd(D, JP));
   const bool cl = want && bwd_lds(J, D, RM, in_n, true) <= 160 * 1024;
@@ -395,10 +423,18 @@ int launch_bwd(const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, int B
   constexpr int KD = seq_kd(D, JP);
   constexpr int KR = NIM * KD > 48 ? 32 / KD : NIM;
   SRF_REQUIRE(cs || X.G == 1, "sdr_seq: a grouped backward needs the forward's stored couplings");
-  auto k = X.G > 1 ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, true>
-                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, true>)
-           : cs    ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR>
-                         : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR>)
+  SRF_REQUIRE(cs || !fact, "sdr_seq: gu factors need the forward's stored couplings");
+  // factor instances for dout 32 only (their consumer, the din = dout = 32 gx / gW pass)
+  constexpr bool FT = D == 32;
+  SRF_REQUIRE(FT || !fact, "sdr_seq: gu factors for dout 32 only, got %d", D);
+  auto k = X.G > 1 ? (fact ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, true, FT>
+                                 : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, true, FT>)
+                           : (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, true>
+                                 : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, true>))
+           : cs    ? (fact ? (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR, false, FT>
+                                 : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR, false, FT>)
+                           : (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, true, KR>
+                                 : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, true, KR>))
                    : (cl ? sdr_seq_bwd_kernel<D, JP, NIM, RM, want, false>
                          : sdr_seq_bwd_kernel<D, JP, NIM, RM, false, false>);
   if (lds > 64 * 1024)
@@ -409,15 +445,15 @@ int launch_bwd(const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, int B
 }
 
 template <int D, int JP>
-int bwd_nim(int nim, int rm, const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, int B, int T, int in_n,
+int bwd_nim(int nim, int rm, const srf::SeqItems& items, const srf_grp::Grp& X, bool cs, bool fact, int B, int T, int in_n,
             int J, int iters, int mask_first, hipStream_t st) {
-  if (rm == 5) return launch_bwd<D, JP, 2, 5>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
-  if (nim == 2) return launch_bwd<D, JP, 2, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
+  if (rm == 5) return launch_bwd<D, JP, 2, 5>(items, X, cs, fact, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 2) return launch_bwd<D, JP, 2, 3>(items, X, cs, fact, B, T, in_n, J, iters, mask_first, st);
   if constexpr (D == 32 && JP == 32)
-    if (nim == 3) return launch_bwd<D, JP, 3, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
-  if (nim == 5) return launch_bwd<D, JP, 5, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
+    if (nim == 3) return launch_bwd<D, JP, 3, 3>(items, X, cs, fact, B, T, in_n, J, iters, mask_first, st);
+  if (nim == 5) return launch_bwd<D, JP, 5, 3>(items, X, cs, fact, B, T, in_n, J, iters, mask_first, st);
   if constexpr (seq_kd(D, JP) <= 8)
-    return launch_bwd<D, JP, 10, 3>(items, X, cs, B, T, in_n, J, iters, mask_first, st);
+    return launch_bwd<D, JP, 10, 3>(items, X, cs, fact, B, T, in_n, J, iters, mask_first, st);
   srf::set_error("sdr_seq: no backward kernel for %d input capsules per lane", nim);
   return SRF_EUNSUPPORTED;
 }
@@ -436,8 +472,11 @@ int sdr_seq_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, 
                 hipStream_t st) {
   // the items of one launch share the kernel: all with stored couplings or none
   const bool cs = items.n > 0 && items.it[0].cs != nullptr;
-  for (int k = 1; k < items.n; ++k)
+  const bool fact = items.n > 0 && items.it[0].fact;
+  for (int k = 1; k < items.n; ++k) {
     SRF_REQUIRE((items.it[k].cs != nullptr) == cs, "sdr_seq: launch items mix stored and recomputed couplings");
+    SRF_REQUIRE((items.it[k].fact != 0) == fact, "sdr_seq: launch items mix gu and gu factors");
+  }
   int nim = 0, rm = 0;
   srf_grp::Grp X;
   if (int rc = srf_grp::setup(items, B, 0, X, st)) return rc;
@@ -448,7 +487,7 @@ int sdr_seq_bwd(const SeqItems& items, int B, int T, int in_n, int J, int dout, 
   const int JP = srf_seq::pow2_at_least(J);
 #define SRF_SEQ_B(DD, PP)     \
   if (dout == DD && JP == PP) \
-    return bwd_nim<DD, PP>(nim, rm, items, X, cs, B, T, in_n, J, iters, mask_first, st);
+    return bwd_nim<DD, PP>(nim, rm, items, X, cs, fact, B, T, in_n, J, iters, mask_first, st);
   SRF_SEQ_CASES(SRF_SEQ_B)
 #undef SRF_SEQ_B
   srf::set_error("sdr_seq: unsupported shape J=%d dout=%d", J, dout);

@@ -758,6 +758,14 @@ SDR_FUSED_GXGW = True
 # only): off the backward's critical chain; False keeps them on the recurrence's stream
 # (bench --sdr-last-gxw-inline, for A/B)
 SDR_LAST_GXW_SIDE = True
+# True (bench --sdr-gu-factors, opt-in): din = dout = 32 layers on the register recurrence
+# with stored couplings (C3) have the recurrence backward write each frame's gu factors
+# (gL^r, gs^r, Vc^r: 55 KB at the C3 last layer) instead of gu (320 KB), and the fused
+# gx / gW pass form gu from them (srf_route_sdr_gx_gw_fact_n).  The recurrence gains
+# (C3 16.0 -> 14.85 ms with gx / gW still reading gu, r06fa), but the factor pass reads
+# gs^r / Vc^r once per input capsule from L2 and runs 482 us per inner diagonal against
+# 131 (C3 25.5 ms, r06fc): off until a pass that reuses them exists
+SDR_GU_FACTORS = False
 # the inner layers' LN + dropout of one anti-diagonal in one launch (srf_capsnorm_*_range_n);
 # False: one launch per layer (bench --sdr-capsnorm-per-layer, for A/B)
 SDR_CAPSNORM_BATCHED = True
@@ -931,13 +939,15 @@ class SdrStack(torch.autograd.Function):
         gbts = [targets[2 * L + 2 * l + 1][0] for l in range(L - 1)]
         g_embs = [torch.zeros_like(e) for e in embs]           # gx scatter targets
         g_vs, gparts, carries, WTs, gus, urs, rws, pws = [], [], [], [], [], [], [], []
+        # per layer: floats of one frame's gu factors (0: the layer writes and reads gu)
+        facts = [_gu_fact_floats(P, l, ctx.css[l] is not None) for l in range(L)]
         for l, (N, din, J, D, mf) in enumerate(P.layers):
             n = J * D
             g_vs.append(torch.empty((B, T, J, D), device=dev) if l < L - 1 else g_v_last)
             gparts.append(torch.empty((B * T, 2 * n), device=dev) if l < L - 1 else None)
             carries.append(torch.zeros((B, n), device=dev))
             WTs.append(torch.empty(Ws[l].numel(), device=dev))
-            gus.append(torch.empty(P.u_floats(l, P.nmax), device=dev))
+            gus.append(torch.empty(B * P.nmax * facts[l] if facts[l] else P.u_floats(l, P.nmax), device=dev))
             urs.append(us[l] if store else P.u_empty(l, P.nmax, dev))
             rws.append(P.recur_ws(l, dev))
             pws.append(torch.empty(max(L_.srf_capsnorm_params_workspace(B * T, n), 16), device=dev,
@@ -951,7 +961,7 @@ class SdrStack(torch.autograd.Function):
         # range k - 1 (stream B) never writes what gx / gW of range k (stream C) read: C
         # waits for B, never B for C (torch's capture crashed on streams ordered both ways)
         if side:
-            gus[L - 1] = torch.empty(P.u_floats(L - 1, T), device=dev)
+            gus[L - 1] = torch.empty(B * T * facts[L - 1] if facts[L - 1] else P.u_floats(L - 1, T), device=dev)
         for s_ in (sa, sb, sc):
             s_.wait_stream(main)
         pa, pb, pc = ctypes_void(sa.cuda_stream), ctypes_void(sb.cuda_stream), ctypes_void(sc.cuda_stream)
@@ -970,7 +980,7 @@ class SdrStack(torch.autograd.Function):
                           gu=_ptr(gus[l]), g0=0 if side and l == L - 1 else t0,
                           gn=T if side and l == L - 1 else P.nmax, g_emb=_ptr(g_embs[l]), g_W=_ptr(gWs[l]),
                           g_bias=_ptr(gbs[l]), accumulate=int(k != P.K - 1), u_bf16=int(P.ubf[l]),
-                          group=P.group(l, dev, backward=True))
+                          group=P.group(l, dev, backward=True), gu_factored=int(facts[l] > 0))
 
         def run(sp, ls, ks, ev=None, gw=True, part='all'):
             """backward of ranges (ls[i], ks[i]) of same-shaped layers, batched: LN
@@ -1003,7 +1013,10 @@ class SdrStack(torch.autograd.Function):
                     return
             if live and not fused:
                 _sdr_call(L_.srf_route_sdr_gx_n, live, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_n')
-            if fused:
+            if fused and facts[ls[0]]:
+                _sdr_call(L_.srf_route_sdr_gx_gw_fact_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, P.iters, sp,
+                          what='sdr_gx_gw_fact_n')
+            elif fused:
                 _sdr_call(L_.srf_route_sdr_gx_gw_n, rr, B, T, N, din, P.lpad, P.rpad, J, D, sp, what='sdr_gx_gw_n')
             if ev is not None:
                 ev.record(streams[id(sp)])
@@ -1056,6 +1069,18 @@ class SdrStack(torch.autograd.Function):
             main.wait_stream(s_)
         ctx.css = None
         return (g_embs[0], None, None, None, None, *_returned(targets))
+
+
+def _gu_fact_floats(P, l, has_couplings):
+    """Floats of one frame's gu factors for layer l's backward, or 0 where the layer
+    writes gu: SDR_GU_FACTORS, the register recurrence with the forward's couplings, the
+    fused gx / gW pass and its shape (din = dout = 32, J a multiple of 16, iters <= 3)."""
+    N, din, J, D, mf = P.layers[l]
+    if not (SDR_GU_FACTORS and SDR_FUSED_GXGW and has_couplings and not P.streamed[l]):
+        return 0
+    if din != 32 or D != 32 or J % 16 or P.iters > 3:
+        return 0
+    return int(_lib.lib().srf_route_sdr_fact_floats(P.in_n(l), J, D, P.iters))
 
 
 def sdr_stack(emb0, plan, training, p_mid, seed, params):

@@ -8,7 +8,7 @@ step (B = 28, T = 800: 20 frame ranges per layer, three streams, the last layer'
 backward grouped) under each schedule the bench can select -- the default (last
 layer's gx / gW on a third stream), that launch inline, separate gx and gW launches,
 one LN launch per layer, and the last layer's recurrence ungrouped or grouped both
-ways -- replays it several times, and checks every replay against eager
+ways, and the opt-in gu factors (ops.SDR_GU_FACTORS) -- replays it several times, and checks every replay against eager
 ``process_train_step`` of the same schedule.
 
 The routing weights are scaled to half the reference init, where the step's gradient
@@ -47,6 +47,7 @@ VARIANTS = {
     'capsnorm_per_layer': {'SDR_CAPSNORM_BATCHED': False},
     'last_ungrouped': {'last_group': (1, 1)},
     'last_grouped_both': {'last_group': (2, 2)},
+    'gu_factors': {'SDR_GU_FACTORS': True},   # recurrence writes gu factors, gx / gW form gu
 }
 
 
