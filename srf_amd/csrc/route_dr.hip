@@ -860,6 +860,9 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
 // adjoint goes through per-wave LDS slabs [31 + window][n_per*32 + 4] (row stride 4
 // mod 32: conflict-free ds_read_b128 / ds_write_b128 for every window offset) and is
 // flushed into g_emb by one atomic add per element, as in route_gux_kernel.
+#ifndef SRF_GUX16_XCD
+#define SRF_GUX16_XCD 1
+#endif
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -886,10 +889,25 @@ __global__ __launch_bounds__(256, kGux16Occ) void route_gux16_kernel(
   const size_t FJD = (size_t)F * JD;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int fl = lane & 31, h = lane >> 5;
+#if SRF_GUX16_XCD
+  // XCD-aware task order: the grid is padded to a multiple of 8 and XCD x (= blockIdx.x
+  // mod 8, the dispatcher's round robin) takes the x-th eighth of the tasks, ordered
+  // n-chunk fastest, then frame tile, then output-capsule group: the n-chunks of one
+  // (frame tile, group) share its gs^r / Vc^r rows through one L2 (they were spread over
+  // four XCDs), and an XCD's W^T planes are its groups' only
+  const int n_ft = (F + 31) / 32, n_tasks = n_ft * n_wgroups * n_chunks;
+  const int task = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+  if (task >= n_tasks) return;
+  const int chunk = task % n_chunks;
+  const int rest = task / n_chunks;
+  const int ft = rest % n_ft;
+  const int wgrp = rest / n_ft;
+#else
   const int chunk = blockIdx.x % n_chunks;
   const int rest = blockIdx.x / n_chunks;
   const int wgrp = rest % n_wgroups;
   const int ft = rest / n_wgroups;
+#endif
   const int f = ft * 32 + fl;
   const FrameLoc loc = frame_loc(f, F, T);
   const int fv = loc.valid ? f : 0;
@@ -2012,7 +2030,8 @@ void launch_gux16(const Geom& g, const float* WT, const float* hdr, const float*
   const int n_wgroups = (g.J + kGux16NW - 1) / kGux16NW;
   const int n_per = gux16_n_per(g);
   const int n_chunks = (g.N + n_per - 1) / n_per;
-  const int grid = (g.F() + 31) / 32 * n_wgroups * n_chunks;
+  int grid = (g.F() + 31) / 32 * n_wgroups * n_chunks;
+  if (SRF_GUX16_XCD) grid = (grid + 7) / 8 * 8;   // the kernel's XCD-aware task order
   hipLaunchKernelGGL((route_gux16_kernel<R>), dim3(grid), dim3(64 * kGux16NW), gux16_lds_bytes(g, n_per), st, WT, hdr,
                      g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, g_emb,
                      cst, glst, JP, gumax);
