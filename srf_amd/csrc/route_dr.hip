@@ -863,6 +863,9 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
 #ifndef SRF_GUX16_XCD
 #define SRF_GUX16_XCD 1
 #endif
+#ifndef SRF_GW16S_XCD
+#define SRF_GW16S_XCD 1
+#endif
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -1611,11 +1614,24 @@ __global__ __launch_bounds__(256, 2) void route_gw16s_kernel(
   const size_t cblk = (size_t)in_n * JP * Fs;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n = lane & 31, h = lane >> 5;
+#if SRF_GW16S_XCD
+  // XCD-aware task order (as route_gux16_kernel): XCD x takes the x-th eighth of the
+  // tasks ordered capsule group fastest, then output-capsule group, then frame split, so
+  // a (split, group)'s gs^r / Vc^r rows stay on one XCD and a split's x planes on the
+  // two or three XCDs that cover it (they were read on all eight)
+  const int n_cc = (in_n + CAP - 1) / CAP, n_tasks = n_cc * n_rt * S;
+  const int task = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+  if (task >= n_tasks) return;
+  const int cc = task % n_cc;
+  const int rtg = (task / n_cc) % n_rt;
+  const int s = task / n_cc / n_rt;
+#else
   int b = blockIdx.x;
   const int s = b % S;
   b /= S;
   const int rtg = b % n_rt;
   const int cc = b / n_rt;
+#endif
   const int jw = rtg * 4 + wv;
   const bool wave_on = jw < J;
   const int j = min(jw, J - 1);
@@ -2152,10 +2168,11 @@ int launch_gw2(const Geom& g, const Gw2Plan& p, const float* xT, const float* sa
   const int grid = p.n_rt * p.n_cc * p.S;
   if constexpr (D == 32) {
     if (use_gw16s(g)) {
+      const int grid16 = SRF_GW16S_XCD ? (grid + 7) / 8 * 8 : grid;   // the kernel's XCD-aware task order
       SRF_REQUIRE(hdr != nullptr && gumax != nullptr, "route_gw16s: needs the forward's header and the gx pass's max");
       const _Float16* x16 = reinterpret_cast<const _Float16*>(xT);
 #define SRF_GW16S(R_)                                                                                              \
-  hipLaunchKernelGGL((route_gw16s_kernel<R_, kGw16Cap>), dim3(grid), dim3(256), 0, st, x16, hdr, gumax, saved, gs, \
+  hipLaunchKernelGGL((route_gw16s_kernel<R_, kGw16Cap>), dim3(grid16), dim3(256), 0, st, x16, hdr, gumax, saved, gs, \
                      cst, glst, g.F(), padded_frames(g), g.in_n(), g.J, g.mask_first, JP, p.n_rt, p.S, p.ft_per, gwp, \
                      gbp, p.pstride)
       if (g.iters == 2)
