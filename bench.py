@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0
 # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py`, averaged per dispatch by
 # scripts/pmcsum.py (KiB per dispatch), per workload
 PMC_TRAFFIC = {'timit_c2': os.path.join(HERE, 'profiles', 'r05_pmc_traffic_c2.json'),
-               'wsj_c4': os.path.join(HERE, 'profiles', 'r05_pmc_c4.json')}
+               'wsj_c4': os.path.join(HERE, 'profiles', 'r06_pmc_c4.json')}
 
 
 def make_config(kw):
@@ -183,7 +183,9 @@ def pmc_traffic(path, kernels, weights):
         return None
     total = 0.0
     for name, w in zip(kernels, weights):
-        cand = [r for r in rows if r['kernel'].startswith(name) and 'FETCH_SIZE' in r and 'WRITE_SIZE' in r]
+        bare = name.replace('void ', '')
+        cand = [r for r in rows if r['kernel'].replace('void ', '').startswith(bare)
+                and 'FETCH_SIZE' in r and 'WRITE_SIZE' in r]
         if not cand:
             return None
         r = max(cand, key=lambda r: r['grid'])
