@@ -170,8 +170,7 @@ typedef struct {
                                   (the timeout word excepted).  Other shapes ignore it. */
   int gu_factored;             /* recur_bwd_n on the register kernels with couplings (C3): gu holds
                                   each frame's gu factors (srf_route_sdr_fact_floats per frame)
-                                  instead of gu; gx_gw_n reads them (din = dout = 32) */
-  float* gumax;                /* gx_gw_n with gu_factored: one float, zero before the launch */
+                                  instead of gu; srf_route_sdr_gx_gw_fact_n reads them */
 } srf_sdr_range;
 /* pose_n fp8: 0 fp32 pose, 1 fp8 pose (fp32 u), 2 fp8 pose storing u in bf16 */
 int srf_route_sdr_pose_n(const srf_sdr_range* ranges, int n, int B, int T, int N, int din, int lpad, int rpad, int J,

@@ -21,8 +21,7 @@ class SdrRange(ctypes.Structure):
                 ('u', _vp), ('v0', _c_int), ('vn', _c_int), ('v', _vp), ('couplings', _vp),
                 ('workspace', _vp), ('workspace_bytes', _c_size), ('g_v', _vp), ('carry', _vp),
                 ('gu', _vp), ('g0', _c_int), ('gn', _c_int), ('g_emb', _vp), ('g_W', _vp), ('g_bias', _vp),
-                ('accumulate', _c_int), ('u_bf16', _c_int), ('group', _c_int), ('gu_factored', _c_int),
-                ('gumax', _vp)]
+                ('accumulate', _c_int), ('u_bf16', _c_int), ('group', _c_int), ('gu_factored', _c_int)]
 
 
 _ranges = ctypes.POINTER(SdrRange)
