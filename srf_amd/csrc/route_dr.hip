@@ -869,8 +869,11 @@ __global__ __launch_bounds__(256, DIN >= 32 ? (R >= 4 ? 2 : 3) : (R >= 4 ? 3 : 4
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+// 4 waves, two workgroups per CU (three, with a two-slot ring, measured slower; 8 waves,
+// one per CU, halving the j-group partial sums the flush adds into g_emb, also slower:
+// C4 7.83-7.86 vs 7.82-7.83 ms, r06j)
 constexpr int kGux16NW = 4;
-constexpr int kGux16Occ = 2;   // workgroups per CU (three, with a two-slot ring, measured slower)
+constexpr int kGux16Occ = 2;
 
 __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -879,7 +882,7 @@ __device__ __forceinline__ f16v mfma32h(const h8& a, const h8& b, const f16v& c)
 // The lane max of |gu| also goes to *gumax (one atomic max per wave; the caller zeroes
 // it): route_gw16s_kernel takes its per-layer exponent from it.
 template <int R>
-__global__ __launch_bounds__(256, kGux16Occ) void route_gux16_kernel(
+__global__ __launch_bounds__(64 * kGux16NW, kGux16Occ) void route_gux16_kernel(
     const float* __restrict__ WT, const float* __restrict__ hdr, int F, int T, int N, int lpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
     const float* __restrict__ gs, float* __restrict__ g_emb, const float* __restrict__ cst,
@@ -1086,11 +1089,7 @@ __global__ __launch_bounds__(256, kGux16Occ) void route_gux16_kernel(
     float v = 0.f;
 #pragma unroll
     for (int q = 0; q < NW; ++q) v += gacc[((size_t)q * nslots + sl) * SROW + rem];
-#ifndef SRF_GUX16_TIMING_NO_FLUSH   // timing builds only: skip the atomics (g_emb wrong)
     if (fo >= 0 && fo < F && v != 0.f) atomicAdd(g_emb + ((size_t)fo * N + n0) * DIN + rem, v);
-#else
-    if (v == 12345.f) g_emb[0] = v;
-#endif
     sl += dsl;
     rem += drem;
     if (rem >= row) rem -= row, ++sl;
