@@ -1060,10 +1060,6 @@ constexpr int kGxfTS = 36;             // row stride of a wave's transposed gu t
 constexpr int kGxfGS = 20;             // frame stride of the gx tile [i][e][f]
 constexpr uint32_t kGxfOff = 0x7FFFFFFFu;   // an absent frame's factor offset (buffer loads read 0)
 
-#ifndef SRF_GXF_SB
-#define SRF_GXF_SB 1
-#endif
-
 template <int IW, int R>
 constexpr size_t gxf_lds_floats() {
   return 2 * (size_t)IW * R * 2 * kGxfJ * 16      // couplings / gL^r [buf][i][r][c|gL][j][f]
@@ -1228,7 +1224,7 @@ __global__ __launch_bounds__(kGxfThreads) void sdr_gxw32f_kernel(GxwfItems items
       for (int s = 0; s < 8; ++s) gu[k][s] = 0.f;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      if (SRF_GXF_SB) __builtin_amdgcn_sched_barrier(0);   // one iteration's vectors in flight at a time
+      __builtin_amdgcn_sched_barrier(0);   // one iteration's vectors in flight at a time
       // the next iteration's vectors in flight through this one (the next tile's first
       // ones are issued after the contractions, to their end of the tile)
       float gsn[8], vcn[8];
@@ -1255,7 +1251,7 @@ __global__ __launch_bounds__(kGxfThreads) void sdr_gxw32f_kernel(GxwfItems items
     float* gxt = gxb + buf * GB;
 #pragma unroll
     for (int k = 0; k < IW; ++k) {
-      if (SRF_GXF_SB) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
       const float* xp = xb + ((k * 2 + h) * 32 + l32) * kGxfXS;
       const f4 x0 = ld4(xp), x1 = ld4(xp + 4);
       const float xx[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -1927,11 +1923,7 @@ srf::SeqItems seq_items(const srf_sdr_range* r, int n, int T, bool bwd, bool kee
                : srf::SeqRange{r[k].t0, r[k].t1, r[k].v0, r[k].vn, 0, T, nullptr};
     I.u_bf16 = r[k].u_bf16;
     I.group = r[k].group;
-#ifdef SRF_SEQ_FACT_FORCE   // A/B timing builds only: factors from every backward with couplings
-    I.fact = bwd && I.cs != nullptr;
-#else
     I.fact = bwd && I.cs != nullptr && r[k].gu_factored;
-#endif
   }
   return it;
 }
