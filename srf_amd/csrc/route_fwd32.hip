@@ -856,14 +856,17 @@ __device__ __forceinline__ void xl_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
 }
 
-template <int BN>
+// CPS capsules per stage buffer (one barrier per stage: CPS = 2 halves the barriers; two
+// buffers of two capsules fill the 160 KiB of LDS at BN = 192)
+template <int BN, int CPS = 1>
 __global__ __launch_bounds__(64 * 2 * (BN / 32)) void route_fwd32_first_full_kernel(
     Args32 A, float* __restrict__ s_out, float* __restrict__ vc_out, float* __restrict__ v_out) {
   constexpr int NWF = BN / 32, NWV = 2 * NWF;         // frame tiles, waves
   constexpr int NPA = kFfA / 1024, NPB = 2 * BN * 64 / 1024, NP = NPA + NPB;   // 1 KiB DMA pieces
   constexpr int NPW = (NP + NWV - 1) / NWV;           // pieces per wave (the last ones may idle)
   constexpr int BPP = BN / 16;                        // B pieces per plane
-  constexpr int kStage = ff_stage<BN>();
+  constexpr int kCap = ff_stage<BN>();                // LDS bytes of one capsule
+  constexpr int kStage = CPS * kCap;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
@@ -908,17 +911,21 @@ __global__ __launch_bounds__(64 * 2 * (BN / 32)) void route_fwd32_first_full_ker
       btt[k] = fc - (fc / A.T) * A.T;
     }
   }
-  auto stage = [&](int i, int buf) {
-    char* dst = smem + buf * kStage;
+  auto stage = [&](int i0, int buf) {
 #pragma unroll
-    for (int k = 0; k < NPW; ++k) {
-      if (!live[k]) continue;   // uniform per wave
-      const int q = wv + k * NWV;
-      if (!is_b[k])
-        glds16(src_b[k] + (size_t)i * capb + src_o[k], dst + q * 1024);
-      else
-        glds16(src_b[k] + x_voff<32>(i, A.N, A.lpad, A.T, A.F, bf_[k], btt[k], bok[k], 0, A.zero_off) + src_o[k],
-               dst + q * 1024);
+    for (int c = 0; c < CPS; ++c) {
+      const int i = min(i0 + c, A.in_n - 1);   // a stage past the last capsule re-DMAs it (not computed)
+      char* dst = smem + buf * kStage + c * kCap;
+#pragma unroll
+      for (int k = 0; k < NPW; ++k) {
+        if (!live[k]) continue;   // uniform per wave
+        const int q = wv + k * NWV;
+        if (!is_b[k])
+          glds16(src_b[k] + (size_t)i * capb + src_o[k], dst + q * 1024);
+        else
+          glds16(src_b[k] + x_voff<32>(i, A.N, A.lpad, A.T, A.F, bf_[k], btt[k], bok[k], 0, A.zero_off) + src_o[k],
+                 dst + q * 1024);
+      }
     }
   };
   // fragment reads: A rows wr*64 + t*32 + r32, B frames wc*32 + r32, chunk 2s + h
@@ -933,25 +940,28 @@ __global__ __launch_bounds__(64 * 2 * (BN / 32)) void route_fwd32_first_full_ker
   f16v acc[2] = {f16v{}, f16v{}};
   const int n_in = A.in_n;
   stage(0, 0);
-  for (int i = 0; i < n_in; ++i) {
-    const int buf = i & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of capsule i has landed
+  for (int i = 0, buf = 0; i < n_in; i += CPS, buf ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of stage i has landed
     __syncthreads();                                    // ... and every wave's; buf ^ 1 no longer read
-    if (i + 1 < n_in) stage(i + 1, buf ^ 1);
-    const char* base = smem + buf * kStage;
-    h8 b[4];
-    b[0] = bfrag(base, 0, 0);   // x hi, k-step 0
-    b[1] = bfrag(base, 1, 0);   // x lo
-    b[2] = bfrag(base, 0, 1);
-    b[3] = bfrag(base, 1, 1);
+    if (i + CPS < n_in) stage(i + CPS, buf ^ 1);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      h8 a[4];
-      a[0] = afrag(base, t, 0, 0);   // W hi, k-step 0
-      a[1] = afrag(base, t, 1, 0);   // W lo
-      a[2] = afrag(base, t, 0, 1);
-      a[3] = afrag(base, t, 1, 1);
-      acc[t] = pose_chain<32>(a, b, acc[t]);
+    for (int c = 0; c < CPS; ++c) {
+      if (c > 0 && i + c >= n_in) break;
+      const char* base = smem + buf * kStage + c * kCap;
+      h8 b[4];
+      b[0] = bfrag(base, 0, 0);   // x hi, k-step 0
+      b[1] = bfrag(base, 1, 0);   // x lo
+      b[2] = bfrag(base, 0, 1);
+      b[3] = bfrag(base, 1, 1);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        h8 a[4];
+        a[0] = afrag(base, t, 0, 0);   // W hi, k-step 0
+        a[1] = afrag(base, t, 1, 0);   // W lo
+        a[2] = afrag(base, t, 0, 1);
+        a[3] = afrag(base, t, 1, 1);
+        acc[t] = pose_chain<32>(a, b, acc[t]);
+      }
     }
   }
   // epilogue: s = c0 (2^-(aw+bx) acc + sum_i b_i), v = squash over the capsule's 32 rows
@@ -2235,6 +2245,9 @@ bool fwd32_first_full_supported(const Fwd32Plan& p, int din, int dout) {
 #ifndef SRF_FF_BN
 #define SRF_FF_BN 0
 #endif
+#ifndef SRF_FF_CPS2
+#define SRF_FF_CPS2 1
+#endif
 static int ff_frames(int n_rt, int F) {
   if (SRF_FF_BN) return SRF_FF_BN;
   int dev = 0, cus = 256;
@@ -2255,12 +2268,13 @@ int fwd32_first_full(const Fwd32Plan& p, const void* planes, void* scratch, int 
   const int nb = (p.JDp / kFfBM) * ((B * T + bn - 1) / bn);
 #define SRF_FF_LAUNCH(BN)                                                                                          \
   if (bn == BN) {                                                                                                 \
-    const size_t lds = 2 * (size_t)ff_stage<BN>();                                                               \
+    constexpr int CPS_ = (BN == 192 && SRF_FF_CPS2) ? 2 : 1;                                                      \
+    const size_t lds = 2 * CPS_ * (size_t)ff_stage<BN>();                                                        \
     if (lds > 64 * 1024)                                                                                          \
-      SRF_HIP_TRY(hipFuncSetAttribute((const void*)route_fwd32_first_full_kernel<BN>,                             \
+      SRF_HIP_TRY(hipFuncSetAttribute((const void*)route_fwd32_first_full_kernel<BN, CPS_>,                       \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                      \
-    hipLaunchKernelGGL(route_fwd32_first_full_kernel<BN>, dim3(nb), dim3(64 * 2 * (BN / 32)), lds, st, a, s_out,  \
-                       vc_out, v_out);                                                                            \
+    hipLaunchKernelGGL((route_fwd32_first_full_kernel<BN, CPS_>), dim3(nb), dim3(64 * 2 * (BN / 32)), lds, st, a, \
+                       s_out, vc_out, v_out);                                                                     \
   }
   SRF_FF_LAUNCH(64)
   SRF_FF_LAUNCH(96)
