@@ -886,7 +886,7 @@ __global__ __launch_bounds__(64 * kGux16NW, kGux16Occ) void route_gux16_kernel(
     const float* __restrict__ WT, const float* __restrict__ hdr, int F, int T, int N, int lpad, int in_n, int J,
     int mask_first, int n_wgroups, int n_chunks, int n_per, const float* __restrict__ saved,
     const float* __restrict__ gs, float* __restrict__ g_emb, const float* __restrict__ cst,
-    const float* __restrict__ glst, int JP, float* __restrict__ gumax) {
+    const float* __restrict__ glst, int JP, float* __restrict__ gumax, int jgpw) {
   static_assert(R >= 2, "stored couplings exist for iters >= 2");
   constexpr int DIN = 32, RV = R - 1, NW = kGux16NW;
   extern __shared__ __attribute__((aligned(16))) float gacc[];
@@ -917,8 +917,6 @@ __global__ __launch_bounds__(64 * kGux16NW, kGux16Occ) void route_gux16_kernel(
   const int f = ft * 32 + fl;
   const FrameLoc loc = frame_loc(f, F, T);
   const int fv = loc.valid ? f : 0;
-  const bool wave_on = wgrp * NW + wv < J;
-  const int j = __builtin_amdgcn_readfirstlane(min(wgrp * NW + wv, J - 1));
   const int n0 = chunk * n_per, nn = min(N, n0 + n_per) - n0;
   const int Wn = in_n / N;
   const int ncap = Wn * nn;
@@ -928,6 +926,14 @@ __global__ __launch_bounds__(64 * kGux16NW, kGux16Occ) void route_gux16_kernel(
   float* slab = gacc + (size_t)wv * nslots * SROW;
   for (int k = threadIdx.x; k < NW * nslots * SROW / 4; k += blockDim.x) st4(gacc + 4 * k, f4{0.f, 0.f, 0.f, 0.f});
   __syncthreads();
+  float gmax = 0.f;
+  // jgpw output-capsule groups of NW per workgroup, one after the other: their gx parts
+  // add up in the waves' slabs, so the flush below adds jgpw times fewer partial sums
+  // into g_emb (one float atomic per element and group)
+  for (int jg = 0; jg < jgpw; ++jg) {
+  const int jw = (wgrp * jgpw + jg) * NW + wv;
+  const bool wave_on = jw < J;
+  const int j = __builtin_amdgcn_readfirstlane(min(jw, J - 1));
 
   // the lane's 16 rows j*32 + 16 ks + 8 h + 0..7 of gs^r (c^0 folded into gs^0) and Vc^r
   const float c0 = (wave_on && !(mask_first && j == 0)) ? 1.f / (float)Jeff : 0.f;
@@ -992,7 +998,6 @@ __global__ __launch_bounds__(64 * kGux16NW, kGux16Occ) void route_gux16_kernel(
   auto advance = [&](int& ww, int& nn_) {
     if (++nn_ == nn) nn_ = 0, ++ww;
   };
-  float gmax = 0.f;
   auto compute = [&](auto slot) {
     constexpr int sl = decltype(slot)::value;
     // gu on packed pairs (v_pk_fma_f32), the lane's max |gu| for the frame's exponent
@@ -1074,6 +1079,7 @@ __global__ __launch_bounds__(64 * kGux16NW, kGux16Occ) void route_gux16_kernel(
     compute(S2{});
   }
 #undef SRF_GUX16_FETCH
+  }   // jg
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) gmax = fmaxf(gmax, __shfl_xor(gmax, o, 64));
   if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(gumax), __float_as_uint(gmax));   // gmax >= 0
@@ -2032,8 +2038,8 @@ inline bool use_gux16(const Geom& g) {
          gux16_lds_bytes(g, 1) <= kGux16LdsMax;
 }
 // n-chunk size: fewest rounds of two workgroups per CU, then fewest capsules each
-int gux16_n_per(const Geom& g) {
-  const int base = (g.F() + 31) / 32 * ((g.J + kGux16NW - 1) / kGux16NW);
+int gux16_n_per(const Geom& g, int jgpw) {
+  const int base = (g.F() + 31) / 32 * ((g.J + kGux16NW - 1) / kGux16NW / jgpw);
   const int slots = 256 * kGux16Occ;
   int best = 1;
   double best_cost = 1e30;
@@ -2041,7 +2047,7 @@ int gux16_n_per(const Geom& g) {
     if (n_per > 1 && gux16_lds_bytes(g, n_per) > kGux16LdsMax) break;
     const int chunks = (g.N + n_per - 1) / n_per;
     const int rounds = (base * chunks + slots - 1) / slots;
-    const double cost = (double)rounds * (gu_window(g) * n_per + 4);
+    const double cost = (double)rounds * (gu_window(g) * n_per * jgpw + 4);
     if (cost < best_cost) {
       best_cost = cost;
       best = n_per;
@@ -2050,17 +2056,22 @@ int gux16_n_per(const Geom& g) {
   return best;
 }
 
+#ifndef SRF_GUX16_JGPW
+#define SRF_GUX16_JGPW 2
+#endif
 template <int R>
 void launch_gux16(const Geom& g, const float* WT, const float* hdr, const float* saved, const float* gs,
                   float* g_emb, const float* cst, const float* glst, int JP, float* gumax, hipStream_t st) {
-  const int n_wgroups = (g.J + kGux16NW - 1) / kGux16NW;
-  const int n_per = gux16_n_per(g);
+  const int n_all = (g.J + kGux16NW - 1) / kGux16NW;   // output-capsule groups of kGux16NW
+  const int jgpw = n_all % SRF_GUX16_JGPW == 0 ? SRF_GUX16_JGPW : 1;
+  const int n_wgroups = n_all / jgpw;
+  const int n_per = gux16_n_per(g, jgpw);
   const int n_chunks = (g.N + n_per - 1) / n_per;
   int grid = (g.F() + 31) / 32 * n_wgroups * n_chunks;
   if (SRF_GUX16_XCD) grid = (grid + 7) / 8 * 8;   // the kernel's XCD-aware task order
   hipLaunchKernelGGL((route_gux16_kernel<R>), dim3(grid), dim3(64 * kGux16NW), gux16_lds_bytes(g, n_per), st, WT, hdr,
                      g.F(), g.T, g.N, g.lpad, g.in_n(), g.J, g.mask_first, n_wgroups, n_chunks, n_per, saved, gs, g_emb,
-                     cst, glst, JP, gumax);
+                     cst, glst, JP, gumax, jgpw);
 }
 
 template <int D, int R>
