@@ -30,6 +30,10 @@ C4_LAYERS = [
     pytest.param((28, 200, 16, 32, 2, 2, 16, 32, 3, False), id='c4_inner_bench'),
     pytest.param((28, 200, 16, 32, 2, 2, 32, 32, 3, True), id='c4_last_bench'),
     pytest.param((28, 199, 16, 32, 2, 2, 16, 32, 3, False), id='c4_inner_ragged_tile'),
+    # an odd input-capsule count (75) on the 192-frame iteration-0 tiles, which stage two
+    # capsules at a time: the last stage's second slot must add nothing
+    pytest.param((28, 200, 15, 32, 2, 2, 32, 32, 3, True), id='c4_last_odd_capsules'),
+    pytest.param((28, 150, 15, 32, 2, 2, 32, 32, 3, True), id='c4_last_odd_capsules_bn128'),   # 128-frame tiles
 ]
 
 
