@@ -1038,6 +1038,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = A.J * DOUT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);   // wave index in an SGPR (stats slots)
   const int r = lane & 31, h = lane >> 5;
   const int bid = blockIdx.x;
   const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
@@ -1186,8 +1187,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       }
       if constexpr (NW > 1) {
         // per-wave stats of the 32 frames -> LDS; half h combines waves [h*NW/2, (h+1)*NW/2)
+        // the stats slot addresses re-derived from the lane id here (asm: not hoisted): held
+        // across the capsule loop they were spilled, and a spill reload's vmcnt(0) drains
+        // the next capsule's operand prefetch
+        int lid;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+        const int sr = lid & 31, sh = lid >> 5;
         float2* slot = st + par * NW * 32;
-        if (h == 0) slot[wv * 32 + r] = make_float2(M, Z);
+        if (sh == 0) slot[wvu * 32 + sr] = make_float2(M, Z);
         if constexpr (XJ) xl_wait();   // x of capsule i + 1 (DMA'd after the last barrier) lands before this one
         __syncthreads();
         // every wave's pose read x of capsule i: its buffer takes capsule i + 2's (unconditional:
@@ -1196,7 +1203,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         constexpr int HW = NW / 2;
         float2 sv[HW];
 #pragma unroll
-        for (int w = 0; w < HW; ++w) sv[w] = slot[(h * HW + w) * 32 + r];
+        for (int w = 0; w < HW; ++w) sv[w] = slot[(sh * HW + w) * 32 + sr];
         float mh = sv[0].x;
 #pragma unroll
         for (int w = 1; w < HW; ++w) mh = fmaxf(mh, sv[w].x);
@@ -1570,6 +1577,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int JD = A.J * DOUT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);   // wave index in an SGPR (stats slots)
   const int r = lane & 31, h = lane >> 5;
   const int bid = blockIdx.x;
   const int ft = bid / A.n_chunks, chunk = bid - ft * A.n_chunks;
@@ -1705,15 +1713,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         S = s0 + s1;
       }
       if constexpr (NW > 1) {
+        int lid;   // the slot addresses from the lane id, as route_fwd32_kernel
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+        const int sr = lid & 31, shf = lid >> 5;
         float* slot = st + par * NW * 32;
-        if (h == 0) slot[wv * 32 + r] = S;
+        if (shf == 0) slot[wvu * 32 + sr] = S;
         if constexpr (XJ) xl_wait();   // x of capsule i + 1 lands before the barrier that publishes it
         __syncthreads();
         if constexpr (XJ) x_dma(xs_b, A.xplane_b, xsrc(i + 2), wv, xbuf(i + 2));   // into capsule i's buffer
         constexpr int HW = NW / 2;
         float sh = 0.f;
 #pragma unroll
-        for (int w = 0; w < HW; ++w) sh += slot[(h * HW + w) * 32 + r];
+        for (int w = 0; w < HW; ++w) sh += slot[(shf * HW + w) * 32 + sr];
         float s0, s1;
         xpair32(sh, s0, s1);
         S = s0 + s1;
