@@ -843,11 +843,22 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_dst) {
 // The DMA is inline asm: issued through the builtin, the compiler stops counting the
 // loads in flight across it and waits for all of them at the next operand use.  Its own
 // waits stay correct, only conservative, with one more load in flight than it knows of.
+// The source as a wave-uniform base (SGPRs) + the lane's 32-bit offset: no 64-bit
+// per-lane address is held across the capsule loop.
 __device__ __forceinline__ void x_dma(const char* xs, uint32_t xplane_b, uint32_t xvo, int wv, char* dst) {
-  const int q = wv & 3;
-  const char* src = xs + (q & 1) * xplane_b + xvo + (q >> 1) * 32;
+  const int q = __builtin_amdgcn_readfirstlane(wv) & 3;
+  const char* base = xs + (q & 1) * xplane_b + (q >> 1) * 32;
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(dst + q * kXlPiece));
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(src) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0), "v"(xvo), "s"(base)
+               : "memory", "m0");
+}
+// The lane id, re-derived where it is used (asm: not hoisted): a per-lane offset held
+// across a capsule loop at 256 registers is spilled, and its reload's vmcnt(0) drains
+// the operand prefetch.
+__device__ __forceinline__ int lane_asm() {
+  int lid;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+  return lid;
 }
 // K: the vector-memory instructions the wave issues after the DMA (they may stay in
 // flight); each kernel's count is checked against its ISA (scripts/dbg/check_xl_wait.py)
@@ -1195,7 +1206,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
         const int sr = lid & 31, sh = lid >> 5;
         float2* slot = st + par * NW * 32;
         if (sh == 0) slot[wvu * 32 + sr] = make_float2(M, Z);
-        if constexpr (XJ) xl_wait();   // x of capsule i + 1 (DMA'd after the last barrier) lands before this one
+        // x of capsule i + 1 (DMA'd after the last barrier) lands before this one; the next
+        // capsule's W / bias loads (5 per tile) and the last capsule's coupling / logZ
+        // stores issued since may stay in flight (scripts/dbg/check_xl_wait4.py)
+        if constexpr (XJ) xl_wait<5 * TW + OWN + 1>();
         __syncthreads();
         // every wave's pose read x of capsule i: its buffer takes capsule i + 2's (unconditional:
         // past the chunk it reloads the last capsule into a buffer no pose reads any more)
@@ -1592,6 +1606,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
   if (DIN <= 16 && NW > 1 && wv >= NW / 2) __builtin_amdgcn_s_setprio(1);   // din 32: measured faster without
   const uint32_t wvo = (uint32_t)(((tbase * 32 + r) * DIN + (DIN >= 16 ? 8 * h : 0)) * 2);
   const uint32_t bvo = (uint32_t)((tbase * 32 + r) * 8);
+  // logZ^r through a buffer descriptor: a 32-bit lane offset instead of a 64-bit
+  // pointer held across the capsule loop (which spilled, its reload's vmcnt(0) draining
+  // the operand prefetch)
+  const __amdgpu_buffer_rsrc_t lzr = make_rsrc(Bk.lz, (size_t)A.in_n * A.Fs * 4);
 
   f4* gsl = reinterpret_cast<f4*>(lds) + (size_t)wv * TW * 4 * 64;
   float* st = lds + (size_t)NW * TW * 4 * 64 * 4;
@@ -1683,7 +1701,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       pose_prog<DIN, TW, XJ, XJ>(fr, ones, u, rs, wvo, bvo,
                                  x_voff<DIN>(in, A.N, A.lpad, A.T, A.F, f, ftt, fvalid, h, A.zero_off), h,
                                  A.wplane_b, A.xplane_b, A.zero_off, (uint32_t)in * A.JDp * DIN * 2,
-                                 (uint32_t)in * A.JDp * 8, xbuf(i) + lane * 16);
+                                 (uint32_t)in * A.JDp * 8, xbuf(i) + lane_asm() * 16);
       // this capsule's couplings: the pose MFMAs in flight hide their latency (no
       // registers held across capsules)
       load_c<OWN>(crow + (size_t)i * cstep, A.Fs, cc);
@@ -1732,7 +1750,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kWavesP
       }
       // logZ of capsule i before the next capsule's operand loads: waiting for it at its
       // store then leaves those (younger) loads in flight
-      const float lzv = Bk.lz[(size_t)i * A.Fs + fc];
+      const float lzv =
+          __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lzr, (uint32_t)fc * 4u, (uint32_t)i * A.Fs * 4u, 0));
       __builtin_amdgcn_sched_barrier(0);
       {
         // (logZ, sigma) of frame f, capsule i: branch-free (wave 0, half 0, valid frames)
