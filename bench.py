@@ -264,12 +264,9 @@ def measure(workload, args, world, rank, dev, flag_group=None):
     if args.sdr_last_gxw_inline:
         from srf_amd import ops
         ops.SDR_LAST_GXW_SIDE = False
-    if args.dr_gw_inline:
+    if args.side_streams:
         from srf_amd import ops
-        ops.DR_GW_SIDE = False
-    if args.cnnfe_wgrad_inline:
-        from srf_amd import ops
-        ops.CNNFE_WGRAD_SIDE = False
+        ops.DR_GW_SIDE = ops.CNNFE_WGRAD_SIDE = True
     if args.dr_chunks:
         # "l:c,l:c" input-capsule chunks of DR layer l's routing passes (A/B of the plan's choice)
         for item in args.dr_chunks.split(','):
@@ -454,10 +451,9 @@ def main():
                          '(default: gu; A/B)')
     ap.add_argument('--sdr-capsnorm-per-layer', action='store_true',
                     help='SDR stack: one LN/dropout launch per inner layer and range (default: one per diagonal)')
-    ap.add_argument('--dr-gw-inline', action='store_true',
-                    help='DR: each layer\'s gW / gbias on the backward\'s stream (default: a side stream; A/B)')
-    ap.add_argument('--cnnfe-wgrad-inline', action='store_true',
-                    help='CNN-FE: the stage-2 weight gradient on the backward\'s stream (default: a side stream; A/B)')
+    ap.add_argument('--side-streams', action='store_true',
+                    help='DR gW / gbias and the CNN-FE stage-2 weight gradient on a side stream (A/B only: '
+                         'replays of a captured step then give wrong W / b gradients at times, ops.DR_GW_SIDE)')
     ap.add_argument('--dr-chunks', default='',
                     help='DR: input-capsule chunks per layer, "l:c,..." (default: the plan\'s choice; A/B)')
     ap.add_argument('--sdr-last-gxw-inline', action='store_true',

@@ -1,6 +1,7 @@
 """torch.autograd wrappers around the C ABI (device memory from torch's caching
 allocator, launches on torch's current HIP stream)."""
 import ctypes
+import os
 
 import torch
 
@@ -72,11 +73,21 @@ class RouteGeom:
 # DR gW / gbias (srf_route_dr_bwd_weights_ex) on a side stream beside the layers below.
 # Each layer's launch is deferred to the next DR backward (or the gradient buckets' next
 # collective, or dr_side_join), so the backward's next kernel is captured first
-# (STACK_CAPTURE_ORDER).  C4 8.31 -> 8.22 ms (r05ci); False: one stream (bench
-# --dr-gw-inline, for A/B).
-DR_GW_SIDE = True
+# (STACK_CAPTURE_ORDER).  C4 8.31 -> 8.22 ms (r05ci).  OFF since round 6, as CNNFE_WGRAD_SIDE: with the side
+# launches on, replays of a captured step gave W / b gradients off by 1e-3 .. 5e-2 of
+# their max in up to ~10 % of replays on some boxes (scripts/dbg/graph_race.py: two
+# processes x 150 replays of the C2-mini step), none on others; keeping the launch's
+# tensors until the join or waiting for the issuing stream's tail did not remove it
+# reliably; one stream: none in 598 replays.  Cause not found; bench --side-streams
+# turns both on (A/B; C4 7.80 -> 7.57 ms, r06gd).
+DR_GW_SIDE = False
 _dr_side = {}        # device index -> side stream
 _dr_pending = []     # (device, event, launch(stream_ptr), tensors the launch reads)
+_dr_keep = []        # tensors of issued side launches, released once the side stream is joined
+# diagnostics (A/B): SRF_SIDE_KEEP=0 releases them at issue (before round 6);
+# SRF_SIDE_WAIT=tail waits for the issuing stream's tail instead of the launch's event
+_SIDE_KEEP = os.environ.get('SRF_SIDE_KEEP', '1') != '0'
+_SIDE_WAIT = os.environ.get('SRF_SIDE_WAIT', 'event')
 
 
 def _dr_side_stream(dev):
@@ -90,11 +101,21 @@ def _dr_issue_pending():
     while _dr_pending:
         dev, ev, launch, keep = _dr_pending.pop(0)
         side = _dr_side_stream(dev)
-        side.wait_event(ev)
+        if _SIDE_WAIT == 'tail':
+            side.wait_stream(torch.cuda.current_stream(dev))
+        else:
+            side.wait_event(ev)
         launch(ctypes_void(side.cuda_stream))
         for t in keep:
             if t is not None:
                 t.record_stream(side)   # the allocator must not hand these out before the launch ran
+        # ... and the tensors stay referenced until the side stream is joined: released
+        # here, inside a capture, a block went back to the graph's pool, a later
+        # allocation of the same capture took it, and in ~5 % of replays the side branch
+        # read memory the main branch was rewriting -- W / b gradients off by 1e-4 .. 1e-1
+        # of their max (scripts/dbg/graph_race.py, tests/test_graph_replay_gpu.py)
+        if _SIDE_KEEP:
+            _dr_keep.append(keep)
 
 
 def dr_side_join():
@@ -104,6 +125,7 @@ def dr_side_join():
     _dr_issue_pending()
     for s in _dr_side.values():
         torch.cuda.current_stream(s.device).wait_stream(s)
+    _dr_keep.clear()
 
 
 _dr_state = {'queued': False, 'main': None}
@@ -120,6 +142,7 @@ def _dr_backward_done():
         s = _dr_side.get(main.device.index)
         if s is not None:
             main.wait_stream(s)
+            _dr_keep.clear()
 
 
 def dr_reset():
@@ -128,6 +151,7 @@ def dr_reset():
     the dead capture, and a flag left set would keep later backwards from installing
     their join.  GraphedTrainStep calls it when its capture raises."""
     _dr_pending.clear()
+    _dr_keep.clear()
     _dr_state['queued'] = False
     _dr_state['main'] = None
 
@@ -278,7 +302,7 @@ CNNFE_PARAMS = ('conv0a_kernel', 'conv0a_bias', 'conv0b_kernel', 'conv0b_bias', 
 # Stage-2 weight gradient (split-transpose, wgrad, reduce: ~240 us at C4) on the side
 # stream beside the stage-2 data gradient and stage 1 (srf_cnnfe_bwd_parts; the parts share
 # no workspace).  False: one srf_cnnfe_bwd call (bench --cnnfe-wgrad-inline, for A/B).
-CNNFE_WGRAD_SIDE = True
+CNNFE_WGRAD_SIDE = False   # off since round 6: see DR_GW_SIDE
 _cnnfe_events = {}   # device index -> the event after the prep part (one CNN-FE per step)
 
 

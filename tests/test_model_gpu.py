@@ -81,6 +81,7 @@ def test_dr_gw_side_stream_matches(cuda, name):
     feats = torch.tensor(z['feats'], dtype=torch.float32, device=cuda)
     inp_len = torch.tensor(z['inp_len'], device=cuda)
     grads = []
+    defaults = (ops.DR_GW_SIDE, ops.CNNFE_WGRAD_SIDE)
     for side in (False, True):
         ops.DR_GW_SIDE = ops.CNNFE_WGRAD_SIDE = side
         try:
@@ -93,7 +94,7 @@ def test_dr_gw_side_stream_matches(cuda, name):
             torch.cuda.synchronize()
             grads.append(model.flat_grad.detach().clone())
         finally:
-            ops.DR_GW_SIDE = ops.CNNFE_WGRAD_SIDE = True
+            ops.DR_GW_SIDE, ops.CNNFE_WGRAD_SIDE = defaults
     err, mag = (grads[0] - grads[1]).abs().max().item(), grads[0].abs().max().item()
     assert err <= 1e-5 * mag, (err, mag)
 
